@@ -1,0 +1,61 @@
+"""DenseCLIP constructor kwargs used by the fixtures and the tests.
+
+CITYSCAPES_CFG is what the reference trainer passes to `DenseCLIP(**...)` for
+seg/configs/denseclip_cityscapes.yaml (train_denseclip.py:958-1005): the model
+section minus `type`/`clip_pretrained`, with `context_length`, `text_dim`,
+`token_embed_dim` passed explicitly and `clip_pretrained_path=None` (the YAML's
+absolute weight path does not exist offline).  TINY_CFG is the same structure at
+toy widths so full weights/gradients fit in a fixture.
+"""
+
+CITYSCAPES_CLASSES = [
+    'road', 'sidewalk', 'building', 'wall', 'fence', 'pole',
+    'traffic light', 'traffic sign', 'vegetation', 'terrain', 'sky',
+    'person', 'rider', 'car', 'truck', 'bus', 'train',
+    'motorcycle', 'bicycle',
+]
+
+CITYSCAPES_CFG = dict(
+    backbone=dict(type='CLIPVisionTransformer', patch_size=16, width=768, layers=12, heads=12,
+                  input_resolution=224, output_dim=768,
+                  out_indices=[0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11]),
+    text_encoder=dict(type='CLIPTextContextEncoder', context_length=22, vocab_size=49408,
+                      transformer_width=512, transformer_heads=8, transformer_layers=12,
+                      embed_dim=512),
+    decode_head=dict(type='FPNHead', in_channels=256, channels=256, num_classes=19,
+                     align_corners=False, dropout_ratio=0.1),
+    depth_head=dict(type='FCNHeadDepth', in_channels=256, channels=128, align_corners=False),
+    neck=dict(type='ViTFeatureFusionNeck', inter_channels=128, out_channels=256),
+    context_decoder=None,
+    auxiliary_head=None,
+    identity_head=None,
+    context_length=6,
+    text_dim=512,
+    token_embed_dim=512,
+    context_feature='attention',
+    score_concat_index=-1,
+    text_head=False,
+    tau=0.05,
+    clip_pretrained_path=None,
+)
+
+TINY_CFG = dict(
+    backbone=dict(type='CLIPVisionTransformer', patch_size=16, width=64, layers=3, heads=2,
+                  input_resolution=32, output_dim=64, out_indices=[0, 1, 2]),
+    text_encoder=dict(type='CLIPTextContextEncoder', context_length=8, vocab_size=49408,
+                      transformer_width=64, transformer_heads=2, transformer_layers=2,
+                      embed_dim=32),
+    decode_head=dict(type='FPNHead', in_channels=32, channels=16, num_classes=19,
+                     align_corners=False),
+    depth_head=dict(type='FCNHeadDepth', in_channels=32, channels=8, align_corners=False),
+    neck=dict(type='ViTFeatureFusionNeck', inter_channels=16, out_channels=32),
+    context_decoder=None,
+    context_length=6,
+    text_dim=32,
+    token_embed_dim=64,
+    context_feature='attention',
+    score_concat_index=-1,
+    text_head=False,
+    tau=0.05,
+    clip_pretrained_path=None,
+)

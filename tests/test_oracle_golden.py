@@ -1,0 +1,88 @@
+"""Pin the CPU oracle against fixtures produced by running the reference itself.
+
+The reference has no tests or golden vectors of its own; these fixtures
+were generated from /root/reference by tests/golden/gen_golden.py.
+"""
+import torch
+import torch.nn.functional as F
+
+from helpers import (TINY_CFG, CITYSCAPES_CFG, spec_state_dict, golden, class_tokens,
+                     images, rel_err, stats)
+from oracle import denseclip_oracle as O
+
+
+def _fwd(name, cfg, x, gt_hw=None, training=False):
+    p = spec_state_dict(name)
+    return O.denseclip_forward(x, p, class_tokens(), cfg, gt_hw=gt_hw, training=training), p
+
+
+def test_tiny_eval_matches_reference():
+    g = golden("tiny_eval")
+    out, _ = _fwd("tiny", TINY_CFG, g["input"])
+    for i in range(3):
+        assert rel_err(out["maps"][i], g[f"map{i}"]) < 1e-5
+    assert rel_err(out["text"], g["text"]) < 1e-5
+    assert rel_err(out["score"], g["score"]) < 1e-5
+    assert rel_err(out["seg_low"], g["seg_low"]) < 1e-5
+    assert rel_err(out["depth_low"], g["depth_low"]) < 1e-5
+    assert rel_err(out["seg"], g["seg"]) < 1e-5
+    assert rel_err(out["depth"], g["depth"]) < 1e-5
+
+
+def test_vitb16_small_matches_reference():
+    g = golden("vitb16_1x128x256")
+    x = images(1, 128, 256)
+    out, _ = _fwd("cityscapes", CITYSCAPES_CFG, x)
+    for i in range(12):
+        fl = out["maps"][i].flatten()
+        assert rel_err(fl[g[f"map_idx{i}"]], g[f"map_val{i}"]) < 1e-4, i
+        assert torch.allclose(stats(out["maps"][i]), g[f"map_stats{i}"], rtol=1e-4, atol=1e-4)
+    assert rel_err(out["maps"][0], g["map0"]) < 1e-5
+    assert rel_err(out["maps"][11], g["map11"]) < 1e-4
+    assert rel_err(out["score"], g["score"]) < 1e-4
+    assert rel_err(out["seg_low"], g["seg_low"]) < 1e-4
+    assert rel_err(out["depth_low"], g["depth_low"]) < 1e-4
+    assert rel_err(out["seg"].flatten()[g["seg_idx"]], g["seg_val"]) < 1e-4
+
+
+def test_bilinear_restatement_matches_torch():
+    x = torch.randn(2, 5, 7, 9)
+    for hw in [(14, 18), (7, 9), (64, 128), (3, 4), (112, 145)]:
+        ref = F.interpolate(x, size=hw, mode="bilinear", align_corners=False)
+        assert (O.bilinear_resize(x, *hw) - ref).abs().max() < 1e-5
+
+
+def test_silog_restatement():
+    pred = torch.rand(2, 1, 8, 8) + 0.5
+    tgt = torch.rand(2, 1, 8, 8) + 0.5
+    m = torch.rand(2, 1, 8, 8) > 0.3
+    d = torch.log(pred) - torch.log(tgt)
+    d = d[m]
+    ref = (d ** 2).mean() - 0.5 * d.mean() ** 2
+    assert abs(float(O.silog_loss(pred, tgt, m)) - float(ref)) < 1e-6
+
+
+def test_tiny_train_step_matches_reference():
+    """Loss and sampled gradients of one seeded train step (BN batch stats, no dropout)."""
+    g = golden("tiny_train")
+    p = spec_state_dict("tiny")
+    p = {k: (v.clone().requires_grad_(True) if v.is_floating_point() else v) for k, v in p.items()}
+    out = O.denseclip_forward(g["input"], p, class_tokens(), TINY_CFG,
+                              gt_hw=tuple(g["seg_t"].shape[-2:]), training=True)
+    ce = F.cross_entropy(out["seg"], g["seg_t"], ignore_index=255)
+    sl = O.silog_loss(out["depth"], g["depth_t"], g["depth_m"].bool())
+    loss = ce + 0.1 * sl
+    assert abs(float(loss) - float(g["loss"][0])) < 1e-4 * abs(float(g["loss"][0]))
+    loss.backward()
+    checked = 0
+    for k in g:
+        if not k.startswith("gnorm/"):
+            continue
+        name = k[len("gnorm/"):]
+        gr = p[name].grad
+        assert gr is not None, name
+        n = float(gr.double().norm())
+        ref = float(g[k])
+        assert abs(n - ref) <= 1e-4 * ref + 1e-7, (name, n, ref)
+        checked += 1
+    assert checked > 50
