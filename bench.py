@@ -1,0 +1,244 @@
+"""Throughput benchmark: DenseCLIP ViT-B/16 fwd+bwd training step at 1024x2048 (BASELINE.json
+metric, configs[1] per GPU: batch 8 per GPU, bf16), data-parallel over RCCL for N > 1.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--mode F|R]
+  torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+One step = forward of the whole DenseCLIP (ViT on the HIP kernels, text encoder, neck,
+heads, bilinear resize to the label size), CE(ignore 255) + 0.1 SILog, backward,
+gradient all-reduce (DDP over RCCL when N > 1) and AdamW.  Mode F (default, full
+fine-tune) trains the ViT too, so its backward kernels run; mode R is the reference
+trainer's regime (backbone + text encoder frozen, train_denseclip.py:1040-1044) and is
+measured as well and reported beside the headline.
+
+rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (the fused attention
+forward), timed with HIP events on its launch stream over the timed region;
+`cpu_baseline` times the CPU oracle (the reference algorithm restated in torch fp32,
+including the same SDPA op the reference calls) on a bounded sample on the host cores.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=8, help="images per GPU")
+    ap.add_argument("--height", type=int, default=1024)
+    ap.add_argument("--width", type=int, default=2048)
+    ap.add_argument("--mode", choices=["F", "R"], default="F")
+    ap.add_argument("--no-mode-r", action="store_true", help="skip the extra mode-R measurement")
+    ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    return ap.parse_args()
+
+
+def attn_flops_fwd(B, N, H, D=64):
+    return 4.0 * B * H * N * N * D  # QK^T and PV
+
+
+def make_model(dev, mode):
+    from denseclip_vit_multimodal_amd.config import build_model, load_yaml
+    cfg = load_yaml("denseclip_cityscapes.yaml")
+    model = build_model(cfg, clip_path_override="")
+    model = model.to(dev)
+    for name, p in model.named_parameters():
+        frozen = name.startswith("text_encoder.")
+        if mode == "R":
+            frozen = frozen or name.startswith("backbone.")
+        # parameters that feed nothing differentiable in this config: the unused CLIP
+        # projection and the score-map branch (its output is discarded, denseclip.py:747)
+        if name in ("backbone.proj", "contexts", "gamma") or name.startswith(("vis_proj.", "global_proj.")):
+            frozen = True
+        p.requires_grad_(not frozen)
+    return model
+
+
+def synth_batch(B, H, W, dev, rank):
+    g = torch.Generator(device="cpu").manual_seed(1234 + rank)
+    img = torch.randn(B, 3, H, W, generator=g).to(dev).to(torch.bfloat16)
+    g = torch.Generator(device="cpu").manual_seed(1235 + rank)
+    seg = torch.randint(0, 19, (B, H, W), generator=g)
+    seg[torch.rand(B, H, W, generator=g) < 0.1] = 255
+    g = torch.Generator(device="cpu").manual_seed(1236 + rank)
+    depth = 1 + 79 * torch.rand(B, 1, H, W, generator=g)
+    mask = torch.rand(B, 1, H, W, generator=g) >= 0.2
+    return img, seg.to(dev), depth.to(dev), mask.to(dev)
+
+
+def run_steps(model, opt, batch, steps, silog):
+    img, seg, depth, mask = batch
+    for _ in range(steps):
+        out = model(img, gt_semantic_seg=seg, gt_depth=depth, return_loss=True)
+        loss = F.cross_entropy(out["main_output"], seg, ignore_index=255) + \
+            0.1 * silog(out["depth_output"], depth, mask)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+    return loss
+
+
+def timed(model, opt, batch, steps, warmup, silog, world):
+    from denseclip_vit_multimodal_amd import ops
+    run_steps(model, opt, batch, warmup, silog)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ops.TIMING = {}
+    t0 = time.perf_counter()
+    loss = run_steps(model, opt, batch, steps, silog)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    summary = ops.timing_summary()
+    ops.TIMING = None
+    if world > 1:
+        t = torch.tensor([dt], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t)
+    return dt, summary, float(loss)
+
+
+def cpu_baseline(H, W, threads):
+    """Oracle (reference algorithm restated in torch fp32 on the host) fwd+bwd, full fine-tune
+    (mode F: ViT + neck + heads trainable), ONE image at the benchmark resolution."""
+    for p in (os.path.join(ROOT, "tests"), os.path.join(ROOT, "tests", "golden")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from helpers import CITYSCAPES_CFG, spec_state_dict, class_tokens, images
+    from oracle import denseclip_oracle as O
+    torch.set_num_threads(threads)
+    O.USE_SDPA = True
+    sd = spec_state_dict("cityscapes")
+    p = {k: (v.requires_grad_(True) if v.is_floating_point() and not k.startswith("text_encoder.") else v)
+         for k, v in sd.items()}
+    x = images(1, H, W)
+    g = torch.Generator().manual_seed(1235)
+    seg = torch.randint(0, 19, (1, H, W), generator=g)
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        pass
+    out = O.denseclip_forward(x, p, class_tokens(), CITYSCAPES_CFG, training=True)
+    loss = F.cross_entropy(out["seg"], seg, ignore_index=255)
+    loss.backward()
+    dt = time.perf_counter() - t0
+    O.USE_SDPA = False
+    return {"value": round(1.0 / dt, 5), "unit": "images/sec", "cores": threads, "kind": "port",
+            "sample": f"1 image {H}x{W}, full DenseCLIP fwd+bwd (mode F, text path frozen), torch fp32 CPU "
+                      f"oracle with SDPA attention, {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.manual_seed(0)
+    from denseclip_vit_multimodal_amd.losses import SILogLoss
+    silog = SILogLoss()
+
+    B, H, W = args.batch, args.height, args.width
+    batch = synth_batch(B, H, W, dev, rank)
+
+    def setup(mode):
+        model = make_model(dev, mode)
+        model.train()
+        if world > 1:
+            from torch.nn.parallel import DistributedDataParallel as DDP
+            model = DDP(model, device_ids=[local], bucket_cap_mb=100, gradient_as_bucket_view=True,
+                        find_unused_parameters=False)
+        params = [p for p in model.parameters() if p.requires_grad]
+        opt = torch.optim.AdamW(params, lr=2e-5, weight_decay=0.01, fused=True)
+        return model, opt
+
+    model, opt = setup(args.mode)
+    dt, summ, loss = timed(model, opt, batch, args.steps, args.warmup, silog, world)
+    value = world * B * args.steps / dt
+    N = (H // 16) * (W // 16) + 1
+    heads = 12
+
+    # roofline of the dominant kernel: the fused attention forward (one kernel per launch)
+    n_att, tot_att, mean_att = summ.get("attn_fwd", (0, 0.0, float("nan")))
+    fl = attn_flops_fwd(B, N, heads)
+    achieved = fl / (mean_att * 1e-3) / 1e12 if n_att else None
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "attn_fwd_pmc.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+    kernels = {k: {"launches": v[0], "ms_total": round(v[1], 3), "ms_mean": round(v[2], 4)} for k, v in summ.items()}
+
+    mode_r = None
+    if args.mode == "F" and not args.no_mode_r:
+        del model, opt
+        torch.cuda.empty_cache()
+        model, opt = setup("R")
+        dtr, _, _ = timed(model, opt, batch, max(3, args.steps // 2), 2, silog, world)
+        mode_r = {"value": round(world * B * max(3, args.steps // 2) / dtr, 4), "unit": "images/sec",
+                  "ms_per_step": round(dtr / max(3, args.steps // 2) * 1e3, 2),
+                  "what": "reference regime: backbone + text encoder frozen (train_denseclip.py:1040-1044)"}
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_baseline == "auto":
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        try:
+            cpu = cpu_baseline(H, W, threads)
+        except Exception as e:  # report, do not hide
+            cpu = {"value": None, "error": repr(e)[:300]}
+
+    if rank == 0:
+        line = {
+            "metric": "images/sec (fwd+bwd) ViT-B/16 DenseCLIP @1024x2048",
+            "value": round(value, 4),
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (randn images, random labels/depth; random-init weights)",
+            "config": {"workload": "DenseCLIP ViT-B/16 seg+depth train step (mode %s), %dx%d" % (args.mode, H, W),
+                       "per_gpu_batch": B, "global_batch": B * world, "tokens_per_image": N,
+                       "parallelism": f"dp{world}", "mode": args.mode},
+            "roofline": {"kernel": "attn_fwd_kernel<bf16>", "bound": "mfma",
+                         "achieved": round(achieved, 2) if achieved else None, "peak": PEAK_BF16_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4) if achieved else None,
+                         "traffic": traffic, "flops_per_launch": fl, "launches": n_att,
+                         "ms_per_launch": round(mean_att, 4) if n_att else None},
+            "kernels": kernels,
+            "mode_R": mode_r,
+            "cpu_baseline": cpu,
+            "loss": round(loss, 4),
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,92 @@
+"""ctypes binding of libdclip.so (the C ABI declared in include/dclip.h).
+
+The library is built in-tree (`python -c "import __graft_entry__; __graft_entry__.build()"`
+or `make -C denseclip_vit_multimodal_amd/csrc`).  There is deliberately NO fallback:
+if the library is missing or a call fails, a RuntimeError is raised.
+"""
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DCLIP_LIB", os.path.join(_HERE, "libdclip.so"))
+
+F32, F16, BF16 = 0, 1, 2
+EPI_STORE, EPI_GELU, EPI_RESIDUAL, EPI_GELU_BWD, EPI_SPLITK = 0, 1, 2, 3, 4
+
+_c_void_p = ctypes.c_void_p
+_i32 = ctypes.c_int
+_i64 = ctypes.c_int64
+_f32 = ctypes.c_float
+
+# name -> argtypes (restype int)
+_SIGS = {
+    "dclip_layernorm_fwd": [_c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p,
+                            _i64, _i64, _f32, _c_void_p],
+    "dclip_layernorm_bwd": [_c_void_p, _i32, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32,
+                            _c_void_p, _c_void_p, _i64, _i64, _c_void_p],
+    "dclip_gemm": [_i32, _i32, _c_void_p, _i64, _c_void_p, _i64, _i64, _i64, _i64, _i32, _c_void_p, _c_void_p,
+                   _i32, _i64, _c_void_p, _i32, _i64, _c_void_p, _i64, _c_void_p],
+    "dclip_attn_fwd": [_i32, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i32, _i32, _f32, _c_void_p],
+    "dclip_attn_bwd": [_i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i32,
+                       _i32, _f32, _c_void_p],
+    "dclip_im2col": [_c_void_p, _i32, _c_void_p, _i32, _i32, _i32, _i32, _i32, _i32, _c_void_p],
+    "dclip_tokens_fwd": [_c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p],
+    "dclip_tokens_bwd": [_c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p],
+    "dclip_pos_interp_fwd": [_c_void_p, _c_void_p, _i32, _i32, _i32, _i32, _c_void_p],
+    "dclip_pos_interp_bwd": [_c_void_p, _c_void_p, _i32, _i32, _i32, _i32, _c_void_p],
+    "dclip_transpose": [_c_void_p, _i32, _i64, _i64, _i64, _c_void_p, _i32, _i64, _i64, _i32, _i64, _i64, _i64,
+                        _i32, _c_void_p, _c_void_p],
+    "dclip_channel_mean": [_c_void_p, _i32, _c_void_p, _i32, _i64, _i32, _c_void_p],
+    "dclip_score_map": [_c_void_p, _i32, _c_void_p, _c_void_p, _i32, _i32, _i32, _i32, _f32, _c_void_p],
+    "dclip_bilinear_fwd": [_c_void_p, _i32, _c_void_p, _i32, _i64, _i32, _i32, _i32, _i32, _c_void_p],
+    "dclip_bilinear_bwd": [_c_void_p, _i32, _c_void_p, _c_void_p, _i64, _i32, _i32, _i32, _i32, _c_void_p],
+    "dclip_cast": [_c_void_p, _i32, _c_void_p, _i32, _i64, _c_void_p],
+}
+EXPORTED = sorted(list(_SIGS) + ["dclip_last_error", "dclip_abi_version"])
+
+_lib = None
+_lock = threading.Lock()
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def load(path=None):
+    """Load libdclip.so (no GPU needed).  Raises if it is missing."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise NativeError(
+                f"libdclip.so not found at {p}: build it with `make -C denseclip_vit_multimodal_amd/csrc` "
+                "(the HIP path has no CPU fallback)")
+        lib = ctypes.CDLL(p)
+        for name, args in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = ctypes.c_int
+        lib.dclip_last_error.restype = ctypes.c_char_p
+        lib.dclip_last_error.argtypes = []
+        lib.dclip_abi_version.restype = ctypes.c_int
+        lib.dclip_abi_version.argtypes = []
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def lib():
+    return load()
+
+
+def call(name, *args):
+    """Invoke a C-ABI entry point; raise NativeError with dclip_last_error() on failure."""
+    L = load()
+    rc = getattr(L, name)(*args)
+    if rc != 0:
+        msg = L.dclip_last_error().decode(errors="replace")
+        raise NativeError(f"{name} failed ({rc}): {msg}")
+    return rc

@@ -1,0 +1,472 @@
+// Fused multi-head attention (head_dim 64) forward and backward for gfx950.
+//
+// Replaces the core of nn.MultiheadAttention(x, x, x, need_weights=False) used by every
+// ViT block (reference seg/denseclip/models.py:275, 287-289 -> F.multi_head_attention_forward
+// -> scaled_dot_product_attention): softmax(q k^T * d^-0.5) v per head, no mask, no dropout.
+// N = 1 + (H/16)(W/16) = 8193 tokens at 1024x2048, so the N x N scores never touch HBM.
+//
+// Layout: q/k/v are read in place from the packed in-projection output
+// qkv (B*N, 3*C), C = H*64 — each row of one head is 128 contiguous bytes — and O is
+// written as (B*N, C), the out-projection's input.  No reshape/permute copies.
+//
+// Forward (one workgroup = 4 waves = 128 query rows of one (batch, head)):
+//   * the S^T = K Q^T product is issued with K as the MFMA A-operand, so each lane owns
+//     one query row and the softmax row statistics are lane-local (plus one exchange
+//     with the partner half-wave),
+//   * the P^T accumulator registers are converted to 16-bit in place and used directly
+//     as the B-operand of O^T += V^T P^T (no LDS round trip for P); V^T fragments come
+//     from the row-major V tile with the gfx950 transposing LDS read ds_read_b64_tr_b16,
+//   * K/V tiles of 64 keys are double-buffered in LDS via 16-byte global_load_lds
+//     with an XOR-swizzled image (bank-conflict-free ds_read_b128 row reads),
+//   * online softmax in the exp2 domain, fp32 statistics; lse stored for backward.
+// Backward (FlashAttention-2 style recompute, no atomics):
+//   delta = rowsum(dO * O);  a query-major pass for dQ (same structure as the forward
+//   plus dP^T = V dO^T and dQ^T += K^T dS^T) and a key-major pass for dK, dV in which
+//   the S / dP accumulators (key on the lane) feed dV^T += dO^T P and dK^T += Q^T dS
+//   directly.
+#include "common.h"
+
+namespace {
+
+constexpr int HD = 64;        // head dim
+constexpr float LOG2E = 1.4426950408889634f;
+
+__device__ __forceinline__ int swz(int row, int col) {
+    // byte offset of 16-bit element (row, col) in a [rows][64] image with 16-byte chunks
+    // XOR-swizzled by ((row >> 1) & 7)
+    return row * 128 + ((((col >> 3) ^ ((row >> 1) & 7))) << 4) + ((col & 7) << 1);
+}
+
+// Stage rows [r0, r0 + nrows) of a row-major matrix (64 contiguous 16-bit columns per
+// row starting at `base`, row stride ld) into a swizzled LDS image.  Rows >= N are
+// clamped to N-1 (their results are masked by the caller).
+template <typename T>
+__device__ __forceinline__ void stage_rows(const T* __restrict__ base, int64_t ld, int r0, int nrows, int N,
+                                           char* lds, int wave, int lane, int nwaves) {
+    const int ninst = nrows / 8;
+    for (int inst = wave; inst < ninst; inst += nwaves) {
+        const int r = inst * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ ((r >> 1) & 7);
+        int gr = r0 + r;
+        gr = gr < N ? gr : N - 1;
+        const T* src = base + (int64_t)gr * ld + c * 8;
+        __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(lds + inst * 1024), 16, 0, 0);
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ typename Mfma<T>::frag row_frag(const char* img, int row, int chunk) {
+    return *(const typename Mfma<T>::frag*)(img + row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4));
+}
+
+// A-operand fragment of X^T for a product that sums over the ROWS of an image whose
+// k-order follows the "accumulator as B-operand" permutation: element j of half h is
+// image row rb*32 + 16s + 8(j>>2) + 4h + (j&3), MFMA row (lane & 31) is image column
+// cb*32 + (lane & 31).  Two transposing 4x16 LDS reads.
+template <typename T>
+__device__ __forceinline__ typename Mfma<T>::frag tr_frag(const char* img, int rb, int s, int cb, int lane) {
+    const int i = lane & 15, q = i >> 2, p = i & 3, g = lane >> 4, h = lane >> 5;
+    const int row = rb * 32 + 16 * s + 4 * h + q;
+    const int col = cb * 32 + (g & 1) * 16 + 4 * p;
+    typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+    i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(img + swz(row, col)));
+    i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(img + swz(row + 8, col)));
+    typedef short s8 __attribute__((ext_vector_type(8)));
+    s8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(typename Mfma<T>::frag, v);
+}
+
+// 16-bit B-operand fragment from accumulator registers 8s..8s+7
+template <typename T>
+__device__ __forceinline__ typename Mfma<T>::frag pack_frag(const f32x16& a, int s) {
+    typename Mfma<T>::frag f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = (T)a[8 * s + j];
+    return f;
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+    f32x16 z;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) z[e] = 0.f;
+    return z;
+}
+
+// dS = P (dP - delta) is ~1/N in magnitude; for fp16 operands it is pre-scaled by 2^8 before
+// the 16-bit conversion (keeps N = 8193 values out of the fp16 subnormal range) and the
+// dQ / dK accumulators are scaled back in the epilogue.  bf16 has the fp32 exponent range.
+template <typename T> struct DsScale { static constexpr float v = 1.0f; };
+template <> struct DsScale<f16> { static constexpr float v = 256.0f; };
+
+// accumulator register r -> row offset within a 32x32 tile (column = lane & 31)
+__device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// ============================================================================ forward
+template <typename T>
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const T* __restrict__ qkv, T* __restrict__ out,
+                                                          float* __restrict__ lse, int N, int H, float c) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 64 * 128];  // [buf][K|V][64 rows][128 B]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int bh = blockIdx.y, b = bh / H, hd = bh % H;
+    const int C = H * HD;
+    const int64_t ld = 3 * (int64_t)C;
+    const T* Qb = qkv + (int64_t)b * N * ld + hd * HD;
+    const T* Kb = Qb + C;
+    const T* Vb = Qb + 2 * C;
+    const int q = blockIdx.x * 128 + wave * 32 + l32;  // this lane's query row
+    const int qc = q < N ? q : N - 1;
+
+    typename Mfma<T>::frag qf[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = *(const typename Mfma<T>::frag*)(Qb + (int64_t)qc * ld + (2 * s + h) * 8);
+
+    f32x16 o[2] = {zero16(), zero16()};
+    float m = -INFINITY, l = 0.f;
+    const int nt = (N + 63) / 64;
+
+    stage_rows<T>(Kb, ld, 0, 64, N, smem, wave, lane, 4);
+    stage_rows<T>(Vb, ld, 0, 64, N, smem + 8192, wave, lane, 4);
+    __syncthreads();
+
+    for (int t = 0; t < nt; ++t) {
+        const char* Kt = smem + (t & 1) * 16384;
+        const char* Vt = Kt + 8192;
+        if (t + 1 < nt) {
+            char* nx = smem + ((t + 1) & 1) * 16384;
+            stage_rows<T>(Kb, ld, (t + 1) * 64, 64, N, nx, wave, lane, 4);
+            stage_rows<T>(Vb, ld, (t + 1) * 64, 64, N, nx + 8192, wave, lane, 4);
+        }
+        // S^T[key][q] for two 32-key blocks
+        f32x16 sacc[2] = {zero16(), zero16()};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+                sacc[kb] = Mfma<T>::mma(row_frag<T>(Kt, kb * 32 + l32, 2 * s + h), qf[s], sacc[kb]);
+        }
+        if ((t + 1) * 64 > N) {  // ragged last tile: keys >= N get -inf
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (t * 64 + kb * 32 + acc_row(r, h) >= N) sacc[kb][r] = -INFINITY;
+        }
+        float mx = -INFINITY;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[kb][r]);
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float mnew = fmaxf(m, mx * c);
+        const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+        float rs = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float p = __builtin_amdgcn_exp2f(fmaf(sacc[kb][r], c, -mnew));
+                sacc[kb][r] = p;
+                rs += p;
+            }
+        rs += __shfl_xor(rs, 32, 64);
+        l = l * alpha + rs;
+        m = mnew;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
+        // O^T[d][q] += V^T[d][key] P^T[key][q]
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const typename Mfma<T>::frag pf = pack_frag<T>(sacc[kb], s);
+#pragma unroll
+                for (int db = 0; db < 2; ++db)
+                    o[db] = Mfma<T>::mma(tr_frag<T>(Vt, kb, s, db, lane), pf, o[db]);
+            }
+        __syncthreads();
+    }
+
+    if (q < N) {
+        const float inv = 1.0f / l;
+        T* orow = out + ((int64_t)b * N + q) * C + hd * HD;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                const int d = db * 32 + 8 * g4 + 4 * h;
+                typedef T t4 __attribute__((ext_vector_type(4)));
+                t4 v = {(T)(o[db][4 * g4] * inv), (T)(o[db][4 * g4 + 1] * inv), (T)(o[db][4 * g4 + 2] * inv),
+                        (T)(o[db][4 * g4 + 3] * inv)};
+                *(t4*)(orow + d) = v;
+            }
+        if (h == 0) lse[(int64_t)bh * N + q] = m + __log2f(l);
+    }
+}
+
+// ============================================================================ backward
+// delta[b][h][q] = sum_d dO[q][h*64+d] * O[q][h*64+d]
+template <typename T>
+__global__ __launch_bounds__(256) void attn_delta_kernel(const T* __restrict__ o, const T* __restrict__ dout,
+                                                         float* __restrict__ delta, int N, int H, int64_t total) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (b*N + q)*H + hd
+    if (i >= total) return;
+    const int hd = (int)(i % H);
+    const int64_t row = i / H;
+    const int64_t b = row / N, q = row % N;
+    const T* a = o + row * (H * HD) + hd * HD;
+    const T* g = dout + row * (H * HD) + hd * HD;
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < HD; k += 8) {
+        typename Mfma<T>::frag va = *(const typename Mfma<T>::frag*)(a + k);
+        typename Mfma<T>::frag vg = *(const typename Mfma<T>::frag*)(g + k);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += (float)va[j] * (float)vg[j];
+    }
+    delta[(b * H + hd) * N + q] = s;
+}
+
+// Query-major dQ pass: 128 queries per workgroup (32 per wave), all key tiles.
+template <typename T>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
+                                                             const float* __restrict__ lse,
+                                                             const float* __restrict__ delta, T* __restrict__ dqkv,
+                                                             int N, int H, float c, float scale) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 64 * 128];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int bh = blockIdx.y, b = bh / H, hd = bh % H;
+    const int C = H * HD;
+    const int64_t ld = 3 * (int64_t)C;
+    const T* Qb = qkv + (int64_t)b * N * ld + hd * HD;
+    const T* Kb = Qb + C;
+    const T* Vb = Qb + 2 * C;
+    const T* dOb = dout + (int64_t)b * N * C + hd * HD;
+    const int q = blockIdx.x * 128 + wave * 32 + l32;
+    const int qc = q < N ? q : N - 1;
+
+    typename Mfma<T>::frag qf[4], gf[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        qf[s] = *(const typename Mfma<T>::frag*)(Qb + (int64_t)qc * ld + (2 * s + h) * 8);
+        gf[s] = *(const typename Mfma<T>::frag*)(dOb + (int64_t)qc * C + (2 * s + h) * 8);
+    }
+    const float Lq = lse[(int64_t)bh * N + qc];
+    const float dq_delta = delta[(int64_t)bh * N + qc];
+
+    f32x16 dq[2] = {zero16(), zero16()};
+    const int nt = (N + 63) / 64;
+    stage_rows<T>(Kb, ld, 0, 64, N, smem, wave, lane, 4);
+    stage_rows<T>(Vb, ld, 0, 64, N, smem + 8192, wave, lane, 4);
+    __syncthreads();
+
+    for (int t = 0; t < nt; ++t) {
+        const char* Kt = smem + (t & 1) * 16384;
+        const char* Vt = Kt + 8192;
+        if (t + 1 < nt) {
+            char* nx = smem + ((t + 1) & 1) * 16384;
+            stage_rows<T>(Kb, ld, (t + 1) * 64, 64, N, nx, wave, lane, 4);
+            stage_rows<T>(Vb, ld, (t + 1) * 64, 64, N, nx + 8192, wave, lane, 4);
+        }
+        f32x16 sacc[2] = {zero16(), zero16()};
+        f32x16 pacc[2] = {zero16(), zero16()};
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) {
+                sacc[kb] = Mfma<T>::mma(row_frag<T>(Kt, kb * 32 + l32, 2 * s + h), qf[s], sacc[kb]);
+                pacc[kb] = Mfma<T>::mma(row_frag<T>(Vt, kb * 32 + l32, 2 * s + h), gf[s], pacc[kb]);
+            }
+        const bool ragged = (t + 1) * 64 > N;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                float p = __builtin_amdgcn_exp2f(fmaf(sacc[kb][r], c, -Lq));
+                if (ragged && t * 64 + kb * 32 + acc_row(r, h) >= N) p = 0.f;
+                sacc[kb][r] = p * (pacc[kb][r] - dq_delta) * DsScale<T>::v;  // dS^T (scaled)
+            }
+        // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const typename Mfma<T>::frag sf = pack_frag<T>(sacc[kb], s);
+#pragma unroll
+                for (int db = 0; db < 2; ++db) dq[db] = Mfma<T>::mma(tr_frag<T>(Kt, kb, s, db, lane), sf, dq[db]);
+            }
+        __syncthreads();
+    }
+    scale *= 1.0f / DsScale<T>::v;
+    if (q < N) {
+        T* row = dqkv + ((int64_t)b * N + q) * ld + hd * HD;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                const int d = db * 32 + 8 * g4 + 4 * h;
+                typedef T t4 __attribute__((ext_vector_type(4)));
+                t4 v = {(T)(dq[db][4 * g4] * scale), (T)(dq[db][4 * g4 + 1] * scale),
+                        (T)(dq[db][4 * g4 + 2] * scale), (T)(dq[db][4 * g4 + 3] * scale)};
+                *(t4*)(row + d) = v;
+            }
+    }
+}
+
+// Key-major dK/dV pass: 128 keys per workgroup (32 per wave), all query slices of 32.
+template <typename T>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
+                                                               const float* __restrict__ lse,
+                                                               const float* __restrict__ delta,
+                                                               T* __restrict__ dqkv, int N, int H, float c,
+                                                               float scale) {
+    // [buf][Q | dO][32 rows][128 B] + [buf][L | delta][32 floats]
+    __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 32 * 128 + 2 * 2 * 32 * 4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int bh = blockIdx.y, b = bh / H, hd = bh % H;
+    const int C = H * HD;
+    const int64_t ld = 3 * (int64_t)C;
+    const T* Qb = qkv + (int64_t)b * N * ld + hd * HD;
+    const T* Kb = Qb + C;
+    const T* Vb = Qb + 2 * C;
+    const T* dOb = dout + (int64_t)b * N * C + hd * HD;
+    const float* Lb = lse + (int64_t)bh * N;
+    const float* Db = delta + (int64_t)bh * N;
+    const int key = blockIdx.x * 128 + wave * 32 + l32;
+    const int kc = key < N ? key : N - 1;
+    float* stat = (float*)(smem + 2 * 2 * 32 * 128);
+
+    typename Mfma<T>::frag kf[4], vf[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        kf[s] = *(const typename Mfma<T>::frag*)(Kb + (int64_t)kc * ld + (2 * s + h) * 8);
+        vf[s] = *(const typename Mfma<T>::frag*)(Vb + (int64_t)kc * ld + (2 * s + h) * 8);
+    }
+    f32x16 dk[2] = {zero16(), zero16()}, dv[2] = {zero16(), zero16()};
+    const int nt = (N + 31) / 32;
+
+    auto stage = [&](int t, int buf) {
+        char* base = smem + buf * 8192;
+        stage_rows<T>(Qb, ld, t * 32, 32, N, base, wave, lane, 4);
+        stage_rows<T>(dOb, C, t * 32, 32, N, base + 4096, wave, lane, 4);
+        if (wave == 0) {
+            // L and delta of the slice also by LDS-DMA (4 B per lane): an ordinary global
+            // load here would make hipcc drain the tile DMA with vmcnt(0) at its use
+            const int r = t * 32 + (lane & 31);
+            const int rc = r < N ? r : N - 1;
+            const float* src = lane < 32 ? Lb + rc : Db + rc;
+            __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(stat + buf * 64), 4, 0, 0);
+        }
+    };
+    stage(0, 0);
+    __syncthreads();
+
+    for (int t = 0; t < nt; ++t) {
+        const int buf = t & 1;
+        const char* Qt = smem + buf * 8192;
+        const char* Gt = Qt + 4096;
+        const float* Ls = stat + buf * 64;
+        const float* Ds = Ls + 32;
+        if (t + 1 < nt) stage(t + 1, buf ^ 1);
+        // S[q][key], dP[q][key]  (query rows in registers, key on the lane)
+        f32x16 sacc = zero16(), pacc = zero16();
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            sacc = Mfma<T>::mma(row_frag<T>(Qt, l32, 2 * s + h), kf[s], sacc);
+            pacc = Mfma<T>::mma(row_frag<T>(Gt, l32, 2 * s + h), vf[s], pacc);
+        }
+        const bool ragged = (t + 1) * 32 > N;
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+            const f32x4 Lv = *(const f32x4*)(Ls + 8 * g4 + 4 * h);
+            const f32x4 Dv = *(const f32x4*)(Ds + 8 * g4 + 4 * h);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int r = 4 * g4 + e;
+                float p = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -Lv[e]));
+                if (ragged && t * 32 + acc_row(r, h) >= N) p = 0.f;
+                sacc[r] = p;                       // P
+                pacc[r] = p * (pacc[r] - Dv[e]) * DsScale<T>::v;  // dS (scaled)
+            }
+        }
+        // dV^T[d][key] += dO^T[d][q] P[q][key] ;  dK^T[d][key] += Q^T[d][q] dS[q][key]
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const typename Mfma<T>::frag pf = pack_frag<T>(sacc, s);
+            const typename Mfma<T>::frag sf = pack_frag<T>(pacc, s);
+#pragma unroll
+            for (int db = 0; db < 2; ++db) {
+                dv[db] = Mfma<T>::mma(tr_frag<T>(Gt, 0, s, db, lane), pf, dv[db]);
+                dk[db] = Mfma<T>::mma(tr_frag<T>(Qt, 0, s, db, lane), sf, dk[db]);
+            }
+        }
+        __syncthreads();
+    }
+    scale *= 1.0f / DsScale<T>::v;
+    if (key < N) {
+        T* rk = dqkv + ((int64_t)b * N + key) * ld + C + hd * HD;
+        T* rv = rk + C;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                const int d = db * 32 + 8 * g4 + 4 * h;
+                typedef T t4 __attribute__((ext_vector_type(4)));
+                t4 a = {(T)(dk[db][4 * g4] * scale), (T)(dk[db][4 * g4 + 1] * scale),
+                        (T)(dk[db][4 * g4 + 2] * scale), (T)(dk[db][4 * g4 + 3] * scale)};
+                t4 v = {(T)dv[db][4 * g4], (T)dv[db][4 * g4 + 1], (T)dv[db][4 * g4 + 2], (T)dv[db][4 * g4 + 3]};
+                *(t4*)(rk + d) = a;
+                *(t4*)(rv + d) = v;
+            }
+    }
+}
+
+template <typename T>
+void fwd_launch(const void* qkv, void* o, float* lse, int B, int N, int H, float scale, hipStream_t st) {
+    dim3 grid((N + 127) / 128, B * H);
+    attn_fwd_kernel<T><<<grid, 256, 0, st>>>((const T*)qkv, (T*)o, lse, N, H, scale * LOG2E);
+}
+
+template <typename T>
+void bwd_launch(const void* qkv, const void* o, const void* dout, const float* lse, float* delta, void* dqkv,
+                int B, int N, int H, float scale, hipStream_t st) {
+    const int64_t total = (int64_t)B * N * H;
+    attn_delta_kernel<T><<<(unsigned)((total + 255) / 256), 256, 0, st>>>((const T*)o, (const T*)dout, delta, N, H,
+                                                                          total);
+    dim3 grid((N + 127) / 128, B * H);
+    attn_bwd_dq_kernel<T><<<grid, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, (T*)dqkv, N, H,
+                                                scale * LOG2E, scale);
+    attn_bwd_dkdv_kernel<T><<<grid, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, (T*)dqkv, N, H,
+                                                  scale * LOG2E, scale);
+}
+
+}  // namespace
+
+extern "C" int dclip_attn_fwd(int dt, const void* qkv, void* o, float* lse, int B, int N, int H, int D,
+                              float scale, void* stream) {
+    DCLIP_HOST_CHECK(D == HD, "dclip_attn_fwd: head_dim must be 64 (got %d)", D);
+    DCLIP_HOST_CHECK(dt == DCLIP_BF16 || dt == DCLIP_F16, "dclip_attn_fwd: dtype must be f16/bf16");
+    DCLIP_HOST_CHECK(B > 0 && N > 0 && H > 0, "dclip_attn_fwd: empty problem");
+    DCLIP_HOST_CHECK(((uintptr_t)qkv % 16) == 0 && ((uintptr_t)o % 16) == 0, "dclip_attn_fwd: unaligned buffers");
+    hipStream_t st = (hipStream_t)stream;
+    if (dt == DCLIP_BF16) fwd_launch<bf16>(qkv, o, lse, B, N, H, scale, st);
+    else fwd_launch<f16>(qkv, o, lse, B, N, H, scale, st);
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int dclip_attn_bwd(int dt, const void* qkv, const void* o, const void* dout, const float* lse,
+                              float* delta_ws, void* dqkv, int B, int N, int H, int D, float scale, void* stream) {
+    DCLIP_HOST_CHECK(D == HD, "dclip_attn_bwd: head_dim must be 64 (got %d)", D);
+    DCLIP_HOST_CHECK(dt == DCLIP_BF16 || dt == DCLIP_F16, "dclip_attn_bwd: dtype must be f16/bf16");
+    DCLIP_HOST_CHECK(B > 0 && N > 0 && H > 0, "dclip_attn_bwd: empty problem");
+    hipStream_t st = (hipStream_t)stream;
+    if (dt == DCLIP_BF16) bwd_launch<bf16>(qkv, o, dout, lse, delta_ws, dqkv, B, N, H, scale, st);
+    else bwd_launch<f16>(qkv, o, dout, lse, delta_ws, dqkv, B, N, H, scale, st);
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}

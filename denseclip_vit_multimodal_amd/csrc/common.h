@@ -1,0 +1,101 @@
+// Shared device helpers for the DenseCLIP gfx950 kernels.
+//
+// Data types on this path: activations/weights feeding MFMA are bf16 or fp16
+// (fp32 accumulate); the residual stream, LayerNorm statistics and all gradient
+// sums are fp32.  Wave = 64 lanes; MFMA shape v_mfma_f32_32x32x16_{bf16,f16}.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dclip.h"
+
+typedef __bf16 bf16;
+typedef _Float16 f16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+
+#define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
+
+#define DCLIP_HOST_CHECK(cond, ...)                                   \
+    do {                                                              \
+        if (!(cond)) {                                                \
+            dclip_set_error(__VA_ARGS__);                             \
+            return DCLIP_ERR_ARG;                                     \
+        }                                                             \
+    } while (0)
+
+#define DCLIP_LAUNCH_CHECK()                                          \
+    do {                                                              \
+        hipError_t e_ = hipGetLastError();                            \
+        if (e_ != hipSuccess) {                                       \
+            dclip_set_error("HIP launch failed: %s", hipGetErrorString(e_)); \
+            return DCLIP_ERR_HIP;                                     \
+        }                                                             \
+    } while (0)
+
+void dclip_set_error(const char* fmt, ...);
+
+// ----------------------------------------------------------------------------- scalar io
+template <typename T> __device__ __forceinline__ float to_f32(T v) { return (float)v; }
+template <typename T> __device__ __forceinline__ T from_f32(float v) { return (T)v; }
+
+// load/store of one element of a runtime-typed buffer (host dispatches on dtype
+// where it matters for speed; this is for the cold paths)
+__device__ __forceinline__ float load_dyn(const void* p, int dt, int64_t i) {
+    if (dt == DCLIP_F32) return ((const float*)p)[i];
+    if (dt == DCLIP_F16) return (float)((const f16*)p)[i];
+    return (float)((const bf16*)p)[i];
+}
+__device__ __forceinline__ void store_dyn(void* p, int dt, int64_t i, float v) {
+    if (dt == DCLIP_F32) ((float*)p)[i] = v;
+    else if (dt == DCLIP_F16) ((f16*)p)[i] = (f16)v;
+    else ((bf16*)p)[i] = (bf16)v;
+}
+
+// ----------------------------------------------------------------------------- wave ops
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// ----------------------------------------------------------------------------- MFMA
+template <typename T> struct Mfma;
+template <> struct Mfma<bf16> {
+    typedef bf16x8 frag;
+    static __device__ __forceinline__ f32x16 mma(frag a, frag b, f32x16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+    }
+};
+template <> struct Mfma<f16> {
+    typedef f16x8 frag;
+    static __device__ __forceinline__ f32x16 mma(frag a, frag b, f32x16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+    }
+};
+
+__device__ __forceinline__ float quick_gelu(float z) {
+    return z / (1.0f + __expf(-1.702f * z));
+}
+__device__ __forceinline__ float quick_gelu_grad(float z) {
+    float s = 1.0f / (1.0f + __expf(-1.702f * z));
+    return s + 1.702f * z * s * (1.0f - s);
+}
+
+// bijective XCD-aware remap of a linear block id (8 XCDs, round-robin dispatch):
+// consecutive logical tiles land on the same XCD so they share its L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
+    const int q = nblk / 8, r = nblk % 8;
+    const int xcd = bid % 8, loc = bid / 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}

@@ -1,0 +1,233 @@
+// LayerNorm forward/backward with fp32 statistics (reference seg/denseclip/models.py:243-249:
+// the reference casts to fp32, runs nn.LayerNorm (eps 1e-5, biased variance) and casts
+// back).  One wave per row, the row held in registers, wave-shuffle reductions.
+// HBM-bound: forward reads the row once (f32) and writes it once (bf16/f16/f32);
+// backward reads dy and x once and writes dx once, with dw/db summed in registers over a
+// grid-strided set of rows and flushed once per block.
+#include "common.h"
+
+namespace {
+
+constexpr int MAXV = 32;  // elements per lane => cols <= 2048
+
+template <typename T>
+__device__ __forceinline__ void load4(const T* p, float* v) {
+    if constexpr (sizeof(T) == 4) {
+        f32x4 x = *(const f32x4*)p;
+        v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3];
+    } else {
+        typedef T t4 __attribute__((ext_vector_type(4)));
+        t4 x = *(const t4*)p;
+        v[0] = (float)x[0]; v[1] = (float)x[1]; v[2] = (float)x[2]; v[3] = (float)x[3];
+    }
+}
+template <typename T>
+__device__ __forceinline__ void store4(T* p, const float* v) {
+    if constexpr (sizeof(T) == 4) {
+        f32x4 x = {v[0], v[1], v[2], v[3]};
+        *(f32x4*)p = x;
+    } else {
+        typedef T t4 __attribute__((ext_vector_type(4)));
+        t4 x = {(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
+        *(t4*)p = x;
+    }
+}
+
+// cols % 4 == 0; lane owns columns 4*lane + 256*i .. +3
+template <typename TX, typename TY>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const TX* __restrict__ x, const float* __restrict__ w,
+                                                     const float* __restrict__ b, TY* __restrict__ y,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                     int64_t rows, int cols, float eps) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const TX* xr = x + row * cols;
+    float v[MAXV];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXV / 4; ++i) {
+        const int c = 4 * lane + 256 * i;
+        if (c < cols) {
+            load4(xr + c, v + 4 * i);
+            s += v[4 * i] + v[4 * i + 1] + v[4 * i + 2] + v[4 * i + 3];
+        }
+    }
+    const float mu = wave_sum(s) / cols;
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXV / 4; ++i) {
+        const int c = 4 * lane + 256 * i;
+        if (c < cols) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float d = v[4 * i + e] - mu;
+                ss += d * d;
+            }
+        }
+    }
+    const float rs = rsqrtf(wave_sum(ss) / cols + eps);
+    TY* yr = y + row * cols;
+#pragma unroll
+    for (int i = 0; i < MAXV / 4; ++i) {
+        const int c = 4 * lane + 256 * i;
+        if (c < cols) {
+            float o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = (v[4 * i + e] - mu) * rs * w[c + e] + b[c + e];
+            store4(yr + c, o);
+        }
+    }
+    if (lane == 0) {
+        if (mean_out) mean_out[row] = mu;
+        if (rstd_out) rstd_out[row] = rs;
+    }
+}
+
+template <typename TDY, typename TX>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const TDY* __restrict__ dy, const TX* __restrict__ x,
+                                                     const float* __restrict__ w, const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd, float* __restrict__ dx,
+                                                     int accumulate, float* __restrict__ dw,
+                                                     float* __restrict__ db, int64_t rows, int cols) {
+    __shared__ float red[2][4][64];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    float aw[MAXV], ab[MAXV];
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) { aw[i] = 0.f; ab[i] = 0.f; }
+    float wl[MAXV];
+#pragma unroll
+    for (int i = 0; i < MAXV / 4; ++i) {
+        const int c = 4 * lane + 256 * i;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) wl[4 * i + e] = c < cols ? w[c + e] : 0.f;
+    }
+    for (int64_t row = (int64_t)blockIdx.x * 4 + wave; row < rows; row += (int64_t)gridDim.x * 4) {
+        const float mu = mean[row], rs = rstd[row];
+        float xh[MAXV], g[MAXV];
+        float sg = 0.f, sgx = 0.f;
+#pragma unroll
+        for (int i = 0; i < MAXV / 4; ++i) {
+            const int c = 4 * lane + 256 * i;
+            if (c < cols) {
+                float dv[4], xv[4];
+                load4(dy + row * cols + c, dv);
+                load4(x + row * cols + c, xv);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int k = 4 * i + e;
+                    xh[k] = (xv[e] - mu) * rs;
+                    g[k] = dv[e] * wl[k];
+                    sg += g[k];
+                    sgx += g[k] * xh[k];
+                    aw[k] += dv[e] * xh[k];
+                    ab[k] += dv[e];
+                }
+            }
+        }
+        const float mg = wave_sum(sg) / cols;
+        const float mgx = wave_sum(sgx) / cols;
+#pragma unroll
+        for (int i = 0; i < MAXV / 4; ++i) {
+            const int c = 4 * lane + 256 * i;
+            if (c < cols) {
+                float o[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int k = 4 * i + e;
+                    o[e] = rs * (g[k] - mg - xh[k] * mgx);
+                }
+                float* d = dx + row * cols + c;
+                if (accumulate) {
+                    f32x4 old = *(f32x4*)d;
+                    o[0] += old[0]; o[1] += old[1]; o[2] += old[2]; o[3] += old[3];
+                }
+                store4(d, o);
+            }
+        }
+    }
+    // block reduction of dw/db (one column group at a time through a small LDS
+    // buffer), then one atomic per column per block
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+        if (256 * (i / 4) >= cols) break;  // block-uniform
+        red[0][wave][lane] = aw[i];
+        red[1][wave][lane] = ab[i];
+        __syncthreads();
+        if (wave == 0) {
+            const int c = 4 * lane + 256 * (i / 4) + (i % 4);
+            if (c < cols) {
+                const float sw = red[0][0][lane] + red[0][1][lane] + red[0][2][lane] + red[0][3][lane];
+                const float sb = red[1][0][lane] + red[1][1][lane] + red[1][2][lane] + red[1][3][lane];
+                if (dw) atomicAdd(dw + c, sw);
+                if (db) atomicAdd(db + c, sb);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+template <typename TX, typename TY>
+void fwd_launch(const void* x, const float* w, const float* b, void* y, float* mean, float* rstd,
+                int64_t rows, int cols, float eps, hipStream_t st) {
+    dim3 grid((unsigned)((rows + 3) / 4));
+    ln_fwd_kernel<TX, TY><<<grid, 256, 0, st>>>((const TX*)x, w, b, (TY*)y, mean, rstd, rows, cols, eps);
+}
+
+template <typename TX>
+void fwd_dispatch_y(int y_dt, const void* x, const float* w, const float* b, void* y, float* mean,
+                    float* rstd, int64_t rows, int cols, float eps, hipStream_t st) {
+    if (y_dt == DCLIP_F32) fwd_launch<TX, float>(x, w, b, y, mean, rstd, rows, cols, eps, st);
+    else if (y_dt == DCLIP_F16) fwd_launch<TX, f16>(x, w, b, y, mean, rstd, rows, cols, eps, st);
+    else fwd_launch<TX, bf16>(x, w, b, y, mean, rstd, rows, cols, eps, st);
+}
+
+template <typename TDY, typename TX>
+void bwd_launch(const void* dy, const void* x, const float* w, const float* mean, const float* rstd,
+                float* dx, int acc, float* dw, float* db, int64_t rows, int cols, hipStream_t st) {
+    int64_t blocks = (rows + 3) / 4;
+    if (blocks > 1024) blocks = 1024;
+    ln_bwd_kernel<TDY, TX><<<(unsigned)blocks, 256, 0, st>>>((const TDY*)dy, (const TX*)x, w, mean, rstd,
+                                                             dx, acc, dw, db, rows, cols);
+}
+
+template <typename TDY>
+void bwd_dispatch_x(int x_dt, const void* dy, const void* x, const float* w, const float* mean,
+                    const float* rstd, float* dx, int acc, float* dw, float* db, int64_t rows, int cols,
+                    hipStream_t st) {
+    if (x_dt == DCLIP_F32) bwd_launch<TDY, float>(dy, x, w, mean, rstd, dx, acc, dw, db, rows, cols, st);
+    else if (x_dt == DCLIP_F16) bwd_launch<TDY, f16>(dy, x, w, mean, rstd, dx, acc, dw, db, rows, cols, st);
+    else bwd_launch<TDY, bf16>(dy, x, w, mean, rstd, dx, acc, dw, db, rows, cols, st);
+}
+
+}  // namespace
+
+extern "C" int dclip_layernorm_fwd(const void* x, int x_dt, const float* w, const float* b, void* y,
+                                   int y_dt, float* mean, float* rstd, int64_t rows, int64_t cols,
+                                   float eps, void* stream) {
+    DCLIP_HOST_CHECK(cols > 0 && cols % 4 == 0 && cols <= 64 * MAXV,
+                     "dclip_layernorm_fwd: cols=%lld must be a multiple of 4 and <= %d", (long long)cols, 64 * MAXV);
+    DCLIP_HOST_CHECK(rows >= 0, "dclip_layernorm_fwd: rows < 0");
+    if (rows == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    if (x_dt == DCLIP_F32) fwd_dispatch_y<float>(y_dt, x, w, b, y, mean, rstd, rows, (int)cols, eps, st);
+    else if (x_dt == DCLIP_F16) fwd_dispatch_y<f16>(y_dt, x, w, b, y, mean, rstd, rows, (int)cols, eps, st);
+    else fwd_dispatch_y<bf16>(y_dt, x, w, b, y, mean, rstd, rows, (int)cols, eps, st);
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int dclip_layernorm_bwd(const void* dy, int dy_dt, const void* x, int x_dt, const float* w,
+                                   const float* mean, const float* rstd, float* dx, int accumulate,
+                                   float* dw, float* db, int64_t rows, int64_t cols, void* stream) {
+    DCLIP_HOST_CHECK(cols > 0 && cols % 4 == 0 && cols <= 64 * MAXV,
+                     "dclip_layernorm_bwd: cols=%lld must be a multiple of 4 and <= %d", (long long)cols, 64 * MAXV);
+    if (rows == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    if (dy_dt == DCLIP_F32) bwd_dispatch_x<float>(x_dt, dy, x, w, mean, rstd, dx, accumulate, dw, db, rows, (int)cols, st);
+    else if (dy_dt == DCLIP_F16) bwd_dispatch_x<f16>(x_dt, dy, x, w, mean, rstd, dx, accumulate, dw, db, rows, (int)cols, st);
+    else bwd_dispatch_x<bf16>(x_dt, dy, x, w, mean, rstd, dx, accumulate, dw, db, rows, (int)cols, st);
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}

@@ -1,0 +1,467 @@
+// HBM-bound kernels around the ViT blocks: patchify (im2col), token assembly, positional
+// embedding interpolation, the per-layer read-out transpose, global average pool, the
+// pixel-text score map, bilinear resize and dtype casts — forward and backward.
+// All loads/stores are 8-16 bytes per lane where the layout allows (Guideline 13).
+#include "common.h"
+
+namespace {
+
+template <typename T>
+__device__ __forceinline__ T cvt(float v) { return (T)v; }
+
+// ---------------------------------------------------------------------------- im2col
+// out[(b*gh + py)*gw + px][(c*p + ky)*p + kx] = img[b][c][py*p + ky][px*p + kx]
+// one thread per 4 consecutive kx (p % 4 == 0)
+template <typename TI, typename TO>
+__global__ void im2col_kernel(const TI* __restrict__ img, TO* __restrict__ out, int B, int Cin, int Hin, int Win,
+                              int p, int gh, int gw, int64_t total4) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total4) return;
+    const int K = Cin * p * p;
+    const int k4 = K / 4;
+    const int64_t row = i / k4;
+    const int col = (int)(i % k4) * 4;
+    const int kx = col % p, ky = (col / p) % p, cc = col / (p * p);
+    const int px = (int)(row % gw);
+    const int py = (int)((row / gw) % gh);
+    const int b = (int)(row / ((int64_t)gw * gh));
+    const TI* src = img + (((int64_t)b * Cin + cc) * Hin + (py * p + ky)) * Win + px * p + kx;
+    TO* dst = out + row * K + col;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dst[e] = (TO)(float)src[e];
+}
+
+// ---------------------------------------------------------------------------- tokens
+template <typename TP>
+__global__ void tokens_fwd_kernel(const TP* __restrict__ patch, const float* __restrict__ cls,
+                                  const float* __restrict__ pos, float* __restrict__ x, int B, int P, int C,
+                                  int64_t total4) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total4) return;
+    const int c4 = C / 4;
+    const int c = (int)(i % c4) * 4;
+    const int64_t row = i / c4;  // b*(P+1) + t
+    const int t = (int)(row % (P + 1));
+    const int64_t b = row / (P + 1);
+    f32x4 pv = *(const f32x4*)(pos + (int64_t)t * C + c);
+    f32x4 v;
+    if (t == 0) {
+        v = *(const f32x4*)(cls + c);
+    } else {
+        const TP* s = patch + (b * P + (t - 1)) * C + c;
+        v[0] = (float)s[0]; v[1] = (float)s[1]; v[2] = (float)s[2]; v[3] = (float)s[3];
+    }
+    *(f32x4*)(x + row * C + c) = v + pv;
+}
+
+template <typename TP>
+__global__ void tokens_bwd_kernel(const float* __restrict__ dx, TP* __restrict__ dpatch, float* __restrict__ dcls,
+                                  float* __restrict__ dpos, int B, int P, int C, int64_t total4) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over (P+1) * C/4
+    if (i >= total4) return;
+    const int c4 = C / 4;
+    const int c = (int)(i % c4) * 4;
+    const int t = (int)(i / c4);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < B; ++b) {
+        const f32x4 g = *(const f32x4*)(dx + ((int64_t)b * (P + 1) + t) * C + c);
+        acc += g;
+        if (t > 0 && dpatch) {
+            TP* d = dpatch + ((int64_t)b * P + (t - 1)) * C + c;
+            d[0] = (TP)g[0]; d[1] = (TP)g[1]; d[2] = (TP)g[2]; d[3] = (TP)g[3];
+        }
+    }
+    if (dpos) *(f32x4*)(dpos + (int64_t)t * C + c) += acc;
+    if (t == 0 && dcls) *(f32x4*)(dcls + c) += acc;
+}
+
+// ---------------------------------------------------------------------------- bilinear
+// PyTorch upsample_bilinear2d, align_corners=False, output size given:
+//   scale = in/out (fp32); src = max(scale*(dst+0.5)-0.5, 0); i0 = (int)src;
+//   i1 = i0 + (i0 < in-1); l1 = src - i0; l0 = 1 - l1
+struct Lerp {
+    int i0, i1;
+    float l0, l1;
+};
+__device__ __forceinline__ Lerp lerp_index(int dst, int in, int out) {
+    const float scale = (float)in / (float)out;
+    float src = scale * ((float)dst + 0.5f) - 0.5f;
+    src = src < 0.f ? 0.f : src;
+    Lerp r;
+    r.i0 = (int)src;
+    if (r.i0 > in - 1) r.i0 = in - 1;
+    r.i1 = r.i0 + (r.i0 < in - 1 ? 1 : 0);
+    r.l1 = src - (float)r.i0;
+    r.l0 = 1.f - r.l1;
+    return r;
+}
+// weight of source index `i` in the interpolation for output index `dst`
+__device__ __forceinline__ float lerp_weight(int dst, int i, int in, int out) {
+    const Lerp L = lerp_index(dst, in, out);
+    return (L.i0 == i ? L.l0 : 0.f) + (L.i1 == i ? L.l1 : 0.f);
+}
+// conservative range of output indices whose interpolation touches source index i
+__device__ __forceinline__ void lerp_range(int i, int in, int out, int* lo, int* hi) {
+    const float inv = (float)out / (float)in;
+    int a = (int)floorf(((float)i - 1.f + 0.5f) * inv - 0.5f) - 2;
+    int b = (int)ceilf(((float)i + 1.f + 0.5f) * inv - 0.5f) + 2;
+    *lo = a < 0 ? 0 : a;
+    *hi = b > out - 1 ? out - 1 : b;
+}
+
+template <typename TI, typename TO>
+__global__ void bilinear_fwd_kernel(const TI* __restrict__ in, TO* __restrict__ out, int64_t NC, int Hi, int Wi,
+                                    int Ho, int Wo) {
+    const int64_t total = NC * Ho * Wo;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int x = (int)(i % Wo);
+        const int y = (int)((i / Wo) % Ho);
+        const int64_t nc = i / ((int64_t)Wo * Ho);
+        const Lerp ly = lerp_index(y, Hi, Ho), lx = lerp_index(x, Wi, Wo);
+        const TI* p = in + nc * Hi * Wi;
+        const float v00 = (float)p[ly.i0 * Wi + lx.i0], v01 = (float)p[ly.i0 * Wi + lx.i1];
+        const float v10 = (float)p[ly.i1 * Wi + lx.i0], v11 = (float)p[ly.i1 * Wi + lx.i1];
+        out[i] = (TO)(ly.l0 * (lx.l0 * v00 + lx.l1 * v01) + ly.l1 * (lx.l0 * v10 + lx.l1 * v11));
+    }
+}
+
+// pass 1: ws[nc][y][ix] = sum_x w_x(x, ix) dout[nc][y][x]
+template <typename TG>
+__global__ void bilinear_bwd_w_kernel(const TG* __restrict__ dout, float* __restrict__ ws, int64_t NC, int Wi,
+                                      int Ho, int Wo) {
+    const int64_t total = NC * Ho * Wi;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int ix = (int)(i % Wi);
+        const int64_t row = i / Wi;  // nc*Ho + y
+        int lo, hi;
+        lerp_range(ix, Wi, Wo, &lo, &hi);
+        const TG* g = dout + row * Wo;
+        float s = 0.f;
+        for (int x = lo; x <= hi; ++x) {
+            const float w = lerp_weight(x, ix, Wi, Wo);
+            if (w != 0.f) s += w * (float)g[x];
+        }
+        ws[i] = s;
+    }
+}
+// pass 2: din[nc][iy][ix] = sum_y w_y(y, iy) ws[nc][y][ix]
+__global__ void bilinear_bwd_h_kernel(const float* __restrict__ ws, float* __restrict__ din, int64_t NC, int Hi,
+                                      int Wi, int Ho) {
+    const int64_t total = NC * Hi * Wi;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int ix = (int)(i % Wi);
+        const int iy = (int)((i / Wi) % Hi);
+        const int64_t nc = i / ((int64_t)Wi * Hi);
+        int lo, hi;
+        lerp_range(iy, Hi, Ho, &lo, &hi);
+        float s = 0.f;
+        for (int y = lo; y <= hi; ++y) {
+            const float w = lerp_weight(y, iy, Hi, Ho);
+            if (w != 0.f) s += w * ws[(nc * Ho + y) * Wi + ix];
+        }
+        din[i] = s;
+    }
+}
+
+// ---------------------------------------------------------------------------- pos interp
+// out[0] = pos[0]; out[1 + y*W + x][c] = bilinear(pos[1 + (iy*g + ix)][c])
+__global__ void pos_interp_fwd_kernel(const float* __restrict__ pos, float* __restrict__ out, int g, int C, int H,
+                                      int W) {
+    const int64_t total = (int64_t)(H * W + 1) * C;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i % C);
+        const int t = (int)(i / C);
+        if (t == 0) {
+            out[i] = pos[c];
+            continue;
+        }
+        const int y = (t - 1) / W, x = (t - 1) % W;
+        const Lerp ly = lerp_index(y, g, H), lx = lerp_index(x, g, W);
+        const float* p = pos + C;
+        const float v00 = p[(ly.i0 * g + lx.i0) * C + c], v01 = p[(ly.i0 * g + lx.i1) * C + c];
+        const float v10 = p[(ly.i1 * g + lx.i0) * C + c], v11 = p[(ly.i1 * g + lx.i1) * C + c];
+        out[i] = ly.l0 * (lx.l0 * v00 + lx.l1 * v01) + ly.l1 * (lx.l0 * v10 + lx.l1 * v11);
+    }
+}
+
+__global__ void pos_interp_bwd_kernel(const float* __restrict__ dout, float* __restrict__ dpos, int g, int C, int H,
+                                      int W) {
+    const int64_t total = (int64_t)(g * g + 1) * C;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i % C);
+        const int t = (int)(i / C);
+        if (t == 0) {
+            dpos[i] += dout[c];
+            continue;
+        }
+        const int iy = (t - 1) / g, ix = (t - 1) % g;
+        int ylo, yhi, xlo, xhi;
+        lerp_range(iy, g, H, &ylo, &yhi);
+        lerp_range(ix, g, W, &xlo, &xhi);
+        float s = 0.f;
+        for (int y = ylo; y <= yhi; ++y) {
+            const float wy = lerp_weight(y, iy, g, H);
+            if (wy == 0.f) continue;
+            for (int x = xlo; x <= xhi; ++x) {
+                const float wx = lerp_weight(x, ix, g, W);
+                if (wx != 0.f) s += wy * wx * dout[(int64_t)(1 + y * W + x) * C + c];
+            }
+        }
+        dpos[i] += s;
+    }
+}
+
+// ---------------------------------------------------------------------------- transpose
+// out[b][c][r] (=|+=) in[b][r0 + r][c]; zero for rows <= r < rows_pad; colsum[c] += sum
+template <typename TI, typename TO, bool ACC>
+__global__ __launch_bounds__(256) void transpose_kernel(const TI* __restrict__ in, int64_t in_bs, int64_t in_ld,
+                                                        int64_t r0, TO* __restrict__ out, int64_t out_bs,
+                                                        int64_t out_ld, int64_t rows, int64_t rows_pad, int64_t cols,
+                                                        float* __restrict__ colsum) {
+    __shared__ float tile[64][65];
+    const int b = blockIdx.z;
+    const int64_t rb = (int64_t)blockIdx.y * 64, cb = (int64_t)blockIdx.x * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
+    const TI* src = in + b * in_bs;
+    for (int k = ty; k < 64; k += 4) {
+        const int64_t r = rb + k, c = cb + tx;
+        float v = 0.f;
+        if (r < rows && c < cols) v = (float)src[(r0 + r) * in_ld + c];
+        tile[k][tx] = v;
+    }
+    __syncthreads();
+    if (colsum != nullptr && ty == 0 && cb + tx < cols) {
+        float s = 0.f;
+        for (int k = 0; k < 64; ++k) s += tile[k][tx];
+        atomicAdd(colsum + cb + tx, s);
+    }
+    TO* dst = out + b * out_bs;
+    for (int k = ty; k < 64; k += 4) {
+        const int64_t c = cb + k, r = rb + tx;
+        if (c < cols && r < rows_pad) {
+            const float v = tile[tx][k];
+            if constexpr (ACC) dst[c * out_ld + r] += v;
+            else dst[c * out_ld + r] = (TO)v;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------- channel mean
+template <typename TI>
+__global__ __launch_bounds__(256) void channel_mean_kernel(const TI* __restrict__ in, float* __restrict__ out,
+                                                           int64_t rows, int C) {
+    __shared__ float red[4][64];
+    const int b = blockIdx.y;
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int ty = threadIdx.x >> 6;
+    float s = 0.f;
+    if (c < C)
+        for (int64_t r = ty; r < rows; r += 4) s += (float)in[((int64_t)b * rows + r) * C + c];
+    red[ty][threadIdx.x & 63] = s;
+    __syncthreads();
+    if (ty == 0 && c < C) out[(int64_t)b * C + c] = (red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                                                     red[3][threadIdx.x]) / (float)rows;
+}
+
+// ---------------------------------------------------------------------------- score map
+// one wave per pixel; text rows normalised once per block into LDS
+template <typename TV>
+__global__ __launch_bounds__(256) void score_map_kernel(const TV* __restrict__ v, const float* __restrict__ t,
+                                                        float* __restrict__ score, int HW, int C, int K, float eps) {
+    extern __shared__ float tn[];  // K * C
+    const int b = blockIdx.y;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // normalise text embeddings of batch b (F.normalize, p=2, dim=2, eps)
+    for (int k = wave; k < K; k += 4) {
+        const float* tr = t + ((int64_t)b * K + k) * C;
+        float ss = 0.f;
+        for (int c = lane; c < C; c += 64) ss += tr[c] * tr[c];
+        ss = wave_sum(ss);
+        const float inv = 1.f / fmaxf(sqrtf(ss), eps);
+        for (int c = lane; c < C; c += 64) tn[k * C + c] = tr[c] * inv;
+    }
+    __syncthreads();
+    for (int p = blockIdx.x * 4 + wave; p < HW; p += gridDim.x * 4) {
+        const TV* vr = v + ((int64_t)b * HW + p) * C;
+        float ss = 0.f;
+        float dots[32];
+#pragma unroll
+        for (int k = 0; k < 32; ++k) dots[k] = 0.f;
+        for (int c = lane; c < C; c += 64) {
+            const float x = (float)vr[c];
+            ss += x * x;
+#pragma unroll
+            for (int k = 0; k < 32; ++k)
+                if (k < K) dots[k] += x * tn[k * C + c];
+        }
+        const float inv = 1.f / fmaxf(sqrtf(wave_sum(ss)), eps);
+#pragma unroll
+        for (int k = 0; k < 32; ++k) {
+            if (k < K) {
+                const float d = wave_sum(dots[k]);
+                if (lane == 0) score[((int64_t)b * K + k) * HW + p] = d * inv;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------- cast
+template <typename TI, typename TO>
+__global__ void cast_kernel(const TI* __restrict__ in, TO* __restrict__ out, int64_t n) {
+    for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n;
+         i += (int64_t)gridDim.x * blockDim.x * 4) {
+        if (i + 3 < n) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) out[i + e] = (TO)(float)in[i + e];
+        } else {
+            for (int64_t j = i; j < n; ++j) out[j] = (TO)(float)in[j];
+        }
+    }
+}
+
+inline unsigned grid_for(int64_t n, int64_t cap = 65536) {
+    int64_t g = (n + 255) / 256;
+    if (g > cap) g = cap;
+    if (g < 1) g = 1;
+    return (unsigned)g;
+}
+
+#define DISPATCH_DT(dt, T, ...)                                  \
+    do {                                                         \
+        if ((dt) == DCLIP_F32) { typedef float T; __VA_ARGS__; } \
+        else if ((dt) == DCLIP_F16) { typedef f16 T; __VA_ARGS__; } \
+        else { typedef bf16 T; __VA_ARGS__; }                    \
+    } while (0)
+
+}  // namespace
+
+extern "C" int dclip_im2col(const void* img, int img_dt, void* out, int out_dt, int B, int Cin, int Hin, int Win,
+                            int p, void* stream) {
+    DCLIP_HOST_CHECK(p % 4 == 0 && p > 0, "dclip_im2col: patch size must be a positive multiple of 4");
+    const int gh = Hin / p, gw = Win / p;
+    DCLIP_HOST_CHECK(gh > 0 && gw > 0, "dclip_im2col: image smaller than one patch");
+    const int64_t total4 = (int64_t)B * gh * gw * Cin * p * p / 4;
+    hipStream_t st = (hipStream_t)stream;
+    DISPATCH_DT(img_dt, TI, DISPATCH_DT(out_dt, TO,
+        im2col_kernel<TI, TO><<<(unsigned)((total4 + 255) / 256), 256, 0, st>>>((const TI*)img, (TO*)out, B, Cin, Hin,
+                                                                             Win, p, gh, gw, total4)));
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int dclip_tokens_fwd(const void* patch, int patch_dt, const float* cls, const float* pos, float* x, int B,
+                                int P, int C, void* stream) {
+    DCLIP_HOST_CHECK(C % 4 == 0, "dclip_tokens_fwd: C %% 4 != 0");
+    const int64_t total4 = (int64_t)B * (P + 1) * C / 4;
+    hipStream_t st = (hipStream_t)stream;
+    DISPATCH_DT(patch_dt, TP,
+        tokens_fwd_kernel<TP><<<(unsigned)((total4 + 255) / 256), 256, 0, st>>>((const TP*)patch, cls, pos, x, B, P,
+                                                                             C, total4));
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int dclip_tokens_bwd(const float* dx, void* dpatch, int dpatch_dt, float* dcls, float* dpos, int B, int P,
+                                int C, void* stream) {
+    DCLIP_HOST_CHECK(C % 4 == 0, "dclip_tokens_bwd: C %% 4 != 0");
+    const int64_t total4 = (int64_t)(P + 1) * C / 4;
+    hipStream_t st = (hipStream_t)stream;
+    DISPATCH_DT(dpatch_dt, TP,
+        tokens_bwd_kernel<TP><<<(unsigned)((total4 + 255) / 256), 256, 0, st>>>(dx, (TP*)dpatch, dcls, dpos, B, P, C,
+                                                                             total4));
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int dclip_pos_interp_fwd(const float* pos, float* out, int g, int C, int H, int W, void* stream) {
+    DCLIP_HOST_CHECK(g > 0 && H > 0 && W > 0, "dclip_pos_interp_fwd: bad sizes");
+    const int64_t total = (int64_t)(H * W + 1) * C;
+    pos_interp_fwd_kernel<<<grid_for(total), 256, 0, (hipStream_t)stream>>>(pos, out, g, C, H, W);
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int dclip_pos_interp_bwd(const float* dout, float* dpos, int g, int C, int H, int W, void* stream) {
+    DCLIP_HOST_CHECK(g > 0 && H > 0 && W > 0, "dclip_pos_interp_bwd: bad sizes");
+    const int64_t total = (int64_t)(g * g + 1) * C;
+    pos_interp_bwd_kernel<<<grid_for(total), 256, 0, (hipStream_t)stream>>>(dout, dpos, g, C, H, W);
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int dclip_transpose(const void* in, int in_dt, int64_t in_bstride, int64_t in_ld, int64_t r0, void* out,
+                               int out_dt, int64_t out_bstride, int64_t out_ld, int batch, int64_t rows,
+                               int64_t rows_pad, int64_t cols, int accumulate, float* colsum, void* stream) {
+    DCLIP_HOST_CHECK(rows_pad >= rows && batch > 0, "dclip_transpose: rows_pad < rows");
+    DCLIP_HOST_CHECK(!accumulate || out_dt == DCLIP_F32, "dclip_transpose: accumulate needs f32 output");
+    if (rows_pad == 0 || cols == 0) return 0;
+    dim3 grid((unsigned)((cols + 63) / 64), (unsigned)((rows_pad + 63) / 64), batch);
+    hipStream_t st = (hipStream_t)stream;
+    if (accumulate) {
+        DISPATCH_DT(in_dt, TI,
+            transpose_kernel<TI, float, true><<<grid, 256, 0, st>>>((const TI*)in, in_bstride, in_ld, r0, (float*)out,
+                                                                   out_bstride, out_ld, rows, rows_pad, cols, colsum));
+    } else {
+        DISPATCH_DT(in_dt, TI, DISPATCH_DT(out_dt, TO,
+            transpose_kernel<TI, TO, false><<<grid, 256, 0, st>>>((const TI*)in, in_bstride, in_ld, r0, (TO*)out,
+                                                                 out_bstride, out_ld, rows, rows_pad, cols, colsum)));
+    }
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int dclip_channel_mean(const void* in, int in_dt, float* out, int B, int64_t rows, int C, void* stream) {
+    DCLIP_HOST_CHECK(rows > 0 && C > 0 && B > 0, "dclip_channel_mean: empty input");
+    dim3 grid((C + 63) / 64, B);
+    hipStream_t st = (hipStream_t)stream;
+    DISPATCH_DT(in_dt, TI, channel_mean_kernel<TI><<<grid, 256, 0, st>>>((const TI*)in, out, rows, C));
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int dclip_score_map(const void* v, int v_dt, const float* t, float* score, int B, int HW, int C, int K,
+                               float eps, void* stream) {
+    DCLIP_HOST_CHECK(K > 0 && K <= 32, "dclip_score_map: K must be in [1, 32] (got %d)", K);
+    DCLIP_HOST_CHECK((size_t)K * C * 4 <= 64 * 1024, "dclip_score_map: K*C too large for LDS");
+    int bx = (HW + 3) / 4;
+    if (bx > 1024) bx = 1024;
+    dim3 grid(bx, B);
+    hipStream_t st = (hipStream_t)stream;
+    DISPATCH_DT(v_dt, TV,
+        score_map_kernel<TV><<<grid, 256, (size_t)K * C * 4, st>>>((const TV*)v, t, score, HW, C, K, eps));
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int dclip_bilinear_fwd(const void* in, int in_dt, void* out, int out_dt, int64_t NC, int Hi, int Wi, int Ho,
+                                  int Wo, void* stream) {
+    DCLIP_HOST_CHECK(Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0, "dclip_bilinear_fwd: bad sizes");
+    const int64_t total = NC * Ho * Wo;
+    hipStream_t st = (hipStream_t)stream;
+    DISPATCH_DT(in_dt, TI, DISPATCH_DT(out_dt, TO,
+        bilinear_fwd_kernel<TI, TO><<<grid_for(total), 256, 0, st>>>((const TI*)in, (TO*)out, NC, Hi, Wi, Ho, Wo)));
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int dclip_bilinear_bwd(const void* dout, int dout_dt, float* din, float* ws, int64_t NC, int Hi, int Wi,
+                                  int Ho, int Wo, void* stream) {
+    DCLIP_HOST_CHECK(Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0, "dclip_bilinear_bwd: bad sizes");
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t t1 = NC * Ho * Wi;
+    DISPATCH_DT(dout_dt, TG,
+        bilinear_bwd_w_kernel<TG><<<grid_for(t1), 256, 0, st>>>((const TG*)dout, ws, NC, Wi, Ho, Wo));
+    const int64_t t2 = NC * Hi * Wi;
+    bilinear_bwd_h_kernel<<<grid_for(t2), 256, 0, st>>>(ws, din, NC, Hi, Wi, Ho);
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int dclip_cast(const void* in, int in_dt, void* out, int out_dt, int64_t n, void* stream) {
+    if (n == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    DISPATCH_DT(in_dt, TI, DISPATCH_DT(out_dt, TO,
+        cast_kernel<TI, TO><<<grid_for((n + 3) / 4), 256, 0, st>>>((const TI*)in, (TO*)out, n)));
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}

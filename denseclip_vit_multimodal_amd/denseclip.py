@@ -1,0 +1,348 @@
+"""DenseCLIP segmentor (reference seg/denseclip/denseclip.py:60-1087), same constructor and
+forward contract, built on the HIP ViT backbone.
+
+Differences from the reference, all deliberate:
+  * errors RAISE (the reference catches everything in forward and returns None outputs,
+    denseclip.py:733-752, which hides kernel failures);
+  * no defensive `.clone()` of the 12 feature maps (denseclip.py:586, 743);
+  * the score map (denseclip.py:670-675) is computed on the HIP kernels from the
+    channel-last view of the last map: vis_proj as an MFMA GEMM and one fused
+    normalise-and-contract kernel.  It is returned by `_process_features` and, exactly as
+    in the reference, not used by the heads (denseclip.py:747);
+  * the final logits/depth resize is the HIP bilinear kernel (fp32 output).
+"""
+import logging
+from collections import OrderedDict
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .heads import FCNHead, IdentityHead
+from .models import (CLIPResNet, CLIPResNetWithAttention, CLIPTextContextEncoder, CLIPTextEncoder,
+                     CLIPVisionTransformer, ContextDecoder, ViTFeatureFusionNeck)
+from .utils import tokenize
+
+logger = logging.getLogger(__name__)
+
+
+class DenseCLIP(nn.Module):
+    def __init__(self, backbone, text_encoder, decode_head, class_names, context_length, depth_head=None,
+                 context_decoder=None, neck=None, context_feature="attention", score_concat_index=3,
+                 text_head=False, tau=0.07, auxiliary_head=None, identity_head=None, train_cfg=None,
+                 test_cfg=None, token_embed_dim=512, text_dim=512, clip_pretrained_path=None, **kwargs):
+        super().__init__()
+        self.class_names = class_names
+        self.num_classes = len(class_names)
+        self.fixed_text_context_length = context_length
+        self.context_feature = context_feature
+        self.score_concat_index = score_concat_index
+        self.text_head = text_head
+        self.tau = tau
+        self.train_cfg = train_cfg
+        self.test_cfg = test_cfg
+        self.align_corners = False
+        self.text_dim = text_dim
+
+        # ---- backbone (denseclip.py:111-126)
+        bcfg = dict(backbone)
+        btype = bcfg.pop("type")
+        if btype == "CLIPVisionTransformer":
+            self.backbone = CLIPVisionTransformer(**bcfg)
+            backbone_out = backbone.get("width", 768)
+        elif btype == "CLIPResNet":
+            self.backbone = CLIPResNet(**bcfg)
+        elif btype == "CLIPResNetWithAttention":
+            self.backbone = CLIPResNetWithAttention(**bcfg)
+        else:
+            raise ValueError(f"Unsupported backbone type: {btype}")
+
+        # ---- text encoder (denseclip.py:130-152)
+        tcfg = dict(text_encoder)
+        ttype = tcfg.pop("type")
+        enc_dim = text_encoder.get("embed_dim")
+        if enc_dim is not None and enc_dim != self.text_dim:
+            self.text_dim = enc_dim
+        tcfg["embed_dim"] = self.text_dim
+        self.is_context_encoder = False
+        if ttype == "CLIPTextEncoder":
+            tcfg["context_length"] = self.fixed_text_context_length
+            self.text_encoder = CLIPTextEncoder(**tcfg)
+        elif ttype == "CLIPTextContextEncoder":
+            if text_encoder.get("context_length") is None:
+                raise ValueError("`context_length` required in CLIPTextContextEncoder config.")
+            self.text_encoder = CLIPTextContextEncoder(**tcfg)
+            self.is_context_encoder = True
+        else:
+            raise ValueError(f"Unsupported text_encoder type: {ttype}")
+
+        if clip_pretrained_path:
+            self._load_clip(clip_pretrained_path)
+
+        # ---- projections (denseclip.py:195-200)
+        self.vis_proj = None
+        self.global_proj = None
+        if backbone_out != self.text_dim:
+            self.vis_proj = nn.Conv2d(backbone_out, self.text_dim, kernel_size=1)
+            self.global_proj = nn.Linear(backbone_out, self.text_dim)
+
+        # ---- context decoder (denseclip.py:204-211)
+        self.context_decoder = None
+        if context_decoder:
+            ccfg = dict(context_decoder)
+            if ccfg.pop("type") != "ContextDecoder":
+                raise ValueError("Unsupported context decoder type")
+            ccfg["visual_dim"] = self.text_dim
+            self.context_decoder = ContextDecoder(**ccfg)
+
+        # ---- neck (denseclip.py:214-287)
+        self.neck = None
+        head_in = backbone_out
+        if neck:
+            ntype = neck.get("type")
+            if ntype == "ViTFeatureFusionNeck":
+                outs = backbone.get("out_indices", [])
+                if not outs:
+                    raise ValueError("Backbone config must specify 'out_indices' when using ViTFeatureFusionNeck.")
+                out_ch = neck.get("out_channels")
+                if not isinstance(out_ch, int) or out_ch <= 0:
+                    raise ValueError("Neck config for 'ViTFeatureFusionNeck' requires a positive 'out_channels'.")
+                self.neck = ViTFeatureFusionNeck([backbone.get("width", 768)] * len(outs), out_ch,
+                                                 neck.get("inter_channels"))
+                head_in = out_ch
+            elif ntype == "FPN":
+                raise NotImplementedError("FPN neck (ResNet configs) is outside the ViT build")
+            else:
+                raise ValueError(f"Unsupported neck type: {ntype}")
+
+        # ---- decode head (denseclip.py:290-323)
+        self.decode_head = None
+        if decode_head:
+            dtype_ = decode_head.get("type")
+            self.align_corners = decode_head.get("align_corners", False)
+            self.num_classes = decode_head.get("num_classes", self.num_classes)
+            hin = decode_head.get("in_channels", head_in)
+            if dtype_ == "FPNHead":
+                ch = decode_head.get("channels", 256)
+                self.decode_head = FCNHead(hin, ch)
+                self.decode_head.classifier = nn.Conv2d(ch, self.num_classes, kernel_size=1)
+            elif dtype_ == "IdentityHead":
+                self.decode_head = IdentityHead()
+            else:
+                raise ValueError(f"Unsupported/unavailable decode_head type: {dtype_}")
+        self.with_decode_head = self.decode_head is not None
+
+        # ---- depth head (denseclip.py:327-357)
+        self.depth_head = None
+        self.with_depth_head = False
+        if depth_head:
+            if depth_head.get("type") == "FCNHeadDepth":
+                ch = depth_head.get("channels", 128)
+                self.depth_head = FCNHead(depth_head.get("in_channels", head_in), ch)
+                self.depth_head.classifier = nn.Conv2d(ch, 1, kernel_size=1)
+                self.with_depth_head = True
+            else:
+                logger.warning(f"Unsupported depth_head type: {depth_head.get('type')}")
+
+        self.auxiliary_head = None
+        self.with_auxiliary_head = False
+        self.identity_head = None
+        self.with_identity_head = False
+
+        # ---- class-name tokens + learnable context (denseclip.py:373-408)
+        self.texts = torch.cat([tokenize(c, context_length=self.fixed_text_context_length) for c in class_names])
+        self.contexts = None
+        self.gamma = None
+        if self.is_context_encoder:
+            n_ctx = getattr(self.text_encoder, "context_length", 77) - self.fixed_text_context_length
+            if n_ctx > 0:
+                self.contexts = nn.Parameter(torch.randn(1, n_ctx, token_embed_dim))
+                nn.init.trunc_normal_(self.contexts, std=0.02)
+            self.gamma = nn.Parameter(torch.ones(self.text_dim) * 1e-4)
+        self._init_non_clip_weights()
+
+    # ------------------------------------------------------------------ init / loading
+    def _load_clip(self, path):
+        """OpenAI CLIP TorchScript checkpoint -> backbone (visual.*) + text encoder
+        (denseclip.py:156-191).  A missing file is logged, as in the reference."""
+        try:
+            sd = torch.jit.load(path, map_location="cpu").state_dict()
+        except (FileNotFoundError, ValueError, RuntimeError) as e:
+            logger.error(f"Error loading CLIP weights from {path}: {e}")
+            return
+        vis = OrderedDict((k[7:], v) for k, v in sd.items() if k.startswith("visual."))
+        if vis:
+            self.backbone.load_state_dict(vis, strict=False)
+        txt = OrderedDict()
+        prefixes = ("transformer.", "token_embedding.", "positional_embedding", "ln_final.", "text_projection")
+        for k, v in sd.items():
+            if not k.startswith(prefixes):
+                continue
+            if k == "positional_embedding":
+                n = self.text_encoder.positional_embedding.shape[0]
+                if v.shape[0] >= n:
+                    txt[k] = v[:n]
+            elif k == "text_projection":
+                if v.shape == self.text_encoder.text_projection.shape:
+                    txt[k] = v
+            else:
+                txt[k] = v
+        if txt:
+            self.text_encoder.load_state_dict(txt, strict=False)
+
+    def _init_weights_fn(self, m):
+        name = m.__class__.__name__
+        if "Conv" in name and hasattr(m, "weight"):
+            nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            if m.bias is not None:
+                nn.init.constant_(m.bias, 0)
+        elif "Linear" in name:
+            nn.init.normal_(m.weight, 0, 0.01)
+            if m.bias is not None:
+                nn.init.constant_(m.bias, 0)
+        elif "BatchNorm" in name or "GroupNorm" in name:
+            nn.init.constant_(m.weight, 1)
+            nn.init.constant_(m.bias, 0)
+
+    def _init_non_clip_weights(self):
+        """denseclip.py:448-513."""
+        for name in ("vis_proj", "global_proj", "context_decoder", "neck", "decode_head", "depth_head"):
+            mod = getattr(self, name)
+            if mod is None:
+                continue
+            mod.apply(self._init_weights_fn)
+            if name in ("decode_head", "depth_head") and isinstance(getattr(mod, "classifier", None), nn.Conv2d):
+                nn.init.normal_(mod.classifier.weight, mean=0, std=0.01)
+                if mod.classifier.bias is not None:
+                    nn.init.constant_(mod.classifier.bias, 0)
+
+    # ------------------------------------------------------------------ forward pieces
+    def extract_feat(self, img):
+        feats = self.backbone(img)
+        if not isinstance(feats, (list, tuple)) or not feats:
+            raise RuntimeError("backbone returned no feature maps")
+        return list(feats)
+
+    def _text_embeddings(self, B, device):
+        texts = self.texts.to(device)
+        if isinstance(self.text_encoder, CLIPTextContextEncoder) and self.contexts is not None:
+            return self.text_encoder(texts, self.contexts).expand(B, -1, -1)
+        return self.text_encoder(texts).expand(B, -1, -1)
+
+    def _process_features(self, x):
+        """Global feature, projections, text embeddings, context fusion and the pixel-text
+        score map (denseclip.py:570-698).  Returns (text, features_for_head, score, x)."""
+        if not isinstance(x, (list, tuple)) or not x:
+            raise ValueError("expected a non-empty list of feature maps")
+        visual = x[-1]
+        if visual.ndim != 4:
+            raise ValueError(f"Expected last backbone feature map to be 4D, got {visual.ndim}D")
+        B, Cv, h, w = visual.shape
+        HW = h * w
+        cdt = visual.dtype if visual.dtype in (torch.bfloat16, torch.float16) else \
+            getattr(self.backbone, "compute_dtype", torch.bfloat16)
+        with torch.no_grad():
+            # channel-last pixel view of the last map (one transpose kernel)
+            pix = ops.transpose(visual.contiguous().view(B, Cv, HW), Cv, HW, cdt, batch=B,
+                                in_bstride=Cv * HW).view(B * HW, Cv)
+            g = ops.channel_mean(pix, B)                                   # adaptive_avg_pool2d
+            if self.global_proj is not None:
+                g = ops.gemm(ops.cast(g, cdt), ops.WEIGHTS.get(self.global_proj.weight, cdt),
+                             bias=self.global_proj.bias.detach(), out_dtype=torch.float32)
+            if self.vis_proj is not None:
+                v = ops.gemm(pix, ops.WEIGHTS.get(self.vis_proj.weight, cdt), bias=self.vis_proj.bias.detach())
+            else:
+                v = pix
+            text = self._text_embeddings(B, visual.device)
+            if self.context_decoder is not None:
+                Ct = v.shape[1]
+                if self.context_feature == "attention":
+                    ctx = torch.cat([g.unsqueeze(1), v.view(B, HW, Ct).float()], dim=1)
+                elif self.context_feature == "backbone":
+                    ctx = v.view(B, HW, Ct).float()
+                else:
+                    raise ValueError(f"Invalid context_feature type: {self.context_feature}")
+                text = text + self.gamma * self.context_decoder(text, ctx)
+            if v.shape[1] != text.shape[2]:
+                raise ValueError(f"Visual dim after proj ({v.shape[1]}) != Text dim ({text.shape[2]}).")
+            score = ops.score_map(v, text, B, HW).view(B, -1, h, w)
+        feats = list(x)
+        if 0 <= self.score_concat_index < len(feats):
+            tgt = feats[self.score_concat_index]
+            sc = ops.upsample(score, tgt.shape[2:]).to(tgt.dtype)
+            feats[self.score_concat_index] = torch.cat([tgt, sc], dim=1)
+        return text, feats, score, list(x)
+
+    def _heads(self, x_maps):
+        if self.neck is not None:
+            fused = self.neck(x_maps)
+            inp = fused[0] if isinstance(fused, (list, tuple)) else fused
+        else:
+            inp = x_maps[-1]
+        seg = self.decode_head(inp) if self.with_decode_head else None
+        depth = self.depth_head(inp) if self.with_depth_head else None
+        return seg, depth
+
+    def forward(self, img, img_metas=None, gt_semantic_seg=None, return_loss=True, **kwargs):
+        """denseclip.py:702-916.  Train: {'main_output','depth_output','aux_losses'};
+        eval: {'seg','depth'} resized to the image."""
+        feats = self.extract_feat(img)
+        text, _, score, _ = self._process_features(feats)
+        maps = feats
+        param = next(self.neck.parameters()) if self.neck is not None else None
+        if param is not None and maps[0].dtype != param.dtype and maps[0].is_cuda:
+            with torch.autocast("cuda", dtype=maps[0].dtype):
+                seg, depth = self._heads(maps)
+        else:
+            seg, depth = self._heads(maps)
+        if return_loss and self.training:
+            gt = None
+            for cand in (gt_semantic_seg, kwargs.get("gt_depth"), kwargs.get("depth_targets"),
+                         kwargs.get("seg_targets")):
+                if cand is not None:
+                    gt = tuple(cand.shape[-2:])
+                    break
+            if seg is not None and gt is not None and tuple(seg.shape[-2:]) != gt:
+                seg = ops.upsample(seg, gt)
+            if depth is not None and gt is not None and tuple(depth.shape[-2:]) != gt:
+                depth = ops.upsample(depth, gt)
+            return {"main_output": seg, "depth_output": depth, "aux_losses": {}}
+        hw = tuple(img.shape[2:])
+        if seg is not None and tuple(seg.shape[-2:]) != hw:
+            seg = ops.upsample(seg, hw)
+        if depth is not None and tuple(depth.shape[-2:]) != hw:
+            depth = ops.upsample(depth, hw)
+        return {"seg": seg, "depth": depth}
+
+    def inference(self, img, img_meta, rescale):
+        out = self.forward(img, img_metas=img_meta, return_loss=False)
+        seg, depth = out.get("seg"), out.get("depth")
+        if rescale and img_meta and "ori_shape" in img_meta[0]:
+            shp = tuple(img_meta[0]["ori_shape"][:2])
+            if seg is not None and tuple(seg.shape[-2:]) != shp:
+                seg = ops.upsample(seg, shp)
+            if depth is not None and tuple(depth.shape[-2:]) != shp:
+                depth = ops.upsample(depth, shp)
+        return {"seg": seg, "depth": depth}
+
+    def simple_test(self, img, img_meta, rescale=True):
+        out = self.inference(img, img_meta, rescale)
+        seg = out["seg"].argmax(dim=1).cpu().numpy()[0] if out["seg"] is not None else None
+        depth = out["depth"].squeeze(1).cpu().numpy()[0] if out["depth"] is not None else None
+        return {"seg": seg, "depth": depth}
+
+    def aug_test(self, imgs, img_metas, rescale=True):
+        segs, depths = [], []
+        for img, meta in zip(imgs, img_metas):
+            out = self.inference(img.unsqueeze(0), [meta], rescale)
+            if out["seg"] is not None:
+                segs.append(out["seg"])
+            if out["depth"] is not None:
+                depths.append(out["depth"])
+        seg = torch.stack(segs).mean(0).argmax(dim=1).squeeze(0).cpu().numpy() if segs else None
+        depth = torch.stack(depths).mean(0).squeeze().cpu().numpy() if depths else None
+        return {"seg": seg, "depth": depth}
+
+    def forward_dummy(self, img):
+        seg, _ = self._heads(self.extract_feat(img))
+        return seg

@@ -1,0 +1,481 @@
+"""DenseCLIP modules with the reference's class names, constructor kwargs and state-dict keys
+(reference seg/denseclip/models.py).  The CLIPVisionTransformer forward — the hot path —
+runs entirely on the HIP kernels of libdclip.so (see ops.py); the text encoder, context
+decoder and fusion neck keep plain torch modules (out of kernel scope).
+"""
+import logging
+import math
+from collections import OrderedDict
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+
+logger = logging.getLogger(__name__)
+
+
+class ConvBNReLU(nn.Sequential):
+    """Conv-BN-ReLU (reference models.py:13-20)."""
+
+    def __init__(self, in_channels, out_channels, kernel_size=3, padding=1, stride=1):
+        super().__init__(
+            nn.Conv2d(in_channels, out_channels, kernel_size, stride=stride, padding=padding, bias=False),
+            nn.BatchNorm2d(out_channels),
+            nn.ReLU(inplace=True),
+        )
+
+
+class Registry:
+    """Name registry (reference models.py:48-67 / heads.py:64-79)."""
+
+    def __init__(self):
+        self._registry = {}
+
+    def register_module(self, name=None):
+        def deco(cls):
+            self._registry[name or cls.__name__] = cls
+            return cls
+        return deco
+
+    def get(self, name):
+        return self._registry.get(name)
+
+    def build(self, cfg, **kwargs):
+        if isinstance(cfg, dict):
+            cfg = dict(cfg)
+            return self._registry[cfg.pop("type")](**cfg, **kwargs)
+        return self._registry[cfg](**kwargs)
+
+
+BACKBONES = Registry()
+
+
+class LayerNorm(nn.LayerNorm):
+    """LayerNorm computed in fp32 and cast back (reference models.py:243-249)."""
+
+    def forward(self, x):
+        orig = x.dtype
+        return super().forward(x.type(torch.float32)).type(orig)
+
+
+class QuickGELU(nn.Module):
+    """x * sigmoid(1.702 x) (reference models.py:252-254)."""
+
+    def forward(self, x):
+        return x * torch.sigmoid(1.702 * x)
+
+
+def drop_path(x, drop_prob=0.0, training=False):
+    if drop_prob == 0.0 or not training:
+        return x
+    keep = 1 - drop_prob
+    shape = (x.shape[0],) + (1,) * (x.ndim - 1)
+    return x.div(keep) * (keep + torch.rand(shape, dtype=x.dtype, device=x.device)).floor_()
+
+
+class DropPath(nn.Module):
+    def __init__(self, drop_prob=None):
+        super().__init__()
+        self.drop_prob = drop_prob
+
+    def forward(self, x):
+        return drop_path(x, self.drop_prob, self.training)
+
+    def extra_repr(self):
+        return f"p={self.drop_prob}"
+
+
+class ResidualAttentionBlock(nn.Module):
+    """Pre-LN block (reference models.py:271-294).  `forward` is the plain-torch path used by
+    the text encoder (masked, LND); the ViT drives the same parameters through the fused
+    HIP block (ops.BlockFn)."""
+
+    def __init__(self, d_model, n_head, attn_mask=None, drop_path=0.0):
+        super().__init__()
+        self.attn = nn.MultiheadAttention(d_model, n_head)
+        self.ln_1 = LayerNorm(d_model)
+        self.mlp = nn.Sequential(OrderedDict([
+            ("c_fc", nn.Linear(d_model, d_model * 4)),
+            ("gelu", QuickGELU()),
+            ("c_proj", nn.Linear(d_model * 4, d_model)),
+        ]))
+        self.ln_2 = LayerNorm(d_model)
+        self.attn_mask = attn_mask
+        self.n_head = n_head
+        self.drop_path = DropPath(drop_path) if drop_path > 0.0 else nn.Identity()
+
+    def attention(self, x):
+        m = self.attn_mask.to(dtype=x.dtype, device=x.device) if self.attn_mask is not None else None
+        return self.attn(x, x, x, need_weights=False, attn_mask=m)[0]
+
+    def forward(self, x):
+        x = x + self.drop_path(self.attention(self.ln_1(x)))
+        return x + self.drop_path(self.mlp(self.ln_2(x)))
+
+    def hip_params(self):
+        return (self.ln_1.weight, self.ln_1.bias, self.attn.in_proj_weight, self.attn.in_proj_bias,
+                self.attn.out_proj.weight, self.attn.out_proj.bias, self.ln_2.weight, self.ln_2.bias,
+                self.mlp.c_fc.weight, self.mlp.c_fc.bias, self.mlp.c_proj.weight, self.mlp.c_proj.bias)
+
+
+class Transformer(nn.Module):
+    """Reference models.py:297-307.  NOTE: `forward` applies every block and then the whole
+    Sequential again — the reference's behaviour, reproduced for parity (text encoder)."""
+
+    def __init__(self, width, layers, heads, attn_mask=None, drop_path_rate=0.0):
+        super().__init__()
+        self.width = width
+        self.layers = layers
+        dpr = [x.item() for x in torch.linspace(0, drop_path_rate, layers)]
+        self.resblocks = nn.Sequential(*[ResidualAttentionBlock(width, heads, attn_mask, dpr[i])
+                                         for i in range(layers)])
+
+    def forward(self, x):
+        for blk in self.resblocks:
+            x = blk(x)
+        return self.resblocks(x)
+
+
+# ============================================================================ ViT backbone
+@BACKBONES.register_module()
+class CLIPVisionTransformer(nn.Module):
+    """CLIP ViT image encoder with per-layer dense read-out (reference models.py:378-597).
+
+    forward(x: (B, 3, H, W)) -> list of (B, width, H // p, W // p) maps, one per
+    out_index in ascending order, in x.dtype.  Runs on the HIP kernels only (x must be a
+    GPU tensor).  The compute dtype of the GEMM/attention operands is bf16 for bf16 input,
+    fp16 for fp16 input and `compute_dtype` (default bf16) for fp32 input; the residual
+    stream and LayerNorms are fp32 throughout.
+    """
+
+    def __init__(self, input_resolution=224, patch_size=16, width=768, layers=12, heads=12, output_dim=768,
+                 drop_path_rate=0.0, out_indices=None, pretrained=None, compute_dtype=torch.bfloat16, **kwargs):
+        super().__init__()
+        self.pretrained = pretrained
+        self.input_resolution = input_resolution
+        self.output_dim = width
+        self.layers = layers
+        self.width = width
+        self.heads = heads
+        self.patch_size = patch_size
+        self.compute_dtype = compute_dtype
+        self.drop_path_rate = drop_path_rate
+        self.conv1 = nn.Conv2d(3, width, kernel_size=patch_size, stride=patch_size, bias=False)
+        scale = width ** -0.5
+        self.class_embedding = nn.Parameter(scale * torch.randn(width))
+        self.grid_size = input_resolution // patch_size
+        self.positional_embedding = nn.Parameter(scale * torch.randn(self.grid_size ** 2 + 1, width))
+        self.ln_pre = LayerNorm(width)
+        self.transformer = Transformer(width, layers, heads, drop_path_rate=drop_path_rate)
+        self.ln_post = LayerNorm(width)
+        self._clip_proj_dim = 512
+        self.proj = nn.Parameter(scale * torch.randn(width, self._clip_proj_dim))
+        if out_indices is None:
+            self.out_indices = [layers - 1]
+        else:
+            if not isinstance(out_indices, (list, tuple)):
+                raise TypeError("out_indices must be list or tuple")
+            for i in out_indices:
+                if not 0 <= i < layers:
+                    raise ValueError(f"Index {i} in out_indices is out of range for {layers} layers.")
+            self.out_indices = sorted(set(out_indices))
+        self.init_weights()
+
+    def _init_weights_default(self, m):
+        if isinstance(m, nn.Linear):
+            nn.init.xavier_uniform_(m.weight)
+            if m.bias is not None:
+                nn.init.constant_(m.bias, 0)
+        elif isinstance(m, nn.LayerNorm):
+            nn.init.constant_(m.bias, 0)
+            nn.init.constant_(m.weight, 1.0)
+        elif isinstance(m, nn.Conv2d):
+            nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            if m.bias is not None:
+                nn.init.constant_(m.bias, 0)
+
+    def init_weights(self, pretrained=None):
+        """OpenAI CLIP TorchScript weights (visual.* keys), pos-embed resized bilinearly to
+        this grid (reference models.py:459-512); default init otherwise."""
+        pretrained = pretrained or self.pretrained
+        if not isinstance(pretrained, str):
+            logger.warning("No pretrained weights specified for ViT. Applying default initialization.")
+            self.apply(self._init_weights_default)
+            return
+        try:
+            ckpt = torch.jit.load(pretrained, map_location="cpu").float().state_dict()
+        except FileNotFoundError:
+            logger.error(f"Pretrained ViT file not found: {pretrained}")
+            return
+        sd = OrderedDict((k[len("visual."):], v) for k, v in ckpt.items() if k.startswith("visual."))
+        if "positional_embedding" in sd and sd["positional_embedding"].shape != self.positional_embedding.shape:
+            pe = sd["positional_embedding"]
+            g0 = int(np.sqrt(pe.shape[0] - 1))
+            if g0 * g0 != pe.shape[0] - 1:
+                sd.pop("positional_embedding")
+            else:
+                grid = pe[1:].reshape(1, g0, g0, -1).permute(0, 3, 1, 2)
+                grid = F.interpolate(grid, size=(self.grid_size, self.grid_size), mode="bilinear",
+                                     align_corners=False)
+                sd["positional_embedding"] = torch.cat([pe[:1], grid.permute(0, 2, 3, 1).reshape(-1, pe.shape[1])])
+        if "proj" in sd and sd["proj"].shape != self.proj.shape:
+            sd.pop("proj")
+        msg = self.load_state_dict(sd, strict=False)
+        logger.info(f"ViT weights loaded: {msg}")
+
+    def _cdt(self, x):
+        if x.dtype in (torch.bfloat16, torch.float16):
+            return x.dtype
+        return self.compute_dtype
+
+    def forward(self, x):
+        if not x.is_cuda:
+            raise RuntimeError("CLIPVisionTransformer runs on the MI355X HIP kernels only (got a CPU tensor)")
+        if self.width != self.heads * 64:
+            raise NotImplementedError(f"the fused attention kernel needs head_dim 64 (width {self.width}, "
+                                      f"heads {self.heads})")
+        if self.training and self.drop_path_rate > 0:
+            raise NotImplementedError("drop_path_rate > 0 in training is not supported by the fused HIP block")
+        B, _, Hin, Win = x.shape
+        p = self.patch_size
+        gh, gw = Hin // p, Win // p
+        Ntok = gh * gw + 1
+        cdt = self._cdt(x)
+        tok = ops.PatchEmbedFn.apply(x, self.conv1.weight, self.class_embedding, self.positional_embedding,
+                                     self.ln_pre.weight, self.ln_pre.bias, p, cdt)
+        outs = []
+        meta = (B, Ntok, self.heads, cdt)
+        rmeta = (B, Ntok, gh, gw, x.dtype)
+        last = max(self.out_indices) if self.out_indices else -1
+        for i, blk in enumerate(self.transformer.resblocks):
+            if i > last:
+                break  # later blocks feed nothing the reference returns
+            tok = ops.BlockFn.apply(tok, meta, *blk.hip_params())
+            if i in self.out_indices:
+                if i == self.layers - 1:
+                    outs.append(ops.ReadoutFn.apply(tok, self.ln_post.weight, self.ln_post.bias, rmeta))
+                else:
+                    outs.append(ops.ReadoutFn.apply(tok, None, None, rmeta))
+        return outs
+
+
+class CLIPResNet(nn.Module):
+    """Importable for API compatibility; ResNet backbones are outside the ViT hot path."""
+
+    def __init__(self, *args, **kwargs):
+        super().__init__()
+        raise NotImplementedError("CLIPResNet is out of scope of the MI355X ViT build (SURVEY §2 row 8)")
+
+
+class CLIPResNetWithAttention(CLIPResNet):
+    pass
+
+
+# ============================================================================ text path
+class CLIPTextEncoder(nn.Module):
+    """Reference models.py:600-714 (plain torch; batch-independent and frozen)."""
+
+    def __init__(self, context_length=77, vocab_size=49408, transformer_width=512, transformer_heads=8,
+                 transformer_layers=12, embed_dim=512, pretrained=None, **kwargs):
+        super().__init__()
+        self.pretrained = pretrained
+        self.context_length = context_length
+        self.transformer = Transformer(transformer_width, transformer_layers, transformer_heads,
+                                       attn_mask=self.build_attention_mask())
+        self.vocab_size = vocab_size
+        self.token_embedding = nn.Embedding(vocab_size, transformer_width)
+        self.positional_embedding = nn.Parameter(torch.empty(context_length, transformer_width))
+        self.ln_final = LayerNorm(transformer_width)
+        self.text_projection = nn.Parameter(torch.empty(transformer_width, embed_dim))
+        self._output_dim = embed_dim
+        self.apply(self._init_weights_default)
+        nn.init.normal_(self.positional_embedding, std=0.01)
+        nn.init.normal_(self.text_projection, std=transformer_width ** -0.5)
+
+    def _init_weights_default(self, m):
+        if isinstance(m, nn.Linear):
+            nn.init.xavier_uniform_(m.weight)
+            if m.bias is not None:
+                nn.init.constant_(m.bias, 0)
+        elif isinstance(m, nn.LayerNorm):
+            nn.init.constant_(m.bias, 0)
+            nn.init.constant_(m.weight, 1.0)
+        elif isinstance(m, nn.Embedding):
+            nn.init.normal_(m.weight, std=0.02)
+
+    def build_attention_mask(self):
+        return torch.full((self.context_length, self.context_length), float("-inf")).triu_(1)
+
+    def forward(self, text):
+        x = self.token_embedding(text)
+        pos = self.positional_embedding[: x.shape[1]]
+        x = (x + pos.to(x.dtype)).permute(1, 0, 2)
+        x = self.transformer(x).permute(1, 0, 2)
+        x = self.ln_final(x)
+        return x[torch.arange(x.shape[0]), text.argmax(dim=-1)] @ self.text_projection
+
+
+class CLIPTextContextEncoder(nn.Module):
+    """Reference models.py:785-864: class tokens with learnable context tokens inserted after
+    SOT, causal mask, EOT read-out.  Plain torch."""
+
+    def __init__(self, context_length=22, vocab_size=49408, transformer_width=512, transformer_heads=8,
+                 transformer_layers=12, embed_dim=512, out_dim=256, pretrained=None, **kwargs):
+        super().__init__()
+        self.pretrained = pretrained
+        self.context_length = context_length
+        self.transformer = Transformer(transformer_width, transformer_layers, transformer_heads,
+                                       attn_mask=self.build_attention_mask())
+        self.embed_dim = embed_dim
+        self.vocab_size = vocab_size
+        self.token_embedding = nn.Embedding(vocab_size, transformer_width)
+        self.positional_embedding = nn.Parameter(torch.empty(context_length, transformer_width))
+        self.ln_final = LayerNorm(transformer_width)
+        self.text_projection = nn.Parameter(torch.empty(transformer_width, embed_dim))
+        # the reference leaves these two as uninitialised torch.empty (models.py:811,813);
+        # give them defined values so an un-loaded model is finite
+        nn.init.normal_(self.positional_embedding, std=0.01)
+        nn.init.normal_(self.text_projection, std=transformer_width ** -0.5)
+
+    def init_weights(self, pretrained=None):
+        pretrained = pretrained or self.pretrained
+        if not isinstance(pretrained, str):
+            return
+        ckpt = torch.jit.load(pretrained, map_location="cpu").float().state_dict()
+        sd = {}
+        for k, v in ckpt.items():
+            if k.startswith("transformer.") or k.startswith("token_embedding") or k.startswith("ln_final") \
+                    or k in ("positional_embedding", "text_projection"):
+                if k == "positional_embedding" and v.shape[0] > self.context_length:
+                    v = v[: self.context_length]
+                sd[k] = v
+        self.load_state_dict(sd, strict=False)
+
+    def build_attention_mask(self):
+        return torch.full((self.context_length, self.context_length), float("-inf")).triu_(1)
+
+    def forward(self, text, context):
+        x_text = self.token_embedding(text)
+        K, N1, C = x_text.shape
+        B, N2, _ = context.shape
+        eos = (text.argmax(dim=-1) + N2).reshape(1, K).expand(B, K).reshape(-1)
+        x_text = x_text.reshape(1, K, N1, C).expand(B, K, N1, C)
+        context = context.reshape(B, 1, N2, C).expand(B, K, N2, C)
+        x = torch.cat([x_text[:, :, 0:1], context, x_text[:, :, 1:]], dim=2).reshape(B * K, N1 + N2, C)
+        x = (x + self.positional_embedding).permute(1, 0, 2)
+        x = self.transformer(x).permute(1, 0, 2)
+        x = self.ln_final(x)
+        x = x[torch.arange(x.shape[0]), eos] @ self.text_projection
+        return x.reshape(B, K, self.embed_dim)
+
+
+# ============================================================================ neck
+class ViTFeatureFusionNeck(nn.Module):
+    """Reference models.py:717-782: per-level 3x3 ConvBNReLU, concat, 1x1 ConvBNReLU."""
+
+    def __init__(self, in_channels_list, out_channels, inter_channels=None):
+        super().__init__()
+        if not isinstance(in_channels_list, (list, tuple)):
+            raise TypeError("in_channels_list must be a list or tuple")
+        inter_channels = inter_channels or out_channels
+        self.num_inputs = len(in_channels_list)
+        self.process_layers = nn.ModuleList(
+            [ConvBNReLU(c, inter_channels, kernel_size=3, padding=1) for c in in_channels_list])
+        self.fusion_layer = ConvBNReLU(inter_channels * self.num_inputs, out_channels, kernel_size=1, padding=0)
+        self.apply(self._init_weights)
+
+    def _init_weights(self, m):
+        if isinstance(m, nn.Conv2d):
+            nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+        elif isinstance(m, (nn.BatchNorm2d, nn.GroupNorm)):
+            nn.init.constant_(m.weight, 1)
+            nn.init.constant_(m.bias, 0)
+
+    def forward(self, features):
+        if len(features) != self.num_inputs:
+            raise ValueError(f"ViTFeatureFusionNeck got {len(features)} inputs, expected {self.num_inputs}")
+        feats = [layer(f) for layer, f in zip(self.process_layers, features)]
+        return [self.fusion_layer(torch.cat(feats, dim=1))]
+
+
+# ============================================================================ context decoder
+class Attention(nn.Module):
+    """Reference models.py:311-344."""
+
+    def __init__(self, dim, num_heads=8, qkv_bias=False, qk_scale=None, attn_drop=0.0, proj_drop=0.0):
+        super().__init__()
+        self.num_heads = num_heads
+        self.scale = qk_scale or (dim // num_heads) ** -0.5
+        self.q_proj = nn.Linear(dim, dim, bias=qkv_bias)
+        self.k_proj = nn.Linear(dim, dim, bias=qkv_bias)
+        self.v_proj = nn.Linear(dim, dim, bias=qkv_bias)
+        self.attn_drop = nn.Dropout(attn_drop)
+        self.proj = nn.Linear(dim, dim)
+        self.proj_drop = nn.Dropout(proj_drop)
+
+    def forward(self, q, k, v):
+        B, Nq, C = q.shape
+        Mk = k.shape[1]
+        h = self.num_heads
+        q = self.q_proj(q).reshape(B, Nq, h, C // h)
+        k = self.k_proj(k).reshape(B, Mk, h, C // h)
+        v = self.v_proj(v).reshape(B, Mk, h, C // h)
+        attn = (torch.einsum("bnkc,bmkc->bknm", q, k) * self.scale).softmax(dim=-1)
+        x = torch.einsum("bknm,bmkc->bnkc", attn, v).reshape(B, Nq, C)
+        return self.proj_drop(self.proj(x))
+
+
+class TransformerDecoderLayer(nn.Module):
+    """Reference models.py:346-375."""
+
+    def __init__(self, d_model, nhead, dropout=0.1):
+        super().__init__()
+        self.self_attn = Attention(d_model, nhead, proj_drop=dropout)
+        self.cross_attn = Attention(d_model, nhead, proj_drop=dropout)
+        self.norm1 = nn.LayerNorm(d_model)
+        self.norm2 = nn.LayerNorm(d_model)
+        self.norm3 = nn.LayerNorm(d_model)
+        self.dropout = nn.Dropout(dropout)
+        self.mlp = nn.Sequential(nn.Linear(d_model, d_model * 4), nn.GELU(), nn.Dropout(dropout),
+                                 nn.Linear(d_model * 4, d_model))
+
+    def forward(self, x, mem):
+        q = k = v = self.norm1(x)
+        x = x + self.self_attn(q, k, v)
+        q = self.norm2(x)
+        x = x + self.cross_attn(q, mem, mem)
+        return x + self.dropout(self.mlp(self.norm3(x)))
+
+
+class ContextDecoder(nn.Module):
+    """Reference models.py:867-917 (text queries cross-attend over the visual context)."""
+
+    def __init__(self, transformer_width=256, transformer_heads=4, transformer_layers=6, visual_dim=1024,
+                 dropout=0.1, **kwargs):
+        super().__init__()
+        self.memory_proj = nn.Sequential(nn.LayerNorm(visual_dim), nn.Linear(visual_dim, transformer_width),
+                                         nn.LayerNorm(transformer_width))
+        self.text_proj = nn.Sequential(nn.LayerNorm(visual_dim), nn.Linear(visual_dim, transformer_width))
+        self.decoder = nn.ModuleList([TransformerDecoderLayer(transformer_width, transformer_heads, dropout)
+                                      for _ in range(transformer_layers)])
+        self.out_proj = nn.Sequential(nn.LayerNorm(transformer_width), nn.Linear(transformer_width, visual_dim))
+        self.apply(self._init_weights)
+
+    def _init_weights(self, m):
+        if isinstance(m, nn.Linear):
+            nn.init.trunc_normal_(m.weight, std=0.02)
+            if m.bias is not None:
+                nn.init.constant_(m.bias, 0)
+        elif isinstance(m, nn.LayerNorm):
+            nn.init.constant_(m.bias, 0)
+            nn.init.constant_(m.weight, 1.0)
+
+    def forward(self, text, visual):
+        visual = self.memory_proj(visual)
+        x = self.text_proj(text)
+        for layer in self.decoder:
+            x = layer(x, visual)
+        return self.out_proj(x)

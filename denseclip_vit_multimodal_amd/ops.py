@@ -1,0 +1,449 @@
+"""Torch-facing wrappers of the HIP C ABI and the autograd Functions of the ViT path.
+
+Every op launches one or more kernels of libdclip.so on the current HIP stream of the
+current device; tensors are only plumbing (device memory + the caching allocator).
+There is no CPU fallback: a CPU tensor or a missing library raises.
+
+Numerics (the contract checked by tests/test_gpu_parity.py):
+  * the residual stream, LayerNorm statistics, bias/LN gradients and weight gradients are
+    fp32; GEMM/attention operands are the compute dtype (bf16 or fp16) with fp32 MFMA
+    accumulation; softmax statistics are fp32.
+"""
+import math
+
+import torch
+
+from . import _native as N
+
+_DT = {torch.float32: N.F32, torch.float16: N.F16, torch.bfloat16: N.BF16}
+
+
+def _dt(t):
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise TypeError(f"unsupported dtype {t.dtype}") from None
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+# Optional per-op device timing: set TIMING = {} to collect name -> [(start, end)] HIP
+# events recorded on the launching stream around each op (bench.py uses it to derive the
+# per-launch kernel duration inside its timed region).
+TIMING = None
+
+
+def _tic():
+    if TIMING is None:
+        return None
+    e = torch.cuda.Event(enable_timing=True)
+    e.record()
+    return e
+
+
+def _toc(name, e0):
+    if e0 is None:
+        return
+    e1 = torch.cuda.Event(enable_timing=True)
+    e1.record()
+    TIMING.setdefault(name, []).append((e0, e1))
+
+
+def timing_summary():
+    """name -> (launches, total ms, mean ms); synchronises."""
+    torch.cuda.synchronize()
+    out = {}
+    for k, evs in (TIMING or {}).items():
+        tot = sum(a.elapsed_time(b) for a, b in evs)
+        out[k] = (len(evs), tot, tot / max(1, len(evs)))
+    return out
+
+
+def _check(*ts):
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError("denseclip HIP op got a CPU tensor: the MI355X path has no CPU fallback")
+        if not t.is_contiguous():
+            raise RuntimeError("denseclip HIP op needs contiguous tensors")
+
+
+# ============================================================================ raw ops
+def layernorm_fwd(x2d, w, b, out_dtype, eps=1e-5, stats=True):
+    _check(x2d, w, b)
+    rows, cols = x2d.shape
+    y = torch.empty(rows, cols, dtype=out_dtype, device=x2d.device)
+    mean = torch.empty(rows, dtype=torch.float32, device=x2d.device) if stats else None
+    rstd = torch.empty(rows, dtype=torch.float32, device=x2d.device) if stats else None
+    N.call("dclip_layernorm_fwd", _p(x2d), _dt(x2d), _p(w), _p(b), _p(y), _DT[out_dtype], _p(mean), _p(rstd),
+           rows, cols, float(eps), _stream())
+    return y, mean, rstd
+
+
+def layernorm_bwd(dy, x, w, mean, rstd, dx, accumulate, dw=None, db=None):
+    _check(dy, x, w, mean, rstd, dx, dw, db)
+    rows, cols = x.shape
+    N.call("dclip_layernorm_bwd", _p(dy), _dt(dy), _p(x), _dt(x), _p(w), _p(mean), _p(rstd), _p(dx),
+           int(accumulate), _p(dw), _p(db), rows, cols, _stream())
+
+
+def gemm(A, B, epi=N.EPI_STORE, bias=None, aux=None, out_dtype=None, out=None, out2=None):
+    """out[m][n] = sum_k A[m][k] B[n][k] (+ epilogue).  A: (M, K), B: (N, K)."""
+    _check(A, B, bias, aux, out, out2)
+    M, K = A.shape
+    Nn, K2 = B.shape
+    assert K == K2, (A.shape, B.shape)
+    if out is None:
+        odt = out_dtype or (torch.float32 if epi == N.EPI_RESIDUAL else A.dtype)
+        out = torch.empty(M, Nn, dtype=odt, device=A.device)
+    if epi == N.EPI_GELU and out2 is None:
+        out2 = torch.empty(M, Nn, dtype=A.dtype, device=A.device)
+    e0 = _tic()
+    N.call("dclip_gemm", epi, _dt(A), _p(A), A.stride(0), _p(B), B.stride(0), M, Nn, K, 1, _p(bias), _p(aux),
+           _dt(aux) if aux is not None else 0, aux.stride(0) if aux is not None else 0, _p(out), _dt(out),
+           out.stride(0), _p(out2), out2.stride(0) if out2 is not None else 0, _stream())
+    _toc("gemm", e0)
+    return (out, out2) if epi == N.EPI_GELU else out
+
+
+def transpose(x, rows, cols, out_dtype, r0=0, batch=1, in_bstride=0, rows_pad=None, colsum=None, out=None,
+              accumulate=False):
+    """out[b][c][r] = x[b][r0 + r][c]  ->  (batch, cols, rows_pad) (2D if batch == 1 and out given 2D)."""
+    _check(x, colsum, out)
+    rows_pad = rows if rows_pad is None else rows_pad
+    if out is None:
+        out = torch.empty(batch, cols, rows_pad, dtype=out_dtype, device=x.device)
+    ld_in = x.shape[-1]
+    N.call("dclip_transpose", _p(x), _dt(x), in_bstride, ld_in, r0, _p(out), _dt(out), cols * rows_pad, rows_pad,
+           batch, rows, rows_pad, cols, int(accumulate), _p(colsum), _stream())
+    return out
+
+
+def cast(x, dtype):
+    _check(x)
+    if x.dtype == dtype:
+        return x
+    y = torch.empty(x.shape, dtype=dtype, device=x.device)
+    N.call("dclip_cast", _p(x), _dt(x), _p(y), _DT[dtype], x.numel(), _stream())
+    return y
+
+
+def weight_grad(dy, x, want_bias=True):
+    """dW = dy^T x (N x K, fp32) and db = colsum(dy) for dy (M, N), x (M, K) (compute dtype).
+
+    Both operands are transposed to k(=m)-contiguous layouts with zero padding of M to a
+    multiple of 64*splits, then one split-K MFMA GEMM with a deterministic slab combine.
+    """
+    M, Nn = dy.shape
+    K = x.shape[1]
+    tiles = math.ceil(Nn / 128) * math.ceil(K / 128)
+    splits = max(1, min(16, round(512 / tiles)))
+    while splits > 1 and M < 64 * splits * 4:
+        splits //= 2
+    m_pad = math.ceil(M / (64 * splits)) * 64 * splits
+    db = torch.zeros(Nn, dtype=torch.float32, device=dy.device) if want_bias else None
+    dyT = transpose(dy, M, Nn, dy.dtype, rows_pad=m_pad, colsum=db).view(Nn, m_pad)
+    xT = transpose(x, M, K, x.dtype, rows_pad=m_pad).view(K, m_pad)
+    dW = torch.empty(Nn, K, dtype=torch.float32, device=dy.device)
+    ws = torch.empty(splits, Nn, K, dtype=torch.float32, device=dy.device)
+    N.call("dclip_gemm", N.EPI_SPLITK, _dt(dyT), _p(dyT), m_pad, _p(xT), m_pad, Nn, K, m_pad, splits, None,
+           _p(ws), N.F32, 0, _p(dW), N.F32, K, None, 0, _stream())
+    return dW, db
+
+
+def attn_fwd(qkv, B, Ntok, H, scale):
+    _check(qkv)
+    C = qkv.shape[1] // 3
+    o = torch.empty(B * Ntok, C, dtype=qkv.dtype, device=qkv.device)
+    lse = torch.empty(B * H * Ntok, dtype=torch.float32, device=qkv.device)
+    e0 = _tic()
+    N.call("dclip_attn_fwd", _dt(qkv), _p(qkv), _p(o), _p(lse), B, Ntok, H, C // H, float(scale), _stream())
+    _toc("attn_fwd", e0)
+    return o, lse
+
+
+def attn_bwd(qkv, o, dout, lse, B, Ntok, H, scale):
+    _check(qkv, o, dout, lse)
+    C = o.shape[1]
+    delta = torch.empty(B * H * Ntok, dtype=torch.float32, device=qkv.device)
+    dqkv = torch.empty_like(qkv)
+    e0 = _tic()
+    N.call("dclip_attn_bwd", _dt(qkv), _p(qkv), _p(o), _p(dout), _p(lse), _p(delta), _p(dqkv), B, Ntok, H, C // H,
+           float(scale), _stream())
+    _toc("attn_bwd", e0)
+    return dqkv
+
+
+def im2col(img, p, out_dtype):
+    _check(img)
+    B, Cin, Hin, Win = img.shape
+    gh, gw = Hin // p, Win // p
+    out = torch.empty(B * gh * gw, Cin * p * p, dtype=out_dtype, device=img.device)
+    N.call("dclip_im2col", _p(img), _dt(img), _p(out), _DT[out_dtype], B, Cin, Hin, Win, p, _stream())
+    return out
+
+
+def pos_interp(pos, g, H, W):
+    _check(pos)
+    out = torch.empty(H * W + 1, pos.shape[1], dtype=torch.float32, device=pos.device)
+    N.call("dclip_pos_interp_fwd", _p(pos), _p(out), g, pos.shape[1], H, W, _stream())
+    return out
+
+
+def pos_interp_bwd(dout, dpos, g, H, W):
+    _check(dout, dpos)
+    N.call("dclip_pos_interp_bwd", _p(dout), _p(dpos), g, dpos.shape[1], H, W, _stream())
+
+
+def channel_mean(x2d, B):
+    _check(x2d)
+    rows = x2d.shape[0] // B
+    out = torch.empty(B, x2d.shape[1], dtype=torch.float32, device=x2d.device)
+    N.call("dclip_channel_mean", _p(x2d), _dt(x2d), _p(out), B, rows, x2d.shape[1], _stream())
+    return out
+
+
+def score_map(v2d, text, B, HW, eps=1e-12):
+    """v2d: (B*HW, C) pixel embeddings; text (B, K, C) f32 -> (B, K, HW) f32."""
+    text = text.float().contiguous()
+    _check(v2d, text)
+    K, C = text.shape[1], text.shape[2]
+    out = torch.empty(B, K, HW, dtype=torch.float32, device=v2d.device)
+    N.call("dclip_score_map", _p(v2d), _dt(v2d), _p(text), _p(out), B, HW, C, K, float(eps), _stream())
+    return out
+
+
+def bilinear(x, Ho, Wo, out_dtype=torch.float32):
+    _check(x)
+    n, c, Hi, Wi = x.shape
+    out = torch.empty(n, c, Ho, Wo, dtype=out_dtype, device=x.device)
+    N.call("dclip_bilinear_fwd", _p(x), _dt(x), _p(out), _DT[out_dtype], n * c, Hi, Wi, Ho, Wo, _stream())
+    return out
+
+
+def bilinear_bwd(dout, Hi, Wi):
+    dout = dout.contiguous()
+    _check(dout)
+    n, c, Ho, Wo = dout.shape
+    din = torch.empty(n, c, Hi, Wi, dtype=torch.float32, device=dout.device)
+    ws = torch.empty(n * c * Ho * Wi, dtype=torch.float32, device=dout.device)
+    N.call("dclip_bilinear_bwd", _p(dout), _dt(dout), _p(din), _p(ws), n * c, Hi, Wi, Ho, Wo, _stream())
+    return din
+
+
+# ============================================================================ weight cache
+class _Cast:
+    """Per-parameter cache of the compute-dtype copy (and its transpose) of a master
+    fp32 weight; refreshed whenever the parameter's version counter moves."""
+
+    def __init__(self):
+        self._c = {}
+
+    def get(self, p, dtype, transposed=False):
+        w = p.detach()
+        key = (id(p), dtype, transposed)
+        ent = self._c.get(key)
+        if ent is not None and ent[0] == w._version and ent[1] == w.data_ptr():
+            return ent[2]
+        w2 = w.reshape(w.shape[0], -1)
+        if transposed:
+            v = transpose(w2.contiguous(), w2.shape[0], w2.shape[1], dtype).view(w2.shape[1], w2.shape[0])
+        else:
+            v = cast(w2.contiguous(), dtype)
+        self._c[key] = (w._version, w.data_ptr(), v)
+        return v
+
+
+WEIGHTS = _Cast()
+
+
+# ============================================================================ autograd
+class PatchEmbedFn(torch.autograd.Function):
+    """conv1 (patchify GEMM) + CLS + interpolated pos-embed + ln_pre
+    (reference models.py:543-559).  Returns the fp32 residual stream (B*N, C)."""
+
+    @staticmethod
+    def forward(ctx, img, conv_w, cls, pos, ln_w, ln_b, patch, cdt):
+        B, _, Hin, Win = img.shape
+        C = conv_w.shape[0]
+        gh, gw = Hin // patch, Win // patch
+        P = gh * gw
+        g = int(math.isqrt(pos.shape[0] - 1))
+        # models.py:518: the embedding is used as-is whenever the token COUNT matches
+        interp = (P != pos.shape[0] - 1)
+        posf = pos_interp(pos.detach().contiguous(), g, gh, gw) if interp else pos.detach().contiguous()
+        patches = im2col(img.contiguous(), patch, cdt)
+        emb = gemm(patches, WEIGHTS.get(conv_w, cdt), out_dtype=torch.float32)
+        x_pre = torch.empty(B * (P + 1), C, dtype=torch.float32, device=img.device)
+        N.call("dclip_tokens_fwd", _p(emb), N.F32, _p(cls.detach().float().contiguous()), _p(posf), _p(x_pre),
+               B, P, C, _stream())
+        x, mean, rstd = layernorm_fwd(x_pre, ln_w.detach(), ln_b.detach(), torch.float32)
+        ctx.save_for_backward(patches, x_pre, mean, rstd, ln_w)
+        ctx.meta = (B, P, C, g, gh, gw, interp, cdt, tuple(conv_w.shape))
+        return x
+
+    @staticmethod
+    def backward(ctx, dx):
+        patches, x_pre, mean, rstd, ln_w = ctx.saved_tensors
+        B, P, C, g, gh, gw, interp, cdt, wshape = ctx.meta
+        dx = dx.contiguous()
+        need = ctx.needs_input_grad
+        dlnw = torch.zeros(C, dtype=torch.float32, device=dx.device)
+        dlnb = torch.zeros(C, dtype=torch.float32, device=dx.device)
+        dxp = torch.empty_like(x_pre)
+        layernorm_bwd(dx, x_pre, ln_w.detach(), mean, rstd, dxp, 0, dlnw, dlnb)
+        demb = torch.empty(B * P, C, dtype=cdt, device=dx.device)
+        dcls = torch.zeros(C, dtype=torch.float32, device=dx.device)
+        dposf = torch.zeros(P + 1, C, dtype=torch.float32, device=dx.device)
+        N.call("dclip_tokens_bwd", _p(dxp), _p(demb), _DT[cdt], _p(dcls), _p(dposf), B, P, C, _stream())
+        dpos = None
+        if need[3]:
+            if interp:
+                dpos = torch.zeros(g * g + 1, C, dtype=torch.float32, device=dx.device)
+                pos_interp_bwd(dposf, dpos, g, gh, gw)
+            else:
+                dpos = dposf
+        dconv = None
+        if need[1]:
+            dW, _ = weight_grad(demb, patches, want_bias=False)
+            dconv = dW.view(wshape)
+        return (None, dconv, dcls if need[2] else None, dpos, dlnw if need[4] else None,
+                dlnb if need[5] else None, None, None)
+
+
+class BlockFn(torch.autograd.Function):
+    """One ResidualAttentionBlock on the fp32 residual stream (reference models.py:291-294):
+        x = x + out_proj(attn(qkv(ln_1(x))))
+        x = x + c_proj(quick_gelu(c_fc(ln_2(x))))
+    LN -> GEMM(+bias) -> fused attention -> GEMM(+bias+residual) -> LN -> GEMM(+bias+QuickGELU)
+    -> GEMM(+bias+residual): 7 kernels, no elementwise passes."""
+
+    @staticmethod
+    def forward(ctx, x, meta, ln1w, ln1b, w_in, b_in, w_out, b_out, ln2w, ln2b, w1, b1, w2, b2):
+        B, Ntok, H, cdt = meta
+        C = x.shape[1]
+        scale = (C // H) ** -0.5
+        xh1, mu1, rs1 = layernorm_fwd(x, ln1w.detach(), ln1b.detach(), cdt)
+        qkv = gemm(xh1, WEIGHTS.get(w_in, cdt), bias=b_in.detach())
+        o, lse = attn_fwd(qkv, B, Ntok, H, scale)
+        xm = gemm(o, WEIGHTS.get(w_out, cdt), N.EPI_RESIDUAL, bias=b_out.detach(), aux=x)
+        xh2, mu2, rs2 = layernorm_fwd(xm, ln2w.detach(), ln2b.detach(), cdt)
+        z, h = gemm(xh2, WEIGHTS.get(w1, cdt), N.EPI_GELU, bias=b1.detach())
+        xo = gemm(h, WEIGHTS.get(w2, cdt), N.EPI_RESIDUAL, bias=b2.detach(), aux=xm)
+        ctx.save_for_backward(x, mu1, rs1, xh1, qkv, o, lse, xm, mu2, rs2, xh2, z, h,
+                              ln1w, w_in, w_out, ln2w, w1, w2)
+        ctx.meta = meta
+        return xo
+
+    @staticmethod
+    def backward(ctx, dxo):
+        (x, mu1, rs1, xh1, qkv, o, lse, xm, mu2, rs2, xh2, z, h,
+         ln1w, w_in, w_out, ln2w, w1, w2) = ctx.saved_tensors
+        B, Ntok, H, cdt = ctx.meta
+        C = x.shape[1]
+        scale = (C // H) ** -0.5
+        need = ctx.needs_input_grad
+        dxo = dxo.contiguous()
+        wg = any(need[2:])
+
+        # ---- MLP: xo = xm + h W2^T + b2,  h = qgelu(z),  z = xh2 W1^T + b1
+        dy = cast(dxo, cdt)
+        dz = gemm(dy, WEIGHTS.get(w2, cdt, transposed=True), N.EPI_GELU_BWD, aux=z)
+        dW2 = db2 = dW1 = db1 = None
+        if wg:
+            dW2, db2 = weight_grad(dy, h)
+        dxh2 = gemm(dz, WEIGHTS.get(w1, cdt, transposed=True), out_dtype=torch.float32)
+        if wg:
+            dW1, db1 = weight_grad(dz, xh2)
+        del dz
+        dxm = dxo.clone()
+        dln2w = torch.zeros(C, dtype=torch.float32, device=x.device)
+        dln2b = torch.zeros(C, dtype=torch.float32, device=x.device)
+        layernorm_bwd(dxh2, xm, ln2w.detach(), mu2, rs2, dxm, 1, dln2w, dln2b)
+        del dxh2
+        # ---- attention: xm = x + o Wout^T + bout
+        dyo = cast(dxm, cdt)
+        do = gemm(dyo, WEIGHTS.get(w_out, cdt, transposed=True))
+        dWo = dbo = dWi = dbi = None
+        if wg:
+            dWo, dbo = weight_grad(dyo, o)
+        del dyo
+        dqkv = attn_bwd(qkv, o, do, lse, B, Ntok, H, scale)
+        del do
+        dxh1 = gemm(dqkv, WEIGHTS.get(w_in, cdt, transposed=True), out_dtype=torch.float32)
+        if wg:
+            dWi, dbi = weight_grad(dqkv, xh1)
+        del dqkv
+        dln1w = torch.zeros(C, dtype=torch.float32, device=x.device)
+        dln1b = torch.zeros(C, dtype=torch.float32, device=x.device)
+        layernorm_bwd(dxh1, x, ln1w.detach(), mu1, rs1, dxm, 1, dln1w, dln1b)
+        g = lambda i, t: t if need[i] else None  # noqa: E731
+        return (dxm if need[0] else None, None, g(2, dln1w), g(3, dln1b), g(4, dWi), g(5, dbi), g(6, dWo),
+                g(7, dbo), g(8, dln2w), g(9, dln2b), g(10, dW1), g(11, db1), g(12, dW2), g(13, db2))
+
+
+class ReadoutFn(torch.autograd.Function):
+    """Per-layer dense read-out (reference models.py:568-582): optional ln_post (only for the
+    last block, models.py:574-576), drop CLS, (B, N, C) -> contiguous (B, C, H, W)."""
+
+    @staticmethod
+    def forward(ctx, x, ln_w, ln_b, meta):
+        B, Ntok, gh, gw, out_dtype = meta
+        C = x.shape[1]
+        mean = rstd = None
+        src = x
+        if ln_w is not None:
+            src, mean, rstd = layernorm_fwd(x, ln_w.detach(), ln_b.detach(), torch.float32)
+        out = transpose(src, gh * gw, C, out_dtype, r0=1, batch=B, in_bstride=Ntok * C)
+        ctx.save_for_backward(x if ln_w is not None else None, mean, rstd, ln_w)
+        ctx.meta = meta
+        ctx.has_ln = ln_w is not None
+        return out.view(B, C, gh, gw)
+
+    @staticmethod
+    def backward(ctx, dmap):
+        x, mean, rstd, ln_w = ctx.saved_tensors
+        B, Ntok, gh, gw, _ = ctx.meta
+        C = dmap.shape[1]
+        dmap = dmap.contiguous()
+        dy = torch.zeros(B * Ntok, C, dtype=torch.float32, device=dmap.device)
+        # dy[b][1 + p][c] = dmap[b][c][p]: transpose of the (C, HW) planes into rows 1..HW
+        P = gh * gw
+        N.call("dclip_transpose", _p(dmap), _dt(dmap), C * P, P, 0, _p(dy) + C * 4, N.F32, Ntok * C, C, B, C, C, P,
+               1, None, _stream())
+        if not ctx.has_ln:
+            return dy, None, None, None
+        dx = torch.empty_like(dy)
+        dw = torch.zeros(C, dtype=torch.float32, device=dy.device)
+        db = torch.zeros(C, dtype=torch.float32, device=dy.device)
+        layernorm_bwd(dy, x, ln_w.detach(), mean, rstd, dx, 0, dw, db)
+        return dx, dw, db, None
+
+
+class UpsampleFn(torch.autograd.Function):
+    """F.interpolate(mode='bilinear', align_corners=False) to (Ho, Wo), fp32 output
+    (reference denseclip.py:847, 860, 899, 909)."""
+
+    @staticmethod
+    def forward(ctx, x, Ho, Wo):
+        ctx.shape = x.shape
+        ctx.in_dtype = x.dtype
+        return bilinear(x.contiguous(), Ho, Wo, torch.float32)
+
+    @staticmethod
+    def backward(ctx, dout):
+        _, _, Hi, Wi = ctx.shape
+        din = bilinear_bwd(dout, Hi, Wi)
+        return din.to(ctx.in_dtype) if ctx.in_dtype != torch.float32 else din, None, None
+
+
+def upsample(x, size):
+    Ho, Wo = int(size[0]), int(size[1])
+    return UpsampleFn.apply(x, Ho, Wo)

@@ -1,0 +1,159 @@
+/*
+ * dclip.h — C ABI of libdclip.so, the MI355X (gfx950) DenseCLIP ViT hot path.
+ *
+ * Every entry point takes plain device pointers, element counts/strides and a
+ * hipStream_t (passed as void*), launches asynchronously on that stream and returns
+ * 0 on success or a negative DCLIP_ERR_* code; dclip_last_error() then holds a
+ * message (thread-local).  No entry point allocates, synchronises or touches the
+ * host side of a tensor, so a caller may capture any sequence in a hipGraph.
+ *
+ * dtype codes: DCLIP_F32 / DCLIP_F16 / DCLIP_BF16.  Matrices are row-major with
+ * explicit leading dimensions (in elements).
+ *
+ * Reference interface each entry point replaces (paths relative to
+ * /root/reference/segmentation):
+ *   dclip_layernorm_fwd/bwd    denseclip/models.py:243-249  LayerNorm.forward (fp32 math)
+ *   dclip_gemm                 nn.Linear in models.py:275-281 (MHA in/out proj, c_fc,
+ *                              c_proj), conv1 patchify models.py:407/546 as GEMM,
+ *                              vis_proj / global_proj denseclip.py:198-199,605-616,
+ *                              and every weight/input gradient of those
+ *   dclip_attn_fwd/bwd         nn.MultiheadAttention core (SDPA) models.py:287-289
+ *   dclip_im2col               conv1 (16x16, stride 16, no bias) models.py:407,546
+ *   dclip_tokens_fwd/bwd       flatten/transpose + CLS + pos add, models.py:548-556
+ *   dclip_pos_interp_fwd/bwd   interpolate_pos_encoding models.py:514-540
+ *   dclip_transpose            per-layer read-out NLC->NCHW models.py:568-582 (and its
+ *                              gradient), NCHW->NHWC for vis_proj, GEMM operand
+ *                              transposes with fused bias-gradient column sums
+ *   dclip_channel_mean         F.adaptive_avg_pool2d(...,(1,1)) denseclip.py:596
+ *   dclip_score_map            F.normalize x2 + einsum('bchw,bkc->bkhw')
+ *                              denseclip.py:672-675
+ *   dclip_bilinear_fwd/bwd     F.interpolate(bilinear, align_corners=False)
+ *                              denseclip.py:847,860,899,909 (logits/depth upsample)
+ *   dclip_cast                 dtype conversion of operands (.type()/.to() casts)
+ */
+#ifndef DCLIP_H
+#define DCLIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DCLIP_F32 0
+#define DCLIP_F16 1
+#define DCLIP_BF16 2
+
+#define DCLIP_OK 0
+#define DCLIP_ERR_ARG (-1)
+#define DCLIP_ERR_HIP (-2)
+
+/* GEMM epilogues (dclip_gemm) */
+#define DCLIP_EPI_STORE 0      /* C = acc (+ bias[n])                                  */
+#define DCLIP_EPI_GELU 1       /* C = z = acc + bias ; C2 = z * sigmoid(1.702 z)       */
+#define DCLIP_EPI_RESIDUAL 2   /* C(f32) = aux(f32) + acc + bias   (aux may alias C)   */
+#define DCLIP_EPI_GELU_BWD 3   /* C = acc * quick_gelu'(aux)       (aux = z)           */
+#define DCLIP_EPI_SPLITK 4     /* C(f32) = sum over K splits (+ bias): partial f32 slabs
+                                  in the caller's workspace aux (splits*M*N f32), then
+                                  one deterministic combine pass (weight gradients)    */
+
+const char* dclip_last_error(void);
+int dclip_abi_version(void);
+
+/* LayerNorm over the last dim (cols), eps, affine w/b (fp32).  y = (x-mu)*rstd*w+b.
+ * mean/rstd (rows) are written when non-null.                                        */
+int dclip_layernorm_fwd(const void* x, int x_dt, const float* w, const float* b,
+                        void* y, int y_dt, float* mean, float* rstd,
+                        int64_t rows, int64_t cols, float eps, void* stream);
+
+/* LayerNorm backward.  dy: grad wrt y (dy_dt), x: the LN input (x_dt), mean/rstd from
+ * the forward.  dx (f32) is overwritten (accumulate=0) or added to (accumulate=1).
+ * dw/db (f32, cols) are ACCUMULATED (callers zero them first).                       */
+int dclip_layernorm_bwd(const void* dy, int dy_dt, const void* x, int x_dt,
+                        const float* w, const float* mean, const float* rstd,
+                        float* dx, int accumulate, float* dw, float* db,
+                        int64_t rows, int64_t cols, void* stream);
+
+/* C[m][n] = sum_k A[m][k] * B[n][k]  ("NT": both operands k-contiguous, ab_dt in
+ * {F16, BF16}), m < M, n < N, k < K (K % 64 == 0, lda/ldb % 8 == 0), then the
+ * epilogue.  bias: f32[N] or null.  aux: epilogue side input (see DCLIP_EPI_*).
+ * splits > 1 (EPI_SPLITK only) splits K into `splits` equal 64-multiple chunks.      */
+int dclip_gemm(int epilogue, int ab_dt,
+               const void* A, int64_t lda, const void* B, int64_t ldb,
+               int64_t M, int64_t N, int64_t K, int splits,
+               const float* bias, const void* aux, int aux_dt, int64_t ld_aux,
+               void* C, int c_dt, int64_t ldc, void* C2, int64_t ldc2, void* stream);
+
+/* Fused multi-head attention over a packed QKV buffer.
+ * qkv: (B*N, 3*H*D) row-major, [q | k | v] each (H, D) head-major (the layout of
+ *      x @ in_proj_weight^T + in_proj_bias, models.py:289 / F.multi_head_attention_forward)
+ * o:   (B*N, H*D) softmax(q k^T * scale) v, heads concatenated
+ * lse: (B, H, N) f32, log2-domain row statistic  max*c + log2(sum), c = scale*log2(e)
+ * D must be 64.                                                                      */
+int dclip_attn_fwd(int dt, const void* qkv, void* o, float* lse,
+                   int B, int N, int H, int D, float scale, void* stream);
+
+/* Attention backward (flash-style recompute from lse; no N x N buffer, no atomics):
+ * a delta pass (rowsum(dout*o)), a query-major dQ pass and a key-major dK/dV pass.
+ * dout: (B*N, H*D) dt.  delta_ws: f32 (B*H*N) workspace.
+ * dqkv: (B*N, 3*H*D) dt output, [dq | dk | dv] in the qkv layout.                   */
+int dclip_attn_bwd(int dt, const void* qkv, const void* o, const void* dout,
+                   const float* lse, float* delta_ws, void* dqkv,
+                   int B, int N, int H, int D, float scale, void* stream);
+
+/* Non-overlapping p x p patches of img (B, Cin, Hin, Win) (img_dt) ->
+ * out (B*gh*gw, Cin*p*p) (out_dt), column order (c, ky, kx) = conv weight flattening,
+ * gh = Hin / p, gw = Win / p (floor, as Conv2d stride p).                            */
+int dclip_im2col(const void* img, int img_dt, void* out, int out_dt,
+                 int B, int Cin, int Hin, int Win, int p, void* stream);
+
+/* Token assembly: x[b][0] = cls + pos[0]; x[b][1+i] = patch[b*P+i] + pos[1+i]
+ * x: f32 (B*(P+1), C).  patch: (B*P, C) patch_dt.  pos: f32 (P+1, C).              */
+int dclip_tokens_fwd(const void* patch, int patch_dt, const float* cls, const float* pos,
+                     float* x, int B, int P, int C, void* stream);
+
+/* Token assembly backward: dpatch[b*P+i] = dx[b][1+i] (dpatch_dt);
+ * dcls += sum_b dx[b][0]; dpos[t] += sum_b dx[b][t]  (dcls/dpos f32, accumulated)   */
+int dclip_tokens_bwd(const float* dx, void* dpatch, int dpatch_dt, float* dcls, float* dpos,
+                     int B, int P, int C, void* stream);
+
+/* Bilinear (align_corners=False) resize of the g x g patch grid of pos (g*g+1, C)
+ * to H x W; out (H*W+1, C), row 0 = pos row 0.                                       */
+int dclip_pos_interp_fwd(const float* pos, float* out, int g, int C, int H, int W,
+                         void* stream);
+/* Its gradient: dpos (g*g+1, C) += interp^T(dout); dout (H*W+1, C).                 */
+int dclip_pos_interp_bwd(const float* dout, float* dpos, int g, int C, int H, int W,
+                         void* stream);
+
+/* Batched transpose: out[b][c][r] (=, or += if accumulate) in[b][r0 + r][c]
+ * for r < rows, c < cols; rows..rows_pad-1 of every out row are written as 0.
+ * colsum (f32, cols) += sum over b, r of in[b][r0+r][c] when non-null.
+ * Strides in elements.  accumulate requires out_dt == F32.                          */
+int dclip_transpose(const void* in, int in_dt, int64_t in_bstride, int64_t in_ld, int64_t r0,
+                    void* out, int out_dt, int64_t out_bstride, int64_t out_ld,
+                    int batch, int64_t rows, int64_t rows_pad, int64_t cols,
+                    int accumulate, float* colsum, void* stream);
+
+/* out[b][c] = mean over r < rows of in[b*rows + r][c]  (in: (B*rows, C) in_dt)        */
+int dclip_channel_mean(const void* in, int in_dt, float* out, int B, int64_t rows, int C,
+                       void* stream);
+
+/* Pixel-text score map.  v: (B*HW, C) v_dt (pixel embeddings, channel-contiguous),
+ * t: f32 (B, K, C).  score f32 (B, K, HW) = <v/max(|v|,eps), t/max(|t|,eps)>.        */
+int dclip_score_map(const void* v, int v_dt, const float* t, float* score,
+                    int B, int HW, int C, int K, float eps, void* stream);
+
+/* Bilinear resize, align_corners=False, of NC planes (NC, Hi, Wi) -> (NC, Ho, Wo).   */
+int dclip_bilinear_fwd(const void* in, int in_dt, void* out, int out_dt,
+                       int64_t NC, int Hi, int Wi, int Ho, int Wo, void* stream);
+/* Its gradient: din f32 (NC, Hi, Wi) = resize^T(dout).  ws: f32 (NC, Ho, Wi).        */
+int dclip_bilinear_bwd(const void* dout, int dout_dt, float* din, float* ws,
+                       int64_t NC, int Hi, int Wi, int Ho, int Wo, void* stream);
+
+/* Element-wise dtype conversion of n elements.                                      */
+int dclip_cast(const void* in, int in_dt, void* out, int out_dt, int64_t n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DCLIP_H */

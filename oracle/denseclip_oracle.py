@@ -36,6 +36,12 @@ import torch.nn.functional as F
 
 LN_EPS = 1e-5
 
+# When True, the unmasked attention core uses torch's scaled_dot_product_attention — the
+# very op the reference reaches through nn.MultiheadAttention (CPU flash kernel, no N x N
+# buffer).  bench.py's cpu_baseline sets it so fwd+bwd at N = 8193 fits in host memory;
+# the parity tests keep the explicit softmax restatement (False).
+USE_SDPA = False
+
 
 # ----------------------------------------------------------------------------- primitives
 def layer_norm(x, w, b, eps=LN_EPS):
@@ -71,6 +77,9 @@ def mha(x, in_w, in_b, out_w, out_b, heads, attn_mask=None, q_chunk=1024):
     k = k.reshape(L, B * heads, d).transpose(0, 1)
     v = v.reshape(L, B * heads, d).transpose(0, 1)
     scale = d ** -0.5
+    if USE_SDPA and attn_mask is None:
+        out = F.scaled_dot_product_attention(q, k, v)
+        return linear(out.transpose(0, 1).reshape(L, B, C), out_w, out_b)
     out = torch.empty_like(q)
     for s in range(0, L, q_chunk):
         e = min(L, s + q_chunk)

@@ -40,8 +40,8 @@ CITYSCAPES_CFG = dict(
 )
 
 TINY_CFG = dict(
-    backbone=dict(type='CLIPVisionTransformer', patch_size=16, width=64, layers=3, heads=2,
-                  input_resolution=32, output_dim=64, out_indices=[0, 1, 2]),
+    backbone=dict(type='CLIPVisionTransformer', patch_size=16, width=128, layers=3, heads=2,
+                  input_resolution=32, output_dim=128, out_indices=[0, 1, 2]),
     text_encoder=dict(type='CLIPTextContextEncoder', context_length=8, vocab_size=49408,
                       transformer_width=64, transformer_heads=2, transformer_layers=2,
                       embed_dim=32),

@@ -1,0 +1,258 @@
+"""Per-kernel numerics on the GPU, each HIP entry point against a plain fp32 torch reference of
+the same op (inputs are the same rounded 16-bit values, so the tolerance only covers the
+kernel's own rounding/accumulation order).  Norm-wise relative error ||y - ref|| / ||ref||."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from helpers import rel_err
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True)
+def _need(hip):
+    torch.manual_seed(0)
+
+
+def ops():
+    from denseclip_vit_multimodal_amd import ops as O
+    return O
+
+
+TOL = {torch.float16: 2e-3, torch.bfloat16: 1.2e-2, torch.float32: 1e-5}
+
+
+# ----------------------------------------------------------------------------- LayerNorm
+@pytest.mark.parametrize("cols", [64, 128, 768, 1024])
+@pytest.mark.parametrize("odt", [torch.float32, torch.bfloat16, torch.float16])
+def test_layernorm_fwd(cols, odt):
+    O = ops()
+    x = torch.randn(517, cols, device=DEV) * 3 + 0.5
+    w = torch.randn(cols, device=DEV)
+    b = torch.randn(cols, device=DEV)
+    y, mu, rs = O.layernorm_fwd(x, w, b, odt)
+    ref = F.layer_norm(x, (cols,), w, b, 1e-5)
+    assert rel_err(y.float(), ref) < (1e-6 if odt == torch.float32 else TOL[odt])
+    assert rel_err(mu, x.mean(1)) < 1e-6
+    assert rel_err(rs, torch.rsqrt(x.var(1, unbiased=False) + 1e-5)) < 1e-5
+
+
+@pytest.mark.parametrize("cols", [128, 768])
+@pytest.mark.parametrize("dydt", [torch.float32, torch.bfloat16])
+def test_layernorm_bwd(cols, dydt):
+    O = ops()
+    rows = 1500
+    x = (torch.randn(rows, cols, device=DEV) * 2).requires_grad_(True)
+    w = torch.randn(cols, device=DEV).requires_grad_(True)
+    b = torch.randn(cols, device=DEV).requires_grad_(True)
+    dy = torch.randn(rows, cols, device=DEV).to(dydt)
+    ref = F.layer_norm(x, (cols,), w, b, 1e-5)
+    ref.backward(dy.float())
+    _, mu, rs = O.layernorm_fwd(x.detach(), w.detach(), b.detach(), torch.float32)
+    prev = torch.randn(rows, cols, device=DEV)
+    dx = prev.clone()
+    dw = torch.zeros(cols, device=DEV)
+    db = torch.zeros(cols, device=DEV)
+    O.layernorm_bwd(dy, x.detach(), w.detach(), mu, rs, dx, 1, dw, db)
+    assert rel_err(dx - prev, x.grad) < 1e-5
+    assert rel_err(dw, w.grad) < 1e-5
+    assert rel_err(db, b.grad) < 1e-5
+
+
+# ----------------------------------------------------------------------------- GEMM
+SHAPES = [(128, 128, 64), (300, 200, 192), (65, 64, 128), (1000, 2304, 768), (4097, 768, 3072), (8, 512, 768)]
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_gemm_store(M, N, K, dt):
+    O = ops()
+    A = torch.randn(M, K, device=DEV).to(dt)
+    B = torch.randn(N, K, device=DEV).to(dt)
+    bias = torch.randn(N, device=DEV)
+    ref = A.float() @ B.float().t() + bias
+    y32 = O.gemm(A, B, bias=bias, out_dtype=torch.float32)
+    assert rel_err(y32, ref) < 1e-5
+    y = O.gemm(A, B, bias=bias)
+    assert y.dtype == dt
+    assert rel_err(y.float(), ref) < TOL[dt]
+
+
+def test_gemm_asymmetric_layout():
+    """A = I with an asymmetric B catches a transposed C write (guide §3)."""
+    O = ops()
+    K = 128
+    A = torch.eye(K, device=DEV).to(torch.bfloat16)
+    Bm = (torch.arange(K, device=DEV).view(-1, 1) * 1000 + torch.arange(K, device=DEV).view(1, -1)) % 97
+    B = Bm.float().to(torch.bfloat16)
+    y = O.gemm(A, B, out_dtype=torch.float32)
+    assert torch.equal(y, B.float().t())
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 256, 128), (2049, 3072, 768)])
+def test_gemm_gelu_and_residual(M, N, K):
+    from denseclip_vit_multimodal_amd import _native as Nat
+    O = ops()
+    dt = torch.bfloat16
+    A = torch.randn(M, K, device=DEV).to(dt)
+    B = (torch.randn(N, K, device=DEV) * K ** -0.5).to(dt)
+    bias = torch.randn(N, device=DEV)
+    z, h = O.gemm(A, B, Nat.EPI_GELU, bias=bias)
+    zr = A.float() @ B.float().t() + bias
+    assert rel_err(z.float(), zr) < TOL[dt]
+    hr = z.float() * torch.sigmoid(1.702 * z.float())
+    assert rel_err(h.float(), hr) < TOL[dt]
+    res = torch.randn(M, N, device=DEV)
+    out = O.gemm(A, B, Nat.EPI_RESIDUAL, bias=bias, aux=res)
+    assert rel_err(out, res + zr) < 1e-5
+    # in place (aux aliases C)
+    res2 = res.clone()
+    O.gemm(A, B, Nat.EPI_RESIDUAL, bias=bias, aux=res2, out=res2)
+    assert rel_err(res2, res + zr) < 1e-5
+    g = torch.randn(M, N, device=DEV).to(dt)
+    Bt = torch.randn(N, N, device=DEV).to(dt)  # dh = g @ Bt^T
+    dz = O.gemm(g, Bt, Nat.EPI_GELU_BWD, aux=z)
+    zf = z.float()
+    s = torch.sigmoid(1.702 * zf)
+    ref = (g.float() @ Bt.float().t()) * (s + 1.702 * zf * s * (1 - s))
+    assert rel_err(dz.float(), ref) < TOL[dt]
+
+
+@pytest.mark.parametrize("M,N,K", [(777, 256, 128), (65544 // 8, 768, 3072), (5000, 2304, 768)])
+def test_weight_grad_splitk(M, N, K):
+    O = ops()
+    dt = torch.bfloat16
+    dy = torch.randn(M, N, device=DEV).to(dt)
+    x = torch.randn(M, K, device=DEV).to(dt)
+    dW, db = O.weight_grad(dy, x)
+    assert rel_err(dW, dy.float().t() @ x.float()) < 1e-5
+    assert rel_err(db, dy.float().sum(0)) < 1e-5
+
+
+# ----------------------------------------------------------------------------- attention
+def attn_ref(qkv, B, N, H):
+    C = qkv.shape[1] // 3
+    q, k, v = qkv.float().view(B, N, 3, H, C // H).permute(2, 0, 3, 1, 4)
+    o = torch.softmax(q @ k.transpose(-1, -2) * (C // H) ** -0.5, -1) @ v
+    return o.permute(0, 2, 1, 3).reshape(B * N, C)
+
+
+@pytest.mark.parametrize("N", [1, 33, 64, 129, 257, 1000])
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+def test_attention_fwd(N, dt):
+    O = ops()
+    B, H = 2, 3
+    C = 64 * H
+    qkv = (torch.randn(B * N, 3 * C, device=DEV) * 1.5).to(dt)
+    o, lse = O.attn_fwd(qkv, B, N, H, 64 ** -0.5)
+    ref = attn_ref(qkv, B, N, H)
+    assert rel_err(o.float(), ref) < TOL[dt]
+    # lse (log2 domain): log2 sum exp(s * scale)
+    q, k, _ = qkv.float().view(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-1, -2)) * 64 ** -0.5
+    lref = torch.logsumexp(s, -1) / math.log(2)
+    assert (lse.view(B, H, N) - lref).abs().max() < 1e-2
+
+
+def test_attention_spiky_rescale():
+    """Force the online-softmax running max to jump late (guide rule 26)."""
+    O = ops()
+    B, H, N = 1, 1, 300
+    C = 64
+    qkv = torch.randn(B * N, 3 * C, device=DEV) * 0.3
+    qkv[:, :64] = 1.0
+    qkv[250, 64:128] = 4.0  # one late key dominates every query
+    qkv = qkv.to(torch.float16)
+    o, _ = O.attn_fwd(qkv, B, N, H, 64 ** -0.5)
+    assert rel_err(o.float(), attn_ref(qkv, B, N, H)) < TOL[torch.float16]
+
+
+@pytest.mark.parametrize("N", [1, 33, 130, 257, 700])
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+def test_attention_bwd(N, dt):
+    O = ops()
+    B, H = 2, 2
+    C = 64 * H
+    qkv = torch.randn(B * N, 3 * C, device=DEV).to(dt)
+    dout = torch.randn(B * N, C, device=DEV).to(dt)
+    o, lse = O.attn_fwd(qkv, B, N, H, 64 ** -0.5)
+    dqkv = O.attn_bwd(qkv, o, dout, lse, B, N, H, 64 ** -0.5)
+    q32 = qkv.float().requires_grad_(True)
+    ref = attn_ref(q32, B, N, H)
+    ref.backward(dout.float())
+    g = q32.grad
+    tol = 4 * TOL[dt]
+    # N = 1: dQ = dK = 0 exactly, so the error is normalised by max(||ref||, 1e-3 ||dout||)
+    floor = 1e-3 * float(dout.float().norm())
+    for sl in (slice(0, C), slice(C, 2 * C), slice(2 * C, 3 * C)):
+        err = float((dqkv[:, sl].float() - g[:, sl]).norm()) / max(float(g[:, sl].norm()), floor)
+        assert err < tol, (sl, err)
+
+
+# ----------------------------------------------------------------------------- misc
+def test_im2col_and_patch_gemm_match_conv():
+    O = ops()
+    img = torch.randn(2, 3, 64, 96, device=DEV)
+    w = torch.randn(128, 3, 16, 16, device=DEV) * 0.05
+    pt = O.im2col(img, 16, torch.float32)
+    ref = F.conv2d(img, w, stride=16).flatten(2).transpose(1, 2).reshape(-1, 128)
+    assert rel_err(pt @ w.view(128, -1).t(), ref) < 1e-5
+
+
+def test_pos_interp_fwd_bwd():
+    from denseclip_vit_multimodal_amd import _native as Nat
+    O = ops()
+    g, C, H, W = 14, 64, 64, 128
+    pos = torch.randn(g * g + 1, C, device=DEV, requires_grad=True)
+    grid = pos[1:].view(1, g, g, C).permute(0, 3, 1, 2)
+    ref = torch.cat([pos[:1], F.interpolate(grid, size=(H, W), mode="bilinear", align_corners=False)
+                     .permute(0, 2, 3, 1).reshape(H * W, C)])
+    out = O.pos_interp(pos.detach(), g, H, W)
+    assert rel_err(out, ref) < 1e-6
+    gout = torch.randn_like(ref)
+    ref.backward(gout)
+    dpos = torch.zeros_like(pos)
+    O.pos_interp_bwd(gout, dpos, g, H, W)
+    assert rel_err(dpos, pos.grad) < 1e-5
+
+
+@pytest.mark.parametrize("hw,out", [((64, 128), (1024, 2048)), ((8, 16), (128, 256)), ((7, 9), (20, 13)),
+                                    ((32, 64), (512, 1024)), ((10, 10), (5, 7))])
+def test_bilinear_fwd_bwd(hw, out):
+    O = ops()
+    x = torch.randn(2, 3, *hw, device=DEV, requires_grad=True)
+    ref = F.interpolate(x, size=out, mode="bilinear", align_corners=False)
+    y = O.bilinear(x.detach(), *out)
+    assert rel_err(y, ref) < 1e-6
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    assert rel_err(O.bilinear_bwd(g, *hw), x.grad) < 1e-5
+
+
+def test_transpose_colsum_pad():
+    O = ops()
+    x = torch.randn(300, 72, device=DEV).to(torch.bfloat16)
+    cs = torch.zeros(72, device=DEV)
+    t = O.transpose(x, 300, 72, torch.bfloat16, rows_pad=384, colsum=cs).view(72, 384)
+    assert torch.equal(t[:, :300], x.t())
+    assert torch.count_nonzero(t[:, 300:]) == 0
+    assert rel_err(cs, x.float().sum(0)) < 1e-6
+
+
+def test_score_map_and_channel_mean():
+    O = ops()
+    B, HW, C, K = 2, 333, 512, 19
+    v = torch.randn(B * HW, C, device=DEV).to(torch.bfloat16)
+    t = torch.randn(B, K, C, device=DEV)
+    s = O.score_map(v, t, B, HW)
+    vn = F.normalize(v.float().view(B, HW, C), dim=2)
+    tn = F.normalize(t, dim=2)
+    ref = torch.einsum("bpc,bkc->bkp", vn, tn)
+    assert rel_err(s, ref) < 1e-5
+    m = O.channel_mean(v, B)
+    assert rel_err(m, v.float().view(B, HW, C).mean(1)) < 1e-6
