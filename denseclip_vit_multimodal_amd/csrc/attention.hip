@@ -16,8 +16,9 @@
 //   * the P^T accumulator registers are converted to 16-bit in place and used directly
 //     as the B-operand of O^T += V^T P^T (no LDS round trip for P); V^T fragments come
 //     from the row-major V tile with the gfx950 transposing LDS read ds_read_b64_tr_b16,
-//   * K/V tiles of 64 keys are double-buffered in LDS via 16-byte global_load_lds
-//     with an XOR-swizzled image (bank-conflict-free ds_read_b128 row reads),
+//   * K/V tiles of 64 keys are double-buffered in LDS, register-staged (global loads
+//     issued at the top of an iteration, LDS writes at its end) into an XOR-swizzled
+//     image (bank-conflict-free ds_read_b128 row reads),
 //   * online softmax in the exp2 domain, fp32 statistics; lse stored for backward.
 // Backward (FlashAttention-2 style recompute, no atomics):
 //   delta = rowsum(dO * O);  a query-major pass for dQ (same structure as the forward
@@ -35,23 +36,6 @@ __device__ __forceinline__ int swz(int row, int col) {
     // byte offset of 16-bit element (row, col) in a [rows][64] image with 16-byte chunks
     // XOR-swizzled by ((row >> 1) & 7)
     return row * 128 + ((((col >> 3) ^ ((row >> 1) & 7))) << 4) + ((col & 7) << 1);
-}
-
-// Stage rows [r0, r0 + nrows) of a row-major matrix (64 contiguous 16-bit columns per
-// row starting at `base`, row stride ld) into a swizzled LDS image.  Rows >= N are
-// clamped to N-1 (their results are masked by the caller).
-template <typename T>
-__device__ __forceinline__ void stage_rows(const T* __restrict__ base, int64_t ld, int r0, int nrows, int N,
-                                           char* lds, int wave, int lane, int nwaves) {
-    const int ninst = nrows / 8;
-    for (int inst = wave; inst < ninst; inst += nwaves) {
-        const int r = inst * 8 + (lane >> 3);
-        const int c = (lane & 7) ^ ((r >> 1) & 7);
-        int gr = r0 + r;
-        gr = gr < N ? gr : N - 1;
-        const T* src = base + (int64_t)gr * ld + c * 8;
-        __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(lds + inst * 1024), 16, 0, 0);
-    }
 }
 
 template <typename T>
@@ -101,50 +85,99 @@ template <> struct DsScale<f16> { static constexpr float v = 256.0f; };
 // accumulator register r -> row offset within a 32x32 tile (column = lane & 31)
 __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
+// ---------------------------------------------------------------------------- staging
+// Register-staged tile copies (issue the global loads early, write LDS late — T14): an
+// LDS-DMA (global_load_lds) prefetch here makes hipcc wait vmcnt(0) before every later
+// LDS read of the other buffer, serialising the prefetch with the compute.
+// A tile of ROWS rows x 128 B: each of the 256 threads moves ROWS/32 chunks of 16 B.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+template <int ROWS>
+struct TileRegs {
+    i32x4 v[ROWS / 32];  // native vector type: HIP's int4 struct arrays end up in scratch
+};
+
+template <typename T, int ROWS>
+__device__ __forceinline__ void tile_load(TileRegs<ROWS>& R, const T* __restrict__ base, int64_t ld, int r0, int N) {
+#pragma unroll
+    for (int i = 0; i < ROWS / 32; ++i) {
+        const int idx = i * 256 + threadIdx.x;  // (row, chunk) = (idx >> 3, idx & 7)
+        int gr = r0 + (idx >> 3);
+        gr = gr < N ? gr : N - 1;
+        R.v[i] = *(const i32x4*)(base + (int64_t)gr * ld + (idx & 7) * 8);
+    }
+}
+
+template <int ROWS>
+__device__ __forceinline__ void tile_store(const TileRegs<ROWS>& R, char* lds) {
+#pragma unroll
+    for (int i = 0; i < ROWS / 32; ++i) {
+        const int idx = i * 256 + threadIdx.x;
+        const int r = idx >> 3, c = idx & 7;
+        *(i32x4*)(lds + r * 128 + ((c ^ ((r >> 1) & 7)) << 4)) = R.v[i];
+    }
+}
+
 // ============================================================================ forward
 template <typename T>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const T* __restrict__ qkv, T* __restrict__ out,
                                                           float* __restrict__ lse, int N, int H, float c) {
+    typedef typename Mfma<T>::frag frag;
     __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 64 * 128];  // [buf][K|V][64 rows][128 B]
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int h = lane >> 5, l32 = lane & 31;
-    const int bh = blockIdx.y, b = bh / H, hd = bh % H;
+    // XCD-aware tile order: the q-blocks of one (batch, head) run on one XCD and share
+    // its L2 copy of that head's K/V stream
+    const int nq = (N + 127) / 128;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int qblk = tile % nq, bh = tile / nq, b = bh / H, hd = bh % H;
     const int C = H * HD;
     const int64_t ld = 3 * (int64_t)C;
     const T* Qb = qkv + (int64_t)b * N * ld + hd * HD;
     const T* Kb = Qb + C;
     const T* Vb = Qb + 2 * C;
-    const int q = blockIdx.x * 128 + wave * 32 + l32;  // this lane's query row
+    const int q = qblk * 128 + wave * 32 + l32;  // this lane's query row
     const int qc = q < N ? q : N - 1;
 
-    typename Mfma<T>::frag qf[4];
+    frag qf[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) qf[s] = *(const typename Mfma<T>::frag*)(Qb + (int64_t)qc * ld + (2 * s + h) * 8);
+    for (int s = 0; s < 4; ++s) qf[s] = *(const frag*)(Qb + (int64_t)qc * ld + (2 * s + h) * 8);
 
     f32x16 o[2] = {zero16(), zero16()};
     float m = -INFINITY, l = 0.f;
     const int nt = (N + 63) / 64;
 
-    stage_rows<T>(Kb, ld, 0, 64, N, smem, wave, lane, 4);
-    stage_rows<T>(Vb, ld, 0, 64, N, smem + 8192, wave, lane, 4);
+    TileRegs<64> rk, rv;
+    tile_load<T, 64>(rk, Kb, ld, 0, N);
+    tile_load<T, 64>(rv, Vb, ld, 0, N);
+    tile_store<64>(rk, smem);
+    tile_store<64>(rv, smem + 8192);
     __syncthreads();
 
     for (int t = 0; t < nt; ++t) {
         const char* Kt = smem + (t & 1) * 16384;
         const char* Vt = Kt + 8192;
-        if (t + 1 < nt) {
-            char* nx = smem + ((t + 1) & 1) * 16384;
-            stage_rows<T>(Kb, ld, (t + 1) * 64, 64, N, nx, wave, lane, 4);
-            stage_rows<T>(Vb, ld, (t + 1) * 64, 64, N, nx + 8192, wave, lane, 4);
+        const bool more = t + 1 < nt;
+        if (more) {
+            tile_load<T, 64>(rk, Kb, ld, (t + 1) * 64, N);
+            tile_load<T, 64>(rv, Vb, ld, (t + 1) * 64, N);
         }
-        // S^T[key][q] for two 32-key blocks
+        // S^T[key][q] for two 32-key blocks; all K fragments issued before the MFMAs
+        frag kf[2][4];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) kf[kb][s] = row_frag<T>(Kt, kb * 32 + l32, 2 * s + h);
         f32x16 sacc[2] = {zero16(), zero16()};
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
+        for (int s = 0; s < 4; ++s)
 #pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-                sacc[kb] = Mfma<T>::mma(row_frag<T>(Kt, kb * 32 + l32, 2 * s + h), qf[s], sacc[kb]);
-        }
+            for (int kb = 0; kb < 2; ++kb) sacc[kb] = Mfma<T>::mma(kf[kb][s], qf[s], sacc[kb]);
+        // V^T fragments of the first key block: in flight during the softmax
+        frag vf[2][2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int db = 0; db < 2; ++db) vf[s][db] = tr_frag<T>(Vt, 0, s, db, lane);
         if ((t + 1) * 64 > N) {  // ragged last tile: keys >= N get -inf
 #pragma unroll
             for (int kb = 0; kb < 2; ++kb)
@@ -159,33 +192,56 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const T* __restrict__ 
             for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[kb][r]);
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
         const float mnew = fmaxf(m, mx * c);
-        const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+        // exact lazy rescale: O and l only need rescaling when some row max grew
+        // (wave-uniform branch; rows whose max did not grow have alpha = 1)
+        if (__any(mnew > m)) {
+            const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+            l *= alpha;
+#pragma unroll
+            for (int db = 0; db < 2; ++db)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
+            m = mnew;
+        }
         float rs = 0.f;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const float p = __builtin_amdgcn_exp2f(fmaf(sacc[kb][r], c, -mnew));
+                const float p = __builtin_amdgcn_exp2f(fmaf(sacc[kb][r], c, -m));
                 sacc[kb][r] = p;
                 rs += p;
             }
         rs += __shfl_xor(rs, 32, 64);
-        l = l * alpha + rs;
-        m = mnew;
-#pragma unroll
-        for (int db = 0; db < 2; ++db)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
+        l += rs;
         // O^T[d][q] += V^T[d][key] P^T[key][q]
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
+        for (int kb = 0; kb < 2; ++kb) {
+            frag vn[2][2];
+            if (kb == 0) {
+#pragma unroll
+                for (int s = 0; s < 2; ++s)
+#pragma unroll
+                    for (int db = 0; db < 2; ++db) vn[s][db] = tr_frag<T>(Vt, 1, s, db, lane);
+            }
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
-                const typename Mfma<T>::frag pf = pack_frag<T>(sacc[kb], s);
+                const frag pf = pack_frag<T>(sacc[kb], s);
 #pragma unroll
-                for (int db = 0; db < 2; ++db)
-                    o[db] = Mfma<T>::mma(tr_frag<T>(Vt, kb, s, db, lane), pf, o[db]);
+                for (int db = 0; db < 2; ++db) o[db] = Mfma<T>::mma(vf[s][db], pf, o[db]);
             }
+            if (kb == 0) {
+#pragma unroll
+                for (int s = 0; s < 2; ++s)
+#pragma unroll
+                    for (int db = 0; db < 2; ++db) vf[s][db] = vn[s][db];
+            }
+        }
+        if (more) {
+            char* nx = smem + ((t + 1) & 1) * 16384;
+            tile_store<64>(rk, nx);
+            tile_store<64>(rv, nx + 8192);
+        }
         __syncthreads();
     }
 
@@ -235,51 +291,69 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const T* __restrict
                                                              const float* __restrict__ lse,
                                                              const float* __restrict__ delta, T* __restrict__ dqkv,
                                                              int N, int H, float c, float scale) {
+    typedef typename Mfma<T>::frag frag;
     __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 64 * 128];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int h = lane >> 5, l32 = lane & 31;
-    const int bh = blockIdx.y, b = bh / H, hd = bh % H;
+    const int nq = (N + 127) / 128;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int qblk = tile % nq, bh = tile / nq, b = bh / H, hd = bh % H;
     const int C = H * HD;
     const int64_t ld = 3 * (int64_t)C;
     const T* Qb = qkv + (int64_t)b * N * ld + hd * HD;
     const T* Kb = Qb + C;
     const T* Vb = Qb + 2 * C;
     const T* dOb = dout + (int64_t)b * N * C + hd * HD;
-    const int q = blockIdx.x * 128 + wave * 32 + l32;
+    const int q = qblk * 128 + wave * 32 + l32;
     const int qc = q < N ? q : N - 1;
 
-    typename Mfma<T>::frag qf[4], gf[4];
+    frag qf[4], gf[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-        qf[s] = *(const typename Mfma<T>::frag*)(Qb + (int64_t)qc * ld + (2 * s + h) * 8);
-        gf[s] = *(const typename Mfma<T>::frag*)(dOb + (int64_t)qc * C + (2 * s + h) * 8);
+        qf[s] = *(const frag*)(Qb + (int64_t)qc * ld + (2 * s + h) * 8);
+        gf[s] = *(const frag*)(dOb + (int64_t)qc * C + (2 * s + h) * 8);
     }
     const float Lq = lse[(int64_t)bh * N + qc];
     const float dq_delta = delta[(int64_t)bh * N + qc];
 
     f32x16 dq[2] = {zero16(), zero16()};
     const int nt = (N + 63) / 64;
-    stage_rows<T>(Kb, ld, 0, 64, N, smem, wave, lane, 4);
-    stage_rows<T>(Vb, ld, 0, 64, N, smem + 8192, wave, lane, 4);
+    TileRegs<64> rk, rv;
+    tile_load<T, 64>(rk, Kb, ld, 0, N);
+    tile_load<T, 64>(rv, Vb, ld, 0, N);
+    tile_store<64>(rk, smem);
+    tile_store<64>(rv, smem + 8192);
     __syncthreads();
 
     for (int t = 0; t < nt; ++t) {
         const char* Kt = smem + (t & 1) * 16384;
         const char* Vt = Kt + 8192;
-        if (t + 1 < nt) {
-            char* nx = smem + ((t + 1) & 1) * 16384;
-            stage_rows<T>(Kb, ld, (t + 1) * 64, 64, N, nx, wave, lane, 4);
-            stage_rows<T>(Vb, ld, (t + 1) * 64, 64, N, nx + 8192, wave, lane, 4);
+        const bool more = t + 1 < nt;
+        if (more) {
+            tile_load<T, 64>(rk, Kb, ld, (t + 1) * 64, N);
+            tile_load<T, 64>(rv, Vb, ld, (t + 1) * 64, N);
         }
         f32x16 sacc[2] = {zero16(), zero16()};
         f32x16 pacc[2] = {zero16(), zero16()};
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
+        for (int kb = 0; kb < 2; ++kb) {
+            frag kf[4], vf[4];
 #pragma unroll
-            for (int kb = 0; kb < 2; ++kb) {
-                sacc[kb] = Mfma<T>::mma(row_frag<T>(Kt, kb * 32 + l32, 2 * s + h), qf[s], sacc[kb]);
-                pacc[kb] = Mfma<T>::mma(row_frag<T>(Vt, kb * 32 + l32, 2 * s + h), gf[s], pacc[kb]);
+            for (int s = 0; s < 4; ++s) {
+                kf[s] = row_frag<T>(Kt, kb * 32 + l32, 2 * s + h);
+                vf[s] = row_frag<T>(Vt, kb * 32 + l32, 2 * s + h);
             }
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                sacc[kb] = Mfma<T>::mma(kf[s], qf[s], sacc[kb]);
+                pacc[kb] = Mfma<T>::mma(vf[s], gf[s], pacc[kb]);
+            }
+        }
+        frag kt[2][2];  // K^T fragments for the first key block, in flight during dS
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int db = 0; db < 2; ++db) kt[s][db] = tr_frag<T>(Kt, 0, s, db, lane);
         const bool ragged = (t + 1) * 64 > N;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
@@ -291,13 +365,32 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const T* __restrict
             }
         // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
+        for (int kb = 0; kb < 2; ++kb) {
+            frag kn[2][2];
+            if (kb == 0) {
+#pragma unroll
+                for (int s = 0; s < 2; ++s)
+#pragma unroll
+                    for (int db = 0; db < 2; ++db) kn[s][db] = tr_frag<T>(Kt, 1, s, db, lane);
+            }
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
-                const typename Mfma<T>::frag sf = pack_frag<T>(sacc[kb], s);
+                const frag sf = pack_frag<T>(sacc[kb], s);
 #pragma unroll
-                for (int db = 0; db < 2; ++db) dq[db] = Mfma<T>::mma(tr_frag<T>(Kt, kb, s, db, lane), sf, dq[db]);
+                for (int db = 0; db < 2; ++db) dq[db] = Mfma<T>::mma(kt[s][db], sf, dq[db]);
             }
+            if (kb == 0) {
+#pragma unroll
+                for (int s = 0; s < 2; ++s)
+#pragma unroll
+                    for (int db = 0; db < 2; ++db) kt[s][db] = kn[s][db];
+            }
+        }
+        if (more) {
+            char* nx = smem + ((t + 1) & 1) * 16384;
+            tile_store<64>(rk, nx);
+            tile_store<64>(rv, nx + 8192);
+        }
         __syncthreads();
     }
     scale *= 1.0f / DsScale<T>::v;
@@ -316,18 +409,23 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const T* __restrict
     }
 }
 
-// Key-major dK/dV pass: 128 keys per workgroup (32 per wave), all query slices of 32.
+// Key-major dK/dV pass: 128 keys per workgroup (32 per wave); query slices of 64 rows
+// (two 32-row sub-slices per barrier).
 template <typename T>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
                                                                const float* __restrict__ lse,
                                                                const float* __restrict__ delta,
                                                                T* __restrict__ dqkv, int N, int H, float c,
                                                                float scale) {
-    // [buf][Q | dO][32 rows][128 B] + [buf][L | delta][32 floats]
-    __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 32 * 128 + 2 * 2 * 32 * 4];
+    typedef typename Mfma<T>::frag frag;
+    constexpr int QS = 64;  // query rows per pipeline stage
+    // [buf][Q | dO][64 rows][128 B] + [buf][L | delta][64 floats]
+    __shared__ __attribute__((aligned(16))) char smem[2 * 2 * QS * 128 + 2 * 2 * QS * 4];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int h = lane >> 5, l32 = lane & 31;
-    const int bh = blockIdx.y, b = bh / H, hd = bh % H;
+    const int nkb = (N + 127) / 128;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int kblk = tile % nkb, bh = tile / nkb, b = bh / H, hd = bh % H;
     const int C = H * HD;
     const int64_t ld = 3 * (int64_t)C;
     const T* Qb = qkv + (int64_t)b * N * ld + hd * HD;
@@ -336,80 +434,106 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const T* __restri
     const T* dOb = dout + (int64_t)b * N * C + hd * HD;
     const float* Lb = lse + (int64_t)bh * N;
     const float* Db = delta + (int64_t)bh * N;
-    const int key = blockIdx.x * 128 + wave * 32 + l32;
+    const int key = kblk * 128 + wave * 32 + l32;
     const int kc = key < N ? key : N - 1;
-    float* stat = (float*)(smem + 2 * 2 * 32 * 128);
+    float* stat = (float*)(smem + 2 * 2 * QS * 128);
 
-    typename Mfma<T>::frag kf[4], vf[4];
+    frag kf[4], vf[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-        kf[s] = *(const typename Mfma<T>::frag*)(Kb + (int64_t)kc * ld + (2 * s + h) * 8);
-        vf[s] = *(const typename Mfma<T>::frag*)(Vb + (int64_t)kc * ld + (2 * s + h) * 8);
+        kf[s] = *(const frag*)(Kb + (int64_t)kc * ld + (2 * s + h) * 8);
+        vf[s] = *(const frag*)(Vb + (int64_t)kc * ld + (2 * s + h) * 8);
     }
     f32x16 dk[2] = {zero16(), zero16()}, dv[2] = {zero16(), zero16()};
-    const int nt = (N + 31) / 32;
+    const int nt = (N + QS - 1) / QS;
 
-    auto stage = [&](int t, int buf) {
-        char* base = smem + buf * 8192;
-        stage_rows<T>(Qb, ld, t * 32, 32, N, base, wave, lane, 4);
-        stage_rows<T>(dOb, C, t * 32, 32, N, base + 4096, wave, lane, 4);
-        if (wave == 0) {
-            // L and delta of the slice also by LDS-DMA (4 B per lane): an ordinary global
-            // load here would make hipcc drain the tile DMA with vmcnt(0) at its use
-            const int r = t * 32 + (lane & 31);
-            const int rc = r < N ? r : N - 1;
-            const float* src = lane < 32 ? Lb + rc : Db + rc;
-            __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(stat + buf * 64), 4, 0, 0);
+    TileRegs<QS> rq, rg;
+    float rstat = 0.f;
+    auto load = [&](int t) {
+        tile_load<T, QS>(rq, Qb, ld, t * QS, N);
+        tile_load<T, QS>(rg, dOb, C, t * QS, N);
+        if (threadIdx.x < 2 * QS) {
+            int r = t * QS + (threadIdx.x & (QS - 1));
+            r = r < N ? r : N - 1;
+            rstat = threadIdx.x < QS ? Lb[r] : Db[r];
         }
     };
-    stage(0, 0);
+    auto store = [&](int buf) {
+        char* base = smem + buf * (2 * QS * 128);
+        tile_store<QS>(rq, base);
+        tile_store<QS>(rg, base + QS * 128);
+        if (threadIdx.x < 2 * QS) stat[buf * 2 * QS + threadIdx.x] = rstat;
+    };
+    load(0);
+    store(0);
     __syncthreads();
 
     for (int t = 0; t < nt; ++t) {
         const int buf = t & 1;
-        const char* Qt = smem + buf * 8192;
-        const char* Gt = Qt + 4096;
-        const float* Ls = stat + buf * 64;
-        const float* Ds = Ls + 32;
-        if (t + 1 < nt) stage(t + 1, buf ^ 1);
-        // S[q][key], dP[q][key]  (query rows in registers, key on the lane)
-        f32x16 sacc = zero16(), pacc = zero16();
+        const bool more = t + 1 < nt;
+        if (more) load(t + 1);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            sacc = Mfma<T>::mma(row_frag<T>(Qt, l32, 2 * s + h), kf[s], sacc);
-            pacc = Mfma<T>::mma(row_frag<T>(Gt, l32, 2 * s + h), vf[s], pacc);
-        }
-        const bool ragged = (t + 1) * 32 > N;
+        for (int sub = 0; sub < QS / 32; ++sub) {
+            const char* Qt = smem + buf * (2 * QS * 128) + sub * 32 * 128;
+            const char* Gt = Qt + QS * 128;
+            const float* Ls = stat + buf * 2 * QS + sub * 32;
+            const float* Ds = Ls + QS;
+            const int q0 = t * QS + sub * 32;
+            // S[q][key], dP[q][key]  (query rows in registers, key on the lane)
+            frag qa[4], ga[4];
 #pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-            const f32x4 Lv = *(const f32x4*)(Ls + 8 * g4 + 4 * h);
-            const f32x4 Dv = *(const f32x4*)(Ds + 8 * g4 + 4 * h);
+            for (int s = 0; s < 4; ++s) {
+                qa[s] = row_frag<T>(Qt, l32, 2 * s + h);
+                ga[s] = row_frag<T>(Gt, l32, 2 * s + h);
+            }
+            f32x16 sacc = zero16(), pacc = zero16();
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int r = 4 * g4 + e;
-                float p = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -Lv[e]));
-                if (ragged && t * 32 + acc_row(r, h) >= N) p = 0.f;
-                sacc[r] = p;                       // P
-                pacc[r] = p * (pacc[r] - Dv[e]) * DsScale<T>::v;  // dS (scaled)
+            for (int s = 0; s < 4; ++s) {
+                sacc = Mfma<T>::mma(qa[s], kf[s], sacc);
+                pacc = Mfma<T>::mma(ga[s], vf[s], pacc);
+            }
+            // dO^T / Q^T fragments for the dV / dK products, in flight during the VALU part
+            frag gt[2][2], qt[2][2];
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int db = 0; db < 2; ++db) {
+                    gt[s][db] = tr_frag<T>(Gt, 0, s, db, lane);
+                    qt[s][db] = tr_frag<T>(Qt, 0, s, db, lane);
+                }
+            const bool ragged = q0 + 32 > N;
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                const f32x4 Lv = *(const f32x4*)(Ls + 8 * g4 + 4 * h);
+                const f32x4 Dv = *(const f32x4*)(Ds + 8 * g4 + 4 * h);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int r = 4 * g4 + e;
+                    float p = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -Lv[e]));
+                    if (ragged && q0 + acc_row(r, h) >= N) p = 0.f;
+                    sacc[r] = p;                                           // P
+                    pacc[r] = p * (pacc[r] - Dv[e]) * DsScale<T>::v;       // dS (scaled)
+                }
+            }
+            // dV^T[d][key] += dO^T[d][q] P[q][key] ;  dK^T[d][key] += Q^T[d][q] dS[q][key]
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const frag pf = pack_frag<T>(sacc, s);
+                const frag sf = pack_frag<T>(pacc, s);
+#pragma unroll
+                for (int db = 0; db < 2; ++db) {
+                    dv[db] = Mfma<T>::mma(gt[s][db], pf, dv[db]);
+                    dk[db] = Mfma<T>::mma(qt[s][db], sf, dk[db]);
+                }
             }
         }
-        // dV^T[d][key] += dO^T[d][q] P[q][key] ;  dK^T[d][key] += Q^T[d][q] dS[q][key]
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const typename Mfma<T>::frag pf = pack_frag<T>(sacc, s);
-            const typename Mfma<T>::frag sf = pack_frag<T>(pacc, s);
-#pragma unroll
-            for (int db = 0; db < 2; ++db) {
-                dv[db] = Mfma<T>::mma(tr_frag<T>(Gt, 0, s, db, lane), pf, dv[db]);
-                dk[db] = Mfma<T>::mma(tr_frag<T>(Qt, 0, s, db, lane), sf, dk[db]);
-            }
-        }
+        if (more) store(buf ^ 1);
         __syncthreads();
     }
     scale *= 1.0f / DsScale<T>::v;
     if (key < N) {
         T* rk = dqkv + ((int64_t)b * N + key) * ld + C + hd * HD;
-        T* rv = rk + C;
+        T* rvp = rk + C;
 #pragma unroll
         for (int db = 0; db < 2; ++db)
 #pragma unroll
@@ -420,14 +544,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const T* __restri
                         (T)(dk[db][4 * g4 + 2] * scale), (T)(dk[db][4 * g4 + 3] * scale)};
                 t4 v = {(T)dv[db][4 * g4], (T)dv[db][4 * g4 + 1], (T)dv[db][4 * g4 + 2], (T)dv[db][4 * g4 + 3]};
                 *(t4*)(rk + d) = a;
-                *(t4*)(rv + d) = v;
+                *(t4*)(rvp + d) = v;
             }
     }
 }
 
 template <typename T>
 void fwd_launch(const void* qkv, void* o, float* lse, int B, int N, int H, float scale, hipStream_t st) {
-    dim3 grid((N + 127) / 128, B * H);
+    dim3 grid(((N + 127) / 128) * B * H);
     attn_fwd_kernel<T><<<grid, 256, 0, st>>>((const T*)qkv, (T*)o, lse, N, H, scale * LOG2E);
 }
 
@@ -437,7 +561,7 @@ void bwd_launch(const void* qkv, const void* o, const void* dout, const float* l
     const int64_t total = (int64_t)B * N * H;
     attn_delta_kernel<T><<<(unsigned)((total + 255) / 256), 256, 0, st>>>((const T*)o, (const T*)dout, delta, N, H,
                                                                           total);
-    dim3 grid((N + 127) / 128, B * H);
+    dim3 grid(((N + 127) / 128) * B * H);
     attn_bwd_dq_kernel<T><<<grid, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, (T*)dqkv, N, H,
                                                 scale * LOG2E, scale);
     attn_bwd_dkdv_kernel<T><<<grid, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, (T*)dqkv, N, H,

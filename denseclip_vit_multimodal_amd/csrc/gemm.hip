@@ -24,6 +24,47 @@ namespace {
 constexpr int BM = 128, BN = 128, BK = 64;
 constexpr int TILE_BYTES = 128 * BK * 2;      // 16 KiB per operand per stage
 constexpr int STAGE_BYTES = 2 * TILE_BYTES;   // A + B
+constexpr int EP_LD = 68;                     // epilogue LDS row stride (floats): 64 + 4 pad
+constexpr int SMEM_BYTES = 4 * 64 * EP_LD * 4 > 2 * STAGE_BYTES ? 4 * 64 * EP_LD * 4 : 2 * STAGE_BYTES;
+
+// 8 consecutive elements of a row: one 16-byte (16-bit types) or two (f32) accesses when
+// the row segment is complete, element-wise otherwise
+template <typename T>
+__device__ __forceinline__ void store8(T* p, const float* v, bool full, int rem) {
+    if (full) {
+        if constexpr (sizeof(T) == 4) {
+            f32x4 a = {v[0], v[1], v[2], v[3]}, b = {v[4], v[5], v[6], v[7]};
+            *(f32x4*)p = a;
+            *(f32x4*)(p + 4) = b;
+        } else {
+            typedef T t8 __attribute__((ext_vector_type(8)));
+            t8 x;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) x[e] = (T)v[e];
+            *(t8*)p = x;
+        }
+    } else {
+        for (int e = 0; e < rem && e < 8; ++e) p[e] = (T)v[e];
+    }
+}
+template <typename T>
+__device__ __forceinline__ void load8(const T* p, float* v, bool full, int rem) {
+    if (full) {
+        if constexpr (sizeof(T) == 4) {
+            const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+            v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+            v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+        } else {
+            typedef T t8 __attribute__((ext_vector_type(8)));
+            const t8 x = *(const t8*)p;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = (float)x[e];
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = e < rem ? (float)p[e] : 0.f;
+    }
+}
 
 template <typename T>
 __device__ __forceinline__ void stage_tile(const T* __restrict__ X, int64_t ldx, int row0, int rows,
@@ -48,13 +89,97 @@ __device__ __forceinline__ typename Mfma<T>::frag read_frag(const char* lds_tile
     return *(const typename Mfma<T>::frag*)(lds_tile + r * 128 + p * 16);
 }
 
+// Shared epilogue of both GEMM kernels.  acc[i][j][4q+e] = C[m][n] with
+// m = m0 + 64wm + 32j + (lane & 31), n = n0 + 64wn + 32i + 8q + 4h + e.
+template <typename T, int EPI, typename OutT>
+__device__ __forceinline__ void gemm_epilogue(f32x16 (&acc)[2][2], char* smem, int M, int N, int m0, int n0,
+                                              const float* __restrict__ bias, const void* __restrict__ aux,
+                                              int64_t ld_aux, void* __restrict__ C, int64_t ldc,
+                                              void* __restrict__ C2, int64_t ldc2, int64_t slab) {
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int h = lane >> 5, l32 = lane & 31;
+    // The accumulator holds C^T (lane = row m, registers along n), so direct stores would
+    // scatter each store instruction over 64 rows.  Instead each wave stages its 64 x 64
+    // fp32 sub-tile (+ bias) in LDS (272-byte padded rows: conflict-free ds_write_b128)
+    // and re-reads it row-contiguous: every global load/store of the epilogue is then a
+    // full 8-element row segment per lane (8 lanes cover one 64-column row).
+    __syncthreads();  // operand LDS no longer needed by any wave
+    float* ep = (float*)smem + wave * (64 * EP_LD);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int col = i * 32 + q * 8 + h * 4;
+                f32x4 v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+                if (bias != nullptr && EPI != DCLIP_EPI_SPLITK && EPI != DCLIP_EPI_GELU_BWD) {
+                    const int n = n0 + wn * 64 + col;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] += (n + e < N) ? bias[n + e] : 0.f;
+                }
+                *(f32x4*)(ep + (j * 32 + l32) * EP_LD + col) = v;
+            }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
+    __builtin_amdgcn_wave_barrier();
+    const int c8 = (lane & 7) * 8;
+    const int nb = n0 + wn * 64 + c8;
+#pragma unroll 2
+    for (int it = 0; it < 8; ++it) {
+        const int r = it * 8 + (lane >> 3);
+        const int m = m0 + wm * 64 + r;
+        if (m >= M || nb >= N) continue;
+        float v[8];
+        {
+            const f32x4 a = *(const f32x4*)(ep + r * EP_LD + c8);
+            const f32x4 b = *(const f32x4*)(ep + r * EP_LD + c8 + 4);
+            v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+            v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+        }
+        const bool full = nb + 8 <= N;
+        if constexpr (EPI == DCLIP_EPI_STORE) {
+            store8<OutT>((OutT*)C + (int64_t)m * ldc + nb, v, full, N - nb);
+        } else if constexpr (EPI == DCLIP_EPI_GELU) {
+            float g[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                // the activation sees the rounded pre-activation, so forward and backward
+                // use the same z
+                v[e] = (float)(OutT)v[e];
+                g[e] = quick_gelu(v[e]);
+            }
+            store8<OutT>((OutT*)C + (int64_t)m * ldc + nb, v, full, N - nb);
+            store8<OutT>((OutT*)C2 + (int64_t)m * ldc2 + nb, g, full, N - nb);
+        } else if constexpr (EPI == DCLIP_EPI_RESIDUAL) {
+            float rsd[8];
+            load8<float>((const float*)aux + (int64_t)m * ld_aux + nb, rsd, full, N - nb);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += rsd[e];
+            store8<float>((float*)C + (int64_t)m * ldc + nb, v, full, N - nb);
+        } else if constexpr (EPI == DCLIP_EPI_GELU_BWD) {
+            float z[8];
+            load8<T>((const T*)aux + (int64_t)m * ld_aux + nb, z, full, N - nb);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] *= quick_gelu_grad(z[e]);
+            store8<OutT>((OutT*)C + (int64_t)m * ldc + nb, v, full, N - nb);
+        } else {  // SPLITK: plain f32 partial slab per K split
+            store8<float>((float*)C + blockIdx.y * slab + (int64_t)m * ldc + nb, v, full, N - nb);
+        }
+    }
+}
+
+
 template <typename T, int EPI, typename OutT>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(
     const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
     int M, int N, int k_chunk, int tiles_m, int tiles_n,
     const float* __restrict__ bias, const void* __restrict__ aux, int64_t ld_aux,
     void* __restrict__ C, int64_t ldc, void* __restrict__ C2, int64_t ldc2, int64_t slab) {
-    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+    __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int wm = wave >> 1, wn = wave & 1;
@@ -102,77 +227,129 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(
         __syncthreads();
     }
 
-    // ---------------------------------------------------------------- epilogue
-    // acc[i][j][4q+e] = C[m][n],  m = m0 + 64wm + 32j + l32,  n = n0 + 64wn + 32i + 8q + 4h + e
+    gemm_epilogue<T, EPI, OutT>(acc, smem, M, N, m0, n0, bias, aux, ld_aux, C, ldc, C2, ldc2, slab);
+}
+
+// ---------------------------------------------------------------------------- "TN"
+// C[m][n] = sum_k A[k][m] * B[k][n]: both operands row-major with the reduction index on
+// the ROWS — the weight-gradient shape dW = dY^T X (k = token, m/n = features).  Tiles of
+// 64 k-rows x 128 columns are staged by global_load_lds (1 KiB = 4 rows x 256 B per
+// wave-instruction, 16-byte chunks XOR-swizzled by (row & 3) << 2 so the transposing
+// reads below are bank-conflict free) and the MFMA fragments (8 consecutive k for one
+// column) are gathered with ds_read_b64_tr_b16.  No transposed copies in HBM.
+template <typename T>
+__device__ __forceinline__ void stage_tile_tn(const T* __restrict__ X, int64_t ldx, int k0, int krows,
+                                              int col0, int cols, char* lds_tile, int wave, int lane) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int m = m0 + wm * 64 + j * 32 + l32;
-        if (m >= M) continue;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int nb = n0 + wn * 64 + i * 32 + q * 8 + h * 4;
-                if (nb >= N) continue;
-                float v[4];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
-                const bool full = nb + 3 < N;
-                if (bias != nullptr && EPI != DCLIP_EPI_SPLITK && EPI != DCLIP_EPI_GELU_BWD) {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) v[e] += (nb + e < N) ? bias[nb + e] : 0.f;
-                }
-                if constexpr (EPI == DCLIP_EPI_STORE) {
-                    OutT* c = (OutT*)C + (int64_t)m * ldc + nb;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        if (full || nb + e < N) c[e] = (OutT)v[e];
-                } else if constexpr (EPI == DCLIP_EPI_GELU) {
-                    OutT* z = (OutT*)C + (int64_t)m * ldc + nb;
-                    OutT* g = (OutT*)C2 + (int64_t)m * ldc2 + nb;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        if (full || nb + e < N) {
-                            // the activation is applied to the rounded pre-activation, so
-                            // that forward and backward see the same z
-                            const OutT zr = (OutT)v[e];
-                            z[e] = zr;
-                            g[e] = (OutT)quick_gelu((float)zr);
-                        }
-                } else if constexpr (EPI == DCLIP_EPI_RESIDUAL) {
-                    const float* r = (const float*)aux + (int64_t)m * ld_aux + nb;
-                    float* c = (float*)C + (int64_t)m * ldc + nb;
-                    if (full) {
-                        f32x4 rv = *(const f32x4*)r;
-                        f32x4 o;
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) o[e] = rv[e] + v[e];
-                        *(f32x4*)c = o;
-                    } else {
-                        for (int e = 0; e < 4; ++e)
-                            if (nb + e < N) c[e] = r[e] + v[e];
-                    }
-                } else if constexpr (EPI == DCLIP_EPI_GELU_BWD) {
-                    const T* z = (const T*)aux + (int64_t)m * ld_aux + nb;
-                    OutT* c = (OutT*)C + (int64_t)m * ldc + nb;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        if (full || nb + e < N) c[e] = (OutT)(v[e] * quick_gelu_grad((float)z[e]));
-                } else {  // SPLITK: plain f32 partial slab per K split
-                    float* c = (float*)C + blockIdx.y * slab + (int64_t)m * ldc + nb;
-                    if (full) {
-                        f32x4 o;
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) o[e] = v[e];
-                        *(f32x4*)c = o;
-                    } else {
-                        for (int e = 0; e < 4; ++e)
-                            if (nb + e < N) c[e] = v[e];
-                    }
-                }
-            }
-        }
+    for (int i = 0; i < 4; ++i) {
+        const int inst = wave * 4 + i;
+        const int r = inst * 4 + (lane >> 4);
+        const int p = lane & 15;
+        const int c = p ^ ((r & 3) << 2);
+        int gr = k0 + r;
+        gr = gr < krows ? gr : krows - 1;
+        int gc = col0 + c * 8;
+        gc = gc + 8 <= cols ? gc : cols - 8;  // tail columns: any in-bounds data, masked later
+        const T* src = X + (int64_t)gr * ldx + gc;
+        __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(lds_tile + inst * 1024), 16, 0, 0);
     }
+}
+
+// fragment of 8 consecutive k rows (k = 16s + 8h + j) for column cb*32 + (lane & 31)
+template <typename T>
+__device__ __forceinline__ typename Mfma<T>::frag tr_frag_tn(const char* img, int s, int col_base, int lane) {
+    const int i = lane & 15, q = i >> 2, p = i & 3, g = lane >> 4, h = lane >> 5;
+    const int row = 16 * s + 8 * h + q;
+    const int col = col_base + (g & 1) * 16 + 4 * p;
+    typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+    auto off = [](int r, int c) { return r * 256 + (((c >> 3) ^ ((r & 3) << 2)) << 4) + ((c & 7) << 1); };
+    i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(img + off(row, col)));
+    i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(img + off(row + 4, col)));
+    typedef short s8 __attribute__((ext_vector_type(8)));
+    s8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(typename Mfma<T>::frag, v);
+}
+
+template <typename T, int EPI, typename OutT>
+__global__ __launch_bounds__(256, 2) void gemm_tn_kernel(
+    const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
+    int M, int N, int Kreal, int k_chunk, int tiles_m, int tiles_n, const float* __restrict__ bias,
+    void* __restrict__ C, int64_t ldc, int64_t slab) {
+    __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int h = lane >> 5;
+
+    const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+    const int m0 = (t / tiles_n) * BM;
+    const int n0 = (t % tiles_n) * BN;
+    const int kbeg = blockIdx.y * k_chunk;
+    int nk = k_chunk / BK;
+    if (kbeg + nk * BK > Kreal) nk = (Kreal - kbeg + BK - 1) / BK;  // fully padded tiles skipped
+    nk = nk < 0 ? 0 : nk;
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    if (nk > 0) {
+        stage_tile_tn<T>(A, lda, kbeg, Kreal, m0, M, smem, wave, lane);
+        stage_tile_tn<T>(B, ldb, kbeg, Kreal, n0, N, smem + TILE_BYTES, wave, lane);
+    }
+    __syncthreads();
+
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        const char* At = smem + cur * STAGE_BYTES;
+        const char* Bt = At + TILE_BYTES;
+        const int k0 = kbeg + kt * BK;
+        if (kt + 1 < nk) {
+            char* nxt = smem + (cur ^ 1) * STAGE_BYTES;
+            stage_tile_tn<T>(A, lda, k0 + BK, Kreal, m0, M, nxt, wave, lane);
+            stage_tile_tn<T>(B, ldb, k0 + BK, Kreal, n0, N, nxt + TILE_BYTES, wave, lane);
+        }
+        const bool ragged = k0 + BK > Kreal;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            typename Mfma<T>::frag fa[2], fb[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) fa[i] = tr_frag_tn<T>(Bt, s, wn * 64 + i * 32, lane);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) fb[j] = tr_frag_tn<T>(At, s, wm * 64 + j * 32, lane);
+            if (ragged) {  // rows past the true K were clamped duplicates: zero them (A side)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e)
+                        if (k0 + 16 * s + 8 * h + e >= Kreal) fb[j][e] = (T)0.f;
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[i][j] = Mfma<T>::mma(fa[i], fb[j], acc[i][j]);
+        }
+        __syncthreads();
+    }
+    gemm_epilogue<T, EPI, OutT>(acc, smem, M, N, m0, n0, bias, nullptr, 0, C, ldc, nullptr, 0, slab);
+}
+
+// per-column sums of a row-major (rows x cols) matrix, accumulated into out (f32)
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ x, int64_t ld, int64_t rows, int cols,
+                                                     int64_t rows_per_block, float* __restrict__ out) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= cols) return;
+    const int64_t r0 = blockIdx.y * rows_per_block;
+    int64_t r1 = r0 + rows_per_block;
+    r1 = r1 < rows ? r1 : rows;
+    float s = 0.f;
+    for (int64_t r = r0; r < r1; ++r) s += (float)x[r * ld + c];
+    atomicAdd(out + c, s);
 }
 
 // out[m][n] = sum_z ws[z][m][n] (+ bias[n]) — the split-K combine (deterministic order)
@@ -282,6 +459,53 @@ extern "C" int dclip_gemm(int epilogue, int ab_dt, const void* A, int64_t lda, c
                  ? dispatch<bf16>(epilogue, c_dt, A, lda, B, ldb, M, N, K, splits, bias, aux, ld_aux, C, ldc, C2, ldc2, st)
                  : dispatch<f16>(epilogue, c_dt, A, lda, B, ldb, M, N, K, splits, bias, aux, ld_aux, C, ldc, C2, ldc2, st);
     if (rc) return rc;
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda, const void* B, int64_t ldb,
+                             int64_t M, int64_t N, int64_t K, int64_t K_pad, int splits, const float* bias,
+                             void* ws, void* C, int64_t ldc, float* colsum_a, void* stream) {
+    DCLIP_HOST_CHECK(ab_dt == DCLIP_BF16 || ab_dt == DCLIP_F16, "dclip_gemm_tn: operands must be f16/bf16");
+    DCLIP_HOST_CHECK(M > 0 && N > 0 && K > 0 && M % 8 == 0 && N % 8 == 0,
+                     "dclip_gemm_tn: M, N must be positive multiples of 8 (M=%lld N=%lld)", (long long)M, (long long)N);
+    DCLIP_HOST_CHECK(splits >= 1 && K_pad >= K && K_pad % (BK * splits) == 0,
+                     "dclip_gemm_tn: K_pad must be >= K and a multiple of 64*splits");
+    DCLIP_HOST_CHECK(lda >= M && ldb >= N && lda % 8 == 0 && ldb % 8 == 0, "dclip_gemm_tn: bad leading dims");
+    DCLIP_HOST_CHECK(((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0, "dclip_gemm_tn: A/B must be 16-byte aligned");
+    DCLIP_HOST_CHECK(epilogue == DCLIP_EPI_STORE || epilogue == DCLIP_EPI_SPLITK,
+                     "dclip_gemm_tn: epilogue must be STORE or SPLITK (f32 output)");
+    DCLIP_HOST_CHECK(epilogue == DCLIP_EPI_STORE ? splits == 1 : ws != nullptr,
+                     "dclip_gemm_tn: STORE needs splits == 1; SPLITK needs a workspace of splits*M*N f32");
+    DCLIP_HOST_CHECK(ldc % 4 == 0, "dclip_gemm_tn: ldc %% 4 != 0");
+    hipStream_t st = (hipStream_t)stream;
+    const int tiles_m = (int)((M + BM - 1) / BM), tiles_n = (int)((N + BN - 1) / BN);
+    const int k_chunk = (int)(K_pad / splits);
+    dim3 grid(tiles_m * tiles_n, splits);
+    if (colsum_a) {
+        const int64_t rpb = 512;
+        dim3 cg((unsigned)((M + 255) / 256), (unsigned)((K + rpb - 1) / rpb));
+        if (ab_dt == DCLIP_BF16) colsum_kernel<bf16><<<cg, 256, 0, st>>>((const bf16*)A, lda, K, (int)M, rpb, colsum_a);
+        else colsum_kernel<f16><<<cg, 256, 0, st>>>((const f16*)A, lda, K, (int)M, rpb, colsum_a);
+    }
+#define TN_LAUNCH(T, EPI, OUT)                                                                               \
+    gemm_tn_kernel<T, EPI, float><<<grid, 256, 0, st>>>((const T*)A, lda, (const T*)B, ldb, (int)M, (int)N,   \
+                                                        (int)K, k_chunk, tiles_m, tiles_n, nullptr, OUT,        \
+                                                        EPI == DCLIP_EPI_SPLITK ? N : ldc, (int64_t)M * N)
+    if (epilogue == DCLIP_EPI_STORE) {
+        DCLIP_HOST_CHECK(bias == nullptr, "dclip_gemm_tn: bias only with SPLITK");
+        if (ab_dt == DCLIP_BF16) TN_LAUNCH(bf16, DCLIP_EPI_STORE, C);
+        else TN_LAUNCH(f16, DCLIP_EPI_STORE, C);
+    } else {
+        if (ab_dt == DCLIP_BF16) TN_LAUNCH(bf16, DCLIP_EPI_SPLITK, ws);
+        else TN_LAUNCH(f16, DCLIP_EPI_SPLITK, ws);
+        const int64_t total4 = M * (N / 4);
+        int blocks = (int)((total4 + 255) / 256);
+        blocks = blocks > 4096 ? 4096 : blocks;
+        splitk_reduce_kernel<<<blocks, 256, 0, st>>>((const float*)ws, splits, M * N, (int)M, (int)N, bias,
+                                                     (float*)C, ldc);
+    }
+#undef TN_LAUNCH
     DCLIP_LAUNCH_CHECK();
     return 0;
 }

@@ -135,27 +135,50 @@ def cast(x, dtype):
     return y
 
 
+def _wgrad_splits(tiles, M, slots=512):
+    """K-split count for a weight-gradient GEMM: fill whole rounds of the 512 resident
+    workgroup slots (256 CUs x 2), fewest splits among the best fills, >= 4 k-tiles each."""
+    best, best_eff = 1, 0.0
+    for s in range(1, 33):
+        if s > 1 and M < 64 * 4 * s:
+            break
+        blocks = tiles * s
+        eff = blocks / (math.ceil(blocks / slots) * slots)
+        if eff > best_eff + 0.02:
+            best, best_eff = s, eff
+    return best
+
+
 def weight_grad(dy, x, want_bias=True):
     """dW = dy^T x (N x K, fp32) and db = colsum(dy) for dy (M, N), x (M, K) (compute dtype).
 
-    Both operands are transposed to k(=m)-contiguous layouts with zero padding of M to a
-    multiple of 64*splits, then one split-K MFMA GEMM with a deterministic slab combine.
-    """
+    One "TN" MFMA GEMM reading both operands in their natural token-major layout (the
+    reduction runs over the rows), split over the M tokens with a deterministic slab
+    combine; no transposed copies."""
+    _check(dy, x)
     M, Nn = dy.shape
     K = x.shape[1]
-    tiles = math.ceil(Nn / 128) * math.ceil(K / 128)
-    splits = max(1, min(16, round(512 / tiles)))
-    while splits > 1 and M < 64 * splits * 4:
-        splits //= 2
-    m_pad = math.ceil(M / (64 * splits)) * 64 * splits
+    splits = _wgrad_splits(math.ceil(Nn / 128) * math.ceil(K / 128), M)
+    k_pad = math.ceil(M / (64 * splits)) * 64 * splits
     db = torch.zeros(Nn, dtype=torch.float32, device=dy.device) if want_bias else None
-    dyT = transpose(dy, M, Nn, dy.dtype, rows_pad=m_pad, colsum=db).view(Nn, m_pad)
-    xT = transpose(x, M, K, x.dtype, rows_pad=m_pad).view(K, m_pad)
     dW = torch.empty(Nn, K, dtype=torch.float32, device=dy.device)
     ws = torch.empty(splits, Nn, K, dtype=torch.float32, device=dy.device)
-    N.call("dclip_gemm", N.EPI_SPLITK, _dt(dyT), _p(dyT), m_pad, _p(xT), m_pad, Nn, K, m_pad, splits, None,
-           _p(ws), N.F32, 0, _p(dW), N.F32, K, None, 0, _stream())
+    e0 = _tic()
+    N.call("dclip_gemm_tn", N.EPI_SPLITK, _dt(dy), _p(dy), dy.stride(0), _p(x), x.stride(0), Nn, K, M, k_pad,
+           splits, None, _p(ws), _p(dW), K, _p(db), _stream())
+    _toc("gemm_wgrad", e0)
     return dW, db
+
+
+def gemm_tn(A, B):
+    """out[m][n] = sum_k A[k][m] B[k][n] (f32)."""
+    _check(A, B)
+    K, M = A.shape
+    Nn = B.shape[1]
+    out = torch.empty(M, Nn, dtype=torch.float32, device=A.device)
+    N.call("dclip_gemm_tn", N.EPI_STORE, _dt(A), _p(A), A.stride(0), _p(B), B.stride(0), M, Nn, K,
+           math.ceil(K / 64) * 64, 1, None, None, _p(out), Nn, None, _stream())
+    return out
 
 
 def attn_fwd(qkv, B, Ntok, H, scale):

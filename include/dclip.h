@@ -84,6 +84,17 @@ int dclip_gemm(int epilogue, int ab_dt,
                const float* bias, const void* aux, int aux_dt, int64_t ld_aux,
                void* C, int c_dt, int64_t ldc, void* C2, int64_t ldc2, void* stream);
 
+/* C[m][n] = sum_k A[k][m] * B[k][n] ("TN": reduction over the ROWS of both operands —
+ * the weight-gradient shape dW = dY^T X without transposed copies).  A: (K, lda >= M),
+ * B: (K, ldb >= N), M % 8 == N % 8 == 0.  The K range is split into `splits` chunks of
+ * K_pad / splits (K_pad >= K, multiple of 64*splits; rows >= K contribute zero).
+ * epilogue STORE (f32 C, splits == 1) or SPLITK (f32 slabs in ws, splits*M*N, then a
+ * combine that adds bias[n] when non-null).  colsum_a (f32, M), when non-null, receives
+ * += the column sums of A over the K rows (the bias gradient of dY).                  */
+int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda, const void* B, int64_t ldb,
+                  int64_t M, int64_t N, int64_t K, int64_t K_pad, int splits, const float* bias,
+                  void* ws, void* C, int64_t ldc, float* colsum_a, void* stream);
+
 /* Fused multi-head attention over a packed QKV buffer.
  * qkv: (B*N, 3*H*D) row-major, [q | k | v] each (H, D) head-major (the layout of
  *      x @ in_proj_weight^T + in_proj_bias, models.py:289 / F.multi_head_attention_forward)

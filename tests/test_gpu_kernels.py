@@ -134,6 +134,14 @@ def test_weight_grad_splitk(M, N, K):
     assert rel_err(db, dy.float().sum(0)) < 1e-5
 
 
+@pytest.mark.parametrize("K,M,N", [(64, 128, 128), (100, 136, 72), (1000, 256, 384), (8193, 768, 768)])
+def test_gemm_tn(K, M, N):
+    O = ops()
+    A = torch.randn(K, M, device=DEV).to(torch.bfloat16)
+    B = torch.randn(K, N, device=DEV).to(torch.bfloat16)
+    assert rel_err(O.gemm_tn(A, B), A.float().t() @ B.float()) < 1e-5
+
+
 # ----------------------------------------------------------------------------- attention
 def attn_ref(qkv, B, N, H):
     C = qkv.shape[1] // 3
