@@ -12,7 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DCLIP_LIB", os.path.join(_HERE, "libdclip.so"))
 
 F32, F16, BF16 = 0, 1, 2
-EPI_STORE, EPI_GELU, EPI_RESIDUAL, EPI_GELU_BWD, EPI_SPLITK = 0, 1, 2, 3, 4
+EPI_STORE, EPI_GELU, EPI_RESIDUAL, EPI_GELU_BWD, EPI_SPLITK, EPI_STORE_SCALED = 0, 1, 2, 3, 4, 5
 
 _c_void_p = ctypes.c_void_p
 _i32 = ctypes.c_int

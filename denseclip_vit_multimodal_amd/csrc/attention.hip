@@ -120,7 +120,7 @@ __device__ __forceinline__ void tile_store(const TileRegs<ROWS>& R, char* lds) {
 // ============================================================================ forward
 template <typename T>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const T* __restrict__ qkv, T* __restrict__ out,
-                                                          float* __restrict__ lse, int N, int H, float c) {
+                                                          float* __restrict__ lse, int N, int H) {
     typedef typename Mfma<T>::frag frag;
     __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 64 * 128];  // [buf][K|V][64 rows][128 B]
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -138,12 +138,15 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const T* __restrict__ 
     const int q = qblk * 128 + wave * 32 + l32;  // this lane's query row
     const int qc = q < N ? q : N - 1;
 
-    frag qf[4];
+    frag qf[4];  // log2-domain queries (pre-multiplied by scale*log2(e) in the qkv buffer)
 #pragma unroll
     for (int s = 0; s < 4; ++s) qf[s] = *(const frag*)(Qb + (int64_t)qc * ld + (2 * s + h) * 8);
 
     f32x16 o[2] = {zero16(), zero16()};
-    float m = -INFINITY, l = 0.f;
+    // running row reference m (log2 units) and -m broadcast as the S accumulator's
+    // initial value, so the MFMA chain returns S' - m and P = exp2(acc) needs no FMA
+    float m = 0.f, l = 0.f;
+    f32x16 negm = zero16();
     const int nt = (N + 63) / 64;
 
     TileRegs<64> rk, rv;
@@ -161,15 +164,17 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const T* __restrict__ 
             tile_load<T, 64>(rk, Kb, ld, (t + 1) * 64, N);
             tile_load<T, 64>(rv, Vb, ld, (t + 1) * 64, N);
         }
-        // S^T[key][q] for two 32-key blocks; all K fragments issued before the MFMAs
+        // S'^T[key][q] - m for two 32-key blocks; all K fragments issued before the MFMAs
         frag kf[2][4];
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int s = 0; s < 4; ++s) kf[kb][s] = row_frag<T>(Kt, kb * 32 + l32, 2 * s + h);
-        f32x16 sacc[2] = {zero16(), zero16()};
+        f32x16 sacc[2];
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
+        for (int kb = 0; kb < 2; ++kb) sacc[kb] = Mfma<T>::mma(kf[kb][0], qf[0], negm);
+#pragma unroll
+        for (int s = 1; s < 4; ++s)
 #pragma unroll
             for (int kb = 0; kb < 2; ++kb) sacc[kb] = Mfma<T>::mma(kf[kb][s], qf[s], sacc[kb]);
         // V^T fragments of the first key block: in flight during the softmax
@@ -185,33 +190,44 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const T* __restrict__ 
                 for (int r = 0; r < 16; ++r)
                     if (t * 64 + kb * 32 + acc_row(r, h) >= N) sacc[kb][r] = -INFINITY;
         }
-        float mx = -INFINITY;
+        // row max (relative to m): 4 independent partial chains, then the partner half
+        float mxp[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[kb][r]);
+            for (int r = 0; r < 16; ++r) mxp[r & 3] = fmaxf(mxp[r & 3], sacc[kb][r]);
+        float mx = fmaxf(fmaxf(mxp[0], mxp[1]), fmaxf(mxp[2], mxp[3]));
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        const float mnew = fmaxf(m, mx * c);
-        // exact lazy rescale: O and l only need rescaling when some row max grew
-        // (wave-uniform branch; rows whose max did not grow have alpha = 1)
-        if (__any(mnew > m)) {
-            const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+        // exact online softmax with the row reference m = running row max: the first tile
+        // sets it, later tiles move it only when the row max grows (wave-uniform branch,
+        // rare after the first tiles).  P = exp2(S' - m) <= 1 with the max element exactly 1.
+        const float shift = t == 0 ? mx : fmaxf(mx, 0.f);
+        if (__any(shift != 0.f)) {
+            // first tile: l = O = 0, and a very negative row max must not make 0 * inf
+            const float alpha = __builtin_amdgcn_exp2f(fminf(-shift, 100.f));
             l *= alpha;
 #pragma unroll
             for (int db = 0; db < 2; ++db)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
-            m = mnew;
+            m += shift;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) negm[r] = -m;
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) sacc[kb][r] -= shift;
         }
-        float rs = 0.f;
+        float rsp[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const float p = __builtin_amdgcn_exp2f(fmaf(sacc[kb][r], c, -m));
+                const float p = __builtin_amdgcn_exp2f(sacc[kb][r]);
                 sacc[kb][r] = p;
-                rs += p;
+                rsp[r & 3] += p;
             }
+        float rs = (rsp[0] + rsp[1]) + (rsp[2] + rsp[3]);
         rs += __shfl_xor(rs, 32, 64);
         l += rs;
         // O^T[d][q] += V^T[d][key] P^T[key][q]
@@ -290,7 +306,7 @@ template <typename T>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
                                                              const float* __restrict__ lse,
                                                              const float* __restrict__ delta, T* __restrict__ dqkv,
-                                                             int N, int H, float c, float scale) {
+                                                             int N, int H, float scale) {
     typedef typename Mfma<T>::frag frag;
     __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 64 * 128];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -313,8 +329,18 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const T* __restrict
         qf[s] = *(const frag*)(Qb + (int64_t)qc * ld + (2 * s + h) * 8);
         gf[s] = *(const frag*)(dOb + (int64_t)qc * C + (2 * s + h) * 8);
     }
-    const float Lq = lse[(int64_t)bh * N + qc];
-    const float dq_delta = delta[(int64_t)bh * N + qc];
+    // row constants as the initial accumulators: S' - L and dP - delta come out of the
+    // MFMA chains directly
+    f32x16 negL, negD;
+    {
+        const float Lq = lse[(int64_t)bh * N + qc];
+        const float Dq = delta[(int64_t)bh * N + qc];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            negL[r] = -Lq;
+            negD[r] = -Dq;
+        }
+    }
 
     f32x16 dq[2] = {zero16(), zero16()};
     const int nt = (N + 63) / 64;
@@ -333,8 +359,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const T* __restrict
             tile_load<T, 64>(rk, Kb, ld, (t + 1) * 64, N);
             tile_load<T, 64>(rv, Vb, ld, (t + 1) * 64, N);
         }
-        f32x16 sacc[2] = {zero16(), zero16()};
-        f32x16 pacc[2] = {zero16(), zero16()};
+        f32x16 sacc[2] = {negL, negL};
+        f32x16 pacc[2] = {negD, negD};
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
             frag kf[4], vf[4];
@@ -359,9 +385,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const T* __restrict
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                float p = __builtin_amdgcn_exp2f(fmaf(sacc[kb][r], c, -Lq));
+                float p = __builtin_amdgcn_exp2f(sacc[kb][r]);
                 if (ragged && t * 64 + kb * 32 + acc_row(r, h) >= N) p = 0.f;
-                sacc[kb][r] = p * (pacc[kb][r] - dq_delta) * DsScale<T>::v;  // dS^T (scaled)
+                sacc[kb][r] = p * pacc[kb][r] * DsScale<T>::v;  // dS^T (scaled)
             }
         // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
 #pragma unroll
@@ -415,8 +441,8 @@ template <typename T>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
                                                                const float* __restrict__ lse,
                                                                const float* __restrict__ delta,
-                                                               T* __restrict__ dqkv, int N, int H, float c,
-                                                               float scale) {
+                                                               T* __restrict__ dqkv, int N, int H,
+                                                               float dk_scale) {
     typedef typename Mfma<T>::frag frag;
     constexpr int QS = 64;  // query rows per pipeline stage
     // [buf][Q | dO][64 rows][128 B] + [buf][L | delta][64 floats]
@@ -455,7 +481,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const T* __restri
         if (threadIdx.x < 2 * QS) {
             int r = t * QS + (threadIdx.x & (QS - 1));
             r = r < N ? r : N - 1;
-            rstat = threadIdx.x < QS ? Lb[r] : Db[r];
+            rstat = -(threadIdx.x < QS ? Lb[r] : Db[r]);  // staged negated: accumulator inits
         }
     };
     auto store = [&](int buf) {
@@ -486,7 +512,17 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const T* __restri
                 qa[s] = row_frag<T>(Qt, l32, 2 * s + h);
                 ga[s] = row_frag<T>(Gt, l32, 2 * s + h);
             }
-            f32x16 sacc = zero16(), pacc = zero16();
+            f32x16 sacc, pacc;  // start from -L[q] / -delta[q] per row
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                const f32x4 Lv = *(const f32x4*)(Ls + 8 * g4 + 4 * h);
+                const f32x4 Dv = *(const f32x4*)(Ds + 8 * g4 + 4 * h);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    sacc[4 * g4 + e] = Lv[e];
+                    pacc[4 * g4 + e] = Dv[e];
+                }
+            }
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 sacc = Mfma<T>::mma(qa[s], kf[s], sacc);
@@ -503,17 +539,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const T* __restri
                 }
             const bool ragged = q0 + 32 > N;
 #pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {
-                const f32x4 Lv = *(const f32x4*)(Ls + 8 * g4 + 4 * h);
-                const f32x4 Dv = *(const f32x4*)(Ds + 8 * g4 + 4 * h);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int r = 4 * g4 + e;
-                    float p = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -Lv[e]));
-                    if (ragged && q0 + acc_row(r, h) >= N) p = 0.f;
-                    sacc[r] = p;                                           // P
-                    pacc[r] = p * (pacc[r] - Dv[e]) * DsScale<T>::v;       // dS (scaled)
-                }
+            for (int r = 0; r < 16; ++r) {
+                float p = __builtin_amdgcn_exp2f(sacc[r]);
+                if (ragged && q0 + acc_row(r, h) >= N) p = 0.f;
+                sacc[r] = p;                                   // P
+                pacc[r] = p * pacc[r] * DsScale<T>::v;         // dS (scaled)
             }
             // dV^T[d][key] += dO^T[d][q] P[q][key] ;  dK^T[d][key] += Q^T[d][q] dS[q][key]
 #pragma unroll
@@ -530,7 +560,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const T* __restri
         if (more) store(buf ^ 1);
         __syncthreads();
     }
-    scale *= 1.0f / DsScale<T>::v;
+    const float scale = dk_scale / DsScale<T>::v;
     if (key < N) {
         T* rk = dqkv + ((int64_t)b * N + key) * ld + C + hd * HD;
         T* rvp = rk + C;
@@ -552,7 +582,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const T* __restri
 template <typename T>
 void fwd_launch(const void* qkv, void* o, float* lse, int B, int N, int H, float scale, hipStream_t st) {
     dim3 grid(((N + 127) / 128) * B * H);
-    attn_fwd_kernel<T><<<grid, 256, 0, st>>>((const T*)qkv, (T*)o, lse, N, H, scale * LOG2E);
+    attn_fwd_kernel<T><<<grid, 256, 0, st>>>((const T*)qkv, (T*)o, lse, N, H);
 }
 
 template <typename T>
@@ -562,10 +592,10 @@ void bwd_launch(const void* qkv, const void* o, const void* dout, const float* l
     attn_delta_kernel<T><<<(unsigned)((total + 255) / 256), 256, 0, st>>>((const T*)o, (const T*)dout, delta, N, H,
                                                                           total);
     dim3 grid(((N + 127) / 128) * B * H);
-    attn_bwd_dq_kernel<T><<<grid, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, (T*)dqkv, N, H,
-                                                scale * LOG2E, scale);
+    // dQ (w.r.t. the unscaled q) = dZ K scale;  dK = dZ^T q scale = dZ^T q' / log2(e)
+    attn_bwd_dq_kernel<T><<<grid, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, (T*)dqkv, N, H, scale);
     attn_bwd_dkdv_kernel<T><<<grid, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, (T*)dqkv, N, H,
-                                                  scale * LOG2E, scale);
+                                                  1.0f / LOG2E);
 }
 
 }  // namespace

@@ -122,6 +122,12 @@ __device__ __forceinline__ void gemm_epilogue(f32x16 (&acc)[2][2], char* smem, i
 #pragma unroll
                     for (int e = 0; e < 4; ++e) v[e] += (n + e < N) ? bias[n + e] : 0.f;
                 }
+                if constexpr (EPI == DCLIP_EPI_STORE_SCALED) {
+                    const int n = n0 + wn * 64 + col;
+                    const float* sc = (const float*)aux;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] *= (n + e < N) ? sc[n + e] : 1.f;
+                }
                 *(f32x4*)(ep + (j * 32 + l32) * EP_LD + col) = v;
             }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
@@ -141,7 +147,7 @@ __device__ __forceinline__ void gemm_epilogue(f32x16 (&acc)[2][2], char* smem, i
             v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
         }
         const bool full = nb + 8 <= N;
-        if constexpr (EPI == DCLIP_EPI_STORE) {
+        if constexpr (EPI == DCLIP_EPI_STORE || EPI == DCLIP_EPI_STORE_SCALED) {
             store8<OutT>((OutT*)C + (int64_t)m * ldc + nb, v, full, N - nb);
         } else if constexpr (EPI == DCLIP_EPI_GELU) {
             float g[8];
@@ -338,18 +344,39 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(
     gemm_epilogue<T, EPI, OutT>(acc, smem, M, N, m0, n0, bias, nullptr, 0, C, ldc, nullptr, 0, slab);
 }
 
-// per-column sums of a row-major (rows x cols) matrix, accumulated into out (f32)
+// per-column sums of a row-major (rows x cols) matrix, accumulated into out (f32):
+// a block covers 64 columns (8 lanes x 8 columns, 16-byte loads) x a chunk of rows
+// (32 row lanes), reduces its 32 partial sums per column in LDS, one atomic per column.
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ x, int64_t ld, int64_t rows, int cols,
                                                      int64_t rows_per_block, float* __restrict__ out) {
-    const int c = blockIdx.x * 256 + threadIdx.x;
-    if (c >= cols) return;
+    __shared__ float red[32][65];
+    const int cx = threadIdx.x & 7, ry = threadIdx.x >> 3;
+    const int c0 = blockIdx.x * 64 + cx * 8;
     const int64_t r0 = blockIdx.y * rows_per_block;
     int64_t r1 = r0 + rows_per_block;
     r1 = r1 < rows ? r1 : rows;
-    float s = 0.f;
-    for (int64_t r = r0; r < r1; ++r) s += (float)x[r * ld + c];
-    atomicAdd(out + c, s);
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (c0 + 8 <= cols) {
+        typedef T t8 __attribute__((ext_vector_type(8)));
+        for (int64_t r = r0 + ry; r < r1; r += 32) {
+            const t8 v = *(const t8*)(x + r * ld + c0);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) s[e] += (float)v[e];
+        }
+    } else {
+        for (int64_t r = r0 + ry; r < r1; r += 32)
+            for (int e = 0; e < 8 && c0 + e < cols; ++e) s[e] += (float)x[r * ld + c0 + e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[ry][cx * 8 + e] = s[e];
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        float t = 0.f;
+        for (int k = 0; k < 32; ++k) t += red[k][threadIdx.x];
+        const int c = blockIdx.x * 64 + threadIdx.x;
+        if (c < cols) atomicAdd(out + c, t);
+    }
 }
 
 // out[m][n] = sum_z ws[z][m][n] (+ bias[n]) — the split-K combine (deterministic order)
@@ -395,6 +422,8 @@ int dispatch(int epi, int c_dt, const void* A, int64_t lda, const void* B, int64
             if (c_dt == DCLIP_F32)
                 return launch<T, DCLIP_EPI_STORE, float>(A, lda, B, ldb, M, N, K, 1, bias, aux, ld_aux, C, ldc, C2, ldc2, st);
             return launch<T, DCLIP_EPI_STORE, T>(A, lda, B, ldb, M, N, K, 1, bias, aux, ld_aux, C, ldc, C2, ldc2, st);
+        case DCLIP_EPI_STORE_SCALED:
+            return launch<T, DCLIP_EPI_STORE_SCALED, T>(A, lda, B, ldb, M, N, K, 1, bias, aux, ld_aux, C, ldc, C2, ldc2, st);
         case DCLIP_EPI_GELU:
             return launch<T, DCLIP_EPI_GELU, T>(A, lda, B, ldb, M, N, K, 1, bias, aux, ld_aux, C, ldc, C2, ldc2, st);
         case DCLIP_EPI_RESIDUAL:
@@ -436,6 +465,10 @@ extern "C" int dclip_gemm(int epilogue, int ab_dt, const void* A, int64_t lda, c
     switch (epilogue) {
         case DCLIP_EPI_STORE:
             DCLIP_HOST_CHECK(c_dt == DCLIP_F32 || c_dt == ab_dt, "dclip_gemm: STORE output must be f32 or the operand dtype");
+            break;
+        case DCLIP_EPI_STORE_SCALED:
+            DCLIP_HOST_CHECK(c_dt == ab_dt && aux != nullptr && aux_dt == DCLIP_F32,
+                             "dclip_gemm: STORE_SCALED needs an f32 per-column scale vector in aux and C of the operand dtype");
             break;
         case DCLIP_EPI_GELU:
             DCLIP_HOST_CHECK(c_dt == ab_dt && C2 != nullptr, "dclip_gemm: GELU needs C and C2 of the operand dtype");
@@ -483,8 +516,8 @@ extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda
     const int k_chunk = (int)(K_pad / splits);
     dim3 grid(tiles_m * tiles_n, splits);
     if (colsum_a) {
-        const int64_t rpb = 512;
-        dim3 cg((unsigned)((M + 255) / 256), (unsigned)((K + rpb - 1) / rpb));
+        const int64_t rpb = 2048;
+        dim3 cg((unsigned)((M + 63) / 64), (unsigned)((K + rpb - 1) / rpb));
         if (ab_dt == DCLIP_BF16) colsum_kernel<bf16><<<cg, 256, 0, st>>>((const bf16*)A, lda, K, (int)M, rpb, colsum_a);
         else colsum_kernel<f16><<<cg, 256, 0, st>>>((const f16*)A, lda, K, (int)M, rpb, colsum_a);
     }

@@ -181,7 +181,26 @@ def gemm_tn(A, B):
     return out
 
 
+LOG2E = 1.4426950408889634
+
+
+def qkv_scale_vector(C, H, device):
+    """Per-column epilogue scale of the in-projection: q columns x d^-0.5 log2(e)
+    (the attention kernels take log2-domain queries), k and v columns x 1."""
+    key = (C, H, str(device))
+    v = _QSCALE.get(key)
+    if v is None:
+        v = torch.ones(3 * C, dtype=torch.float32, device=device)
+        v[:C] = (C // H) ** -0.5 * LOG2E
+        _QSCALE[key] = v
+    return v
+
+
+_QSCALE = {}
+
+
 def attn_fwd(qkv, B, Ntok, H, scale):
+    """qkv with the q columns pre-multiplied by scale*log2(e) (qkv_scale_vector)."""
     _check(qkv)
     C = qkv.shape[1] // 3
     o = torch.empty(B * Ntok, C, dtype=qkv.dtype, device=qkv.device)
@@ -354,7 +373,8 @@ class BlockFn(torch.autograd.Function):
         C = x.shape[1]
         scale = (C // H) ** -0.5
         xh1, mu1, rs1 = layernorm_fwd(x, ln1w.detach(), ln1b.detach(), cdt)
-        qkv = gemm(xh1, WEIGHTS.get(w_in, cdt), bias=b_in.detach())
+        qkv = gemm(xh1, WEIGHTS.get(w_in, cdt), N.EPI_STORE_SCALED, bias=b_in.detach(),
+                   aux=qkv_scale_vector(C, H, x.device))
         o, lse = attn_fwd(qkv, B, Ntok, H, scale)
         xm = gemm(o, WEIGHTS.get(w_out, cdt), N.EPI_RESIDUAL, bias=b_out.detach(), aux=x)
         xh2, mu2, rs2 = layernorm_fwd(xm, ln2w.detach(), ln2b.detach(), cdt)

@@ -56,6 +56,9 @@ extern "C" {
 #define DCLIP_EPI_SPLITK 4     /* C(f32) = sum over K splits (+ bias): partial f32 slabs
                                   in the caller's workspace aux (splits*M*N f32), then
                                   one deterministic combine pass (weight gradients)    */
+#define DCLIP_EPI_STORE_SCALED 5 /* C = (acc + bias[n]) * aux[n], aux = f32 per-column scale
+                                  (the q columns of the in-projection pre-multiplied by
+                                  d^-0.5 * log2(e) for dclip_attn_*)                    */
 
 const char* dclip_last_error(void);
 int dclip_abi_version(void);
@@ -98,6 +101,8 @@ int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda, const voi
 /* Fused multi-head attention over a packed QKV buffer.
  * qkv: (B*N, 3*H*D) row-major, [q | k | v] each (H, D) head-major (the layout of
  *      x @ in_proj_weight^T + in_proj_bias, models.py:289 / F.multi_head_attention_forward)
+ *      with the q columns PRE-MULTIPLIED by c = scale * log2(e) ("log2-domain queries",
+ *      produced for free by the in-projection GEMM's DCLIP_EPI_STORE_SCALED epilogue)
  * o:   (B*N, H*D) softmax(q k^T * scale) v, heads concatenated
  * lse: (B, H, N) f32, log2-domain row statistic  max*c + log2(sum), c = scale*log2(e)
  * D must be 64.                                                                      */
@@ -107,7 +112,9 @@ int dclip_attn_fwd(int dt, const void* qkv, void* o, float* lse,
 /* Attention backward (flash-style recompute from lse; no N x N buffer, no atomics):
  * a delta pass (rowsum(dout*o)), a query-major dQ pass and a key-major dK/dV pass.
  * dout: (B*N, H*D) dt.  delta_ws: f32 (B*H*N) workspace.
- * dqkv: (B*N, 3*H*D) dt output, [dq | dk | dv] in the qkv layout.                   */
+ * qkv as for dclip_attn_fwd (q pre-multiplied by scale*log2(e)); `scale` = d^-0.5.
+ * dqkv: (B*N, 3*H*D) dt output, [dq | dk | dv] in the qkv layout: gradients with
+ * respect to the UNSCALED q, k, v (i.e. the in-projection output before the q scale).  */
 int dclip_attn_bwd(int dt, const void* qkv, const void* o, const void* dout,
                    const float* lse, float* delta_ws, void* dqkv,
                    int B, int N, int H, int D, float scale, void* stream);

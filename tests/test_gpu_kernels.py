@@ -143,6 +143,18 @@ def test_gemm_tn(K, M, N):
 
 
 # ----------------------------------------------------------------------------- attention
+def prescale(qkv, H):
+    """The kernels take log2-domain queries (q * d^-0.5 * log2 e, rounded to the operand
+    dtype); returns (kernel input, the equivalent unscaled fp32 qkv for the reference)."""
+    C = qkv.shape[1] // 3
+    c = 64 ** -0.5 * math.log2(math.e)
+    ks = qkv.clone()
+    ks[:, :C] = (qkv[:, :C].float() * c).to(qkv.dtype)
+    ref = qkv.float().clone()
+    ref[:, :C] = ks[:, :C].float() / c
+    return ks, ref
+
+
 def attn_ref(qkv, B, N, H):
     C = qkv.shape[1] // 3
     q, k, v = qkv.float().view(B, N, 3, H, C // H).permute(2, 0, 3, 1, 4)
@@ -156,28 +168,32 @@ def test_attention_fwd(N, dt):
     O = ops()
     B, H = 2, 3
     C = 64 * H
-    qkv = (torch.randn(B * N, 3 * C, device=DEV) * 1.5).to(dt)
+    qkv, qref = prescale((torch.randn(B * N, 3 * C, device=DEV) * 1.5).to(dt), H)
     o, lse = O.attn_fwd(qkv, B, N, H, 64 ** -0.5)
-    ref = attn_ref(qkv, B, N, H)
+    ref = attn_ref(qref, B, N, H)
     assert rel_err(o.float(), ref) < TOL[dt]
     # lse (log2 domain): log2 sum exp(s * scale)
-    q, k, _ = qkv.float().view(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    q, k, _ = qref.view(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
     s = (q @ k.transpose(-1, -2)) * 64 ** -0.5
     lref = torch.logsumexp(s, -1) / math.log(2)
     assert (lse.view(B, H, N) - lref).abs().max() < 1e-2
 
 
-def test_attention_spiky_rescale():
-    """Force the online-softmax running max to jump late (guide rule 26)."""
+@pytest.mark.parametrize("spike", [4.0, 40.0, -40.0])
+def test_attention_spiky_rescale(spike):
+    """Force the softmax reference to jump late, by more and less than the deferred
+    re-referencing threshold, and all-negative logits (guide rule 26)."""
     O = ops()
     B, H, N = 1, 1, 300
     C = 64
     qkv = torch.randn(B * N, 3 * C, device=DEV) * 0.3
     qkv[:, :64] = 1.0
-    qkv[250, 64:128] = 4.0  # one late key dominates every query
-    qkv = qkv.to(torch.float16)
+    qkv[250, 64:128] = spike  # one late key dominates (or trails) every query
+    if spike < 0:
+        qkv[:, 64:128] = spike * (1 + 0.01 * torch.randn(N, 64, device=DEV))
+    qkv, qref = prescale(qkv.to(torch.float16), H)
     o, _ = O.attn_fwd(qkv, B, N, H, 64 ** -0.5)
-    assert rel_err(o.float(), attn_ref(qkv, B, N, H)) < TOL[torch.float16]
+    assert rel_err(o.float(), attn_ref(qref, B, N, H)) < TOL[torch.float16]
 
 
 @pytest.mark.parametrize("N", [1, 33, 130, 257, 700])
@@ -186,11 +202,11 @@ def test_attention_bwd(N, dt):
     O = ops()
     B, H = 2, 2
     C = 64 * H
-    qkv = torch.randn(B * N, 3 * C, device=DEV).to(dt)
+    qkv, qref = prescale(torch.randn(B * N, 3 * C, device=DEV).to(dt), H)
     dout = torch.randn(B * N, C, device=DEV).to(dt)
     o, lse = O.attn_fwd(qkv, B, N, H, 64 ** -0.5)
     dqkv = O.attn_bwd(qkv, o, dout, lse, B, N, H, 64 ** -0.5)
-    q32 = qkv.float().requires_grad_(True)
+    q32 = qref.clone().requires_grad_(True)
     ref = attn_ref(q32, B, N, H)
     ref.backward(dout.float())
     g = q32.grad

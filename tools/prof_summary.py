@@ -14,8 +14,9 @@ from collections import defaultdict
 
 
 def short(name):
-    n = re.sub(r"\(.*", "", name)
-    n = n.replace("void ", "").replace("(anonymous namespace)::", "")
+    n = name.replace("(anonymous namespace)::", "")
+    n = re.sub(r"\(.*", "", n)
+    n = n.replace("void ", "")
     m = re.search(r"_ZN12_GLOBAL__N_1\d+(\w+?)I", n)
     if m:
         n = m.group(1) + n[n.find("I", m.end() - 1):][:40]
