@@ -25,16 +25,16 @@ _SIGS = {
                             _i64, _i64, _f32, _c_void_p],
     "dclip_layernorm_bwd": [_c_void_p, _i32, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32,
                             _c_void_p, _c_void_p, _i64, _i64, _c_void_p],
-    "dclip_gemm": [_i32, _i32, _c_void_p, _i64, _c_void_p, _i64, _i64, _i64, _i64, _i32, _c_void_p, _c_void_p,
+    "dclip_gemm": [_i32, _i32, _c_void_p, _i64, _c_void_p, _i64, _i64, _i64, _i64, _i32, _f32, _c_void_p, _c_void_p,
                    _i32, _i64, _c_void_p, _i32, _i64, _c_void_p, _i64, _c_void_p],
-    "dclip_gemm_tn": [_i32, _i32, _c_void_p, _i64, _c_void_p, _i64, _i64, _i64, _i64, _i64, _i32, _c_void_p,
+    "dclip_gemm_tn": [_i32, _i32, _c_void_p, _i64, _c_void_p, _i64, _i64, _i64, _i64, _i64, _i32, _f32, _c_void_p,
                       _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p],
     "dclip_attn_fwd": [_i32, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i32, _i32, _f32, _c_void_p],
     "dclip_attn_bwd": [_i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i32,
                        _i32, _f32, _c_void_p],
     "dclip_im2col": [_c_void_p, _i32, _c_void_p, _i32, _i32, _i32, _i32, _i32, _i32, _c_void_p],
     "dclip_tokens_fwd": [_c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p],
-    "dclip_tokens_bwd": [_c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p],
+    "dclip_tokens_bwd": [_c_void_p, _c_void_p, _i32, _f32, _c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p],
     "dclip_pos_interp_fwd": [_c_void_p, _c_void_p, _i32, _i32, _i32, _i32, _c_void_p],
     "dclip_pos_interp_bwd": [_c_void_p, _c_void_p, _i32, _i32, _i32, _i32, _c_void_p],
     "dclip_transpose": [_c_void_p, _i32, _i64, _i64, _i64, _c_void_p, _i32, _i64, _i64, _i32, _i64, _i64, _i64,
@@ -43,7 +43,7 @@ _SIGS = {
     "dclip_score_map": [_c_void_p, _i32, _c_void_p, _c_void_p, _i32, _i32, _i32, _i32, _f32, _c_void_p],
     "dclip_bilinear_fwd": [_c_void_p, _i32, _c_void_p, _i32, _i64, _i32, _i32, _i32, _i32, _c_void_p],
     "dclip_bilinear_bwd": [_c_void_p, _i32, _c_void_p, _c_void_p, _i64, _i32, _i32, _i32, _i32, _c_void_p],
-    "dclip_cast": [_c_void_p, _i32, _c_void_p, _i32, _i64, _c_void_p],
+    "dclip_cast": [_c_void_p, _i32, _c_void_p, _i32, _i64, _f32, _c_void_p],
 }
 EXPORTED = sorted(list(_SIGS) + ["dclip_last_error", "dclip_abi_version"])
 

@@ -76,11 +76,13 @@ __device__ __forceinline__ f32x16 zero16() {
     return z;
 }
 
-// dS = P (dP - delta) is ~1/N in magnitude; for fp16 operands it is pre-scaled by 2^8 before
-// the 16-bit conversion (keeps N = 8193 values out of the fp16 subnormal range) and the
-// dQ / dK accumulators are scaled back in the epilogue.  bf16 has the fp32 exponent range.
+// dS = P (dP - delta) is ~|dO|/N in magnitude; for fp16 operands it is pre-scaled by 2^4
+// before the 16-bit conversion (with dO already gradient-scaled to amax ~16 by the host,
+// ops.grad_scale, this keeps N = 8193 values out of the fp16 subnormal range without
+// overflow risk) and the dQ / dK accumulators are scaled back in the epilogue.  bf16 has
+// the fp32 exponent range.
 template <typename T> struct DsScale { static constexpr float v = 1.0f; };
-template <> struct DsScale<f16> { static constexpr float v = 256.0f; };
+template <> struct DsScale<f16> { static constexpr float v = 16.0f; };
 
 // accumulator register r -> row offset within a 32x32 tile (column = lane & 31)
 __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }

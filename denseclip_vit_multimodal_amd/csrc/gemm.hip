@@ -95,7 +95,7 @@ template <typename T, int EPI, typename OutT>
 __device__ __forceinline__ void gemm_epilogue(f32x16 (&acc)[2][2], char* smem, int M, int N, int m0, int n0,
                                               const float* __restrict__ bias, const void* __restrict__ aux,
                                               int64_t ld_aux, void* __restrict__ C, int64_t ldc,
-                                              void* __restrict__ C2, int64_t ldc2, int64_t slab) {
+                                              void* __restrict__ C2, int64_t ldc2, int64_t slab, float alpha) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int wm = wave >> 1, wn = wave & 1;
@@ -116,7 +116,7 @@ __device__ __forceinline__ void gemm_epilogue(f32x16 (&acc)[2][2], char* smem, i
                 const int col = i * 32 + q * 8 + h * 4;
                 f32x4 v;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+                for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e] * alpha;
                 if (bias != nullptr && EPI != DCLIP_EPI_SPLITK && EPI != DCLIP_EPI_GELU_BWD) {
                     const int n = n0 + wn * 64 + col;
 #pragma unroll
@@ -184,7 +184,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(
     const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
     int M, int N, int k_chunk, int tiles_m, int tiles_n,
     const float* __restrict__ bias, const void* __restrict__ aux, int64_t ld_aux,
-    void* __restrict__ C, int64_t ldc, void* __restrict__ C2, int64_t ldc2, int64_t slab) {
+    void* __restrict__ C, int64_t ldc, void* __restrict__ C2, int64_t ldc2, int64_t slab, float alpha) {
     __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -233,7 +233,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(
         __syncthreads();
     }
 
-    gemm_epilogue<T, EPI, OutT>(acc, smem, M, N, m0, n0, bias, aux, ld_aux, C, ldc, C2, ldc2, slab);
+    gemm_epilogue<T, EPI, OutT>(acc, smem, M, N, m0, n0, bias, aux, ld_aux, C, ldc, C2, ldc2, slab, alpha);
 }
 
 // ---------------------------------------------------------------------------- "TN"
@@ -280,7 +280,7 @@ template <typename T, int EPI, typename OutT>
 __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(
     const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
     int M, int N, int Kreal, int k_chunk, int tiles_m, int tiles_n, const float* __restrict__ bias,
-    void* __restrict__ C, int64_t ldc, int64_t slab) {
+    void* __restrict__ C, int64_t ldc, int64_t slab, float alpha) {
     __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -341,7 +341,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(
         }
         __syncthreads();
     }
-    gemm_epilogue<T, EPI, OutT>(acc, smem, M, N, m0, n0, bias, nullptr, 0, C, ldc, nullptr, 0, slab);
+    gemm_epilogue<T, EPI, OutT>(acc, smem, M, N, m0, n0, bias, nullptr, 0, C, ldc, nullptr, 0, slab, alpha);
 }
 
 // per-column sums of a row-major (rows x cols) matrix, accumulated into out (f32):
@@ -349,7 +349,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(
 // (32 row lanes), reduces its 32 partial sums per column in LDS, one atomic per column.
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ x, int64_t ld, int64_t rows, int cols,
-                                                     int64_t rows_per_block, float* __restrict__ out) {
+                                                     int64_t rows_per_block, float alpha, float* __restrict__ out) {
     __shared__ float red[32][65];
     const int cx = threadIdx.x & 7, ry = threadIdx.x >> 3;
     const int c0 = blockIdx.x * 64 + cx * 8;
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ x, in
         float t = 0.f;
         for (int k = 0; k < 32; ++k) t += red[k][threadIdx.x];
         const int c = blockIdx.x * 64 + threadIdx.x;
-        if (c < cols) atomicAdd(out + c, t);
+        if (c < cols) atomicAdd(out + c, t * alpha);
     }
 }
 
@@ -402,38 +402,38 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, i
 
 template <typename T, int EPI, typename OutT>
 int launch(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
-           int splits, const float* bias, const void* aux, int64_t ld_aux, void* C, int64_t ldc,
+           int splits, float alpha, const float* bias, const void* aux, int64_t ld_aux, void* C, int64_t ldc,
            void* C2, int64_t ldc2, hipStream_t st) {
     const int tiles_m = (int)((M + BM - 1) / BM), tiles_n = (int)((N + BN - 1) / BN);
     const int k_chunk = (int)(K / splits);
     dim3 grid(tiles_m * tiles_n, splits);
     gemm_nt_kernel<T, EPI, OutT><<<grid, 256, 0, st>>>(
         (const T*)A, lda, (const T*)B, ldb, (int)M, (int)N, k_chunk, tiles_m, tiles_n, bias, aux,
-        ld_aux, C, ldc, C2, ldc2, (int64_t)M * N);
+        ld_aux, C, ldc, C2, ldc2, (int64_t)M * N, alpha);
     return 0;
 }
 
 template <typename T>
 int dispatch(int epi, int c_dt, const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M,
-             int64_t N, int64_t K, int splits, const float* bias, const void* aux, int64_t ld_aux,
+             int64_t N, int64_t K, int splits, float alpha, const float* bias, const void* aux, int64_t ld_aux,
              void* C, int64_t ldc, void* C2, int64_t ldc2, hipStream_t st) {
     switch (epi) {
         case DCLIP_EPI_STORE:
             if (c_dt == DCLIP_F32)
-                return launch<T, DCLIP_EPI_STORE, float>(A, lda, B, ldb, M, N, K, 1, bias, aux, ld_aux, C, ldc, C2, ldc2, st);
-            return launch<T, DCLIP_EPI_STORE, T>(A, lda, B, ldb, M, N, K, 1, bias, aux, ld_aux, C, ldc, C2, ldc2, st);
+                return launch<T, DCLIP_EPI_STORE, float>(A, lda, B, ldb, M, N, K, 1, alpha, bias, aux, ld_aux, C, ldc, C2, ldc2, st);
+            return launch<T, DCLIP_EPI_STORE, T>(A, lda, B, ldb, M, N, K, 1, alpha, bias, aux, ld_aux, C, ldc, C2, ldc2, st);
         case DCLIP_EPI_STORE_SCALED:
-            return launch<T, DCLIP_EPI_STORE_SCALED, T>(A, lda, B, ldb, M, N, K, 1, bias, aux, ld_aux, C, ldc, C2, ldc2, st);
+            return launch<T, DCLIP_EPI_STORE_SCALED, T>(A, lda, B, ldb, M, N, K, 1, alpha, bias, aux, ld_aux, C, ldc, C2, ldc2, st);
         case DCLIP_EPI_GELU:
-            return launch<T, DCLIP_EPI_GELU, T>(A, lda, B, ldb, M, N, K, 1, bias, aux, ld_aux, C, ldc, C2, ldc2, st);
+            return launch<T, DCLIP_EPI_GELU, T>(A, lda, B, ldb, M, N, K, 1, alpha, bias, aux, ld_aux, C, ldc, C2, ldc2, st);
         case DCLIP_EPI_RESIDUAL:
-            return launch<T, DCLIP_EPI_RESIDUAL, float>(A, lda, B, ldb, M, N, K, 1, bias, aux, ld_aux, C, ldc, C2, ldc2, st);
+            return launch<T, DCLIP_EPI_RESIDUAL, float>(A, lda, B, ldb, M, N, K, 1, alpha, bias, aux, ld_aux, C, ldc, C2, ldc2, st);
         case DCLIP_EPI_GELU_BWD:
-            return launch<T, DCLIP_EPI_GELU_BWD, T>(A, lda, B, ldb, M, N, K, 1, bias, aux, ld_aux, C, ldc, C2, ldc2, st);
+            return launch<T, DCLIP_EPI_GELU_BWD, T>(A, lda, B, ldb, M, N, K, 1, alpha, bias, aux, ld_aux, C, ldc, C2, ldc2, st);
         case DCLIP_EPI_SPLITK: {
             // partial slabs in the caller's workspace (aux), then one combine pass
             float* ws = (float*)const_cast<void*>(aux);
-            launch<T, DCLIP_EPI_SPLITK, float>(A, lda, B, ldb, M, N, K, splits, nullptr, nullptr, 0,
+            launch<T, DCLIP_EPI_SPLITK, float>(A, lda, B, ldb, M, N, K, splits, alpha, nullptr, nullptr, 0,
                                                ws, N, nullptr, 0, st);
             const int64_t total4 = M * (N / 4);
             int blocks = (int)((total4 + 255) / 256);
@@ -449,7 +449,7 @@ int dispatch(int epi, int c_dt, const void* A, int64_t lda, const void* B, int64
 }  // namespace
 
 extern "C" int dclip_gemm(int epilogue, int ab_dt, const void* A, int64_t lda, const void* B,
-                          int64_t ldb, int64_t M, int64_t N, int64_t K, int splits,
+                          int64_t ldb, int64_t M, int64_t N, int64_t K, int splits, float alpha,
                           const float* bias, const void* aux, int aux_dt, int64_t ld_aux, void* C,
                           int c_dt, int64_t ldc, void* C2, int64_t ldc2, void* stream) {
     DCLIP_HOST_CHECK(ab_dt == DCLIP_BF16 || ab_dt == DCLIP_F16, "dclip_gemm: operands must be f16/bf16");
@@ -489,15 +489,15 @@ extern "C" int dclip_gemm(int epilogue, int ab_dt, const void* A, int64_t lda, c
     }
     hipStream_t st = (hipStream_t)stream;
     int rc = ab_dt == DCLIP_BF16
-                 ? dispatch<bf16>(epilogue, c_dt, A, lda, B, ldb, M, N, K, splits, bias, aux, ld_aux, C, ldc, C2, ldc2, st)
-                 : dispatch<f16>(epilogue, c_dt, A, lda, B, ldb, M, N, K, splits, bias, aux, ld_aux, C, ldc, C2, ldc2, st);
+                 ? dispatch<bf16>(epilogue, c_dt, A, lda, B, ldb, M, N, K, splits, alpha, bias, aux, ld_aux, C, ldc, C2, ldc2, st)
+                 : dispatch<f16>(epilogue, c_dt, A, lda, B, ldb, M, N, K, splits, alpha, bias, aux, ld_aux, C, ldc, C2, ldc2, st);
     if (rc) return rc;
     DCLIP_LAUNCH_CHECK();
     return 0;
 }
 
 extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda, const void* B, int64_t ldb,
-                             int64_t M, int64_t N, int64_t K, int64_t K_pad, int splits, const float* bias,
+                             int64_t M, int64_t N, int64_t K, int64_t K_pad, int splits, float alpha, const float* bias,
                              void* ws, void* C, int64_t ldc, float* colsum_a, void* stream) {
     DCLIP_HOST_CHECK(ab_dt == DCLIP_BF16 || ab_dt == DCLIP_F16, "dclip_gemm_tn: operands must be f16/bf16");
     DCLIP_HOST_CHECK(M > 0 && N > 0 && K > 0 && M % 8 == 0 && N % 8 == 0,
@@ -518,13 +518,13 @@ extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda
     if (colsum_a) {
         const int64_t rpb = 2048;
         dim3 cg((unsigned)((M + 63) / 64), (unsigned)((K + rpb - 1) / rpb));
-        if (ab_dt == DCLIP_BF16) colsum_kernel<bf16><<<cg, 256, 0, st>>>((const bf16*)A, lda, K, (int)M, rpb, colsum_a);
-        else colsum_kernel<f16><<<cg, 256, 0, st>>>((const f16*)A, lda, K, (int)M, rpb, colsum_a);
+        if (ab_dt == DCLIP_BF16) colsum_kernel<bf16><<<cg, 256, 0, st>>>((const bf16*)A, lda, K, (int)M, rpb, alpha, colsum_a);
+        else colsum_kernel<f16><<<cg, 256, 0, st>>>((const f16*)A, lda, K, (int)M, rpb, alpha, colsum_a);
     }
 #define TN_LAUNCH(T, EPI, OUT)                                                                               \
     gemm_tn_kernel<T, EPI, float><<<grid, 256, 0, st>>>((const T*)A, lda, (const T*)B, ldb, (int)M, (int)N,   \
                                                         (int)K, k_chunk, tiles_m, tiles_n, nullptr, OUT,        \
-                                                        EPI == DCLIP_EPI_SPLITK ? N : ldc, (int64_t)M * N)
+                                                        EPI == DCLIP_EPI_SPLITK ? N : ldc, (int64_t)M * N, alpha)
     if (epilogue == DCLIP_EPI_STORE) {
         DCLIP_HOST_CHECK(bias == nullptr, "dclip_gemm_tn: bias only with SPLITK");
         if (ab_dt == DCLIP_BF16) TN_LAUNCH(bf16, DCLIP_EPI_STORE, C);

@@ -55,8 +55,9 @@ __global__ void tokens_fwd_kernel(const TP* __restrict__ patch, const float* __r
 }
 
 template <typename TP>
-__global__ void tokens_bwd_kernel(const float* __restrict__ dx, TP* __restrict__ dpatch, float* __restrict__ dcls,
-                                  float* __restrict__ dpos, int B, int P, int C, int64_t total4) {
+__global__ void tokens_bwd_kernel(const float* __restrict__ dx, TP* __restrict__ dpatch, float dpatch_scale,
+                                  float* __restrict__ dcls, float* __restrict__ dpos, int B, int P, int C,
+                                  int64_t total4) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over (P+1) * C/4
     if (i >= total4) return;
     const int c4 = C / 4;
@@ -68,7 +69,8 @@ __global__ void tokens_bwd_kernel(const float* __restrict__ dx, TP* __restrict__
         acc += g;
         if (t > 0 && dpatch) {
             TP* d = dpatch + ((int64_t)b * P + (t - 1)) * C + c;
-            d[0] = (TP)g[0]; d[1] = (TP)g[1]; d[2] = (TP)g[2]; d[3] = (TP)g[3];
+            d[0] = (TP)(g[0] * dpatch_scale); d[1] = (TP)(g[1] * dpatch_scale);
+            d[2] = (TP)(g[2] * dpatch_scale); d[3] = (TP)(g[3] * dpatch_scale);
         }
     }
     if (dpos) *(f32x4*)(dpos + (int64_t)t * C + c) += acc;
@@ -307,14 +309,14 @@ __global__ __launch_bounds__(256) void score_map_kernel(const TV* __restrict__ v
 
 // ---------------------------------------------------------------------------- cast
 template <typename TI, typename TO>
-__global__ void cast_kernel(const TI* __restrict__ in, TO* __restrict__ out, int64_t n) {
+__global__ void cast_kernel(const TI* __restrict__ in, TO* __restrict__ out, int64_t n, float scale) {
     for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n;
          i += (int64_t)gridDim.x * blockDim.x * 4) {
         if (i + 3 < n) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) out[i + e] = (TO)(float)in[i + e];
+            for (int e = 0; e < 4; ++e) out[i + e] = (TO)((float)in[i + e] * scale);
         } else {
-            for (int64_t j = i; j < n; ++j) out[j] = (TO)(float)in[j];
+            for (int64_t j = i; j < n; ++j) out[j] = (TO)((float)in[j] * scale);
         }
     }
 }
@@ -361,13 +363,13 @@ extern "C" int dclip_tokens_fwd(const void* patch, int patch_dt, const float* cl
     return 0;
 }
 
-extern "C" int dclip_tokens_bwd(const float* dx, void* dpatch, int dpatch_dt, float* dcls, float* dpos, int B, int P,
-                                int C, void* stream) {
+extern "C" int dclip_tokens_bwd(const float* dx, void* dpatch, int dpatch_dt, float dpatch_scale, float* dcls,
+                                float* dpos, int B, int P, int C, void* stream) {
     DCLIP_HOST_CHECK(C % 4 == 0, "dclip_tokens_bwd: C %% 4 != 0");
     const int64_t total4 = (int64_t)(P + 1) * C / 4;
     hipStream_t st = (hipStream_t)stream;
     DISPATCH_DT(dpatch_dt, TP,
-        tokens_bwd_kernel<TP><<<(unsigned)((total4 + 255) / 256), 256, 0, st>>>(dx, (TP*)dpatch, dcls, dpos, B, P, C,
+        tokens_bwd_kernel<TP><<<(unsigned)((total4 + 255) / 256), 256, 0, st>>>(dx, (TP*)dpatch, dpatch_scale, dcls, dpos, B, P, C,
                                                                              total4));
     DCLIP_LAUNCH_CHECK();
     return 0;
@@ -457,11 +459,11 @@ extern "C" int dclip_bilinear_bwd(const void* dout, int dout_dt, float* din, flo
     return 0;
 }
 
-extern "C" int dclip_cast(const void* in, int in_dt, void* out, int out_dt, int64_t n, void* stream) {
+extern "C" int dclip_cast(const void* in, int in_dt, void* out, int out_dt, int64_t n, float scale, void* stream) {
     if (n == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
     DISPATCH_DT(in_dt, TI, DISPATCH_DT(out_dt, TO,
-        cast_kernel<TI, TO><<<grid_for((n + 3) / 4), 256, 0, st>>>((const TI*)in, (TO*)out, n)));
+        cast_kernel<TI, TO><<<grid_for((n + 3) / 4), 256, 0, st>>>((const TI*)in, (TO*)out, n, scale)));
     DCLIP_LAUNCH_CHECK();
     return 0;
 }

@@ -94,8 +94,8 @@ def layernorm_bwd(dy, x, w, mean, rstd, dx, accumulate, dw=None, db=None):
            int(accumulate), _p(dw), _p(db), rows, cols, _stream())
 
 
-def gemm(A, B, epi=N.EPI_STORE, bias=None, aux=None, out_dtype=None, out=None, out2=None):
-    """out[m][n] = sum_k A[m][k] B[n][k] (+ epilogue).  A: (M, K), B: (N, K)."""
+def gemm(A, B, epi=N.EPI_STORE, bias=None, aux=None, out_dtype=None, out=None, out2=None, alpha=1.0):
+    """out[m][n] = alpha * sum_k A[m][k] B[n][k] (+ epilogue).  A: (M, K), B: (N, K)."""
     _check(A, B, bias, aux, out, out2)
     M, K = A.shape
     Nn, K2 = B.shape
@@ -106,7 +106,7 @@ def gemm(A, B, epi=N.EPI_STORE, bias=None, aux=None, out_dtype=None, out=None, o
     if epi == N.EPI_GELU and out2 is None:
         out2 = torch.empty(M, Nn, dtype=A.dtype, device=A.device)
     e0 = _tic()
-    N.call("dclip_gemm", epi, _dt(A), _p(A), A.stride(0), _p(B), B.stride(0), M, Nn, K, 1, _p(bias), _p(aux),
+    N.call("dclip_gemm", epi, _dt(A), _p(A), A.stride(0), _p(B), B.stride(0), M, Nn, K, 1, float(alpha), _p(bias), _p(aux),
            _dt(aux) if aux is not None else 0, aux.stride(0) if aux is not None else 0, _p(out), _dt(out),
            out.stride(0), _p(out2), out2.stride(0) if out2 is not None else 0, _stream())
     _toc("gemm", e0)
@@ -126,13 +126,34 @@ def transpose(x, rows, cols, out_dtype, r0=0, batch=1, in_bstride=0, rows_pad=No
     return out
 
 
-def cast(x, dtype):
+def cast(x, dtype, scale=1.0):
+    """(dtype)(x * scale)."""
     _check(x)
-    if x.dtype == dtype:
+    if x.dtype == dtype and scale == 1.0:
         return x
     y = torch.empty(x.shape, dtype=dtype, device=x.device)
-    N.call("dclip_cast", _p(x), _dt(x), _p(y), _DT[dtype], x.numel(), _stream())
+    N.call("dclip_cast", _p(x), _dt(x), _p(y), _DT[dtype], x.numel(), float(scale), _stream())
     return y
+
+
+FP16_GRAD_AMAX = 16.0
+
+
+def grad_scale(g, cdt):
+    """Power-of-two scale for casting the fp32 gradient g to the compute dtype.
+
+    bf16 has the fp32 exponent range: 1.0, no host round trip.  fp16 does not: the
+    gradients of a segmentation loss averaged over ~10^5-10^7 pixels sit at 1e-5..1e-9,
+    in (or below) fp16's subnormal range, so they are scaled to amax ~ FP16_GRAD_AMAX
+    before the cast and every fp32 result computed from them is unscaled by the GEMM's
+    alpha (one device->host read of amax per backward block, fp16 mode only)."""
+    if cdt != torch.float16:
+        return 1.0
+    amax = float(g.detach().abs().amax())
+    if not math.isfinite(amax) or amax == 0.0:
+        return 1.0
+    e = math.floor(math.log2(FP16_GRAD_AMAX / amax))
+    return float(2.0 ** max(-60, min(60, e)))
 
 
 def _wgrad_splits(tiles, M, slots=512):
@@ -149,8 +170,9 @@ def _wgrad_splits(tiles, M, slots=512):
     return best
 
 
-def weight_grad(dy, x, want_bias=True):
-    """dW = dy^T x (N x K, fp32) and db = colsum(dy) for dy (M, N), x (M, K) (compute dtype).
+def weight_grad(dy, x, want_bias=True, alpha=1.0):
+    """dW = alpha dy^T x (N x K, fp32) and db = alpha colsum(dy) for dy (M, N), x (M, K)
+    (compute dtype).
 
     One "TN" MFMA GEMM reading both operands in their natural token-major layout (the
     reduction runs over the rows), split over the M tokens with a deterministic slab
@@ -165,7 +187,7 @@ def weight_grad(dy, x, want_bias=True):
     ws = torch.empty(splits, Nn, K, dtype=torch.float32, device=dy.device)
     e0 = _tic()
     N.call("dclip_gemm_tn", N.EPI_SPLITK, _dt(dy), _p(dy), dy.stride(0), _p(x), x.stride(0), Nn, K, M, k_pad,
-           splits, None, _p(ws), _p(dW), K, _p(db), _stream())
+           splits, float(alpha), None, _p(ws), _p(dW), K, _p(db), _stream())
     _toc("gemm_wgrad", e0)
     return dW, db
 
@@ -177,7 +199,7 @@ def gemm_tn(A, B):
     Nn = B.shape[1]
     out = torch.empty(M, Nn, dtype=torch.float32, device=A.device)
     N.call("dclip_gemm_tn", N.EPI_STORE, _dt(A), _p(A), A.stride(0), _p(B), B.stride(0), M, Nn, K,
-           math.ceil(K / 64) * 64, 1, None, None, _p(out), Nn, None, _stream())
+           math.ceil(K / 64) * 64, 1, 1.0, None, None, _p(out), Nn, None, _stream())
     return out
 
 
@@ -344,7 +366,8 @@ class PatchEmbedFn(torch.autograd.Function):
         demb = torch.empty(B * P, C, dtype=cdt, device=dx.device)
         dcls = torch.zeros(C, dtype=torch.float32, device=dx.device)
         dposf = torch.zeros(P + 1, C, dtype=torch.float32, device=dx.device)
-        N.call("dclip_tokens_bwd", _p(dxp), _p(demb), _DT[cdt], _p(dcls), _p(dposf), B, P, C, _stream())
+        s = grad_scale(dxp, cdt) if need[1] else 1.0
+        N.call("dclip_tokens_bwd", _p(dxp), _p(demb), _DT[cdt], float(s), _p(dcls), _p(dposf), B, P, C, _stream())
         dpos = None
         if need[3]:
             if interp:
@@ -354,7 +377,7 @@ class PatchEmbedFn(torch.autograd.Function):
                 dpos = dposf
         dconv = None
         if need[1]:
-            dW, _ = weight_grad(demb, patches, want_bias=False)
+            dW, _ = weight_grad(demb, patches, want_bias=False, alpha=1.0 / s)
             dconv = dW.view(wshape)
         return (None, dconv, dcls if need[2] else None, dpos, dlnw if need[4] else None,
                 dlnb if need[5] else None, None, None)
@@ -397,14 +420,16 @@ class BlockFn(torch.autograd.Function):
         wg = any(need[2:])
 
         # ---- MLP: xo = xm + h W2^T + b2,  h = qgelu(z),  z = xh2 W1^T + b1
-        dy = cast(dxo, cdt)
+        # (s1, s2: power-of-two gradient scales, 1.0 unless fp16 — see grad_scale)
+        s1 = grad_scale(dxo, cdt)
+        dy = cast(dxo, cdt, s1)
         dz = gemm(dy, WEIGHTS.get(w2, cdt, transposed=True), N.EPI_GELU_BWD, aux=z)
         dW2 = db2 = dW1 = db1 = None
         if wg:
-            dW2, db2 = weight_grad(dy, h)
-        dxh2 = gemm(dz, WEIGHTS.get(w1, cdt, transposed=True), out_dtype=torch.float32)
+            dW2, db2 = weight_grad(dy, h, alpha=1.0 / s1)
+        dxh2 = gemm(dz, WEIGHTS.get(w1, cdt, transposed=True), out_dtype=torch.float32, alpha=1.0 / s1)
         if wg:
-            dW1, db1 = weight_grad(dz, xh2)
+            dW1, db1 = weight_grad(dz, xh2, alpha=1.0 / s1)
         del dz
         dxm = dxo.clone()
         dln2w = torch.zeros(C, dtype=torch.float32, device=x.device)
@@ -412,17 +437,18 @@ class BlockFn(torch.autograd.Function):
         layernorm_bwd(dxh2, xm, ln2w.detach(), mu2, rs2, dxm, 1, dln2w, dln2b)
         del dxh2
         # ---- attention: xm = x + o Wout^T + bout
-        dyo = cast(dxm, cdt)
+        s2 = grad_scale(dxm, cdt)
+        dyo = cast(dxm, cdt, s2)
         do = gemm(dyo, WEIGHTS.get(w_out, cdt, transposed=True))
         dWo = dbo = dWi = dbi = None
         if wg:
-            dWo, dbo = weight_grad(dyo, o)
+            dWo, dbo = weight_grad(dyo, o, alpha=1.0 / s2)
         del dyo
-        dqkv = attn_bwd(qkv, o, do, lse, B, Ntok, H, scale)
+        dqkv = attn_bwd(qkv, o, do, lse, B, Ntok, H, scale)  # linear in dO: carries s2
         del do
-        dxh1 = gemm(dqkv, WEIGHTS.get(w_in, cdt, transposed=True), out_dtype=torch.float32)
+        dxh1 = gemm(dqkv, WEIGHTS.get(w_in, cdt, transposed=True), out_dtype=torch.float32, alpha=1.0 / s2)
         if wg:
-            dWi, dbi = weight_grad(dqkv, xh1)
+            dWi, dbi = weight_grad(dqkv, xh1, alpha=1.0 / s2)
         del dqkv
         dln1w = torch.zeros(C, dtype=torch.float32, device=x.device)
         dln1b = torch.zeros(C, dtype=torch.float32, device=x.device)

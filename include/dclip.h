@@ -77,25 +77,26 @@ int dclip_layernorm_bwd(const void* dy, int dy_dt, const void* x, int x_dt,
                         float* dx, int accumulate, float* dw, float* db,
                         int64_t rows, int64_t cols, void* stream);
 
-/* C[m][n] = sum_k A[m][k] * B[n][k]  ("NT": both operands k-contiguous, ab_dt in
+/* C[m][n] = alpha * sum_k A[m][k] * B[n][k]  ("NT": both operands k-contiguous, ab_dt in
  * {F16, BF16}), m < M, n < N, k < K (K % 64 == 0, lda/ldb % 8 == 0), then the
  * epilogue.  bias: f32[N] or null.  aux: epilogue side input (see DCLIP_EPI_*).
+ * alpha undoes a gradient scale carried by an operand (fp16 backward; 1 otherwise).
  * splits > 1 (EPI_SPLITK only) splits K into `splits` equal 64-multiple chunks.      */
 int dclip_gemm(int epilogue, int ab_dt,
                const void* A, int64_t lda, const void* B, int64_t ldb,
-               int64_t M, int64_t N, int64_t K, int splits,
+               int64_t M, int64_t N, int64_t K, int splits, float alpha,
                const float* bias, const void* aux, int aux_dt, int64_t ld_aux,
                void* C, int c_dt, int64_t ldc, void* C2, int64_t ldc2, void* stream);
 
-/* C[m][n] = sum_k A[k][m] * B[k][n] ("TN": reduction over the ROWS of both operands —
+/* C[m][n] = alpha * sum_k A[k][m] * B[k][n] ("TN": reduction over the ROWS of both operands —
  * the weight-gradient shape dW = dY^T X without transposed copies).  A: (K, lda >= M),
  * B: (K, ldb >= N), M % 8 == N % 8 == 0.  The K range is split into `splits` chunks of
  * K_pad / splits (K_pad >= K, multiple of 64*splits; rows >= K contribute zero).
  * epilogue STORE (f32 C, splits == 1) or SPLITK (f32 slabs in ws, splits*M*N, then a
  * combine that adds bias[n] when non-null).  colsum_a (f32, M), when non-null, receives
- * += the column sums of A over the K rows (the bias gradient of dY).                  */
+ * += alpha * the column sums of A over the K rows (the bias gradient of dY).          */
 int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda, const void* B, int64_t ldb,
-                  int64_t M, int64_t N, int64_t K, int64_t K_pad, int splits, const float* bias,
+                  int64_t M, int64_t N, int64_t K, int64_t K_pad, int splits, float alpha, const float* bias,
                   void* ws, void* C, int64_t ldc, float* colsum_a, void* stream);
 
 /* Fused multi-head attention over a packed QKV buffer.
@@ -130,10 +131,10 @@ int dclip_im2col(const void* img, int img_dt, void* out, int out_dt,
 int dclip_tokens_fwd(const void* patch, int patch_dt, const float* cls, const float* pos,
                      float* x, int B, int P, int C, void* stream);
 
-/* Token assembly backward: dpatch[b*P+i] = dx[b][1+i] (dpatch_dt);
+/* Token assembly backward: dpatch[b*P+i] = dpatch_scale * dx[b][1+i] (dpatch_dt);
  * dcls += sum_b dx[b][0]; dpos[t] += sum_b dx[b][t]  (dcls/dpos f32, accumulated)   */
-int dclip_tokens_bwd(const float* dx, void* dpatch, int dpatch_dt, float* dcls, float* dpos,
-                     int B, int P, int C, void* stream);
+int dclip_tokens_bwd(const float* dx, void* dpatch, int dpatch_dt, float dpatch_scale, float* dcls,
+                     float* dpos, int B, int P, int C, void* stream);
 
 /* Bilinear (align_corners=False) resize of the g x g patch grid of pos (g*g+1, C)
  * to H x W; out (H*W+1, C), row 0 = pos row 0.                                       */
@@ -168,8 +169,9 @@ int dclip_bilinear_fwd(const void* in, int in_dt, void* out, int out_dt,
 int dclip_bilinear_bwd(const void* dout, int dout_dt, float* din, float* ws,
                        int64_t NC, int Hi, int Wi, int Ho, int Wo, void* stream);
 
-/* Element-wise dtype conversion of n elements.                                      */
-int dclip_cast(const void* in, int in_dt, void* out, int out_dt, int64_t n, void* stream);
+/* Element-wise dtype conversion of n elements: out = (out_dt)(in * scale).  A power-of-two
+ * scale keeps fp16 gradients out of the subnormal range (see dclip_gemm's alpha).     */
+int dclip_cast(const void* in, int in_dt, void* out, int out_dt, int64_t n, float scale, void* stream);
 
 #ifdef __cplusplus
 }
