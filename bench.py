@@ -55,42 +55,18 @@ def attn_flops_fwd(B, N, H, D=64):
 
 def make_model(dev, mode):
     from denseclip_vit_multimodal_amd.config import build_model, load_yaml
+    from denseclip_vit_multimodal_amd.train import freeze_for_mode
     cfg = load_yaml("denseclip_cityscapes.yaml")
-    model = build_model(cfg, clip_path_override="")
-    model = model.to(dev)
-    for name, p in model.named_parameters():
-        frozen = name.startswith("text_encoder.")
-        if mode == "R":
-            frozen = frozen or name.startswith("backbone.")
-        # parameters that feed nothing differentiable in this config: the unused CLIP
-        # projection and the score-map branch (its output is discarded, denseclip.py:747)
-        if name in ("backbone.proj", "contexts", "gamma") or name.startswith(("vis_proj.", "global_proj.")):
-            frozen = True
-        p.requires_grad_(not frozen)
+    model = build_model(cfg, clip_path_override="").to(dev)
+    freeze_for_mode(model, mode)
     return model
 
 
-def synth_batch(B, H, W, dev, rank):
-    g = torch.Generator(device="cpu").manual_seed(1234 + rank)
-    img = torch.randn(B, 3, H, W, generator=g).to(dev).to(torch.bfloat16)
-    g = torch.Generator(device="cpu").manual_seed(1235 + rank)
-    seg = torch.randint(0, 19, (B, H, W), generator=g)
-    seg[torch.rand(B, H, W, generator=g) < 0.1] = 255
-    g = torch.Generator(device="cpu").manual_seed(1236 + rank)
-    depth = 1 + 79 * torch.rand(B, 1, H, W, generator=g)
-    mask = torch.rand(B, 1, H, W, generator=g) >= 0.2
-    return img, seg.to(dev), depth.to(dev), mask.to(dev)
-
-
 def run_steps(model, opt, batch, steps, silog):
-    img, seg, depth, mask = batch
+    from denseclip_vit_multimodal_amd.train import train_step
+    loss = None
     for _ in range(steps):
-        out = model(img, gt_semantic_seg=seg, gt_depth=depth, return_loss=True)
-        loss = F.cross_entropy(out["main_output"], seg, ignore_index=255) + \
-            0.1 * silog(out["depth_output"], depth, mask)
-        opt.zero_grad(set_to_none=True)
-        loss.backward()
-        opt.step()
+        loss = train_step(model, opt, batch, silog)
     return loss
 
 
@@ -159,6 +135,7 @@ def main():
     from denseclip_vit_multimodal_amd.losses import SILogLoss
     silog = SILogLoss()
 
+    from denseclip_vit_multimodal_amd.train import synth_batch, wrap_ddp, make_optimizer
     B, H, W = args.batch, args.height, args.width
     batch = synth_batch(B, H, W, dev, rank)
 
@@ -166,11 +143,8 @@ def main():
         model = make_model(dev, mode)
         model.train()
         if world > 1:
-            from torch.nn.parallel import DistributedDataParallel as DDP
-            model = DDP(model, device_ids=[local], bucket_cap_mb=100, gradient_as_bucket_view=True,
-                        find_unused_parameters=False)
-        params = [p for p in model.parameters() if p.requires_grad]
-        opt = torch.optim.AdamW(params, lr=2e-5, weight_decay=0.01, fused=True)
+            model = wrap_ddp(model, dev)
+        opt = make_optimizer([p for p in model.parameters() if p.requires_grad])
         return model, opt
 
     model, opt = setup(args.mode)

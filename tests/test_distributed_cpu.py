@@ -1,0 +1,132 @@
+"""World-size-2 data-parallel step on CPU (gloo): the N > 1 path of bench.py / train.py.
+
+The HIP ViT cannot run on a CPU host, so the DDP-wrapped module here is the trainable set
+of the reference regime (mode R: neck + decode head + depth head, train_denseclip.py:
+1040-1044) fed with per-rank feature maps; everything around it is the package's own
+data-parallel code (train.wrap_ddp, train.loss_fn, train.make_optimizer, utils.
+init_distributed).  Checked: rank-sharded batches average to the single-process gradient
+of the concatenated batch (DDP all-reduce = weak scaling with fixed per-rank work), and the
+AdamW step leaves both ranks with identical parameters.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+import torch.nn as nn
+import torch.nn.functional as F
+
+from helpers import TINY_CFG, CITYSCAPES_CLASSES, rel_err
+
+
+class _HeadsOnly(nn.Module):
+    """neck -> decode/depth heads -> resize to the label size (DenseCLIP._heads + the
+    train-branch resize of denseclip.py:838-868), on given maps."""
+
+    def __init__(self, model):
+        super().__init__()
+        self.neck, self.decode_head, self.depth_head = model.neck, model.decode_head, model.depth_head
+
+    def forward(self, maps, gt_semantic_seg=None, gt_depth=None, return_loss=True):
+        x = self.neck(list(maps.unbind(0)))
+        x = x[0] if isinstance(x, (list, tuple)) else x
+        hw = gt_semantic_seg.shape[-2:]
+        seg = F.interpolate(self.decode_head(x), size=hw, mode="bilinear", align_corners=False)
+        depth = F.interpolate(self.depth_head(x), size=hw, mode="bilinear", align_corners=False)
+        return {"main_output": seg, "depth_output": depth, "aux_losses": {}}
+
+
+def _model():
+    from denseclip_vit_multimodal_amd import DenseCLIP
+    from denseclip_vit_multimodal_amd.train import freeze_for_mode
+    torch.manual_seed(0)
+    m = DenseCLIP(class_names=CITYSCAPES_CLASSES, **TINY_CFG)
+    trainable = freeze_for_mode(m, "R")
+    names = {n for n, p in m.named_parameters() if p.requires_grad}
+    assert names and all(n.startswith(("neck.", "decode_head.", "depth_head.")) for n in names)
+    assert len(trainable) == len(names)
+    h = _HeadsOnly(m)
+    h.eval()  # BN batch statistics are per-rank in the reference too; eval keeps the check exact
+    for mod in h.modules():
+        for p in mod.parameters(recurse=False):
+            p.requires_grad_(True)
+    return h
+
+
+def _batch(rank, B=2, layers=3, C=128, h=4, w=8, H=16, W=32):
+    from denseclip_vit_multimodal_amd.train import synth_batch
+    g = torch.Generator().manual_seed(100 + rank)
+    maps = torch.randn(layers, B, C, h, w, generator=g)
+    _, seg, depth, mask = synth_batch(B, H, W, torch.device("cpu"), rank=rank, image_dtype=torch.float32)
+    return maps, seg, depth, mask
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    from denseclip_vit_multimodal_amd.utils import init_distributed, cleanup
+    from denseclip_vit_multimodal_amd.train import wrap_ddp, loss_fn, make_optimizer
+    init_distributed(rank, world, backend="gloo")
+    try:
+        model = wrap_ddp(_model())
+        opt = make_optimizer([p for p in model.parameters() if p.requires_grad])
+        maps, seg, depth, mask = _batch(rank)
+        out = model(maps, gt_semantic_seg=seg, gt_depth=depth)
+        loss = loss_fn(out, seg, depth, mask)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        grads = {n: p.grad.clone() for n, p in model.module.named_parameters()}
+        opt.step()
+        params = {n: p.detach().clone() for n, p in model.module.named_parameters()}
+        torch.save({"grads": grads, "params": params, "loss": loss.detach()},
+                   os.path.join(out_dir, f"rank{rank}.pt"))
+    finally:
+        cleanup()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.timeout(300)
+def test_ddp_world2_matches_single_process(tmp_path):
+    from denseclip_vit_multimodal_amd.train import loss_fn
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    r = [torch.load(tmp_path / f"rank{i}.pt", weights_only=True) for i in range(world)]
+
+    # single process: mean of the per-rank losses over the same shards (same thread count
+    # as the workers, so oneDNN picks the same conv algorithms)
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)
+    ref = _model()
+    total = 0
+    for rank in range(world):
+        maps, seg, depth, mask = _batch(rank)
+        out = ref(maps, gt_semantic_seg=seg, gt_depth=depth)
+        total = total + loss_fn(out, seg, depth, mask)
+    (total / world).backward()
+    torch.set_num_threads(nt)
+    for n, p in ref.named_parameters():
+        for i in range(world):
+            g = r[i]["grads"][n]
+            assert rel_err(g, p.grad) < 1e-4, (n, i, rel_err(g, p.grad))  # fp32 sum-order noise only
+    for n in r[0]["params"]:
+        assert torch.equal(r[0]["params"][n], r[1]["params"][n]), n
+    assert not torch.equal(r[0]["loss"], r[1]["loss"])  # the shards really differ
+
+
+def test_rank_shards_are_distinct():
+    from denseclip_vit_multimodal_amd.train import synth_batch
+    a = synth_batch(1, 32, 64, torch.device("cpu"), rank=0, image_dtype=torch.float32)
+    b = synth_batch(1, 32, 64, torch.device("cpu"), rank=1, image_dtype=torch.float32)
+    a2 = synth_batch(1, 32, 64, torch.device("cpu"), rank=0, image_dtype=torch.float32)
+    assert all(torch.equal(x, y) for x, y in zip(a, a2))
+    assert not torch.equal(a[0], b[0]) and not torch.equal(a[1], b[1])
+    seg = a[1]
+    frac_ignore = float((seg == 255).float().mean())
+    assert 0.05 < frac_ignore < 0.15 and int(seg[seg != 255].max()) < 19
