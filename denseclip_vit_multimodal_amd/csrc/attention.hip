@@ -7,40 +7,47 @@
 //
 // Layout: q/k/v are read in place from the packed in-projection output
 // qkv (B*N, 3*C), C = H*64 — each row of one head is 128 contiguous bytes — and O is
-// written as (B*N, C), the out-projection's input.  No reshape/permute copies.
+// written as (B*N, C), the out-projection's input.  No reshape/permute copies.  The q
+// columns arrive pre-multiplied by d^-0.5 * log2(e) (the in-projection GEMM's epilogue),
+// so every softmax runs in the exp2 domain with no per-score multiply.
 //
-// Forward (one workgroup = 4 waves = 128 query rows of one (batch, head)):
-//   * the S^T = K Q^T product is issued with K as the MFMA A-operand, so each lane owns
-//     one query row and the softmax row statistics are lane-local (plus one exchange
-//     with the partner half-wave),
-//   * the P^T accumulator registers are converted to 16-bit in place and used directly
-//     as the B-operand of O^T += V^T P^T (no LDS round trip for P); V^T fragments come
-//     from the row-major V tile with the gfx950 transposing LDS read ds_read_b64_tr_b16,
-//   * K/V tiles of 64 keys are double-buffered in LDS, register-staged (global loads
-//     issued at the top of an iteration, LDS writes at its end) into an XOR-swizzled
-//     image (bank-conflict-free ds_read_b128 row reads),
-//   * online softmax in the exp2 domain, fp32 statistics; lse stored for backward.
-// Backward (FlashAttention-2 style recompute, no atomics):
-//   delta = rowsum(dO * O);  a query-major pass for dQ (same structure as the forward
-//   plus dP^T = V dO^T and dQ^T += K^T dS^T) and a key-major pass for dK, dV in which
-//   the S / dP accumulators (key on the lane) feed dV^T += dO^T P and dK^T += Q^T dS
-//   directly.
+// Common structure (all three kernels): one workgroup = NW waves of 32 rows each (rows =
+// queries for the forward and dQ passes, keys for the dK/dV pass); the streamed operand is
+// staged in 64-row tiles through registers (global loads issued at the top of an
+// iteration, LDS writes at its end — T14) into a 2-slot LDS ring with one barrier per
+// tile; the loop is unrolled by two so every LDS address is a base register plus an
+// immediate.  LDS image: 128-byte rows whose 16-byte chunks are XOR-swizzled by xsw(row),
+// chosen so that both the ds_read_b128 row reads (32 consecutive rows, one chunk) and the
+// ds_read_b64_tr_b16 transposed reads (4 rows x 4 chunks per half-wave) are bank-conflict
+// free (the previous ((row >> 1) & 7) swizzle left the transposed reads 2-way).
+//
+// Forward: S^T = K Q^T is issued with K as the MFMA A-operand, so each lane owns one query
+// row and the softmax statistics are lane-local; P^T accumulators are converted in place
+// and fed as the B-operand of O^T += V^T P^T; V^T fragments come from the row-major V tile
+// via ds_read_b64_tr_b16.  Software-pipelined: iteration t issues S(t+1) beside the
+// softmax of tile t and O += V(t)^T P(t)^T (K runs one tile ahead of V in separate rings).
+// Backward (FlashAttention-2 style recompute from the log2-domain lse, no atomics):
+//   delta = rowsum(dO * O);  a query-major pass for dQ (S^T, dP^T = V dO^T, dQ^T += K^T dS^T)
+//   and a key-major pass for dK, dV in which the S / dP accumulators (key on the lane)
+//   feed dV^T += dO^T P and dK^T += Q^T dS directly.
 #include "common.h"
 
 namespace {
 
-constexpr int HD = 64;        // head dim
+constexpr int HD = 64;  // head dim
 constexpr float LOG2E = 1.4426950408889634f;
 
+// chunk XOR of row r: bit 2 from row bit 1, bits 1..0 from row bits 4..3
+__device__ __forceinline__ int xsw(int row) { return (((row >> 1) & 1) << 2) | ((row >> 3) & 3); }
+
+// byte offset of 16-bit element (row, col) in a [rows][64] image
 __device__ __forceinline__ int swz(int row, int col) {
-    // byte offset of 16-bit element (row, col) in a [rows][64] image with 16-byte chunks
-    // XOR-swizzled by ((row >> 1) & 7)
-    return row * 128 + ((((col >> 3) ^ ((row >> 1) & 7))) << 4) + ((col & 7) << 1);
+    return row * 128 + (((col >> 3) ^ xsw(row)) << 4) + ((col & 7) << 1);
 }
 
 template <typename T>
 __device__ __forceinline__ typename Mfma<T>::frag row_frag(const char* img, int row, int chunk) {
-    return *(const typename Mfma<T>::frag*)(img + row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4));
+    return *(const typename Mfma<T>::frag*)(img + row * 128 + ((chunk ^ xsw(row)) << 4));
 }
 
 // A-operand fragment of X^T for a product that sums over the ROWS of an image whose
@@ -76,6 +83,13 @@ __device__ __forceinline__ f32x16 zero16() {
     return z;
 }
 
+__device__ __forceinline__ f32x16 splat16(float v) {
+    f32x16 z;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) z[e] = v;
+    return z;
+}
+
 // dS = P (dP - delta) is ~|dO|/N in magnitude; for fp16 operands it is pre-scaled by 2^4
 // before the 16-bit conversion (with dO already gradient-scaled to amax ~16 by the host,
 // ops.grad_scale, this keeps N = 8193 values out of the fp16 subnormal range without
@@ -87,196 +101,234 @@ template <> struct DsScale<f16> { static constexpr float v = 16.0f; };
 // accumulator register r -> row offset within a 32x32 tile (column = lane & 31)
 __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
+// row max / sum across the two half-waves (lanes l and l ^ 32) on the VALU
+__device__ __forceinline__ float xhalf_max(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xhalf_sum(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // ---------------------------------------------------------------------------- staging
-// Register-staged tile copies (issue the global loads early, write LDS late — T14): an
-// LDS-DMA (global_load_lds) prefetch here makes hipcc wait vmcnt(0) before every later
-// LDS read of the other buffer, serialising the prefetch with the compute.
-// A tile of ROWS rows x 128 B: each of the 256 threads moves ROWS/32 chunks of 16 B.
+// A tile of ROWS rows x 128 B = ROWS*8 chunks of 16 B over the NT threads of the workgroup.
 typedef int i32x4 __attribute__((ext_vector_type(4)));
-template <int ROWS>
+template <int ROWS, int NT>
 struct TileRegs {
-    i32x4 v[ROWS / 32];  // native vector type: HIP's int4 struct arrays end up in scratch
+    static constexpr int PER = ROWS * 8 / NT;
+    i32x4 v[PER];  // native vector type: HIP's int4 struct arrays end up in scratch
 };
 
-template <typename T, int ROWS>
-__device__ __forceinline__ void tile_load(TileRegs<ROWS>& R, const T* __restrict__ base, int64_t ld, int r0, int N) {
+// rows >= N are clamped to N - 1 (duplicates of a valid row; callers neutralise them)
+template <typename T, int ROWS, int NT>
+__device__ __forceinline__ void tile_load(TileRegs<ROWS, NT>& R, const T* __restrict__ base, int64_t ld, int r0,
+                                          int N) {
 #pragma unroll
-    for (int i = 0; i < ROWS / 32; ++i) {
-        const int idx = i * 256 + threadIdx.x;  // (row, chunk) = (idx >> 3, idx & 7)
+    for (int i = 0; i < TileRegs<ROWS, NT>::PER; ++i) {
+        const int idx = i * NT + threadIdx.x;  // (row, chunk) = (idx >> 3, idx & 7)
         int gr = r0 + (idx >> 3);
         gr = gr < N ? gr : N - 1;
         R.v[i] = *(const i32x4*)(base + (int64_t)gr * ld + (idx & 7) * 8);
     }
 }
 
-template <int ROWS>
-__device__ __forceinline__ void tile_store(const TileRegs<ROWS>& R, char* lds) {
+template <int ROWS, int NT>
+__device__ __forceinline__ void tile_store(const TileRegs<ROWS, NT>& R, char* lds) {
 #pragma unroll
-    for (int i = 0; i < ROWS / 32; ++i) {
-        const int idx = i * 256 + threadIdx.x;
+    for (int i = 0; i < TileRegs<ROWS, NT>::PER; ++i) {
+        const int idx = i * NT + threadIdx.x;
         const int r = idx >> 3, c = idx & 7;
-        *(i32x4*)(lds + r * 128 + ((c ^ ((r >> 1) & 7)) << 4)) = R.v[i];
+        *(i32x4*)(lds + r * 128 + ((c ^ xsw(r)) << 4)) = R.v[i];
     }
 }
 
 // ============================================================================ forward
+// S^T - m for a 64-key tile (two 32-key blocks), all K fragments issued before the MFMAs
 template <typename T>
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const T* __restrict__ qkv, T* __restrict__ out,
-                                                          float* __restrict__ lse, int N, int H) {
-    typedef typename Mfma<T>::frag frag;
-    __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 64 * 128];  // [buf][K|V][64 rows][128 B]
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int h = lane >> 5, l32 = lane & 31;
-    // XCD-aware tile order: the q-blocks of one (batch, head) run on one XCD and share
-    // its L2 copy of that head's K/V stream
-    const int nq = (N + 127) / 128;
-    const int tile = xcd_remap(blockIdx.x, gridDim.x);
-    const int qblk = tile % nq, bh = tile / nq, b = bh / H, hd = bh % H;
-    const int C = H * HD;
-    const int64_t ld = 3 * (int64_t)C;
-    const T* Qb = qkv + (int64_t)b * N * ld + hd * HD;
-    const T* Kb = Qb + C;
-    const T* Vb = Qb + 2 * C;
-    const int q = qblk * 128 + wave * 32 + l32;  // this lane's query row
-    const int qc = q < N ? q : N - 1;
-
-    frag qf[4];  // log2-domain queries (pre-multiplied by scale*log2(e) in the qkv buffer)
+__device__ __forceinline__ void s_tile(f32x16 (&sacc)[2], const char* Kt, const typename Mfma<T>::frag (&qf)[4],
+                                       const f32x16& init, int l32, int h) {
+    typename Mfma<T>::frag kf[2][4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) qf[s] = *(const frag*)(Qb + (int64_t)qc * ld + (2 * s + h) * 8);
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) kf[kb][s] = row_frag<T>(Kt, kb * 32 + l32, 2 * s + h);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) sacc[kb] = Mfma<T>::mma(kf[kb][0], qf[0], init);
+#pragma unroll
+    for (int s = 1; s < 4; ++s)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) sacc[kb] = Mfma<T>::mma(kf[kb][s], qf[s], sacc[kb]);
+}
 
-    f32x16 o[2] = {zero16(), zero16()};
-    // running row reference m (log2 units) and -m broadcast as the S accumulator's
-    // initial value, so the MFMA chain returns S' - m and P = exp2(acc) needs no FMA
-    float m = 0.f, l = 0.f;
-    f32x16 negm = zero16();
-    const int nt = (N + 63) / 64;
+__device__ __forceinline__ float tile_rowmax(const f32x16 (&sacc)[2]) {
+    float mxp[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mxp[r & 3] = fmaxf(mxp[r & 3], sacc[kb][r]);
+    return xhalf_max(fmaxf(fmaxf(mxp[0], mxp[1]), fmaxf(mxp[2], mxp[3])));
+}
 
-    TileRegs<64> rk, rv;
-    tile_load<T, 64>(rk, Kb, ld, 0, N);
-    tile_load<T, 64>(rv, Vb, ld, 0, N);
-    tile_store<64>(rk, smem);
-    tile_store<64>(rv, smem + 8192);
-    __syncthreads();
+template <typename T, int NT>
+struct FwdCtx {
+    typedef typename Mfma<T>::frag frag;
+    char* smem;  // K ring [2][8 KiB] | V ring [2][8 KiB]
+    const T* Kb;
+    const T* Vb;
+    int64_t ld;
+    int N, nt, lane, l32, h;
+    bool ragged;
+    frag qf[4];
+    f32x16 o[2];
+    f32x16 negm;
+    float m, l;
+    TileRegs<64, NT> rk, rv;
+};
 
-    for (int t = 0; t < nt; ++t) {
-        const char* Kt = smem + (t & 1) * 16384;
-        const char* Vt = Kt + 8192;
-        const bool more = t + 1 < nt;
-        if (more) {
-            tile_load<T, 64>(rk, Kb, ld, (t + 1) * 64, N);
-            tile_load<T, 64>(rv, Vb, ld, (t + 1) * 64, N);
-        }
-        // S'^T[key][q] - m for two 32-key blocks; all K fragments issued before the MFMAs
-        frag kf[2][4];
+// One key tile t (LDS slot parity P = t & 1): softmax + PV of tile t from sc, S(t+1) into sn.
+//   * deferred max (T13): the row reference m moves only when a row max exceeds it by
+//     more than THR = 8 (log2 units), so P <= 2^8 (exact in 16-bit relative terms) and the
+//     O / l rescale is a rare wave-uniform branch;
+//   * the ragged last tile needs no mask on S: keys >= N are clamped copies of key N-1
+//     (their scores duplicate a valid score, so row maxima are unchanged); their P is
+//     zeroed in the last iteration only;
+//   * row sums stay per-lane partials until the epilogue.
+template <typename T, int NT, int P>
+__device__ __forceinline__ void fwd_step(FwdCtx<T, NT>& c, int t, f32x16 (&sc)[2], f32x16 (&sn)[2]) {
+    typedef typename Mfma<T>::frag frag;
+    constexpr float THR = 8.0f;
+    char* const Ks = c.smem;
+    char* const Vs = c.smem + 2 * 8192;
+    if (c.ragged && t == c.nt - 1) {
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-            for (int s = 0; s < 4; ++s) kf[kb][s] = row_frag<T>(Kt, kb * 32 + l32, 2 * s + h);
-        f32x16 sacc[2];
+            for (int r = 0; r < 16; ++r)
+                if (t * 64 + kb * 32 + acc_row(r, c.h) >= c.N) sc[kb][r] = -INFINITY;
+    }
+    // prefetch K(t+2), V(t+1) into registers (clamped rows past the end are harmless)
+    tile_load<T, 64, NT>(c.rk, c.Kb, c.ld, (t + 2) * 64, c.N);
+    tile_load<T, 64, NT>(c.rv, c.Vb, c.ld, (t + 1) * 64, c.N);
+    __builtin_amdgcn_sched_barrier(0);  // keep the loads at the top (hipcc sinks them otherwise)
+    // S(t+1) - m on the matrix pipe ...
+    s_tile<T>(sn, Ks + (P ^ 1) * 8192, c.qf, c.negm, c.l32, c.h);
+    // ... beside the softmax of tile t and O^T += V(t)^T P(t)^T
+    const char* Vt = Vs + P * 8192;
+    float rsp[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb) sacc[kb] = Mfma<T>::mma(kf[kb][0], qf[0], negm);
-#pragma unroll
-        for (int s = 1; s < 4; ++s)
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb) sacc[kb] = Mfma<T>::mma(kf[kb][s], qf[s], sacc[kb]);
-        // V^T fragments of the first key block: in flight during the softmax
+    for (int kb = 0; kb < 2; ++kb) {
         frag vf[2][2];
 #pragma unroll
         for (int s = 0; s < 2; ++s)
 #pragma unroll
-            for (int db = 0; db < 2; ++db) vf[s][db] = tr_frag<T>(Vt, 0, s, db, lane);
-        if ((t + 1) * 64 > N) {  // ragged last tile: keys >= N get -inf
+            for (int db = 0; db < 2; ++db) vf[s][db] = tr_frag<T>(Vt, kb, s, db, c.lane);
 #pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    if (t * 64 + kb * 32 + acc_row(r, h) >= N) sacc[kb][r] = -INFINITY;
+        for (int r = 0; r < 16; ++r) {
+            const float p = __builtin_amdgcn_exp2f(sc[kb][r]);
+            sc[kb][r] = p;
+            rsp[r & 3] += p;
         }
-        // row max (relative to m): 4 independent partial chains, then the partner half
-        float mxp[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const frag pf = pack_frag<T>(sc[kb], s);
+#pragma unroll
+            for (int db = 0; db < 2; ++db) c.o[db] = Mfma<T>::mma(vf[s][db], pf, c.o[db]);
+        }
+    }
+    c.l += (rsp[0] + rsp[1]) + (rsp[2] + rsp[3]);
+    // statistics of tile t+1 (garbage, and unused, in the last iteration)
+    const float mx = tile_rowmax(sn);
+    if (__any(mx > THR)) {  // rare: move the reference of the rows whose max grew
+        const float shift = fmaxf(mx, 0.f);
+        const float alpha = __builtin_amdgcn_exp2f(-shift);
+        c.l *= alpha;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) c.o[db][r] *= alpha;
+        c.m += shift;
+        c.negm = splat16(-c.m);
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) mxp[r & 3] = fmaxf(mxp[r & 3], sacc[kb][r]);
-        float mx = fmaxf(fmaxf(mxp[0], mxp[1]), fmaxf(mxp[2], mxp[3]));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        // exact online softmax with the row reference m = running row max: the first tile
-        // sets it, later tiles move it only when the row max grows (wave-uniform branch,
-        // rare after the first tiles).  P = exp2(S' - m) <= 1 with the max element exactly 1.
-        const float shift = t == 0 ? mx : fmaxf(mx, 0.f);
-        if (__any(shift != 0.f)) {
-            // first tile: l = O = 0, and a very negative row max must not make 0 * inf
-            const float alpha = __builtin_amdgcn_exp2f(fminf(-shift, 100.f));
-            l *= alpha;
+            for (int r = 0; r < 16; ++r) sn[kb][r] -= shift;
+    }
+    tile_store<64, NT>(c.rk, Ks + P * 8192);        // K(t+2) over K(t)
+    tile_store<64, NT>(c.rv, Vs + (P ^ 1) * 8192);  // V(t+1) over V(t-1)
+    __syncthreads();
+}
+
+template <typename T, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_kernel(const T* __restrict__ qkv, T* __restrict__ out,
+                                                                   float* __restrict__ lse, int N, int H) {
+    constexpr int NT = 64 * NW, QB = 32 * NW;
+    typedef typename Mfma<T>::frag frag;
+    __shared__ __attribute__((aligned(16))) char smem[4 * 64 * 128];
+    FwdCtx<T, NT> c;
+    c.smem = smem;
+    c.lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    c.h = c.lane >> 5;
+    c.l32 = c.lane & 31;
+    const int nq = (N + QB - 1) / QB;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int qblk = tile % nq, bh = tile / nq, b = bh / H, hd = bh % H;
+    const int C = H * HD;
+    c.ld = 3 * (int64_t)C;
+    const T* Qb = qkv + (int64_t)b * N * c.ld + hd * HD;
+    c.Kb = Qb + C;
+    c.Vb = Qb + 2 * C;
+    c.N = N;
+    c.nt = (N + 63) / 64;
+    c.ragged = (N & 63) != 0;
+    const int q = qblk * QB + wave * 32 + c.l32;
+    const int qc = q < N ? q : N - 1;
 #pragma unroll
-            for (int db = 0; db < 2; ++db)
+    for (int s = 0; s < 4; ++s) c.qf[s] = *(const frag*)(Qb + (int64_t)qc * c.ld + (2 * s + c.h) * 8);
+
+    tile_load<T, 64, NT>(c.rk, c.Kb, c.ld, 0, N);
+    tile_load<T, 64, NT>(c.rv, c.Vb, c.ld, 0, N);
+    tile_store<64, NT>(c.rk, smem);
+    tile_store<64, NT>(c.rv, smem + 2 * 8192);
+    tile_load<T, 64, NT>(c.rk, c.Kb, c.ld, 64, N);  // K(1) (clamped rows when nt == 1: never used)
+    tile_store<64, NT>(c.rk, smem + 8192);
+    __syncthreads();
+
+    // S(0) and the initial row reference m = its row max
+    f32x16 sA[2], sB[2];
+    s_tile<T>(sA, smem, c.qf, zero16(), c.l32, c.h);
+    __syncthreads();  // every wave's K(0) reads are done before iteration 0 overwrites that slot
+    c.m = tile_rowmax(sA);
+    c.negm = splat16(-c.m);
 #pragma unroll
-                for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
-            m += shift;
+    for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) negm[r] = -m;
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) sacc[kb][r] -= shift;
-        }
-        float rsp[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float p = __builtin_amdgcn_exp2f(sacc[kb][r]);
-                sacc[kb][r] = p;
-                rsp[r & 3] += p;
-            }
-        float rs = (rsp[0] + rsp[1]) + (rsp[2] + rsp[3]);
-        rs += __shfl_xor(rs, 32, 64);
-        l += rs;
-        // O^T[d][q] += V^T[d][key] P^T[key][q]
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
-            frag vn[2][2];
-            if (kb == 0) {
-#pragma unroll
-                for (int s = 0; s < 2; ++s)
-#pragma unroll
-                    for (int db = 0; db < 2; ++db) vn[s][db] = tr_frag<T>(Vt, 1, s, db, lane);
-            }
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const frag pf = pack_frag<T>(sacc[kb], s);
-#pragma unroll
-                for (int db = 0; db < 2; ++db) o[db] = Mfma<T>::mma(vf[s][db], pf, o[db]);
-            }
-            if (kb == 0) {
-#pragma unroll
-                for (int s = 0; s < 2; ++s)
-#pragma unroll
-                    for (int db = 0; db < 2; ++db) vf[s][db] = vn[s][db];
-            }
-        }
-        if (more) {
-            char* nx = smem + ((t + 1) & 1) * 16384;
-            tile_store<64>(rk, nx);
-            tile_store<64>(rv, nx + 8192);
-        }
-        __syncthreads();
+        for (int r = 0; r < 16; ++r) sA[kb][r] -= c.m;
+    c.o[0] = zero16();
+    c.o[1] = zero16();
+    c.l = 0.f;
+
+    for (int t = 0; t < c.nt; t += 2) {
+        fwd_step<T, NT, 0>(c, t, sA, sB);
+        if (t + 1 < c.nt) fwd_step<T, NT, 1>(c, t + 1, sB, sA);
     }
 
+    const float lt = xhalf_sum(c.l);
     if (q < N) {
-        const float inv = 1.0f / l;
+        const float inv = 1.0f / lt;
         T* orow = out + ((int64_t)b * N + q) * C + hd * HD;
 #pragma unroll
         for (int db = 0; db < 2; ++db)
 #pragma unroll
             for (int g4 = 0; g4 < 4; ++g4) {
-                const int d = db * 32 + 8 * g4 + 4 * h;
+                const int d = db * 32 + 8 * g4 + 4 * c.h;
                 typedef T t4 __attribute__((ext_vector_type(4)));
-                t4 v = {(T)(o[db][4 * g4] * inv), (T)(o[db][4 * g4 + 1] * inv), (T)(o[db][4 * g4 + 2] * inv),
-                        (T)(o[db][4 * g4 + 3] * inv)};
+                t4 v = {(T)(c.o[db][4 * g4] * inv), (T)(c.o[db][4 * g4 + 1] * inv),
+                        (T)(c.o[db][4 * g4 + 2] * inv), (T)(c.o[db][4 * g4 + 3] * inv)};
                 *(t4*)(orow + d) = v;
             }
-        if (h == 0) lse[(int64_t)bh * N + q] = m + __log2f(l);
+        if (c.h == 0) lse[(int64_t)bh * N + q] = c.m + __log2f(lt);
     }
 }
 
@@ -303,288 +355,349 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const T* __restrict__ o
     delta[(b * H + hd) * N + q] = s;
 }
 
-// Query-major dQ pass: 128 queries per workgroup (32 per wave), all key tiles.
-template <typename T>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
-                                                             const float* __restrict__ lse,
-                                                             const float* __restrict__ delta, T* __restrict__ dqkv,
-                                                             int N, int H, float scale) {
+// ---------------------------------------------------------------------------- dQ pass
+template <typename T, int NT>
+struct DqCtx {
     typedef typename Mfma<T>::frag frag;
-    __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 64 * 128];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int h = lane >> 5, l32 = lane & 31;
-    const int nq = (N + 127) / 128;
-    const int tile = xcd_remap(blockIdx.x, gridDim.x);
-    const int qblk = tile % nq, bh = tile / nq, b = bh / H, hd = bh % H;
-    const int C = H * HD;
-    const int64_t ld = 3 * (int64_t)C;
-    const T* Qb = qkv + (int64_t)b * N * ld + hd * HD;
-    const T* Kb = Qb + C;
-    const T* Vb = Qb + 2 * C;
-    const T* dOb = dout + (int64_t)b * N * C + hd * HD;
-    const int q = qblk * 128 + wave * 32 + l32;
-    const int qc = q < N ? q : N - 1;
-
+    char* smem;  // [slot][K | V][64 rows][128 B]
+    const T* Kb;
+    const T* Vb;
+    int64_t ld;
+    int N, nt, lane, l32, h;
+    bool ragged;
     frag qf[4], gf[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        qf[s] = *(const frag*)(Qb + (int64_t)qc * ld + (2 * s + h) * 8);
-        gf[s] = *(const frag*)(dOb + (int64_t)qc * C + (2 * s + h) * 8);
-    }
-    // row constants as the initial accumulators: S' - L and dP - delta come out of the
-    // MFMA chains directly
     f32x16 negL, negD;
-    {
-        const float Lq = lse[(int64_t)bh * N + qc];
-        const float Dq = delta[(int64_t)bh * N + qc];
+    f32x16 dq[2];
+    TileRegs<64, NT> rk, rv;
+};
+
+// key tile t in LDS slot P: S^T - L, dP^T - delta (row constants as the initial
+// accumulators), dS^T = P (dP - delta), dQ^T += K^T dS^T; prefetches tile t+1.
+template <typename T, int NT, int P>
+__device__ __forceinline__ void dq_step(DqCtx<T, NT>& c, int t) {
+    typedef typename Mfma<T>::frag frag;
+    const char* Kt = c.smem + P * 16384;
+    const char* Vt = Kt + 8192;
+    tile_load<T, 64, NT>(c.rk, c.Kb, c.ld, (t + 1) * 64, c.N);
+    tile_load<T, 64, NT>(c.rv, c.Vb, c.ld, (t + 1) * 64, c.N);
+    __builtin_amdgcn_sched_barrier(0);
+    f32x16 sacc[2] = {c.negL, c.negL};
+    f32x16 pacc[2] = {c.negD, c.negD};
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            negL[r] = -Lq;
-            negD[r] = -Dq;
+    for (int kb = 0; kb < 2; ++kb) {
+        frag kf[4], vf[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            kf[s] = row_frag<T>(Kt, kb * 32 + c.l32, 2 * s + c.h);
+            vf[s] = row_frag<T>(Vt, kb * 32 + c.l32, 2 * s + c.h);
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            sacc[kb] = Mfma<T>::mma(kf[s], c.qf[s], sacc[kb]);
+            pacc[kb] = Mfma<T>::mma(vf[s], c.gf[s], pacc[kb]);
         }
     }
-
-    f32x16 dq[2] = {zero16(), zero16()};
-    const int nt = (N + 63) / 64;
-    TileRegs<64> rk, rv;
-    tile_load<T, 64>(rk, Kb, ld, 0, N);
-    tile_load<T, 64>(rv, Vb, ld, 0, N);
-    tile_store<64>(rk, smem);
-    tile_store<64>(rv, smem + 8192);
-    __syncthreads();
-
-    for (int t = 0; t < nt; ++t) {
-        const char* Kt = smem + (t & 1) * 16384;
-        const char* Vt = Kt + 8192;
-        const bool more = t + 1 < nt;
-        if (more) {
-            tile_load<T, 64>(rk, Kb, ld, (t + 1) * 64, N);
-            tile_load<T, 64>(rv, Vb, ld, (t + 1) * 64, N);
-        }
-        f32x16 sacc[2] = {negL, negL};
-        f32x16 pacc[2] = {negD, negD};
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
-            frag kf[4], vf[4];
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                kf[s] = row_frag<T>(Kt, kb * 32 + l32, 2 * s + h);
-                vf[s] = row_frag<T>(Vt, kb * 32 + l32, 2 * s + h);
-            }
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                sacc[kb] = Mfma<T>::mma(kf[s], qf[s], sacc[kb]);
-                pacc[kb] = Mfma<T>::mma(vf[s], gf[s], pacc[kb]);
-            }
-        }
-        frag kt[2][2];  // K^T fragments for the first key block, in flight during dS
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-            for (int db = 0; db < 2; ++db) kt[s][db] = tr_frag<T>(Kt, 0, s, db, lane);
-        const bool ragged = (t + 1) * 64 > N;
+    if (c.ragged && t == c.nt - 1) {  // keys >= N (clamped copies): P = 0
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                float p = __builtin_amdgcn_exp2f(sacc[kb][r]);
-                if (ragged && t * 64 + kb * 32 + acc_row(r, h) >= N) p = 0.f;
-                sacc[kb][r] = p * pacc[kb][r] * DsScale<T>::v;  // dS^T (scaled)
-            }
-        // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
+            for (int r = 0; r < 16; ++r)
+                if (t * 64 + kb * 32 + acc_row(r, c.h) >= c.N) sacc[kb][r] = -INFINITY;
+    }
+    frag kt[2][2];  // K^T fragments for the first key block, in flight during dS
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
-            frag kn[2][2];
-            if (kb == 0) {
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
-                for (int s = 0; s < 2; ++s)
+        for (int db = 0; db < 2; ++db) kt[s][db] = tr_frag<T>(Kt, 0, s, db, c.lane);
 #pragma unroll
-                    for (int db = 0; db < 2; ++db) kn[s][db] = tr_frag<T>(Kt, 1, s, db, lane);
-            }
+    for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const frag sf = pack_frag<T>(sacc[kb], s);
+        for (int r = 0; r < 16; ++r)
+            sacc[kb][r] = __builtin_amdgcn_exp2f(sacc[kb][r]) * pacc[kb][r] * DsScale<T>::v;  // dS^T
+    // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
 #pragma unroll
-                for (int db = 0; db < 2; ++db) dq[db] = Mfma<T>::mma(kt[s][db], sf, dq[db]);
-            }
-            if (kb == 0) {
+    for (int kb = 0; kb < 2; ++kb) {
+        frag kn[2][2];
+        if (kb == 0) {
 #pragma unroll
-                for (int s = 0; s < 2; ++s)
+            for (int s = 0; s < 2; ++s)
 #pragma unroll
-                    for (int db = 0; db < 2; ++db) kt[s][db] = kn[s][db];
-            }
+                for (int db = 0; db < 2; ++db) kn[s][db] = tr_frag<T>(Kt, 1, s, db, c.lane);
         }
-        if (more) {
-            char* nx = smem + ((t + 1) & 1) * 16384;
-            tile_store<64>(rk, nx);
-            tile_store<64>(rv, nx + 8192);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const frag sf = pack_frag<T>(sacc[kb], s);
+#pragma unroll
+            for (int db = 0; db < 2; ++db) c.dq[db] = Mfma<T>::mma(kt[s][db], sf, c.dq[db]);
         }
-        __syncthreads();
+        if (kb == 0) {
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int db = 0; db < 2; ++db) kt[s][db] = kn[s][db];
+        }
+    }
+    tile_store<64, NT>(c.rk, c.smem + (P ^ 1) * 16384);
+    tile_store<64, NT>(c.rv, c.smem + (P ^ 1) * 16384 + 8192);
+    __syncthreads();
+}
+
+// Query-major dQ pass: 32*NW queries per workgroup (32 per wave), all key tiles.
+template <typename T, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const T* __restrict__ qkv,
+                                                                      const T* __restrict__ dout,
+                                                                      const float* __restrict__ lse,
+                                                                      const float* __restrict__ delta,
+                                                                      T* __restrict__ dqkv, int N, int H,
+                                                                      float scale) {
+    constexpr int NT = 64 * NW, QB = 32 * NW;
+    typedef typename Mfma<T>::frag frag;
+    __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 64 * 128];
+    DqCtx<T, NT> c;
+    c.smem = smem;
+    c.lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    c.h = c.lane >> 5;
+    c.l32 = c.lane & 31;
+    const int nq = (N + QB - 1) / QB;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int qblk = tile % nq, bh = tile / nq, b = bh / H, hd = bh % H;
+    const int C = H * HD;
+    c.ld = 3 * (int64_t)C;
+    const T* Qb = qkv + (int64_t)b * N * c.ld + hd * HD;
+    c.Kb = Qb + C;
+    c.Vb = Qb + 2 * C;
+    const T* dOb = dout + (int64_t)b * N * C + hd * HD;
+    c.N = N;
+    c.nt = (N + 63) / 64;
+    c.ragged = (N & 63) != 0;
+    const int q = qblk * QB + wave * 32 + c.l32;
+    const int qc = q < N ? q : N - 1;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        c.qf[s] = *(const frag*)(Qb + (int64_t)qc * c.ld + (2 * s + c.h) * 8);
+        c.gf[s] = *(const frag*)(dOb + (int64_t)qc * C + (2 * s + c.h) * 8);
+    }
+    c.negL = splat16(-lse[(int64_t)bh * N + qc]);
+    c.negD = splat16(-delta[(int64_t)bh * N + qc]);
+    c.dq[0] = zero16();
+    c.dq[1] = zero16();
+
+    tile_load<T, 64, NT>(c.rk, c.Kb, c.ld, 0, N);
+    tile_load<T, 64, NT>(c.rv, c.Vb, c.ld, 0, N);
+    tile_store<64, NT>(c.rk, smem);
+    tile_store<64, NT>(c.rv, smem + 8192);
+    __syncthreads();
+
+    for (int t = 0; t < c.nt; t += 2) {
+        dq_step<T, NT, 0>(c, t);
+        if (t + 1 < c.nt) dq_step<T, NT, 1>(c, t + 1);
     }
     scale *= 1.0f / DsScale<T>::v;
     if (q < N) {
-        T* row = dqkv + ((int64_t)b * N + q) * ld + hd * HD;
+        T* row = dqkv + ((int64_t)b * N + q) * c.ld + hd * HD;
 #pragma unroll
         for (int db = 0; db < 2; ++db)
 #pragma unroll
             for (int g4 = 0; g4 < 4; ++g4) {
-                const int d = db * 32 + 8 * g4 + 4 * h;
+                const int d = db * 32 + 8 * g4 + 4 * c.h;
                 typedef T t4 __attribute__((ext_vector_type(4)));
-                t4 v = {(T)(dq[db][4 * g4] * scale), (T)(dq[db][4 * g4 + 1] * scale),
-                        (T)(dq[db][4 * g4 + 2] * scale), (T)(dq[db][4 * g4 + 3] * scale)};
+                t4 v = {(T)(c.dq[db][4 * g4] * scale), (T)(c.dq[db][4 * g4 + 1] * scale),
+                        (T)(c.dq[db][4 * g4 + 2] * scale), (T)(c.dq[db][4 * g4 + 3] * scale)};
                 *(t4*)(row + d) = v;
             }
     }
 }
 
-// Key-major dK/dV pass: 128 keys per workgroup (32 per wave); query slices of 64 rows
-// (two 32-row sub-slices per barrier).
-template <typename T>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
-                                                               const float* __restrict__ lse,
-                                                               const float* __restrict__ delta,
-                                                               T* __restrict__ dqkv, int N, int H,
-                                                               float dk_scale) {
+// ---------------------------------------------------------------------------- dK/dV pass
+template <typename T, int NT>
+struct DkvCtx {
     typedef typename Mfma<T>::frag frag;
-    constexpr int QS = 64;  // query rows per pipeline stage
-    // [buf][Q | dO][64 rows][128 B] + [buf][L | delta][64 floats]
-    __shared__ __attribute__((aligned(16))) char smem[2 * 2 * QS * 128 + 2 * 2 * QS * 4];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int h = lane >> 5, l32 = lane & 31;
-    const int nkb = (N + 127) / 128;
+    char* smem;  // [slot][Q | dO][64 rows][128 B] + [slot][-L | -delta][64 floats]
+    const T* Qb;
+    const T* dOb;
+    const float* Lb;
+    const float* Db;
+    int64_t ld;
+    int C, N, nt, lane, l32, h;
+    frag kf[4], vf[4];
+    f32x16 dk[2], dv[2];
+    TileRegs<64, NT> rq, rg;
+    float rstat;
+};
+
+// stage query slice t: Q, dO rows and the negated row statistics (accumulator inits).
+// Query rows >= N get -L = -inf (P = 0, hence dS = 0) and -delta = 0: their clamped Q / dO
+// copies then contribute nothing to dK / dV.
+template <typename T, int NT>
+__device__ __forceinline__ void dkv_load(DkvCtx<T, NT>& c, int t) {
+    tile_load<T, 64, NT>(c.rq, c.Qb, c.ld, t * 64, c.N);
+    tile_load<T, 64, NT>(c.rg, c.dOb, c.C, t * 64, c.N);
+    if (threadIdx.x < 128) {
+        const int r = t * 64 + (threadIdx.x & 63);
+        const int rc = r < c.N ? r : c.N - 1;
+        const float v = threadIdx.x < 64 ? c.Lb[rc] : c.Db[rc];
+        c.rstat = r < c.N ? -v : (threadIdx.x < 64 ? -INFINITY : 0.f);
+    }
+}
+
+template <typename T, int NT>
+__device__ __forceinline__ void dkv_store(DkvCtx<T, NT>& c, int slot) {
+    char* base = c.smem + slot * 16384;
+    tile_store<64, NT>(c.rq, base);
+    tile_store<64, NT>(c.rg, base + 8192);
+    float* stat = (float*)(c.smem + 2 * 16384);
+    if (threadIdx.x < 128) stat[slot * 128 + threadIdx.x] = c.rstat;
+}
+
+template <typename T, int NT, int P>
+__device__ __forceinline__ void dkv_step(DkvCtx<T, NT>& c, int t) {
+    typedef typename Mfma<T>::frag frag;
+    dkv_load<T, NT>(c, t + 1);  // clamped past the end: harmless, never used
+    __builtin_amdgcn_sched_barrier(0);
+    const float* stat = (const float*)(c.smem + 2 * 16384) + P * 128;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+        const char* Qt = c.smem + P * 16384 + sub * 32 * 128;
+        const char* Gt = Qt + 8192;
+        const float* Ls = stat + sub * 32;
+        const float* Ds = Ls + 64;
+        // S[q][key], dP[q][key]  (query rows in registers, key on the lane)
+        frag qa[4], ga[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            qa[s] = row_frag<T>(Qt, c.l32, 2 * s + c.h);
+            ga[s] = row_frag<T>(Gt, c.l32, 2 * s + c.h);
+        }
+        f32x16 sacc, pacc;  // start from -L[q] / -delta[q] per row
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+            const f32x4 Lv = *(const f32x4*)(Ls + 8 * g4 + 4 * c.h);
+            const f32x4 Dv = *(const f32x4*)(Ds + 8 * g4 + 4 * c.h);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                sacc[4 * g4 + e] = Lv[e];
+                pacc[4 * g4 + e] = Dv[e];
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            sacc = Mfma<T>::mma(qa[s], c.kf[s], sacc);
+            pacc = Mfma<T>::mma(ga[s], c.vf[s], pacc);
+        }
+        // dO^T / Q^T fragments for the dV / dK products, in flight during the VALU part
+        frag gt[2][2], qt[2][2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int db = 0; db < 2; ++db) {
+                gt[s][db] = tr_frag<T>(Gt, 0, s, db, c.lane);
+                qt[s][db] = tr_frag<T>(Qt, 0, s, db, c.lane);
+            }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float p = __builtin_amdgcn_exp2f(sacc[r]);
+            sacc[r] = p;                                // P
+            pacc[r] = p * pacc[r] * DsScale<T>::v;      // dS (scaled)
+        }
+        // dV^T[d][key] += dO^T[d][q] P[q][key] ;  dK^T[d][key] += Q^T[d][q] dS[q][key]
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const frag pf = pack_frag<T>(sacc, s);
+            const frag sf = pack_frag<T>(pacc, s);
+#pragma unroll
+            for (int db = 0; db < 2; ++db) {
+                c.dv[db] = Mfma<T>::mma(gt[s][db], pf, c.dv[db]);
+                c.dk[db] = Mfma<T>::mma(qt[s][db], sf, c.dk[db]);
+            }
+        }
+    }
+    dkv_store<T, NT>(c, P ^ 1);
+    __syncthreads();
+}
+
+// Key-major dK/dV pass: 32*NW keys per workgroup (32 per wave); query slices of 64 rows
+// (two 32-row sub-slices per barrier).
+template <typename T, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const T* __restrict__ qkv,
+                                                                        const T* __restrict__ dout,
+                                                                        const float* __restrict__ lse,
+                                                                        const float* __restrict__ delta,
+                                                                        T* __restrict__ dqkv, int N, int H,
+                                                                        float dk_scale) {
+    constexpr int NT = 64 * NW, KB = 32 * NW;
+    typedef typename Mfma<T>::frag frag;
+    __shared__ __attribute__((aligned(16))) char smem[2 * 16384 + 2 * 128 * 4];
+    DkvCtx<T, NT> c;
+    c.smem = smem;
+    c.lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    c.h = c.lane >> 5;
+    c.l32 = c.lane & 31;
+    const int nkb = (N + KB - 1) / KB;
     const int tile = xcd_remap(blockIdx.x, gridDim.x);
     const int kblk = tile % nkb, bh = tile / nkb, b = bh / H, hd = bh % H;
-    const int C = H * HD;
-    const int64_t ld = 3 * (int64_t)C;
-    const T* Qb = qkv + (int64_t)b * N * ld + hd * HD;
-    const T* Kb = Qb + C;
-    const T* Vb = Qb + 2 * C;
-    const T* dOb = dout + (int64_t)b * N * C + hd * HD;
-    const float* Lb = lse + (int64_t)bh * N;
-    const float* Db = delta + (int64_t)bh * N;
-    const int key = kblk * 128 + wave * 32 + l32;
+    c.C = H * HD;
+    c.ld = 3 * (int64_t)c.C;
+    c.Qb = qkv + (int64_t)b * N * c.ld + hd * HD;
+    const T* Kb = c.Qb + c.C;
+    const T* Vb = c.Qb + 2 * c.C;
+    c.dOb = dout + (int64_t)b * N * c.C + hd * HD;
+    c.Lb = lse + (int64_t)bh * N;
+    c.Db = delta + (int64_t)bh * N;
+    c.N = N;
+    c.nt = (N + 63) / 64;
+    const int key = kblk * KB + wave * 32 + c.l32;
     const int kc = key < N ? key : N - 1;
-    float* stat = (float*)(smem + 2 * 2 * QS * 128);
-
-    frag kf[4], vf[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-        kf[s] = *(const frag*)(Kb + (int64_t)kc * ld + (2 * s + h) * 8);
-        vf[s] = *(const frag*)(Vb + (int64_t)kc * ld + (2 * s + h) * 8);
+        c.kf[s] = *(const frag*)(Kb + (int64_t)kc * c.ld + (2 * s + c.h) * 8);
+        c.vf[s] = *(const frag*)(Vb + (int64_t)kc * c.ld + (2 * s + c.h) * 8);
     }
-    f32x16 dk[2] = {zero16(), zero16()}, dv[2] = {zero16(), zero16()};
-    const int nt = (N + QS - 1) / QS;
+    c.dk[0] = zero16();
+    c.dk[1] = zero16();
+    c.dv[0] = zero16();
+    c.dv[1] = zero16();
+    c.rstat = 0.f;
 
-    TileRegs<QS> rq, rg;
-    float rstat = 0.f;
-    auto load = [&](int t) {
-        tile_load<T, QS>(rq, Qb, ld, t * QS, N);
-        tile_load<T, QS>(rg, dOb, C, t * QS, N);
-        if (threadIdx.x < 2 * QS) {
-            int r = t * QS + (threadIdx.x & (QS - 1));
-            r = r < N ? r : N - 1;
-            rstat = -(threadIdx.x < QS ? Lb[r] : Db[r]);  // staged negated: accumulator inits
-        }
-    };
-    auto store = [&](int buf) {
-        char* base = smem + buf * (2 * QS * 128);
-        tile_store<QS>(rq, base);
-        tile_store<QS>(rg, base + QS * 128);
-        if (threadIdx.x < 2 * QS) stat[buf * 2 * QS + threadIdx.x] = rstat;
-    };
-    load(0);
-    store(0);
+    dkv_load<T, NT>(c, 0);
+    dkv_store<T, NT>(c, 0);
     __syncthreads();
-
-    for (int t = 0; t < nt; ++t) {
-        const int buf = t & 1;
-        const bool more = t + 1 < nt;
-        if (more) load(t + 1);
-#pragma unroll
-        for (int sub = 0; sub < QS / 32; ++sub) {
-            const char* Qt = smem + buf * (2 * QS * 128) + sub * 32 * 128;
-            const char* Gt = Qt + QS * 128;
-            const float* Ls = stat + buf * 2 * QS + sub * 32;
-            const float* Ds = Ls + QS;
-            const int q0 = t * QS + sub * 32;
-            // S[q][key], dP[q][key]  (query rows in registers, key on the lane)
-            frag qa[4], ga[4];
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                qa[s] = row_frag<T>(Qt, l32, 2 * s + h);
-                ga[s] = row_frag<T>(Gt, l32, 2 * s + h);
-            }
-            f32x16 sacc, pacc;  // start from -L[q] / -delta[q] per row
-#pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {
-                const f32x4 Lv = *(const f32x4*)(Ls + 8 * g4 + 4 * h);
-                const f32x4 Dv = *(const f32x4*)(Ds + 8 * g4 + 4 * h);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    sacc[4 * g4 + e] = Lv[e];
-                    pacc[4 * g4 + e] = Dv[e];
-                }
-            }
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                sacc = Mfma<T>::mma(qa[s], kf[s], sacc);
-                pacc = Mfma<T>::mma(ga[s], vf[s], pacc);
-            }
-            // dO^T / Q^T fragments for the dV / dK products, in flight during the VALU part
-            frag gt[2][2], qt[2][2];
-#pragma unroll
-            for (int s = 0; s < 2; ++s)
-#pragma unroll
-                for (int db = 0; db < 2; ++db) {
-                    gt[s][db] = tr_frag<T>(Gt, 0, s, db, lane);
-                    qt[s][db] = tr_frag<T>(Qt, 0, s, db, lane);
-                }
-            const bool ragged = q0 + 32 > N;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                float p = __builtin_amdgcn_exp2f(sacc[r]);
-                if (ragged && q0 + acc_row(r, h) >= N) p = 0.f;
-                sacc[r] = p;                                   // P
-                pacc[r] = p * pacc[r] * DsScale<T>::v;         // dS (scaled)
-            }
-            // dV^T[d][key] += dO^T[d][q] P[q][key] ;  dK^T[d][key] += Q^T[d][q] dS[q][key]
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const frag pf = pack_frag<T>(sacc, s);
-                const frag sf = pack_frag<T>(pacc, s);
-#pragma unroll
-                for (int db = 0; db < 2; ++db) {
-                    dv[db] = Mfma<T>::mma(gt[s][db], pf, dv[db]);
-                    dk[db] = Mfma<T>::mma(qt[s][db], sf, dk[db]);
-                }
-            }
-        }
-        if (more) store(buf ^ 1);
-        __syncthreads();
+    for (int t = 0; t < c.nt; t += 2) {
+        dkv_step<T, NT, 0>(c, t);
+        if (t + 1 < c.nt) dkv_step<T, NT, 1>(c, t + 1);
     }
     const float scale = dk_scale / DsScale<T>::v;
     if (key < N) {
-        T* rk = dqkv + ((int64_t)b * N + key) * ld + C + hd * HD;
-        T* rvp = rk + C;
+        T* rk = dqkv + ((int64_t)b * N + key) * c.ld + c.C + hd * HD;
+        T* rvp = rk + c.C;
 #pragma unroll
         for (int db = 0; db < 2; ++db)
 #pragma unroll
             for (int g4 = 0; g4 < 4; ++g4) {
-                const int d = db * 32 + 8 * g4 + 4 * h;
+                const int d = db * 32 + 8 * g4 + 4 * c.h;
                 typedef T t4 __attribute__((ext_vector_type(4)));
-                t4 a = {(T)(dk[db][4 * g4] * scale), (T)(dk[db][4 * g4 + 1] * scale),
-                        (T)(dk[db][4 * g4 + 2] * scale), (T)(dk[db][4 * g4 + 3] * scale)};
-                t4 v = {(T)dv[db][4 * g4], (T)dv[db][4 * g4 + 1], (T)dv[db][4 * g4 + 2], (T)dv[db][4 * g4 + 3]};
+                t4 a = {(T)(c.dk[db][4 * g4] * scale), (T)(c.dk[db][4 * g4 + 1] * scale),
+                        (T)(c.dk[db][4 * g4 + 2] * scale), (T)(c.dk[db][4 * g4 + 3] * scale)};
+                t4 v = {(T)c.dv[db][4 * g4], (T)c.dv[db][4 * g4 + 1], (T)c.dv[db][4 * g4 + 2],
+                        (T)c.dv[db][4 * g4 + 3]};
                 *(t4*)(rk + d) = a;
                 *(t4*)(rvp + d) = v;
             }
     }
 }
 
+// ---------------------------------------------------------------------------- launch
+template <typename T, int NW>
+void fwd_launch_nw(const void* qkv, void* o, float* lse, int B, int N, int H, hipStream_t st) {
+    dim3 grid(((N + 32 * NW - 1) / (32 * NW)) * B * H);
+    attn_fwd_kernel<T, NW><<<grid, 64 * NW, 0, st>>>((const T*)qkv, (T*)o, lse, N, H);
+}
+
 template <typename T>
-void fwd_launch(const void* qkv, void* o, float* lse, int B, int N, int H, float scale, hipStream_t st) {
-    dim3 grid(((N + 127) / 128) * B * H);
-    attn_fwd_kernel<T><<<grid, 256, 0, st>>>((const T*)qkv, (T*)o, lse, N, H);
+void fwd_launch(const void* qkv, void* o, float* lse, int B, int N, int H, hipStream_t st) {
+    if (dclip_option(DCLIP_OPT_ATTN_FWD_WAVES) == 4) fwd_launch_nw<T, 4>(qkv, o, lse, B, N, H, st);
+    else fwd_launch_nw<T, 8>(qkv, o, lse, B, N, H, st);
 }
 
 template <typename T>
@@ -593,11 +706,25 @@ void bwd_launch(const void* qkv, const void* o, const void* dout, const float* l
     const int64_t total = (int64_t)B * N * H;
     attn_delta_kernel<T><<<(unsigned)((total + 255) / 256), 256, 0, st>>>((const T*)o, (const T*)dout, delta, N, H,
                                                                           total);
-    dim3 grid(((N + 127) / 128) * B * H);
     // dQ (w.r.t. the unscaled q) = dZ K scale;  dK = dZ^T q scale = dZ^T q' / log2(e)
-    attn_bwd_dq_kernel<T><<<grid, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, (T*)dqkv, N, H, scale);
-    attn_bwd_dkdv_kernel<T><<<grid, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, (T*)dqkv, N, H,
-                                                  1.0f / LOG2E);
+    if (dclip_option(DCLIP_OPT_ATTN_DQ_WAVES) != 8) {
+        dim3 grid(((N + 127) / 128) * B * H);
+        attn_bwd_dq_kernel<T, 4><<<grid, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, (T*)dqkv, N, H,
+                                                       scale);
+    } else {
+        dim3 grid(((N + 255) / 256) * B * H);
+        attn_bwd_dq_kernel<T, 8><<<grid, 512, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, (T*)dqkv, N, H,
+                                                       scale);
+    }
+    if (dclip_option(DCLIP_OPT_ATTN_DKDV_WAVES) != 8) {
+        dim3 grid(((N + 127) / 128) * B * H);
+        attn_bwd_dkdv_kernel<T, 4><<<grid, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, (T*)dqkv, N, H,
+                                                         1.0f / LOG2E);
+    } else {
+        dim3 grid(((N + 255) / 256) * B * H);
+        attn_bwd_dkdv_kernel<T, 8><<<grid, 512, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, (T*)dqkv, N, H,
+                                                         1.0f / LOG2E);
+    }
 }
 
 }  // namespace
@@ -609,8 +736,8 @@ extern "C" int dclip_attn_fwd(int dt, const void* qkv, void* o, float* lse, int 
     DCLIP_HOST_CHECK(B > 0 && N > 0 && H > 0, "dclip_attn_fwd: empty problem");
     DCLIP_HOST_CHECK(((uintptr_t)qkv % 16) == 0 && ((uintptr_t)o % 16) == 0, "dclip_attn_fwd: unaligned buffers");
     hipStream_t st = (hipStream_t)stream;
-    if (dt == DCLIP_BF16) fwd_launch<bf16>(qkv, o, lse, B, N, H, scale, st);
-    else fwd_launch<f16>(qkv, o, lse, B, N, H, scale, st);
+    if (dt == DCLIP_BF16) fwd_launch<bf16>(qkv, o, lse, B, N, H, st);
+    else fwd_launch<f16>(qkv, o, lse, B, N, H, st);
     DCLIP_LAUNCH_CHECK();
     return 0;
 }

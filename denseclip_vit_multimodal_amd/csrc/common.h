@@ -39,6 +39,7 @@ typedef short i16x4 __attribute__((ext_vector_type(4)));
     } while (0)
 
 void dclip_set_error(const char* fmt, ...);
+int dclip_option(int id);  // current value of a dclip_set_option knob (0 = default)
 
 // ----------------------------------------------------------------------------- scalar io
 template <typename T> __device__ __forceinline__ float to_f32(T v) { return (float)v; }

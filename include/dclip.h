@@ -63,6 +63,14 @@ extern "C" {
 const char* dclip_last_error(void);
 int dclip_abi_version(void);
 
+/* Kernel-variant knobs for A/B tuning in one process (process-global, not thread-safe;
+ * 0 restores the default).  Results do not depend on them beyond fp32 summation order.  */
+#define DCLIP_OPT_ATTN_FWD_WAVES 0   /* 4 or 8 (default) waves = 128 / 256 queries per workgroup */
+#define DCLIP_OPT_ATTN_DQ_WAVES 1    /* 4 (default) or 8: dQ pass queries per workgroup / 32      */
+#define DCLIP_OPT_ATTN_DKDV_WAVES 2  /* 4 (default) or 8: dK/dV pass keys per workgroup / 32      */
+#define DCLIP_OPT_COUNT 8
+int dclip_set_option(int id, int value);
+
 /* LayerNorm over the last dim (cols), eps, affine w/b (fp32).  y = (x-mu)*rstd*w+b.
  * mean/rstd (rows) are written when non-null.                                        */
 int dclip_layernorm_fwd(const void* x, int x_dt, const float* w, const float* b,

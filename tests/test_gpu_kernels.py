@@ -179,10 +179,37 @@ def test_attention_fwd(N, dt):
     assert (lse.view(B, H, N) - lref).abs().max() < 1e-2
 
 
-@pytest.mark.parametrize("spike", [4.0, 40.0, -40.0])
-def test_attention_spiky_rescale(spike):
-    """Force the softmax reference to jump late, by more and less than the deferred
-    re-referencing threshold, and all-negative logits (guide rule 26)."""
+@pytest.fixture
+def attn_variant(request):
+    """Select attention kernel variants (waves per workgroup of the forward, dQ and dK/dV
+    passes) through dclip_set_option; restore the defaults."""
+    from denseclip_vit_multimodal_amd import _native as N
+    fwd, dq, dkdv = request.param
+    N.call("dclip_set_option", N.OPT_ATTN_FWD_WAVES, fwd)
+    N.call("dclip_set_option", N.OPT_ATTN_DQ_WAVES, dq)
+    N.call("dclip_set_option", N.OPT_ATTN_DKDV_WAVES, dkdv)
+    yield request.param
+    for o in (N.OPT_ATTN_FWD_WAVES, N.OPT_ATTN_DQ_WAVES, N.OPT_ATTN_DKDV_WAVES):
+        N.call("dclip_set_option", o, 0)
+
+
+@pytest.mark.parametrize("attn_variant", [(4, 4, 4), (8, 8, 8)], indirect=True)
+@pytest.mark.parametrize("N", [1, 63, 64, 65, 129, 300, 1000])
+def test_attention_fwd_variants(attn_variant, N):
+    O = ops()
+    B, H = 2, 2
+    C = 64 * H
+    qkv, qref = prescale((torch.randn(B * N, 3 * C, device=DEV) * 1.5).to(torch.bfloat16), H)
+    o, _ = O.attn_fwd(qkv, B, N, H, 64 ** -0.5)
+    assert rel_err(o.float(), attn_ref(qref, B, N, H)) < TOL[torch.bfloat16]
+
+
+@pytest.mark.parametrize("attn_variant", [(8, 4, 4), (4, 4, 4)], indirect=True)
+@pytest.mark.parametrize("spike", [0.5, 0.8, 4.0, 40.0, -40.0])
+def test_attention_spiky_rescale(spike, attn_variant):
+    """Force the softmax reference to jump late, by less (0.5: +5.8 in log2 units) and more
+    (0.8: +9.2; 4, 40) than the deferred re-referencing threshold (8), and all-negative
+    logits (guide rule 26)."""
     O = ops()
     B, H, N = 1, 1, 300
     C = 64
@@ -196,9 +223,10 @@ def test_attention_spiky_rescale(spike):
     assert rel_err(o.float(), attn_ref(qref, B, N, H)) < TOL[torch.float16]
 
 
-@pytest.mark.parametrize("N", [1, 33, 130, 257, 700])
+@pytest.mark.parametrize("attn_variant", [(8, 4, 4), (8, 8, 8)], indirect=True)
+@pytest.mark.parametrize("N", [1, 33, 63, 64, 65, 130, 257, 700])
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
-def test_attention_bwd(N, dt):
+def test_attention_bwd(N, dt, attn_variant):
     O = ops()
     B, H = 2, 2
     C = 64 * H
