@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("DCLIP_LIB", os.path.join(_HERE, "libdclip.so"))
 
 F32, F16, BF16 = 0, 1, 2
 EPI_STORE, EPI_GELU, EPI_RESIDUAL, EPI_GELU_BWD, EPI_SPLITK, EPI_STORE_SCALED = 0, 1, 2, 3, 4, 5
-OPT_ATTN_FWD_WAVES, OPT_ATTN_DQ_WAVES, OPT_ATTN_DKDV_WAVES = 0, 1, 2
+OPT_ATTN_FWD_WAVES, OPT_ATTN_DQ_WAVES, OPT_ATTN_DKDV_WAVES, OPT_GEMM_TILE, OPT_GEMM_TN_TILE = 0, 1, 2, 3, 4
 
 _c_void_p = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -46,6 +46,7 @@ _SIGS = {
     "dclip_bilinear_bwd": [_c_void_p, _i32, _c_void_p, _c_void_p, _i64, _i32, _i32, _i32, _i32, _c_void_p],
     "dclip_cast": [_c_void_p, _i32, _c_void_p, _i32, _i64, _f32, _c_void_p],
     "dclip_set_option": [_i32, _i32],
+    "dclip_gemm_tn_plan": [_i64, _i64, _i64, _c_void_p, _c_void_p],
 }
 EXPORTED = sorted(list(_SIGS) + ["dclip_last_error", "dclip_abi_version"])
 

@@ -27,9 +27,9 @@
 // via ds_read_b64_tr_b16.  Software-pipelined: iteration t issues S(t+1) beside the
 // softmax of tile t and O += V(t)^T P(t)^T (K runs one tile ahead of V in separate rings).
 // Backward (FlashAttention-2 style recompute from the log2-domain lse, no atomics):
-//   delta = rowsum(dO * O);  a query-major pass for dQ (S^T, dP^T = V dO^T, dQ^T += K^T dS^T)
-//   and a key-major pass for dK, dV in which the S / dP accumulators (key on the lane)
-//   feed dV^T += dO^T P and dK^T += Q^T dS directly.
+//   a query-major pass for dQ (S^T, dP^T = V dO^T, dQ^T += K^T dS^T; it also writes
+//   delta = rowsum(dO * O)) and a key-major pass for dK, dV in which the S / dP
+//   accumulators (key on the lane) feed dV^T += dO^T P and dK^T += Q^T dS directly.
 #include "common.h"
 
 namespace {
@@ -333,28 +333,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_kernel(const T* __re
 }
 
 // ============================================================================ backward
-// delta[b][h][q] = sum_d dO[q][h*64+d] * O[q][h*64+d]
-template <typename T>
-__global__ __launch_bounds__(256) void attn_delta_kernel(const T* __restrict__ o, const T* __restrict__ dout,
-                                                         float* __restrict__ delta, int N, int H, int64_t total) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (b*N + q)*H + hd
-    if (i >= total) return;
-    const int hd = (int)(i % H);
-    const int64_t row = i / H;
-    const int64_t b = row / N, q = row % N;
-    const T* a = o + row * (H * HD) + hd * HD;
-    const T* g = dout + row * (H * HD) + hd * HD;
-    float s = 0.f;
-#pragma unroll
-    for (int k = 0; k < HD; k += 8) {
-        typename Mfma<T>::frag va = *(const typename Mfma<T>::frag*)(a + k);
-        typename Mfma<T>::frag vg = *(const typename Mfma<T>::frag*)(g + k);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) s += (float)va[j] * (float)vg[j];
-    }
-    delta[(b * H + hd) * N + q] = s;
-}
-
 // ---------------------------------------------------------------------------- dQ pass
 template <typename T, int NT>
 struct DqCtx {
@@ -443,11 +421,14 @@ __device__ __forceinline__ void dq_step(DqCtx<T, NT>& c, int t) {
 }
 
 // Query-major dQ pass: 32*NW queries per workgroup (32 per wave), all key tiles.
+// Also computes delta = rowsum(dO * O) for its queries (the dK/dV pass, launched next on
+// the same stream, reads it) — no separate delta launch.
 template <typename T, int NW>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const T* __restrict__ qkv,
+                                                                      const T* __restrict__ o,
                                                                       const T* __restrict__ dout,
                                                                       const float* __restrict__ lse,
-                                                                      const float* __restrict__ delta,
+                                                                      float* __restrict__ delta,
                                                                       T* __restrict__ dqkv, int N, int H,
                                                                       float scale) {
     constexpr int NT = 64 * NW, QB = 32 * NW;
@@ -479,7 +460,19 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const T* _
         c.gf[s] = *(const frag*)(dOb + (int64_t)qc * C + (2 * s + c.h) * 8);
     }
     c.negL = splat16(-lse[(int64_t)bh * N + qc]);
-    c.negD = splat16(-delta[(int64_t)bh * N + qc]);
+    {
+        const T* Orow = o + ((int64_t)b * N + qc) * C + hd * HD;
+        float dpart = 0.f;  // this lane's half of the 64 dims (chunks h, 2+h, 4+h, 6+h)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const frag of = *(const frag*)(Orow + (2 * s + c.h) * 8);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) dpart += (float)of[j] * (float)c.gf[s][j];
+        }
+        const float dl = xhalf_sum(dpart);
+        if (q < N && c.h == 0) delta[(int64_t)bh * N + q] = dl;
+        c.negD = splat16(-dl);
+    }
     c.dq[0] = zero16();
     c.dq[1] = zero16();
 
@@ -533,21 +526,23 @@ template <typename T, int NT>
 __device__ __forceinline__ void dkv_load(DkvCtx<T, NT>& c, int t) {
     tile_load<T, 64, NT>(c.rq, c.Qb, c.ld, t * 64, c.N);
     tile_load<T, 64, NT>(c.rg, c.dOb, c.C, t * 64, c.N);
-    if (threadIdx.x < 128) {
+    if (threadIdx.x < 128) {  // the raw value: it is used only at store time (no early vmcnt wait)
         const int r = t * 64 + (threadIdx.x & 63);
         const int rc = r < c.N ? r : c.N - 1;
-        const float v = threadIdx.x < 64 ? c.Lb[rc] : c.Db[rc];
-        c.rstat = r < c.N ? -v : (threadIdx.x < 64 ? -INFINITY : 0.f);
+        c.rstat = threadIdx.x < 64 ? c.Lb[rc] : c.Db[rc];
     }
 }
 
 template <typename T, int NT>
-__device__ __forceinline__ void dkv_store(DkvCtx<T, NT>& c, int slot) {
+__device__ __forceinline__ void dkv_store(DkvCtx<T, NT>& c, int slot, int t) {
     char* base = c.smem + slot * 16384;
     tile_store<64, NT>(c.rq, base);
     tile_store<64, NT>(c.rg, base + 8192);
     float* stat = (float*)(c.smem + 2 * 16384);
-    if (threadIdx.x < 128) stat[slot * 128 + threadIdx.x] = c.rstat;
+    if (threadIdx.x < 128) {
+        const bool valid = t * 64 + (int)(threadIdx.x & 63) < c.N;
+        stat[slot * 128 + threadIdx.x] = valid ? -c.rstat : (threadIdx.x < 64 ? -INFINITY : 0.f);
+    }
 }
 
 template <typename T, int NT, int P>
@@ -612,7 +607,7 @@ __device__ __forceinline__ void dkv_step(DkvCtx<T, NT>& c, int t) {
             }
         }
     }
-    dkv_store<T, NT>(c, P ^ 1);
+    dkv_store<T, NT>(c, P ^ 1, t + 1);
     __syncthreads();
 }
 
@@ -661,7 +656,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const T*
     c.rstat = 0.f;
 
     dkv_load<T, NT>(c, 0);
-    dkv_store<T, NT>(c, 0);
+    dkv_store<T, NT>(c, 0, 0);
     __syncthreads();
     for (int t = 0; t < c.nt; t += 2) {
         dkv_step<T, NT, 0>(c, t);
@@ -703,18 +698,15 @@ void fwd_launch(const void* qkv, void* o, float* lse, int B, int N, int H, hipSt
 template <typename T>
 void bwd_launch(const void* qkv, const void* o, const void* dout, const float* lse, float* delta, void* dqkv,
                 int B, int N, int H, float scale, hipStream_t st) {
-    const int64_t total = (int64_t)B * N * H;
-    attn_delta_kernel<T><<<(unsigned)((total + 255) / 256), 256, 0, st>>>((const T*)o, (const T*)dout, delta, N, H,
-                                                                          total);
     // dQ (w.r.t. the unscaled q) = dZ K scale;  dK = dZ^T q scale = dZ^T q' / log2(e)
-    if (dclip_option(DCLIP_OPT_ATTN_DQ_WAVES) != 8) {
+    if (dclip_option(DCLIP_OPT_ATTN_DQ_WAVES) == 4) {
         dim3 grid(((N + 127) / 128) * B * H);
-        attn_bwd_dq_kernel<T, 4><<<grid, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, (T*)dqkv, N, H,
-                                                       scale);
+        attn_bwd_dq_kernel<T, 4><<<grid, 256, 0, st>>>((const T*)qkv, (const T*)o, (const T*)dout, lse, delta,
+                                                       (T*)dqkv, N, H, scale);
     } else {
         dim3 grid(((N + 255) / 256) * B * H);
-        attn_bwd_dq_kernel<T, 8><<<grid, 512, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, (T*)dqkv, N, H,
-                                                       scale);
+        attn_bwd_dq_kernel<T, 8><<<grid, 512, 0, st>>>((const T*)qkv, (const T*)o, (const T*)dout, lse, delta,
+                                                       (T*)dqkv, N, H, scale);
     }
     if (dclip_option(DCLIP_OPT_ATTN_DKDV_WAVES) != 8) {
         dim3 grid(((N + 127) / 128) * B * H);

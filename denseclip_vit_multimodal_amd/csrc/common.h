@@ -85,6 +85,27 @@ template <> struct Mfma<f16> {
     }
 };
 
+// v_mfma_f32_16x16x32_{bf16,f16}: lane l holds A[l & 15][8(l >> 4) + j], B[8(l >> 4) + j][l & 15]
+// and D[4(l >> 4) + e][l & 15]
+template <typename T> struct Mfma16;
+template <> struct Mfma16<bf16> {
+    static __device__ __forceinline__ f32x4 mma(bf16x8 a, bf16x8 b, f32x4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+    }
+};
+template <> struct Mfma16<f16> {
+    static __device__ __forceinline__ f32x4 mma(f16x8 a, f16x8 b, f32x4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+    }
+};
+
+// s_waitcnt vmcnt(N) only (expcnt / lgkmcnt left at their maxima), N a compile-time constant
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt(0x0F70 | (N & 15) | ((N >> 4) << 14));
+}
+
 __device__ __forceinline__ float quick_gelu(float z) {
     return z / (1.0f + __expf(-1.702f * z));
 }

@@ -236,6 +236,205 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(
     gemm_epilogue<T, EPI, OutT>(acc, smem, M, N, m0, n0, bias, aux, ld_aux, C, ldc, C2, ldc2, slab, alpha);
 }
 
+// ---------------------------------------------------------------------------- large tiles
+// The production NT kernel for the token GEMMs (M = B*N ~ 65k rows): BM x BN x 64 tiles,
+// 8 waves (WM x WN), MFMA v_mfma_f32_16x16x32 issued swapped (A-operand = B rows) so the
+// accumulator holds C^T.  Operands move global -> LDS by 16-byte global_load_lds into a
+// STAGES-deep ring (XOR swizzle applied to the per-lane SOURCE address, conflict-free
+// ds_read_b128 fragment reads); one raw s_barrier per K-step with a COUNTED vmcnt, so up
+// to STAGES-2 future tiles stay in flight across the barrier (a __syncthreads() would
+// drain them: it waits vmcnt(0)).  Epilogue: each wave stages 32-row slices of its fp32
+// sub-tile in LDS and re-reads them row-contiguous (8 columns per lane) for the fused
+// bias / scale / QuickGELU / residual / QuickGELU' / split-K stores.
+
+// one row segment of 8 columns [nb, nb + 8) of output row m: v = alpha * acc
+template <typename T, int EPI, typename OutT>
+__device__ __forceinline__ void epi_row8(float (&v)[8], int m, int nb, int N, const float* __restrict__ bias,
+                                         const void* __restrict__ aux, int64_t ld_aux, void* __restrict__ C,
+                                         int64_t ldc, void* __restrict__ C2, int64_t ldc2, int64_t slab) {
+    const bool full = nb + 8 <= N;
+    const int rem = N - nb;
+    if (bias != nullptr && EPI != DCLIP_EPI_SPLITK && EPI != DCLIP_EPI_GELU_BWD) {
+        float bv[8];
+        load8<float>(bias + nb, bv, full, rem);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += bv[e];
+    }
+    if constexpr (EPI == DCLIP_EPI_STORE_SCALED) {
+        float sv[8];
+        load8<float>((const float*)aux + nb, sv, full, rem);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] *= sv[e];
+    }
+    if constexpr (EPI == DCLIP_EPI_STORE || EPI == DCLIP_EPI_STORE_SCALED) {
+        store8<OutT>((OutT*)C + (int64_t)m * ldc + nb, v, full, rem);
+    } else if constexpr (EPI == DCLIP_EPI_GELU) {
+        float g[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            v[e] = (float)(OutT)v[e];  // the activation sees the rounded pre-activation
+            g[e] = quick_gelu(v[e]);
+        }
+        store8<OutT>((OutT*)C + (int64_t)m * ldc + nb, v, full, rem);
+        store8<OutT>((OutT*)C2 + (int64_t)m * ldc2 + nb, g, full, rem);
+    } else if constexpr (EPI == DCLIP_EPI_RESIDUAL) {
+        float rsd[8];
+        load8<float>((const float*)aux + (int64_t)m * ld_aux + nb, rsd, full, rem);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += rsd[e];
+        store8<float>((float*)C + (int64_t)m * ldc + nb, v, full, rem);
+    } else if constexpr (EPI == DCLIP_EPI_GELU_BWD) {
+        float z[8];
+        load8<T>((const T*)aux + (int64_t)m * ld_aux + nb, z, full, rem);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] *= quick_gelu_grad(z[e]);
+        store8<OutT>((OutT*)C + (int64_t)m * ldc + nb, v, full, rem);
+    } else {  // SPLITK: plain f32 partial slab per K split
+        store8<float>((float*)C + blockIdx.y * slab + (int64_t)m * ldc + nb, v, full, rem);
+    }
+}
+
+template <int BM, int BN, int WM, int WN, int STAGES>
+struct BigCfg {
+    static constexpr int NW = WM * WN, NT = 64 * NW;
+    static constexpr int WTM = BM / WM, WTN = BN / WN;  // per-wave output tile
+    static constexpr int MB = WTM / 16, NB = WTN / 16;   // 16x16 blocks per wave
+    static constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE_BYTES = A_BYTES + B_BYTES;
+    static constexpr int A_INST = BM / 8 / NW, B_INST = BN / 8 / NW;  // 1-KiB glds per wave per stage
+    static constexpr int G = A_INST + B_INST;                          // glds per thread per stage
+    static constexpr int EP_LD = WTN + 4;                              // epilogue row stride (floats)
+    static constexpr int EP_BYTES = NW * 32 * EP_LD * 4;
+    static constexpr int SMEM = STAGES * STAGE_BYTES > EP_BYTES ? STAGES * STAGE_BYTES : EP_BYTES;
+    static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "staging split");
+    static_assert(WTM % 32 == 0 && WTN % 16 == 0 && WTN <= 64, "wave tile");
+};
+
+// Epilogue of the large-tile kernels: 32-row slices of the wave's WTM x WTN tile go through
+// LDS (f32, padded rows) and are re-read row-contiguous, 8 columns per lane.
+// acc[i][j] holds C[mw + 16 j + (lane & 15)][nw + 16 i + 4 (lane >> 4) + e].
+template <typename T, int EPI, typename OutT, typename Cfg>
+__device__ __forceinline__ void big_epilogue(f32x4 (&acc)[Cfg::NB][Cfg::MB], char* smem, int M, int N, int mw, int nw,
+                                             const float* __restrict__ bias, const void* __restrict__ aux,
+                                             int64_t ld_aux, void* __restrict__ C, int64_t ldc, void* __restrict__ C2,
+                                             int64_t ldc2, int64_t slab, float alpha) {
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int l16 = lane & 15, lq = lane >> 4;
+    __syncthreads();  // every wave is done with the operand ring
+    float* ep = (float*)smem + wave * (32 * Cfg::EP_LD);
+    constexpr int LPR = Cfg::WTN / 8;  // lanes per output row
+    constexpr int RPP = 64 / LPR;      // rows per pass
+    const int c8 = (lane % LPR) * 8;
+    const int nb = nw + c8;
+#pragma unroll
+    for (int sl = 0; sl < Cfg::MB / 2; ++sl) {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+            for (int i = 0; i < Cfg::NB; ++i) {
+                f32x4 v = acc[i][2 * sl + jj];
+                v *= alpha;
+                *(f32x4*)(ep + (jj * 16 + l16) * Cfg::EP_LD + i * 16 + 4 * lq) = v;
+            }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int it = 0; it < 32 / RPP; ++it) {
+            const int r = it * RPP + lane / LPR;
+            const int m = mw + sl * 32 + r;
+            if (m < M && nb < N) {
+                float v[8];
+                const f32x4 a = *(const f32x4*)(ep + r * Cfg::EP_LD + c8);
+                const f32x4 b = *(const f32x4*)(ep + r * Cfg::EP_LD + c8 + 4);
+                v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+                v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+                epi_row8<T, EPI, OutT>(v, m, nb, N, bias, aux, ld_aux, C, ldc, C2, ldc2, slab);
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();  // reads of this slice done before the next slice's writes
+    }
+}
+
+template <typename T, int ROWS_INST>
+__device__ __forceinline__ void stage_rows(const T* __restrict__ X, int64_t ldx, int row0, int rows, int k0,
+                                           char* lds, int wave, int lane) {
+#pragma unroll
+    for (int i = 0; i < ROWS_INST; ++i) {
+        const int inst = wave * ROWS_INST + i;
+        const int r = inst * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ ((r >> 1) & 7);
+        int gr = row0 + r;
+        gr = gr < rows ? gr : rows - 1;
+        __builtin_amdgcn_global_load_lds((const void*)(X + (int64_t)gr * ldx + k0 + c * 8), LDS_PTR(lds + inst * 1024),
+                                         16, 0, 0);
+    }
+}
+
+template <typename T, int EPI, typename OutT, int BM, int BN, int WM, int WN, int STAGES>
+__global__ __launch_bounds__(64 * WM * WN, 1) void gemm_nt_big_kernel(
+    const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
+    int M, int N, int k_chunk, int tiles_m, int tiles_n,
+    const float* __restrict__ bias, const void* __restrict__ aux, int64_t ld_aux,
+    void* __restrict__ C, int64_t ldc, void* __restrict__ C2, int64_t ldc2, int64_t slab, float alpha) {
+    typedef BigCfg<BM, BN, WM, WN, STAGES> Cfg;
+    typedef typename Mfma<T>::frag frag;
+    __shared__ __attribute__((aligned(16))) char smem[Cfg::SMEM];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int l16 = lane & 15, lq = lane >> 4;
+
+    const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+    const int m0 = (t / tiles_n) * BM;
+    const int n0 = (t % tiles_n) * BN;
+    const int kbeg = blockIdx.y * k_chunk;
+    const int nk = k_chunk / BK;
+
+    f32x4 acc[Cfg::NB][Cfg::MB];
+#pragma unroll
+    for (int i = 0; i < Cfg::NB; ++i)
+#pragma unroll
+        for (int j = 0; j < Cfg::MB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto stage = [&](int kt, int slot) {
+        char* base = smem + slot * Cfg::STAGE_BYTES;
+        stage_rows<T, Cfg::A_INST>(A, lda, m0, M, kbeg + kt * BK, base, wave, lane);
+        stage_rows<T, Cfg::B_INST>(B, ldb, n0, N, kbeg + kt * BK, base + Cfg::A_BYTES, wave, lane);
+    };
+#pragma unroll
+    for (int s = 0; s < STAGES - 1; ++s)
+        if (s < nk) stage(s, s);
+
+    for (int kt = 0; kt < nk; ++kt) {
+        // tile kt has landed when at most min(STAGES-2, nk-1-kt) younger tiles are in flight
+        if (kt + STAGES - 2 <= nk - 1) wait_vmcnt<Cfg::G * (STAGES - 2)>();
+        else wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();  // tile kt visible to every wave; slot of tile kt-1 free
+        __builtin_amdgcn_sched_barrier(0);
+        if (kt + STAGES - 1 < nk) stage(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+        const char* At = smem + (kt % STAGES) * Cfg::STAGE_BYTES;
+        const char* Bt = At + Cfg::A_BYTES;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            frag fb[Cfg::NB], fa[Cfg::MB];
+            const int ch = ks * 4 + lq;
+#pragma unroll
+            for (int i = 0; i < Cfg::NB; ++i) fb[i] = read_frag<T>(Bt, wn * Cfg::WTN + i * 16 + l16, ch);
+#pragma unroll
+            for (int j = 0; j < Cfg::MB; ++j) fa[j] = read_frag<T>(At, wm * Cfg::WTM + j * 16 + l16, ch);
+#pragma unroll
+            for (int j = 0; j < Cfg::MB; ++j)
+#pragma unroll
+                for (int i = 0; i < Cfg::NB; ++i) acc[i][j] = Mfma16<T>::mma(fb[i], fa[j], acc[i][j]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+
+    big_epilogue<T, EPI, OutT, Cfg>(acc, smem, M, N, m0 + wm * Cfg::WTM, n0 + wn * Cfg::WTN, bias, aux, ld_aux,
+                                     C, ldc, C2, ldc2, slab, alpha);
+}
+
 // ---------------------------------------------------------------------------- "TN"
 // C[m][n] = sum_k A[k][m] * B[k][n]: both operands row-major with the reduction index on
 // the ROWS — the weight-gradient shape dW = dY^T X (k = token, m/n = features).  Tiles of
@@ -344,6 +543,120 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(
     gemm_epilogue<T, EPI, OutT>(acc, smem, M, N, m0, n0, bias, nullptr, 0, C, ldc, nullptr, 0, slab, alpha);
 }
 
+// ---------------------------------------------------------------------------- "TN", large tiles
+// Weight-gradient GEMM on 256 x 256 output tiles, 8 waves (2 x 4), 16x16x32 MFMA.  A K-tile is
+// 64 token rows x 256 feature columns of each operand (512-B rows in LDS), staged by
+// global_load_lds in 1-KiB pieces (2 rows); fragments of 8 consecutive tokens for one column
+// come from two ds_read_b64_tr_b16.  The 16-byte chunks of an LDS row are XOR-swizzled by
+// 2 * tn_sw(row) so each half-wave's transposed reads (rows {0-3, 8-11} or {4-7, 12-15} of a
+// 16-row group, 32 bytes each) hit 64 distinct banks; the swizzle is applied to the per-lane
+// source address (LDS-DMA writes lane-linearly).
+__device__ __forceinline__ int tn_sw(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
+__device__ __forceinline__ int tn_off(int r, int col) {
+    return r * 512 + ((((col >> 3) ^ (2 * tn_sw(r)))) << 4) + ((col & 7) << 1);
+}
+
+// fragment: element j = row (ks*32 + 8 (lane >> 4) + j), column col0 + (lane & 15)
+template <typename T>
+__device__ __forceinline__ typename Mfma<T>::frag tn_frag(const char* img, int ks, int col0, int lane) {
+    const int i = lane & 15, q = i >> 2, p = i & 3, g = lane >> 4;
+    const int row = ks * 32 + 8 * g + q;
+    const int col = col0 + 4 * p;
+    typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+    i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(img + tn_off(row, col)));
+    i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(img + tn_off(row + 4, col)));
+    typedef short s8 __attribute__((ext_vector_type(8)));
+    s8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(typename Mfma<T>::frag, v);
+}
+
+// 64 rows x 256 columns (clamped: rows to krows - 1, columns to cols - 8) -> [64][512 B] image
+template <typename T>
+__device__ __forceinline__ void stage_tn_big(const T* __restrict__ X, int64_t ldx, int k0, int krows, int col0,
+                                             int cols, char* lds, int wave, int lane) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int piece = wave * 4 + i;  // 32 pieces of 2 rows
+        const int r = piece * 2 + (lane >> 5);
+        const int c = (lane & 31) ^ (2 * tn_sw(r));
+        int gr = k0 + r;
+        gr = gr < krows ? gr : krows - 1;
+        int gc = col0 + c * 8;
+        gc = gc + 8 <= cols ? gc : cols - 8;
+        __builtin_amdgcn_global_load_lds((const void*)(X + (int64_t)gr * ldx + gc), LDS_PTR(lds + piece * 1024), 16,
+                                         0, 0);
+    }
+}
+
+template <typename T, int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(const T* __restrict__ A, int64_t lda,
+                                                             const T* __restrict__ B, int64_t ldb, int M, int N,
+                                                             int Kreal, int k_chunk, int tiles_m, int tiles_n,
+                                                             void* __restrict__ C, int64_t ldc, int64_t slab,
+                                                             float alpha) {
+    typedef BigCfg<256, 256, 2, 4, 2> Cfg;
+    typedef typename Mfma<T>::frag frag;
+    constexpr int STAGE = 2 * 64 * 512;  // A | B
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE > Cfg::EP_BYTES ? 2 * STAGE : Cfg::EP_BYTES];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int wm = wave / 4, wn = wave % 4;
+    const int lq = lane >> 4;
+
+    const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+    const int m0 = (t / tiles_n) * 256;
+    const int n0 = (t % tiles_n) * 256;
+    const int kbeg = blockIdx.y * k_chunk;
+    int nk = k_chunk / BK;
+    if (kbeg + nk * BK > Kreal) nk = (Kreal - kbeg + BK - 1) / BK;  // fully padded tiles skipped
+    nk = nk < 0 ? 0 : nk;
+
+    f32x4 acc[Cfg::NB][Cfg::MB];
+#pragma unroll
+    for (int i = 0; i < Cfg::NB; ++i)
+#pragma unroll
+        for (int j = 0; j < Cfg::MB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto stage = [&](int kt, int slot) {
+        char* base = smem + slot * STAGE;
+        stage_tn_big<T>(A, lda, kbeg + kt * BK, Kreal, m0, M, base, wave, lane);
+        stage_tn_big<T>(B, ldb, kbeg + kt * BK, Kreal, n0, N, base + 64 * 512, wave, lane);
+    };
+    if (nk > 0) stage(0, 0);
+    for (int kt = 0; kt < nk; ++kt) {
+        wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();  // tile kt visible to every wave; slot of tile kt-1 free
+        __builtin_amdgcn_sched_barrier(0);
+        if (kt + 1 < nk) stage(kt + 1, (kt + 1) & 1);
+        const char* At = smem + (kt & 1) * STAGE;
+        const char* Bt = At + 64 * 512;
+        const int k0 = kbeg + kt * BK;
+        const bool ragged = k0 + BK > Kreal;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            frag fb[Cfg::NB], fa[Cfg::MB];
+#pragma unroll
+            for (int i = 0; i < Cfg::NB; ++i) fb[i] = tn_frag<T>(Bt, ks, wn * Cfg::WTN + i * 16, lane);
+#pragma unroll
+            for (int j = 0; j < Cfg::MB; ++j) fa[j] = tn_frag<T>(At, ks, wm * Cfg::WTM + j * 16, lane);
+            if (ragged) {  // token rows past Kreal were clamped duplicates: zero them (A side)
+#pragma unroll
+                for (int j = 0; j < Cfg::MB; ++j)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e)
+                        if (k0 + ks * 32 + 8 * lq + e >= Kreal) fa[j][e] = (T)0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < Cfg::MB; ++j)
+#pragma unroll
+                for (int i = 0; i < Cfg::NB; ++i) acc[i][j] = Mfma16<T>::mma(fb[i], fa[j], acc[i][j]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    big_epilogue<T, EPI, float, Cfg>(acc, smem, M, N, m0 + wm * Cfg::WTM, n0 + wn * Cfg::WTN, nullptr, nullptr, 0,
+                                     C, ldc, nullptr, 0, slab, alpha);
+}
+
 // per-column sums of a row-major (rows x cols) matrix, accumulated into out (f32):
 // a block covers 64 columns (8 lanes x 8 columns, 16-byte loads) x a chunk of rows
 // (32 row lanes), reduces its 32 partial sums per column in LDS, one atomic per column.
@@ -400,10 +713,41 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, i
     }
 }
 
+template <typename T, int EPI, typename OutT, int TBM, int TBN, int WM, int WN, int STAGES>
+void launch_big(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
+                int splits, float alpha, const float* bias, const void* aux, int64_t ld_aux, void* C, int64_t ldc,
+                void* C2, int64_t ldc2, hipStream_t st) {
+    const int tiles_m = (int)((M + TBM - 1) / TBM), tiles_n = (int)((N + TBN - 1) / TBN);
+    dim3 grid(tiles_m * tiles_n, splits);
+    gemm_nt_big_kernel<T, EPI, OutT, TBM, TBN, WM, WN, STAGES><<<grid, 64 * WM * WN, 0, st>>>(
+        (const T*)A, lda, (const T*)B, ldb, (int)M, (int)N, (int)(K / splits), tiles_m, tiles_n, bias, aux, ld_aux,
+        C, ldc, C2, ldc2, (int64_t)M * N, alpha);
+}
+
+// tile configuration: DCLIP_OPT_GEMM_TILE 1 = 128x128 (4 waves, 2 workgroups/CU), 2 = 256x256
+// (8 waves, 2-stage ring), 3 = 256x128 (8 waves, 3-stage ring), 0 = automatic
+inline int gemm_tile_choice(int64_t M, int64_t N) {
+    const int opt = dclip_option(DCLIP_OPT_GEMM_TILE);
+    if (opt != 0) return opt;
+    if (M < 4096) return 1;
+    return 2;
+}
+
 template <typename T, int EPI, typename OutT>
 int launch(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
            int splits, float alpha, const float* bias, const void* aux, int64_t ld_aux, void* C, int64_t ldc,
            void* C2, int64_t ldc2, hipStream_t st) {
+    const int choice = gemm_tile_choice(M, N);
+    if (choice == 2) {
+        launch_big<T, EPI, OutT, 256, 256, 2, 4, 2>(A, lda, B, ldb, M, N, K, splits, alpha, bias, aux, ld_aux, C,
+                                                    ldc, C2, ldc2, st);
+        return 0;
+    }
+    if (choice == 3) {
+        launch_big<T, EPI, OutT, 256, 128, 4, 2, 3>(A, lda, B, ldb, M, N, K, splits, alpha, bias, aux, ld_aux, C,
+                                                    ldc, C2, ldc2, st);
+        return 0;
+    }
     const int tiles_m = (int)((M + BM - 1) / BM), tiles_n = (int)((N + BN - 1) / BN);
     const int k_chunk = (int)(K / splits);
     dim3 grid(tiles_m * tiles_n, splits);
@@ -496,6 +840,34 @@ extern "C" int dclip_gemm(int epilogue, int ab_dt, const void* A, int64_t lda, c
     return 0;
 }
 
+// K-split plan of dclip_gemm_tn: minimise (rounds of resident workgroups x k-rows per split) x
+// tile time + the f32 partial-slab round trip through HBM (write + combine read), with at
+// least 4 64-row k-tiles per split.  Slots: 256 CUs x 1 workgroup (256x256 kernel) or x 2
+// (128x128); tile time at ~5 TFLOP/s per CU, slabs at ~5 TB/s.
+extern "C" int dclip_gemm_tn_plan(int64_t M, int64_t N, int64_t K, int* splits_out, int64_t* k_pad_out) {
+    DCLIP_HOST_CHECK(M > 0 && N > 0 && K > 0 && splits_out && k_pad_out, "dclip_gemm_tn_plan: bad arguments");
+    const bool big = dclip_option(DCLIP_OPT_GEMM_TN_TILE) != 1 && M >= 256 && N >= 256;
+    const int64_t tile = big ? 256 : 128;
+    const int64_t tiles = ((M + tile - 1) / tile) * ((N + tile - 1) / tile);
+    const int64_t slots = big ? 256 : 512;
+    int best = 1;
+    double best_t = 1e30;
+    for (int sp = 1; sp <= 32; ++sp) {
+        if (sp > 1 && K < 64 * 4 * (int64_t)sp) break;
+        const int64_t blocks = tiles * sp;
+        const double rounds = (double)((blocks + slots - 1) / slots);
+        const double krows = (double)((K + 64 * sp - 1) / (64 * sp) * 64);
+        const double t = rounds * krows * (2.0 * tile * tile / 5e12) + (sp > 1 ? sp * 8.0 * M * N / 5e12 : 0.0);
+        if (t < best_t * 0.98) {
+            best = sp;
+            best_t = t;
+        }
+    }
+    *splits_out = best;
+    *k_pad_out = ((K + 64 * best - 1) / (64 * best)) * 64 * best;
+    return 0;
+}
+
 extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda, const void* B, int64_t ldb,
                              int64_t M, int64_t N, int64_t K, int64_t K_pad, int splits, float alpha, const float* bias,
                              void* ws, void* C, int64_t ldc, float* colsum_a, void* stream) {
@@ -525,13 +897,29 @@ extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda
     gemm_tn_kernel<T, EPI, float><<<grid, 256, 0, st>>>((const T*)A, lda, (const T*)B, ldb, (int)M, (int)N,   \
                                                         (int)K, k_chunk, tiles_m, tiles_n, nullptr, OUT,        \
                                                         EPI == DCLIP_EPI_SPLITK ? N : ldc, (int64_t)M * N, alpha)
+    const bool big = dclip_option(DCLIP_OPT_GEMM_TN_TILE) != 1 && M >= 256 && N >= 256;
+#define TN_BIG(T, EPI, OUT)                                                                                    \
+    gemm_tn_big_kernel<T, EPI><<<dim3(tm2 * tn2, splits), 512, 0, st>>>(                                       \
+        (const T*)A, lda, (const T*)B, ldb, (int)M, (int)N, (int)K, k_chunk, tm2, tn2, OUT,                     \
+        EPI == DCLIP_EPI_SPLITK ? N : ldc, (int64_t)M * N, alpha)
+    const int tm2 = (int)((M + 255) / 256), tn2 = (int)((N + 255) / 256);
     if (epilogue == DCLIP_EPI_STORE) {
         DCLIP_HOST_CHECK(bias == nullptr, "dclip_gemm_tn: bias only with SPLITK");
-        if (ab_dt == DCLIP_BF16) TN_LAUNCH(bf16, DCLIP_EPI_STORE, C);
-        else TN_LAUNCH(f16, DCLIP_EPI_STORE, C);
+        if (big) {
+            if (ab_dt == DCLIP_BF16) TN_BIG(bf16, DCLIP_EPI_STORE, C);
+            else TN_BIG(f16, DCLIP_EPI_STORE, C);
+        } else {
+            if (ab_dt == DCLIP_BF16) TN_LAUNCH(bf16, DCLIP_EPI_STORE, C);
+            else TN_LAUNCH(f16, DCLIP_EPI_STORE, C);
+        }
     } else {
-        if (ab_dt == DCLIP_BF16) TN_LAUNCH(bf16, DCLIP_EPI_SPLITK, ws);
-        else TN_LAUNCH(f16, DCLIP_EPI_SPLITK, ws);
+        if (big) {
+            if (ab_dt == DCLIP_BF16) TN_BIG(bf16, DCLIP_EPI_SPLITK, ws);
+            else TN_BIG(f16, DCLIP_EPI_SPLITK, ws);
+        } else {
+            if (ab_dt == DCLIP_BF16) TN_LAUNCH(bf16, DCLIP_EPI_SPLITK, ws);
+            else TN_LAUNCH(f16, DCLIP_EPI_SPLITK, ws);
+        }
         const int64_t total4 = M * (N / 4);
         int blocks = (int)((total4 + 255) / 256);
         blocks = blocks > 4096 ? 4096 : blocks;
@@ -539,6 +927,7 @@ extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda
                                                      (float*)C, ldc);
     }
 #undef TN_LAUNCH
+#undef TN_BIG
     DCLIP_LAUNCH_CHECK();
     return 0;
 }

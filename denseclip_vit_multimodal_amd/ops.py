@@ -15,6 +15,8 @@ import torch
 
 from . import _native as N
 
+N_ = N
+
 _DT = {torch.float32: N.F32, torch.float16: N.F16, torch.bfloat16: N.BF16}
 
 
@@ -156,18 +158,13 @@ def grad_scale(g, cdt):
     return float(2.0 ** max(-60, min(60, e)))
 
 
-def _wgrad_splits(tiles, M, slots=512):
-    """K-split count for a weight-gradient GEMM: fill whole rounds of the 512 resident
-    workgroup slots (256 CUs x 2), fewest splits among the best fills, >= 4 k-tiles each."""
-    best, best_eff = 1, 0.0
-    for s in range(1, 33):
-        if s > 1 and M < 64 * 4 * s:
-            break
-        blocks = tiles * s
-        eff = blocks / (math.ceil(blocks / slots) * slots)
-        if eff > best_eff + 0.02:
-            best, best_eff = s, eff
-    return best
+def _tn_plan(M, N, K):
+    """(splits, K_pad) for a TN GEMM with an M x N output over K rows (libdclip's heuristic)."""
+    import ctypes
+    sp = ctypes.c_int(0)
+    kp = ctypes.c_int64(0)
+    N_.call("dclip_gemm_tn_plan", M, N, K, ctypes.addressof(sp), ctypes.addressof(kp))
+    return sp.value, kp.value
 
 
 def weight_grad(dy, x, want_bias=True, alpha=1.0):
@@ -180,8 +177,7 @@ def weight_grad(dy, x, want_bias=True, alpha=1.0):
     _check(dy, x)
     M, Nn = dy.shape
     K = x.shape[1]
-    splits = _wgrad_splits(math.ceil(Nn / 128) * math.ceil(K / 128), M)
-    k_pad = math.ceil(M / (64 * splits)) * 64 * splits
+    splits, k_pad = _tn_plan(Nn, K, M)
     db = torch.zeros(Nn, dtype=torch.float32, device=dy.device) if want_bias else None
     dW = torch.empty(Nn, K, dtype=torch.float32, device=dy.device)
     ws = torch.empty(splits, Nn, K, dtype=torch.float32, device=dy.device)

@@ -66,8 +66,10 @@ int dclip_abi_version(void);
 /* Kernel-variant knobs for A/B tuning in one process (process-global, not thread-safe;
  * 0 restores the default).  Results do not depend on them beyond fp32 summation order.  */
 #define DCLIP_OPT_ATTN_FWD_WAVES 0   /* 4 or 8 (default) waves = 128 / 256 queries per workgroup */
-#define DCLIP_OPT_ATTN_DQ_WAVES 1    /* 4 (default) or 8: dQ pass queries per workgroup / 32      */
+#define DCLIP_OPT_ATTN_DQ_WAVES 1    /* 4 or 8 (default): dQ pass queries per workgroup / 32      */
 #define DCLIP_OPT_ATTN_DKDV_WAVES 2  /* 4 (default) or 8: dK/dV pass keys per workgroup / 32      */
+#define DCLIP_OPT_GEMM_TILE 3        /* dclip_gemm tiles: 0 auto (default), 1 128x128, 2 256x256, 3 256x128 */
+#define DCLIP_OPT_GEMM_TN_TILE 4     /* dclip_gemm_tn tiles: 0 auto (default: 256x256 when M, N >= 256), 1 128x128 */
 #define DCLIP_OPT_COUNT 8
 int dclip_set_option(int id, int value);
 
@@ -103,6 +105,10 @@ int dclip_gemm(int epilogue, int ab_dt,
  * epilogue STORE (f32 C, splits == 1) or SPLITK (f32 slabs in ws, splits*M*N, then a
  * combine that adds bias[n] when non-null).  colsum_a (f32, M), when non-null, receives
  * += alpha * the column sums of A over the K rows (the bias gradient of dY).          */
+/* The K-split plan dclip_gemm_tn runs best with for an M x N output over K rows
+ * (splits, and K_pad = K rounded up to 64*splits); host-side only, no GPU work.      */
+int dclip_gemm_tn_plan(int64_t M, int64_t N, int64_t K, int* splits, int64_t* K_pad);
+
 int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda, const void* B, int64_t ldb,
                   int64_t M, int64_t N, int64_t K, int64_t K_pad, int splits, float alpha, const float* bias,
                   void* ws, void* C, int64_t ldc, float* colsum_a, void* stream);
@@ -119,8 +125,8 @@ int dclip_attn_fwd(int dt, const void* qkv, void* o, float* lse,
                    int B, int N, int H, int D, float scale, void* stream);
 
 /* Attention backward (flash-style recompute from lse; no N x N buffer, no atomics):
- * a delta pass (rowsum(dout*o)), a query-major dQ pass and a key-major dK/dV pass.
- * dout: (B*N, H*D) dt.  delta_ws: f32 (B*H*N) workspace.
+ * a query-major dQ pass (which also writes delta = rowsum(dout*o) to delta_ws) and a
+ * key-major dK/dV pass.  dout: (B*N, H*D) dt.  delta_ws: f32 (B*H*N) workspace.
  * qkv as for dclip_attn_fwd (q pre-multiplied by scale*log2(e)); `scale` = d^-0.5.
  * dqkv: (B*N, 3*H*D) dt output, [dq | dk | dv] in the qkv layout: gradients with
  * respect to the UNSCALED q, k, v (i.e. the in-projection output before the q scale).  */

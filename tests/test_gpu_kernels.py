@@ -66,11 +66,21 @@ def test_layernorm_bwd(cols, dydt):
 
 # ----------------------------------------------------------------------------- GEMM
 SHAPES = [(128, 128, 64), (300, 200, 192), (65, 64, 128), (1000, 2304, 768), (4097, 768, 3072), (8, 512, 768)]
+TILES = [1, 2, 3]  # dclip_set_option(DCLIP_OPT_GEMM_TILE): 128x128, 256x256, 256x128
 
 
+@pytest.fixture
+def gemm_tile(request):
+    from denseclip_vit_multimodal_amd import _native as N
+    N.call("dclip_set_option", N.OPT_GEMM_TILE, request.param)
+    yield request.param
+    N.call("dclip_set_option", N.OPT_GEMM_TILE, 0)
+
+
+@pytest.mark.parametrize("gemm_tile", TILES, indirect=True)
 @pytest.mark.parametrize("M,N,K", SHAPES)
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
-def test_gemm_store(M, N, K, dt):
+def test_gemm_store(M, N, K, dt, gemm_tile):
     O = ops()
     A = torch.randn(M, K, device=DEV).to(dt)
     B = torch.randn(N, K, device=DEV).to(dt)
@@ -83,7 +93,8 @@ def test_gemm_store(M, N, K, dt):
     assert rel_err(y.float(), ref) < TOL[dt]
 
 
-def test_gemm_asymmetric_layout():
+@pytest.mark.parametrize("gemm_tile", TILES, indirect=True)
+def test_gemm_asymmetric_layout(gemm_tile):
     """A = I with an asymmetric B catches a transposed C write (guide §3)."""
     O = ops()
     K = 128
@@ -94,8 +105,9 @@ def test_gemm_asymmetric_layout():
     assert torch.equal(y, B.float().t())
 
 
+@pytest.mark.parametrize("gemm_tile", TILES, indirect=True)
 @pytest.mark.parametrize("M,N,K", [(300, 256, 128), (2049, 3072, 768)])
-def test_gemm_gelu_and_residual(M, N, K):
+def test_gemm_gelu_and_residual(M, N, K, gemm_tile):
     from denseclip_vit_multimodal_amd import _native as Nat
     O = ops()
     dt = torch.bfloat16
@@ -123,8 +135,17 @@ def test_gemm_gelu_and_residual(M, N, K):
     assert rel_err(dz.float(), ref) < TOL[dt]
 
 
-@pytest.mark.parametrize("M,N,K", [(777, 256, 128), (65544 // 8, 768, 3072), (5000, 2304, 768)])
-def test_weight_grad_splitk(M, N, K):
+@pytest.fixture
+def tn_tile(request):
+    from denseclip_vit_multimodal_amd import _native as N
+    N.call("dclip_set_option", N.OPT_GEMM_TN_TILE, request.param)
+    yield request.param
+    N.call("dclip_set_option", N.OPT_GEMM_TN_TILE, 0)
+
+
+@pytest.mark.parametrize("tn_tile", [0, 1], indirect=True)
+@pytest.mark.parametrize("M,N,K", [(777, 256, 128), (65544 // 8, 768, 3072), (5000, 2304, 768), (300, 264, 520)])
+def test_weight_grad_splitk(M, N, K, tn_tile):
     O = ops()
     dt = torch.bfloat16
     dy = torch.randn(M, N, device=DEV).to(dt)
@@ -134,8 +155,9 @@ def test_weight_grad_splitk(M, N, K):
     assert rel_err(db, dy.float().sum(0)) < 1e-5
 
 
-@pytest.mark.parametrize("K,M,N", [(64, 128, 128), (100, 136, 72), (1000, 256, 384), (8193, 768, 768)])
-def test_gemm_tn(K, M, N):
+@pytest.mark.parametrize("tn_tile", [0, 1], indirect=True)
+@pytest.mark.parametrize("K,M,N", [(64, 128, 128), (100, 136, 72), (1000, 256, 384), (8193, 768, 768), (70, 264, 520)])
+def test_gemm_tn(K, M, N, tn_tile):
     O = ops()
     A = torch.randn(K, M, device=DEV).to(torch.bfloat16)
     B = torch.randn(K, N, device=DEV).to(torch.bfloat16)
