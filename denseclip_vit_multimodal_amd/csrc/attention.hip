@@ -351,7 +351,7 @@ struct DqCtx {
 
 // key tile t in LDS slot P: S^T - L, dP^T - delta (row constants as the initial
 // accumulators), dS^T = P (dP - delta), dQ^T += K^T dS^T; prefetches tile t+1.
-template <typename T, int NT, int P>
+template <typename T, int NT, int P, bool MASK>
 __device__ __forceinline__ void dq_step(DqCtx<T, NT>& c, int t) {
     typedef typename Mfma<T>::frag frag;
     const char* Kt = c.smem + P * 16384;
@@ -375,7 +375,7 @@ __device__ __forceinline__ void dq_step(DqCtx<T, NT>& c, int t) {
             pacc[kb] = Mfma<T>::mma(vf[s], c.gf[s], pacc[kb]);
         }
     }
-    if (c.ragged && t == c.nt - 1) {  // keys >= N (clamped copies): P = 0
+    if constexpr (MASK) {  // last tile only (peeled): keys >= N (clamped copies) get P = 0
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -451,7 +451,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const T* _
     const T* dOb = dout + (int64_t)b * N * C + hd * HD;
     c.N = N;
     c.nt = (N + 63) / 64;
-    c.ragged = (N & 63) != 0;
     const int q = qblk * QB + wave * 32 + c.l32;
     const int qc = q < N ? q : N - 1;
 #pragma unroll
@@ -482,9 +481,18 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const T* _
     tile_store<64, NT>(c.rv, smem + 8192);
     __syncthreads();
 
-    for (int t = 0; t < c.nt; t += 2) {
-        dq_step<T, NT, 0>(c, t);
-        if (t + 1 < c.nt) dq_step<T, NT, 1>(c, t + 1);
+    // steady state without the key mask (no branch between the S/dP MFMAs and the VALU that
+    // consumes them), then the last one or two tiles with it
+    int t = 0;
+    for (; t + 2 < c.nt; t += 2) {
+        dq_step<T, NT, 0, false>(c, t);
+        dq_step<T, NT, 1, false>(c, t + 1);
+    }
+    if (t + 1 < c.nt) {
+        dq_step<T, NT, 0, false>(c, t);
+        dq_step<T, NT, 1, true>(c, t + 1);
+    } else {
+        dq_step<T, NT, 0, true>(c, t);
     }
     scale *= 1.0f / DsScale<T>::v;
     if (q < N) {
@@ -503,10 +511,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const T* _
 }
 
 // ---------------------------------------------------------------------------- dK/dV pass
-template <typename T, int NT>
+template <typename T, int NT, int QS>
 struct DkvCtx {
     typedef typename Mfma<T>::frag frag;
-    char* smem;  // [slot][Q | dO][64 rows][128 B] + [slot][-L | -delta][64 floats]
+    static constexpr int SLOT = 2 * QS * 128;  // [Q | dO][QS rows][128 B]
+    char* smem;  // [slot][Q | dO] + [slot][-L | -delta][QS floats]
     const T* Qb;
     const T* dOb;
     const float* Lb;
@@ -515,48 +524,49 @@ struct DkvCtx {
     int C, N, nt, lane, l32, h;
     frag kf[4], vf[4];
     f32x16 dk[2], dv[2];
-    TileRegs<64, NT> rq, rg;
+    TileRegs<QS, NT> rq, rg;
     float rstat;
 };
 
 // stage query slice t: Q, dO rows and the negated row statistics (accumulator inits).
 // Query rows >= N get -L = -inf (P = 0, hence dS = 0) and -delta = 0: their clamped Q / dO
 // copies then contribute nothing to dK / dV.
-template <typename T, int NT>
-__device__ __forceinline__ void dkv_load(DkvCtx<T, NT>& c, int t) {
-    tile_load<T, 64, NT>(c.rq, c.Qb, c.ld, t * 64, c.N);
-    tile_load<T, 64, NT>(c.rg, c.dOb, c.C, t * 64, c.N);
-    if (threadIdx.x < 128) {  // the raw value: it is used only at store time (no early vmcnt wait)
-        const int r = t * 64 + (threadIdx.x & 63);
+template <typename T, int NT, int QS>
+__device__ __forceinline__ void dkv_load(DkvCtx<T, NT, QS>& c, int t) {
+    static_assert(NT >= 2 * QS, "one thread per staged statistic");
+    tile_load<T, QS, NT>(c.rq, c.Qb, c.ld, t * QS, c.N);
+    tile_load<T, QS, NT>(c.rg, c.dOb, c.C, t * QS, c.N);
+    if (threadIdx.x < 2 * QS) {  // the raw value: it is used only at store time (no early vmcnt wait)
+        const int r = t * QS + (threadIdx.x % QS);
         const int rc = r < c.N ? r : c.N - 1;
-        c.rstat = threadIdx.x < 64 ? c.Lb[rc] : c.Db[rc];
+        c.rstat = threadIdx.x < QS ? c.Lb[rc] : c.Db[rc];
     }
 }
 
-template <typename T, int NT>
-__device__ __forceinline__ void dkv_store(DkvCtx<T, NT>& c, int slot, int t) {
-    char* base = c.smem + slot * 16384;
-    tile_store<64, NT>(c.rq, base);
-    tile_store<64, NT>(c.rg, base + 8192);
-    float* stat = (float*)(c.smem + 2 * 16384);
-    if (threadIdx.x < 128) {
-        const bool valid = t * 64 + (int)(threadIdx.x & 63) < c.N;
-        stat[slot * 128 + threadIdx.x] = valid ? -c.rstat : (threadIdx.x < 64 ? -INFINITY : 0.f);
+template <typename T, int NT, int QS>
+__device__ __forceinline__ void dkv_store(DkvCtx<T, NT, QS>& c, int slot, int t) {
+    char* base = c.smem + slot * c.SLOT;
+    tile_store<QS, NT>(c.rq, base);
+    tile_store<QS, NT>(c.rg, base + QS * 128);
+    float* stat = (float*)(c.smem + 2 * c.SLOT);
+    if (threadIdx.x < 2 * QS) {
+        const bool valid = t * QS + (int)(threadIdx.x % QS) < c.N;
+        stat[slot * 2 * QS + threadIdx.x] = valid ? -c.rstat : (threadIdx.x < QS ? -INFINITY : 0.f);
     }
 }
 
-template <typename T, int NT, int P>
-__device__ __forceinline__ void dkv_step(DkvCtx<T, NT>& c, int t) {
+template <typename T, int NT, int QS, int P>
+__device__ __forceinline__ void dkv_step(DkvCtx<T, NT, QS>& c, int t) {
     typedef typename Mfma<T>::frag frag;
-    dkv_load<T, NT>(c, t + 1);  // clamped past the end: harmless, never used
+    dkv_load<T, NT, QS>(c, t + 1);  // clamped past the end: harmless, never used
     __builtin_amdgcn_sched_barrier(0);
-    const float* stat = (const float*)(c.smem + 2 * 16384) + P * 128;
+    const float* stat = (const float*)(c.smem + 2 * c.SLOT) + P * 2 * QS;
 #pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-        const char* Qt = c.smem + P * 16384 + sub * 32 * 128;
-        const char* Gt = Qt + 8192;
+    for (int sub = 0; sub < QS / 32; ++sub) {
+        const char* Qt = c.smem + P * c.SLOT + sub * 32 * 128;
+        const char* Gt = Qt + QS * 128;
         const float* Ls = stat + sub * 32;
-        const float* Ds = Ls + 64;
+        const float* Ds = Ls + QS;
         // S[q][key], dP[q][key]  (query rows in registers, key on the lane)
         frag qa[4], ga[4];
 #pragma unroll
@@ -607,13 +617,13 @@ __device__ __forceinline__ void dkv_step(DkvCtx<T, NT>& c, int t) {
             }
         }
     }
-    dkv_store<T, NT>(c, P ^ 1, t + 1);
+    dkv_store<T, NT, QS>(c, P ^ 1, t + 1);
     __syncthreads();
 }
 
-// Key-major dK/dV pass: 32*NW keys per workgroup (32 per wave); query slices of 64 rows
-// (two 32-row sub-slices per barrier).
-template <typename T, int NW>
+// Key-major dK/dV pass: 32*NW keys per workgroup (32 per wave); query slices of QS rows
+// (QS / 32 sub-slices of 32 rows per barrier).
+template <typename T, int NW, int QS>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const T* __restrict__ qkv,
                                                                         const T* __restrict__ dout,
                                                                         const float* __restrict__ lse,
@@ -622,8 +632,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const T*
                                                                         float dk_scale) {
     constexpr int NT = 64 * NW, KB = 32 * NW;
     typedef typename Mfma<T>::frag frag;
-    __shared__ __attribute__((aligned(16))) char smem[2 * 16384 + 2 * 128 * 4];
-    DkvCtx<T, NT> c;
+    __shared__ __attribute__((aligned(16))) char smem[2 * 2 * QS * 128 + 2 * 2 * QS * 4];
+    DkvCtx<T, NT, QS> c;
     c.smem = smem;
     c.lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -641,7 +651,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const T*
     c.Lb = lse + (int64_t)bh * N;
     c.Db = delta + (int64_t)bh * N;
     c.N = N;
-    c.nt = (N + 63) / 64;
+    c.nt = (N + QS - 1) / QS;
     const int key = kblk * KB + wave * 32 + c.l32;
     const int kc = key < N ? key : N - 1;
 #pragma unroll
@@ -655,12 +665,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const T*
     c.dv[1] = zero16();
     c.rstat = 0.f;
 
-    dkv_load<T, NT>(c, 0);
-    dkv_store<T, NT>(c, 0, 0);
+    dkv_load<T, NT, QS>(c, 0);
+    dkv_store<T, NT, QS>(c, 0, 0);
     __syncthreads();
     for (int t = 0; t < c.nt; t += 2) {
-        dkv_step<T, NT, 0>(c, t);
-        if (t + 1 < c.nt) dkv_step<T, NT, 1>(c, t + 1);
+        dkv_step<T, NT, QS, 0>(c, t);
+        if (t + 1 < c.nt) dkv_step<T, NT, QS, 1>(c, t + 1);
     }
     const float scale = dk_scale / DsScale<T>::v;
     if (key < N) {
@@ -708,14 +718,23 @@ void bwd_launch(const void* qkv, const void* o, const void* dout, const float* l
         attn_bwd_dq_kernel<T, 8><<<grid, 512, 0, st>>>((const T*)qkv, (const T*)o, (const T*)dout, lse, delta,
                                                        (T*)dqkv, N, H, scale);
     }
+    const bool qs128 = dclip_option(DCLIP_OPT_ATTN_DKDV_QS) == 128;
     if (dclip_option(DCLIP_OPT_ATTN_DKDV_WAVES) != 8) {
         dim3 grid(((N + 127) / 128) * B * H);
-        attn_bwd_dkdv_kernel<T, 4><<<grid, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, (T*)dqkv, N, H,
-                                                         1.0f / LOG2E);
+        if (qs128)
+            attn_bwd_dkdv_kernel<T, 4, 128><<<grid, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta,
+                                                                  (T*)dqkv, N, H, 1.0f / LOG2E);
+        else
+            attn_bwd_dkdv_kernel<T, 4, 64><<<grid, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta,
+                                                                 (T*)dqkv, N, H, 1.0f / LOG2E);
     } else {
         dim3 grid(((N + 255) / 256) * B * H);
-        attn_bwd_dkdv_kernel<T, 8><<<grid, 512, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, (T*)dqkv, N, H,
-                                                         1.0f / LOG2E);
+        if (qs128)
+            attn_bwd_dkdv_kernel<T, 8, 128><<<grid, 512, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta,
+                                                                  (T*)dqkv, N, H, 1.0f / LOG2E);
+        else
+            attn_bwd_dkdv_kernel<T, 8, 64><<<grid, 512, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta,
+                                                                 (T*)dqkv, N, H, 1.0f / LOG2E);
     }
 }
 

@@ -294,18 +294,21 @@ __device__ __forceinline__ void epi_row8(float (&v)[8], int m, int nb, int N, co
     }
 }
 
-template <int BM, int BN, int WM, int WN, int STAGES>
+template <int BM, int BN, int WM, int WN, int STAGES, int BKT = 64>
 struct BigCfg {
     static constexpr int NW = WM * WN, NT = 64 * NW;
     static constexpr int WTM = BM / WM, WTN = BN / WN;  // per-wave output tile
     static constexpr int MB = WTM / 16, NB = WTN / 16;   // 16x16 blocks per wave
-    static constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE_BYTES = A_BYTES + B_BYTES;
-    static constexpr int A_INST = BM / 8 / NW, B_INST = BN / 8 / NW;  // 1-KiB glds per wave per stage
+    static constexpr int KB = BKT, ROWB = 2 * BKT;       // k per stage, LDS bytes per row
+    static constexpr int RPI = 1024 / ROWB;              // rows per 1-KiB glds piece
+    static constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, STAGE_BYTES = A_BYTES + B_BYTES;
+    static constexpr int A_INST = BM / RPI / NW, B_INST = BN / RPI / NW;  // 1-KiB glds per wave per stage
     static constexpr int G = A_INST + B_INST;                          // glds per thread per stage
     static constexpr int EP_LD = WTN + 4;                              // epilogue row stride (floats)
     static constexpr int EP_BYTES = NW * 32 * EP_LD * 4;
     static constexpr int SMEM = STAGES * STAGE_BYTES > EP_BYTES ? STAGES * STAGE_BYTES : EP_BYTES;
-    static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "staging split");
+    static_assert(BM % (RPI * NW) == 0 && BN % (RPI * NW) == 0, "staging split");
+    static_assert(BKT == 64 || BKT == 32, "k per stage");
     static_assert(WTM % 32 == 0 && WTN % 16 == 0 && WTN <= 64, "wave tile");
 };
 
@@ -356,14 +359,23 @@ __device__ __forceinline__ void big_epilogue(f32x4 (&acc)[Cfg::NB][Cfg::MB], cha
     }
 }
 
-template <typename T, int ROWS_INST>
+// chunk XOR of LDS row r: 128-B rows (BK 64): (r >> 1) & 7; 64-B rows (BK 32): ((r >> 3) & 1) << 1
+// — both make the 16x16x32 fragment reads (16 rows x one chunk per 16 lanes) conflict-free
+template <int BKT>
+__device__ __forceinline__ int big_sw(int r) {
+    if constexpr (BKT == 64) return (r >> 1) & 7;
+    else return ((r >> 3) & 1) << 1;
+}
+
+template <typename T, int ROWS_INST, int BKT>
 __device__ __forceinline__ void stage_rows(const T* __restrict__ X, int64_t ldx, int row0, int rows, int k0,
                                            char* lds, int wave, int lane) {
+    constexpr int CPR = BKT / 8;  // 16-B chunks per row
 #pragma unroll
     for (int i = 0; i < ROWS_INST; ++i) {
         const int inst = wave * ROWS_INST + i;
-        const int r = inst * 8 + (lane >> 3);
-        const int c = (lane & 7) ^ ((r >> 1) & 7);
+        const int r = inst * (64 / CPR) + lane / CPR;
+        const int c = (lane % CPR) ^ big_sw<BKT>(r);
         int gr = row0 + r;
         gr = gr < rows ? gr : rows - 1;
         __builtin_amdgcn_global_load_lds((const void*)(X + (int64_t)gr * ldx + k0 + c * 8), LDS_PTR(lds + inst * 1024),
@@ -371,13 +383,18 @@ __device__ __forceinline__ void stage_rows(const T* __restrict__ X, int64_t ldx,
     }
 }
 
-template <typename T, int EPI, typename OutT, int BM, int BN, int WM, int WN, int STAGES>
+template <typename T, int BKT>
+__device__ __forceinline__ typename Mfma<T>::frag big_frag(const char* img, int r, int chunk) {
+    return *(const typename Mfma<T>::frag*)(img + r * (2 * BKT) + ((chunk ^ big_sw<BKT>(r)) << 4));
+}
+
+template <typename T, int EPI, typename OutT, int BM, int BN, int WM, int WN, int STAGES, int BKT>
 __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_nt_big_kernel(
     const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
     int M, int N, int k_chunk, int tiles_m, int tiles_n,
     const float* __restrict__ bias, const void* __restrict__ aux, int64_t ld_aux,
     void* __restrict__ C, int64_t ldc, void* __restrict__ C2, int64_t ldc2, int64_t slab, float alpha) {
-    typedef BigCfg<BM, BN, WM, WN, STAGES> Cfg;
+    typedef BigCfg<BM, BN, WM, WN, STAGES, BKT> Cfg;
     typedef typename Mfma<T>::frag frag;
     __shared__ __attribute__((aligned(16))) char smem[Cfg::SMEM];
     const int lane = threadIdx.x & 63;
@@ -389,7 +406,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_nt_big_kernel(
     const int m0 = (t / tiles_n) * BM;
     const int n0 = (t % tiles_n) * BN;
     const int kbeg = blockIdx.y * k_chunk;
-    const int nk = k_chunk / BK;
+    const int nk = k_chunk / BKT;
 
     f32x4 acc[Cfg::NB][Cfg::MB];
 #pragma unroll
@@ -399,8 +416,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_nt_big_kernel(
 
     auto stage = [&](int kt, int slot) {
         char* base = smem + slot * Cfg::STAGE_BYTES;
-        stage_rows<T, Cfg::A_INST>(A, lda, m0, M, kbeg + kt * BK, base, wave, lane);
-        stage_rows<T, Cfg::B_INST>(B, ldb, n0, N, kbeg + kt * BK, base + Cfg::A_BYTES, wave, lane);
+        stage_rows<T, Cfg::A_INST, BKT>(A, lda, m0, M, kbeg + kt * BKT, base, wave, lane);
+        stage_rows<T, Cfg::B_INST, BKT>(B, ldb, n0, N, kbeg + kt * BKT, base + Cfg::A_BYTES, wave, lane);
     };
 #pragma unroll
     for (int s = 0; s < STAGES - 1; ++s)
@@ -416,13 +433,13 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_nt_big_kernel(
         const char* At = smem + (kt % STAGES) * Cfg::STAGE_BYTES;
         const char* Bt = At + Cfg::A_BYTES;
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
+        for (int ks = 0; ks < BKT / 32; ++ks) {
             frag fb[Cfg::NB], fa[Cfg::MB];
             const int ch = ks * 4 + lq;
 #pragma unroll
-            for (int i = 0; i < Cfg::NB; ++i) fb[i] = read_frag<T>(Bt, wn * Cfg::WTN + i * 16 + l16, ch);
+            for (int i = 0; i < Cfg::NB; ++i) fb[i] = big_frag<T, BKT>(Bt, wn * Cfg::WTN + i * 16 + l16, ch);
 #pragma unroll
-            for (int j = 0; j < Cfg::MB; ++j) fa[j] = read_frag<T>(At, wm * Cfg::WTM + j * 16 + l16, ch);
+            for (int j = 0; j < Cfg::MB; ++j) fa[j] = big_frag<T, BKT>(At, wm * Cfg::WTM + j * 16 + l16, ch);
 #pragma unroll
             for (int j = 0; j < Cfg::MB; ++j)
 #pragma unroll
@@ -713,19 +730,20 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, i
     }
 }
 
-template <typename T, int EPI, typename OutT, int TBM, int TBN, int WM, int WN, int STAGES>
+template <typename T, int EPI, typename OutT, int TBM, int TBN, int WM, int WN, int STAGES, int BKT = 64>
 void launch_big(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
                 int splits, float alpha, const float* bias, const void* aux, int64_t ld_aux, void* C, int64_t ldc,
                 void* C2, int64_t ldc2, hipStream_t st) {
     const int tiles_m = (int)((M + TBM - 1) / TBM), tiles_n = (int)((N + TBN - 1) / TBN);
     dim3 grid(tiles_m * tiles_n, splits);
-    gemm_nt_big_kernel<T, EPI, OutT, TBM, TBN, WM, WN, STAGES><<<grid, 64 * WM * WN, 0, st>>>(
+    gemm_nt_big_kernel<T, EPI, OutT, TBM, TBN, WM, WN, STAGES, BKT><<<grid, 64 * WM * WN, 0, st>>>(
         (const T*)A, lda, (const T*)B, ldb, (int)M, (int)N, (int)(K / splits), tiles_m, tiles_n, bias, aux, ld_aux,
         C, ldc, C2, ldc2, (int64_t)M * N, alpha);
 }
 
 // tile configuration: DCLIP_OPT_GEMM_TILE 1 = 128x128 (4 waves, 2 workgroups/CU), 2 = 256x256
-// (8 waves, 2-stage ring), 3 = 256x128 (8 waves, 3-stage ring), 0 = automatic
+// (8 waves, 2-stage ring of 64-deep k-tiles), 3 = 256x128 (8 waves, 3-stage ring),
+// 4 = 256x256 with a 4-stage ring of 32-deep k-tiles, 0 = automatic
 inline int gemm_tile_choice(int64_t M, int64_t N) {
     const int opt = dclip_option(DCLIP_OPT_GEMM_TILE);
     if (opt != 0) return opt;
@@ -746,6 +764,11 @@ int launch(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, in
     if (choice == 3) {
         launch_big<T, EPI, OutT, 256, 128, 4, 2, 3>(A, lda, B, ldb, M, N, K, splits, alpha, bias, aux, ld_aux, C,
                                                     ldc, C2, ldc2, st);
+        return 0;
+    }
+    if (choice == 4) {
+        launch_big<T, EPI, OutT, 256, 256, 2, 4, 4, 32>(A, lda, B, ldb, M, N, K, splits, alpha, bias, aux, ld_aux, C,
+                                                        ldc, C2, ldc2, st);
         return 0;
     }
     const int tiles_m = (int)((M + BM - 1) / BM), tiles_n = (int)((N + BN - 1) / BN);

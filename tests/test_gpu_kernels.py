@@ -66,7 +66,7 @@ def test_layernorm_bwd(cols, dydt):
 
 # ----------------------------------------------------------------------------- GEMM
 SHAPES = [(128, 128, 64), (300, 200, 192), (65, 64, 128), (1000, 2304, 768), (4097, 768, 3072), (8, 512, 768)]
-TILES = [1, 2, 3]  # dclip_set_option(DCLIP_OPT_GEMM_TILE): 128x128, 256x256, 256x128
+TILES = [1, 2, 3, 4]  # dclip_set_option(DCLIP_OPT_GEMM_TILE): 128x128, 256x256, 256x128, 256x256 k32
 
 
 @pytest.fixture
@@ -206,12 +206,14 @@ def attn_variant(request):
     """Select attention kernel variants (waves per workgroup of the forward, dQ and dK/dV
     passes) through dclip_set_option; restore the defaults."""
     from denseclip_vit_multimodal_amd import _native as N
-    fwd, dq, dkdv = request.param
+    fwd, dq, dkdv = request.param[:3]
+    qs = request.param[3] if len(request.param) > 3 else 0
     N.call("dclip_set_option", N.OPT_ATTN_FWD_WAVES, fwd)
     N.call("dclip_set_option", N.OPT_ATTN_DQ_WAVES, dq)
     N.call("dclip_set_option", N.OPT_ATTN_DKDV_WAVES, dkdv)
+    N.call("dclip_set_option", N.OPT_ATTN_DKDV_QS, qs)
     yield request.param
-    for o in (N.OPT_ATTN_FWD_WAVES, N.OPT_ATTN_DQ_WAVES, N.OPT_ATTN_DKDV_WAVES):
+    for o in (N.OPT_ATTN_FWD_WAVES, N.OPT_ATTN_DQ_WAVES, N.OPT_ATTN_DKDV_WAVES, N.OPT_ATTN_DKDV_QS):
         N.call("dclip_set_option", o, 0)
 
 
@@ -245,7 +247,7 @@ def test_attention_spiky_rescale(spike, attn_variant):
     assert rel_err(o.float(), attn_ref(qref, B, N, H)) < TOL[torch.float16]
 
 
-@pytest.mark.parametrize("attn_variant", [(8, 4, 4), (8, 8, 8)], indirect=True)
+@pytest.mark.parametrize("attn_variant", [(8, 4, 4), (8, 8, 8), (8, 8, 8, 128), (8, 8, 4, 128)], indirect=True)
 @pytest.mark.parametrize("N", [1, 33, 63, 64, 65, 130, 257, 700])
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
 def test_attention_bwd(N, dt, attn_variant):
