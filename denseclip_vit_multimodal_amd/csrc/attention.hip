@@ -67,13 +67,19 @@ __device__ __forceinline__ typename Mfma<T>::frag tr_frag(const char* img, int r
     return __builtin_bit_cast(typename Mfma<T>::frag, v);
 }
 
-// 16-bit B-operand fragment from accumulator registers 8s..8s+7
+// 16-bit B-operand fragment from accumulator registers 8s..8s+7 (built from explicit
+// register pairs: one v_cvt_pk per dword, no 16-bit re-alignment)
 template <typename T>
 __device__ __forceinline__ typename Mfma<T>::frag pack_frag(const f32x16& a, int s) {
-    typename Mfma<T>::frag f;
+    typedef T t2 __attribute__((ext_vector_type(2)));
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 w;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = (T)a[8 * s + j];
-    return f;
+    for (int j = 0; j < 4; ++j) {
+        const t2 p = {(T)a[8 * s + 2 * j], (T)a[8 * s + 2 * j + 1]};
+        w[j] = __builtin_bit_cast(unsigned, p);
+    }
+    return __builtin_bit_cast(typename Mfma<T>::frag, w);
 }
 
 __device__ __forceinline__ f32x16 zero16() {
@@ -120,7 +126,7 @@ struct TileRegs {
     i32x4 v[PER];  // native vector type: HIP's int4 struct arrays end up in scratch
 };
 
-// rows >= N are clamped to N - 1 (duplicates of a valid row; callers neutralise them)
+// rows outside [0, N) are clamped into it (duplicates of a valid row; callers neutralise them)
 template <typename T, int ROWS, int NT>
 __device__ __forceinline__ void tile_load(TileRegs<ROWS, NT>& R, const T* __restrict__ base, int64_t ld, int r0,
                                           int N) {
@@ -129,6 +135,7 @@ __device__ __forceinline__ void tile_load(TileRegs<ROWS, NT>& R, const T* __rest
         const int idx = i * NT + threadIdx.x;  // (row, chunk) = (idx >> 3, idx & 7)
         int gr = r0 + (idx >> 3);
         gr = gr < N ? gr : N - 1;
+        gr = gr > 0 ? gr : 0;
         R.v[i] = *(const i32x4*)(base + (int64_t)gr * ld + (idx & 7) * 8);
     }
 }
@@ -334,95 +341,92 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_kernel(const T* __re
 
 // ============================================================================ backward
 // ---------------------------------------------------------------------------- dQ pass
+// Query-major dQ pass, software-pipelined over 32-key units: while the VALU turns unit u's
+// S / dP accumulators into dS (exp2, multiply, pack) the matrix pipe already runs the
+// S / dP chain of unit u+1, and unit u's dQ^T += K^T dS^T follows.  Keys are staged in
+// 64-key tiles (two units) through a 3-slot LDS ring — unit u+1 may sit in the next tile —
+// with one barrier per tile; the loop is unrolled by three (slot offsets are immediates).
+// The key tiles are aligned to the END of the sequence (tile t = keys 64t - off ..
+// 64t - off + 63, off = (64 - N % 64) % 64), so the only ragged tile is tile 0; it is
+// processed in the prologue with its mask (keys < 0), and the steady-state loop has none.
 template <typename T, int NT>
 struct DqCtx {
     typedef typename Mfma<T>::frag frag;
-    char* smem;  // [slot][K | V][64 rows][128 B]
+    char* smem;  // [slot 0..2][K | V][64 rows][128 B]
     const T* Kb;
     const T* Vb;
     int64_t ld;
-    int N, nt, lane, l32, h;
-    bool ragged;
+    int N, nt, off, lane, l32, h;
     frag qf[4], gf[4];
-    f32x16 negL, negD;
+    float negL, negD;  // row constants (splat into the accumulators per unit)
     f32x16 dq[2];
     TileRegs<64, NT> rk, rv;
 };
 
-// key tile t in LDS slot P: S^T - L, dP^T - delta (row constants as the initial
-// accumulators), dS^T = P (dP - delta), dQ^T += K^T dS^T; prefetches tile t+1.
-template <typename T, int NT, int P, bool MASK>
-__device__ __forceinline__ void dq_step(DqCtx<T, NT>& c, int t) {
+// S^T - L and dP^T - delta of the 32-key block `kb` of the tile image at Kt (V at Kt + 8 KiB)
+template <typename T, int NT>
+__device__ __forceinline__ void dq_sdp(DqCtx<T, NT>& c, const char* Kt, int kb, f32x16& sacc, f32x16& pacc) {
     typedef typename Mfma<T>::frag frag;
-    const char* Kt = c.smem + P * 16384;
-    const char* Vt = Kt + 8192;
-    tile_load<T, 64, NT>(c.rk, c.Kb, c.ld, (t + 1) * 64, c.N);
-    tile_load<T, 64, NT>(c.rv, c.Vb, c.ld, (t + 1) * 64, c.N);
-    __builtin_amdgcn_sched_barrier(0);
-    f32x16 sacc[2] = {c.negL, c.negL};
-    f32x16 pacc[2] = {c.negD, c.negD};
+    frag kf[4], vf[4];
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-        frag kf[4], vf[4];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            kf[s] = row_frag<T>(Kt, kb * 32 + c.l32, 2 * s + c.h);
-            vf[s] = row_frag<T>(Vt, kb * 32 + c.l32, 2 * s + c.h);
-        }
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            sacc[kb] = Mfma<T>::mma(kf[s], c.qf[s], sacc[kb]);
-            pacc[kb] = Mfma<T>::mma(vf[s], c.gf[s], pacc[kb]);
-        }
+    for (int s = 0; s < 4; ++s) {
+        kf[s] = row_frag<T>(Kt, kb * 32 + c.l32, 2 * s + c.h);
+        vf[s] = row_frag<T>(Kt + 8192, kb * 32 + c.l32, 2 * s + c.h);
     }
-    if constexpr (MASK) {  // last tile only (peeled): keys >= N (clamped copies) get P = 0
+    sacc = splat16(c.negL);
+    pacc = splat16(c.negD);
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                if (t * 64 + kb * 32 + acc_row(r, c.h) >= c.N) sacc[kb][r] = -INFINITY;
+    for (int s = 0; s < 4; ++s) {
+        sacc = Mfma<T>::mma(kf[s], c.qf[s], sacc);
+        pacc = Mfma<T>::mma(vf[s], c.gf[s], pacc);
     }
-    frag kt[2][2];  // K^T fragments for the first key block, in flight during dS
+}
+
+// dS^T of one unit (consumes sacc / pacc), then dQ^T[d][q] += K^T[d][key] dS^T[key][q]
+template <typename T, int NT, bool MASK>
+__device__ __forceinline__ void dq_ds(DqCtx<T, NT>& c, const char* Kt, int kb, int key0, f32x16& sacc,
+                                      const f32x16& pacc) {
+    typedef typename Mfma<T>::frag frag;
+    frag kt[2][2];
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-        for (int db = 0; db < 2; ++db) kt[s][db] = tr_frag<T>(Kt, 0, s, db, c.lane);
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+        for (int db = 0; db < 2; ++db) kt[s][db] = tr_frag<T>(Kt, kb, s, db, c.lane);
+    if constexpr (MASK) {  // tile 0 only: keys < 0 (clamped copies of key 0) get P = 0
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-            sacc[kb][r] = __builtin_amdgcn_exp2f(sacc[kb][r]) * pacc[kb][r] * DsScale<T>::v;  // dS^T
-    // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-        frag kn[2][2];
-        if (kb == 0) {
-#pragma unroll
-            for (int s = 0; s < 2; ++s)
-#pragma unroll
-                for (int db = 0; db < 2; ++db) kn[s][db] = tr_frag<T>(Kt, 1, s, db, c.lane);
-        }
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const frag sf = pack_frag<T>(sacc[kb], s);
-#pragma unroll
-            for (int db = 0; db < 2; ++db) c.dq[db] = Mfma<T>::mma(kt[s][db], sf, c.dq[db]);
-        }
-        if (kb == 0) {
-#pragma unroll
-            for (int s = 0; s < 2; ++s)
-#pragma unroll
-                for (int db = 0; db < 2; ++db) kt[s][db] = kn[s][db];
-        }
+            if (key0 + acc_row(r, c.h) < 0) sacc[r] = -INFINITY;
     }
-    tile_store<64, NT>(c.rk, c.smem + (P ^ 1) * 16384);
-    tile_store<64, NT>(c.rv, c.smem + (P ^ 1) * 16384 + 8192);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sacc[r] = __builtin_amdgcn_exp2f(sacc[r]) * pacc[r] * DsScale<T>::v;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const frag sf = pack_frag<T>(sacc, s);
+#pragma unroll
+        for (int db = 0; db < 2; ++db) c.dq[db] = Mfma<T>::mma(kt[s][db], sf, c.dq[db]);
+    }
+}
+
+// tile T in slot P = T % 3; on entry (sA, pA) = unit (T, 0), on exit (sA, pA) = unit (T+1, 0)
+template <typename T, int NT, int P>
+__device__ __forceinline__ void dq_step(DqCtx<T, NT>& c, int t, f32x16& sA, f32x16& pA, f32x16& sB, f32x16& pB) {
+    const char* Kt = c.smem + P * 16384;
+    const char* Kn = c.smem + ((P + 1) % 3) * 16384;
+    tile_load<T, 64, NT>(c.rk, c.Kb, c.ld, (t + 2) * 64 - c.off, c.N);
+    tile_load<T, 64, NT>(c.rv, c.Vb, c.ld, (t + 2) * 64 - c.off, c.N);
+    __builtin_amdgcn_sched_barrier(0);                   // keep the prefetch at the top
+    dq_sdp<T, NT>(c, Kt, 1, sB, pB);                     // unit (t, 1) on the matrix pipe ...
+    dq_ds<T, NT, false>(c, Kt, 0, 0, sA, pA);            // ... beside dS / dQ of unit (t, 0)
+    dq_sdp<T, NT>(c, Kn, 0, sA, pA);                     // unit (t+1, 0) ...
+    dq_ds<T, NT, false>(c, Kt, 1, 0, sB, pB);            // ... beside unit (t, 1)
+    tile_store<64, NT>(c.rk, c.smem + ((P + 2) % 3) * 16384);
+    tile_store<64, NT>(c.rv, c.smem + ((P + 2) % 3) * 16384 + 8192);
     __syncthreads();
 }
 
-// Query-major dQ pass: 32*NW queries per workgroup (32 per wave), all key tiles.
-// Also computes delta = rowsum(dO * O) for its queries (the dK/dV pass, launched next on
-// the same stream, reads it) — no separate delta launch.
+// Query-major dQ pass: 32*NW queries per workgroup (32 per wave), all key tiles.  Also
+// computes delta = rowsum(dO * O) for its queries (the dK/dV pass, launched next on the same
+// stream, reads it) — no separate delta launch.
 template <typename T, int NW>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const T* __restrict__ qkv,
                                                                       const T* __restrict__ o,
@@ -433,7 +437,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const T* _
                                                                       float scale) {
     constexpr int NT = 64 * NW, QB = 32 * NW;
     typedef typename Mfma<T>::frag frag;
-    __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 64 * 128];
+    __shared__ __attribute__((aligned(16))) char smem[3 * 16384];
     DqCtx<T, NT> c;
     c.smem = smem;
     c.lane = threadIdx.x & 63;
@@ -458,7 +462,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const T* _
         c.qf[s] = *(const frag*)(Qb + (int64_t)qc * c.ld + (2 * s + c.h) * 8);
         c.gf[s] = *(const frag*)(dOb + (int64_t)qc * C + (2 * s + c.h) * 8);
     }
-    c.negL = splat16(-lse[(int64_t)bh * N + qc]);
+    c.negL = -lse[(int64_t)bh * N + qc];
     {
         const T* Orow = o + ((int64_t)b * N + qc) * C + hd * HD;
         float dpart = 0.f;  // this lane's half of the 64 dims (chunks h, 2+h, 4+h, 6+h)
@@ -470,29 +474,38 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const T* _
         }
         const float dl = xhalf_sum(dpart);
         if (q < N && c.h == 0) delta[(int64_t)bh * N + q] = dl;
-        c.negD = splat16(-dl);
+        c.negD = -dl;
     }
     c.dq[0] = zero16();
     c.dq[1] = zero16();
 
-    tile_load<T, 64, NT>(c.rk, c.Kb, c.ld, 0, N);
-    tile_load<T, 64, NT>(c.rv, c.Vb, c.ld, 0, N);
-    tile_store<64, NT>(c.rk, smem);
-    tile_store<64, NT>(c.rv, smem + 8192);
-    __syncthreads();
-
-    // steady state without the key mask (no branch between the S/dP MFMAs and the VALU that
-    // consumes them), then the last one or two tiles with it
-    int t = 0;
-    for (; t + 2 < c.nt; t += 2) {
-        dq_step<T, NT, 0, false>(c, t);
-        dq_step<T, NT, 1, false>(c, t + 1);
+    // tiles 0..2 into slots 0..2 (rows clamped into [0, N): copies past the ends are harmless)
+    c.off = (64 - (N & 63)) & 63;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        tile_load<T, 64, NT>(c.rk, c.Kb, c.ld, i * 64 - c.off, N);
+        tile_load<T, 64, NT>(c.rv, c.Vb, c.ld, i * 64 - c.off, N);
+        tile_store<64, NT>(c.rk, smem + i * 16384);
+        tile_store<64, NT>(c.rv, smem + i * 16384 + 8192);
     }
-    if (t + 1 < c.nt) {
-        dq_step<T, NT, 0, false>(c, t);
-        dq_step<T, NT, 1, true>(c, t + 1);
-    } else {
-        dq_step<T, NT, 0, true>(c, t);
+    __syncthreads();
+    // tile 0 (the ragged one) in full, then the first unit of tile 1
+    f32x16 sA, pA, sB, pB;
+    dq_sdp<T, NT>(c, smem, 0, sA, pA);
+    dq_sdp<T, NT>(c, smem, 1, sB, pB);
+    dq_ds<T, NT, true>(c, smem, 0, -c.off, sA, pA);
+    dq_ds<T, NT, true>(c, smem, 1, 32 - c.off, sB, pB);
+    dq_sdp<T, NT>(c, smem + 16384, 0, sA, pA);
+    __syncthreads();  // slot 0 is refilled at the end of tile 1
+
+    int t = 1;
+    while (true) {  // unrolled by three: every slot offset is an immediate
+        if (t >= c.nt) break;
+        dq_step<T, NT, 1>(c, t++, sA, pA, sB, pB);
+        if (t >= c.nt) break;
+        dq_step<T, NT, 2>(c, t++, sA, pA, sB, pB);
+        if (t >= c.nt) break;
+        dq_step<T, NT, 0>(c, t++, sA, pA, sB, pB);
     }
     scale *= 1.0f / DsScale<T>::v;
     if (q < N) {
