@@ -14,7 +14,7 @@ ok() { # continue only after a clean exit or an ordinary test failure
 }
 
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 480 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1; ok $? pytest
+  timeout -k 10 480 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; ok $? pytest
   tail -5 $OUT/pytest_gpu.log
 fi
 timeout -k 10 420 python bench.py --steps ${STEPS:-5} --warmup 2 > $OUT/bench.log 2>&1; ok $? bench

@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 OUT=${1:-gpurun_out/pmc_attn}
 shift || true
 mkdir -p $OUT
-run() { timeout -k 10 300 rocprofv3 --kernel-trace --pmc "$@" -d $OUT/p$PASS -o run --output-format csv -- python tools/attn_probe.py 2 $PROBE_ARGS > $OUT/p$PASS.log 2>&1; PASS=$((PASS+1)); }
+run() { timeout -s KILL 120 rocprofv3 --kernel-trace --pmc "$@" -d $OUT/p$PASS -o run --output-format csv -- python tools/attn_probe.py 2 $PROBE_ARGS > $OUT/p$PASS.log 2>&1; PASS=$((PASS+1)); }
 PASS=1
 run SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE
 run SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VALU_TRANS_F32
