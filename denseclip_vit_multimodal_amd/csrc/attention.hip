@@ -46,7 +46,7 @@ __device__ __forceinline__ int swz(int row, int col) {
 }
 
 template <typename T>
-__device__ __forceinline__ typename Mfma<T>::frag row_frag(const char* img, int row, int chunk) {
+__device__ __forceinline__ typename Mfma<T>::frag row_frag(const char* __restrict__ img, int row, int chunk) {
     return *(const typename Mfma<T>::frag*)(img + row * 128 + ((chunk ^ xsw(row)) << 4));
 }
 
@@ -55,7 +55,7 @@ __device__ __forceinline__ typename Mfma<T>::frag row_frag(const char* img, int 
 // image row rb*32 + 16s + 8(j>>2) + 4h + (j&3), MFMA row (lane & 31) is image column
 // cb*32 + (lane & 31).  Two transposing 4x16 LDS reads.
 template <typename T>
-__device__ __forceinline__ typename Mfma<T>::frag tr_frag(const char* img, int rb, int s, int cb, int lane) {
+__device__ __forceinline__ typename Mfma<T>::frag tr_frag(const char* __restrict__ img, int rb, int s, int cb, int lane) {
     const int i = lane & 15, q = i >> 2, p = i & 3, g = lane >> 4, h = lane >> 5;
     const int row = rb * 32 + 16 * s + 4 * h + q;
     const int col = cb * 32 + (g & 1) * 16 + 4 * p;
@@ -337,6 +337,633 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_kernel(const T* __re
             }
         if (c.h == 0) lse[(int64_t)bh * N + q] = c.m + __log2f(lt);
     }
+}
+
+// ============================================================================ forward, CLS split
+// Shapes with N = 1 + 64k (the CLS token plus a multiple of 64 patches: every 16-px ViT at
+// H, W multiples of 128 — the benchmark's 1024x2048 gives N = 8193) take the CLS token out of
+// the tiled sweep on both sides:
+//   * key 0 is folded into every query row's softmax state in the prologue (VALU dot
+//     products), so the main loop sweeps keys 1..N-1 in full 64-key tiles: no mask, no clamp;
+//   * queries 1..N-1 form (N-1)/QB full query blocks.  (The generic kernel's extra block per
+//     (batch, head) computes ONE row at the cost of a full key sweep.)  Query 0 is a split-key
+//     VALU pass, one 64-key tile per wave (attn_row0_part_kernel), and a merge
+//     (attn_row0_merge_kernel) that runs before the main pass.  The partials are parked in o
+//     itself — rows 1.. of each batch, which the main pass overwrites afterwards — so the ABI
+//     needs no workspace.
+// Staging: K and V tiles go HBM/L2 -> LDS by LDS-DMA (buffer_load ... lds, one 1-KiB piece of
+// 8 rows per wave-instruction; the XOR swizzle is applied to the per-lane SOURCE offset, the
+// LDS destination is lane-linear) into 4-slot rings, three tiles ahead of their use: no
+// staging registers, no ds_write, and the one barrier per tile sits at the top of the step
+// behind a counted vmcnt.  Per-lane voffsets are fixed for the whole sweep; each tile is a
+// scalar soffset.
+// Softmax reference (T13 variant): P = exp2(S - m) is taken against the current reference
+// and the tile's per-lane row sums are checked instead of a per-tile row max: when a lane's
+// partial sum exceeds 2^12 (some P > 2^12, or an overflow) the tile is re-done — S(t) is
+// recomputed from K(t), still in its slot, the reference moves to the tile's row max and O,
+// l and S(t+1) are rescaled — BEFORE P(t) enters O or l.  Without a firing every P <= 2^12
+// (representable in fp16; the relative rounding of 16-bit P does not depend on its size).
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+template <typename T, int NW>
+struct Fwd2Ctx {
+    typedef typename Mfma<T>::frag frag;
+    static constexpr int PIECES = 8 / NW;  // 1-KiB pieces of a 64-row tile per wave
+    char* smem;  // K ring [4][8 KiB] | V ring [4][8 KiB]
+    rsrc_t rs;   // this batch's qkv rows
+    uint32_t voffK[PIECES], voffV[PIECES];
+    uint32_t ldb;  // row pitch (bytes)
+    int nt, l32, h, lane, wave;
+    frag qf[4];
+    f32x16 o[2];
+    f32x16 negm;
+    float m;
+    float l4[4];  // per-lane partial row sums (combined in the epilogue)
+};
+
+// issue tile `t` (keys 1 + 64t ..) of K and V into ring slot `slot` (LDS-DMA, this wave's pieces)
+template <typename T, int NW>
+__device__ __forceinline__ void fwd2_issue(Fwd2Ctx<T, NW>& c, int t, int slot) {
+#if defined(__HIP_DEVICE_COMPILE__)  // the LDS-DMA builtin has no host-pass declaration
+    const uint32_t soff = (uint32_t)(1 + 64 * t) * c.ldb;
+#pragma unroll
+    for (int i = 0; i < Fwd2Ctx<T, NW>::PIECES; ++i) {
+        const int piece = c.wave + i * NW;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rs, LDS_PTR(c.smem + slot * 8192 + piece * 1024), 16, c.voffK[i],
+                                                 soff, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < Fwd2Ctx<T, NW>::PIECES; ++i) {
+        const int piece = c.wave + i * NW;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rs, LDS_PTR(c.smem + 4 * 8192 + slot * 8192 + piece * 1024), 16,
+                                                 c.voffV[i], soff, 0, 0);
+    }
+#endif
+}
+
+__device__ __forceinline__ float tile_rowmax2(const f32x16 (&sacc)[2]) {
+    float mx[4] = {sacc[0][0], sacc[0][1], sacc[0][2], sacc[0][3]};
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = (kb == 0 ? 4 : 0); r < 16; r += 4)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) mx[j] = fmaxf(mx[j], sacc[kb][r + j]);
+    return xhalf_max(fmaxf(fmaxf(mx[0], mx[1]), fmaxf(mx[2], mx[3])));
+}
+
+// P = exp2(s) in place, per-lane partial row sums into rsp
+__device__ __forceinline__ void exp_tile(f32x16 (&s)[2], float (&rsp)[4]) {
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float p = __builtin_amdgcn_exp2f(s[kb][r]);
+            s[kb][r] = p;
+            if (kb == 0 && r < 4) rsp[r] = p;
+            else rsp[r & 3] += p;
+        }
+}
+
+// step t (LDS slot Q = t % 4): S(t+1) into sn; P(t) from sc, the reference check, PV(t)
+template <typename T, int NW, int Q>
+__device__ __forceinline__ void fwd2_step(Fwd2Ctx<T, NW>& c, int t, f32x16 (&sc)[2], f32x16 (&sn)[2]) {
+    typedef typename Mfma<T>::frag frag;
+    constexpr float LIM = 4096.0f;
+    const char* Ks = c.smem;
+    const char* Vs = c.smem + 4 * 8192;
+    // K(t+1), V(t) have landed (own pieces: the wave's younger 3 tiles stay in flight), and
+    // every wave is done with step t-1 (slot (t+3) % 4 = (t-1) % 4 is free)
+    wait_vmcnt<3 * 2 * Fwd2Ctx<T, NW>::PIECES / 2>();
+    __builtin_amdgcn_s_barrier();  // bare: __syncthreads' release fence would drain all LDS-DMA
+    const int tn = t + 3 < c.nt ? t + 3 : c.nt - 1;
+    fwd2_issue<T, NW>(c, tn, (Q + 3) & 3);
+    s_tile<T>(sn, Ks + ((Q + 1) % 4) * 8192, c.qf, c.negm, c.l32, c.h);
+    float rsp[4];
+    exp_tile(sc, rsp);
+    const float tot = (rsp[0] + rsp[1]) + (rsp[2] + rsp[3]);
+    if (__any(!(tot <= LIM))) {  // rare: move the reference to the tile's row max and redo P(t)
+        f32x16 sr[2];
+        s_tile<T>(sr, Ks + Q * 8192, c.qf, c.negm, c.l32, c.h);
+        const float shift = fmaxf(tile_rowmax2(sr), 0.f);
+        const float alpha = __builtin_amdgcn_exp2f(-shift);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c.l4[j] *= alpha;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) c.o[db][r] *= alpha;
+        c.m += shift;
+        c.negm = splat16(-c.m);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                sn[kb][r] -= shift;
+                sc[kb][r] = sr[kb][r] - shift;
+            }
+        exp_tile(sc, rsp);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c.l4[j] += rsp[j];
+    const char* Vt = Vs + Q * 8192;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+        frag vf[2][2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int db = 0; db < 2; ++db) vf[s][db] = tr_frag<T>(Vt, kb, s, db, c.lane);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const frag pf = pack_frag<T>(sc[kb], s);
+#pragma unroll
+            for (int db = 0; db < 2; ++db) c.o[db] = Mfma<T>::mma(vf[s][db], pf, c.o[db]);
+        }
+    }
+}
+
+// 16-B stores of one output row held as the O^T accumulator layout (T21): lane h of a row
+// holds columns 8G + 4h .. 8G + 4h + 3 of every 8-column group G; one permlane32 swap per
+// dword pairs groups (G, G+1) into 16 contiguous bytes per lane.
+template <typename T>
+__device__ __forceinline__ void store_row_t21(T* row, const f32x16 (&acc)[2], float scale, int h) {
+    typedef T t2 __attribute__((ext_vector_type(2)));
+    unsigned w[8][2];  // group G = 4 db + g: two dwords (columns +0..1, +2..3 of this lane's half)
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const t2 p = {(T)(acc[db][4 * g + 2 * j] * scale), (T)(acc[db][4 * g + 2 * j + 1] * scale)};
+                w[4 * db + g][j] = __builtin_bit_cast(unsigned, p);
+            }
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int G = 0; G < 8; G += 2) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const auto r = __builtin_amdgcn_permlane32_swap(w[G][j], w[G + 1][j], false, false);
+            w[G][j] = r[0];
+            w[G + 1][j] = r[1];
+        }
+        const u32x4 v = {w[G][0], w[G][1], w[G + 1][0], w[G + 1][1]};
+        *(u32x4*)((char*)row + 16 * G + 16 * h) = v;
+    }
+}
+
+template <typename T, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd2_kernel(const T* __restrict__ qkv, T* __restrict__ out,
+                                                                    float* __restrict__ lse, int N, int H) {
+    constexpr int QB = 32 * NW;
+    typedef typename Mfma<T>::frag frag;
+    __shared__ __attribute__((aligned(16))) char smem[8 * 8192];
+    Fwd2Ctx<T, NW> c;
+    c.smem = smem;
+    c.lane = threadIdx.x & 63;
+    c.wave = threadIdx.x >> 6;
+    c.h = c.lane >> 5;
+    c.l32 = c.lane & 31;
+    const int nq = (N - 1) / QB;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int qblk = tile % nq, bh = tile / nq, b = bh / H, hd = bh % H;
+    const int C = H * HD;
+    const int64_t ld = 3 * (int64_t)C;
+    const T* Bb = qkv + (int64_t)b * N * ld;  // this batch's rows
+    c.ldb = (uint32_t)(ld * sizeof(T));
+    c.nt = (N - 1) / 64;
+    // queries first: their register loads must not queue behind the DMA in vmcnt order
+    const int q = 1 + qblk * QB + c.wave * 32 + c.l32;
+    const T* Qrow = Bb + (int64_t)q * ld + hd * HD;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) c.qf[s] = *(const frag*)(Qrow + (2 * s + c.h) * 8);
+    const T* K0 = Bb + C + hd * HD;  // key 0 (CLS)
+    const T* V0 = Bb + 2 * C + hd * HD;
+    frag k0[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) k0[s] = *(const frag*)(K0 + (2 * s + c.h) * 8);
+    typedef T t4 __attribute__((ext_vector_type(4)));
+    t4 v0[2][4];
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) v0[db][g] = *(const t4*)(V0 + db * 32 + 8 * g + 4 * c.h);
+
+    c.rs = make_rsrc(Bb, (uint32_t)N * c.ldb);
+#pragma unroll
+    for (int i = 0; i < Fwd2Ctx<T, NW>::PIECES; ++i) {  // lane -> (row, physical chunk) of its piece
+        const int r = (c.wave + i * NW) * 8 + (c.lane >> 3);
+        const uint32_t base = (uint32_t)r * c.ldb + (uint32_t)(((c.lane & 7) ^ xsw(r)) * 16);
+        c.voffK[i] = base + (uint32_t)((C + hd * HD) * sizeof(T));
+        c.voffV[i] = base + (uint32_t)((2 * C + hd * HD) * sizeof(T));
+    }
+    fwd2_issue<T, NW>(c, 0, 0);
+    fwd2_issue<T, NW>(c, c.nt > 1 ? 1 : 0, 1);
+    fwd2_issue<T, NW>(c, c.nt > 2 ? 2 : c.nt - 1, 2);
+
+    // key 0 on the VALU while the tiles fly: s0 = q . k0 (each half-wave holds half the dims)
+    float part = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) part += (float)c.qf[s][j] * (float)k0[s][j];
+    const float s0 = xhalf_sum(part);
+
+    wait_vmcnt<2 * 2 * Fwd2Ctx<T, NW>::PIECES>();  // tile 0 has landed (tiles 1, 2 in flight)
+    __builtin_amdgcn_s_barrier();
+    f32x16 sA[2], sB[2];
+    s_tile<T>(sA, smem, c.qf, zero16(), c.l32, c.h);
+    c.m = fmaxf(tile_rowmax2(sA), s0);
+    c.negm = splat16(-c.m);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sA[kb][r] -= c.m;
+    const float p0 = __builtin_amdgcn_exp2f(s0 - c.m);
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) c.o[db][4 * g + e] = p0 * (float)v0[db][g][e];
+    c.l4[0] = c.h == 0 ? p0 : 0.f;
+    c.l4[1] = c.l4[2] = c.l4[3] = 0.f;
+    if (c.wave >= NW / 2) __builtin_amdgcn_s_setprio(1);  // static priority for the younger half
+
+    int t = 0;
+    while (true) {  // unrolled by four: ring slots are immediates
+        if (t >= c.nt) break;
+        fwd2_step<T, NW, 0>(c, t++, sA, sB);
+        if (t >= c.nt) break;
+        fwd2_step<T, NW, 1>(c, t++, sB, sA);
+        if (t >= c.nt) break;
+        fwd2_step<T, NW, 2>(c, t++, sA, sB);
+        if (t >= c.nt) break;
+        fwd2_step<T, NW, 3>(c, t++, sB, sA);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    wait_vmcnt<0>();  // no LDS-DMA may still be landing when the workgroup retires
+
+    const float lt = xhalf_sum((c.l4[0] + c.l4[1]) + (c.l4[2] + c.l4[3]));
+    store_row_t21<T>(out + ((int64_t)b * N + q) * C + hd * HD, c.o, 1.0f / lt, c.h);
+    if (c.h == 0) lse[(int64_t)bh * N + q] = c.m + __log2f(lt);
+}
+
+// ---------------------------------------------------------------------------- pipelined variant
+// Same CLS split, staging and reference check as attn_fwd2_kernel, software-pipelined one
+// tile further: the PV product of tile t-1 is deferred into step t, so one step is a single
+// basic block (the rare re-reference branch aside) whose MFMAs — PV(t-1) and S(t+1) — need
+// nothing from the step's VALU work — exp / row sums / packing of P(t) — and the compiler
+// can fill the MFMA gaps from it.  V runs two tiles ahead (its slot must survive the step
+// after the tile's softmax), K three.
+//   NW waves x NB 32-row blocks per wave, 32 * NW * NB = 256 rows per workgroup:
+//   * NW = 8, NB = 1: two waves per SIMD; S(t+1) goes to the second register set (sc / sn
+//     alternate), so its MFMAs also overlap the exp of P(t);
+//   * NW = 4, NB = 2: one wave per SIMD with 64 rows: each K / V^T fragment read from LDS
+//     feeds two MFMAs (half the LDS traffic per FLOP); S(t+1) reuses P(t)'s registers.
+template <typename T, int NW, int NB>
+struct Fwd3Ctx {
+    typedef typename Mfma<T>::frag frag;
+    static constexpr int PIECES = 8 / NW;  // 1-KiB pieces of a 64-row tile per wave
+    char* smem;  // K ring [4][8 KiB] | V ring [4][8 KiB]
+    rsrc_t rs;
+    uint32_t voffK[PIECES], voffV[PIECES];
+    uint32_t ldb;
+    int nt, l32, h, lane, wave;
+    frag qf[NB][4];
+    f32x16 o[NB][2];
+    f32x16 negm[NB];
+    float m[NB];
+    float l4[NB][4];
+};
+
+template <typename T, int NW, int NB>
+__device__ __forceinline__ void fwd3_issue(Fwd3Ctx<T, NW, NB>& c, int t, int slot, int vbase) {
+#if defined(__HIP_DEVICE_COMPILE__)  // the LDS-DMA builtin has no host-pass declaration
+    const uint32_t soff = (uint32_t)(1 + 64 * t) * c.ldb;
+#pragma unroll
+    for (int i = 0; i < Fwd3Ctx<T, NW, NB>::PIECES; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rs, LDS_PTR(c.smem + vbase + slot * 8192 + (c.wave + NW * i) * 1024),
+                                                 16, vbase ? c.voffV[i] : c.voffK[i], soff, 0, 0);
+#endif
+}
+
+// packed 16-bit P fragments of one 32-row block: [kb][s]
+template <typename T>
+struct PPack {
+    typename Mfma<T>::frag f[2][2];
+};
+
+template <typename T>
+__device__ __forceinline__ void pack_tile(PPack<T>& pp, const f32x16 (&p)[2]) {
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) pp.f[kb][s] = pack_frag<T>(p[kb], s);
+}
+
+// O += P V for the V tile image at Vt (both blocks share each V^T fragment)
+template <typename T, int NW, int NB>
+__device__ __forceinline__ void fwd3_pv(Fwd3Ctx<T, NW, NB>& c, const char* Vt, const PPack<T> (&pp)[NB]) {
+    typedef typename Mfma<T>::frag frag;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+        frag vf[2][2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int db = 0; db < 2; ++db) vf[s][db] = tr_frag<T>(Vt, kb, s, db, c.lane);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int db = 0; db < 2; ++db)
+#pragma unroll
+                for (int b = 0; b < NB; ++b) c.o[b][db] = Mfma<T>::mma(vf[s][db], pp[b].f[kb][s], c.o[b][db]);
+    }
+}
+
+// step t (slot Q = t % 4).  On entry sc[b] = S(t) - m of block b and pp[b] = packed P(t-1);
+// on exit sn[b] = S(t+1) - m and pp[b] = packed P(t).  sn may be sc itself (NB = 2).
+template <typename T, int NW, int NB, int Q>
+__device__ __forceinline__ void fwd3_step(Fwd3Ctx<T, NW, NB>& c, int t, f32x16 (&sc)[NB][2], f32x16 (&sn)[NB][2],
+                                          PPack<T> (&pp)[NB]) {
+    typedef typename Mfma<T>::frag frag;
+    constexpr int PIECES = Fwd3Ctx<T, NW, NB>::PIECES;
+    constexpr float LIM = 4096.0f;
+    const char* Ks = c.smem;
+    const char* Vs = c.smem + 4 * 8192;
+    // own pieces of K(t+1) (and V(t-1)) landed (V(t+1), tile t+2 stay in flight), then a bare
+    // barrier: everyone's pieces landed and everyone's reads of step t-1 are consumed.  (Not
+    // __syncthreads: its release fence drains every LDS-DMA in flight.)
+    wait_vmcnt<3 * PIECES>();
+    __builtin_amdgcn_s_barrier();
+    fwd3_issue<T, NW, NB>(c, t + 3 < c.nt ? t + 3 : c.nt - 1, (Q + 3) & 3, 0);
+    fwd3_issue<T, NW, NB>(c, t + 2 < c.nt ? t + 2 : c.nt - 1, (Q + 2) & 3, 4 * 8192);
+    const char* Kt = Ks + ((Q + 1) & 3) * 8192;
+    frag kf[2][4];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) kf[kb][s] = row_frag<T>(Kt, kb * 32 + c.l32, 2 * s + c.h);
+    fwd3_pv<T, NW, NB>(c, Vs + ((Q + 3) & 3) * 8192, pp);  // PV(t-1)
+    // P(t) = exp2(S(t) - m) in place and packed (pp's P(t-1) has gone into the MFMAs above),
+    // block by block, each followed by its S(t+1) chains (each K fragment feeds every block)
+    float rsp[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        exp_tile(sc[b], rsp[b]);
+        pack_tile<T>(pp[b], sc[b]);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            sn[b][kb] = Mfma<T>::mma(kf[kb][0], c.qf[b][0], c.negm[b]);
+#pragma unroll
+            for (int s = 1; s < 4; ++s) sn[b][kb] = Mfma<T>::mma(kf[kb][s], c.qf[b][s], sn[b][kb]);
+        }
+    }
+    bool fire = false;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) fire = fire || !(((rsp[b][0] + rsp[b][1]) + (rsp[b][2] + rsp[b][3])) <= LIM);
+    if (__any(fire)) {  // rare: re-reference every block on tile t (S(t) recomputed from K(t))
+        const char* K0t = Ks + Q * 8192;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) kf[kb][s] = row_frag<T>(K0t, kb * 32 + c.l32, 2 * s + c.h);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            f32x16 p[2];
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) {
+                p[kb] = Mfma<T>::mma(kf[kb][0], c.qf[b][0], c.negm[b]);
+#pragma unroll
+                for (int s = 1; s < 4; ++s) p[kb] = Mfma<T>::mma(kf[kb][s], c.qf[b][s], p[kb]);
+            }
+            const float shift = fmaxf(tile_rowmax2(p), 0.f);
+            const float alpha = __builtin_amdgcn_exp2f(-shift);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) c.l4[b][j] *= alpha;
+#pragma unroll
+            for (int db = 0; db < 2; ++db)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) c.o[b][db][r] *= alpha;
+            c.m[b] += shift;
+            c.negm[b] = splat16(-c.m[b]);
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    sn[b][kb][r] -= shift;
+                    p[kb][r] -= shift;
+                }
+            exp_tile(p, rsp[b]);
+            pack_tile<T>(pp[b], p);
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c.l4[b][j] += rsp[b][j];
+}
+
+template <typename T, int NW, int NB>
+__global__ __launch_bounds__(64 * NW, NB == 2 ? 1 : 8 / NW) void attn_fwd3_kernel(const T* __restrict__ qkv, T* __restrict__ out,
+                                                                    float* __restrict__ lse, int N, int H) {
+    static_assert(NW * NB == 8, "256 rows per workgroup");
+    typedef typename Mfma<T>::frag frag;
+    constexpr int PIECES = Fwd3Ctx<T, NW, NB>::PIECES;
+    __shared__ __attribute__((aligned(16))) char smem[8 * 8192];
+    Fwd3Ctx<T, NW, NB> c;
+    c.smem = smem;
+    c.lane = threadIdx.x & 63;
+    c.wave = threadIdx.x >> 6;
+    c.h = c.lane >> 5;
+    c.l32 = c.lane & 31;
+    const int nq = (N - 1) / 256;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int qblk = tile % nq, bh = tile / nq, b = bh / H, hd = bh % H;
+    const int C = H * HD;
+    const int64_t ld = 3 * (int64_t)C;
+    const T* Bb = qkv + (int64_t)b * N * ld;
+    c.ldb = (uint32_t)(ld * sizeof(T));
+    c.nt = (N - 1) / 64;
+    // queries first: their register loads must not queue behind the DMA in vmcnt order
+    const int q0 = 1 + qblk * 256 + c.wave * 32 * NB + c.l32;  // block bb: q0 + 32 bb
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb) {
+        const T* Qrow = Bb + (int64_t)(q0 + 32 * bb) * ld + hd * HD;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) c.qf[bb][s] = *(const frag*)(Qrow + (2 * s + c.h) * 8);
+    }
+    const T* K0 = Bb + C + hd * HD;  // key 0 (CLS)
+    const T* V0 = Bb + 2 * C + hd * HD;
+    frag k0[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) k0[s] = *(const frag*)(K0 + (2 * s + c.h) * 8);
+    typedef T t4 __attribute__((ext_vector_type(4)));
+    t4 v0[2][4];
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) v0[db][g] = *(const t4*)(V0 + db * 32 + 8 * g + 4 * c.h);
+
+    c.rs = make_rsrc(Bb, (uint32_t)N * c.ldb);
+#pragma unroll
+    for (int i = 0; i < PIECES; ++i) {  // lane -> (row, physical chunk) of its piece
+        const int r = (c.wave + NW * i) * 8 + (c.lane >> 3);
+        const uint32_t base = (uint32_t)r * c.ldb + (uint32_t)(((c.lane & 7) ^ xsw(r)) * 16);
+        c.voffK[i] = base + (uint32_t)((C + hd * HD) * sizeof(T));
+        c.voffV[i] = base + (uint32_t)((2 * C + hd * HD) * sizeof(T));
+    }
+    const int t1 = c.nt > 1 ? 1 : 0, t2 = c.nt > 2 ? 2 : c.nt - 1;
+    fwd3_issue<T, NW, NB>(c, 0, 0, 0);          // K(0)
+    fwd3_issue<T, NW, NB>(c, 0, 3, 4 * 8192);   // "V(-1)": any finite tile (PV(-1) multiplies it by P = 0)
+    fwd3_issue<T, NW, NB>(c, t1, 1, 0);         // K(1)
+    fwd3_issue<T, NW, NB>(c, 0, 0, 4 * 8192);   // V(0)
+    fwd3_issue<T, NW, NB>(c, t2, 2, 0);         // K(2)
+    fwd3_issue<T, NW, NB>(c, t1, 1, 4 * 8192);  // V(1)
+
+    // key 0 on the VALU while the tiles fly: s0 = q . k0 (each half-wave holds half the dims)
+    float s0[NB];
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb) {
+        float part = 0.f;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) part += (float)c.qf[bb][s][j] * (float)k0[s][j];
+        s0[bb] = xhalf_sum(part);
+    }
+    wait_vmcnt<5 * PIECES>();  // K(0) landed
+    __builtin_amdgcn_s_barrier();
+    f32x16 sA[NB][2], sB[NB][2];
+    PPack<T> pp[NB];
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb) {
+        s_tile<T>(sA[bb], smem, c.qf[bb], zero16(), c.l32, c.h);
+        c.m[bb] = fmaxf(tile_rowmax2(sA[bb]), s0[bb]);
+        c.negm[bb] = splat16(-c.m[bb]);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sA[bb][kb][r] -= c.m[bb];
+        const float p0 = __builtin_amdgcn_exp2f(s0[bb] - c.m[bb]);
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) c.o[bb][db][4 * g + e] = p0 * (float)v0[db][g][e];
+        c.l4[bb][0] = c.h == 0 ? p0 : 0.f;
+        c.l4[bb][1] = c.l4[bb][2] = c.l4[bb][3] = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) pp[bb].f[kb][s] = pack_frag<T>(zero16(), s);  // P(-1) = 0
+    }
+    if (NW == 8 && c.wave >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the younger half
+
+    int t = 0;
+    if constexpr (NB == 1) {  // two register sets alternate
+        while (true) {
+            if (t >= c.nt) break;
+            fwd3_step<T, NW, NB, 0>(c, t++, sA, sB, pp);
+            if (t >= c.nt) break;
+            fwd3_step<T, NW, NB, 1>(c, t++, sB, sA, pp);
+            if (t >= c.nt) break;
+            fwd3_step<T, NW, NB, 2>(c, t++, sA, sB, pp);
+            if (t >= c.nt) break;
+            fwd3_step<T, NW, NB, 3>(c, t++, sB, sA, pp);
+        }
+    } else {  // S(t+1) reuses P(t)'s registers
+        while (true) {
+            if (t >= c.nt) break;
+            fwd3_step<T, NW, NB, 0>(c, t++, sA, sA, pp);
+            if (t >= c.nt) break;
+            fwd3_step<T, NW, NB, 1>(c, t++, sA, sA, pp);
+            if (t >= c.nt) break;
+            fwd3_step<T, NW, NB, 2>(c, t++, sA, sA, pp);
+            if (t >= c.nt) break;
+            fwd3_step<T, NW, NB, 3>(c, t++, sA, sA, pp);
+        }
+    }
+    __builtin_amdgcn_s_setprio(0);
+    // the deferred PV of the last tile (nt - 1)
+    wait_vmcnt<0>();
+    __syncthreads();
+    fwd3_pv<T, NW, NB>(c, smem + 4 * 8192 + ((c.nt - 1) & 3) * 8192, pp);
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb) {
+        const float lt = xhalf_sum((c.l4[bb][0] + c.l4[bb][1]) + (c.l4[bb][2] + c.l4[bb][3]));
+        const int q = q0 + 32 * bb;
+        store_row_t21<T>(out + ((int64_t)b * N + q) * C + hd * HD, c.o[bb], 1.0f / lt, c.h);
+        if (c.h == 0) lse[(int64_t)bh * N + q] = c.m[bb] + __log2f(lt);
+    }
+}
+
+// query 0 (CLS) against one 64-key tile per wave: partial (max, sum, o[64]) for the merge.
+// Partials of (b, h, split) live at o + b*N*C + C (row 1 of batch b, overwritten later by the
+// main pass), (h * nsplit + split) * 66 floats.
+template <typename T>
+__global__ __launch_bounds__(64) void attn_row0_part_kernel(const T* __restrict__ qkv, T* __restrict__ out, int N,
+                                                            int H, int nsplit) {
+    const int lane = threadIdx.x;
+    const int sp = blockIdx.x % nsplit, bh = blockIdx.x / nsplit, b = bh / H, hd = bh % H;
+    const int C = H * HD;
+    const int64_t ld = 3 * (int64_t)C;
+    const T* Bb = qkv + (int64_t)b * N * ld;
+    const int key = sp * 64 + lane;
+    const int kc = key < N ? key : N - 1;
+    typedef T t8 __attribute__((ext_vector_type(8)));
+    const T* q0 = Bb + hd * HD;
+    const T* kr = Bb + (int64_t)kc * ld + C + hd * HD;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const t8 qa = *(const t8*)(q0 + 8 * i);
+        const t8 ka = *(const t8*)(kr + 8 * i);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += (float)qa[j] * (float)ka[j];
+    }
+    if (key >= N) s = -INFINITY;
+    const float mt = wave_max(s);
+    const float p = __builtin_amdgcn_exp2f(s - mt);
+    const float lt = wave_sum(p);
+    // o[d = lane] = sum_k p_k V[k][d]
+    const int nk = min(64, N - sp * 64);
+    const T* vcol = Bb + (int64_t)(sp * 64) * ld + 2 * C + hd * HD + lane;
+    float o = 0.f;
+    for (int k = 0; k < nk; ++k) o += __shfl(p, k, 64) * (float)vcol[(int64_t)k * ld];
+    float* ws = (float*)(out + (int64_t)b * N * C + C) + (int64_t)(hd * nsplit + sp) * 66;
+    ws[2 + lane] = o;
+    if (lane == 0) {
+        ws[0] = mt;
+        ws[1] = lt;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void attn_row0_merge_kernel(T* __restrict__ out, float* __restrict__ lse, int N,
+                                                             int H, int nsplit) {
+    const int lane = threadIdx.x;
+    const int bh = blockIdx.x, b = bh / H, hd = bh % H;
+    const int C = H * HD;
+    const float* ws = (const float*)(out + (int64_t)b * N * C + C) + (int64_t)hd * nsplit * 66;
+    float M = -INFINITY;
+    for (int s = 0; s < nsplit; ++s) M = fmaxf(M, ws[s * 66]);
+    float L = 0.f, O = 0.f;
+    for (int s = 0; s < nsplit; ++s) {
+        const float w = __builtin_amdgcn_exp2f(ws[s * 66] - M);
+        L += w * ws[s * 66 + 1];
+        O += w * ws[s * 66 + 2 + lane];
+    }
+    __syncthreads();  // all lanes have read the partials before row 0 is written (row 0 != partial rows)
+    out[(int64_t)b * N * C + hd * HD + lane] = (T)(O / L);
+    if (lane == 0) lse[(int64_t)bh * N] = M + __log2f(L);
 }
 
 // ============================================================================ backward
@@ -712,9 +1339,41 @@ void fwd_launch_nw(const void* qkv, void* o, float* lse, int B, int N, int H, hi
     attn_fwd_kernel<T, NW><<<grid, 64 * NW, 0, st>>>((const T*)qkv, (T*)o, lse, N, H);
 }
 
+// CLS-split path (attn_fwd2_kernel) when N - 1 is a multiple of the query block
+template <typename T, int NW>
+bool fwd2_launch_nw(const void* qkv, void* o, float* lse, int B, int N, int H, hipStream_t st) {
+    constexpr int QB = 32 * NW;
+    if (N < 1 + QB || (N - 1) % QB != 0) return false;
+    const int nsplit = (N + 63) / 64;
+    attn_row0_part_kernel<T><<<B * H * nsplit, 64, 0, st>>>((const T*)qkv, (T*)o, N, H, nsplit);
+    attn_row0_merge_kernel<T><<<B * H, 64, 0, st>>>((T*)o, lse, N, H, nsplit);
+    const dim3 grid(B * H * ((N - 1) / QB));
+    attn_fwd2_kernel<T, NW><<<grid, 64 * NW, 0, st>>>((const T*)qkv, (T*)o, lse, N, H);
+    return true;
+}
+
+// pipelined CLS-split path (attn_fwd3_kernel) when N - 1 is a multiple of 256
+template <typename T, int NW, int NB>
+bool fwd3_launch(const void* qkv, void* o, float* lse, int B, int N, int H, hipStream_t st) {
+    if (N < 257 || (N - 1) % 256 != 0) return false;
+    const int nsplit = (N + 63) / 64;
+    attn_row0_part_kernel<T><<<B * H * nsplit, 64, 0, st>>>((const T*)qkv, (T*)o, N, H, nsplit);
+    attn_row0_merge_kernel<T><<<B * H, 64, 0, st>>>((T*)o, lse, N, H, nsplit);
+    attn_fwd3_kernel<T, NW, NB><<<B * H * ((N - 1) / 256), 64 * NW, 0, st>>>((const T*)qkv, (T*)o, lse, N, H);
+    return true;
+}
+
 template <typename T>
 void fwd_launch(const void* qkv, void* o, float* lse, int B, int N, int H, hipStream_t st) {
-    if (dclip_option(DCLIP_OPT_ATTN_FWD_WAVES) == 4) fwd_launch_nw<T, 4>(qkv, o, lse, B, N, H, st);
+    const int nw = dclip_option(DCLIP_OPT_ATTN_FWD_WAVES) == 4 ? 4 : 8;
+    const int kopt = dclip_option(DCLIP_OPT_ATTN_FWD_KERNEL);
+    if (kopt == 2 && fwd3_launch<T, 4, 2>(qkv, o, lse, B, N, H, st)) return;
+    if (kopt == 3 && fwd3_launch<T, 8, 1>(qkv, o, lse, B, N, H, st)) return;
+    if (kopt != 1) {  // 0: CLS-split when the shape allows it
+        if (nw == 4 ? fwd2_launch_nw<T, 4>(qkv, o, lse, B, N, H, st) : fwd2_launch_nw<T, 8>(qkv, o, lse, B, N, H, st))
+            return;
+    }
+    if (nw == 4) fwd_launch_nw<T, 4>(qkv, o, lse, B, N, H, st);
     else fwd_launch_nw<T, 8>(qkv, o, lse, B, N, H, st);
 }
 

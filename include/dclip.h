@@ -71,6 +71,7 @@ int dclip_abi_version(void);
 #define DCLIP_OPT_GEMM_TILE 3        /* dclip_gemm tiles: 0 auto (default), 1 128x128, 2 256x256, 3 256x128, 4 256x256 k32x4 */
 #define DCLIP_OPT_GEMM_TN_TILE 4     /* dclip_gemm_tn tiles: 0 auto (default: 256x256 when M, N >= 256), 1 128x128 */
 #define DCLIP_OPT_ATTN_DKDV_QS 5     /* dK/dV pass query rows per barrier: 64 (default) or 128 */
+#define DCLIP_OPT_ATTN_FWD_KERNEL 6  /* 0 (default): CLS-split kernel when N-1 is a multiple of the query block; 1: generic */
 #define DCLIP_OPT_COUNT 8
 int dclip_set_option(int id, int value);
 

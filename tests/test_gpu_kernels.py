@@ -228,6 +228,64 @@ def test_attention_fwd_variants(attn_variant, N):
     assert rel_err(o.float(), attn_ref(qref, B, N, H)) < TOL[torch.bfloat16]
 
 
+@pytest.fixture
+def fwd_kernel(request):
+    """(kernel, waves): kernel 0 = CLS-split forward where N - 1 is a multiple of the query
+    block (else the generic kernel), 1 = always the generic kernel, 2 = the wide CLS-split
+    kernel (4 waves x 64 rows) where N - 1 is a multiple of 256."""
+    from denseclip_vit_multimodal_amd import _native as N
+    N.call("dclip_set_option", N.OPT_ATTN_FWD_KERNEL, request.param[0])
+    N.call("dclip_set_option", N.OPT_ATTN_FWD_WAVES, request.param[1])
+    yield request.param
+    N.call("dclip_set_option", N.OPT_ATTN_FWD_KERNEL, 0)
+    N.call("dclip_set_option", N.OPT_ATTN_FWD_WAVES, 0)
+
+
+@pytest.mark.parametrize("fwd_kernel", [(0, 8), (0, 4), (1, 8), (2, 0), (3, 0)], indirect=True)
+@pytest.mark.parametrize("N", [129, 257, 513, 2049])
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+def test_attention_fwd_cls_split(N, dt, fwd_kernel):
+    """N = 1 + 64k: key 0 folded in on the VALU, query 0 by the split-key row pass + merge."""
+    O = ops()
+    B, H = 3, 2
+    C = 64 * H
+    qkv, qref = prescale((torch.randn(B * N, 3 * C, device=DEV) * 1.5).to(dt), H)
+    o, lse = O.attn_fwd(qkv, B, N, H, 64 ** -0.5)
+    ref = attn_ref(qref, B, N, H)
+    assert rel_err(o.float(), ref) < TOL[dt]
+    assert rel_err(o.float().view(B, N, C)[:, 0], ref.view(B, N, C)[:, 0]) < TOL[dt]  # the CLS row
+    q, k, _ = qref.view(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    lref = torch.logsumexp((q @ k.transpose(-1, -2)) * 64 ** -0.5, -1) / math.log(2)
+    assert (lse.view(B, H, N) - lref).abs().max() < 1e-2
+
+
+@pytest.mark.parametrize("fwd_kernel", [(0, 8), (0, 4), (2, 0), (3, 0)], indirect=True)
+@pytest.mark.parametrize("where,spike", [(0, 4.0), (0, 40.0), (0, -40.0), (200, 0.8), (200, 40.0), (256, 40.0)])
+def test_attention_cls_split_spikes(where, spike, fwd_kernel):
+    """A dominating (or vanishing) key at the CLS position, inside the sweep and at its last
+    key: the prologue's key-0 fold, the deferred re-referencing and the row-0 merge."""
+    O = ops()
+    B, H, N = 1, 1, 257
+    qkv = torch.randn(B * N, 3 * 64, device=DEV) * 0.3
+    qkv[:, :64] = 1.0
+    qkv[where, 64:128] = spike
+    qkv, qref = prescale(qkv.to(torch.float16), H)
+    o, _ = O.attn_fwd(qkv, B, N, H, 64 ** -0.5)
+    assert rel_err(o.float(), attn_ref(qref, B, N, H)) < TOL[torch.float16]
+
+
+def test_attention_fwd_full_length():
+    """The benchmark's sequence length (N = 8193, CLS-split path) against fp32 torch."""
+    O = ops()
+    B, H, N = 1, 2, 8193
+    C = 64 * H
+    qkv, qref = prescale(torch.randn(B * N, 3 * C, device=DEV).to(torch.bfloat16), H)
+    o, lse = O.attn_fwd(qkv, B, N, H, 64 ** -0.5)
+    ref = attn_ref(qref, B, N, H)
+    assert rel_err(o.float(), ref) < TOL[torch.bfloat16]
+    assert rel_err(o.float()[:1], ref[:1]) < TOL[torch.bfloat16]
+
+
 @pytest.mark.parametrize("attn_variant", [(8, 4, 4), (4, 4, 4)], indirect=True)
 @pytest.mark.parametrize("spike", [0.5, 0.8, 4.0, 40.0, -40.0])
 def test_attention_spiky_rescale(spike, attn_variant):
