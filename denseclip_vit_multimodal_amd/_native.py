@@ -46,6 +46,10 @@ _SIGS = {
     "dclip_bilinear_fwd": [_c_void_p, _i32, _c_void_p, _i32, _i64, _i32, _i32, _i32, _i32, _c_void_p],
     "dclip_bilinear_bwd": [_c_void_p, _i32, _c_void_p, _c_void_p, _i64, _i32, _i32, _i32, _i32, _c_void_p],
     "dclip_cast": [_c_void_p, _i32, _c_void_p, _i32, _i64, _f32, _c_void_p],
+    "dclip_conv3x3": [_i32, _i32, _c_void_p, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _c_void_p, _i32, _c_void_p,
+                      _i32, _i64, _i32, _i32, _i32, _c_void_p],
+    "dclip_conv3x3_wgrad": [_i32, _c_void_p, _i64, _i32, _c_void_p, _i64, _i64, _i64, _i32, _i32, _i32, _i32,
+                            _c_void_p, _c_void_p, _i32, _c_void_p],
     "dclip_set_option": [_i32, _i32],
     "dclip_gemm_tn_plan": [_i64, _i64, _i64, _c_void_p, _c_void_p],
 }

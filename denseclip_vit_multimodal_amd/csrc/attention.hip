@@ -653,6 +653,15 @@ __device__ __forceinline__ void fwd3_issue(Fwd3Ctx<T, NW, NB>& c, int t, int slo
 #endif
 }
 
+// Q fragment (block b, k-step s) of this lane: registers (NB = 1) or the wave's LDS copy
+// (NB = 2: 32 fewer live VGPRs, which keeps S, P and the K / V^T fragments in arch VGPRs)
+template <typename T, int NW, int NB>
+__device__ __forceinline__ typename Mfma<T>::frag fwd3_q(const Fwd3Ctx<T, NW, NB>& c, int b, int s) {
+    if constexpr (NB == 1) return c.qf[b][s];
+    else
+        return *(const typename Mfma<T>::frag*)(c.smem + 8 * 8192 + c.wave * 8192 + ((b * 4 + s) * 64 + c.lane) * 16);
+}
+
 // packed 16-bit P fragments of one 32-row block: [kb][s]
 template <typename T>
 struct PPack {
@@ -720,9 +729,9 @@ __device__ __forceinline__ void fwd3_step(Fwd3Ctx<T, NW, NB>& c, int t, f32x16 (
         pack_tile<T>(pp[b], sc[b]);
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
-            sn[b][kb] = Mfma<T>::mma(kf[kb][0], c.qf[b][0], c.negm[b]);
+            sn[b][kb] = Mfma<T>::mma(kf[kb][0], fwd3_q(c, b, 0), c.negm[b]);
 #pragma unroll
-            for (int s = 1; s < 4; ++s) sn[b][kb] = Mfma<T>::mma(kf[kb][s], c.qf[b][s], sn[b][kb]);
+            for (int s = 1; s < 4; ++s) sn[b][kb] = Mfma<T>::mma(kf[kb][s], fwd3_q(c, b, s), sn[b][kb]);
         }
     }
     bool fire = false;
@@ -739,9 +748,9 @@ __device__ __forceinline__ void fwd3_step(Fwd3Ctx<T, NW, NB>& c, int t, f32x16 (
             f32x16 p[2];
 #pragma unroll
             for (int kb = 0; kb < 2; ++kb) {
-                p[kb] = Mfma<T>::mma(kf[kb][0], c.qf[b][0], c.negm[b]);
+                p[kb] = Mfma<T>::mma(kf[kb][0], fwd3_q(c, b, 0), c.negm[b]);
 #pragma unroll
-                for (int s = 1; s < 4; ++s) p[kb] = Mfma<T>::mma(kf[kb][s], c.qf[b][s], p[kb]);
+                for (int s = 1; s < 4; ++s) p[kb] = Mfma<T>::mma(kf[kb][s], fwd3_q(c, b, s), p[kb]);
             }
             const float shift = fmaxf(tile_rowmax2(p), 0.f);
             const float alpha = __builtin_amdgcn_exp2f(-shift);
@@ -776,7 +785,7 @@ __global__ __launch_bounds__(64 * NW, NB == 2 ? 1 : 8 / NW) void attn_fwd3_kerne
     static_assert(NW * NB == 8, "256 rows per workgroup");
     typedef typename Mfma<T>::frag frag;
     constexpr int PIECES = Fwd3Ctx<T, NW, NB>::PIECES;
-    __shared__ __attribute__((aligned(16))) char smem[8 * 8192];
+    __shared__ __attribute__((aligned(16))) char smem[8 * 8192 + (NB == 2 ? NW * 8192 : 0)];
     Fwd3Ctx<T, NW, NB> c;
     c.smem = smem;
     c.lane = threadIdx.x & 63;
@@ -840,6 +849,13 @@ __global__ __launch_bounds__(64 * NW, NB == 2 ? 1 : 8 / NW) void attn_fwd3_kerne
     }
     wait_vmcnt<5 * PIECES>();  // K(0) landed
     __builtin_amdgcn_s_barrier();
+    if constexpr (NB == 2) {  // the wave's own Q fragments to LDS (read back by the same wave only)
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb)
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+                *(frag*)(smem + 8 * 8192 + c.wave * 8192 + ((bb * 4 + s) * 64 + c.lane) * 16) = c.qf[bb][s];
+    }
     f32x16 sA[NB][2], sB[NB][2];
     PPack<T> pp[NB];
 #pragma unroll

@@ -319,7 +319,8 @@ template <typename T, int EPI, typename OutT, typename Cfg>
 __device__ __forceinline__ void big_epilogue(f32x4 (&acc)[Cfg::NB][Cfg::MB], char* smem, int M, int N, int mw, int nw,
                                              const float* __restrict__ bias, const void* __restrict__ aux,
                                              int64_t ld_aux, void* __restrict__ C, int64_t ldc, void* __restrict__ C2,
-                                             int64_t ldc2, int64_t slab, float alpha) {
+                                             int64_t ldc2, int64_t slab, float alpha, int map_hw = 0,
+                                             int map_gap = 0, int map_off = 0) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int l16 = lane & 15, lq = lane >> 4;
@@ -351,7 +352,10 @@ __device__ __forceinline__ void big_epilogue(f32x4 (&acc)[Cfg::NB][Cfg::MB], cha
                 const f32x4 b = *(const f32x4*)(ep + r * Cfg::EP_LD + c8 + 4);
                 v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
                 v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
-                epi_row8<T, EPI, OutT>(v, m, nb, N, bias, aux, ld_aux, C, ldc, C2, ldc2, slab);
+                // output row: m, or (map_hw > 0) pixel m of a channels-last image whose batches of
+                // map_hw pixels are separated by map_gap rows and start map_off rows in
+                const int row = map_hw ? m + (m / map_hw) * map_gap + map_off : m;
+                epi_row8<T, EPI, OutT>(v, row, nb, N, bias, aux, ld_aux, C, ldc, C2, ldc2, slab);
             }
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);
@@ -730,6 +734,242 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, i
     }
 }
 
+// ---------------------------------------------------------------------------- 3x3 convolution
+// Implicit-GEMM 3x3 / stride 1 / pad 1 convolution on channels-last pixel rows — the
+// ViTFeatureFusionNeck's per-level ConvBNReLU convs (reference models.py:741-745, 13-20) run
+// straight on the ViT's token-major read-out: pixel (b, y, x) of a map is the row
+//   base + b * bstride + off + (y * W + x) * ld
+// (for a token buffer: bstride = N * C, off = C (the CLS row), ld = C), so the NCHW
+// materialisation and the NHWC transposes around a library conv disappear.
+//   forward: out[m][co] = sum_{tap, ci} in[m + d(tap)][ci] w[co][tap][ci]   (M = B H W pixels)
+//   dgrad:   din[m][ci] = sum_{tap, co} dout[m - d(tap)][co] w[co][tap][ci] (the same kernel
+//            with dir = -1 and the weights re-laid out as [ci][tap][co])
+//   wgrad:   dw[co][tap][ci] = sum_m dout[m][co] in[m + d(tap)][ci]          ("TN", below)
+// d(tap) = (tap / 3 - 1, tap % 3 - 1) in (y, x); taps outside the image read a zero row.
+// A k-block of 64 channels never straddles two taps (Cin % 64 == 0).
+struct PixGeo {
+    int64_t bstride, off;  // elements
+    int ld, H, W;
+};
+
+// p = q * d + r for 0 <= p < 2^24 via a float reciprocal and one correction step each way
+__device__ __forceinline__ int fdiv(int p, int d, float inv) {
+    int q = (int)((float)p * inv);
+    const int r = p - q * d;
+    q += (r >= d) - (r < 0);
+    return q;
+}
+
+// per-lane row (pixel) coordinates of the A rows this lane stages: ROWS_INST rows
+template <int ROWS_INST, int BKT>
+struct ConvRows {
+    int64_t base[ROWS_INST];  // element offset of the pixel
+    int y[ROWS_INST], x[ROWS_INST];
+};
+
+template <typename T, int ROWS_INST, int BKT>
+__device__ __forceinline__ void conv_rows_init(ConvRows<ROWS_INST, BKT>& R, const PixGeo g, int M, int m0, int wave,
+                                               int lane) {
+    constexpr int CPR = BKT / 8;
+    const int HW = g.H * g.W;
+    const float invHW = 1.0f / (float)HW, invW = 1.0f / (float)g.W;
+#pragma unroll
+    for (int i = 0; i < ROWS_INST; ++i) {
+        const int inst = wave * ROWS_INST + i;
+        int m = m0 + inst * (64 / CPR) + lane / CPR;
+        m = m < M ? m : M - 1;
+        const int b = fdiv(m, HW, invHW);
+        const int p = m - b * HW;
+        const int y = fdiv(p, g.W, invW);
+        R.y[i] = y;
+        R.x[i] = p - y * g.W;
+        R.base[i] = (int64_t)b * g.bstride + g.off + (int64_t)p * g.ld;
+    }
+}
+
+template <typename T, int ROWS_INST, int BKT>
+__device__ __forceinline__ void stage_conv_rows(const T* __restrict__ X, const T* __restrict__ zero,
+                                                const ConvRows<ROWS_INST, BKT>& R, const PixGeo g, int Cin, int dir,
+                                                int k0, char* lds, int wave, int lane) {
+    constexpr int CPR = BKT / 8;
+    const int tap = k0 / Cin, ci = k0 - tap * Cin;  // wave-uniform
+    const int dy = (tap / 3 - 1) * dir, dx = (tap % 3 - 1) * dir;
+    const int64_t shift = ((int64_t)dy * g.W + dx) * g.ld + ci;
+#pragma unroll
+    for (int i = 0; i < ROWS_INST; ++i) {
+        const int inst = wave * ROWS_INST + i;
+        const int r = inst * (64 / CPR) + lane / CPR;
+        const int c = (lane % CPR) ^ big_sw<BKT>(r);
+        const int yy = R.y[i] + dy, xx = R.x[i] + dx;
+        const bool ok = yy >= 0 && yy < g.H && xx >= 0 && xx < g.W;
+        const T* src = ok ? X + R.base[i] + shift + c * 8 : zero + c * 8;
+        __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(lds + inst * 1024), 16, 0, 0);
+    }
+}
+
+// out (row-mapped, see big_epilogue) = implicit-GEMM conv; B: weights [Nout][9 * Cin] in (tap, ci) order
+template <typename T, int EPI, typename OutT, int BM, int BN, int WM, int WN, int STAGES>
+__global__ __launch_bounds__(64 * WM * WN, 1) void conv_nt_kernel(
+    const T* __restrict__ X, const T* __restrict__ zero, PixGeo g, int Cin, int dir, const T* __restrict__ Bw,
+    int64_t ldb, int M, int N, int tiles_m, int tiles_n, const void* __restrict__ aux, int64_t ld_aux,
+    void* __restrict__ C, int64_t ldc, int map_hw, int map_gap, int map_off) {
+    constexpr int BKT = 64;
+    typedef BigCfg<BM, BN, WM, WN, STAGES, BKT> Cfg;
+    typedef typename Mfma<T>::frag frag;
+    __shared__ __attribute__((aligned(16))) char smem[Cfg::SMEM];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int l16 = lane & 15, lq = lane >> 4;
+
+    const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+    const int m0 = (t / tiles_n) * BM;
+    const int n0 = (t % tiles_n) * BN;
+    const int nk = 9 * Cin / BKT;
+
+    ConvRows<Cfg::A_INST, BKT> R;
+    conv_rows_init<T, Cfg::A_INST, BKT>(R, g, M, m0, wave, lane);
+    f32x4 acc[Cfg::NB][Cfg::MB];
+#pragma unroll
+    for (int i = 0; i < Cfg::NB; ++i)
+#pragma unroll
+        for (int j = 0; j < Cfg::MB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto stage = [&](int kt, int slot) {
+        char* base = smem + slot * Cfg::STAGE_BYTES;
+        stage_conv_rows<T, Cfg::A_INST, BKT>(X, zero, R, g, Cin, dir, kt * BKT, base, wave, lane);
+        stage_rows<T, Cfg::B_INST, BKT>(Bw, ldb, n0, N, kt * BKT, base + Cfg::A_BYTES, wave, lane);
+    };
+#pragma unroll
+    for (int s = 0; s < STAGES - 1; ++s)
+        if (s < nk) stage(s, s);
+    for (int kt = 0; kt < nk; ++kt) {
+        if (kt + STAGES - 2 <= nk - 1) wait_vmcnt<Cfg::G * (STAGES - 2)>();
+        else wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (kt + STAGES - 1 < nk) stage(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+        const char* At = smem + (kt % STAGES) * Cfg::STAGE_BYTES;
+        const char* Bt = At + Cfg::A_BYTES;
+#pragma unroll
+        for (int ks = 0; ks < BKT / 32; ++ks) {
+            frag fb[Cfg::NB], fa[Cfg::MB];
+            const int ch = ks * 4 + lq;
+#pragma unroll
+            for (int i = 0; i < Cfg::NB; ++i) fb[i] = big_frag<T, BKT>(Bt, wn * Cfg::WTN + i * 16 + l16, ch);
+#pragma unroll
+            for (int j = 0; j < Cfg::MB; ++j) fa[j] = big_frag<T, BKT>(At, wm * Cfg::WTM + j * 16 + l16, ch);
+#pragma unroll
+            for (int j = 0; j < Cfg::MB; ++j)
+#pragma unroll
+                for (int i = 0; i < Cfg::NB; ++i) acc[i][j] = Mfma16<T>::mma(fb[i], fa[j], acc[i][j]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    big_epilogue<T, EPI, OutT, Cfg>(acc, smem, M, N, m0 + wm * Cfg::WTM, n0 + wn * Cfg::WTN, nullptr, aux, ld_aux, C,
+                                     ldc, nullptr, 0, 0, 1.0f, map_hw, map_gap, map_off);
+}
+
+// wgrad: dw[n = tap * Cin + ci][co]^T ... computed as C[m = co][n] = sum_p dout[p][co] * in[p + d(tap)][ci]
+// with the 128 x 128 "TN" tile (both operands staged as 64 pixel rows x 128 columns; the B
+// rows of a tile are the input pixels shifted by the tile's tap, zero rows outside the image).
+template <typename T>
+__device__ __forceinline__ void stage_tile_tn_conv(const T* __restrict__ X, const T* __restrict__ zero, const PixGeo g,
+                                                   int tap, int ci0, int k0, int krows, char* lds_tile, int wave,
+                                                   int lane) {
+    const int HW = g.H * g.W;
+    const float invHW = 1.0f / (float)HW, invW = 1.0f / (float)g.W;
+    const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int inst = wave * 4 + i;
+        const int r = inst * 4 + (lane >> 4);
+        const int pc = lane & 15;
+        const int c = pc ^ ((r & 3) << 2);
+        int m = k0 + r;
+        const bool in_k = m < krows;
+        m = in_k ? m : krows - 1;
+        const int b = fdiv(m, HW, invHW);
+        const int p = m - b * HW;
+        const int y = fdiv(p, g.W, invW);
+        const int yy = y + dy, xx = p - y * g.W + dx;
+        const bool ok = in_k && yy >= 0 && yy < g.H && xx >= 0 && xx < g.W;
+        const T* src = ok ? X + (int64_t)b * g.bstride + g.off + ((int64_t)yy * g.W + xx) * g.ld + ci0 + c * 8
+                          : zero + (c & 7) * 8;
+        __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(lds_tile + inst * 1024), 16, 0, 0);
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const T* __restrict__ dY, int64_t ldy,
+                                                            const T* __restrict__ X, const T* __restrict__ zero,
+                                                            PixGeo g, int Cin, int M, int N, int Kpix, int k_chunk,
+                                                            int tiles_m, int tiles_n, float* __restrict__ C,
+                                                            int64_t slab) {
+    __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+    const int m0 = (t / tiles_n) * BM;
+    const int n0 = (t % tiles_n) * BN;
+    const int tap = n0 / Cin, ci0 = n0 - tap * Cin;  // a tile's 128 columns lie in one tap
+    const int kbeg = blockIdx.y * k_chunk;
+    int nk = k_chunk / BK;
+    if (kbeg + nk * BK > Kpix) nk = (Kpix - kbeg + BK - 1) / BK;
+    nk = nk < 0 ? 0 : nk;
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    if (nk > 0) {
+        stage_tile_tn<T>(dY, ldy, kbeg, Kpix, m0, M, smem, wave, lane);
+        stage_tile_tn_conv<T>(X, zero, g, tap, ci0, kbeg, Kpix, smem + TILE_BYTES, wave, lane);
+    }
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        const char* At = smem + cur * STAGE_BYTES;
+        const char* Bt = At + TILE_BYTES;
+        const int k0 = kbeg + kt * BK;
+        if (kt + 1 < nk) {
+            char* nxt = smem + (cur ^ 1) * STAGE_BYTES;
+            stage_tile_tn<T>(dY, ldy, k0 + BK, Kpix, m0, M, nxt, wave, lane);
+            stage_tile_tn_conv<T>(X, zero, g, tap, ci0, k0 + BK, Kpix, nxt + TILE_BYTES, wave, lane);
+        }
+        // pixel rows past Kpix: the B rows are zero, so the clamped A duplicates add nothing
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            typename Mfma<T>::frag fa[2], fb[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) fa[i] = tr_frag_tn<T>(Bt, s, wn * 64 + i * 32, lane);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) fb[j] = tr_frag_tn<T>(At, s, wm * 64 + j * 32, lane);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[i][j] = Mfma<T>::mma(fa[i], fb[j], acc[i][j]);
+        }
+        __syncthreads();
+    }
+    gemm_epilogue<T, DCLIP_EPI_SPLITK, float>(acc, smem, M, N, m0, n0, nullptr, nullptr, 0, C, N, nullptr, 0, slab,
+                                               1.0f);
+}
+
+// 256 bytes of zeros in device memory: the source of every out-of-image tap
+const void* conv_zero_row() {
+    static void* z = nullptr;
+    if (!z) {
+        if (hipMalloc(&z, 256) != hipSuccess) return nullptr;
+        if (hipMemset(z, 0, 256) != hipSuccess) return nullptr;
+    }
+    return z;
+}
+
 template <typename T, int EPI, typename OutT, int TBM, int TBN, int WM, int WN, int STAGES, int BKT = 64>
 void launch_big(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
                 int splits, float alpha, const float* bias, const void* aux, int64_t ld_aux, void* C, int64_t ldc,
@@ -951,6 +1191,82 @@ extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda
     }
 #undef TN_LAUNCH
 #undef TN_BIG
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
+
+// ---------------------------------------------------------------------------- conv ABI
+extern "C" int dclip_conv3x3(int mode, int ab_dt, const void* X, int64_t x_bstride, int64_t x_off, int64_t x_ld,
+                             int B, int H, int W, int Cin, const void* Wt, int Nout, void* out, int out_dt,
+                             int64_t out_ld, int out_gap, int out_off, int accumulate, void* stream) {
+    DCLIP_HOST_CHECK(ab_dt == DCLIP_BF16 || ab_dt == DCLIP_F16, "dclip_conv3x3: operands must be f16/bf16");
+    DCLIP_HOST_CHECK(mode == 0 || mode == 1, "dclip_conv3x3: mode 0 (forward) or 1 (input gradient)");
+    DCLIP_HOST_CHECK(B > 0 && H > 0 && W > 0 && Cin > 0 && Nout > 0 && Cin % 64 == 0 && Nout % 8 == 0,
+                     "dclip_conv3x3: Cin %% 64 == 0 and Nout %% 8 == 0 required (Cin=%d Nout=%d)", Cin, Nout);
+    DCLIP_HOST_CHECK((int64_t)B * H * W < (1ll << 24), "dclip_conv3x3: too many pixels");
+    DCLIP_HOST_CHECK(x_ld % 8 == 0 && x_bstride % 8 == 0 && x_off % 8 == 0 && x_ld >= Cin,
+                     "dclip_conv3x3: input strides must be multiples of 8 elements");
+    DCLIP_HOST_CHECK(((uintptr_t)X % 16) == 0 && ((uintptr_t)Wt % 16) == 0, "dclip_conv3x3: unaligned operands");
+    DCLIP_HOST_CHECK(out_dt == ab_dt || out_dt == DCLIP_F32, "dclip_conv3x3: output must be f32 or the operand dtype");
+    DCLIP_HOST_CHECK(!accumulate || out_dt == DCLIP_F32, "dclip_conv3x3: accumulate needs an f32 output");
+    const void* zero = conv_zero_row();
+    DCLIP_HOST_CHECK(zero != nullptr, "dclip_conv3x3: zero row allocation failed");
+    hipStream_t st = (hipStream_t)stream;
+    const PixGeo g{x_bstride, x_off, (int)x_ld, H, W};
+    const int M = B * H * W;
+    const int dir = mode == 0 ? 1 : -1;
+    constexpr int TBM = 256, TBN = 128;
+    const int tiles_m = (M + TBM - 1) / TBM, tiles_n = (Nout + TBN - 1) / TBN;
+    const int map_hw = out_gap ? H * W : 0;
+#define CONV_LAUNCH(T, EPI, OUTT)                                                                                    \
+    conv_nt_kernel<T, EPI, OUTT, TBM, TBN, 4, 2, 3><<<tiles_m * tiles_n, 512, 0, st>>>(                             \
+        (const T*)X, (const T*)zero, g, Cin, dir, (const T*)Wt, 9 * (int64_t)Cin, M, Nout, tiles_m, tiles_n, out,    \
+        out_ld, out, out_ld, map_hw, out_gap, out_off)
+    if (ab_dt == DCLIP_BF16) {
+        if (accumulate) CONV_LAUNCH(bf16, DCLIP_EPI_RESIDUAL, float);
+        else if (out_dt == DCLIP_F32) CONV_LAUNCH(bf16, DCLIP_EPI_STORE, float);
+        else CONV_LAUNCH(bf16, DCLIP_EPI_STORE, bf16);
+    } else {
+        if (accumulate) CONV_LAUNCH(f16, DCLIP_EPI_RESIDUAL, float);
+        else if (out_dt == DCLIP_F32) CONV_LAUNCH(f16, DCLIP_EPI_STORE, float);
+        else CONV_LAUNCH(f16, DCLIP_EPI_STORE, f16);
+    }
+#undef CONV_LAUNCH
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int dclip_conv3x3_wgrad(int ab_dt, const void* dY, int64_t ldy, int Nout, const void* X, int64_t x_bstride,
+                                   int64_t x_off, int64_t x_ld, int B, int H, int W, int Cin, float* dW, void* ws,
+                                   int splits, void* stream) {
+    DCLIP_HOST_CHECK(ab_dt == DCLIP_BF16 || ab_dt == DCLIP_F16, "dclip_conv3x3_wgrad: operands must be f16/bf16");
+    DCLIP_HOST_CHECK(Cin % 128 == 0 && Nout % 8 == 0 && Nout > 0 && ldy % 8 == 0 && ldy >= Nout,
+                     "dclip_conv3x3_wgrad: Cin %% 128 == 0 and Nout %% 8 == 0 required");
+    DCLIP_HOST_CHECK(x_ld % 8 == 0 && x_bstride % 8 == 0 && x_off % 8 == 0, "dclip_conv3x3_wgrad: bad strides");
+    DCLIP_HOST_CHECK(splits >= 1 && ws != nullptr, "dclip_conv3x3_wgrad: workspace of splits * Nout * 9 * Cin f32");
+    DCLIP_HOST_CHECK((int64_t)B * H * W < (1ll << 24), "dclip_conv3x3_wgrad: too many pixels");
+    const void* zero = conv_zero_row();
+    DCLIP_HOST_CHECK(zero != nullptr, "dclip_conv3x3_wgrad: zero row allocation failed");
+    hipStream_t st = (hipStream_t)stream;
+    const PixGeo g{x_bstride, x_off, (int)x_ld, H, W};
+    const int Kpix = B * H * W;
+    const int N = 9 * Cin;
+    const int kp = (Kpix + 64 * splits - 1) / (64 * splits) * 64;  // pixel rows per split
+    const int tiles_m = (Nout + BM - 1) / BM, tiles_n = N / BN;
+    dim3 grid(tiles_m * tiles_n, splits);
+    if (ab_dt == DCLIP_BF16)
+        conv_wgrad_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)dY, ldy, (const bf16*)X, (const bf16*)zero, g,
+                                                      Cin, Nout, N, Kpix, kp, tiles_m, tiles_n, (float*)ws,
+                                                      (int64_t)Nout * N);
+    else
+        conv_wgrad_kernel<f16><<<grid, 256, 0, st>>>((const f16*)dY, ldy, (const f16*)X, (const f16*)zero, g, Cin,
+                                                     Nout, N, Kpix, kp, tiles_m, tiles_n, (float*)ws,
+                                                     (int64_t)Nout * N);
+    const int64_t total4 = (int64_t)Nout * (N / 4);
+    int blocks = (int)((total4 + 255) / 256);
+    blocks = blocks > 4096 ? 4096 : blocks;
+    splitk_reduce_kernel<<<blocks, 256, 0, st>>>((const float*)ws, splits, (int64_t)Nout * N, Nout, N, nullptr, dW,
+                                                 N);
     DCLIP_LAUNCH_CHECK();
     return 0;
 }

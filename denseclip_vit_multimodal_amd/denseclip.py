@@ -242,9 +242,8 @@ class DenseCLIP(nn.Module):
         cdt = visual.dtype if visual.dtype in (torch.bfloat16, torch.float16) else \
             getattr(self.backbone, "compute_dtype", torch.bfloat16)
         with torch.no_grad():
-            # channel-last pixel view of the last map (one transpose kernel)
-            pix = ops.transpose(visual.contiguous().view(B, Cv, HW), Cv, HW, cdt, batch=B,
-                                in_bstride=Cv * HW).view(B * HW, Cv)
+            # channel-last pixel rows of the last map (the read-out is a channels-last view)
+            pix = visual.permute(0, 2, 3, 1).reshape(B * HW, Cv).to(cdt).contiguous()
             g = ops.channel_mean(pix, B)                                   # adaptive_avg_pool2d
             if self.global_proj is not None:
                 g = ops.gemm(ops.cast(g, cdt), ops.WEIGHTS.get(self.global_proj.weight, cdt),

@@ -394,11 +394,32 @@ class ViTFeatureFusionNeck(nn.Module):
             nn.init.constant_(m.weight, 1)
             nn.init.constant_(m.bias, 0)
 
+    @staticmethod
+    def _conv_bn_relu(layer, x):
+        """ConvBNReLU with the conv on the MFMA implicit-GEMM kernels for 16-bit maps where
+        the shape allows (3x3: Cin % 128 == 0; 1x1: Cin, Cout % 64 == 0), BN (batch
+        statistics in train mode) and ReLU on the channels-last result.  fp32 maps (fp32
+        images) keep fp32 convs, the reference's arithmetic."""
+        conv, bn, act = layer[0], layer[1], layer[2]
+        if x.dtype in (torch.bfloat16, torch.float16) and conv.kernel_size == (3, 3) \
+                and ops.conv3x3_supported(x, conv.weight):
+            y = ops.Conv3x3Fn.apply(x, conv.weight, x.dtype)
+        elif x.dtype in (torch.bfloat16, torch.float16) and conv.kernel_size == (1, 1) \
+                and ops.conv1x1_supported(x, conv.weight):
+            y = ops.Conv1x1Fn.apply(x, conv.weight, conv.bias, x.dtype)
+        else:
+            y = conv(x)
+        return act(bn(y))
+
     def forward(self, features):
         if len(features) != self.num_inputs:
             raise ValueError(f"ViTFeatureFusionNeck got {len(features)} inputs, expected {self.num_inputs}")
-        feats = [layer(f) for layer, f in zip(self.process_layers, features)]
-        return [self.fusion_layer(torch.cat(feats, dim=1))]
+        if not features[0].is_cuda:
+            feats = [layer(f) for layer, f in zip(self.process_layers, features)]
+            return [self.fusion_layer(torch.cat(feats, dim=1))]
+        feats = [self._conv_bn_relu(layer, f) for layer, f in zip(self.process_layers, features)]
+        cat = torch.cat(feats, dim=1)  # channels-last in, channels-last out
+        return [self._conv_bn_relu(self.fusion_layer, cat)]
 
 
 # ============================================================================ context decoder

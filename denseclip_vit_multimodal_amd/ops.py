@@ -39,6 +39,7 @@ def _stream():
 # events recorded on the launching stream around each op (bench.py uses it to derive the
 # per-launch kernel duration inside its timed region).
 TIMING = None
+STATS = {}  # path counters (tests check which path ran)
 
 
 def _tic():
@@ -67,13 +68,16 @@ def timing_summary():
     return out
 
 
-def _check(*ts):
-    for t in ts:
+def _check(*ts, strided=()):
+    """Every tensor on the GPU; contiguous unless listed in `strided` (ops that take explicit
+    strides, e.g. channels-last pixel-row views)."""
+    for t in ts + tuple(strided):
         if t is None:
             continue
         if not t.is_cuda:
             raise RuntimeError("denseclip HIP op got a CPU tensor: the MI355X path has no CPU fallback")
-        if not t.is_contiguous():
+    for t in ts:
+        if t is not None and not t.is_contiguous():
             raise RuntimeError("denseclip HIP op needs contiguous tensors")
 
 
@@ -321,6 +325,18 @@ class _Cast:
         return v
 
 
+    def get_with(self, p, dtype, tag, fn):
+        """Cached fn(p) (a derived layout of parameter p in dtype), refreshed when p changes."""
+        w = p.detach()
+        key = (id(p), dtype, tag)
+        ent = self._c.get(key)
+        if ent is not None and ent[0] == w._version and ent[1] == w.data_ptr():
+            return ent[2]
+        v = fn(w).to(dtype).contiguous()
+        self._c[key] = (w._version, w.data_ptr(), v)
+        return v
+
+
 WEIGHTS = _Cast()
 
 
@@ -456,33 +472,44 @@ class BlockFn(torch.autograd.Function):
 
 class ReadoutFn(torch.autograd.Function):
     """Per-layer dense read-out (reference models.py:568-582): optional ln_post (only for the
-    last block, models.py:574-576), drop CLS, (B, N, C) -> contiguous (B, C, H, W)."""
+    last block, models.py:574-576), drop CLS, (B, N, C) -> (B, C, H, W).
+
+    The map is returned as a channels-last VIEW of a token buffer (B*N, C) in the map dtype
+    (strides (N*C, 1, W*C, C), offset C: the CLS row of each batch is skipped), so the neck's
+    implicit-GEMM convs read the tokens in place: one cast (or the ln_post output) instead
+    of an NCHW transpose.  `.contiguous()` gives the reference's NCHW layout."""
 
     @staticmethod
     def forward(ctx, x, ln_w, ln_b, meta):
         B, Ntok, gh, gw, out_dtype = meta
         C = x.shape[1]
         mean = rstd = None
-        src = x
         if ln_w is not None:
-            src, mean, rstd = layernorm_fwd(x, ln_w.detach(), ln_b.detach(), torch.float32)
-        out = transpose(src, gh * gw, C, out_dtype, r0=1, batch=B, in_bstride=Ntok * C)
+            buf, mean, rstd = layernorm_fwd(x, ln_w.detach(), ln_b.detach(), out_dtype)
+        elif out_dtype == torch.float32:
+            buf = x.clone()
+        else:
+            buf = cast(x, out_dtype)
         ctx.save_for_backward(x if ln_w is not None else None, mean, rstd, ln_w)
         ctx.meta = meta
         ctx.has_ln = ln_w is not None
-        return out.view(B, C, gh, gw)
+        return buf.as_strided((B, C, gh, gw), (Ntok * C, 1, gw * C, C), C)
 
     @staticmethod
     def backward(ctx, dmap):
         x, mean, rstd, ln_w = ctx.saved_tensors
         B, Ntok, gh, gw, _ = ctx.meta
         C = dmap.shape[1]
-        dmap = dmap.contiguous()
-        dy = torch.zeros(B * Ntok, C, dtype=torch.float32, device=dmap.device)
-        # dy[b][1 + p][c] = dmap[b][c][p]: transpose of the (C, HW) planes into rows 1..HW
-        P = gh * gw
-        N.call("dclip_transpose", _p(dmap), _dt(dmap), C * P, P, 0, _p(dy) + C * 4, N.F32, Ntok * C, C, B, C, C, P,
-               1, None, _stream())
+        if dmap.stride() == (Ntok * C, 1, gw * C, C) and dmap.storage_offset() >= C and \
+                dmap.untyped_storage().nbytes() >= (dmap.storage_offset() - C + B * Ntok * C) * dmap.element_size():
+            # token-buffer layout (Conv3x3Fn's input gradient): take the buffer as it is
+            STATS["readout_zero_copy"] = STATS.get("readout_zero_copy", 0) + 1
+            base = dmap.as_strided((B * Ntok, C), (C, 1), dmap.storage_offset() - C)
+            dy = base.float() if base.dtype != torch.float32 else base.clone()
+            dy.view(B, Ntok, C)[:, 0].zero_()
+        else:
+            dy = torch.zeros(B * Ntok, C, dtype=torch.float32, device=dmap.device)
+            dy.view(B, Ntok, C)[:, 1:].copy_(dmap.permute(0, 2, 3, 1).reshape(B, gh * gw, C))
         if not ctx.has_ln:
             return dy, None, None, None
         dx = torch.empty_like(dy)
@@ -512,3 +539,152 @@ class UpsampleFn(torch.autograd.Function):
 def upsample(x, size):
     Ho, Wo = int(size[0]), int(size[1])
     return UpsampleFn.apply(x, Ho, Wo)
+
+
+# ============================================================================ neck convs
+def _pad64(n):
+    return (n + 63) // 64 * 64
+
+
+def pixel_rows(xmap, cdt):
+    """Channels-last pixel-row geometry of an NCHW-shaped map (B, C, H, W): returns
+    (tensor whose data_ptr is pixel (0, 0, 0), batch stride, pixel pitch), all in elements.
+    Token-buffer views (ReadoutFn) and channels_last tensors are used in place; anything
+    else gets one NHWC copy."""
+    B, C, H, W = xmap.shape
+    st = xmap.stride()
+    if xmap.dtype == cdt and st[1] == 1 and st[3] == C and st[2] == W * C and st[0] % 8 == 0 and C % 8 == 0 \
+            and xmap.data_ptr() % 16 == 0:
+        return xmap, st[0], C
+    xr = xmap.to(cdt).permute(0, 2, 3, 1).contiguous()
+    return xr, H * W * C, C
+
+
+def conv3x3_fwd(xmap, w_rows, cout_pad, cdt):
+    """out (B*H*W, cout_pad) = 3x3 / pad 1 conv of xmap with w_rows (cout_pad, 9*Cin) in
+    (ky, kx, ci) order (models.py:741-745 via ConvBNReLU, 13-20)."""
+    B, Cin, H, W = xmap.shape
+    xr, bs, ld = pixel_rows(xmap, cdt)
+    _check(w_rows, strided=(xr,))
+    out = torch.empty(B * H * W, cout_pad, dtype=cdt, device=xmap.device)
+    N.call("dclip_conv3x3", 0, _dt(w_rows), _p(xr), bs, 0, ld, B, H, W, Cin, _p(w_rows), cout_pad, _p(out), _dt(out),
+           cout_pad, 0, 0, 0, _stream())
+    return out, (xr, bs, ld)
+
+
+class Conv3x3Fn(torch.autograd.Function):
+    """3x3 / stride 1 / pad 1 convolution without bias (the neck's per-level conv,
+    reference models.py:17 inside ConvBNReLU, models.py:741-745) as implicit MFMA GEMMs on
+    channels-last pixel rows: forward, input gradient (dgrad) and weight gradient (wgrad).
+    Returns a channels-last (B, Cout, H, W) tensor.  The input gradient has the input's own
+    layout (for a ViT token-buffer view: a token buffer whose CLS rows are zero), which
+    ReadoutFn.backward takes without a copy."""
+
+    @staticmethod
+    def forward(ctx, xmap, weight, cdt):
+        B, Cin, H, W = xmap.shape
+        Cout = weight.shape[0]
+        cp = _pad64(Cout)
+
+        def rows(w):  # (Cout, Cin, 3, 3) -> (cp, 9*Cin), (ky, kx, ci) order, zero rows past Cout
+            r = w.permute(0, 2, 3, 1).reshape(Cout, 9 * Cin)
+            return torch.cat([r, r.new_zeros(cp - Cout, 9 * Cin)]) if cp > Cout else r
+
+        w_rows = WEIGHTS.get_with(weight, cdt, "conv3x3_rows", rows)
+        out, (xr, bs, ld) = conv3x3_fwd(xmap, w_rows, cp, cdt)
+        ctx.save_for_backward(xr, weight)
+        ctx.geo = (B, Cin, H, W, Cout, cp, bs, ld, xmap.dtype, tuple(xmap.stride()), xmap.storage_offset() -
+                   (xr.storage_offset() if xr is xmap else 0), xr is xmap)
+        ctx.cdt = cdt
+        y = out.as_strided((B, Cout, H, W), (H * W * cp, 1, W * cp, cp))
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xr, weight = ctx.saved_tensors
+        B, Cin, H, W, Cout, cp, bs, ld, in_dt, in_strides, _, in_place = ctx.geo
+        cdt = ctx.cdt
+        M = B * H * W
+        dyr = torch.zeros(M, cp, dtype=cdt, device=dy.device)
+        dyr[:, :Cout] = dy.permute(0, 2, 3, 1).reshape(M, Cout)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            def trows(w):  # (Cout, Cin, 3, 3) -> (Cin, 9*cp): [ci][tap][co], zero columns past Cout
+                t = w.permute(1, 2, 3, 0)  # ci, ky, kx, co
+                if cp > Cout:
+                    t = torch.cat([t, t.new_zeros(Cin, 3, 3, cp - Cout)], dim=3)
+                return t.reshape(Cin, 9 * cp)
+
+            w_t = WEIGHTS.get_with(weight, cdt, "conv3x3_dgrad", trows)
+            if in_place and in_strides[0] == bs:
+                # same layout as the input view: batches of bs elements, pixel rows after a gap
+                gap_rows = (bs - H * W * ld) // ld
+                buf = torch.zeros(B * bs, dtype=cdt, device=dy.device)
+                N.call("dclip_conv3x3", 1, _dt(w_t), _p(dyr), H * W * cp, 0, cp, B, H, W, cp, _p(w_t), Cin, _p(buf),
+                       _dt(buf), ld, gap_rows, gap_rows, 0, _stream())
+                dx = buf.as_strided((B, Cin, H, W), (bs, 1, W * ld, ld), gap_rows * ld)
+            else:
+                buf = torch.empty(M, Cin, dtype=cdt, device=dy.device)
+                N.call("dclip_conv3x3", 1, _dt(w_t), _p(dyr), H * W * cp, 0, cp, B, H, W, cp, _p(w_t), Cin, _p(buf),
+                       _dt(buf), Cin, 0, 0, 0, _stream())
+                dx = buf.as_strided((B, Cin, H, W), (H * W * Cin, 1, W * Cin, Cin))
+            if in_dt != cdt:
+                dx = dx.to(in_dt)
+        if ctx.needs_input_grad[1]:
+            tiles = (cp + 127) // 128 * (9 * Cin // 128)
+            splits = max(1, min(32, 512 // max(1, tiles), M // 4096 or 1))
+            ws = torch.empty(splits, cp, 9 * Cin, dtype=torch.float32, device=dy.device)
+            dwr = torch.empty(cp, 9 * Cin, dtype=torch.float32, device=dy.device)
+            e0 = _tic()
+            N.call("dclip_conv3x3_wgrad", _dt(dyr), _p(dyr), cp, cp, _p(xr), bs, 0, ld, B, H, W, Cin, _p(dwr), _p(ws),
+                   splits, _stream())
+            _toc("conv_wgrad", e0)
+            dw = dwr[:Cout].view(Cout, 3, 3, Cin).permute(0, 3, 1, 2).contiguous().to(weight.dtype)
+        return dx, dw, None
+
+
+def conv3x3_supported(xmap, weight):
+    return (xmap.is_cuda and xmap.dim() == 4 and weight.shape[2:] == (3, 3) and xmap.shape[1] % 128 == 0
+            and weight.shape[1] == xmap.shape[1])
+
+
+class Conv1x1Fn(torch.autograd.Function):
+    """1x1 convolution with optional bias on a channels-last map (the neck's fusion conv,
+    reference models.py:750 via ConvBNReLU) as one MFMA GEMM over pixel rows; gradients by
+    the NT GEMM (input) and the TN weight-gradient GEMM."""
+
+    @staticmethod
+    def forward(ctx, xmap, weight, bias, cdt):
+        B, Cin, H, W = xmap.shape
+        Cout = weight.shape[0]
+        # (B*H*W, Cin) pixel rows: a view of a channels-last map, else one NHWC copy
+        x2 = xmap.to(cdt).permute(0, 2, 3, 1).reshape(B * H * W, Cin).contiguous()
+        out = gemm(x2, WEIGHTS.get(weight, cdt), bias=bias.detach() if bias is not None else None)
+        ctx.save_for_backward(x2, weight)
+        ctx.meta = (B, Cin, H, W, Cout, bias is not None, xmap.dtype)
+        ctx.cdt = cdt
+        return out.as_strided((B, Cout, H, W), (H * W * Cout, 1, W * Cout, Cout))
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight = ctx.saved_tensors
+        B, Cin, H, W, Cout, has_b, in_dt = ctx.meta
+        cdt = ctx.cdt
+        d2 = dy.permute(0, 2, 3, 1).reshape(B * H * W, Cout)
+        d2 = d2.to(cdt).contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = gemm(d2, WEIGHTS.get(weight, cdt, transposed=True))
+            dx = dx.as_strided((B, Cin, H, W), (H * W * Cin, 1, W * Cin, Cin))
+            if in_dt != cdt:
+                dx = dx.to(in_dt)
+        if ctx.needs_input_grad[1] or (has_b and ctx.needs_input_grad[2]):
+            dWm, dbm = weight_grad(d2, x2, want_bias=has_b)
+            dw = dWm.view_as(weight).to(weight.dtype)
+            db = dbm
+        return dx, dw, db, None
+
+
+def conv1x1_supported(xmap, weight):
+    return (xmap.is_cuda and xmap.dim() == 4 and weight.shape[2:] == (1, 1) and xmap.shape[1] % 64 == 0
+            and weight.shape[0] % 64 == 0)  # K of the forward and of the input-gradient GEMM

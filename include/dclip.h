@@ -18,6 +18,7 @@
  *                              vis_proj / global_proj denseclip.py:198-199,605-616,
  *                              and every weight/input gradient of those
  *   dclip_attn_fwd/bwd         nn.MultiheadAttention core (SDPA) models.py:287-289
+ *   dclip_conv3x3(_wgrad)      ViTFeatureFusionNeck 3x3 ConvBNReLU convs models.py:741-745
  *   dclip_im2col               conv1 (16x16, stride 16, no bias) models.py:407,546
  *   dclip_tokens_fwd/bwd       flatten/transpose + CLS + pos add, models.py:548-556
  *   dclip_pos_interp_fwd/bwd   interpolate_pos_encoding models.py:514-540
@@ -184,6 +185,29 @@ int dclip_bilinear_fwd(const void* in, int in_dt, void* out, int out_dt,
 /* Its gradient: din f32 (NC, Hi, Wi) = resize^T(dout).  ws: f32 (NC, Ho, Wi).        */
 int dclip_bilinear_bwd(const void* dout, int dout_dt, float* din, float* ws,
                        int64_t NC, int Hi, int Wi, int Ho, int Wo, void* stream);
+
+/* 3x3 / stride 1 / pad 1 convolution as an implicit GEMM on channels-last pixel rows
+ * (the ViTFeatureFusionNeck's per-level convs, reference models.py:741-745 / 13-20, run on
+ * the ViT token read-out without NCHW copies).  Input pixel (b, y, x) of the B x H x W image
+ * is the row X + b*x_bstride + x_off + (y*W + x)*x_ld (elements, all multiples of 8); for a
+ * ViT token buffer (B*N, C): x_bstride = N*C, x_off = C (skips CLS), x_ld = C.
+ *   mode 0 (forward):  out[p][n] = sum_{tap, c} X[p + d(tap)][c] * Wt[n][tap*Cin + c]
+ *   mode 1 (dgrad):    out[p][n] = sum_{tap, c} X[p - d(tap)][c] * Wt[n][tap*Cin + c]
+ *                      (X = dOut with Cin = Cout channels, Wt[ci][tap*Cout + co] = w[co][ci][tap])
+ * d(tap) = (tap/3 - 1, tap%3 - 1); out-of-image taps read zeros.  Cin % 64 == 0.
+ * Output row of pixel p: p, or with out_gap > 0: p + (p / (H*W))*out_gap + out_off (e.g.
+ * gap 1, off 1 writes into rows 1.. of each batch of a (B*N, C) token buffer); out_ld is
+ * its row pitch.  out_dt: f32 or the operand dtype; accumulate=1 (f32 only) adds.        */
+int dclip_conv3x3(int mode, int ab_dt, const void* X, int64_t x_bstride, int64_t x_off, int64_t x_ld,
+                  int B, int H, int W, int Cin, const void* Wt, int Nout, void* out, int out_dt,
+                  int64_t out_ld, int out_gap, int out_off, int accumulate, void* stream);
+
+/* Weight gradient of the 3x3 conv: dW[co][tap*Cin + c] = sum_p dY[p][co] * X[p + d(tap)][c]
+ * (f32, Nout x 9*Cin), pixels split into `splits` chunks summed through ws
+ * (splits * Nout * 9*Cin f32) in a fixed order.  Cin % 128 == 0.                       */
+int dclip_conv3x3_wgrad(int ab_dt, const void* dY, int64_t ldy, int Nout, const void* X, int64_t x_bstride,
+                        int64_t x_off, int64_t x_ld, int B, int H, int W, int Cin, float* dW, void* ws,
+                        int splits, void* stream);
 
 /* Element-wise dtype conversion of n elements: out = (out_dt)(in * scale).  A power-of-two
  * scale keeps fp16 gradients out of the subnormal range (see dclip_gemm's alpha).     */

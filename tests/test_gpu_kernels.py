@@ -390,3 +390,101 @@ def test_score_map_and_channel_mean():
     assert rel_err(s, ref) < 1e-5
     m = O.channel_mean(v, B)
     assert rel_err(m, v.float().view(B, HW, C).mean(1)) < 1e-6
+
+
+# ----------------------------------------------------------------------------- neck convs
+def _tok_view(B, H, W, C, dt):
+    """A ViT-style token buffer (B*(1+H*W), C) and its channels-last map view (ReadoutFn layout)."""
+    Nt = 1 + H * W
+    buf = torch.randn(B * Nt, C, device=DEV).to(dt)
+    return buf, buf.as_strided((B, C, H, W), (Nt * C, 1, W * C, C), C)
+
+
+@pytest.mark.parametrize("B,Cin,H,W,Cout", [(2, 128, 5, 7, 64), (1, 768, 16, 32, 128), (2, 128, 8, 16, 16),
+                                            (3, 256, 3, 130, 192)])
+@pytest.mark.parametrize("layout", ["tokens", "nchw"])
+def test_conv3x3_fn_vs_torch(B, Cin, H, W, Cout, layout):
+    """Implicit-GEMM 3x3 conv (forward, input and weight gradients) vs fp32 F.conv2d on the
+    same bf16-rounded operands."""
+    O = ops()
+    dt = torch.bfloat16
+    if layout == "tokens":
+        _, x = _tok_view(B, H, W, Cin, dt)
+    else:
+        x = torch.randn(B, Cin, H, W, device=DEV).to(dt)
+    w = (torch.randn(Cout, Cin, 3, 3, device=DEV) * (9 * Cin) ** -0.5).requires_grad_(True)
+    xg = x.detach().requires_grad_(True)
+    y = O.Conv3x3Fn.apply(xg, w, dt)
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().to(dt).float().requires_grad_(True)
+    ref = F.conv2d(xr, wr, padding=1)
+    assert y.shape == ref.shape
+    assert rel_err(y.float(), ref) < 8e-3
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    y.backward(g.to(dt))
+    assert rel_err(xg.grad.float(), xr.grad) < 1.5e-2
+    assert rel_err(w.grad, wr.grad) < 1.5e-2
+
+
+def test_conv3x3_dgrad_token_layout_and_readout():
+    """ReadoutFn -> Conv3x3Fn: the conv's input gradient keeps the token layout (CLS rows
+    zero) and the read-out takes it without a copy; the residual-stream gradient matches
+    fp32 autograd through F.conv2d on the NCHW map."""
+    O = ops()
+    B, C, H, W, Cout = 2, 128, 6, 10, 64
+    Nt = 1 + H * W
+    tok = torch.randn(B * Nt, C, device=DEV).requires_grad_(True)
+    w = torch.randn(Cout, C, 3, 3, device=DEV) * 0.05
+    m = O.ReadoutFn.apply(tok, None, None, (B, Nt, H, W, torch.bfloat16))
+    assert m.shape == (B, C, H, W) and m.stride() == (Nt * C, 1, W * C, C)
+    y = O.Conv3x3Fn.apply(m, w, torch.bfloat16)
+    g = torch.randn(B, Cout, H, W, device=DEV)
+    n0 = O.STATS.get("readout_zero_copy", 0)
+    (y.float() * g).sum().backward()
+    assert O.STATS.get("readout_zero_copy", 0) == n0 + 1
+    tr = tok.detach().to(torch.bfloat16).float().requires_grad_(True)
+    mr = tr.view(B, Nt, C)[:, 1:].reshape(B, H, W, C).permute(0, 3, 1, 2)
+    (F.conv2d(mr, w.to(torch.bfloat16).float(), padding=1) * g).sum().backward()
+    assert torch.count_nonzero(tok.grad.view(B, Nt, C)[:, 0]) == 0
+    assert rel_err(tok.grad, tr.grad) < 1.5e-2
+
+
+@pytest.mark.parametrize("B,Cin,H,W,Cout", [(2, 1536, 8, 16, 256), (1, 64, 3, 5, 64)])
+def test_conv1x1_fn_vs_torch(B, Cin, H, W, Cout):
+    O = ops()
+    dt = torch.bfloat16
+    x = torch.randn(B, Cin, H, W, device=DEV).to(dt).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Cout, Cin, 1, 1, device=DEV) * Cin ** -0.5).requires_grad_(True)
+    b = torch.randn(Cout, device=DEV).requires_grad_(True)
+    xg = x.detach().requires_grad_(True)
+    y = O.Conv1x1Fn.apply(xg, w, b, dt)
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().to(dt).float().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True)
+    ref = F.conv2d(xr, wr, br)
+    assert rel_err(y.float(), ref) < 8e-3
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    y.backward(g.to(dt))
+    assert rel_err(xg.grad.float(), xr.grad) < 1.5e-2
+    assert rel_err(w.grad, wr.grad) < 1.5e-2
+    assert rel_err(b.grad, br.grad) < 1e-2
+
+
+@pytest.mark.parametrize("train", [False, True])
+def test_neck_hip_vs_torch(train):
+    """ViTFeatureFusionNeck on token-view maps (HIP convs) vs the same module in fp32 torch."""
+    from denseclip_vit_multimodal_amd.models import ViTFeatureFusionNeck
+    torch.manual_seed(3)
+    B, C, H, W = 2, 256, 8, 16
+    neck = ViTFeatureFusionNeck([C] * 3, 256, 128).to(DEV)
+    ref_neck = ViTFeatureFusionNeck([C] * 3, 256, 128).to(DEV)
+    ref_neck.load_state_dict(neck.state_dict())
+    neck.train(train)
+    ref_neck.train(train)
+    maps = [_tok_view(B, H, W, C, torch.bfloat16)[1] for _ in range(3)]
+    out = neck(maps)[0]
+    ref = ref_neck([m.float().contiguous() for m in maps])[0]
+    assert out.shape == ref.shape
+    assert rel_err(out.float(), ref) < 3e-2
