@@ -168,9 +168,192 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TDY* __restrict__ dy,
     }
 }
 
+// ---------------------------------------------------------------------------- fast path
+// cols = 256 * NV (768 = ViT-B, 1024 = ViT-L): persistent waves walk rows grid-strided with
+// the NEXT row's loads issued before the current row is reduced (one row of loads always in
+// flight per wave), w / b held in registers, register arrays sized exactly (no MAXV
+// footprint, so occupancy is not register-bound).
+template <typename TX, typename TY, int NV>
+__global__ __launch_bounds__(256) void ln_fwd_fast(const TX* __restrict__ x, const float* __restrict__ w,
+                                                   const float* __restrict__ b, TY* __restrict__ y,
+                                                   float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                   int64_t rows, float eps) {
+    constexpr int cols = 256 * NV;
+    const int lane = threadIdx.x & 63;
+    const int64_t stride = (int64_t)gridDim.x * 4;
+    int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    float wl[4 * NV], bl[4 * NV], v[4 * NV], nv[4 * NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        load4(w + 4 * lane + 256 * i, wl + 4 * i);
+        load4(b + 4 * lane + 256 * i, bl + 4 * i);
+        load4(x + row * cols + 4 * lane + 256 * i, v + 4 * i);
+    }
+    while (true) {
+        const int64_t nrow = row + stride;
+        if (nrow < rows) {
+#pragma unroll
+            for (int i = 0; i < NV; ++i) load4(x + nrow * cols + 4 * lane + 256 * i, nv + 4 * i);
+        }
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4 * NV; ++k) s += v[k];
+        const float mu = wave_sum(s) * (1.0f / cols);
+        float ss = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4 * NV; ++k) {
+            const float d = v[k] - mu;
+            ss += d * d;
+        }
+        const float rs = rsqrtf(wave_sum(ss) * (1.0f / cols) + eps);
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            float o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = (v[4 * i + e] - mu) * rs * wl[4 * i + e] + bl[4 * i + e];
+            store4(y + row * cols + 4 * lane + 256 * i, o);
+        }
+        if (lane == 0) {
+            if (mean_out) mean_out[row] = mu;
+            if (rstd_out) rstd_out[row] = rs;
+        }
+        if (nrow >= rows) break;
+        row = nrow;
+#pragma unroll
+        for (int k = 0; k < 4 * NV; ++k) v[k] = nv[k];
+    }
+}
+
+// 8 waves per block and at most 512 blocks: the dw / db partial sums of a block are reduced
+// in LDS and added with ONE atomic per column per block — every block adds into the same
+// 2 * cols floats, so the atomic count (not the bytes) sets that tail's cost
+template <typename TDY, typename TX, int NV>
+__global__ __launch_bounds__(512) void ln_bwd_fast(const TDY* __restrict__ dy, const TX* __restrict__ x,
+                                                   const float* __restrict__ w, const float* __restrict__ mean,
+                                                   const float* __restrict__ rstd, float* __restrict__ dx,
+                                                   int accumulate, float* __restrict__ dw, float* __restrict__ db,
+                                                   int64_t rows) {
+    constexpr int cols = 256 * NV;
+    __shared__ float red[8][2][4 * NV][64];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int64_t stride = (int64_t)gridDim.x * 8;
+    float aw[4 * NV], ab[4 * NV], wl[4 * NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) load4(w + 4 * lane + 256 * i, wl + 4 * i);
+#pragma unroll
+    for (int k = 0; k < 4 * NV; ++k) aw[k] = ab[k] = 0.f;
+    int64_t row = (int64_t)blockIdx.x * 8 + wave;
+    // everything a row needs (dy, x, the accumulated dx, its statistics) is loaded one row
+    // ahead, so no load latency is exposed per row
+    float dv[4 * NV], xv[4 * NV], old[4 * NV], ndv[4 * NV], nxv[4 * NV], nold[4 * NV];
+    float mu = 0.f, rs = 0.f, nmu = 0.f, nrs = 0.f;
+    if (row < rows) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            load4(dy + row * cols + 4 * lane + 256 * i, dv + 4 * i);
+            load4(x + row * cols + 4 * lane + 256 * i, xv + 4 * i);
+            if (accumulate) load4(dx + row * cols + 4 * lane + 256 * i, old + 4 * i);
+        }
+        mu = mean[row];
+        rs = rstd[row];
+    }
+    while (row < rows) {
+        const int64_t nrow = row + stride;
+        if (nrow < rows) {
+#pragma unroll
+            for (int i = 0; i < NV; ++i) {
+                load4(dy + nrow * cols + 4 * lane + 256 * i, ndv + 4 * i);
+                load4(x + nrow * cols + 4 * lane + 256 * i, nxv + 4 * i);
+                if (accumulate) load4(dx + nrow * cols + 4 * lane + 256 * i, nold + 4 * i);
+            }
+            nmu = mean[nrow];
+            nrs = rstd[nrow];
+        }
+        float sg = 0.f, sgx = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4 * NV; ++k) {
+            const float xh = (xv[k] - mu) * rs;
+            const float g = dv[k] * wl[k];
+            sg += g;
+            sgx += g * xh;
+            aw[k] += dv[k] * xh;
+            ab[k] += dv[k];
+            xv[k] = xh;  // keep x-hat
+        }
+        const float mg = wave_sum(sg) * (1.0f / cols);
+        const float mgx = wave_sum(sgx) * (1.0f / cols);
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            float o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int k = 4 * i + e;
+                o[e] = rs * (dv[k] * wl[k] - mg - xv[k] * mgx);
+                if (accumulate) o[e] += old[k];
+            }
+            store4(dx + row * cols + 4 * lane + 256 * i, o);
+        }
+        row = nrow;
+        mu = nmu;
+        rs = nrs;
+#pragma unroll
+        for (int k = 0; k < 4 * NV; ++k) {
+            dv[k] = ndv[k];
+            xv[k] = nxv[k];
+            old[k] = nold[k];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4 * NV; ++k) {
+        red[wave][0][k][lane] = aw[k];
+        red[wave][1][k][lane] = ab[k];
+    }
+    __syncthreads();
+    // thread t sums the 8 waves' partials of entries t, t + 512, ... of the [2][4NV][64] table
+    for (int e = threadIdx.x; e < 2 * 4 * NV * 64; e += 512) {
+        const int which = e / (4 * NV * 64), k = (e / 64) % (4 * NV), l = e % 64;
+        float sum = 0.f;
+#pragma unroll
+        for (int wv = 0; wv < 8; ++wv) sum += red[wv][which][k][l];
+        const int c = 4 * l + 256 * (k / 4) + (k % 4);
+        float* out = which ? db : dw;
+        if (out) atomicAdd(out + c, sum);
+    }
+}
+
+// blocks of 4 waves: enough persistent waves to fill the chip (8 per SIMD), fewer for small inputs
+inline int64_t ln_blocks(int64_t rows, int64_t cap) {
+    int64_t blocks = (rows + 3) / 4;
+    return blocks > cap ? cap : blocks;
+}
+
+template <typename TX, typename TY, int NV>
+void fwd_fast(const void* x, const float* w, const float* b, void* y, float* mean, float* rstd, int64_t rows,
+              float eps, hipStream_t st) {
+    ln_fwd_fast<TX, TY, NV><<<(unsigned)ln_blocks(rows, 2048), 256, 0, st>>>((const TX*)x, w, b, (TY*)y, mean, rstd,
+                                                                            rows, eps);
+}
+
+template <typename TDY, typename TX, int NV>
+void bwd_fast(const void* dy, const void* x, const float* w, const float* mean, const float* rstd, float* dx, int acc,
+              float* dw, float* db, int64_t rows, hipStream_t st) {
+    int64_t blocks = (rows + 7) / 8;
+    blocks = blocks > 512 ? 512 : blocks;
+    ln_bwd_fast<TDY, TX, NV><<<(unsigned)blocks, 512, 0, st>>>((const TDY*)dy, (const TX*)x, w, mean, rstd, dx, acc,
+                                                              dw, db, rows);
+}
+
 template <typename TX, typename TY>
 void fwd_launch(const void* x, const float* w, const float* b, void* y, float* mean, float* rstd,
                 int64_t rows, int cols, float eps, hipStream_t st) {
+    switch (cols) {
+        case 512: return fwd_fast<TX, TY, 2>(x, w, b, y, mean, rstd, rows, eps, st);
+        case 768: return fwd_fast<TX, TY, 3>(x, w, b, y, mean, rstd, rows, eps, st);
+        case 1024: return fwd_fast<TX, TY, 4>(x, w, b, y, mean, rstd, rows, eps, st);
+        default: break;
+    }
     dim3 grid((unsigned)((rows + 3) / 4));
     ln_fwd_kernel<TX, TY><<<grid, 256, 0, st>>>((const TX*)x, w, b, (TY*)y, mean, rstd, rows, cols, eps);
 }
@@ -186,6 +369,12 @@ void fwd_dispatch_y(int y_dt, const void* x, const float* w, const float* b, voi
 template <typename TDY, typename TX>
 void bwd_launch(const void* dy, const void* x, const float* w, const float* mean, const float* rstd,
                 float* dx, int acc, float* dw, float* db, int64_t rows, int cols, hipStream_t st) {
+    switch (cols) {
+        case 512: return bwd_fast<TDY, TX, 2>(dy, x, w, mean, rstd, dx, acc, dw, db, rows, st);
+        case 768: return bwd_fast<TDY, TX, 3>(dy, x, w, mean, rstd, dx, acc, dw, db, rows, st);
+        case 1024: return bwd_fast<TDY, TX, 4>(dy, x, w, mean, rstd, dx, acc, dw, db, rows, st);
+        default: break;
+    }
     int64_t blocks = (rows + 3) / 4;
     if (blocks > 1024) blocks = 1024;
     ln_bwd_kernel<TDY, TX><<<(unsigned)blocks, 256, 0, st>>>((const TDY*)dy, (const TX*)x, w, mean, rstd,

@@ -28,11 +28,13 @@ TOL = {torch.float16: 2e-3, torch.bfloat16: 1.2e-2, torch.float32: 1e-5}
 
 
 # ----------------------------------------------------------------------------- LayerNorm
-@pytest.mark.parametrize("cols", [64, 128, 768, 1024])
+@pytest.mark.parametrize("rows", [517, 20011])
+@pytest.mark.parametrize("cols", [64, 128, 512, 768, 1024])
 @pytest.mark.parametrize("odt", [torch.float32, torch.bfloat16, torch.float16])
-def test_layernorm_fwd(cols, odt):
+def test_layernorm_fwd(cols, odt, rows):
+    """cols = 256k take the persistent prefetching kernel (rows > 8192: several rows per wave)."""
     O = ops()
-    x = torch.randn(517, cols, device=DEV) * 3 + 0.5
+    x = torch.randn(rows, cols, device=DEV) * 3 + 0.5
     w = torch.randn(cols, device=DEV)
     b = torch.randn(cols, device=DEV)
     y, mu, rs = O.layernorm_fwd(x, w, b, odt)
@@ -42,11 +44,12 @@ def test_layernorm_fwd(cols, odt):
     assert rel_err(rs, torch.rsqrt(x.var(1, unbiased=False) + 1e-5)) < 1e-5
 
 
-@pytest.mark.parametrize("cols", [128, 768])
+@pytest.mark.parametrize("rows", [1500, 20011])
+@pytest.mark.parametrize("acc", [0, 1])
+@pytest.mark.parametrize("cols", [128, 768, 1024])
 @pytest.mark.parametrize("dydt", [torch.float32, torch.bfloat16])
-def test_layernorm_bwd(cols, dydt):
+def test_layernorm_bwd(cols, dydt, acc, rows):
     O = ops()
-    rows = 1500
     x = (torch.randn(rows, cols, device=DEV) * 2).requires_grad_(True)
     w = torch.randn(cols, device=DEV).requires_grad_(True)
     b = torch.randn(cols, device=DEV).requires_grad_(True)
@@ -58,8 +61,8 @@ def test_layernorm_bwd(cols, dydt):
     dx = prev.clone()
     dw = torch.zeros(cols, device=DEV)
     db = torch.zeros(cols, device=DEV)
-    O.layernorm_bwd(dy, x.detach(), w.detach(), mu, rs, dx, 1, dw, db)
-    assert rel_err(dx - prev, x.grad) < 1e-5
+    O.layernorm_bwd(dy, x.detach(), w.detach(), mu, rs, dx, acc, dw, db)
+    assert rel_err(dx - prev if acc else dx, x.grad) < 1e-5
     assert rel_err(dw, w.grad) < 1e-5
     assert rel_err(db, b.grad) < 1e-5
 
