@@ -220,7 +220,6 @@ __global__ __launch_bounds__(256) void ln_fwd_fast(const TX* __restrict__ x, con
         }
         if (nrow >= rows) break;
         row = nrow;
-#pragma unroll
         for (int k = 0; k < 4 * NV; ++k) v[k] = nv[k];
     }
 }

@@ -43,6 +43,10 @@ class DenseCLIP(nn.Module):
         self.test_cfg = test_cfg
         self.align_corners = False
         self.text_dim = text_dim
+        # True: the train-mode forward returns the heads' low-res outputs and train.loss_fn
+        # evaluates upsample + CE / SILog in fused kernels (ops.UpsampleCEFn / UpsampleSILogFn).
+        # False (default): the reference contract — upsampled 'main_output' / 'depth_output'.
+        self.fused_head_loss = False
 
         # ---- backbone (denseclip.py:111-126)
         bcfg = dict(backbone)
@@ -294,6 +298,11 @@ class DenseCLIP(nn.Module):
                 seg, depth = self._heads(maps)
         else:
             seg, depth = self._heads(maps)
+        if return_loss and self.training and self.fused_head_loss:
+            # low-res head outputs for train.loss_fn's fused upsample + CE / SILog kernels
+            # (same loss and gradients; the 1024x2048 logits are never materialised)
+            return {"main_output": None, "depth_output": None, "aux_losses": {},
+                    "main_output_lowres": seg, "depth_output_lowres": depth}
         if return_loss and self.training:
             gt = None
             for cand in (gt_semantic_seg, kwargs.get("gt_depth"), kwargs.get("depth_targets"),

@@ -688,3 +688,76 @@ class Conv1x1Fn(torch.autograd.Function):
 def conv1x1_supported(xmap, weight):
     return (xmap.is_cuda and xmap.dim() == 4 and weight.shape[2:] == (1, 1) and xmap.shape[1] % 64 == 0
             and weight.shape[0] % 64 == 0)  # K of the forward and of the input-gradient GEMM
+
+
+# ============================================================================ fused head losses
+_LAB_DT = {torch.int64: 0, torch.int32: 1, torch.uint8: 2}
+
+
+class UpsampleCEFn(torch.autograd.Function):
+    """F.cross_entropy(F.interpolate(logits, (H, W), bilinear, align_corners=False), labels,
+    ignore_index) (reference denseclip.py:847 resize + train_denseclip.py:1265-1314 CE) in one
+    pass over the labels: the upsampled logits are never materialised; the gradient wrt the
+    low-res logits is produced in the same pass (scaled by grad / #valid in backward)."""
+
+    @staticmethod
+    def forward(ctx, logits, labels, ignore_index):
+        B, K, h, w = logits.shape
+        H, W = labels.shape[-2:]
+        lg = logits.detach().contiguous()
+        lab = labels.contiguous()
+        _check(lg, lab)
+        if lab.dtype not in _LAB_DT:
+            lab = lab.long()
+        sums = torch.zeros(1, dtype=torch.float64, device=lg.device)
+        cnt = torch.zeros(1, dtype=torch.int32, device=lg.device)
+        grad = torch.zeros(B, K, h, w, dtype=torch.float32, device=lg.device)
+        e0 = _tic()
+        N.call("dclip_upsample_ce", _dt(lg), _p(lg), B, K, h, w, _p(lab), _LAB_DT[lab.dtype], H, W, int(ignore_index),
+               _p(sums), _p(cnt), _p(grad), _stream())
+        _toc("upsample_ce", e0)
+        n = cnt.to(torch.float64).clamp(min=1)
+        ctx.save_for_backward(grad, n)
+        ctx.in_dtype = logits.dtype
+        return (sums / n).to(torch.float32).reshape(())
+
+    @staticmethod
+    def backward(ctx, g):
+        grad, n = ctx.saved_tensors
+        d = grad * (g.to(torch.float64) / n).to(torch.float32)
+        return d.to(ctx.in_dtype), None, None
+
+
+class UpsampleSILogFn(torch.autograd.Function):
+    """SILogLoss(lambd, eps)(F.interpolate(pred, (H, W), bilinear, align_corners=False),
+    target, mask) (reference losses.py:21-78 on the resized depth, denseclip.py:860) without
+    materialising the resized prediction: a sums pass in forward, a gradient pass in backward."""
+
+    @staticmethod
+    def forward(ctx, pred, target, mask, lambd, eps):
+        B, _, h, w = pred.shape
+        H, W = target.shape[-2:]
+        pd = pred.detach().contiguous()
+        tg = target.detach().reshape(B, H, W).float().contiguous()
+        mk = mask.reshape(B, H, W).to(torch.uint8).contiguous() if mask is not None else None
+        _check(pd, tg, mk)
+        sums = torch.zeros(3, dtype=torch.float64, device=pd.device)
+        N.call("dclip_upsample_silog", 0, _dt(pd), _p(pd), B, h, w, _p(tg), _p(mk), H, W, float(eps), float(lambd),
+               _p(sums), None, _stream())
+        T = sums[2].clamp(min=1)
+        loss = sums[1] / T - lambd * sums[0] ** 2 / T ** 2
+        loss = torch.where(sums[2] > 0, loss, torch.zeros_like(loss))
+        ctx.save_for_backward(pd, tg, mk, sums)
+        ctx.args = (lambd, eps, pred.dtype)
+        return loss.to(torch.float32)
+
+    @staticmethod
+    def backward(ctx, g):
+        pd, tg, mk, sums = ctx.saved_tensors
+        lambd, eps, in_dtype = ctx.args
+        B, _, h, w = pd.shape
+        H, W = tg.shape[-2:]
+        grad = torch.zeros(B, 1, h, w, dtype=torch.float32, device=pd.device)
+        N.call("dclip_upsample_silog", 1, _dt(pd), _p(pd), B, h, w, _p(tg), _p(mk), H, W, float(eps), float(lambd),
+               _p(sums), _p(grad), _stream())
+        return (grad * g.to(torch.float32)).to(in_dtype), None, None, None, None

@@ -54,8 +54,17 @@ def synth_batch(B, H, W, device, rank=0, image_dtype=torch.bfloat16, num_classes
 
 
 def loss_fn(out, seg, depth, mask, silog=None):
-    """CE(ignore 255) + 0.1 * SILog (train_denseclip.py:1265-1314)."""
+    """CE(ignore 255) + 0.1 * SILog (train_denseclip.py:1265-1314).  With a model in
+    fused_head_loss mode the outputs are the heads' low-res maps and the resize + loss run
+    as one fused kernel each (identical loss and gradients)."""
     silog = silog or SILogLoss()
+    if out.get("main_output_lowres") is not None:
+        from . import ops
+        loss = ops.UpsampleCEFn.apply(out["main_output_lowres"], seg, 255)
+        if out.get("depth_output_lowres") is not None:
+            loss = loss + 0.1 * ops.UpsampleSILogFn.apply(out["depth_output_lowres"], depth, mask, silog.lambd,
+                                                          silog.eps)
+        return loss
     loss = F.cross_entropy(out["main_output"], seg, ignore_index=255)
     if out.get("depth_output") is not None:
         loss = loss + 0.1 * silog(out["depth_output"], depth, mask)

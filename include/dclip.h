@@ -19,6 +19,8 @@
  *                              and every weight/input gradient of those
  *   dclip_attn_fwd/bwd         nn.MultiheadAttention core (SDPA) models.py:287-289
  *   dclip_conv3x3(_wgrad)      ViTFeatureFusionNeck 3x3 ConvBNReLU convs models.py:741-745
+ *   dclip_upsample_ce/silog    logits/depth resize + CE / SILog losses denseclip.py:843-868,
+ *                              train_denseclip.py:1265-1314, losses.py:21-78
  *   dclip_im2col               conv1 (16x16, stride 16, no bias) models.py:407,546
  *   dclip_tokens_fwd/bwd       flatten/transpose + CLS + pos add, models.py:548-556
  *   dclip_pos_interp_fwd/bwd   interpolate_pos_encoding models.py:514-540
@@ -208,6 +210,24 @@ int dclip_conv3x3(int mode, int ab_dt, const void* X, int64_t x_bstride, int64_t
 int dclip_conv3x3_wgrad(int ab_dt, const void* dY, int64_t ldy, int Nout, const void* X, int64_t x_bstride,
                         int64_t x_off, int64_t x_ld, int B, int H, int W, int Cin, float* dW, void* ws,
                         int splits, void* stream);
+
+/* Fused bilinear upsample (align_corners=False) + loss + gradient of the heads
+ * (denseclip.py:843-868 resize, train_denseclip.py:1265-1314 losses), without materialising
+ * the upsampled tensors.  logits: (B, K, h, w) low_dt; labels: (B, H, W) int64 (lab_dt 0),
+ * int32 (1) or uint8 (2); pixels whose label is ignore_index (or outside [0, K)) are skipped.
+ *   dclip_upsample_ce:    loss_sum (f64[1]) += sum of -log softmax(up(logits))[label],
+ *                         count (u32[1]) += #valid, grad (f32, B*K*h*w, accumulated)
+ *                         += up^T(softmax - onehot)   (the caller scales by 1/count)
+ *   dclip_upsample_silog: pred (B, 1, h, w); target f32 (B, H, W); mask u8 (B, H, W) or null.
+ *                         pass 0: sums (f64[3]) += (sum d, sum d^2, T), d = log(max(up(pred),
+ *                         eps)) - log(max(target, eps)) on the mask; pass 1 (sums complete):
+ *                         grad (f32, B*h*w) += up^T((2d/T - 2 lambd S/T^2) / up(pred))
+ *                         (zero where up(pred) < eps).  K == 19 for the CE kernel.       */
+int dclip_upsample_ce(int low_dt, const void* logits, int B, int K, int h, int w, const void* labels, int lab_dt,
+                      int H, int W, int ignore_index, double* loss_sum, unsigned* count, float* grad, void* stream);
+int dclip_upsample_silog(int pass, int low_dt, const void* pred, int B, int h, int w, const float* target,
+                         const uint8_t* mask, int H, int W, float eps, float lambd, double* sums, float* grad,
+                         void* stream);
 
 /* Element-wise dtype conversion of n elements: out = (out_dt)(in * scale).  A power-of-two
  * scale keeps fp16 gradients out of the subnormal range (see dclip_gemm's alpha).     */

@@ -187,3 +187,35 @@ def test_full_resolution_properties():
     assert rel_err(seg_low2[1:], seg_low1) < 1e-2
     ref = F.interpolate(seg_low2, size=(1024, 2048), mode="bilinear", align_corners=False)
     assert rel_err(out2["seg"], ref) < 1e-2
+
+
+@pytest.mark.parametrize("img_dtype", [torch.float32, torch.bfloat16])
+def test_fused_head_loss_matches_materialised(img_dtype):
+    """fused_head_loss (resize + CE / SILog in one kernel each) gives the loss and every
+    parameter gradient of the reference formulation (materialised resize, F.cross_entropy,
+    SILogLoss) on the same model and batch."""
+    from denseclip_vit_multimodal_amd.train import loss_fn, synth_batch
+    torch.manual_seed(0)
+    m = build("tiny", TINY_CFG, torch.bfloat16)
+    m.train()
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.eval()
+    for p in m.parameters():
+        p.requires_grad_(True)
+    img, seg, depth, mask = synth_batch(2, 64, 128, DEV, image_dtype=img_dtype)
+    res = []
+    for fused in (False, True):
+        m.fused_head_loss = fused
+        m.zero_grad(set_to_none=True)
+        out = m(img, gt_semantic_seg=seg, gt_depth=depth, return_loss=True)
+        loss = loss_fn(out, seg, depth, mask)
+        loss.backward()
+        res.append((float(loss), {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}))
+    (l0, g0), (l1, g1) = res
+    assert abs(l0 - l1) < 1e-4 * abs(l0), (l0, l1)
+    assert g0.keys() == g1.keys() and len(g0) > 20
+    for k in g0:
+        # heads / neck: the two formulations agree to fp32 rounding; behind them the bf16 ViT
+        # backward re-rounds a ~1e-6 different input gradient (module docstring: ill-conditioned)
+        assert rel_err(g1[k], g0[k]) < (2e-2 if k.startswith("backbone.") else 2e-3), k
