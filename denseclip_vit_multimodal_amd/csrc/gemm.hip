@@ -970,11 +970,79 @@ const void* conv_zero_row() {
     return z;
 }
 
+// grow-only device scratch for the M-tail split (one stream at a time: the library's ops are
+// stream-ordered on the caller's stream)
+float* tail_scratch(size_t floats) {
+    static float* buf = nullptr;
+    static size_t cap = 0;
+    if (floats > cap) {
+        if (buf) (void)hipFree(buf);
+        buf = nullptr;
+        cap = 0;
+        if (hipMalloc(&buf, floats * sizeof(float)) != hipSuccess) return nullptr;
+        cap = floats;
+    }
+    return buf;
+}
+
+// sum of the tail's split-K slabs + the GEMM's epilogue for rows m0 + r (r < rows), 8 columns
+// per thread
+template <typename T, int EPI, typename OutT>
+__global__ void tail_combine_kernel(const float* __restrict__ ws, int splits, int rows, int N, int64_t m0,
+                                    const float* __restrict__ bias, const void* __restrict__ aux, int64_t ld_aux,
+                                    void* __restrict__ C, int64_t ldc, void* __restrict__ C2, int64_t ldc2) {
+    const int n8 = (N + 7) / 8;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= rows * n8) return;
+    const int r = i / n8, nb = (i % n8) * 8;
+    const bool full = nb + 8 <= N;
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int sp = 0; sp < splits; ++sp) {
+        float t[8];
+        load8<float>(ws + ((int64_t)sp * rows + r) * N + nb, t, full, N - nb);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += t[e];
+    }
+    epi_row8<T, EPI, OutT>(v, (int)(m0 + r), nb, N, bias, aux, ld_aux, C, ldc, C2, ldc2, 0);
+}
+
 template <typename T, int EPI, typename OutT, int TBM, int TBN, int WM, int WN, int STAGES, int BKT = 64>
 void launch_big(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
                 int splits, float alpha, const float* bias, const void* aux, int64_t ld_aux, void* C, int64_t ldc,
                 void* C2, int64_t ldc2, hipStream_t st) {
-    const int tiles_m = (int)((M + TBM - 1) / TBM), tiles_n = (int)((N + TBN - 1) / TBN);
+    int tiles_m = (int)((M + TBM - 1) / TBM);
+    const int tiles_n = (int)((N + TBN - 1) / TBN);
+    // M-tail split: the token GEMMs have M = B*(1 + HW) = 256k + B rows, so the last, nearly
+    // empty row of tiles adds a whole extra round of workgroups (e.g. 771 tiles on 256 CUs).
+    // When it does, the full row tiles run here and the tail rows as K-split slabs over many
+    // workgroups plus a combine that applies the epilogue.
+    const int64_t Mfull = (M / TBM) * TBM, tail = M - Mfull;
+    auto rounds = [](int64_t t) { return (t + 255) / 256; };
+    // Only for long K: the tail launch + combine cost ~20-30 us, about one round of a K = 768
+    // tile (measured: no gain there), against ~80 us for a round at K = 3072.
+    if (EPI != DCLIP_EPI_SPLITK && splits == 1 && tail > 0 && tail <= 64 && Mfull > 0 && K >= 1536 &&
+        rounds((int64_t)tiles_m * tiles_n) > rounds((Mfull / TBM) * tiles_n)) {
+        const int ksteps = (int)(K / BKT);
+        int ts = 1;
+        for (int c = 16; c >= 1; --c)
+            if (ksteps % c == 0) {
+                ts = c;
+                break;
+            }
+        float* ws = tail_scratch((size_t)ts * tail * N);
+        if (ws != nullptr) {
+            tiles_m = (int)(Mfull / TBM);
+            const int ttm = 1;
+            gemm_nt_big_kernel<T, DCLIP_EPI_SPLITK, float, TBM, TBN, WM, WN, STAGES, BKT>
+                <<<dim3(ttm * tiles_n, ts), 64 * WM * WN, 0, st>>>(
+                    (const T*)A + Mfull * lda, lda, (const T*)B, ldb, (int)tail, (int)N, (int)(K / ts), ttm, tiles_n,
+                    nullptr, nullptr, 0, ws, N, nullptr, 0, tail * N, alpha);
+            const int threads = (int)(tail * ((N + 7) / 8));
+            tail_combine_kernel<T, EPI, OutT><<<(threads + 255) / 256, 256, 0, st>>>(
+                ws, ts, (int)tail, (int)N, Mfull, bias, aux, ld_aux, C, ldc, C2, ldc2);
+            M = Mfull;
+        }
+    }
     dim3 grid(tiles_m * tiles_n, splits);
     gemm_nt_big_kernel<T, EPI, OutT, TBM, TBN, WM, WN, STAGES, BKT><<<grid, 64 * WM * WN, 0, st>>>(
         (const T*)A, lda, (const T*)B, ldb, (int)M, (int)N, (int)(K / splits), tiles_m, tiles_n, bias, aux, ld_aux,

@@ -68,7 +68,8 @@ def test_layernorm_bwd(cols, dydt, acc, rows):
 
 
 # ----------------------------------------------------------------------------- GEMM
-SHAPES = [(128, 128, 64), (300, 200, 192), (65, 64, 128), (1000, 2304, 768), (4097, 768, 3072), (8, 512, 768)]
+SHAPES = [(128, 128, 64), (300, 200, 192), (65, 64, 128), (1000, 2304, 768), (4097, 768, 3072), (8, 512, 768),
+          (65544, 768, 1536)]  # the last: M = 256k + 8 takes the M-tail split-K path on the big tiles
 TILES = [1, 2, 3, 4]  # dclip_set_option(DCLIP_OPT_GEMM_TILE): 128x128, 256x256, 256x128, 256x256 k32
 
 
@@ -97,6 +98,22 @@ def test_gemm_store(M, N, K, dt, gemm_tile):
 
 
 @pytest.mark.parametrize("gemm_tile", TILES, indirect=True)
+def test_gemm_store_scaled_tail(gemm_tile):
+    """STORE_SCALED (the QKV epilogue) at M = 8 x 8193 with K >= 1536: tail rows by split-K."""
+    from denseclip_vit_multimodal_amd import _native as Nat
+    O = ops()
+    M, N, K = 65544, 2304, 1536
+    A = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    B = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
+    bias = torch.randn(N, device=DEV)
+    sc = torch.rand(N, device=DEV) + 0.5
+    y = O.gemm(A, B, Nat.EPI_STORE_SCALED, bias=bias, aux=sc)
+    ref = (A.float() @ B.float().t() + bias) * sc
+    assert rel_err(y.float(), ref) < TOL[torch.bfloat16]
+    assert rel_err(y[-8:].float(), ref[-8:]) < TOL[torch.bfloat16]
+
+
+@pytest.mark.parametrize("gemm_tile", TILES, indirect=True)
 def test_gemm_asymmetric_layout(gemm_tile):
     """A = I with an asymmetric B catches a transposed C write (guide §3)."""
     O = ops()
@@ -109,7 +126,7 @@ def test_gemm_asymmetric_layout(gemm_tile):
 
 
 @pytest.mark.parametrize("gemm_tile", TILES, indirect=True)
-@pytest.mark.parametrize("M,N,K", [(300, 256, 128), (2049, 3072, 768)])
+@pytest.mark.parametrize("M,N,K", [(300, 256, 128), (2049, 3072, 768), (65544, 768, 1536)])
 def test_gemm_gelu_and_residual(M, N, K, gemm_tile):
     from denseclip_vit_multimodal_amd import _native as Nat
     O = ops()
