@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("DCLIP_LIB", os.path.join(_HERE, "libdclip.so"))
 F32, F16, BF16 = 0, 1, 2
 EPI_STORE, EPI_GELU, EPI_RESIDUAL, EPI_GELU_BWD, EPI_SPLITK, EPI_STORE_SCALED = 0, 1, 2, 3, 4, 5
 OPT_ATTN_FWD_WAVES, OPT_ATTN_DQ_WAVES, OPT_ATTN_DKDV_WAVES, OPT_GEMM_TILE, OPT_GEMM_TN_TILE = 0, 1, 2, 3, 4
-OPT_ATTN_DKDV_QS, OPT_ATTN_FWD_KERNEL = 5, 6
+OPT_ATTN_DKDV_QS, OPT_ATTN_FWD_KERNEL, OPT_ATTN_BWD_KERNEL = 5, 6, 7
 
 _c_void_p = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -55,6 +55,7 @@ _SIGS = {
     "dclip_conv3x3_wgrad": [_i32, _c_void_p, _i64, _i32, _c_void_p, _i64, _i64, _i64, _i32, _i32, _i32, _i32,
                             _c_void_p, _c_void_p, _i32, _c_void_p],
     "dclip_set_option": [_i32, _i32],
+    "dclip_attn_bwd_workspace": [_i32, _i32, _i32],
     "dclip_gemm_tn_plan": [_i64, _i64, _i64, _c_void_p, _c_void_p],
 }
 EXPORTED = sorted(list(_SIGS) + ["dclip_last_error", "dclip_abi_version"])
@@ -87,6 +88,7 @@ def load(path=None):
         lib.dclip_last_error.argtypes = []
         lib.dclip_abi_version.restype = ctypes.c_int
         lib.dclip_abi_version.argtypes = []
+        lib.dclip_attn_bwd_workspace.restype = ctypes.c_int64  # a size, not a status
         if path is None:
             _lib = lib
         return lib

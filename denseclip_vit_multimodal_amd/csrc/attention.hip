@@ -526,7 +526,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd2_kernel(const T* __r
     Fwd2Ctx<T, NW> c;
     c.smem = smem;
     c.lane = threadIdx.x & 63;
-    c.wave = threadIdx.x >> 6;
+    c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (scalar) for the DMA
     c.h = c.lane >> 5;
     c.l32 = c.lane & 31;
     const int nq = (N - 1) / QB;
@@ -789,7 +789,7 @@ __global__ __launch_bounds__(64 * NW, NB == 2 ? 1 : 8 / NW) void attn_fwd3_kerne
     Fwd3Ctx<T, NW, NB> c;
     c.smem = smem;
     c.lane = threadIdx.x & 63;
-    c.wave = threadIdx.x >> 6;
+    c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (scalar) for the DMA
     c.h = c.lane >> 5;
     c.l32 = c.lane & 31;
     const int nq = (N - 1) / 256;
@@ -883,28 +883,20 @@ __global__ __launch_bounds__(64 * NW, NB == 2 ? 1 : 8 / NW) void attn_fwd3_kerne
     }
     if (NW == 8 && c.wave >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the younger half
 
-    int t = 0;
+    // nt = (N-1)/64 is a multiple of 4 here: one loop exit (several exits cost spills)
     if constexpr (NB == 1) {  // two register sets alternate
-        while (true) {
-            if (t >= c.nt) break;
-            fwd3_step<T, NW, NB, 0>(c, t++, sA, sB, pp);
-            if (t >= c.nt) break;
-            fwd3_step<T, NW, NB, 1>(c, t++, sB, sA, pp);
-            if (t >= c.nt) break;
-            fwd3_step<T, NW, NB, 2>(c, t++, sA, sB, pp);
-            if (t >= c.nt) break;
-            fwd3_step<T, NW, NB, 3>(c, t++, sB, sA, pp);
+        for (int t = 0; t < c.nt; t += 4) {
+            fwd3_step<T, NW, NB, 0>(c, t, sA, sB, pp);
+            fwd3_step<T, NW, NB, 1>(c, t + 1, sB, sA, pp);
+            fwd3_step<T, NW, NB, 2>(c, t + 2, sA, sB, pp);
+            fwd3_step<T, NW, NB, 3>(c, t + 3, sB, sA, pp);
         }
     } else {  // S(t+1) reuses P(t)'s registers
-        while (true) {
-            if (t >= c.nt) break;
-            fwd3_step<T, NW, NB, 0>(c, t++, sA, sA, pp);
-            if (t >= c.nt) break;
-            fwd3_step<T, NW, NB, 1>(c, t++, sA, sA, pp);
-            if (t >= c.nt) break;
-            fwd3_step<T, NW, NB, 2>(c, t++, sA, sA, pp);
-            if (t >= c.nt) break;
-            fwd3_step<T, NW, NB, 3>(c, t++, sA, sA, pp);
+        for (int t = 0; t < c.nt; t += 4) {
+            fwd3_step<T, NW, NB, 0>(c, t, sA, sA, pp);
+            fwd3_step<T, NW, NB, 1>(c, t + 1, sA, sA, pp);
+            fwd3_step<T, NW, NB, 2>(c, t + 2, sA, sA, pp);
+            fwd3_step<T, NW, NB, 3>(c, t + 3, sA, sA, pp);
         }
     }
     __builtin_amdgcn_s_setprio(0);
@@ -1166,6 +1158,306 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const T* _
     }
 }
 
+// ---------------------------------------------------------------------------- dQ pass, CLS split
+// The dQ pass on N = 1 + 256k: the same 32-key unit pipeline as attn_bwd_dq_kernel, with the
+// forward's CLS split (key 0 folded into each query's dQ on the VALU in the prologue, queries
+// 1..N-1 in full 256-row blocks, query 0 by the split-key row pass attn_bwd_row0_dq_*), K / V
+// tiles by LDS-DMA into a 4-slot ring three tiles ahead (no staging registers, no ds_write,
+// a bare barrier behind a counted vmcnt) and widened dQ stores.
+template <typename T, int NW>
+struct Dq2Ctx {
+    typedef typename Mfma<T>::frag frag;
+    static constexpr int PIECES = 8 / NW;  // 1-KiB pieces of a 64-row K (and of a V) tile per wave
+    char* smem;  // [slot 0..3][K | V][64 rows][128 B]
+    rsrc_t rs;
+    uint32_t voffK[PIECES], voffV[PIECES];
+    uint32_t ldb;
+    int nt, lane, l32, h, wave;
+    frag qf[4], gf[4];
+    float negL, negD;
+    f32x16 dq[2];
+};
+
+template <typename T, int NW>
+__device__ __forceinline__ void dq2_issue(Dq2Ctx<T, NW>& c, int t, int slot) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t soff = (uint32_t)(1 + 64 * t) * c.ldb;
+#pragma unroll
+    for (int i = 0; i < Dq2Ctx<T, NW>::PIECES; ++i) {
+        const int piece = c.wave + NW * i;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rs, LDS_PTR(c.smem + slot * 16384 + piece * 1024), 16, c.voffK[i],
+                                                 soff, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rs, LDS_PTR(c.smem + slot * 16384 + 8192 + piece * 1024), 16,
+                                                 c.voffV[i], soff, 0, 0);
+    }
+#endif
+}
+
+// S^T - L and dP^T - delta of the 32-key block `kb` of the tile image at Kt (V at Kt + 8 KiB)
+template <typename T, int NW>
+__device__ __forceinline__ void dq2_sdp(const Dq2Ctx<T, NW>& c, const char* Kt, int kb, f32x16& sacc, f32x16& pacc) {
+    typedef typename Mfma<T>::frag frag;
+    frag kf[4], vf[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        kf[s] = row_frag<T>(Kt, kb * 32 + c.l32, 2 * s + c.h);
+        vf[s] = row_frag<T>(Kt + 8192, kb * 32 + c.l32, 2 * s + c.h);
+    }
+    sacc = splat16(c.negL);
+    pacc = splat16(c.negD);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        sacc = Mfma<T>::mma(kf[s], c.qf[s], sacc);
+        pacc = Mfma<T>::mma(vf[s], c.gf[s], pacc);
+    }
+}
+
+// dS^T of one unit (consumes sacc / pacc), then dQ^T[d][q] += K^T[d][key] dS^T[key][q]
+template <typename T, int NW>
+__device__ __forceinline__ void dq2_ds(Dq2Ctx<T, NW>& c, const char* Kt, int kb, f32x16& sacc, const f32x16& pacc) {
+    typedef typename Mfma<T>::frag frag;
+    frag kt[2][2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int db = 0; db < 2; ++db) kt[s][db] = tr_frag<T>(Kt, kb, s, db, c.lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sacc[r] = __builtin_amdgcn_exp2f(sacc[r]) * pacc[r] * DsScale<T>::v;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const frag sf = pack_frag<T>(sacc, s);
+#pragma unroll
+        for (int db = 0; db < 2; ++db) c.dq[db] = Mfma<T>::mma(kt[s][db], sf, c.dq[db]);
+    }
+}
+
+// tile t in slot Q = t % 4; on entry (sA, pA) = unit (t, 0), on exit (sA, pA) = unit (t+1, 0)
+template <typename T, int NW, int Q>
+__device__ __forceinline__ void dq2_step(Dq2Ctx<T, NW>& c, int t, f32x16& sA, f32x16& pA, f32x16& sB, f32x16& pB) {
+    constexpr int PIECES = Dq2Ctx<T, NW>::PIECES;
+    const char* Kt = c.smem + Q * 16384;
+    const char* Kn = c.smem + ((Q + 1) & 3) * 16384;
+    wait_vmcnt<2 * PIECES>();      // own pieces of tile t+1 landed (tile t+2 in flight)
+    __builtin_amdgcn_s_barrier();  // everyone's; everyone done with step t-1 (slot (t+3) % 4 free)
+    dq2_issue<T, NW>(c, t + 3 < c.nt ? t + 3 : c.nt - 1, (Q + 3) & 3);
+    dq2_sdp<T, NW>(c, Kt, 1, sB, pB);  // unit (t, 1) on the matrix pipe ...
+    dq2_ds<T, NW>(c, Kt, 0, sA, pA);   // ... beside dS / dQ of unit (t, 0)
+    dq2_sdp<T, NW>(c, Kn, 0, sA, pA);  // unit (t+1, 0) ...
+    dq2_ds<T, NW>(c, Kt, 1, sB, pB);   // ... beside unit (t, 1)
+}
+
+template <typename T, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq2_kernel(const T* __restrict__ qkv,
+                                                                       const T* __restrict__ o,
+                                                                       const T* __restrict__ dout,
+                                                                       const float* __restrict__ lse,
+                                                                       float* __restrict__ delta,
+                                                                       T* __restrict__ dqkv, int N, int H,
+                                                                       float scale) {
+    constexpr int QB = 32 * NW, PIECES = Dq2Ctx<T, NW>::PIECES;
+    typedef typename Mfma<T>::frag frag;
+    __shared__ __attribute__((aligned(16))) char smem[4 * 16384];
+    Dq2Ctx<T, NW> c;
+    c.smem = smem;
+    c.lane = threadIdx.x & 63;
+    c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (scalar) for the DMA
+    c.h = c.lane >> 5;
+    c.l32 = c.lane & 31;
+    const int nq = (N - 1) / QB;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int qblk = tile % nq, bh = tile / nq, b = bh / H, hd = bh % H;
+    const int C = H * HD;
+    const int64_t ld = 3 * (int64_t)C;
+    const T* Bb = qkv + (int64_t)b * N * ld;
+    c.ldb = (uint32_t)(ld * sizeof(T));
+    c.nt = (N - 1) / 64;
+    const int q = 1 + qblk * QB + c.wave * 32 + c.l32;
+    // register loads first (their waits must not queue behind the DMA)
+    const T* dOb = dout + (int64_t)b * N * C + hd * HD;
+    const T* Orow = o + ((int64_t)b * N + q) * C + hd * HD;
+    frag of[4], k0[4], v0[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        c.qf[s] = *(const frag*)(Bb + (int64_t)q * ld + hd * HD + (2 * s + c.h) * 8);
+        c.gf[s] = *(const frag*)(dOb + (int64_t)q * C + (2 * s + c.h) * 8);
+        of[s] = *(const frag*)(Orow + (2 * s + c.h) * 8);
+        k0[s] = *(const frag*)(Bb + C + hd * HD + (2 * s + c.h) * 8);
+        v0[s] = *(const frag*)(Bb + 2 * C + hd * HD + (2 * s + c.h) * 8);
+    }
+    typedef T t4 __attribute__((ext_vector_type(4)));
+    t4 k0d[2][4];  // key 0 at this lane's dQ^T rows d = 32 db + 8 g + 4 h + e
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) k0d[db][g] = *(const t4*)(Bb + C + hd * HD + db * 32 + 8 * g + 4 * c.h);
+    const float L = lse[(int64_t)bh * N + q];
+
+    c.rs = make_rsrc(Bb, (uint32_t)N * c.ldb);
+#pragma unroll
+    for (int i = 0; i < PIECES; ++i) {
+        const int r = (c.wave + NW * i) * 8 + (c.lane >> 3);
+        const uint32_t base = (uint32_t)r * c.ldb + (uint32_t)(((c.lane & 7) ^ xsw(r)) * 16);
+        c.voffK[i] = base + (uint32_t)((C + hd * HD) * sizeof(T));
+        c.voffV[i] = base + (uint32_t)((2 * C + hd * HD) * sizeof(T));
+    }
+    dq2_issue<T, NW>(c, 0, 0);
+    dq2_issue<T, NW>(c, c.nt > 1 ? 1 : 0, 1);
+    dq2_issue<T, NW>(c, c.nt > 2 ? 2 : c.nt - 1, 2);
+
+    // delta = rowsum(dO * O); key 0 (CLS) folded into dQ on the VALU:
+    //   dS_0 = P_0 (dP_0 - delta), P_0 = exp2(q . k0 - L), dP_0 = dO . v0;  dQ^T[d] += dS_0 k0[d]
+    float dpart = 0.f, spart = 0.f, ppart = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            dpart += (float)of[s][j] * (float)c.gf[s][j];
+            spart += (float)c.qf[s][j] * (float)k0[s][j];
+            ppart += (float)c.gf[s][j] * (float)v0[s][j];
+        }
+    const float dl = xhalf_sum(dpart);
+    if (c.h == 0) delta[(int64_t)bh * N + q] = dl;
+    c.negL = -L;
+    c.negD = -dl;
+    const float p0 = __builtin_amdgcn_exp2f(xhalf_sum(spart) - L);
+    const float ds0 = p0 * (xhalf_sum(ppart) - dl) * DsScale<T>::v;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) c.dq[db][4 * g + e] = ds0 * (float)k0d[db][g][e];
+
+    wait_vmcnt<2 * PIECES>();  // tiles 0 and 1 landed (tile 2 in flight)
+    __builtin_amdgcn_s_barrier();
+    f32x16 sA, pA, sB, pB;
+    dq2_sdp<T, NW>(c, smem, 0, sA, pA);
+    for (int t = 0; t < c.nt; t += 4) {  // nt = (N-1)/64 is a multiple of 4: one loop exit
+        dq2_step<T, NW, 0>(c, t, sA, pA, sB, pB);
+        dq2_step<T, NW, 1>(c, t + 1, sA, pA, sB, pB);
+        dq2_step<T, NW, 2>(c, t + 2, sA, pA, sB, pB);
+        dq2_step<T, NW, 3>(c, t + 3, sA, pA, sB, pB);
+    }
+    wait_vmcnt<0>();
+    store_row_t21<T>(dqkv + ((int64_t)b * N + q) * ld + hd * HD, c.dq, scale / DsScale<T>::v, c.h);
+}
+
+// ---------------------------------------------------------------------------- row 0 of the backward
+// Query 0 (the dQ row of the CLS token and its delta) and key 0 (the dK / dV rows of the CLS
+// token) for the CLS-split passes: split over 64-key (resp. 64-query) chunks, one wave per
+// chunk, lane = key (resp. query); partial sums in the workspace after delta (B*H*N floats),
+// at ws0 + (bh * nsplit + split) * 192: [0, 64) dQ_0, [64, 128) dK_0, [128, 192) dV_0; the
+// merges sum the chunks in a fixed order.
+template <typename T>
+__global__ __launch_bounds__(64) void attn_bwd_row0_dq_part(const T* __restrict__ qkv, const T* __restrict__ o,
+                                                            const T* __restrict__ dout, const float* __restrict__ lse,
+                                                            float* __restrict__ ws0, int N, int H, int nsplit) {
+    const int lane = threadIdx.x;
+    const int sp = blockIdx.x % nsplit, bh = blockIdx.x / nsplit, b = bh / H, hd = bh % H;
+    const int C = H * HD;
+    const int64_t ld = 3 * (int64_t)C;
+    const T* Bb = qkv + (int64_t)b * N * ld + hd * HD;
+    const T* dO0 = dout + (int64_t)b * N * C + hd * HD;
+    const T* O0 = o + (int64_t)b * N * C + hd * HD;
+    const float L0 = lse[(int64_t)bh * N];
+    const float d0 = wave_sum((float)dO0[lane] * (float)O0[lane]);  // delta of query 0
+    const int key = sp * 64 + lane;
+    const int kc = key < N ? key : N - 1;
+    typedef T t8 __attribute__((ext_vector_type(8)));
+    float s = 0.f, dp = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const t8 qa = *(const t8*)(Bb + 8 * i);
+        const t8 ka = *(const t8*)(Bb + (int64_t)kc * ld + C + 8 * i);
+        const t8 ga = *(const t8*)(dO0 + 8 * i);
+        const t8 va = *(const t8*)(Bb + (int64_t)kc * ld + 2 * C + 8 * i);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            s += (float)qa[j] * (float)ka[j];
+            dp += (float)ga[j] * (float)va[j];
+        }
+    }
+    const float ds = key < N ? __builtin_amdgcn_exp2f(s - L0) * (dp - d0) : 0.f;
+    const int nk = min(64, N - sp * 64);
+    const T* kcol = Bb + (int64_t)(sp * 64) * ld + C + lane;
+    float acc = 0.f;
+    for (int k = 0; k < nk; ++k) acc += __shfl(ds, k, 64) * (float)kcol[(int64_t)k * ld];
+    ws0[((int64_t)bh * nsplit + sp) * 192 + lane] = acc;
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void attn_bwd_row0_dq_merge(const T* __restrict__ o, const T* __restrict__ dout,
+                                                             const float* __restrict__ ws0, float* __restrict__ delta,
+                                                             T* __restrict__ dqkv, int N, int H, int nsplit,
+                                                             float scale) {
+    const int lane = threadIdx.x;
+    const int bh = blockIdx.x, b = bh / H, hd = bh % H;
+    const int C = H * HD;
+    float acc = 0.f;
+    for (int sp = 0; sp < nsplit; ++sp) acc += ws0[((int64_t)bh * nsplit + sp) * 192 + lane];
+    dqkv[(int64_t)b * N * 3 * C + hd * HD + lane] = (T)(acc * scale);
+    const float d0 = wave_sum((float)dout[(int64_t)b * N * C + hd * HD + lane] * (float)o[(int64_t)b * N * C + hd * HD + lane]);
+    if (lane == 0) delta[(int64_t)bh * N] = d0;
+}
+
+// key 0: lane = query q of the chunk; P = exp2(q . k0 - L_q), dS = P (dO_q . v0 - delta_q);
+// dV_0[d] += P dO_q[d], dK_0[d] += dS q[d]  (the unscaled sums; the merge applies the scales)
+template <typename T>
+__global__ __launch_bounds__(64) void attn_bwd_row0_dkdv_part(const T* __restrict__ qkv, const T* __restrict__ dout,
+                                                              const float* __restrict__ lse,
+                                                              const float* __restrict__ delta,
+                                                              float* __restrict__ ws0, int N, int H, int nsplit) {
+    const int lane = threadIdx.x;
+    const int sp = blockIdx.x % nsplit, bh = blockIdx.x / nsplit, b = bh / H, hd = bh % H;
+    const int C = H * HD;
+    const int64_t ld = 3 * (int64_t)C;
+    const T* Bb = qkv + (int64_t)b * N * ld + hd * HD;
+    const T* dOb = dout + (int64_t)b * N * C + hd * HD;
+    const int qr = sp * 64 + lane;
+    const int qc = qr < N ? qr : N - 1;
+    typedef T t8 __attribute__((ext_vector_type(8)));
+    float s = 0.f, dp = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const t8 qa = *(const t8*)(Bb + (int64_t)qc * ld + 8 * i);
+        const t8 ka = *(const t8*)(Bb + C + 8 * i);
+        const t8 ga = *(const t8*)(dOb + (int64_t)qc * C + 8 * i);
+        const t8 va = *(const t8*)(Bb + 2 * C + 8 * i);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            s += (float)qa[j] * (float)ka[j];
+            dp += (float)ga[j] * (float)va[j];
+        }
+    }
+    const float p = qr < N ? __builtin_amdgcn_exp2f(s - lse[(int64_t)bh * N + qc]) : 0.f;
+    const float ds = p * (dp - delta[(int64_t)bh * N + qc]);
+    const int nq = min(64, N - sp * 64);
+    float ak = 0.f, av = 0.f;
+    for (int k = 0; k < nq; ++k) {
+        const int64_t row = sp * 64 + k;
+        ak += __shfl(ds, k, 64) * (float)Bb[row * ld + lane];
+        av += __shfl(p, k, 64) * (float)dOb[row * C + lane];
+    }
+    ws0[((int64_t)bh * nsplit + sp) * 192 + 64 + lane] = ak;
+    ws0[((int64_t)bh * nsplit + sp) * 192 + 128 + lane] = av;
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void attn_bwd_row0_dkdv_merge(const float* __restrict__ ws0, T* __restrict__ dqkv,
+                                                               int N, int H, int nsplit, float dk_scale) {
+    const int lane = threadIdx.x;
+    const int bh = blockIdx.x, b = bh / H, hd = bh % H;
+    const int C = H * HD;
+    float ak = 0.f, av = 0.f;
+    for (int sp = 0; sp < nsplit; ++sp) {
+        ak += ws0[((int64_t)bh * nsplit + sp) * 192 + 64 + lane];
+        av += ws0[((int64_t)bh * nsplit + sp) * 192 + 128 + lane];
+    }
+    T* row = dqkv + (int64_t)b * N * 3 * C + hd * HD;
+    row[C + lane] = (T)(ak * dk_scale);
+    row[2 * C + lane] = (T)av;
+}
+
 // ---------------------------------------------------------------------------- dK/dV pass
 template <typename T, int NT, int QS>
 struct DkvCtx {
@@ -1348,6 +1640,215 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const T*
     }
 }
 
+// ---------------------------------------------------------------------------- dK/dV pass, CLS split
+// Key-major dK/dV pass on N = 1 + 32*NW*k: keys 1..N-1 in full blocks (key 0 by the row-0
+// kernels above), query 0 folded into every key's dK / dV on the VALU in the prologue, and
+// query slices 1 + 64t .. 64 + 64t staged by LDS-DMA — Q and dO pieces plus the slice's L and
+// delta (one masked dword DMA per wave) — into a 4-slot ring three slices ahead, one bare
+// barrier per slice behind a counted vmcnt.  The statistics are negated where they seed the
+// S / dP accumulators.
+template <typename T, int NW>
+struct Dkv2Ctx {
+    typedef typename Mfma<T>::frag frag;
+    static constexpr int PIECES = 16 / NW;  // 1-KiB pieces of a slice (Q + dO) per wave
+    static constexpr int SLOT = 2 * 8192 + 2 * 256;  // [Q | dO | L | delta]
+    static constexpr int SPW = 128 / NW;             // statistics per wave per slice
+    char* smem;
+    rsrc_t rs, rg, rl, rd;  // qkv rows, dO rows, lse, delta of this (batch, head)
+    uint32_t voff[PIECES];
+    uint32_t ldq, ldg;       // row pitches (bytes)
+    int nt, lane, l32, h, wave;
+    frag kf[4], vf[4];
+    f32x16 dk[2], dv[2];
+};
+
+template <typename T, int NW>
+__device__ __forceinline__ void dkv2_issue(Dkv2Ctx<T, NW>& c, int t, int slot) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef Dkv2Ctx<T, NW> X;
+    char* base = c.smem + slot * X::SLOT;
+    const int r0 = 1 + 64 * t;
+#pragma unroll
+    for (int i = 0; i < X::PIECES; ++i) {
+        const int piece = c.wave * X::PIECES + i;  // 0..7 Q, 8..15 dO
+        if (piece < 8)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rs, LDS_PTR(base + piece * 1024), 16, c.voff[i],
+                                                     (uint32_t)r0 * c.ldq, 0, 0);
+        else
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rg, LDS_PTR(base + piece * 1024), 16, c.voff[i],
+                                                     (uint32_t)r0 * c.ldg, 0, 0);
+    }
+    // statistics: waves 0 .. NW/2-1 load L, the others delta, SPW values each
+    const int part = c.wave % (NW / 2);
+    const bool is_l = c.wave < NW / 2;
+    if (c.lane < X::SPW)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(is_l ? c.rl : c.rd,
+                                                 LDS_PTR(base + 16384 + (is_l ? 0 : 256) + part * X::SPW * 4), 4,
+                                                 (uint32_t)(part * X::SPW + c.lane) * 4, (uint32_t)r0 * 4, 0, 0);
+#endif
+}
+
+template <typename T, int NW, int Q>
+__device__ __forceinline__ void dkv2_step(Dkv2Ctx<T, NW>& c, int t) {
+    typedef typename Mfma<T>::frag frag;
+    typedef Dkv2Ctx<T, NW> X;
+    wait_vmcnt<2 * (X::PIECES + 1)>();  // own pieces of slice t landed (slices t+1, t+2 in flight)
+    __builtin_amdgcn_s_barrier();       // everyone's; everyone done with step t-1
+    dkv2_issue<T, NW>(c, t + 3 < c.nt ? t + 3 : c.nt - 1, (Q + 3) & 3);
+    const char* base = c.smem + Q * X::SLOT;
+    const float* Lsl = (const float*)(base + 16384);
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+        const char* Qt = base + sub * 32 * 128;
+        const char* Gt = base + 8192 + sub * 32 * 128;
+        const float* Ls = Lsl + sub * 32;
+        const float* Ds = Lsl + 64 + sub * 32;
+        frag qa[4], ga[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            qa[s] = row_frag<T>(Qt, c.l32, 2 * s + c.h);
+            ga[s] = row_frag<T>(Gt, c.l32, 2 * s + c.h);
+        }
+        f32x16 sacc, pacc;  // start from -L[q] / -delta[q] per row
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+            const f32x4 Lv = *(const f32x4*)(Ls + 8 * g4 + 4 * c.h);
+            const f32x4 Dv = *(const f32x4*)(Ds + 8 * g4 + 4 * c.h);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                sacc[4 * g4 + e] = -Lv[e];
+                pacc[4 * g4 + e] = -Dv[e];
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            sacc = Mfma<T>::mma(qa[s], c.kf[s], sacc);
+            pacc = Mfma<T>::mma(ga[s], c.vf[s], pacc);
+        }
+        frag gt[2][2], qt[2][2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int db = 0; db < 2; ++db) {
+                gt[s][db] = tr_frag<T>(Gt, 0, s, db, c.lane);
+                qt[s][db] = tr_frag<T>(Qt, 0, s, db, c.lane);
+            }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float p = __builtin_amdgcn_exp2f(sacc[r]);
+            sacc[r] = p;
+            pacc[r] = p * pacc[r] * DsScale<T>::v;
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const frag pf = pack_frag<T>(sacc, s);
+            const frag sf = pack_frag<T>(pacc, s);
+#pragma unroll
+            for (int db = 0; db < 2; ++db) {
+                c.dv[db] = Mfma<T>::mma(gt[s][db], pf, c.dv[db]);
+                c.dk[db] = Mfma<T>::mma(qt[s][db], sf, c.dk[db]);
+            }
+        }
+    }
+}
+
+template <typename T, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv2_kernel(const T* __restrict__ qkv,
+                                                                         const T* __restrict__ dout,
+                                                                         const float* __restrict__ lse,
+                                                                         const float* __restrict__ delta,
+                                                                         T* __restrict__ dqkv, int N, int H,
+                                                                         float dk_scale) {
+    constexpr int KB = 32 * NW;
+    typedef Dkv2Ctx<T, NW> X;
+    typedef typename Mfma<T>::frag frag;
+    __shared__ __attribute__((aligned(16))) char smem[4 * X::SLOT];
+    X c;
+    c.smem = smem;
+    c.lane = threadIdx.x & 63;
+    c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (scalar) for the DMA
+    c.h = c.lane >> 5;
+    c.l32 = c.lane & 31;
+    const int nkb = (N - 1) / KB;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int kblk = tile % nkb, bh = tile / nkb, b = bh / H, hd = bh % H;
+    const int C = H * HD;
+    const int64_t ld = 3 * (int64_t)C;
+    const T* Bb = qkv + (int64_t)b * N * ld;
+    const T* dOb = dout + (int64_t)b * N * C;
+    c.ldq = (uint32_t)(ld * sizeof(T));
+    c.ldg = (uint32_t)(C * sizeof(T));
+    c.nt = (N - 1) / 64;
+    const int key = 1 + kblk * KB + c.wave * 32 + c.l32;
+    // register loads first
+    frag q0[4], g0[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        c.kf[s] = *(const frag*)(Bb + (int64_t)key * ld + C + hd * HD + (2 * s + c.h) * 8);
+        c.vf[s] = *(const frag*)(Bb + (int64_t)key * ld + 2 * C + hd * HD + (2 * s + c.h) * 8);
+        q0[s] = *(const frag*)(Bb + hd * HD + (2 * s + c.h) * 8);
+        g0[s] = *(const frag*)(dOb + hd * HD + (2 * s + c.h) * 8);
+    }
+    typedef T t4 __attribute__((ext_vector_type(4)));
+    t4 q0d[2][4], g0d[2][4];  // query 0's q and dO at this lane's accumulator rows d
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            q0d[db][g] = *(const t4*)(Bb + hd * HD + db * 32 + 8 * g + 4 * c.h);
+            g0d[db][g] = *(const t4*)(dOb + hd * HD + db * 32 + 8 * g + 4 * c.h);
+        }
+    const float L0 = lse[(int64_t)bh * N], d0 = delta[(int64_t)bh * N];
+
+    c.rs = make_rsrc(Bb, (uint32_t)N * c.ldq);
+    c.rg = make_rsrc(dOb, (uint32_t)N * c.ldg);
+    c.rl = make_rsrc(lse + (int64_t)bh * N, (uint32_t)N * 4);
+    c.rd = make_rsrc(delta + (int64_t)bh * N, (uint32_t)N * 4);
+#pragma unroll
+    for (int i = 0; i < X::PIECES; ++i) {
+        const int piece = c.wave * X::PIECES + i;
+        const int r = (piece & 7) * 8 + (c.lane >> 3);  // row within the 64-row Q (or dO) image
+        const uint32_t chunk = (uint32_t)(((c.lane & 7) ^ xsw(r)) * 16);
+        c.voff[i] = piece < 8 ? (uint32_t)r * c.ldq + chunk + (uint32_t)(hd * HD * sizeof(T))
+                              : (uint32_t)r * c.ldg + chunk + (uint32_t)(hd * HD * sizeof(T));
+    }
+    dkv2_issue<T, NW>(c, 0, 0);
+    dkv2_issue<T, NW>(c, c.nt > 1 ? 1 : 0, 1);
+    dkv2_issue<T, NW>(c, c.nt > 2 ? 2 : c.nt - 1, 2);
+
+    // query 0 (CLS) folded in: P = exp2(q0 . k - L0), dS = P (dO0 . v - delta0)
+    float spart = 0.f, ppart = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            spart += (float)q0[s][j] * (float)c.kf[s][j];
+            ppart += (float)g0[s][j] * (float)c.vf[s][j];
+        }
+    const float p0 = __builtin_amdgcn_exp2f(xhalf_sum(spart) - L0);
+    const float ds0 = p0 * (xhalf_sum(ppart) - d0) * DsScale<T>::v;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                c.dv[db][4 * g + e] = p0 * (float)g0d[db][g][e];
+                c.dk[db][4 * g + e] = ds0 * (float)q0d[db][g][e];
+            }
+
+    for (int t = 0; t < c.nt; t += 4) {  // nt = (N-1)/64 is a multiple of 4: one loop exit
+        dkv2_step<T, NW, 0>(c, t);
+        dkv2_step<T, NW, 1>(c, t + 1);
+        dkv2_step<T, NW, 2>(c, t + 2);
+        dkv2_step<T, NW, 3>(c, t + 3);
+    }
+    wait_vmcnt<0>();
+    T* rk = dqkv + ((int64_t)b * N + key) * ld + C + hd * HD;
+    store_row_t21<T>(rk, c.dk, dk_scale / DsScale<T>::v, c.h);
+    store_row_t21<T>(rk + C, c.dv, 1.0f, c.h);
+}
+
 // ---------------------------------------------------------------------------- launch
 template <typename T, int NW>
 void fwd_launch_nw(const void* qkv, void* o, float* lse, int B, int N, int H, hipStream_t st) {
@@ -1393,9 +1894,31 @@ void fwd_launch(const void* qkv, void* o, float* lse, int B, int N, int H, hipSt
     else fwd_launch_nw<T, 8>(qkv, o, lse, B, N, H, st);
 }
 
+// CLS-split backward when N - 1 is a multiple of 256 (dQ blocks of 256, dK/dV blocks of 128)
+template <typename T>
+bool bwd2_launch(const void* qkv, const void* o, const void* dout, const float* lse, float* delta, void* dqkv, int B,
+                 int N, int H, float scale, hipStream_t st) {
+    if (N < 257 || (N - 1) % 256 != 0 || dclip_option(DCLIP_OPT_ATTN_BWD_KERNEL) == 1) return false;
+    const int nsplit = (N + 63) / 64;
+    float* ws0 = delta + (int64_t)B * H * N;
+    attn_bwd_row0_dq_part<T><<<B * H * nsplit, 64, 0, st>>>((const T*)qkv, (const T*)o, (const T*)dout, lse, ws0, N, H,
+                                                            nsplit);
+    attn_bwd_row0_dq_merge<T><<<B * H, 64, 0, st>>>((const T*)o, (const T*)dout, ws0, delta, (T*)dqkv, N, H, nsplit,
+                                                    scale);
+    attn_bwd_dq2_kernel<T, 8><<<B * H * ((N - 1) / 256), 512, 0, st>>>((const T*)qkv, (const T*)o, (const T*)dout, lse,
+                                                                      delta, (T*)dqkv, N, H, scale);
+    attn_bwd_row0_dkdv_part<T><<<B * H * nsplit, 64, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, ws0, N, H,
+                                                              nsplit);
+    attn_bwd_row0_dkdv_merge<T><<<B * H, 64, 0, st>>>(ws0, (T*)dqkv, N, H, nsplit, 1.0f / LOG2E);
+    attn_bwd_dkdv2_kernel<T, 4><<<B * H * ((N - 1) / 128), 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta,
+                                                                        (T*)dqkv, N, H, 1.0f / LOG2E);
+    return true;
+}
+
 template <typename T>
 void bwd_launch(const void* qkv, const void* o, const void* dout, const float* lse, float* delta, void* dqkv,
                 int B, int N, int H, float scale, hipStream_t st) {
+    if (bwd2_launch<T>(qkv, o, dout, lse, delta, dqkv, B, N, H, scale, st)) return;
     // dQ (w.r.t. the unscaled q) = dZ K scale;  dK = dZ^T q scale = dZ^T q' / log2(e)
     if (dclip_option(DCLIP_OPT_ATTN_DQ_WAVES) == 4) {
         dim3 grid(((N + 127) / 128) * B * H);
@@ -1439,6 +1962,11 @@ extern "C" int dclip_attn_fwd(int dt, const void* qkv, void* o, float* lse, int 
     else fwd_launch<f16>(qkv, o, lse, B, N, H, st);
     DCLIP_LAUNCH_CHECK();
     return 0;
+}
+
+extern "C" int64_t dclip_attn_bwd_workspace(int B, int N, int H) {
+    // delta (B*H*N) + the CLS-split row-0 partials (B*H*ceil(N/64)*192)
+    return (int64_t)B * H * N + (int64_t)B * H * ((N + 63) / 64) * 192;
 }
 
 extern "C" int dclip_attn_bwd(int dt, const void* qkv, const void* o, const void* dout, const float* lse,

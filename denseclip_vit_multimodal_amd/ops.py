@@ -236,7 +236,8 @@ def attn_fwd(qkv, B, Ntok, H, scale):
 def attn_bwd(qkv, o, dout, lse, B, Ntok, H, scale):
     _check(qkv, o, dout, lse)
     C = o.shape[1]
-    delta = torch.empty(B * H * Ntok, dtype=torch.float32, device=qkv.device)
+    # delta (B*H*N) + the CLS-split row-0 partials (dclip_attn_bwd_workspace)
+    delta = torch.empty(N.lib().dclip_attn_bwd_workspace(B, Ntok, H), dtype=torch.float32, device=qkv.device)
     dqkv = torch.empty_like(qkv)
     e0 = _tic()
     N.call("dclip_attn_bwd", _dt(qkv), _p(qkv), _p(o), _p(dout), _p(lse), _p(delta), _p(dqkv), B, Ntok, H, C // H,

@@ -74,6 +74,7 @@ int dclip_abi_version(void);
 #define DCLIP_OPT_GEMM_TILE 3        /* dclip_gemm tiles: 0 auto (default), 1 128x128, 2 256x256, 3 256x128, 4 256x256 k32x4 */
 #define DCLIP_OPT_GEMM_TN_TILE 4     /* dclip_gemm_tn tiles: 0 auto (default: 256x256 when M, N >= 256), 1 128x128 */
 #define DCLIP_OPT_ATTN_DKDV_QS 5     /* dK/dV pass query rows per barrier: 64 (default) or 128 */
+#define DCLIP_OPT_ATTN_BWD_KERNEL 7  /* 0 (default): CLS-split passes when N-1 is a multiple of 256; 1: generic */
 #define DCLIP_OPT_ATTN_FWD_KERNEL 6  /* 0 (default): CLS-split kernel when N-1 is a multiple of the query block; 1: generic */
 #define DCLIP_OPT_COUNT 8
 int dclip_set_option(int id, int value);
@@ -131,13 +132,15 @@ int dclip_attn_fwd(int dt, const void* qkv, void* o, float* lse,
 
 /* Attention backward (flash-style recompute from lse; no N x N buffer, no atomics):
  * a query-major dQ pass (which also writes delta = rowsum(dout*o) to delta_ws) and a
- * key-major dK/dV pass.  dout: (B*N, H*D) dt.  delta_ws: f32 (B*H*N) workspace.
+ * key-major dK/dV pass.  dout: (B*N, H*D) dt.  delta_ws: f32 workspace of
+ * dclip_attn_bwd_workspace(B, N, H) floats (its first B*H*N receive delta).
  * qkv as for dclip_attn_fwd (q pre-multiplied by scale*log2(e)); `scale` = d^-0.5.
  * dqkv: (B*N, 3*H*D) dt output, [dq | dk | dv] in the qkv layout: gradients with
  * respect to the UNSCALED q, k, v (i.e. the in-projection output before the q scale).  */
 int dclip_attn_bwd(int dt, const void* qkv, const void* o, const void* dout,
                    const float* lse, float* delta_ws, void* dqkv,
                    int B, int N, int H, int D, float scale, void* stream);
+int64_t dclip_attn_bwd_workspace(int B, int N, int H);
 
 /* Non-overlapping p x p patches of img (B, Cin, Hin, Win) (img_dt) ->
  * out (B*gh*gw, Cin*p*p) (out_dt), column order (c, ky, kx) = conv weight flattening,

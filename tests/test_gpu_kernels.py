@@ -290,8 +290,11 @@ def test_attention_cls_split_spikes(where, spike, fwd_kernel):
     qkv[:, :64] = 1.0
     qkv[where, 64:128] = spike
     qkv, qref = prescale(qkv.to(torch.float16), H)
-    o, _ = O.attn_fwd(qkv, B, N, H, 64 ** -0.5)
+    o, lse = O.attn_fwd(qkv, B, N, H, 64 ** -0.5)
     assert rel_err(o.float(), attn_ref(qref, B, N, H)) < TOL[torch.float16]
+    q, k, _ = qref.view(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    lref = torch.logsumexp((q @ k.transpose(-1, -2)) * 64 ** -0.5, -1) / math.log(2)
+    assert (lse.view(B, H, N) - lref).abs().max() < 1e-2  # the backward recomputes P from it
 
 
 def test_attention_fwd_full_length():
@@ -346,6 +349,77 @@ def test_attention_bwd(N, dt, attn_variant):
     for sl in (slice(0, C), slice(C, 2 * C), slice(2 * C, 3 * C)):
         err = float((dqkv[:, sl].float() - g[:, sl]).norm()) / max(float(g[:, sl].norm()), floor)
         assert err < tol, (sl, err)
+
+
+@pytest.fixture
+def bwd_kernel(request):
+    """0: CLS-split backward passes where N - 1 is a multiple of 256, 1: always the generic ones."""
+    from denseclip_vit_multimodal_amd import _native as N
+    N.call("dclip_set_option", N.OPT_ATTN_BWD_KERNEL, request.param)
+    yield request.param
+    N.call("dclip_set_option", N.OPT_ATTN_BWD_KERNEL, 0)
+
+
+def _attn_bwd_check(B, H, N, dt, spike=None):
+    O = ops()
+    C = 64 * H
+    qkv = torch.randn(B * N, 3 * C, device=DEV)
+    if spike is not None:  # one key (position, value) dominating every query
+        qkv[:, :C] = 1.0
+        qkv[spike[0], C:2 * C] = spike[1]
+    qkv, qref = prescale(qkv.to(dt), H)
+    dout = torch.randn(B * N, C, device=DEV).to(dt)
+    o, lse = O.attn_fwd(qkv, B, N, H, 64 ** -0.5)
+    dqkv = O.attn_bwd(qkv, o, dout, lse, B, N, H, 64 ** -0.5)
+    q32 = qref.clone().requires_grad_(True)
+    ref = attn_ref(q32, B, N, H)
+    ref.backward(dout.float())
+    g = q32.grad
+    errs = []
+    # N = 1-style floor (test_attention_bwd): gradients that cancel to ~0 are judged against |dout|
+    floor = 1e-3 * float(dout.float().norm())
+    for sl in (slice(0, C), slice(C, 2 * C), slice(2 * C, 3 * C)):
+        errs.append(float((dqkv[:, sl].float() - g[:, sl]).norm()) / max(float(g[:, sl].norm()), floor))
+        # the CLS row (query 0 / key 0, computed by the row-0 passes on the split path)
+        r0 = [i * N for i in range(B)]
+        errs.append(float((dqkv[r0, sl].float() - g[r0, sl]).norm()) / max(float(g[r0, sl].norm()), floor))
+    return errs
+
+
+@pytest.mark.parametrize("bwd_kernel", [0, 1], indirect=True)
+@pytest.mark.parametrize("N", [257, 513, 2049])
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+def test_attention_bwd_cls_split(N, dt, bwd_kernel):
+    errs = _attn_bwd_check(3, 2, N, dt)
+    assert max(errs) < 4 * TOL[dt], errs
+
+
+@pytest.fixture
+def bwd_kernel_pair():
+    from denseclip_vit_multimodal_amd import _native as N
+    yield lambda k: N.call("dclip_set_option", N.OPT_ATTN_BWD_KERNEL, k)
+    N.call("dclip_set_option", N.OPT_ATTN_BWD_KERNEL, 0)
+
+
+@pytest.mark.parametrize("where,spike", [(0, 4.0), (0, -20.0), (100, 4.0), (256, 8.0)])
+def test_attention_bwd_cls_split_spikes(where, spike, bwd_kernel_pair):
+    """One key dominating every query (at the CLS position, inside, at the end): dS = P (dP -
+    delta) cancels, so both backward variants carry the fp16 rounding of O in delta; the
+    CLS-split passes must be as accurate as the generic ones."""
+    res = []
+    for k in (1, 0):
+        bwd_kernel_pair(k)
+        torch.manual_seed(11)
+        res.append(_attn_bwd_check(1, 1, 257, torch.float16, spike=(where, spike)))
+    gen, split = res
+    for a, b in zip(split, gen):
+        assert a < 1.5 * b + 4 * TOL[torch.float16], (split, gen)
+
+
+def test_attention_bwd_full_length():
+    """N = 8193 (the benchmark's sequence) through the CLS-split passes, against fp32 autograd."""
+    errs = _attn_bwd_check(1, 1, 8193, torch.bfloat16)
+    assert max(errs) < 4 * TOL[torch.bfloat16], errs
 
 
 # ----------------------------------------------------------------------------- misc

@@ -14,7 +14,7 @@ from denseclip_vit_multimodal_amd import _native as N
 def declared_symbols():
     with open(os.path.join(ROOT, "include", "dclip.h")) as f:
         src = f.read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(dclip_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(dclip_\w+)\s*\(", src, re.M)))
 
 
 def test_header_and_binding_agree():

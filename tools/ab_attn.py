@@ -25,7 +25,7 @@ qkv = torch.randn(B * NT, 3 * C, device="cuda").to(torch.bfloat16)
 dout = torch.randn(B * NT, C, device="cuda").to(torch.bfloat16)
 o = torch.empty(B * NT, C, device="cuda", dtype=torch.bfloat16)
 lse = torch.empty(B * H * NT, device="cuda")
-delta = torch.empty(B * H * NT, device="cuda")
+delta = torch.empty(libs[0].dclip_attn_bwd_workspace(B, NT, H), device="cuda")
 dqkv = torch.empty_like(qkv)
 st = torch.cuda.current_stream().cuda_stream
 

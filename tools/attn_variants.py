@@ -15,7 +15,7 @@ from denseclip_vit_multimodal_amd import _native as N  # noqa: E402
 
 B, NT, C, H = 8, 8193, 768, 12
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-# variants: "fwd_waves,dq_waves,dkdv_waves[,dkdv_qs]" strings after the round count
+# variants: "fwd_waves,dq_waves,dkdv_waves[,dkdv_qs[,bwd_kernel]]" strings after the round count
 torch.manual_seed(0)
 qkv = torch.randn(B * NT, 3 * C, device="cuda").to(torch.bfloat16)
 dout = torch.randn(B * NT, C, device="cuda").to(torch.bfloat16)
@@ -34,7 +34,8 @@ def ev_time(fn, reps=3):
     return a.elapsed_time(b) / reps
 
 
-def setopt(fw, dq, dkdv, qs=0):
+def setopt(fw, dq, dkdv, qs=0, bk=0):
+    N.call("dclip_set_option", N.OPT_ATTN_BWD_KERNEL, bk)  # 0 CLS-split passes, 1 generic
     N.call("dclip_set_option", N.OPT_ATTN_DKDV_QS, qs)
     N.call("dclip_set_option", N.OPT_ATTN_FWD_WAVES, fw)
     N.call("dclip_set_option", N.OPT_ATTN_DQ_WAVES, dq)
