@@ -347,7 +347,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_kernel(const T* __re
 //     products), so the main loop sweeps keys 1..N-1 in full 64-key tiles: no mask, no clamp;
 //   * queries 1..N-1 form (N-1)/QB full query blocks.  (The generic kernel's extra block per
 //     (batch, head) computes ONE row at the cost of a full key sweep.)  Query 0 is a split-key
-//     VALU pass, one 64-key tile per wave (attn_row0_part_kernel), and a merge
+//     VALU pass, 1024 keys per workgroup (attn_row0_part_kernel), and a merge
 //     (attn_row0_merge_kernel) that runs before the main pass.  The partials are parked in o
 //     itself — rows 1.. of each batch, which the main pass overwrites afterwards — so the ABI
 //     needs no workspace.
@@ -913,44 +913,111 @@ __global__ __launch_bounds__(64 * NW, NB == 2 ? 1 : 8 / NW) void attn_fwd3_kerne
     }
 }
 
-// query 0 (CLS) against one 64-key tile per wave: partial (max, sum, o[64]) for the merge.
-// Partials of (b, h, split) live at o + b*N*C + C (row 1 of batch b, overwritten later by the
-// main pass), (h * nsplit + split) * 66 floats.
+// ---------------------------------------------------------------------------- row 0 (CLS) passes
+// Query 0 against every key (forward) and its backward partners are row-vector work: a
+// workgroup of 4 waves takes a chunk of R0_CHUNK keys (or queries), 8 lanes per row — 16 B
+// each of its 128-B head slice, so a wave-instruction reads 8 full lines — and 8 rows per
+// wave-instruction; the 8 lane groups are merged by shuffles and every wave leaves one
+// partial in a workspace, which a one-workgroup-per-(b, h) merge sums in a fixed order.
+constexpr int R0_CHUNK = 1024;
+constexpr int R0_PARTS = 4;  // partials per chunk (one per wave)
+
+__device__ __forceinline__ float grp8_sum(float v) {  // over the 8 lanes of an aligned group
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    v += __shfl_xor(v, 4, 64);
+    return v;
+}
+__device__ __forceinline__ float grps_sum(float v) {  // over the 8 groups of the wave
+    v += __shfl_xor(v, 8, 64);
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    return v;
+}
 template <typename T>
-__global__ __launch_bounds__(64) void attn_row0_part_kernel(const T* __restrict__ qkv, T* __restrict__ out, int N,
+__device__ __forceinline__ float dot8(const float (&a)[8], const T __attribute__((ext_vector_type(8))) & b) {
+    float d = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) d += a[e] * (float)b[e];
+    return d;
+}
+template <typename T>
+__device__ __forceinline__ void load8f(const T* p, float (&f)[8]) {
+    typedef T t8 __attribute__((ext_vector_type(8)));
+    const t8 v = *(const t8*)p;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = (float)v[e];
+}
+// lanes 8g + sub of group g = 0 store the wave's 64-float vector v (8 per lane) at dst
+__device__ __forceinline__ void store_grp0(float* dst, const float (&v)[8], int lane) {
+    if (lane < 8) {
+        *(f32x4*)(dst + lane * 8) = f32x4{v[0], v[1], v[2], v[3]};
+        *(f32x4*)(dst + lane * 8 + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    }
+}
+
+// Forward: partial (max, sum, o[64]) of query 0 over the wave's 256 keys, online softmax per
+// lane group over 4 batches of 8 keys.  Partials of (b, h, part) are parked in o + b*N*C + C
+// (rows 1.. of batch b, rewritten later by the main pass), (h * nparts + part) * 66 floats.
+template <typename T>
+__global__ __launch_bounds__(256) void attn_row0_part_kernel(const T* __restrict__ qkv, T* __restrict__ out, int N,
                                                             int H, int nsplit) {
-    const int lane = threadIdx.x;
+    typedef T t8 __attribute__((ext_vector_type(8)));
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int sub = lane & 7, grp = lane >> 3;
     const int sp = blockIdx.x % nsplit, bh = blockIdx.x / nsplit, b = bh / H, hd = bh % H;
     const int C = H * HD;
     const int64_t ld = 3 * (int64_t)C;
-    const T* Bb = qkv + (int64_t)b * N * ld;
-    const int key = sp * 64 + lane;
-    const int kc = key < N ? key : N - 1;
-    typedef T t8 __attribute__((ext_vector_type(8)));
-    const T* q0 = Bb + hd * HD;
-    const T* kr = Bb + (int64_t)kc * ld + C + hd * HD;
-    float s = 0.f;
+    const T* Bb = qkv + (int64_t)b * N * ld + hd * HD + sub * 8;
+    float qf[8];
+    load8f(Bb, qf);
+    float m = -INFINITY, l = 0.f, o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int kb = sp * R0_CHUNK + wave * (R0_CHUNK / R0_PARTS) + grp;
+#pragma unroll 1
+    for (int c = 0; c < R0_CHUNK / R0_PARTS / 64; ++c) {
+        t8 ka[8], va[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const t8 qa = *(const t8*)(q0 + 8 * i);
-        const t8 ka = *(const t8*)(kr + 8 * i);
+        for (int i = 0; i < 8; ++i) {
+            const int key = kb + (c * 8 + i) * 8;
+            const int64_t kc = key < N ? key : N - 1;
+            ka[i] = *(const t8*)(Bb + kc * ld + C);
+            va[i] = *(const t8*)(Bb + kc * ld + 2 * C);
+        }
+        float sc[8], mc = m;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) s += (float)qa[j] * (float)ka[j];
+        for (int i = 0; i < 8; ++i) {
+            const float d = grp8_sum(dot8<T>(qf, ka[i]));
+            sc[i] = kb + (c * 8 + i) * 8 < N ? d : -INFINITY;
+            mc = fmaxf(mc, sc[i]);
+        }
+        if (mc > -INFINITY) {  // uniform over the lane group
+            const float a = __builtin_amdgcn_exp2f(m - mc);
+            l *= a;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] *= a;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float p = __builtin_amdgcn_exp2f(sc[i] - mc);
+                l += p;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) o[e] += p * (float)va[i][e];
+            }
+            m = mc;
+        }
     }
-    if (key >= N) s = -INFINITY;
-    const float mt = wave_max(s);
-    const float p = __builtin_amdgcn_exp2f(s - mt);
-    const float lt = wave_sum(p);
-    // o[d = lane] = sum_k p_k V[k][d]
-    const int nk = min(64, N - sp * 64);
-    const T* vcol = Bb + (int64_t)(sp * 64) * ld + 2 * C + hd * HD + lane;
-    float o = 0.f;
-    for (int k = 0; k < nk; ++k) o += __shfl(p, k, 64) * (float)vcol[(int64_t)k * ld];
-    float* ws = (float*)(out + (int64_t)b * N * C + C) + (int64_t)(hd * nsplit + sp) * 66;
-    ws[2 + lane] = o;
+    float mw = fmaxf(m, __shfl_xor(m, 8, 64));
+    mw = fmaxf(mw, __shfl_xor(mw, 16, 64));
+    mw = fmaxf(mw, __shfl_xor(mw, 32, 64));
+    const float a = m > -INFINITY ? __builtin_amdgcn_exp2f(m - mw) : 0.f;
+    l = grps_sum(l * a);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = grps_sum(o[e] * a);
+    const int nparts = nsplit * R0_PARTS;
+    float* ws = (float*)(out + (int64_t)b * N * C + C) + (int64_t)(hd * nparts + sp * R0_PARTS + wave) * 66;
+    store_grp0(ws + 2, o, lane);
     if (lane == 0) {
-        ws[0] = mt;
-        ws[1] = lt;
+        ws[0] = mw;
+        ws[1] = l;
     }
 }
 
@@ -960,11 +1027,14 @@ __global__ __launch_bounds__(64) void attn_row0_merge_kernel(T* __restrict__ out
     const int lane = threadIdx.x;
     const int bh = blockIdx.x, b = bh / H, hd = bh % H;
     const int C = H * HD;
-    const float* ws = (const float*)(out + (int64_t)b * N * C + C) + (int64_t)hd * nsplit * 66;
+    const int nparts = nsplit * R0_PARTS;
+    const float* ws = (const float*)(out + (int64_t)b * N * C + C) + (int64_t)hd * nparts * 66;
     float M = -INFINITY;
-    for (int s = 0; s < nsplit; ++s) M = fmaxf(M, ws[s * 66]);
+#pragma unroll 4
+    for (int s = 0; s < nparts; ++s) M = fmaxf(M, ws[s * 66]);
     float L = 0.f, O = 0.f;
-    for (int s = 0; s < nsplit; ++s) {
+#pragma unroll 4
+    for (int s = 0; s < nparts; ++s) {
         const float w = __builtin_amdgcn_exp2f(ws[s * 66] - M);
         L += w * ws[s * 66 + 1];
         O += w * ws[s * 66 + 2 + lane];
@@ -1344,45 +1414,55 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq2_kernel(const T* 
 
 // ---------------------------------------------------------------------------- row 0 of the backward
 // Query 0 (the dQ row of the CLS token and its delta) and key 0 (the dK / dV rows of the CLS
-// token) for the CLS-split passes: split over 64-key (resp. 64-query) chunks, one wave per
-// chunk, lane = key (resp. query); partial sums in the workspace after delta (B*H*N floats),
-// at ws0 + (bh * nsplit + split) * 192: [0, 64) dQ_0, [64, 128) dK_0, [128, 192) dV_0; the
-// merges sum the chunks in a fixed order.
+// token) for the CLS-split passes, in the row-pass layout of the forward's (8 lanes per key or
+// query, R0_CHUNK rows per workgroup, one partial per wave); partials in the workspace after
+// delta (B*H*N floats), at ws0 + (bh * nparts + part) * 192: [0, 64) dQ_0, [64, 128) dK_0,
+// [128, 192) dV_0; the merges sum them in a fixed order.
+// query 0: dQ_0 += dS_k K_k, dS_k = exp2(q0 . k - L0) (dO0 . v_k - delta0)  (unscaled sums)
 template <typename T>
-__global__ __launch_bounds__(64) void attn_bwd_row0_dq_part(const T* __restrict__ qkv, const T* __restrict__ o,
+__global__ __launch_bounds__(256) void attn_bwd_row0_dq_part(const T* __restrict__ qkv, const T* __restrict__ o,
                                                             const T* __restrict__ dout, const float* __restrict__ lse,
                                                             float* __restrict__ ws0, int N, int H, int nsplit) {
-    const int lane = threadIdx.x;
+    typedef T t8 __attribute__((ext_vector_type(8)));
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int sub = lane & 7, grp = lane >> 3;
     const int sp = blockIdx.x % nsplit, bh = blockIdx.x / nsplit, b = bh / H, hd = bh % H;
     const int C = H * HD;
     const int64_t ld = 3 * (int64_t)C;
-    const T* Bb = qkv + (int64_t)b * N * ld + hd * HD;
-    const T* dO0 = dout + (int64_t)b * N * C + hd * HD;
-    const T* O0 = o + (int64_t)b * N * C + hd * HD;
+    const T* Bb = qkv + (int64_t)b * N * ld + hd * HD + sub * 8;
+    float qf[8], gf[8], of[8];
+    load8f(Bb, qf);
+    load8f(dout + (int64_t)b * N * C + hd * HD + sub * 8, gf);
+    load8f(o + (int64_t)b * N * C + hd * HD + sub * 8, of);
+    float d0 = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) d0 += gf[e] * of[e];
+    d0 = grp8_sum(d0);  // delta of query 0
     const float L0 = lse[(int64_t)bh * N];
-    const float d0 = wave_sum((float)dO0[lane] * (float)O0[lane]);  // delta of query 0
-    const int key = sp * 64 + lane;
-    const int kc = key < N ? key : N - 1;
-    typedef T t8 __attribute__((ext_vector_type(8)));
-    float s = 0.f, dp = 0.f;
+    float dq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int kb = sp * R0_CHUNK + wave * (R0_CHUNK / R0_PARTS) + grp;
+#pragma unroll 1
+    for (int c = 0; c < R0_CHUNK / R0_PARTS / 64; ++c) {
+        t8 ka[8], va[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const t8 qa = *(const t8*)(Bb + 8 * i);
-        const t8 ka = *(const t8*)(Bb + (int64_t)kc * ld + C + 8 * i);
-        const t8 ga = *(const t8*)(dO0 + 8 * i);
-        const t8 va = *(const t8*)(Bb + (int64_t)kc * ld + 2 * C + 8 * i);
+        for (int i = 0; i < 8; ++i) {
+            const int key = kb + (c * 8 + i) * 8;
+            const int64_t kc = key < N ? key : N - 1;
+            ka[i] = *(const t8*)(Bb + kc * ld + C);
+            va[i] = *(const t8*)(Bb + kc * ld + 2 * C);
+        }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            s += (float)qa[j] * (float)ka[j];
-            dp += (float)ga[j] * (float)va[j];
+        for (int i = 0; i < 8; ++i) {
+            const float sv = grp8_sum(dot8<T>(qf, ka[i]));
+            const float dp = grp8_sum(dot8<T>(gf, va[i]));
+            const float ds = kb + (c * 8 + i) * 8 < N ? __builtin_amdgcn_exp2f(sv - L0) * (dp - d0) : 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) dq[e] += ds * (float)ka[i][e];
         }
     }
-    const float ds = key < N ? __builtin_amdgcn_exp2f(s - L0) * (dp - d0) : 0.f;
-    const int nk = min(64, N - sp * 64);
-    const T* kcol = Bb + (int64_t)(sp * 64) * ld + C + lane;
-    float acc = 0.f;
-    for (int k = 0; k < nk; ++k) acc += __shfl(ds, k, 64) * (float)kcol[(int64_t)k * ld];
-    ws0[((int64_t)bh * nsplit + sp) * 192 + lane] = acc;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dq[e] = grps_sum(dq[e]);
+    store_grp0(ws0 + ((int64_t)bh * nsplit * R0_PARTS + sp * R0_PARTS + wave) * 192, dq, lane);
 }
 
 template <typename T>
@@ -1393,53 +1473,71 @@ __global__ __launch_bounds__(64) void attn_bwd_row0_dq_merge(const T* __restrict
     const int lane = threadIdx.x;
     const int bh = blockIdx.x, b = bh / H, hd = bh % H;
     const int C = H * HD;
+    const int nparts = nsplit * R0_PARTS;
     float acc = 0.f;
-    for (int sp = 0; sp < nsplit; ++sp) acc += ws0[((int64_t)bh * nsplit + sp) * 192 + lane];
+#pragma unroll 4
+    for (int s = 0; s < nparts; ++s) acc += ws0[((int64_t)bh * nparts + s) * 192 + lane];
     dqkv[(int64_t)b * N * 3 * C + hd * HD + lane] = (T)(acc * scale);
     const float d0 = wave_sum((float)dout[(int64_t)b * N * C + hd * HD + lane] * (float)o[(int64_t)b * N * C + hd * HD + lane]);
     if (lane == 0) delta[(int64_t)bh * N] = d0;
 }
 
-// key 0: lane = query q of the chunk; P = exp2(q . k0 - L_q), dS = P (dO_q . v0 - delta_q);
-// dV_0[d] += P dO_q[d], dK_0[d] += dS q[d]  (the unscaled sums; the merge applies the scales)
+// key 0: per query q, P = exp2(q . k0 - L_q), dS = P (dO_q . v0 - delta_q);
+// dV_0 += P dO_q, dK_0 += dS q  (the unscaled sums; the merge applies the scales)
 template <typename T>
-__global__ __launch_bounds__(64) void attn_bwd_row0_dkdv_part(const T* __restrict__ qkv, const T* __restrict__ dout,
+__global__ __launch_bounds__(256) void attn_bwd_row0_dkdv_part(const T* __restrict__ qkv, const T* __restrict__ dout,
                                                               const float* __restrict__ lse,
                                                               const float* __restrict__ delta,
                                                               float* __restrict__ ws0, int N, int H, int nsplit) {
-    const int lane = threadIdx.x;
+    typedef T t8 __attribute__((ext_vector_type(8)));
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int sub = lane & 7, grp = lane >> 3;
     const int sp = blockIdx.x % nsplit, bh = blockIdx.x / nsplit, b = bh / H, hd = bh % H;
     const int C = H * HD;
     const int64_t ld = 3 * (int64_t)C;
-    const T* Bb = qkv + (int64_t)b * N * ld + hd * HD;
-    const T* dOb = dout + (int64_t)b * N * C + hd * HD;
-    const int qr = sp * 64 + lane;
-    const int qc = qr < N ? qr : N - 1;
-    typedef T t8 __attribute__((ext_vector_type(8)));
-    float s = 0.f, dp = 0.f;
+    const T* Bb = qkv + (int64_t)b * N * ld + hd * HD + sub * 8;
+    const T* dOb = dout + (int64_t)b * N * C + hd * HD + sub * 8;
+    const float* Lb = lse + (int64_t)bh * N;
+    const float* Db = delta + (int64_t)bh * N;
+    float kf[8], vf[8];
+    load8f(Bb + C, kf);
+    load8f(Bb + 2 * C, vf);
+    float dk[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, dv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int qb = sp * R0_CHUNK + wave * (R0_CHUNK / R0_PARTS) + grp;
+#pragma unroll 1
+    for (int c = 0; c < R0_CHUNK / R0_PARTS / 64; ++c) {
+        t8 qa[8], ga[8];
+        float Lq[8], Dq[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const t8 qa = *(const t8*)(Bb + (int64_t)qc * ld + 8 * i);
-        const t8 ka = *(const t8*)(Bb + C + 8 * i);
-        const t8 ga = *(const t8*)(dOb + (int64_t)qc * C + 8 * i);
-        const t8 va = *(const t8*)(Bb + 2 * C + 8 * i);
+        for (int i = 0; i < 8; ++i) {
+            const int q = qb + (c * 8 + i) * 8;
+            const int64_t qc = q < N ? q : N - 1;
+            qa[i] = *(const t8*)(Bb + qc * ld);
+            ga[i] = *(const t8*)(dOb + qc * C);
+            Lq[i] = Lb[qc];
+            Dq[i] = Db[qc];
+        }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            s += (float)qa[j] * (float)ka[j];
-            dp += (float)ga[j] * (float)va[j];
+        for (int i = 0; i < 8; ++i) {
+            const float sv = grp8_sum(dot8<T>(kf, qa[i]));
+            const float dp = grp8_sum(dot8<T>(vf, ga[i]));
+            const float p = qb + (c * 8 + i) * 8 < N ? __builtin_amdgcn_exp2f(sv - Lq[i]) : 0.f;
+            const float ds = p * (dp - Dq[i]);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                dk[e] += ds * (float)qa[i][e];
+                dv[e] += p * (float)ga[i][e];
+            }
         }
     }
-    const float p = qr < N ? __builtin_amdgcn_exp2f(s - lse[(int64_t)bh * N + qc]) : 0.f;
-    const float ds = p * (dp - delta[(int64_t)bh * N + qc]);
-    const int nq = min(64, N - sp * 64);
-    float ak = 0.f, av = 0.f;
-    for (int k = 0; k < nq; ++k) {
-        const int64_t row = sp * 64 + k;
-        ak += __shfl(ds, k, 64) * (float)Bb[row * ld + lane];
-        av += __shfl(p, k, 64) * (float)dOb[row * C + lane];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        dk[e] = grps_sum(dk[e]);
+        dv[e] = grps_sum(dv[e]);
     }
-    ws0[((int64_t)bh * nsplit + sp) * 192 + 64 + lane] = ak;
-    ws0[((int64_t)bh * nsplit + sp) * 192 + 128 + lane] = av;
+    float* w = ws0 + ((int64_t)bh * nsplit * R0_PARTS + sp * R0_PARTS + wave) * 192;
+    store_grp0(w + 64, dk, lane);
+    store_grp0(w + 128, dv, lane);
 }
 
 template <typename T>
@@ -1448,10 +1546,12 @@ __global__ __launch_bounds__(64) void attn_bwd_row0_dkdv_merge(const float* __re
     const int lane = threadIdx.x;
     const int bh = blockIdx.x, b = bh / H, hd = bh % H;
     const int C = H * HD;
+    const int nparts = nsplit * R0_PARTS;
     float ak = 0.f, av = 0.f;
-    for (int sp = 0; sp < nsplit; ++sp) {
-        ak += ws0[((int64_t)bh * nsplit + sp) * 192 + 64 + lane];
-        av += ws0[((int64_t)bh * nsplit + sp) * 192 + 128 + lane];
+#pragma unroll 4
+    for (int s = 0; s < nparts; ++s) {
+        ak += ws0[((int64_t)bh * nparts + s) * 192 + 64 + lane];
+        av += ws0[((int64_t)bh * nparts + s) * 192 + 128 + lane];
     }
     T* row = dqkv + (int64_t)b * N * 3 * C + hd * HD;
     row[C + lane] = (T)(ak * dk_scale);
@@ -1861,8 +1961,8 @@ template <typename T, int NW>
 bool fwd2_launch_nw(const void* qkv, void* o, float* lse, int B, int N, int H, hipStream_t st) {
     constexpr int QB = 32 * NW;
     if (N < 1 + QB || (N - 1) % QB != 0) return false;
-    const int nsplit = (N + 63) / 64;
-    attn_row0_part_kernel<T><<<B * H * nsplit, 64, 0, st>>>((const T*)qkv, (T*)o, N, H, nsplit);
+    const int nsplit = (N + R0_CHUNK - 1) / R0_CHUNK;
+    attn_row0_part_kernel<T><<<B * H * nsplit, 256, 0, st>>>((const T*)qkv, (T*)o, N, H, nsplit);
     attn_row0_merge_kernel<T><<<B * H, 64, 0, st>>>((T*)o, lse, N, H, nsplit);
     const dim3 grid(B * H * ((N - 1) / QB));
     attn_fwd2_kernel<T, NW><<<grid, 64 * NW, 0, st>>>((const T*)qkv, (T*)o, lse, N, H);
@@ -1873,8 +1973,8 @@ bool fwd2_launch_nw(const void* qkv, void* o, float* lse, int B, int N, int H, h
 template <typename T, int NW, int NB>
 bool fwd3_launch(const void* qkv, void* o, float* lse, int B, int N, int H, hipStream_t st) {
     if (N < 257 || (N - 1) % 256 != 0) return false;
-    const int nsplit = (N + 63) / 64;
-    attn_row0_part_kernel<T><<<B * H * nsplit, 64, 0, st>>>((const T*)qkv, (T*)o, N, H, nsplit);
+    const int nsplit = (N + R0_CHUNK - 1) / R0_CHUNK;
+    attn_row0_part_kernel<T><<<B * H * nsplit, 256, 0, st>>>((const T*)qkv, (T*)o, N, H, nsplit);
     attn_row0_merge_kernel<T><<<B * H, 64, 0, st>>>((T*)o, lse, N, H, nsplit);
     attn_fwd3_kernel<T, NW, NB><<<B * H * ((N - 1) / 256), 64 * NW, 0, st>>>((const T*)qkv, (T*)o, lse, N, H);
     return true;
@@ -1899,15 +1999,15 @@ template <typename T>
 bool bwd2_launch(const void* qkv, const void* o, const void* dout, const float* lse, float* delta, void* dqkv, int B,
                  int N, int H, float scale, hipStream_t st) {
     if (N < 257 || (N - 1) % 256 != 0 || dclip_option(DCLIP_OPT_ATTN_BWD_KERNEL) == 1) return false;
-    const int nsplit = (N + 63) / 64;
+    const int nsplit = (N + R0_CHUNK - 1) / R0_CHUNK;
     float* ws0 = delta + (int64_t)B * H * N;
-    attn_bwd_row0_dq_part<T><<<B * H * nsplit, 64, 0, st>>>((const T*)qkv, (const T*)o, (const T*)dout, lse, ws0, N, H,
+    attn_bwd_row0_dq_part<T><<<B * H * nsplit, 256, 0, st>>>((const T*)qkv, (const T*)o, (const T*)dout, lse, ws0, N, H,
                                                             nsplit);
     attn_bwd_row0_dq_merge<T><<<B * H, 64, 0, st>>>((const T*)o, (const T*)dout, ws0, delta, (T*)dqkv, N, H, nsplit,
                                                     scale);
     attn_bwd_dq2_kernel<T, 8><<<B * H * ((N - 1) / 256), 512, 0, st>>>((const T*)qkv, (const T*)o, (const T*)dout, lse,
                                                                       delta, (T*)dqkv, N, H, scale);
-    attn_bwd_row0_dkdv_part<T><<<B * H * nsplit, 64, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, ws0, N, H,
+    attn_bwd_row0_dkdv_part<T><<<B * H * nsplit, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, ws0, N, H,
                                                               nsplit);
     attn_bwd_row0_dkdv_merge<T><<<B * H, 64, 0, st>>>(ws0, (T*)dqkv, N, H, nsplit, 1.0f / LOG2E);
     attn_bwd_dkdv2_kernel<T, 4><<<B * H * ((N - 1) / 128), 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta,

@@ -456,6 +456,105 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_nt_big_kernel(
                                      C, ldc, C2, ldc2, slab, alpha);
 }
 
+// ---------------------------------------------------------------------------- ping-pong 256x256
+// The same 256x256 tile, 8 waves (2 x 4, 128 x 64 per wave) and 128 KiB of LDS as
+// gemm_nt_big_kernel, with the K-loop cut into phases of 16 MFMAs and the two wave groups
+// (rows 0-127 / 128-255 of the tile) run one barrier apart, so that on every SIMD (one wave
+// of each group) one wave's MFMAs overlap the other's fragment reads.
+//   * a 64-deep K-tile lives in the LDS as two K-halves of 32 (A 256 x 64 B + B 256 x 64 B
+//     each), 2 tiles resident: 4 half-slots of 32 KiB;
+//   * phases per K-tile: (rows 0-63 of the wave tile, K-half 0), (rows 64-127, K-half 0),
+//     (rows 0-63, K-half 1), (rows 64-127, K-half 1): 4 x 4 MFMA 16x16x32 each; B fragments
+//     are read at the first phase of a K-half and reused by the second;
+//   * K-half 0 of tile t+1 is issued (LDS-DMA, 4 per thread) at phase 0 of tile t, K-half 1
+//     at phase 2; each is retired by a counted vmcnt(4) two phases later — one phase before
+//     it is read — so the next K-half stays in flight across every barrier, and every
+//     half-slot is rewritten 3 phases after its last read (safe under the one-barrier stagger).
+template <typename T, int QM, bool LOADB>
+__device__ __forceinline__ void pp_phase(f32x4 (&acc)[4][8], typename Mfma<T>::frag (&fa)[4],
+                                         typename Mfma<T>::frag (&fb)[4], const char* half, int arow, int brow,
+                                         int lq) {
+    if constexpr (LOADB) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fb[i] = big_frag<T, 32>(half + 16384, brow + i * 16, lq);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fa[j] = big_frag<T, 32>(half, arow + QM * 64 + j * 16, lq);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this phase's fragments are in registers
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][QM * 4 + j] = Mfma16<T>::mma(fb[i], fa[j], acc[i][QM * 4 + j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <typename T, int EPI, typename OutT>
+__global__ __launch_bounds__(512, 1) void gemm_nt_pp_kernel(
+    const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
+    int M, int N, int k_chunk, int tiles_m, int tiles_n,
+    const float* __restrict__ bias, const void* __restrict__ aux, int64_t ld_aux,
+    void* __restrict__ C, int64_t ldc, void* __restrict__ C2, int64_t ldc2, int64_t slab, float alpha) {
+    typedef BigCfg<256, 256, 2, 4, 2, 64> Cfg;
+    typedef typename Mfma<T>::frag frag;
+    constexpr int HALF = 32768;
+    __shared__ __attribute__((aligned(16))) char smem[Cfg::SMEM];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wr = wave >> 2, wc = wave & 3;
+    const int l16 = lane & 15, lq = lane >> 4;
+    const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+    const int m0 = (t / tiles_n) * 256;
+    const int n0 = (t % tiles_n) * 256;
+    const int kbeg = blockIdx.y * k_chunk;
+    const int nk = k_chunk / 64;
+    const int arow = wr * 128 + l16, brow = wc * 64 + l16;
+
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    frag fa[4], fb[4];
+
+    auto stage = [&](int kt, int kh) {
+        char* base = smem + ((kt & 1) * 2 + kh) * HALF;
+        const int k0 = kbeg + kt * 64 + kh * 32;
+        stage_rows<T, 2, 32>(A, lda, m0, M, k0, base, wave, lane);
+        stage_rows<T, 2, 32>(B, ldb, n0, N, k0, base + 16384, wave, lane);
+    };
+    stage(0, 0);
+    stage(0, 1);
+    wait_vmcnt<4>();  // K-half 0 of tile 0 landed (K-half 1 in flight)
+    __builtin_amdgcn_s_barrier();
+    if (wr == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind group 0
+
+    for (int kt = 0; kt < nk; ++kt) {
+        const char* h0 = smem + (kt & 1) * 2 * HALF;
+        const char* h1 = h0 + HALF;
+        const bool more = kt + 1 < nk;
+        if (more) stage(kt + 1, 0);
+        pp_phase<T, 0, true>(acc, fa, fb, h0, arow, brow, lq);
+        if (more) wait_vmcnt<4>();  // K-half 1 of tile kt (read from the next phase on)
+        else wait_vmcnt<0>();
+        pp_phase<T, 1, false>(acc, fa, fb, h0, arow, brow, lq);
+        if (more) stage(kt + 1, 1);
+        pp_phase<T, 0, true>(acc, fa, fb, h1, arow, brow, lq);
+        if (more) wait_vmcnt<4>();  // K-half 0 of tile kt+1
+        pp_phase<T, 1, false>(acc, fa, fb, h1, arow, brow, lq);
+    }
+    if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
+
+    big_epilogue<T, EPI, OutT, Cfg>(acc, smem, M, N, m0 + wr * 128, n0 + wc * 64, bias, aux, ld_aux, C, ldc, C2, ldc2,
+                                     slab, alpha);
+}
+
 // ---------------------------------------------------------------------------- "TN"
 // C[m][n] = sum_k A[k][m] * B[k][n]: both operands row-major with the reduction index on
 // the ROWS — the weight-gradient shape dW = dY^T X (k = token, m/n = features).  Tiles of
@@ -1006,7 +1105,8 @@ __global__ void tail_combine_kernel(const float* __restrict__ ws, int splits, in
     epi_row8<T, EPI, OutT>(v, (int)(m0 + r), nb, N, bias, aux, ld_aux, C, ldc, C2, ldc2, 0);
 }
 
-template <typename T, int EPI, typename OutT, int TBM, int TBN, int WM, int WN, int STAGES, int BKT = 64>
+template <typename T, int EPI, typename OutT, int TBM, int TBN, int WM, int WN, int STAGES, int BKT = 64,
+          bool PP = false>
 void launch_big(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
                 int splits, float alpha, const float* bias, const void* aux, int64_t ld_aux, void* C, int64_t ldc,
                 void* C2, int64_t ldc2, hipStream_t st) {
@@ -1044,14 +1144,22 @@ void launch_big(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t 
         }
     }
     dim3 grid(tiles_m * tiles_n, splits);
-    gemm_nt_big_kernel<T, EPI, OutT, TBM, TBN, WM, WN, STAGES, BKT><<<grid, 64 * WM * WN, 0, st>>>(
-        (const T*)A, lda, (const T*)B, ldb, (int)M, (int)N, (int)(K / splits), tiles_m, tiles_n, bias, aux, ld_aux,
-        C, ldc, C2, ldc2, (int64_t)M * N, alpha);
+    if constexpr (PP) {
+        static_assert(TBM == 256 && TBN == 256 && WM == 2 && WN == 4, "ping-pong geometry");
+        gemm_nt_pp_kernel<T, EPI, OutT><<<grid, 512, 0, st>>>(
+            (const T*)A, lda, (const T*)B, ldb, (int)M, (int)N, (int)(K / splits), tiles_m, tiles_n, bias, aux, ld_aux,
+            C, ldc, C2, ldc2, (int64_t)M * N, alpha);
+    } else {
+        gemm_nt_big_kernel<T, EPI, OutT, TBM, TBN, WM, WN, STAGES, BKT><<<grid, 64 * WM * WN, 0, st>>>(
+            (const T*)A, lda, (const T*)B, ldb, (int)M, (int)N, (int)(K / splits), tiles_m, tiles_n, bias, aux,
+            ld_aux, C, ldc, C2, ldc2, (int64_t)M * N, alpha);
+    }
 }
 
 // tile configuration: DCLIP_OPT_GEMM_TILE 1 = 128x128 (4 waves, 2 workgroups/CU), 2 = 256x256
 // (8 waves, 2-stage ring of 64-deep k-tiles), 3 = 256x128 (8 waves, 3-stage ring),
-// 4 = 256x256 with a 4-stage ring of 32-deep k-tiles, 0 = automatic
+// 4 = 256x256 with a 4-stage ring of 32-deep k-tiles, 5 = 256x256 ping-pong (gemm_nt_pp_kernel),
+// 0 = automatic
 inline int gemm_tile_choice(int64_t M, int64_t N) {
     const int opt = dclip_option(DCLIP_OPT_GEMM_TILE);
     if (opt != 0) return opt;
@@ -1072,6 +1180,11 @@ int launch(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, in
     if (choice == 3) {
         launch_big<T, EPI, OutT, 256, 128, 4, 2, 3>(A, lda, B, ldb, M, N, K, splits, alpha, bias, aux, ld_aux, C,
                                                     ldc, C2, ldc2, st);
+        return 0;
+    }
+    if (choice == 5) {
+        launch_big<T, EPI, OutT, 256, 256, 2, 4, 2, 64, true>(A, lda, B, ldb, M, N, K, splits, alpha, bias, aux,
+                                                              ld_aux, C, ldc, C2, ldc2, st);
         return 0;
     }
     if (choice == 4) {

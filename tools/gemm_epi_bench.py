@@ -2,7 +2,7 @@
 GEMM with the plain bf16 STORE epilogue, at the bench shape (M = 8 x 8193), interleaved rounds —
 isolates what each fused epilogue costs.
 
-  python tools/gemm_epi_bench.py [rounds] [tile]
+  python tools/gemm_epi_bench.py [rounds] [tile,tile,...]   (DCLIP_OPT_GEMM_TILE values, A/B'd)
 """
 import os
 import sys
@@ -16,8 +16,7 @@ from denseclip_vit_multimodal_amd import _native as N  # noqa: E402
 M, C, H = 8 * 8193, 768, 12
 bf = torch.bfloat16
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-if len(sys.argv) > 2:
-    N.call("dclip_set_option", N.OPT_GEMM_TILE, int(sys.argv[2]))
+tiles = [int(t) for t in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0]
 torch.manual_seed(0)
 
 
@@ -55,13 +54,17 @@ cases = [
     ("dxh2 STORE f32", lambda: O.gemm(a3072, w2, out_dtype=torch.float32), lambda: O.gemm(a3072, w2),
      2.0 * M * 4 * C * C),
 ]
-res = {c[0]: ([], []) for c in cases}
+res = {(c[0], t): ([], []) for c in cases for t in tiles}
 for r in range(rounds):
     for name, epi, plain, fl in cases:
-        res[name][0].append(ev(epi))
-        res[name][1].append(ev(plain))
+        for t in tiles:
+            N.call("dclip_set_option", N.OPT_GEMM_TILE, t)
+            res[(name, t)][0].append(ev(epi))
+            res[(name, t)][1].append(ev(plain))
+N.call("dclip_set_option", N.OPT_GEMM_TILE, 0)
 for name, epi, plain, fl in cases:
-    e = sorted(res[name][0])[rounds // 2]
-    p = sorted(res[name][1])[rounds // 2]
-    print(f"{name:18s} epilogue {e:7.3f} ms {fl / e / 1e9:7.1f} TF/s | plain bf16 store {p:7.3f} ms "
-          f"{fl / p / 1e9:7.1f} TF/s", flush=True)
+    for t in tiles:
+        e = sorted(res[(name, t)][0])[rounds // 2]
+        p = sorted(res[(name, t)][1])[rounds // 2]
+        print(f"tile {t} {name:18s} epilogue {e:7.3f} ms {fl / e / 1e9:7.1f} TF/s | plain bf16 store {p:7.3f} ms "
+              f"{fl / p / 1e9:7.1f} TF/s", flush=True)

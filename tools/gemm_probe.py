@@ -8,6 +8,8 @@ import torch  # noqa: E402
 from denseclip_vit_multimodal_amd import ops as O  # noqa: E402
 from denseclip_vit_multimodal_amd import _native as N  # noqa: E402
 
+if os.environ.get("GEMM_TILE"):
+    N.call("dclip_set_option", N.OPT_GEMM_TILE, int(os.environ["GEMM_TILE"]))
 M, C = 8 * 8193, 768
 bf = torch.bfloat16
 x = torch.randn(M, C, device="cuda").to(bf)

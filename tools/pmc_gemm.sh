@@ -1,5 +1,5 @@
 #!/bin/bash
-# PMC passes over tools/gemm_probe.py:  bash tools/pmc_gemm.sh out_dir
+# PMC passes over tools/gemm_probe.py:  bash tools/pmc_gemm.sh out_dir   (GEMM_TILE env passes through)
 set -e
 export TMPDIR=/tmp
 OUT=${1:-gpurun_out/pmc_gemm}
