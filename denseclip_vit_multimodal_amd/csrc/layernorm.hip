@@ -84,11 +84,17 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const TX* __restrict__ x, c
     }
 }
 
+// optional 16-bit copy of the backward's output (the next GEMM's operand): lp_dt F16 / BF16
+__device__ __forceinline__ void store_lp(void* lp, int lp_dt, int64_t off, const float* o) {
+    if (lp_dt == DCLIP_BF16) store4((bf16*)lp + off, o);
+    else store4((f16*)lp + off, o);
+}
+
 template <typename TDY, typename TX>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const TDY* __restrict__ dy, const TX* __restrict__ x,
                                                      const float* __restrict__ w, const float* __restrict__ mean,
-                                                     const float* __restrict__ rstd, float* __restrict__ dx,
-                                                     int accumulate, float* __restrict__ dw,
+                                                     const float* __restrict__ rstd, const float* res, float* dx,
+                                                     void* __restrict__ lp, int lp_dt, float* __restrict__ dw,
                                                      float* __restrict__ db, int64_t rows, int cols) {
     __shared__ float red[2][4][64];
     const int lane = threadIdx.x & 63;
@@ -138,12 +144,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TDY* __restrict__ dy,
                     const int k = 4 * i + e;
                     o[e] = rs * (g[k] - mg - xh[k] * mgx);
                 }
-                float* d = dx + row * cols + c;
-                if (accumulate) {
-                    f32x4 old = *(f32x4*)d;
+                if (res) {
+                    const f32x4 old = *(const f32x4*)(res + row * cols + c);
                     o[0] += old[0]; o[1] += old[1]; o[2] += old[2]; o[3] += old[3];
                 }
-                store4(d, o);
+                store4(dx + row * cols + c, o);
+                if (lp) store_lp(lp, lp_dt, row * cols + c, o);
             }
         }
     }
@@ -230,9 +236,9 @@ __global__ __launch_bounds__(256) void ln_fwd_fast(const TX* __restrict__ x, con
 template <typename TDY, typename TX, int NV>
 __global__ __launch_bounds__(512) void ln_bwd_fast(const TDY* __restrict__ dy, const TX* __restrict__ x,
                                                    const float* __restrict__ w, const float* __restrict__ mean,
-                                                   const float* __restrict__ rstd, float* __restrict__ dx,
-                                                   int accumulate, float* __restrict__ dw, float* __restrict__ db,
-                                                   int64_t rows) {
+                                                   const float* __restrict__ rstd, const float* res, float* dx,
+                                                   void* __restrict__ lp, int lp_dt, float* __restrict__ dw,
+                                                   float* __restrict__ db, int64_t rows) {
     constexpr int cols = 256 * NV;
     __shared__ float red[8][2][4 * NV][64];
     const int lane = threadIdx.x & 63;
@@ -253,7 +259,7 @@ __global__ __launch_bounds__(512) void ln_bwd_fast(const TDY* __restrict__ dy, c
         for (int i = 0; i < NV; ++i) {
             load4(dy + row * cols + 4 * lane + 256 * i, dv + 4 * i);
             load4(x + row * cols + 4 * lane + 256 * i, xv + 4 * i);
-            if (accumulate) load4(dx + row * cols + 4 * lane + 256 * i, old + 4 * i);
+            if (res) load4(res + row * cols + 4 * lane + 256 * i, old + 4 * i);
         }
         mu = mean[row];
         rs = rstd[row];
@@ -265,7 +271,7 @@ __global__ __launch_bounds__(512) void ln_bwd_fast(const TDY* __restrict__ dy, c
             for (int i = 0; i < NV; ++i) {
                 load4(dy + nrow * cols + 4 * lane + 256 * i, ndv + 4 * i);
                 load4(x + nrow * cols + 4 * lane + 256 * i, nxv + 4 * i);
-                if (accumulate) load4(dx + nrow * cols + 4 * lane + 256 * i, nold + 4 * i);
+                if (res) load4(res + nrow * cols + 4 * lane + 256 * i, nold + 4 * i);
             }
             nmu = mean[nrow];
             nrs = rstd[nrow];
@@ -290,9 +296,10 @@ __global__ __launch_bounds__(512) void ln_bwd_fast(const TDY* __restrict__ dy, c
             for (int e = 0; e < 4; ++e) {
                 const int k = 4 * i + e;
                 o[e] = rs * (dv[k] * wl[k] - mg - xv[k] * mgx);
-                if (accumulate) o[e] += old[k];
+                if (res) o[e] += old[k];
             }
             store4(dx + row * cols + 4 * lane + 256 * i, o);
+            if (lp) store_lp(lp, lp_dt, row * cols + 4 * lane + 256 * i, o);
         }
         row = nrow;
         mu = nmu;
@@ -336,12 +343,12 @@ void fwd_fast(const void* x, const float* w, const float* b, void* y, float* mea
 }
 
 template <typename TDY, typename TX, int NV>
-void bwd_fast(const void* dy, const void* x, const float* w, const float* mean, const float* rstd, float* dx, int acc,
-              float* dw, float* db, int64_t rows, hipStream_t st) {
+void bwd_fast(const void* dy, const void* x, const float* w, const float* mean, const float* rstd, const float* res,
+              float* dx, void* lp, int lp_dt, float* dw, float* db, int64_t rows, hipStream_t st) {
     int64_t blocks = (rows + 7) / 8;
     blocks = blocks > 512 ? 512 : blocks;
-    ln_bwd_fast<TDY, TX, NV><<<(unsigned)blocks, 512, 0, st>>>((const TDY*)dy, (const TX*)x, w, mean, rstd, dx, acc,
-                                                              dw, db, rows);
+    ln_bwd_fast<TDY, TX, NV><<<(unsigned)blocks, 512, 0, st>>>((const TDY*)dy, (const TX*)x, w, mean, rstd, res, dx,
+                                                              lp, lp_dt, dw, db, rows);
 }
 
 template <typename TX, typename TY>
@@ -367,26 +374,27 @@ void fwd_dispatch_y(int y_dt, const void* x, const float* w, const float* b, voi
 
 template <typename TDY, typename TX>
 void bwd_launch(const void* dy, const void* x, const float* w, const float* mean, const float* rstd,
-                float* dx, int acc, float* dw, float* db, int64_t rows, int cols, hipStream_t st) {
+                const float* res, float* dx, void* lp, int lp_dt, float* dw, float* db, int64_t rows, int cols,
+                hipStream_t st) {
     switch (cols) {
-        case 512: return bwd_fast<TDY, TX, 2>(dy, x, w, mean, rstd, dx, acc, dw, db, rows, st);
-        case 768: return bwd_fast<TDY, TX, 3>(dy, x, w, mean, rstd, dx, acc, dw, db, rows, st);
-        case 1024: return bwd_fast<TDY, TX, 4>(dy, x, w, mean, rstd, dx, acc, dw, db, rows, st);
+        case 512: return bwd_fast<TDY, TX, 2>(dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, rows, st);
+        case 768: return bwd_fast<TDY, TX, 3>(dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, rows, st);
+        case 1024: return bwd_fast<TDY, TX, 4>(dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, rows, st);
         default: break;
     }
     int64_t blocks = (rows + 3) / 4;
     if (blocks > 1024) blocks = 1024;
     ln_bwd_kernel<TDY, TX><<<(unsigned)blocks, 256, 0, st>>>((const TDY*)dy, (const TX*)x, w, mean, rstd,
-                                                             dx, acc, dw, db, rows, cols);
+                                                             res, dx, lp, lp_dt, dw, db, rows, cols);
 }
 
 template <typename TDY>
 void bwd_dispatch_x(int x_dt, const void* dy, const void* x, const float* w, const float* mean,
-                    const float* rstd, float* dx, int acc, float* dw, float* db, int64_t rows, int cols,
-                    hipStream_t st) {
-    if (x_dt == DCLIP_F32) bwd_launch<TDY, float>(dy, x, w, mean, rstd, dx, acc, dw, db, rows, cols, st);
-    else if (x_dt == DCLIP_F16) bwd_launch<TDY, f16>(dy, x, w, mean, rstd, dx, acc, dw, db, rows, cols, st);
-    else bwd_launch<TDY, bf16>(dy, x, w, mean, rstd, dx, acc, dw, db, rows, cols, st);
+                    const float* rstd, const float* res, float* dx, void* lp, int lp_dt, float* dw, float* db,
+                    int64_t rows, int cols, hipStream_t st) {
+    if (x_dt == DCLIP_F32) bwd_launch<TDY, float>(dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, rows, cols, st);
+    else if (x_dt == DCLIP_F16) bwd_launch<TDY, f16>(dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, rows, cols, st);
+    else bwd_launch<TDY, bf16>(dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, rows, cols, st);
 }
 
 }  // namespace
@@ -406,16 +414,27 @@ extern "C" int dclip_layernorm_fwd(const void* x, int x_dt, const float* w, cons
     return 0;
 }
 
+extern "C" int dclip_layernorm_bwd_res(const void* dy, int dy_dt, const void* x, int x_dt, const float* w,
+                                       const float* mean, const float* rstd, const float* res, float* dx, void* lp,
+                                       int lp_dt, float* dw, float* db, int64_t rows, int64_t cols, void* stream) {
+    DCLIP_HOST_CHECK(cols > 0 && cols % 4 == 0 && cols <= 64 * MAXV,
+                     "dclip_layernorm_bwd: cols=%lld must be a multiple of 4 and <= %d", (long long)cols, 64 * MAXV);
+    DCLIP_HOST_CHECK(lp == nullptr || lp_dt == DCLIP_BF16 || lp_dt == DCLIP_F16,
+                     "dclip_layernorm_bwd_res: lp_dt must be F16 or BF16");
+    if (rows == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    if (dy_dt == DCLIP_F32)
+        bwd_dispatch_x<float>(x_dt, dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, rows, (int)cols, st);
+    else if (dy_dt == DCLIP_F16)
+        bwd_dispatch_x<f16>(x_dt, dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, rows, (int)cols, st);
+    else bwd_dispatch_x<bf16>(x_dt, dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, rows, (int)cols, st);
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
+
 extern "C" int dclip_layernorm_bwd(const void* dy, int dy_dt, const void* x, int x_dt, const float* w,
                                    const float* mean, const float* rstd, float* dx, int accumulate,
                                    float* dw, float* db, int64_t rows, int64_t cols, void* stream) {
-    DCLIP_HOST_CHECK(cols > 0 && cols % 4 == 0 && cols <= 64 * MAXV,
-                     "dclip_layernorm_bwd: cols=%lld must be a multiple of 4 and <= %d", (long long)cols, 64 * MAXV);
-    if (rows == 0) return 0;
-    hipStream_t st = (hipStream_t)stream;
-    if (dy_dt == DCLIP_F32) bwd_dispatch_x<float>(x_dt, dy, x, w, mean, rstd, dx, accumulate, dw, db, rows, (int)cols, st);
-    else if (dy_dt == DCLIP_F16) bwd_dispatch_x<f16>(x_dt, dy, x, w, mean, rstd, dx, accumulate, dw, db, rows, (int)cols, st);
-    else bwd_dispatch_x<bf16>(x_dt, dy, x, w, mean, rstd, dx, accumulate, dw, db, rows, (int)cols, st);
-    DCLIP_LAUNCH_CHECK();
-    return 0;
+    return dclip_layernorm_bwd_res(dy, dy_dt, x, x_dt, w, mean, rstd, accumulate ? dx : nullptr, dx, nullptr, 0, dw,
+                                   db, rows, cols, stream);
 }

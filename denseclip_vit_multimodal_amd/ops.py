@@ -93,11 +93,15 @@ def layernorm_fwd(x2d, w, b, out_dtype, eps=1e-5, stats=True):
     return y, mean, rstd
 
 
-def layernorm_bwd(dy, x, w, mean, rstd, dx, accumulate, dw=None, db=None):
-    _check(dy, x, w, mean, rstd, dx, dw, db)
+def layernorm_bwd(dy, x, w, mean, rstd, dx, accumulate, dw=None, db=None, res=None, lp=None):
+    """dx (=, or += if accumulate) LN^T(dy); with res: dx = res + LN^T(dy) (accumulate ignored);
+    with lp: also lp = (lp.dtype) dx."""
+    _check(dy, x, w, mean, rstd, dx, dw, db, res, lp)
     rows, cols = x.shape
-    N.call("dclip_layernorm_bwd", _p(dy), _dt(dy), _p(x), _dt(x), _p(w), _p(mean), _p(rstd), _p(dx),
-           int(accumulate), _p(dw), _p(db), rows, cols, _stream())
+    if res is None and accumulate:
+        res = dx
+    N.call("dclip_layernorm_bwd_res", _p(dy), _dt(dy), _p(x), _dt(x), _p(w), _p(mean), _p(rstd), _p(res), _p(dx),
+           _p(lp), _dt(lp) if lp is not None else 0, _p(dw), _p(db), rows, cols, _stream())
 
 
 def gemm(A, B, epi=N.EPI_STORE, bias=None, aux=None, out_dtype=None, out=None, out2=None, alpha=1.0):
@@ -444,14 +448,20 @@ class BlockFn(torch.autograd.Function):
         if wg:
             dW1, db1 = weight_grad(dz, xh2, alpha=1.0 / s1)
         del dz
-        dxm = dxo.clone()
         dln2w = torch.zeros(C, dtype=torch.float32, device=x.device)
         dln2b = torch.zeros(C, dtype=torch.float32, device=x.device)
-        layernorm_bwd(dxh2, xm, ln2w.detach(), mu2, rs2, dxm, 1, dln2w, dln2b)
+        dxm = torch.empty_like(dxo)
+        if cdt == torch.bfloat16:  # no gradient scaling: the attention branch's operand comes out of the LN pass
+            dyo = torch.empty(dxo.shape, dtype=cdt, device=dxo.device)
+            layernorm_bwd(dxh2, xm, ln2w.detach(), mu2, rs2, dxm, 0, dln2w, dln2b, res=dxo, lp=dyo)
+            s2 = 1.0
+        else:
+            layernorm_bwd(dxh2, xm, ln2w.detach(), mu2, rs2, dxm, 0, dln2w, dln2b, res=dxo)
         del dxh2
         # ---- attention: xm = x + o Wout^T + bout
-        s2 = grad_scale(dxm, cdt)
-        dyo = cast(dxm, cdt, s2)
+        if cdt != torch.bfloat16:
+            s2 = grad_scale(dxm, cdt)
+            dyo = cast(dxm, cdt, s2)
         do = gemm(dyo, WEIGHTS.get(w_out, cdt, transposed=True))
         dWo = dbo = dWi = dbi = None
         if wg:

@@ -92,6 +92,14 @@ int dclip_layernorm_bwd(const void* dy, int dy_dt, const void* x, int x_dt,
                         const float* w, const float* mean, const float* rstd,
                         float* dx, int accumulate, float* dw, float* db,
                         int64_t rows, int64_t cols, void* stream);
+/* The same with the residual branch's gradient fused in: dx = res + LN^T(dy) (res f32, may be
+ * null or alias dx) and, when lp is non-null, a 16-bit copy lp = (lp_dt) dx (lp_dt F16 or
+ * BF16) — the next GEMM's operand, without a separate clone / cast pass (the
+ * x + f(LN(x)) residual of models.py:292-293, backward).                              */
+int dclip_layernorm_bwd_res(const void* dy, int dy_dt, const void* x, int x_dt,
+                            const float* w, const float* mean, const float* rstd,
+                            const float* res, float* dx, void* lp, int lp_dt, float* dw, float* db,
+                            int64_t rows, int64_t cols, void* stream);
 
 /* C[m][n] = alpha * sum_k A[m][k] * B[n][k]  ("NT": both operands k-contiguous, ab_dt in
  * {F16, BF16}), m < M, n < N, k < K (K % 64 == 0, lda/ldb % 8 == 0), then the

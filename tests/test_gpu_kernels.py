@@ -67,6 +67,28 @@ def test_layernorm_bwd(cols, dydt, acc, rows):
     assert rel_err(db, b.grad) < 1e-5
 
 
+@pytest.mark.parametrize("cols", [128, 768])
+@pytest.mark.parametrize("lpdt", [None, torch.bfloat16, torch.float16])
+def test_layernorm_bwd_res(cols, lpdt):
+    """dx = res + LN^T(dy) into a fresh buffer, plus the 16-bit copy of dx (the block
+    backward's fused residual + cast)."""
+    O = ops()
+    rows = 3001
+    x = (torch.randn(rows, cols, device=DEV) * 2).requires_grad_(True)
+    w = torch.randn(cols, device=DEV)
+    dy = torch.randn(rows, cols, device=DEV).to(torch.bfloat16)
+    F.layer_norm(x, (cols,), w, None, 1e-5).backward(dy.float())
+    _, mu, rs = O.layernorm_fwd(x.detach(), w, torch.zeros_like(w), torch.float32)
+    res = torch.randn(rows, cols, device=DEV)
+    dx = torch.full((rows, cols), float("nan"), device=DEV)
+    lp = torch.empty(rows, cols, device=DEV, dtype=lpdt) if lpdt else None
+    dw = torch.zeros(cols, device=DEV)
+    O.layernorm_bwd(dy, x.detach(), w, mu, rs, dx, 0, dw, None, res=res, lp=lp)
+    assert rel_err(dx, res + x.grad) < 1e-5
+    if lp is not None:
+        assert torch.equal(lp, dx.to(lpdt))
+
+
 # ----------------------------------------------------------------------------- GEMM
 SHAPES = [(128, 128, 64), (300, 200, 192), (65, 64, 128), (1000, 2304, 768), (4097, 768, 3072), (8, 512, 768),
           (65544, 768, 1536)]  # the last: M = 256k + 8 takes the M-tail split-K path on the big tiles
