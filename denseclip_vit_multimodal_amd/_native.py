@@ -91,6 +91,11 @@ def load(path=None):
         lib.dclip_abi_version.restype = ctypes.c_int
         lib.dclip_abi_version.argtypes = []
         lib.dclip_attn_bwd_workspace.restype = ctypes.c_int64  # a size, not a status
+        # kernel-variant knobs for A/B runs: DCLIP_OPTIONS="id=value,..." (DCLIP_OPT_* ids of dclip.h)
+        for kv in filter(None, os.environ.get("DCLIP_OPTIONS", "").split(",")):
+            k, v = kv.split("=")
+            if lib.dclip_set_option(int(k), int(v)) != 0:
+                raise NativeError(f"DCLIP_OPTIONS: {lib.dclip_last_error().decode()}")
         if path is None:
             _lib = lib
         return lib

@@ -555,6 +555,173 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp_kernel(
                                      slab, alpha);
 }
 
+// ---------------------------------------------------------------------------- persistent 256x256
+// One workgroup per CU walks its tiles (u = round * G + xcd_remap(block), G = grid size) as ONE
+// continuous K-stream over the 2-slot LDS ring of gemm_nt_big_kernel: the last K-step of a
+// tile already stages K-step 0 of the next, and the epilogue runs from the accumulators
+// straight to global memory (no LDS, no barrier) while those loads fly, so neither the
+// epilogue's stores nor the next tile's first load latency stall the MFMA pipe the way a
+// grid of one-tile workgroups does (whose epilogues all run at once, round after round).
+// Full tiles only (M % 256 == 0, N % 256 == 0; the launcher peels an M tail): no masks, so the
+// epilogue issues at least 16 row-segment stores of C per lane after those loads, which lets
+// the next tile's first wait count them (vmcnt(PERS_EPI_MIN)) instead of draining them.
+// 16-bit outputs pair lanes l and l + 16 (adjacent 4-column groups) with one exchange so that
+// every store is 16 contiguous bytes.
+constexpr int PERS_EPI_MIN = 16;
+
+// 16-bit row segments: v0 / v1 = this lane's 4 columns of blocks i and i + 1 (columns
+// 16 i + 4 lq + e); after the exchange with lane ^ 16 an even-lq lane stores block i's columns
+// 4 lq .. 4 lq + 7 and an odd-lq lane block i+1's columns 4 (lq - 1) .. 4 lq + 3.
+template <typename OutT>
+__device__ __forceinline__ void store_pair16(OutT* row_base, int col_i, const f32x4& v0, const f32x4& v1, int lq) {
+    typedef OutT t2 __attribute__((ext_vector_type(2)));
+    const t2 a0 = {(OutT)v0[0], (OutT)v0[1]}, a1 = {(OutT)v0[2], (OutT)v0[3]};
+    const t2 b0 = {(OutT)v1[0], (OutT)v1[1]}, b1 = {(OutT)v1[2], (OutT)v1[3]};
+    const unsigned p0x = __builtin_bit_cast(unsigned, a0), p0y = __builtin_bit_cast(unsigned, a1);
+    const unsigned p1x = __builtin_bit_cast(unsigned, b0), p1y = __builtin_bit_cast(unsigned, b1);
+    const bool odd = lq & 1;
+    const unsigned rx = __shfl_xor(odd ? p0x : p1x, 16, 64), ry = __shfl_xor(odd ? p0y : p1y, 16, 64);
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 w = odd ? u32x4{rx, ry, p1x, p1y} : u32x4{p0x, p0y, rx, ry};
+    const int col = odd ? col_i + 16 - 4 : col_i;  // col_i = 16 i + 4 lq (+ tile offset)
+    *(u32x4*)(row_base + col) = w;
+}
+
+template <typename OutT>
+__device__ __forceinline__ void store4_out(OutT* p, const f32x4& v) {
+    if constexpr (sizeof(OutT) == 4) {
+        *(f32x4*)p = v;
+    } else {
+        typedef OutT t4 __attribute__((ext_vector_type(4)));
+        const t4 x = {(OutT)v[0], (OutT)v[1], (OutT)v[2], (OutT)v[3]};
+        *(t4*)p = x;
+    }
+}
+
+template <typename T, int EPI, typename OutT>
+__global__ __launch_bounds__(512, 1) void gemm_nt_pers_kernel(
+    const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb, int K, int tiles_m, int tiles_n,
+    const float* __restrict__ bias, const void* __restrict__ aux, int64_t ld_aux, void* __restrict__ C, int64_t ldc,
+    void* __restrict__ C2, int64_t ldc2, float alpha) {
+    typedef BigCfg<256, 256, 2, 4, 2, 64> Cfg;
+    typedef typename Mfma<T>::frag frag;
+    __shared__ __attribute__((aligned(16))) char smem[Cfg::SMEM];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    const int l16 = lane & 15, lq = lane >> 4;
+    const int ntiles = tiles_m * tiles_n;
+    const int G = gridDim.x;
+    const int r = xcd_remap(blockIdx.x, G);  // the G tiles of a round in XCD-contiguous ranges
+    const int nk = K / 64;
+    const int M = tiles_m * 256, N = tiles_n * 256;
+
+    auto stage = [&](int m0, int n0, int kt, int slot) {
+        char* base = smem + slot * Cfg::STAGE_BYTES;
+        stage_rows<T, Cfg::A_INST, 64>(A, lda, m0, M, kt * 64, base, wave, lane);
+        stage_rows<T, Cfg::B_INST, 64>(B, ldb, n0, N, kt * 64, base + Cfg::A_BYTES, wave, lane);
+    };
+    int u = r;
+    if (u >= ntiles) return;
+    int m0 = (u / tiles_n) * 256, n0 = (u % tiles_n) * 256;
+    stage(m0, n0, 0, 0);
+    int slot = 0;
+    bool first = true;
+    while (true) {
+        f32x4 acc[Cfg::NB][Cfg::MB];
+#pragma unroll
+        for (int i = 0; i < Cfg::NB; ++i)
+#pragma unroll
+            for (int j = 0; j < Cfg::MB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int un = u + G;
+        const int nm0 = (un / tiles_n) * 256, nn0 = (un % tiles_n) * 256;
+        for (int kt = 0; kt < nk; ++kt) {
+            if (kt == 0 && !first) wait_vmcnt<PERS_EPI_MIN>();  // this K-step's loads, not the epilogue's stores
+            else wait_vmcnt<0>();
+            __builtin_amdgcn_s_barrier();  // K-step kt visible to every wave; the other slot free
+            __builtin_amdgcn_sched_barrier(0);
+            if (kt + 1 < nk) {
+                stage(m0, n0, kt + 1, slot ^ 1);
+            } else if (un < ntiles) {
+                stage(nm0, nn0, 0, slot ^ 1);
+            }
+            const char* At = smem + slot * Cfg::STAGE_BYTES;
+            const char* Bt = At + Cfg::A_BYTES;
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                frag fb[Cfg::NB], fa[Cfg::MB];
+                const int ch = ks * 4 + lq;
+#pragma unroll
+                for (int i = 0; i < Cfg::NB; ++i) fb[i] = big_frag<T, 64>(Bt, wn * Cfg::WTN + i * 16 + l16, ch);
+#pragma unroll
+                for (int j = 0; j < Cfg::MB; ++j) fa[j] = big_frag<T, 64>(At, wm * Cfg::WTM + j * 16 + l16, ch);
+#pragma unroll
+                for (int j = 0; j < Cfg::MB; ++j)
+#pragma unroll
+                    for (int i = 0; i < Cfg::NB; ++i) acc[i][j] = Mfma16<T>::mma(fb[i], fa[j], acc[i][j]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            slot ^= 1;
+        }
+        // epilogue: acc[i][j] = C[mw + 16 j + l16][nw + 16 i + 4 lq + e]
+        const int mw = m0 + wm * 128, nw = n0 + wn * 64;
+        f32x4 bv[Cfg::NB], sv[Cfg::NB];  // per-column constants of this lane's 16 columns
+#pragma unroll
+        for (int i = 0; i < Cfg::NB; ++i) {
+            const int col = nw + 16 * i + 4 * lq;
+            bv[i] = (bias != nullptr && EPI != DCLIP_EPI_GELU_BWD) ? *(const f32x4*)(bias + col)
+                                                                  : f32x4{0.f, 0.f, 0.f, 0.f};
+            if constexpr (EPI == DCLIP_EPI_STORE_SCALED) sv[i] = *(const f32x4*)((const float*)aux + col);
+        }
+#pragma unroll
+        for (int j = 0; j < Cfg::MB; ++j) {
+            const int64_t row = mw + 16 * j + l16;
+#pragma unroll
+            for (int i = 0; i < Cfg::NB; i += 2) {
+                const int col = nw + 16 * i + 4 * lq;
+                f32x4 v[2] = {acc[i][j] * alpha + bv[i], acc[i + 1][j] * alpha + bv[i + 1]};
+                if constexpr (EPI == DCLIP_EPI_RESIDUAL || sizeof(OutT) == 4) {
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        if constexpr (EPI == DCLIP_EPI_RESIDUAL)
+                            v[h] += *(const f32x4*)((const float*)aux + row * ld_aux + col + 16 * h);
+                        store4_out<OutT>((OutT*)C + row * ldc + col + 16 * h, v[h]);
+                    }
+                } else if constexpr (EPI == DCLIP_EPI_STORE) {
+                    store_pair16<OutT>((OutT*)C + row * ldc, col, v[0], v[1], lq);
+                } else if constexpr (EPI == DCLIP_EPI_STORE_SCALED) {
+                    store_pair16<OutT>((OutT*)C + row * ldc, col, v[0] * sv[i], v[1] * sv[i + 1], lq);
+                } else if constexpr (EPI == DCLIP_EPI_GELU) {
+                    f32x4 g[2];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            v[h][e] = (float)(OutT)v[h][e];  // the activation sees the rounded pre-activation
+                            g[h][e] = quick_gelu(v[h][e]);
+                        }
+                    store_pair16<OutT>((OutT*)C + row * ldc, col, v[0], v[1], lq);
+                    store_pair16<OutT>((OutT*)C2 + row * ldc2, col, g[0], g[1], lq);
+                } else if constexpr (EPI == DCLIP_EPI_GELU_BWD) {
+                    typedef T t4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const t4 z = *(const t4*)((const T*)aux + row * ld_aux + col + 16 * h);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[h][e] *= quick_gelu_grad((float)z[e]);
+                    }
+                    store_pair16<OutT>((OutT*)C + row * ldc, col, v[0], v[1], lq);
+                }
+            }
+        }
+        if (un >= ntiles) break;
+        u = un;
+        m0 = nm0;
+        n0 = nn0;
+        first = false;
+    }
+}
+
 // ---------------------------------------------------------------------------- "TN"
 // C[m][n] = sum_k A[k][m] * B[k][n]: both operands row-major with the reduction index on
 // the ROWS — the weight-gradient shape dW = dY^T X (k = token, m/n = features).  Tiles of
@@ -1156,15 +1323,74 @@ void launch_big(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t 
     }
 }
 
+// persistent path (gemm_nt_pers_kernel) for the full 256-row tiles; an M tail of <= 64 rows by
+// K-split slabs + an epilogue-applying combine.  Returns false when the shape does not fit it.
+int cu_count() {
+    static int n[64] = {0};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64) return 256;
+    if (n[dev] == 0) {
+        int c = 0;
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+        n[dev] = c;
+    }
+    return n[dev];
+}
+
+template <typename T, int EPI, typename OutT>
+bool launch_pers(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
+                 float alpha, const float* bias, const void* aux, int64_t ld_aux, void* C, int64_t ldc, void* C2,
+                 int64_t ldc2, hipStream_t st) {
+    if constexpr (EPI == DCLIP_EPI_SPLITK) {
+        return false;
+    } else {
+        const int64_t Mfull = (M / 256) * 256, tail = M - Mfull;
+        const int G = cu_count();
+        if (N % 256 != 0 || tail > 64 || (Mfull / 256) * (N / 256) < 2 * G) return false;
+        if (EPI == DCLIP_EPI_STORE_SCALED || (bias != nullptr && EPI != DCLIP_EPI_GELU_BWD)) {
+            // 16-byte per-column vector loads
+            if (((uintptr_t)(EPI == DCLIP_EPI_STORE_SCALED ? aux : bias) % 16) != 0) return false;
+            if (bias != nullptr && ((uintptr_t)bias % 16) != 0) return false;
+        }
+        if (ldc % 4 != 0 || (C2 != nullptr && ldc2 % 4 != 0) || (EPI == DCLIP_EPI_RESIDUAL && ld_aux % 4 != 0) ||
+            (EPI == DCLIP_EPI_GELU_BWD && ld_aux % 4 != 0))
+            return false;
+        if (tail > 0) {
+            const int tiles_n = (int)(N / 256);
+            const int ksteps = (int)(K / 64);
+            int ts = 1;
+            for (int c = 16; c >= 1; --c)
+                if (ksteps % c == 0) {
+                    ts = c;
+                    break;
+                }
+            float* ws = tail_scratch((size_t)ts * tail * N);
+            if (ws == nullptr) return false;
+            gemm_nt_big_kernel<T, DCLIP_EPI_SPLITK, float, 256, 256, 2, 4, 2, 64>
+                <<<dim3(tiles_n, ts), 512, 0, st>>>((const T*)A + Mfull * lda, lda, (const T*)B, ldb, (int)tail, (int)N,
+                                                    (int)(K / ts), 1, tiles_n, nullptr, nullptr, 0, ws, N, nullptr, 0,
+                                                    tail * N, alpha);
+            const int threads = (int)(tail * ((N + 7) / 8));
+            tail_combine_kernel<T, EPI, OutT><<<(threads + 255) / 256, 256, 0, st>>>(
+                ws, ts, (int)tail, (int)N, Mfull, bias, aux, ld_aux, C, ldc, C2, ldc2);
+        }
+        gemm_nt_pers_kernel<T, EPI, OutT><<<G, 512, 0, st>>>((const T*)A, lda, (const T*)B, ldb, (int)K,
+                                                             (int)(Mfull / 256), (int)(N / 256), bias, aux, ld_aux,
+                                                             C, ldc, C2, ldc2, alpha);
+        return true;
+    }
+}
+
 // tile configuration: DCLIP_OPT_GEMM_TILE 1 = 128x128 (4 waves, 2 workgroups/CU), 2 = 256x256
 // (8 waves, 2-stage ring of 64-deep k-tiles), 3 = 256x128 (8 waves, 3-stage ring),
 // 4 = 256x256 with a 4-stage ring of 32-deep k-tiles, 5 = 256x256 ping-pong (gemm_nt_pp_kernel),
-// 0 = automatic
+// 6 = persistent 256x256 (gemm_nt_pers_kernel) where the shape allows it, 0 = automatic
 inline int gemm_tile_choice(int64_t M, int64_t N) {
     const int opt = dclip_option(DCLIP_OPT_GEMM_TILE);
     if (opt != 0) return opt;
     if (M < 4096) return 1;
-    return 2;
+    return 6;  // persistent where the shape allows it (falls back to the 256x256 grid kernel)
 }
 
 template <typename T, int EPI, typename OutT>
@@ -1179,6 +1405,14 @@ int launch(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, in
     }
     if (choice == 3) {
         launch_big<T, EPI, OutT, 256, 128, 4, 2, 3>(A, lda, B, ldb, M, N, K, splits, alpha, bias, aux, ld_aux, C,
+                                                    ldc, C2, ldc2, st);
+        return 0;
+    }
+    if (choice == 6 && splits == 1 &&
+        launch_pers<T, EPI, OutT>(A, lda, B, ldb, M, N, K, alpha, bias, aux, ld_aux, C, ldc, C2, ldc2, st))
+        return 0;
+    if (choice == 6) {
+        launch_big<T, EPI, OutT, 256, 256, 2, 4, 2>(A, lda, B, ldb, M, N, K, splits, alpha, bias, aux, ld_aux, C,
                                                     ldc, C2, ldc2, st);
         return 0;
     }
