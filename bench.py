@@ -169,6 +169,13 @@ def main():
         with open(pmc) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
     kernels = {k: {"launches": v[0], "ms_total": round(v[1], 3), "ms_mean": round(v[2], 4)} for k, v in summ.items()}
+    # the attention backward (row-0 passes + dQ pass + dK/dV pass per launch): useful work = the
+    # 5 N^2-matmuls of flash backward (2.5x the forward's), same HIP-event timing
+    n_ab, _, mean_ab = summ.get("attn_bwd", (0, 0.0, float("nan")))
+    fl_b = 2.5 * fl
+    ach_b = fl_b / (mean_ab * 1e-3) / 1e12 if n_ab else None
+    # whole-model MFMA utilisation: 3 x 4.068 TFLOP per image fwd+bwd in mode F
+    model_fl = (3 * 4.068e12 if args.mode == "F" else 4.44e12) * H * W / (1024 * 2048)
 
     mode_r = None
     if args.mode == "F" and not args.no_mode_r:
@@ -211,6 +218,14 @@ def main():
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4) if achieved else None,
                          "traffic": traffic, "flops_per_launch": fl, "launches": n_att,
                          "ms_per_launch": round(mean_att, 4) if n_att else None},
+            "roofline_attn_bwd": {"kernel": "attn_bwd_dq2_kernel + attn_bwd_dkdv2_kernel (+ row-0 passes)",
+                                  "bound": "mfma", "achieved": round(ach_b, 2) if ach_b else None,
+                                  "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                                  "frac": round(ach_b / PEAK_BF16_TFLOPS, 4) if ach_b else None,
+                                  "flops_per_launch": fl_b, "launches": n_ab,
+                                  "ms_per_launch": round(mean_ab, 4) if n_ab else None},
+            "model_mfma": {"flops_per_image": model_fl, "achieved_tflops": round(value / world * model_fl / 1e12, 1),
+                           "frac": round(value / world * model_fl / 1e12 / PEAK_BF16_TFLOPS, 4)},
             "kernels": kernels,
             "mode_R": mode_r,
             "cpu_baseline": cpu,

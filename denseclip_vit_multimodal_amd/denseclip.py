@@ -47,6 +47,7 @@ class DenseCLIP(nn.Module):
         # evaluates upsample + CE / SILog in fused kernels (ops.UpsampleCEFn / UpsampleSILogFn).
         # False (default): the reference contract — upsampled 'main_output' / 'depth_output'.
         self.fused_head_loss = False
+        self.graph_text = True  # replay the frozen text path from a HIP graph (see _text_embeddings)
 
         # ---- backbone (denseclip.py:111-126)
         bcfg = dict(backbone)
@@ -227,11 +228,41 @@ class DenseCLIP(nn.Module):
             raise RuntimeError("backbone returned no feature maps")
         return list(feats)
 
-    def _text_embeddings(self, B, device):
-        texts = self.texts.to(device)
+    def _text_forward(self, texts):
         if isinstance(self.text_encoder, CLIPTextContextEncoder) and self.contexts is not None:
-            return self.text_encoder(texts, self.contexts).expand(B, -1, -1)
-        return self.text_encoder(texts).expand(B, -1, -1)
+            return self.text_encoder(texts, self.contexts)
+        return self.text_encoder(texts)
+
+    def _text_embeddings(self, B, device):
+        """Class-name embeddings (denseclip.py:627-640).  The text path is batch-independent and,
+        when frozen (the reference regime and the full fine-tune both freeze it,
+        train_denseclip.py:1040-1044), a fixed chain of ~400 small kernels: on a GPU it is
+        captured once into a HIP graph and REPLAYED every step (recomputed, not cached), which
+        removes the per-kernel launch gaps; any trainable text parameter, or a parameter
+        re-allocated since the capture, falls back to eager execution / a new capture."""
+        if getattr(self, "_texts_dev", None) is None or self._texts_dev.device != device:
+            self._texts_dev = self.texts.to(device)
+        texts = self._texts_dev
+        params = list(self.text_encoder.parameters())
+        if self.contexts is not None:
+            params.append(self.contexts)
+        frozen = not any(p.requires_grad for p in params)
+        if not (self.graph_text and frozen and device.type == "cuda"):
+            return self._text_forward(texts).expand(B, -1, -1)
+        key = (device, tuple(p.data_ptr() for p in params), torch.is_autocast_enabled())
+        g = getattr(self, "_text_graph", None)
+        if g is None or g[0] != key:
+            side = torch.cuda.Stream(device=device)
+            side.wait_stream(torch.cuda.current_stream(device))
+            with torch.cuda.stream(side), torch.no_grad():
+                self._text_forward(texts)  # warm-up outside the capture (allocator, library handles)
+            torch.cuda.current_stream(device).wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            with torch.no_grad(), torch.cuda.graph(graph):
+                out = self._text_forward(texts)
+            self._text_graph = g = (key, graph, out)
+        g[1].replay()
+        return g[2].expand(B, -1, -1)
 
     def _process_features(self, x):
         """Global feature, projections, text embeddings, context fusion and the pixel-text

@@ -108,7 +108,15 @@ class ResidualAttentionBlock(nn.Module):
         self.drop_path = DropPath(drop_path) if drop_path > 0.0 else nn.Identity()
 
     def attention(self, x):
-        m = self.attn_mask.to(dtype=x.dtype, device=x.device) if self.attn_mask is not None else None
+        m = None
+        if self.attn_mask is not None:
+            # the mask is not a buffer (state-dict keys as in the reference): keep a device copy
+            # instead of a host->device copy (and host sync) per call
+            key = (x.device, x.dtype)
+            if getattr(self, "_mask_key", None) != key:
+                self._mask_dev = self.attn_mask.to(dtype=x.dtype, device=x.device)
+                self._mask_key = key
+            m = self._mask_dev
         return self.attn(x, x, x, need_weights=False, attn_mask=m)[0]
 
     def forward(self, x):
@@ -315,7 +323,7 @@ class CLIPTextEncoder(nn.Module):
         x = (x + pos.to(x.dtype)).permute(1, 0, 2)
         x = self.transformer(x).permute(1, 0, 2)
         x = self.ln_final(x)
-        return x[torch.arange(x.shape[0]), text.argmax(dim=-1)] @ self.text_projection
+        return x[torch.arange(x.shape[0], device=x.device), text.argmax(dim=-1)] @ self.text_projection
 
 
 class CLIPTextContextEncoder(nn.Module):
@@ -368,7 +376,7 @@ class CLIPTextContextEncoder(nn.Module):
         x = (x + self.positional_embedding).permute(1, 0, 2)
         x = self.transformer(x).permute(1, 0, 2)
         x = self.ln_final(x)
-        x = x[torch.arange(x.shape[0]), eos] @ self.text_projection
+        x = x[torch.arange(x.shape[0], device=x.device), eos] @ self.text_projection
         return x.reshape(B, K, self.embed_dim)
 
 

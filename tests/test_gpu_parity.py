@@ -219,3 +219,34 @@ def test_fused_head_loss_matches_materialised(img_dtype):
         # heads / neck: the two formulations agree to fp32 rounding; behind them the bf16 ViT
         # backward re-rounds a ~1e-6 different input gradient (module docstring: ill-conditioned)
         assert rel_err(g1[k], g0[k]) < (2e-2 if k.startswith("backbone.") else 2e-3), k
+
+
+def test_text_path_graph_replay_matches_eager():
+    """The frozen text path replayed from its captured HIP graph gives the eager result, is
+    recomputed on every replay (a changed context token changes it), and a trainable text
+    parameter falls back to eager execution."""
+    m = build("tiny", TINY_CFG, torch.bfloat16)
+    for p in m.text_encoder.parameters():
+        p.requires_grad_(False)
+    if m.contexts is not None:
+        m.contexts.requires_grad_(False)
+    dev = torch.device(DEV)
+    m.graph_text = False
+    eager = m._text_embeddings(2, dev).clone()
+    m.graph_text = True
+    g1 = m._text_embeddings(2, dev).clone()
+    g2 = m._text_embeddings(2, dev).clone()
+    assert m._text_graph is not None
+    assert torch.allclose(g1, eager, rtol=1e-5, atol=1e-6) and torch.equal(g1, g2)
+    if m.contexts is not None:
+        with torch.no_grad():
+            m.contexts.add_(0.5)  # in place: same storage, the graph reads the new values
+        g3 = m._text_embeddings(2, dev).clone()
+        m.graph_text = False
+        assert not torch.equal(g3, g1)
+        assert torch.allclose(g3, m._text_embeddings(2, dev), rtol=1e-5, atol=1e-6)
+        m.graph_text = True
+    m.text_encoder.text_projection.requires_grad_(True)
+    graph_before = m._text_graph
+    m._text_embeddings(2, dev)
+    assert m._text_graph is graph_before  # eager path taken: no new capture, no replay needed
