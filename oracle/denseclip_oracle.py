@@ -192,6 +192,40 @@ def text_context_encoder(tokens, contexts, p, pre="text_encoder.", heads=8, laye
     return x.reshape(B, K, -1)
 
 
+def _ln(x, p, pre, eps=LN_EPS):
+    return layer_norm(x, p[pre + "weight"], p[pre + "bias"], eps)
+
+
+def _decoder_attention(q, kv, p, pre, heads):
+    """Attention.forward (models.py:328-344): bias-free q/k/v projections, per-head softmax of
+    q.k * d^-0.5 over the memory, output projection (dropout = identity)."""
+    B, N, C = q.shape
+    M = kv.shape[1]
+    qh = linear(q, p[pre + "q_proj.weight"]).reshape(B, N, heads, C // heads)
+    kh = linear(kv, p[pre + "k_proj.weight"]).reshape(B, M, heads, C // heads)
+    vh = linear(kv, p[pre + "v_proj.weight"]).reshape(B, M, heads, C // heads)
+    a = (torch.einsum("bnkc,bmkc->bknm", qh, kh) * (C // heads) ** -0.5).softmax(dim=-1)
+    x = torch.einsum("bknm,bmkc->bnkc", a, vh).reshape(B, N, C)
+    return linear(x, p[pre + "proj.weight"], p[pre + "proj.bias"])
+
+
+def context_decoder(text, visual, p, pre="context_decoder.", heads=4, layers=6):
+    """ContextDecoder.forward (models.py:910-917) over TransformerDecoderLayer (models.py:369-375):
+    memory = LN(Linear(LN(visual))), x = Linear(LN(text)); per layer x += SelfAttn(LN1 x),
+    x += CrossAttn(LN2 x, memory), x += MLP(LN3 x) (exact GELU); out = Linear(LN(x))."""
+    mem = _ln(linear(_ln(visual, p, pre + "memory_proj.0."), p[pre + "memory_proj.1.weight"],
+                     p[pre + "memory_proj.1.bias"]), p, pre + "memory_proj.2.")
+    x = linear(_ln(text, p, pre + "text_proj.0."), p[pre + "text_proj.1.weight"], p[pre + "text_proj.1.bias"])
+    for i in range(layers):
+        L = f"{pre}decoder.{i}."
+        y = _ln(x, p, L + "norm1.")
+        x = x + _decoder_attention(y, y, p, L + "self_attn.", heads)
+        x = x + _decoder_attention(_ln(x, p, L + "norm2."), mem, p, L + "cross_attn.", heads)
+        h = F.gelu(linear(_ln(x, p, L + "norm3."), p[L + "mlp.0.weight"], p[L + "mlp.0.bias"]))
+        x = x + linear(h, p[L + "mlp.3.weight"], p[L + "mlp.3.bias"])
+    return linear(_ln(x, p, pre + "out_proj.0."), p[pre + "out_proj.1.weight"], p[pre + "out_proj.1.bias"])
+
+
 def l2_normalize(x, dim, eps=1e-12):
     """F.normalize(p=2): x / max(||x||, eps)."""
     n = x.norm(p=2, dim=dim, keepdim=True).clamp(min=eps)
@@ -267,6 +301,19 @@ def denseclip_forward(img, p, tokens, cfg, gt_hw=None, training=False):
     contexts = p["contexts"]
     text = text_context_encoder(tokens, contexts, p, heads=te.get("transformer_heads", 8),
                                 layers=te.get("transformer_layers", 12)).expand(B, -1, -1)
+    cd = cfg.get("context_decoder")
+    if cd:
+        # 'attention' context (denseclip.py:627-633): [projected global; projected pixels],
+        # fused as text + gamma * ContextDecoder(text, context) (denseclip.py:661-665)
+        vis = maps[-1]
+        g = vis.mean(dim=(2, 3))
+        if "global_proj.weight" in p:
+            g = linear(g, p["global_proj.weight"], p["global_proj.bias"])
+        if "vis_proj.weight" in p:
+            vis = F.conv2d(vis, p["vis_proj.weight"], p["vis_proj.bias"])
+        ctx = torch.cat([g.unsqueeze(1), vis.flatten(2).permute(0, 2, 1)], dim=1)
+        text = text + p["gamma"] * context_decoder(text, ctx, p, heads=cd.get("transformer_heads", 4),
+                                                   layers=cd.get("transformer_layers", 6))
     score, _ = score_map(maps[-1], text, p)
     fused = neck(maps, p, training=training)
     seg_low = fcn_head(fused, p, "decode_head.", training)

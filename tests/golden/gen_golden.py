@@ -4,6 +4,7 @@ Run ONLY in the development container (the reference tree does not travel to the
 GPU box):
 
     python tests/golden/gen_golden.py            # writes tests/golden/*.safetensors
+    python tests/golden/gen_golden.py ctx        # only the ContextDecoder fixture (+ manifest)
 
 The reference package imports `timm`, `ftfy` and `torchvision`, none of which are
 installed here.  The shims below are written into a temporary directory at run
@@ -36,7 +37,7 @@ from safetensors.torch import save_file
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 from weights_spec import fill_state_dict  # noqa: E402
-from model_configs import TINY_CFG, CITYSCAPES_CFG, CITYSCAPES_CLASSES  # noqa: E402
+from model_configs import TINY_CFG, TINY_CTX_CFG, CTX_GAMMA, CITYSCAPES_CFG, CITYSCAPES_CLASSES  # noqa: E402
 
 REF_SEG = "/root/reference/segmentation"
 
@@ -186,6 +187,21 @@ def gen_tiny():
     print("tiny: loss", loss.item())
 
 
+def gen_tiny_ctx():
+    """The tiny model with the ContextDecoder branch, eval: class embeddings after the context
+    fusion, the score map and the (unaffected) low-res seg logits."""
+    model = build_reference(TINY_CTX_CFG).eval()
+    with torch.no_grad():
+        model.gamma.fill_(CTX_GAMMA)  # a trained-scale fusion weight, so the branch moves the result
+    cap = capture(model)
+    x = images(1, 64, 128, seed=1234)
+    with torch.no_grad():
+        model(x, return_loss=False)
+    t = {"input": x, "text": cap["text"], "score": cap["score"], "seg_low": cap["seg_low"]}
+    save_file({k: v.contiguous() for k, v in t.items()}, os.path.join(HERE, "tiny_ctx_eval.safetensors"))
+    print("tiny_ctx: text norm", t["text"].norm().item())
+
+
 def gen_full(name, b, h, w, keep_full_maps=(0, 11)):
     model = build_reference(CITYSCAPES_CFG).eval()
     cap = capture(model)
@@ -226,7 +242,7 @@ def gen_manifest():
     """state_dict key -> (shape, dtype) of the reference model for both configs."""
     import json
     man = {}
-    for name, cfg in (("tiny", TINY_CFG), ("cityscapes", CITYSCAPES_CFG)):
+    for name, cfg in (("tiny", TINY_CFG), ("tiny_ctx", TINY_CTX_CFG), ("cityscapes", CITYSCAPES_CFG)):
         from denseclip import DenseCLIP
         sd = DenseCLIP(class_names=CITYSCAPES_CLASSES, **dict(cfg)).state_dict()
         man[name] = {k: [list(v.shape), str(v.dtype)] for k, v in sd.items()}
@@ -237,8 +253,13 @@ def gen_manifest():
 if __name__ == "__main__":
     torch.set_num_threads(os.cpu_count())
     install_shims()
+    if sys.argv[1:] == ["ctx"]:
+        gen_manifest()
+        gen_tiny_ctx()
+        sys.exit(0)
     gen_tokens()
     gen_manifest()
     gen_tiny()
+    gen_tiny_ctx()
     gen_full("vitb16_1x128x256", 1, 128, 256)
     gen_full("vitb16_2x512x1024", 2, 512, 1024, keep_full_maps=())

@@ -59,3 +59,12 @@ TINY_CFG = dict(
     tau=0.05,
     clip_pretrained_path=None,
 )
+
+# TINY_CFG with the ContextDecoder branch (denseclip.py:204-211, 627-665):
+# the class embeddings cross-attend over [global; pixel] visual context and the decoder's
+# output is added with the learnable gamma before the score map
+TINY_CTX_CFG = dict(TINY_CFG, context_decoder=dict(type='ContextDecoder', transformer_width=32,
+                                                   transformer_heads=2, transformer_layers=2, dropout=0.1))
+# the fixture's gamma (the spec weights' value is ~1e-4 scale, which would leave the branch
+# below the comparison tolerance)
+CTX_GAMMA = 0.5

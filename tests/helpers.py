@@ -14,7 +14,7 @@ for p in (ROOT, GOLDEN):
         sys.path.insert(0, p)
 
 from weights_spec import value_for  # noqa: E402
-from model_configs import TINY_CFG, CITYSCAPES_CFG, CITYSCAPES_CLASSES  # noqa: E402
+from model_configs import TINY_CFG, TINY_CTX_CFG, CTX_GAMMA, CITYSCAPES_CFG, CITYSCAPES_CLASSES  # noqa: E402
 
 
 def manifest(name):
@@ -33,6 +33,8 @@ def spec_state_dict(name, seed=0):
             sd[k] = value_for(k, shape, seed)
         else:
             sd[k] = torch.zeros(shape, dtype=_DT[dt])
+    if name == "tiny_ctx":
+        sd["gamma"] = torch.full_like(sd["gamma"], CTX_GAMMA)  # as gen_golden.gen_tiny_ctx
     return sd
 
 

@@ -19,7 +19,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from helpers import (TINY_CFG, CITYSCAPES_CFG, CITYSCAPES_CLASSES, spec_state_dict, golden, class_tokens,
+from helpers import (TINY_CFG, TINY_CTX_CFG, CITYSCAPES_CFG, CITYSCAPES_CLASSES, spec_state_dict, golden, class_tokens,
                      images, rel_err, stats)
 
 pytestmark = pytest.mark.gpu
@@ -250,3 +250,21 @@ def test_text_path_graph_replay_matches_eager():
     graph_before = m._text_graph
     m._text_embeddings(2, dev)
     assert m._text_graph is graph_before  # eager path taken: no new capture, no replay needed
+
+
+@pytest.mark.parametrize("graph_text", [False, True])
+def test_tiny_context_decoder_vs_reference(graph_text):
+    """The ContextDecoder branch on the GPU (text path and decoder in torch, ViT / projections /
+    score map on the HIP kernels) against the reference's context-fused class embeddings and
+    score map."""
+    g = golden("tiny_ctx_eval")
+    m = build("tiny_ctx", TINY_CTX_CFG, torch.float16)
+    if graph_text:
+        for p in list(m.text_encoder.parameters()) + [m.contexts]:
+            p.requires_grad_(False)
+    cap = capture(m)
+    with torch.no_grad():
+        m(g["input"].to(DEV), return_loss=False)
+    assert rel_err(cap["text"].cpu(), g["text"]) < 1e-3
+    assert rel_err(cap["score"].cpu(), g["score"]) < 1e-3
+    assert rel_err(cap["seg_low"].cpu(), g["seg_low"]) < 1e-3

@@ -6,7 +6,7 @@ were generated from /root/reference by tests/golden/gen_golden.py.
 import torch
 import torch.nn.functional as F
 
-from helpers import (TINY_CFG, CITYSCAPES_CFG, spec_state_dict, golden, class_tokens,
+from helpers import (TINY_CFG, TINY_CTX_CFG, CITYSCAPES_CFG, spec_state_dict, golden, class_tokens,
                      images, rel_err, stats)
 from oracle import denseclip_oracle as O
 
@@ -27,6 +27,19 @@ def test_tiny_eval_matches_reference():
     assert rel_err(out["depth_low"], g["depth_low"]) < 1e-5
     assert rel_err(out["seg"], g["seg"]) < 1e-5
     assert rel_err(out["depth"], g["depth"]) < 1e-5
+
+
+def test_tiny_context_decoder_matches_reference():
+    """The ContextDecoder branch: context-fused class embeddings and the
+    score map they produce, against the reference run with the same weights."""
+    g = golden("tiny_ctx_eval")
+    out, p = _fwd("tiny_ctx", TINY_CTX_CFG, g["input"])
+    assert rel_err(out["text"], g["text"]) < 1e-5
+    assert rel_err(out["score"], g["score"]) < 1e-5
+    assert rel_err(out["seg_low"], g["seg_low"]) < 1e-5
+    # the branch is live: without it the embeddings differ well beyond the tolerance
+    plain, _ = _fwd("tiny_ctx", dict(TINY_CTX_CFG, context_decoder=None), g["input"])
+    assert rel_err(plain["text"], g["text"]) > 1e-3
 
 
 def test_vitb16_small_matches_reference():
