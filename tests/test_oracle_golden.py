@@ -39,7 +39,7 @@ def test_tiny_context_decoder_matches_reference():
     assert rel_err(out["seg_low"], g["seg_low"]) < 1e-5
     # the branch is live: without it the embeddings differ well beyond the tolerance
     plain, _ = _fwd("tiny_ctx", dict(TINY_CTX_CFG, context_decoder=None), g["input"])
-    assert rel_err(plain["text"], g["text"]) > 1e-3
+    assert rel_err(plain["text"], g["text"]) > 0.1  # measured 0.48
 
 
 def test_vitb16_small_matches_reference():
