@@ -57,6 +57,9 @@ _SIGS = {
     "dclip_conv3x3_wgrad": [_i32, _c_void_p, _i64, _i32, _c_void_p, _i64, _i64, _i64, _i32, _i32, _i32, _i32,
                             _c_void_p, _c_void_p, _i32, _c_void_p],
     "dclip_set_option": [_i32, _i32],
+    "dclip_cityscapes_prepare": [_c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p, _i32, _i32,
+                                 _c_void_p, _c_void_p, _f32, _f32, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p,
+                                 _c_void_p],
     "dclip_attn_bwd_workspace": [_i32, _i32, _i32],
     "dclip_gemm_tn_plan": [_i64, _i64, _i64, _c_void_p, _c_void_p],
 }

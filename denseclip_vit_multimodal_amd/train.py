@@ -7,7 +7,10 @@ step (its CLI, logging, metrics and checkpointing are out of scope — DESIGN.md
   * loss                   train_denseclip.py:1086-1095, 1265-1314: CE(ignore 255) + 0.1 SILog
   * optimiser              train_denseclip.py:1061: AdamW(lr 2e-5, weight decay 0.01)
   * per-rank data          DistributedSampler (train_denseclip.py:242): rank r sees its own
-                           shard; here synthetic Cityscapes-shaped tensors seeded per rank.
+                           shard; here synthetic Cityscapes-shaped tensors seeded per rank
+                           (real data: data.CityscapesDepthSegDataset + data.prepare_batch).
+  * checkpoints            train_denseclip.py:1012-1034 (--load), 1107-1133 (--resume),
+                           1491-1521 (save): {'epoch', 'state_dict', 'optimizer'[, 'scheduler']}.
 Mode "R" is the reference regime (backbone + text frozen); mode "F" also trains the ViT,
 which exercises the HIP backward kernels (the north star's roofline applies there).
 """
@@ -97,3 +100,51 @@ def train_step(model, opt, batch, silog=None):
     loss.backward()
     opt.step()
     return loss.detach()
+
+
+# ---------------------------------------------------------------------------- checkpoints
+def _unwrap(model):
+    return model.module if hasattr(model, "module") else model
+
+
+def save_checkpoint(path, model, optimizer, epoch, scheduler=None):
+    """The reference trainer's checkpoint (train_denseclip.py:1499-1512): the UNWRAPPED model's
+    state dict (no 'module.' prefix), the optimizer's and optionally the scheduler's."""
+    state = {"epoch": epoch, "state_dict": _unwrap(model).state_dict(), "optimizer": optimizer.state_dict()}
+    if scheduler is not None:
+        state["scheduler"] = scheduler.state_dict()
+    torch.save(state, path)
+
+
+def _model_weights(ckpt):
+    """Weight dict of a checkpoint as --load reads it (train_denseclip.py:1019-1021): under
+    'state_dict', 'model_state_dict' or 'model', or the dict itself; a 'module.' prefix on every
+    key (a DDP-saved model) is stripped."""
+    for key in ("state_dict", "model_state_dict", "model"):
+        if key in ckpt:
+            ckpt = ckpt[key]
+            break
+    if ckpt and all(k.startswith("module.") for k in ckpt):
+        ckpt = {k[len("module."):]: v for k, v in ckpt.items()}
+    return ckpt
+
+
+def load_weights(path, model, map_location="cpu"):
+    """--load (train_denseclip.py:1012-1024): non-strict load of a checkpoint's model weights;
+    returns the load message.  Files are read with weights_only=True; an unreadable file raises
+    (the reference logs and continues)."""
+    ckpt = torch.load(path, map_location=map_location, weights_only=True)
+    return _unwrap(model).load_state_dict(_model_weights(ckpt), strict=False)
+
+
+def resume(path, model, optimizer=None, scheduler=None, map_location="cpu"):
+    """--resume (train_denseclip.py:1107-1133): model, optimizer and scheduler state; returns the
+    epoch to start from (saved epoch + 1)."""
+    ckpt = torch.load(path, map_location=map_location, weights_only=True)
+    if "state_dict" in ckpt:
+        _unwrap(model).load_state_dict(_model_weights(ckpt), strict=False)
+    if optimizer is not None and "optimizer" in ckpt:
+        optimizer.load_state_dict(ckpt["optimizer"])
+    if scheduler is not None and "scheduler" in ckpt:
+        scheduler.load_state_dict(ckpt["scheduler"])
+    return ckpt.get("epoch", -1) + 1

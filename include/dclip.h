@@ -33,6 +33,7 @@
  *   dclip_bilinear_fwd/bwd     F.interpolate(bilinear, align_corners=False)
  *                              denseclip.py:847,860,899,909 (logits/depth upsample)
  *   dclip_cast                 dtype conversion of operands (.type()/.to() casts)
+ *   dclip_cityscapes_prepare   Cityscapes label remap, disparity->depth, crop/flip/normalise
  */
 #ifndef DCLIP_H
 #define DCLIP_H
@@ -239,6 +240,21 @@ int dclip_upsample_ce(int low_dt, const void* logits, int B, int K, int h, int w
 int dclip_upsample_silog(int pass, int low_dt, const void* pred, int B, int h, int w, const float* target,
                          const uint8_t* mask, int H, int W, float eps, float lambd, double* sums, float* grad,
                          void* stream);
+
+/* Cityscapes depth + segmentation batch preparation (datasets/cityscapes_depth_seg.py:129-170,
+ * 218 and the trainer's RandomCrop / HorizontalFlip / Normalize / ToTensorV2,
+ * train_denseclip.py:143-149).  Inputs: decoded planes of B images of H x W — img uint8
+ * (B, H, W, 3) RGB, ids uint8 (B, H, W) Cityscapes label ids, disp uint16 (B, H, W) disparity;
+ * crop int32 (B, 3) = (y0, x0, flip) per image, window [y0, y0 + h) x [x0, x0 + w) inside the
+ * image (mirrored when flip != 0).  Outputs for the h x w crops: out_img (B, 3, h, w) out_dt
+ * = (x - 255 mean) * (1 / (255 std)); out_seg int64 (B, h, w) train ids (ids >= 34 -> 255);
+ * out_depth f32 (B, h, w) = bf / ((d - 1) / 256 + 1e-6) where d > 0, (d - 1) / 256 > 1e-3 and
+ * the depth <= depth_max, else 0; out_mask uint8 (B, h, w) = depth > 0.  All device pointers
+ * (mean, stdv: 3 host floats).                                                          */
+int dclip_cityscapes_prepare(const uint8_t* img, const uint8_t* ids, const uint16_t* disp, int B, int H, int W,
+                             const int* crop, int h, int w, const float* mean, const float* stdv, float bf,
+                             float depth_max, void* out_img, int out_dt, int64_t* out_seg, float* out_depth,
+                             uint8_t* out_mask, void* stream);
 
 /* Element-wise dtype conversion of n elements: out = (out_dt)(in * scale).  A power-of-two
  * scale keeps fp16 gradients out of the subnormal range (see dclip_gemm's alpha).     */

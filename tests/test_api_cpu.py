@@ -96,3 +96,36 @@ def test_silog_loss_matches_oracle():
     m = torch.rand(2, 1, 8, 8) > 0.4
     assert abs(float(SILogLoss()(pred, tgt, m)) - float(O.silog_loss(pred, tgt, m))) < 1e-6
     assert float(SILogLoss()(pred, tgt, torch.zeros_like(m))) == 0.0
+
+
+def test_checkpoint_roundtrip_reference_format(tmp_path):
+    """save_checkpoint writes the reference trainer's layout ({'epoch', 'state_dict',
+    'optimizer'}, unwrapped keys); load_weights / resume read it back, also with a DDP-style
+    'module.' prefix."""
+    import torch
+    from denseclip_vit_multimodal_amd import DenseCLIP
+    from denseclip_vit_multimodal_amd.train import save_checkpoint, load_weights, resume, make_optimizer
+    from helpers import TINY_CFG, CITYSCAPES_CLASSES
+    torch.manual_seed(0)
+    m = DenseCLIP(class_names=CITYSCAPES_CLASSES, **TINY_CFG)
+    opt = make_optimizer([p for p in m.parameters()], fused=False)
+    for p in m.parameters():
+        p.grad = torch.randn_like(p) * 1e-3
+    opt.step()
+    path = str(tmp_path / "epoch_3.pth")
+    save_checkpoint(path, m, opt, epoch=2)
+    ck = torch.load(path, weights_only=True)
+    assert set(ck) == {"epoch", "state_dict", "optimizer"} and ck["epoch"] == 2
+    assert not any(k.startswith("module.") for k in ck["state_dict"])
+    m2 = DenseCLIP(class_names=CITYSCAPES_CLASSES, **TINY_CFG)
+    opt2 = make_optimizer([p for p in m2.parameters()], fused=False)
+    assert resume(path, m2, opt2) == 3
+    for (k, a), b in zip(m.state_dict().items(), m2.state_dict().values()):
+        assert torch.equal(a, b), k
+    assert opt2.state_dict()["state"].keys() == opt.state_dict()["state"].keys()
+    ddp_style = str(tmp_path / "ddp.pth")
+    torch.save({"model": {"module." + k: v for k, v in m.state_dict().items()}}, ddp_style)
+    m3 = DenseCLIP(class_names=CITYSCAPES_CLASSES, **TINY_CFG)
+    msg = load_weights(ddp_style, m3)
+    assert not msg.missing_keys and not msg.unexpected_keys
+    assert all(torch.equal(a, b) for a, b in zip(m.state_dict().values(), m3.state_dict().values()))
