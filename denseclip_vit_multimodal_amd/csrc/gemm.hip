@@ -959,7 +959,18 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ x, in
     float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (c0 + 8 <= cols) {
         typedef T t8 __attribute__((ext_vector_type(8)));
-        for (int64_t r = r0 + ry; r < r1; r += 32) {
+        int64_t r = r0 + ry;
+        // 8 rows per thread in flight (independent 16-byte loads), then the remainder
+        for (; r + 7 * 32 < r1; r += 8 * 32) {
+            t8 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = *(const t8*)(x + (r + 32 * u) * ld + c0);
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) s[e] += (float)v[u][e];
+        }
+        for (; r < r1; r += 32) {
             const t8 v = *(const t8*)(x + r * ld + c0);
 #pragma unroll
             for (int e = 0; e < 8; ++e) s[e] += (float)v[e];
