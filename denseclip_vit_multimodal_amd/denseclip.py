@@ -258,7 +258,8 @@ class DenseCLIP(nn.Module):
                 self._text_forward(texts)  # warm-up outside the capture (allocator, library handles)
             torch.cuda.current_stream(device).wait_stream(side)
             graph = torch.cuda.CUDAGraph()
-            with torch.no_grad(), torch.cuda.graph(graph):
+            # thread-local capture: other threads' HIP calls (RCCL / DDP helpers) stay legal
+            with torch.no_grad(), torch.cuda.graph(graph, capture_error_mode="thread_local"):
                 out = self._text_forward(texts)
             self._text_graph = g = (key, graph, out)
         g[1].replay()

@@ -268,3 +268,19 @@ def test_tiny_context_decoder_vs_reference(graph_text):
     assert rel_err(cap["text"].cpu(), g["text"]) < 1e-3
     assert rel_err(cap["score"].cpu(), g["score"]) < 1e-3
     assert rel_err(cap["seg_low"].cpu(), g["seg_low"]) < 1e-3
+
+
+def test_ddp_two_ranks_one_gpu_graphed_text_path():
+    """DDP train steps (gloo, 2 ranks sharing the GPU) with fused losses and the HIP-graph text
+    path: the capture coexists with the communication threads and the ranks stay in sync."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29561",
+                        os.path.join(root, "tools", "ddp_gpu_check.py")],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "parameters identical across ranks: True" in r.stdout
