@@ -33,6 +33,13 @@ import torch.nn.functional as F  # noqa: E402
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
 PEAK_HBM_GBS = 8000.0
 FUSED_HEAD_LOSS = True  # resize + CE / SILog fused (same loss; no 1024x2048 logits in HBM)
+# backbone kwargs per --arch: ViT-B/16 is seg/configs/denseclip_cityscapes.yaml's own backbone;
+# ViT-L/14 (BASELINE configs[3]) is tests/golden/model_configs.py's VITL14_CFG backbone
+ARCHS = {
+    "vitb16": None,
+    "vitl14": dict(type="CLIPVisionTransformer", patch_size=14, width=1024, layers=24, heads=16,
+                   input_resolution=224, output_dim=1024, out_indices=[5, 11, 17, 23]),
+}
 
 
 def parse():
@@ -47,6 +54,8 @@ def parse():
     ap.add_argument("--no-mode-r", action="store_true", help="skip the extra mode-R measurement")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--arch", choices=sorted(ARCHS), default="vitb16",
+                    help="vitb16: the headline (BASELINE configs[1]); vitl14: BASELINE configs[3]'s backbone")
     ap.add_argument("--unfused-head-loss", action="store_true",
                     help="materialise the resized logits/depth and use F.cross_entropy + SILogLoss")
     return ap.parse_args()
@@ -56,10 +65,26 @@ def attn_flops_fwd(B, N, H, D=64):
     return 4.0 * B * H * N * N * D  # QK^T and PV
 
 
-def make_model(dev, mode):
+def model_fwd_flops(H, W, arch):
+    """Algorithmic forward FLOPs per image (SURVEY 8(d)'s formulas): ViT attention L*4N^2C,
+    linears L*24NC^2, patchify 2*P*C*3p^2, neck (3x3 convs C->128 per read-out + 1x1 fusion
+    -> 256) and a 12 GFLOP allowance for projections / score map / heads (ViT-B at 1024x2048:
+    4.068 TFLOP)."""
+    b = ARCHS[arch] or dict(patch_size=16, width=768, layers=12, heads=12, out_indices=list(range(12)))
+    p, C, L, nl = b["patch_size"], b["width"], b["layers"], len(b["out_indices"])
+    P = (H // p) * (W // p)
+    N = P + 1
+    vit = L * (4.0 * N * N * C + 24.0 * N * C * C) + 2.0 * P * C * 3 * p * p
+    neck = nl * 2.0 * P * 9 * C * 128 + 2.0 * P * 128 * nl * 256
+    return vit + neck + 12e9 * P / 8192
+
+
+def make_model(dev, mode, arch="vitb16"):
     from denseclip_vit_multimodal_amd.config import build_model, load_yaml
     from denseclip_vit_multimodal_amd.train import freeze_for_mode
     cfg = load_yaml("denseclip_cityscapes.yaml")
+    if ARCHS[arch] is not None:
+        cfg["model"]["backbone"] = dict(ARCHS[arch])
     model = build_model(cfg, clip_path_override="").to(dev)
     freeze_for_mode(model, mode)
     model.fused_head_loss = FUSED_HEAD_LOSS
@@ -146,7 +171,7 @@ def main():
     batch = synth_batch(B, H, W, dev, rank)
 
     def setup(mode):
-        model = make_model(dev, mode)
+        model = make_model(dev, mode, args.arch)
         model.train()
         if world > 1:
             model = wrap_ddp(model, dev)
@@ -156,8 +181,9 @@ def main():
     model, opt = setup(args.mode)
     dt, summ, loss = timed(model, opt, batch, args.steps, args.warmup, silog, world)
     value = world * B * args.steps / dt
-    N = (H // 16) * (W // 16) + 1
-    heads = 12
+    bb = ARCHS[args.arch] or dict(patch_size=16, heads=12)
+    N = (H // bb["patch_size"]) * (W // bb["patch_size"]) + 1
+    heads = bb["heads"]
 
     # roofline of the dominant kernel: the fused attention forward (one kernel per launch)
     n_att, tot_att, mean_att = summ.get("attn_fwd", (0, 0.0, float("nan")))
@@ -165,7 +191,7 @@ def main():
     achieved = fl / (mean_att * 1e-3) / 1e12 if n_att else None
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "attn_fwd_pmc.json")
-    if os.path.exists(pmc):
+    if os.path.exists(pmc) and args.arch == "vitb16":
         with open(pmc) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
     kernels = {k: {"launches": v[0], "ms_total": round(v[1], 3), "ms_mean": round(v[2], 4)} for k, v in summ.items()}
@@ -175,7 +201,10 @@ def main():
     fl_b = 2.5 * fl
     ach_b = fl_b / (mean_ab * 1e-3) / 1e12 if n_ab else None
     # whole-model MFMA utilisation: 3 x 4.068 TFLOP per image fwd+bwd in mode F
-    model_fl = (3 * 4.068e12 if args.mode == "F" else 4.44e12) * H * W / (1024 * 2048)
+    if args.arch == "vitb16":
+        model_fl = (3 * 4.068e12 if args.mode == "F" else 4.44e12) * H * W / (1024 * 2048)
+    else:
+        model_fl = 3 * model_fwd_flops(H, W, args.arch) if args.mode == "F" else None
 
     mode_r = None
     if args.mode == "F" and not args.no_mode_r:
@@ -188,7 +217,7 @@ def main():
                   "what": "reference regime: backbone + text encoder frozen (train_denseclip.py:1040-1044)"}
 
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_baseline == "auto":
+    if rank == 0 and world == 1 and args.cpu_baseline == "auto" and args.arch == "vitb16":
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         try:
             cpu = cpu_baseline(H, W, threads)
@@ -197,7 +226,8 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "images/sec (fwd+bwd) ViT-B/16 DenseCLIP @1024x2048",
+            "metric": "images/sec (fwd+bwd) %s DenseCLIP @%dx%d" % (
+                {"vitb16": "ViT-B/16", "vitl14": "ViT-L/14"}[args.arch], H, W),
             "value": round(value, 4),
             "unit": "images/sec",
             "n_gpus": world,
@@ -209,7 +239,8 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic (randn images, random labels/depth; random-init weights)",
-            "config": {"workload": "DenseCLIP ViT-B/16 seg+depth train step (mode %s), %dx%d" % (args.mode, H, W),
+            "config": {"workload": "DenseCLIP %s seg+depth train step (mode %s), %dx%d" % (
+                           {"vitb16": "ViT-B/16", "vitl14": "ViT-L/14"}[args.arch], args.mode, H, W),
                        "per_gpu_batch": B, "global_batch": B * world, "tokens_per_image": N,
                        "parallelism": f"dp{world}", "mode": args.mode,
                        "head_loss": "fused resize+CE/SILog" if FUSED_HEAD_LOSS else "materialised resize"},
@@ -225,7 +256,7 @@ def main():
                                   "flops_per_launch": fl_b, "launches": n_ab,
                                   "ms_per_launch": round(mean_ab, 4) if n_ab else None},
             "model_mfma": {"flops_per_image": model_fl, "achieved_tflops": round(value / world * model_fl / 1e12, 1),
-                           "frac": round(value / world * model_fl / 1e12 / PEAK_BF16_TFLOPS, 4)},
+                           "frac": round(value / world * model_fl / 1e12 / PEAK_BF16_TFLOPS, 4)} if model_fl else None,
             "kernels": kernels,
             "mode_R": mode_r,
             "cpu_baseline": cpu,

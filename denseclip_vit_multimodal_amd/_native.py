@@ -36,7 +36,7 @@ _SIGS = {
     "dclip_attn_fwd": [_i32, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i32, _i32, _f32, _c_void_p],
     "dclip_attn_bwd": [_i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i32,
                        _i32, _f32, _c_void_p],
-    "dclip_im2col": [_c_void_p, _i32, _c_void_p, _i32, _i32, _i32, _i32, _i32, _i32, _c_void_p],
+    "dclip_im2col": [_c_void_p, _i32, _c_void_p, _i32, _i64, _i32, _i32, _i32, _i32, _i32, _c_void_p],
     "dclip_tokens_fwd": [_c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p],
     "dclip_tokens_bwd": [_c_void_p, _c_void_p, _i32, _f32, _c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p],
     "dclip_pos_interp_fwd": [_c_void_p, _c_void_p, _i32, _i32, _i32, _i32, _c_void_p],

@@ -10,25 +10,49 @@ template <typename T>
 __device__ __forceinline__ T cvt(float v) { return (T)v; }
 
 // ---------------------------------------------------------------------------- im2col
-// out[(b*gh + py)*gw + px][(c*p + ky)*p + kx] = img[b][c][py*p + ky][px*p + kx]
-// one thread per 4 consecutive kx (p % 4 == 0)
+// out[(b*gh + py)*gw + px][(c*p + ky)*p + kx] = img[b][c][py*p + ky][px*p + kx], rows of ldo
+// elements whose columns K = Cin*p*p .. ldo-1 are zero (the GEMM's K padding: p = 14 gives
+// K = 588, padded to 640).  p % 4 == 0: one thread per 4 consecutive kx; otherwise one thread
+// per output element (patchify is ~0.3 % of the step either way).
 template <typename TI, typename TO>
 __global__ void im2col_kernel(const TI* __restrict__ img, TO* __restrict__ out, int B, int Cin, int Hin, int Win,
-                              int p, int gh, int gw, int64_t total4) {
+                              int p, int gh, int gw, int64_t ldo, int64_t total4) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= total4) return;
-    const int K = Cin * p * p;
-    const int k4 = K / 4;
-    const int64_t row = i / k4;
-    const int col = (int)(i % k4) * 4;
+    const int64_t l4 = ldo / 4;
+    const int64_t row = i / l4;
+    const int col = (int)(i % l4) * 4;
+    TO* dst = out + row * ldo + col;
+    if (col >= Cin * p * p) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dst[e] = (TO)0.0f;
+        return;
+    }
     const int kx = col % p, ky = (col / p) % p, cc = col / (p * p);
     const int px = (int)(row % gw);
     const int py = (int)((row / gw) % gh);
     const int b = (int)(row / ((int64_t)gw * gh));
     const TI* src = img + (((int64_t)b * Cin + cc) * Hin + (py * p + ky)) * Win + px * p + kx;
-    TO* dst = out + row * K + col;
 #pragma unroll
     for (int e = 0; e < 4; ++e) dst[e] = (TO)(float)src[e];
+}
+
+template <typename TI, typename TO>
+__global__ void im2col_any_kernel(const TI* __restrict__ img, TO* __restrict__ out, int B, int Cin, int Hin, int Win,
+                                  int p, int gh, int gw, int64_t ldo, int64_t total) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int64_t row = i / ldo;
+    const int col = (int)(i % ldo);
+    if (col >= Cin * p * p) {
+        out[i] = (TO)0.0f;
+        return;
+    }
+    const int kx = col % p, ky = (col / p) % p, cc = col / (p * p);
+    const int px = (int)(row % gw);
+    const int py = (int)((row / gw) % gh);
+    const int b = (int)(row / ((int64_t)gw * gh));
+    out[i] = (TO)(float)img[(((int64_t)b * Cin + cc) * Hin + (py * p + ky)) * Win + px * p + kx];
 }
 
 // ---------------------------------------------------------------------------- tokens
@@ -337,16 +361,27 @@ inline unsigned grid_for(int64_t n, int64_t cap = 65536) {
 
 }  // namespace
 
-extern "C" int dclip_im2col(const void* img, int img_dt, void* out, int out_dt, int B, int Cin, int Hin, int Win,
-                            int p, void* stream) {
-    DCLIP_HOST_CHECK(p % 4 == 0 && p > 0, "dclip_im2col: patch size must be a positive multiple of 4");
+extern "C" int dclip_im2col(const void* img, int img_dt, void* out, int out_dt, int64_t ldo, int B, int Cin, int Hin,
+                            int Win, int p, void* stream) {
+    DCLIP_HOST_CHECK(p > 0, "dclip_im2col: patch size must be positive");
     const int gh = Hin / p, gw = Win / p;
     DCLIP_HOST_CHECK(gh > 0 && gw > 0, "dclip_im2col: image smaller than one patch");
-    const int64_t total4 = (int64_t)B * gh * gw * Cin * p * p / 4;
+    DCLIP_HOST_CHECK(ldo >= (int64_t)Cin * p * p && ldo % 4 == 0,
+                     "dclip_im2col: ldo must be >= Cin*p*p and a multiple of 4");
+    const int64_t rows = (int64_t)B * gh * gw;
     hipStream_t st = (hipStream_t)stream;
-    DISPATCH_DT(img_dt, TI, DISPATCH_DT(out_dt, TO,
-        im2col_kernel<TI, TO><<<(unsigned)((total4 + 255) / 256), 256, 0, st>>>((const TI*)img, (TO*)out, B, Cin, Hin,
-                                                                             Win, p, gh, gw, total4)));
+    if (p % 4 == 0) {
+        const int64_t total4 = rows * ldo / 4;
+        DISPATCH_DT(img_dt, TI, DISPATCH_DT(out_dt, TO,
+            im2col_kernel<TI, TO><<<(unsigned)((total4 + 255) / 256), 256, 0, st>>>((const TI*)img, (TO*)out, B, Cin,
+                                                                                 Hin, Win, p, gh, gw, ldo, total4)));
+    } else {
+        const int64_t total = rows * ldo;
+        DISPATCH_DT(img_dt, TI, DISPATCH_DT(out_dt, TO,
+            im2col_any_kernel<TI, TO><<<(unsigned)((total + 255) / 256), 256, 0, st>>>((const TI*)img, (TO*)out, B,
+                                                                                    Cin, Hin, Win, p, gh, gw, ldo,
+                                                                                    total)));
+    }
     DCLIP_LAUNCH_CHECK();
     return 0;
 }

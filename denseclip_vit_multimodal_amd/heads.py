@@ -3,7 +3,7 @@ builds for 'FPNHead' / 'FCNHeadDepth', denseclip.py:22-23, 305-309, 343-349)."""
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .models import Registry
+from .models import BatchNorm2d, Registry
 
 
 class FCNHead(nn.Sequential):
@@ -15,7 +15,7 @@ class FCNHead(nn.Sequential):
         inter = in_channels // 4
         super().__init__(
             nn.Conv2d(in_channels, inter, 3, padding=1, bias=False),
-            nn.BatchNorm2d(inter),
+            BatchNorm2d(inter),
             nn.ReLU(),
             nn.Dropout(0.1),
             nn.Conv2d(inter, channels, 1),
@@ -30,7 +30,7 @@ class ConvModule(nn.Module):
         super().__init__()
         self.conv = nn.Conv2d(in_channels, out_channels, kernel_size, stride=stride, padding=padding,
                               dilation=dilation, groups=groups, bias=bias)
-        self.norm = nn.BatchNorm2d(out_channels) if norm_cfg is not None else None
+        self.norm = BatchNorm2d(out_channels) if norm_cfg is not None else None
         self.activate = nn.ReLU(inplace=True) if act_cfg is not None else None
 
     def forward(self, x):

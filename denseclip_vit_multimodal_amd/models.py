@@ -17,13 +17,27 @@ from . import ops
 logger = logging.getLogger(__name__)
 
 
+class BatchNorm2d(nn.BatchNorm2d):
+    """nn.BatchNorm2d (same parameters, buffers and state-dict keys) whose GPU forward runs
+    torch's native kernels instead of MIOpen: MIOpen's batch-norm segfaults on the host for a
+    bf16 channels-last (1, 128, 73, 146) map in train mode — the ViT-L/14 neck at 1024x2048 —
+    while fp32, NCHW, other sizes and the native kernels are fine (tools/bn_probe.py,
+    gpurun_out/bn_probe.log)."""
+
+    def forward(self, x):
+        if x.is_cuda:
+            with torch.backends.cudnn.flags(enabled=False):
+                return super().forward(x)
+        return super().forward(x)
+
+
 class ConvBNReLU(nn.Sequential):
     """Conv-BN-ReLU (reference models.py:13-20)."""
 
     def __init__(self, in_channels, out_channels, kernel_size=3, padding=1, stride=1):
         super().__init__(
             nn.Conv2d(in_channels, out_channels, kernel_size, stride=stride, padding=padding, bias=False),
-            nn.BatchNorm2d(out_channels),
+            BatchNorm2d(out_channels),
             nn.ReLU(inplace=True),
         )
 

@@ -251,12 +251,24 @@ def attn_bwd(qkv, o, dout, lse, B, Ntok, H, scale):
 
 
 def im2col(img, p, out_dtype):
+    """Patch rows (B*gh*gw, K_pad): K = Cin*p*p zero-padded to a multiple of 64 (the GEMM's K
+    step; p = 14 gives 588 -> 640)."""
     _check(img)
     B, Cin, Hin, Win = img.shape
     gh, gw = Hin // p, Win // p
-    out = torch.empty(B * gh * gw, Cin * p * p, dtype=out_dtype, device=img.device)
-    N.call("dclip_im2col", _p(img), _dt(img), _p(out), _DT[out_dtype], B, Cin, Hin, Win, p, _stream())
+    k_pad = -(-Cin * p * p // 64) * 64
+    out = torch.empty(B * gh * gw, k_pad, dtype=out_dtype, device=img.device)
+    N.call("dclip_im2col", _p(img), _dt(img), _p(out), _DT[out_dtype], k_pad, B, Cin, Hin, Win, p, _stream())
     return out
+
+
+def _patch_weight(conv_w, cdt, k_pad):
+    """conv1 weight as GEMM rows (C, K_pad) in cdt, zero columns past Cin*p*p."""
+    K = conv_w[0].numel()
+    if K == k_pad:
+        return WEIGHTS.get(conv_w, cdt)
+    return WEIGHTS.get_with(conv_w, cdt, ("kpad", k_pad),
+                            lambda w: torch.nn.functional.pad(w.reshape(w.shape[0], -1).float(), (0, k_pad - K)))
 
 
 def pos_interp(pos, g, H, W):
@@ -361,7 +373,7 @@ class PatchEmbedFn(torch.autograd.Function):
         interp = (P != pos.shape[0] - 1)
         posf = pos_interp(pos.detach().contiguous(), g, gh, gw) if interp else pos.detach().contiguous()
         patches = im2col(img.contiguous(), patch, cdt)
-        emb = gemm(patches, WEIGHTS.get(conv_w, cdt), out_dtype=torch.float32)
+        emb = gemm(patches, _patch_weight(conv_w, cdt, patches.shape[1]), out_dtype=torch.float32)
         x_pre = torch.empty(B * (P + 1), C, dtype=torch.float32, device=img.device)
         N.call("dclip_tokens_fwd", _p(emb), N.F32, _p(cls.detach().float().contiguous()), _p(posf), _p(x_pre),
                B, P, C, _stream())
@@ -395,7 +407,8 @@ class PatchEmbedFn(torch.autograd.Function):
         dconv = None
         if need[1]:
             dW, _ = weight_grad(demb, patches, want_bias=False, alpha=1.0 / s)
-            dconv = dW.view(wshape)
+            K = math.prod(wshape[1:])
+            dconv = (dW if dW.shape[1] == K else dW[:, :K]).reshape(wshape)
         return (None, dconv, dcls if need[2] else None, dpos, dlnw if need[4] else None,
                 dlnb if need[5] else None, None, None)
 

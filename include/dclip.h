@@ -152,9 +152,11 @@ int dclip_attn_bwd(int dt, const void* qkv, const void* o, const void* dout,
 int64_t dclip_attn_bwd_workspace(int B, int N, int H);
 
 /* Non-overlapping p x p patches of img (B, Cin, Hin, Win) (img_dt) ->
- * out (B*gh*gw, Cin*p*p) (out_dt), column order (c, ky, kx) = conv weight flattening,
- * gh = Hin / p, gw = Win / p (floor, as Conv2d stride p).                            */
-int dclip_im2col(const void* img, int img_dt, void* out, int out_dt,
+ * out (B*gh*gw, ldo) (out_dt), column order (c, ky, kx) = conv weight flattening,
+ * gh = Hin / p, gw = Win / p (floor, as Conv2d stride p).  Columns Cin*p*p .. ldo-1
+ * are written as zeros: ldo = the patch GEMM's K padded to 64 (p = 14: 588 -> 640).
+ * ldo % 4 == 0.                                                                        */
+int dclip_im2col(const void* img, int img_dt, void* out, int out_dt, int64_t ldo,
                  int B, int Cin, int Hin, int Win, int p, void* stream);
 
 /* Token assembly: x[b][0] = cls + pos[0]; x[b][1+i] = patch[b*P+i] + pos[1+i]

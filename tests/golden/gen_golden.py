@@ -5,6 +5,7 @@ GPU box):
 
     python tests/golden/gen_golden.py            # writes tests/golden/*.safetensors
     python tests/golden/gen_golden.py ctx        # only the ContextDecoder fixture (+ manifest)
+    python tests/golden/gen_golden.py vitl14     # only the ViT-L/14 fixture (+ manifest)
 
 The reference package imports `timm`, `ftfy` and `torchvision`, none of which are
 installed here.  The shims below are written into a temporary directory at run
@@ -37,7 +38,8 @@ from safetensors.torch import save_file
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 from weights_spec import fill_state_dict  # noqa: E402
-from model_configs import TINY_CFG, TINY_CTX_CFG, CTX_GAMMA, CITYSCAPES_CFG, CITYSCAPES_CLASSES  # noqa: E402
+from model_configs import (TINY_CFG, TINY_CTX_CFG, CTX_GAMMA, CITYSCAPES_CFG, CITYSCAPES_CLASSES,  # noqa: E402
+                           VITL14_CFG)
 
 REF_SEG = "/root/reference/segmentation"
 
@@ -202,8 +204,8 @@ def gen_tiny_ctx():
     print("tiny_ctx: text norm", t["text"].norm().item())
 
 
-def gen_full(name, b, h, w, keep_full_maps=(0, 11)):
-    model = build_reference(CITYSCAPES_CFG).eval()
+def gen_full(name, b, h, w, keep_full_maps=(0, 11), cfg=CITYSCAPES_CFG):
+    model = build_reference(cfg).eval()
     cap = capture(model)
     x = images(b, h, w, seed=1234)
     with torch.no_grad():
@@ -227,6 +229,12 @@ def gen_full(name, b, h, w, keep_full_maps=(0, 11)):
     print(name, "done")
 
 
+def gen_vitl14():
+    """BASELINE config 4 at a test size: 120x230 is not a multiple of the patch (14), so the
+    patchify floor (8x16 grid, N = 129) is exercised too (models.py:543-556)."""
+    gen_full("vitl14_1x120x230", 1, 120, 230, keep_full_maps=(0, 3), cfg=VITL14_CFG)
+
+
 def gen_tokens():
     """Token ids of the 19 Cityscapes class names from the reference tokenizer
     (seg/denseclip/utils.py:301-314, context_length 6 as in the YAML)."""
@@ -242,7 +250,8 @@ def gen_manifest():
     """state_dict key -> (shape, dtype) of the reference model for both configs."""
     import json
     man = {}
-    for name, cfg in (("tiny", TINY_CFG), ("tiny_ctx", TINY_CTX_CFG), ("cityscapes", CITYSCAPES_CFG)):
+    for name, cfg in (("tiny", TINY_CFG), ("tiny_ctx", TINY_CTX_CFG), ("cityscapes", CITYSCAPES_CFG),
+                      ("vitl14", VITL14_CFG)):
         from denseclip import DenseCLIP
         sd = DenseCLIP(class_names=CITYSCAPES_CLASSES, **dict(cfg)).state_dict()
         man[name] = {k: [list(v.shape), str(v.dtype)] for k, v in sd.items()}
@@ -257,9 +266,14 @@ if __name__ == "__main__":
         gen_manifest()
         gen_tiny_ctx()
         sys.exit(0)
+    if sys.argv[1:] == ["vitl14"]:
+        gen_manifest()
+        gen_vitl14()
+        sys.exit(0)
     gen_tokens()
     gen_manifest()
     gen_tiny()
     gen_tiny_ctx()
     gen_full("vitb16_1x128x256", 1, 128, 256)
     gen_full("vitb16_2x512x1024", 2, 512, 1024, keep_full_maps=())
+    gen_vitl14()

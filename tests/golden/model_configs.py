@@ -68,3 +68,11 @@ TINY_CTX_CFG = dict(TINY_CFG, context_decoder=dict(type='ContextDecoder', transf
 # the fixture's gamma (the spec weights' value is ~1e-4 scale, which would leave the branch
 # below the comparison tolerance)
 CTX_GAMMA = 0.5
+
+# BASELINE config 4: ViT-L/14 (width 1024, 24 layers, 16 heads of 64, patch 14).  The reference
+# ships no ViT-L YAML; this is CITYSCAPES_CFG with the backbone swapped and four read-outs (the
+# quarter-depth layers, the usual dense-prediction choice for a 24-layer ViT) — the neck's
+# in_channels follow from width x len(out_indices) exactly as for ViT-B (denseclip.py:224-262).
+VITL14_CFG = dict(CITYSCAPES_CFG,
+                  backbone=dict(type='CLIPVisionTransformer', patch_size=14, width=1024, layers=24, heads=16,
+                                input_resolution=224, output_dim=1024, out_indices=[5, 11, 17, 23]))

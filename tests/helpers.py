@@ -14,7 +14,8 @@ for p in (ROOT, GOLDEN):
         sys.path.insert(0, p)
 
 from weights_spec import value_for  # noqa: E402
-from model_configs import TINY_CFG, TINY_CTX_CFG, CTX_GAMMA, CITYSCAPES_CFG, CITYSCAPES_CLASSES  # noqa: E402
+from model_configs import (TINY_CFG, TINY_CTX_CFG, CTX_GAMMA, CITYSCAPES_CFG, CITYSCAPES_CLASSES,  # noqa: E402,F401
+                           VITL14_CFG)
 
 
 def manifest(name):

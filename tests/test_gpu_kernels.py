@@ -445,13 +445,19 @@ def test_attention_bwd_full_length():
 
 
 # ----------------------------------------------------------------------------- misc
-def test_im2col_and_patch_gemm_match_conv():
+@pytest.mark.parametrize("p,hw", [(16, (64, 96)), (16, (70, 100)), (14, (64, 96)), (14, (120, 230))])
+def test_im2col_and_patch_gemm_match_conv(p, hw):
+    """Patch rows zero-padded to K_pad = ceil(3p^2 / 64) * 64 (p = 14: 588 -> 640); sizes that
+    are not multiples of p keep the floor grid like Conv2d(stride p)."""
     O = ops()
-    img = torch.randn(2, 3, 64, 96, device=DEV)
-    w = torch.randn(128, 3, 16, 16, device=DEV) * 0.05
-    pt = O.im2col(img, 16, torch.float32)
-    ref = F.conv2d(img, w, stride=16).flatten(2).transpose(1, 2).reshape(-1, 128)
-    assert rel_err(pt @ w.view(128, -1).t(), ref) < 1e-5
+    img = torch.randn(2, 3, *hw, device=DEV)
+    w = torch.randn(128, 3, p, p, device=DEV) * 0.05
+    pt = O.im2col(img, p, torch.float32)
+    K = 3 * p * p
+    assert pt.shape == (2 * (hw[0] // p) * (hw[1] // p), -(-K // 64) * 64)
+    assert (pt[:, K:] == 0).all()
+    ref = F.conv2d(img, w, stride=p).flatten(2).transpose(1, 2).reshape(-1, 128)
+    assert rel_err(pt[:, :K] @ w.view(128, -1).t(), ref) < 1e-5
 
 
 def test_pos_interp_fwd_bwd():

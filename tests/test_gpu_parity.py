@@ -19,7 +19,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from helpers import (TINY_CFG, TINY_CTX_CFG, CITYSCAPES_CFG, CITYSCAPES_CLASSES, spec_state_dict, golden, class_tokens,
+from helpers import (TINY_CFG, TINY_CTX_CFG, CITYSCAPES_CFG, VITL14_CFG, CITYSCAPES_CLASSES, spec_state_dict, golden, class_tokens,
                      images, rel_err, stats)
 
 pytestmark = pytest.mark.gpu
@@ -144,6 +144,55 @@ def test_tiny_train_step_grads_vs_reference():
     assert n == sum(1 for k in g if k.startswith("gnorm/")) and n >= 60, n  # every golden parameter
     elem.sort()
     assert elem[len(elem) // 2] < 0.06, elem[len(elem) // 2]
+
+
+@pytest.mark.parametrize("cdt,tol", [(torch.float16, 1e-3), (torch.bfloat16, 1e-2)])
+def test_vitl14_120x230_vs_reference(cdt, tol):
+    """BASELINE config 4's architecture (ViT-L/14, 24 layers x 16 heads, patch 14) against the
+    reference at 120x230 (not a multiple of 14: floor grid 8x16, N = 129)."""
+    g = golden("vitl14_1x120x230")
+    m = build("vitl14", VITL14_CFG, cdt)
+    cap = capture(m)
+    with torch.no_grad():
+        out = m(images(1, 120, 230).to(DEV), return_loss=False)
+    assert rel_err(cap["maps"][0], g["map0"]) < tol
+    assert rel_err(cap["maps"][3], g["map3"]) < tol
+    for i in range(4):
+        fl = cap["maps"][i].flatten().cpu()
+        assert rel_err(fl[g[f"map_idx{i}"]], g[f"map_val{i}"]) < 2 * tol, i
+    assert rel_err(cap["score"], g["score"]) < tol
+    assert rel_err(cap["seg_low"], g["seg_low"]) < tol
+    assert rel_err(cap["depth_low"], g["depth_low"]) < tol
+    assert rel_err(out["seg"].flatten().cpu()[g["seg_idx"]], g["seg_val"]) < tol
+
+
+def test_vitl14_full_resolution_train_step():
+    """ViT-L/14 at 1024x2048 (grid 73x146, N = 10659 = 1 + 64*166 + 34: the ragged-N attention
+    kernels): one bf16 fwd+bwd on one image gives finite backbone gradients, and the eval
+    forward of the same image is per-image independent within a batch of two."""
+    m = build("vitl14", VITL14_CFG, torch.bfloat16)
+    m.train()
+    for p in m.parameters():
+        p.requires_grad_(True)
+    x = images(2, 1024, 2048).to(DEV).to(torch.bfloat16)
+    seg_t = torch.randint(0, 19, (1, 1024, 2048), device=DEV)
+    o = m(x[:1].contiguous(), gt_semantic_seg=seg_t, return_loss=True)
+    assert o["main_output"].shape == (1, 19, 1024, 2048)
+    F.cross_entropy(o["main_output"], seg_t, ignore_index=255).backward()
+    for name in ("conv1.weight", "transformer.resblocks.0.attn.in_proj_weight",
+                 "transformer.resblocks.23.mlp.c_proj.weight"):
+        gr = dict(m.backbone.named_parameters())[name].grad
+        assert gr is not None and torch.isfinite(gr).all() and gr.abs().sum() > 0, name
+    m.eval()
+    cap = capture(m)
+    with torch.no_grad():
+        m(x, return_loss=False)
+        seg2 = cap["seg_low"].clone()
+        assert cap["maps"][0].shape == (2, 1024, 73, 146)
+        m(x[1:].contiguous(), return_loss=False)
+        seg1 = cap["seg_low"]
+    assert torch.isfinite(seg2).all()
+    assert rel_err(seg2[1:], seg1) < 1e-2
 
 
 def test_backbone_grads_vs_oracle_vitb16():

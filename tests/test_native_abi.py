@@ -48,7 +48,7 @@ def test_no_oracle_in_product_package():
     (lambda L: L.dclip_attn_fwd(2, None, None, None, 1, 8, 2, 32, 1.0, None), "head_dim must be 64"),
     (lambda L: L.dclip_layernorm_fwd(None, 0, None, None, None, 0, None, None, 4, 4098, 1e-5, None), "cols"),
     (lambda L: L.dclip_score_map(None, 0, None, None, 1, 4, 512, 40, 1e-12, None), "K must be"),
-    (lambda L: L.dclip_im2col(None, 0, None, 0, 1, 3, 8, 8, 16, None), "smaller than one patch"),
+    (lambda L: L.dclip_im2col(None, 0, None, 0, 768, 1, 3, 8, 8, 16, None), "smaller than one patch"),
 ])
 def test_argument_errors_are_reported(call, needle):
     L = N.load()

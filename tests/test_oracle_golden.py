@@ -6,7 +6,7 @@ were generated from /root/reference by tests/golden/gen_golden.py.
 import torch
 import torch.nn.functional as F
 
-from helpers import (TINY_CFG, TINY_CTX_CFG, CITYSCAPES_CFG, spec_state_dict, golden, class_tokens,
+from helpers import (TINY_CFG, TINY_CTX_CFG, CITYSCAPES_CFG, VITL14_CFG, spec_state_dict, golden, class_tokens,
                      images, rel_err, stats)
 from oracle import denseclip_oracle as O
 
@@ -52,6 +52,25 @@ def test_vitb16_small_matches_reference():
         assert torch.allclose(stats(out["maps"][i]), g[f"map_stats{i}"], rtol=1e-4, atol=1e-4)
     assert rel_err(out["maps"][0], g["map0"]) < 1e-5
     assert rel_err(out["maps"][11], g["map11"]) < 1e-4
+    assert rel_err(out["score"], g["score"]) < 1e-4
+    assert rel_err(out["seg_low"], g["seg_low"]) < 1e-4
+    assert rel_err(out["depth_low"], g["depth_low"]) < 1e-4
+    assert rel_err(out["seg"].flatten()[g["seg_idx"]], g["seg_val"]) < 1e-4
+
+
+def test_vitl14_small_matches_reference():
+    """BASELINE config 4's architecture (ViT-L/14: width 1024, 24 layers, 16 heads, patch 14)
+    at 120x230, which is not a multiple of 14: the patchify keeps the 8x16 floor grid."""
+    g = golden("vitl14_1x120x230")
+    x = images(1, 120, 230)
+    out, _ = _fwd("vitl14", VITL14_CFG, x)
+    assert len(out["maps"]) == 4 and out["maps"][0].shape == (1, 1024, 8, 16)
+    for i in range(4):
+        fl = out["maps"][i].flatten()
+        assert rel_err(fl[g[f"map_idx{i}"]], g[f"map_val{i}"]) < 1e-4, i
+        assert torch.allclose(stats(out["maps"][i]), g[f"map_stats{i}"], rtol=1e-4, atol=1e-4)
+    assert rel_err(out["maps"][0], g["map0"]) < 1e-5
+    assert rel_err(out["maps"][3], g["map3"]) < 1e-4
     assert rel_err(out["score"], g["score"]) < 1e-4
     assert rel_err(out["seg_low"], g["seg_low"]) < 1e-4
     assert rel_err(out["depth_low"], g["depth_low"]) < 1e-4
