@@ -31,6 +31,7 @@ import torch.distributed as dist  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
+PEAK_FP8_TFLOPS = 5000.0  # MI355X dense fp8 (block-scaled f8f6f4 MFMA at 2x the bf16 rate)
 PEAK_HBM_GBS = 8000.0
 FUSED_HEAD_LOSS = True  # resize + CE / SILog fused (same loss; no 1024x2048 logits in HBM)
 # backbone kwargs per --arch: ViT-B/16 is seg/configs/denseclip_cityscapes.yaml's own backbone;
@@ -56,6 +57,10 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--arch", choices=sorted(ARCHS), default="vitb16",
                     help="vitb16: the headline (BASELINE configs[1]); vitl14: BASELINE configs[3]'s backbone")
+    ap.add_argument("--infer", action="store_true",
+                    help="inference forward only (eval mode, seg + depth at full resolution, no grad)")
+    ap.add_argument("--attn-fp8", action="store_true",
+                    help="attention on the e4m3 MFMA kernel (BASELINE configs[4]; inference only, implies --infer)")
     ap.add_argument("--unfused-head-loss", action="store_true",
                     help="materialise the resized logits/depth and use F.cross_entropy + SILogLoss")
     return ap.parse_args()
@@ -95,7 +100,12 @@ def run_steps(model, opt, batch, steps, silog):
     from denseclip_vit_multimodal_amd.train import train_step
     loss = None
     for _ in range(steps):
-        loss = train_step(model, opt, batch, silog)
+        if opt is None:  # inference: eval forward, seg + depth resized to the image
+            with torch.no_grad():
+                out = model(batch[0], return_loss=False)
+            loss = out["seg"][0, 0, 0, 0]
+        else:
+            loss = train_step(model, opt, batch, silog)
     return loss
 
 
@@ -153,6 +163,7 @@ def cpu_baseline(H, W, threads):
 def main():
     global FUSED_HEAD_LOSS
     args = parse()
+    args.infer = args.infer or args.attn_fp8
     FUSED_HEAD_LOSS = not args.unfused_head_loss
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -172,6 +183,10 @@ def main():
 
     def setup(mode):
         model = make_model(dev, mode, args.arch)
+        if args.infer:  # replicas: no gradients, no collective
+            model.eval()
+            model.backbone.attn_fp8 = args.attn_fp8
+            return model, None
         model.train()
         if world > 1:
             model = wrap_ddp(model, dev)
@@ -186,12 +201,14 @@ def main():
     heads = bb["heads"]
 
     # roofline of the dominant kernel: the fused attention forward (one kernel per launch)
-    n_att, tot_att, mean_att = summ.get("attn_fwd", (0, 0.0, float("nan")))
+    akey = "attn_fwd_fp8" if args.attn_fp8 else "attn_fwd"
+    peak_attn = PEAK_FP8_TFLOPS if args.attn_fp8 else PEAK_BF16_TFLOPS
+    n_att, tot_att, mean_att = summ.get(akey, (0, 0.0, float("nan")))
     fl = attn_flops_fwd(B, N, heads)
     achieved = fl / (mean_att * 1e-3) / 1e12 if n_att else None
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "attn_fwd_pmc.json")
-    if os.path.exists(pmc) and args.arch == "vitb16":
+    if os.path.exists(pmc) and args.arch == "vitb16" and not args.infer:
         with open(pmc) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
     kernels = {k: {"launches": v[0], "ms_total": round(v[1], 3), "ms_mean": round(v[2], 4)} for k, v in summ.items()}
@@ -201,13 +218,15 @@ def main():
     fl_b = 2.5 * fl
     ach_b = fl_b / (mean_ab * 1e-3) / 1e12 if n_ab else None
     # whole-model MFMA utilisation: 3 x 4.068 TFLOP per image fwd+bwd in mode F
-    if args.arch == "vitb16":
+    if args.infer:
+        model_fl = model_fwd_flops(H, W, args.arch)
+    elif args.arch == "vitb16":
         model_fl = (3 * 4.068e12 if args.mode == "F" else 4.44e12) * H * W / (1024 * 2048)
     else:
         model_fl = 3 * model_fwd_flops(H, W, args.arch) if args.mode == "F" else None
 
     mode_r = None
-    if args.mode == "F" and not args.no_mode_r:
+    if args.mode == "F" and not args.no_mode_r and not args.infer:
         del model, opt
         torch.cuda.empty_cache()
         model, opt = setup("R")
@@ -217,7 +236,7 @@ def main():
                   "what": "reference regime: backbone + text encoder frozen (train_denseclip.py:1040-1044)"}
 
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_baseline == "auto" and args.arch == "vitb16":
+    if rank == 0 and world == 1 and args.cpu_baseline == "auto" and args.arch == "vitb16" and not args.infer:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         try:
             cpu = cpu_baseline(H, W, threads)
@@ -226,7 +245,8 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "images/sec (fwd+bwd) %s DenseCLIP @%dx%d" % (
+            "metric": "images/sec (%s) %s DenseCLIP @%dx%d" % (
+                "fwd, inference" if args.infer else "fwd+bwd",
                 {"vitb16": "ViT-B/16", "vitl14": "ViT-L/14"}[args.arch], H, W),
             "value": round(value, 4),
             "unit": "images/sec",
@@ -237,16 +257,19 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "bf16 (attention e4m3)" if args.attn_fp8 else "bf16",
             "data": "synthetic (randn images, random labels/depth; random-init weights)",
-            "config": {"workload": "DenseCLIP %s seg+depth train step (mode %s), %dx%d" % (
-                           {"vitb16": "ViT-B/16", "vitl14": "ViT-L/14"}[args.arch], args.mode, H, W),
+            "config": {"workload": "DenseCLIP %s seg+depth %s, %dx%d" % (
+                           {"vitb16": "ViT-B/16", "vitl14": "ViT-L/14"}[args.arch],
+                           "inference forward" + (" (fp8 attention)" if args.attn_fp8 else "") if args.infer
+                           else "train step (mode %s)" % args.mode, H, W),
                        "per_gpu_batch": B, "global_batch": B * world, "tokens_per_image": N,
                        "parallelism": f"dp{world}", "mode": args.mode,
                        "head_loss": "fused resize+CE/SILog" if FUSED_HEAD_LOSS else "materialised resize"},
-            "roofline": {"kernel": "attn_fwd_kernel<bf16>", "bound": "mfma",
-                         "achieved": round(achieved, 2) if achieved else None, "peak": PEAK_BF16_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4) if achieved else None,
+            "roofline": {"kernel": "attn_fp8_kernel (+ amax / pack)" if args.attn_fp8 else "attn_fwd_kernel<bf16>",
+                         "bound": "mfma",
+                         "achieved": round(achieved, 2) if achieved else None, "peak": peak_attn,
+                         "unit": "TFLOP/s", "frac": round(achieved / peak_attn, 4) if achieved else None,
                          "traffic": traffic, "flops_per_launch": fl, "launches": n_att,
                          "ms_per_launch": round(mean_att, 4) if n_att else None},
             "roofline_attn_bwd": {"kernel": "attn_bwd_dq2_kernel + attn_bwd_dkdv2_kernel (+ row-0 passes)",
@@ -255,7 +278,7 @@ def main():
                                   "frac": round(ach_b / PEAK_BF16_TFLOPS, 4) if ach_b else None,
                                   "flops_per_launch": fl_b, "launches": n_ab,
                                   "ms_per_launch": round(mean_ab, 4) if n_ab else None},
-            "model_mfma": {"flops_per_image": model_fl, "achieved_tflops": round(value / world * model_fl / 1e12, 1),
+            "model_mfma": {"flops_per_image": model_fl, "peak_tflops": PEAK_BF16_TFLOPS, "achieved_tflops": round(value / world * model_fl / 1e12, 1),
                            "frac": round(value / world * model_fl / 1e12 / PEAK_BF16_TFLOPS, 4)} if model_fl else None,
             "kernels": kernels,
             "mode_R": mode_r,

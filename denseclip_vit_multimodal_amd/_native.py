@@ -61,6 +61,8 @@ _SIGS = {
                                  _c_void_p, _c_void_p, _f32, _f32, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p,
                                  _c_void_p],
     "dclip_attn_bwd_workspace": [_i32, _i32, _i32],
+    "dclip_attn_fwd_fp8": [_i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i32, _i32, _c_void_p],
+    "dclip_attn_fwd_fp8_workspace": [_i32, _i32, _i32],
     "dclip_gemm_tn_plan": [_i64, _i64, _i64, _c_void_p, _c_void_p],
 }
 EXPORTED = sorted(list(_SIGS) + ["dclip_last_error", "dclip_abi_version"])
@@ -94,6 +96,7 @@ def load(path=None):
         lib.dclip_abi_version.restype = ctypes.c_int
         lib.dclip_abi_version.argtypes = []
         lib.dclip_attn_bwd_workspace.restype = ctypes.c_int64  # a size, not a status
+        lib.dclip_attn_fwd_fp8_workspace.restype = ctypes.c_int64
         # kernel-variant knobs for A/B runs: DCLIP_OPTIONS="id=value,..." (DCLIP_OPT_* ids of dclip.h)
         for kv in filter(None, os.environ.get("DCLIP_OPTIONS", "").split(",")):
             k, v = kv.split("=")

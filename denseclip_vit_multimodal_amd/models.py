@@ -170,11 +170,14 @@ class CLIPVisionTransformer(nn.Module):
     out_index in ascending order, in x.dtype.  Runs on the HIP kernels only (x must be a
     GPU tensor).  The compute dtype of the GEMM/attention operands is bf16 for bf16 input,
     fp16 for fp16 input and `compute_dtype` (default bf16) for fp32 input; the residual
-    stream and LayerNorms are fp32 throughout.
+    stream and LayerNorms are fp32 throughout.  `attn_fp8=True` (BASELINE config 5, inference
+    only) runs the attention core on the e4m3 MFMA kernel (dclip_attn_fwd_fp8); a backward
+    through it raises.
     """
 
     def __init__(self, input_resolution=224, patch_size=16, width=768, layers=12, heads=12, output_dim=768,
-                 drop_path_rate=0.0, out_indices=None, pretrained=None, compute_dtype=torch.bfloat16, **kwargs):
+                 drop_path_rate=0.0, out_indices=None, pretrained=None, compute_dtype=torch.bfloat16,
+                 attn_fp8=False, **kwargs):
         super().__init__()
         self.pretrained = pretrained
         self.input_resolution = input_resolution
@@ -184,6 +187,7 @@ class CLIPVisionTransformer(nn.Module):
         self.heads = heads
         self.patch_size = patch_size
         self.compute_dtype = compute_dtype
+        self.attn_fp8 = bool(attn_fp8)
         self.drop_path_rate = drop_path_rate
         self.conv1 = nn.Conv2d(3, width, kernel_size=patch_size, stride=patch_size, bias=False)
         scale = width ** -0.5
@@ -269,7 +273,7 @@ class CLIPVisionTransformer(nn.Module):
         tok = ops.PatchEmbedFn.apply(x, self.conv1.weight, self.class_embedding, self.positional_embedding,
                                      self.ln_pre.weight, self.ln_pre.bias, p, cdt)
         outs = []
-        meta = (B, Ntok, self.heads, cdt)
+        meta = (B, Ntok, self.heads, cdt, self.attn_fp8)
         rmeta = (B, Ntok, gh, gw, x.dtype)
         last = max(self.out_indices) if self.out_indices else -1
         for i, blk in enumerate(self.transformer.resblocks):

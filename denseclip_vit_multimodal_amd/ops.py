@@ -237,6 +237,20 @@ def attn_fwd(qkv, B, Ntok, H, scale):
     return o, lse
 
 
+def attn_fwd_fp8(qkv, B, Ntok, H):
+    """fp8 (e4m3) attention forward, inference only (BASELINE config 5): the same qkv / o / lse
+    contract as attn_fwd, on the block-scaled fp8 MFMA (dclip_attn_fwd_fp8)."""
+    _check(qkv)
+    C = qkv.shape[1] // 3
+    o = torch.empty(B * Ntok, C, dtype=qkv.dtype, device=qkv.device)
+    lse = torch.empty(B * H * Ntok, dtype=torch.float32, device=qkv.device)
+    ws = torch.empty(N.lib().dclip_attn_fwd_fp8_workspace(B, Ntok, H), dtype=torch.uint8, device=qkv.device)
+    e0 = _tic()
+    N.call("dclip_attn_fwd_fp8", _dt(qkv), _p(qkv), _p(o), _p(lse), _p(ws), B, Ntok, H, C // H, _stream())
+    _toc("attn_fwd_fp8", e0)
+    return o, lse
+
+
 def attn_bwd(qkv, o, dout, lse, B, Ntok, H, scale):
     _check(qkv, o, dout, lse)
     C = o.shape[1]
@@ -422,13 +436,13 @@ class BlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, meta, ln1w, ln1b, w_in, b_in, w_out, b_out, ln2w, ln2b, w1, b1, w2, b2):
-        B, Ntok, H, cdt = meta
+        B, Ntok, H, cdt, fp8 = meta
         C = x.shape[1]
         scale = (C // H) ** -0.5
         xh1, mu1, rs1 = layernorm_fwd(x, ln1w.detach(), ln1b.detach(), cdt)
         qkv = gemm(xh1, WEIGHTS.get(w_in, cdt), N.EPI_STORE_SCALED, bias=b_in.detach(),
                    aux=qkv_scale_vector(C, H, x.device))
-        o, lse = attn_fwd(qkv, B, Ntok, H, scale)
+        o, lse = attn_fwd_fp8(qkv, B, Ntok, H) if fp8 else attn_fwd(qkv, B, Ntok, H, scale)
         xm = gemm(o, WEIGHTS.get(w_out, cdt), N.EPI_RESIDUAL, bias=b_out.detach(), aux=x)
         xh2, mu2, rs2 = layernorm_fwd(xm, ln2w.detach(), ln2b.detach(), cdt)
         z, h = gemm(xh2, WEIGHTS.get(w1, cdt), N.EPI_GELU, bias=b1.detach())
@@ -442,7 +456,9 @@ class BlockFn(torch.autograd.Function):
     def backward(ctx, dxo):
         (x, mu1, rs1, xh1, qkv, o, lse, xm, mu2, rs2, xh2, z, h,
          ln1w, w_in, w_out, ln2w, w1, w2) = ctx.saved_tensors
-        B, Ntok, H, cdt = ctx.meta
+        B, Ntok, H, cdt, fp8 = ctx.meta
+        if fp8:
+            raise RuntimeError("fp8 attention is forward-only (inference); train with attn_fp8=False")
         C = x.shape[1]
         scale = (C // H) ** -0.5
         need = ctx.needs_input_grad

@@ -151,6 +151,16 @@ int dclip_attn_bwd(int dt, const void* qkv, const void* o, const void* dout,
                    int B, int N, int H, int D, float scale, void* stream);
 int64_t dclip_attn_bwd_workspace(int B, int N, int H);
 
+/* fp8 attention forward (BASELINE config 5; inference only — there is no fp8 backward).
+ * Same qkv / o / lse contract as dclip_attn_fwd (q pre-multiplied by d^-0.5*log2(e)), computed
+ * on the block-scaled e4m3 MFMA v_mfma_scale_f32_32x32x64_f8f6f4: q, k, v are quantised to
+ * OCP e4m3 with one scale per (image, head, q|k|v) = 448 / amax, P to e4m3 unscaled (P <= 1).
+ * ws: dclip_attn_fwd_fp8_workspace(B, N, H) bytes, 256-byte aligned (the packed q8 / k8 /
+ * transposed v8 planes and the amax table).  H <= 64, D must be 64.                      */
+int dclip_attn_fwd_fp8(int dt, const void* qkv, void* o, float* lse, void* ws,
+                       int B, int N, int H, int D, void* stream);
+int64_t dclip_attn_fwd_fp8_workspace(int B, int N, int H);
+
 /* Non-overlapping p x p patches of img (B, Cin, Hin, Win) (img_dt) ->
  * out (B*gh*gw, ldo) (out_dt), column order (c, ky, kx) = conv weight flattening,
  * gh = Hin / p, gw = Win / p (floor, as Conv2d stride p).  Columns Cin*p*p .. ldo-1
