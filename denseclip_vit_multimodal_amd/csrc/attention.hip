@@ -1322,6 +1322,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq2_kernel(const T* 
                                                                        const T* __restrict__ dout,
                                                                        const float* __restrict__ lse,
                                                                        float* __restrict__ delta,
+                                                                       float* __restrict__ nstat,
                                                                        T* __restrict__ dqkv, int N, int H,
                                                                        float scale) {
     constexpr int QB = 32 * NW, PIECES = Dq2Ctx<T, NW>::PIECES;
@@ -1386,7 +1387,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq2_kernel(const T* 
             ppart += (float)c.gf[s][j] * (float)v0[s][j];
         }
     const float dl = xhalf_sum(dpart);
-    if (c.h == 0) delta[(int64_t)bh * N + q] = dl;
+    if (c.h == 0) {
+        delta[(int64_t)bh * N + q] = dl;
+        // negated copies for the dK/dV pass, whose S / dP chains start from -L / -delta
+        nstat[(int64_t)bh * N + q] = -L;
+        nstat[(int64_t)gridDim.x / nq * N + (int64_t)bh * N + q] = -dl;
+    }
     c.negL = -L;
     c.negD = -dl;
     const float p0 = __builtin_amdgcn_exp2f(xhalf_sum(spart) - L);
@@ -1755,8 +1761,9 @@ struct Dkv2Ctx {
     static constexpr int SPW = 128 / NW;             // statistics per wave per slice
     char* smem;
     rsrc_t rs, rg, rl, rd;  // qkv rows, dO rows, lse, delta of this (batch, head)
+    rsrc_t rmine;           // this wave's piece source (rs for the Q waves, rg for the dO waves)
     uint32_t voff[PIECES];
-    uint32_t ldq, ldg;       // row pitches (bytes)
+    uint32_t ldq, ldg, ldmine;  // row pitches (bytes)
     int nt, lane, l32, h, wave;
     frag kf[4], vf[4];
     f32x16 dk[2], dv[2];
@@ -1768,16 +1775,14 @@ __device__ __forceinline__ void dkv2_issue(Dkv2Ctx<T, NW>& c, int t, int slot) {
     typedef Dkv2Ctx<T, NW> X;
     char* base = c.smem + slot * X::SLOT;
     const int r0 = 1 + 64 * t;
+    // a wave's pieces are all Q (waves 0 .. NW/2-1) or all dO: its source resource and row
+    // pitch were chosen once at setup, so the issue is one straight-line block (no branches
+    // splitting the step's schedule)
+    const uint32_t soff = (uint32_t)r0 * c.ldmine;
 #pragma unroll
-    for (int i = 0; i < X::PIECES; ++i) {
-        const int piece = c.wave * X::PIECES + i;  // 0..7 Q, 8..15 dO
-        if (piece < 8)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rs, LDS_PTR(base + piece * 1024), 16, c.voff[i],
-                                                     (uint32_t)r0 * c.ldq, 0, 0);
-        else
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rg, LDS_PTR(base + piece * 1024), 16, c.voff[i],
-                                                     (uint32_t)r0 * c.ldg, 0, 0);
-    }
+    for (int i = 0; i < X::PIECES; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rmine, LDS_PTR(base + (c.wave * X::PIECES + i) * 1024), 16,
+                                                 c.voff[i], soff, 0, 0);
     // statistics: waves 0 .. NW/2-1 load L, the others delta, SPW values each
     const int part = c.wave % (NW / 2);
     const bool is_l = c.wave < NW / 2;
@@ -1816,8 +1821,8 @@ __device__ __forceinline__ void dkv2_step(Dkv2Ctx<T, NW>& c, int t) {
             const f32x4 Dv = *(const f32x4*)(Ds + 8 * g4 + 4 * c.h);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                sacc[4 * g4 + e] = -Lv[e];
-                pacc[4 * g4 + e] = -Dv[e];
+                sacc[4 * g4 + e] = Lv[e];  // already negated by the dQ pass (no VALU here)
+                pacc[4 * g4 + e] = Dv[e];
             }
         }
 #pragma unroll
@@ -1857,6 +1862,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv2_kernel(const T
                                                                          const T* __restrict__ dout,
                                                                          const float* __restrict__ lse,
                                                                          const float* __restrict__ delta,
+                                                                         const float* __restrict__ nlse,
+                                                                         const float* __restrict__ ndelta,
                                                                          T* __restrict__ dqkv, int N, int H,
                                                                          float dk_scale) {
     constexpr int KB = 32 * NW;
@@ -1902,8 +1909,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv2_kernel(const T
 
     c.rs = make_rsrc(Bb, (uint32_t)N * c.ldq);
     c.rg = make_rsrc(dOb, (uint32_t)N * c.ldg);
-    c.rl = make_rsrc(lse + (int64_t)bh * N, (uint32_t)N * 4);
-    c.rd = make_rsrc(delta + (int64_t)bh * N, (uint32_t)N * 4);
+    c.rl = make_rsrc(nlse + (int64_t)bh * N, (uint32_t)N * 4);
+    c.rd = make_rsrc(ndelta + (int64_t)bh * N, (uint32_t)N * 4);
+    static_assert(8 % X::PIECES == 0, "a wave's pieces must not straddle the Q / dO boundary");
+    const bool q_wave = c.wave * X::PIECES < 8;
+    c.rmine = q_wave ? c.rs : c.rg;
+    c.ldmine = q_wave ? c.ldq : c.ldg;
 #pragma unroll
     for (int i = 0; i < X::PIECES; ++i) {
         const int piece = c.wave * X::PIECES + i;
@@ -2001,17 +2012,18 @@ bool bwd2_launch(const void* qkv, const void* o, const void* dout, const float* 
     if (N < 257 || (N - 1) % 256 != 0 || dclip_option(DCLIP_OPT_ATTN_BWD_KERNEL) == 1) return false;
     const int nsplit = (N + R0_CHUNK - 1) / R0_CHUNK;
     float* ws0 = delta + (int64_t)B * H * N;
+    float* nstat = ws0 + (int64_t)B * H * ((N + 63) / 64) * 192;  // [-lse | -delta], B*H*N each
     attn_bwd_row0_dq_part<T><<<B * H * nsplit, 256, 0, st>>>((const T*)qkv, (const T*)o, (const T*)dout, lse, ws0, N, H,
                                                             nsplit);
     attn_bwd_row0_dq_merge<T><<<B * H, 64, 0, st>>>((const T*)o, (const T*)dout, ws0, delta, (T*)dqkv, N, H, nsplit,
                                                     scale);
     attn_bwd_dq2_kernel<T, 8><<<B * H * ((N - 1) / 256), 512, 0, st>>>((const T*)qkv, (const T*)o, (const T*)dout, lse,
-                                                                      delta, (T*)dqkv, N, H, scale);
+                                                                      delta, nstat, (T*)dqkv, N, H, scale);
     attn_bwd_row0_dkdv_part<T><<<B * H * nsplit, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, ws0, N, H,
                                                               nsplit);
     attn_bwd_row0_dkdv_merge<T><<<B * H, 64, 0, st>>>(ws0, (T*)dqkv, N, H, nsplit, 1.0f / LOG2E);
-    attn_bwd_dkdv2_kernel<T, 4><<<B * H * ((N - 1) / 128), 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta,
-                                                                        (T*)dqkv, N, H, 1.0f / LOG2E);
+    attn_bwd_dkdv2_kernel<T, 4><<<B * H * ((N - 1) / 128), 256, 0, st>>>(
+        (const T*)qkv, (const T*)dout, lse, delta, nstat, nstat + (int64_t)B * H * N, (T*)dqkv, N, H, 1.0f / LOG2E);
     return true;
 }
 
@@ -2065,8 +2077,9 @@ extern "C" int dclip_attn_fwd(int dt, const void* qkv, void* o, float* lse, int 
 }
 
 extern "C" int64_t dclip_attn_bwd_workspace(int B, int N, int H) {
-    // delta (B*H*N) + the CLS-split row-0 partials (B*H*ceil(N/64)*192)
-    return (int64_t)B * H * N + (int64_t)B * H * ((N + 63) / 64) * 192;
+    // delta (B*H*N) + the CLS-split row-0 partials (B*H*ceil(N/64)*192) + the negated
+    // statistics the CLS-split dK/dV pass reads (-lse, -delta: 2*B*H*N)
+    return 3 * (int64_t)B * H * N + (int64_t)B * H * ((N + 63) / 64) * 192;
 }
 
 extern "C" int dclip_attn_bwd(int dt, const void* qkv, const void* o, const void* dout, const float* lse,

@@ -142,7 +142,8 @@ int dclip_attn_fwd(int dt, const void* qkv, void* o, float* lse,
 /* Attention backward (flash-style recompute from lse; no N x N buffer, no atomics):
  * a query-major dQ pass (which also writes delta = rowsum(dout*o) to delta_ws) and a
  * key-major dK/dV pass.  dout: (B*N, H*D) dt.  delta_ws: f32 workspace of
- * dclip_attn_bwd_workspace(B, N, H) floats (its first B*H*N receive delta).
+ * dclip_attn_bwd_workspace(B, N, H) floats (its first B*H*N receive delta; the rest holds
+ * the CLS-split row-0 partials and the negated lse / delta planes of the dK/dV pass).
  * qkv as for dclip_attn_fwd (q pre-multiplied by scale*log2(e)); `scale` = d^-0.5.
  * dqkv: (B*N, 3*H*D) dt output, [dq | dk | dv] in the qkv layout: gradients with
  * respect to the UNSCALED q, k, v (i.e. the in-projection output before the q scale).  */
