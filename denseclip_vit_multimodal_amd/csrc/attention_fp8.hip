@@ -34,6 +34,8 @@
 // contiguous bytes too.
 #include "common.h"
 
+#include <type_traits>
+
 namespace {
 
 typedef int i32x8 __attribute__((ext_vector_type(8)));
@@ -213,7 +215,15 @@ __global__ void __launch_bounds__(512) attn_fp8_kernel(const uint8_t* __restrict
     store_unit(0, pre);
     if (nunit > 1) pre = load_unit(1);
     __syncthreads();
-    for (int u = 0; u < nunit; ++u) {
+    // one 64-key unit; TAIL: the last unit when N is not a multiple of 64 (keys >= N masked).
+    // VALU per unit and lane is the limit at the fp8 MFMA rate (4 MFMAs = 256 cycles against
+    // 32 exponentials = 256 issue cycles), so: raw v_exp_f32 (no denormal range-reduction
+    // sequence), the dequantisation scale folded into the exponent's FMA, the maximum taken
+    // on the raw scores (sscale > 0: max(raw) * sscale == max(raw * sscale) exactly), the mask
+    // only in the peeled tail unit, and the O / l rescale skipped when no lane's maximum moved
+    // (alpha == 1 exactly then: the skipped multiplications were identities).
+    auto unit = [&](int u, auto tail_tag) {
+        constexpr bool TAIL = decltype(tail_tag)::value;
         const int buf = u & 1;
         if (u + 1 < nunit) {
             store_unit(buf ^ 1, pre);  // buffer buf^1 was last read in unit u-1 (barrier below)
@@ -229,48 +239,55 @@ __global__ void __launch_bounds__(512) attn_fp8_kernel(const uint8_t* __restrict
         for (int i = 0; i < 16; ++i) zero[i] = 0.f;
         f32x16 s0 = mfma_fp8(ka, qf, zero);
         f32x16 s1 = mfma_fp8(kb, qf, zero);
-        // scores in the log2 domain; keys past N masked in the last unit
-        float mx = -INFINITY;
-        const int kbase = u * 64 + 4 * half;
-        const bool tail = (u + 1) * 64 > N;
+        if constexpr (TAIL) {
+            const int kbase = u * 64 + 4 * half;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int kr = (i & 3) + 8 * (i >> 2);
-            float a = s0[i] * sscale, c = s1[i] * sscale;
-            if (tail) {
-                if (kbase + kr >= N) a = -INFINITY;
-                if (kbase + 32 + kr >= N) c = -INFINITY;
+            for (int i = 0; i < 16; ++i) {
+                const int kr = (i & 3) + 8 * (i >> 2);
+                if (kbase + kr >= N) s0[i] = -INFINITY;
+                if (kbase + 32 + kr >= N) s1[i] = -INFINITY;
             }
-            s0[i] = a;
-            s1[i] = c;
-            mx = fmaxf(mx, fmaxf(a, c));
         }
+        float mx = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) mx = fmaxf(mx, fmaxf(s0[i], s1[i]));
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));  // the other half holds the query's other keys
-        const float mnew = fmaxf(m, mx);
-        const float alpha = exp2f(m - mnew);
-        m = mnew;
+        const float mnew = fmaxf(m, mx * sscale);
+        if (__builtin_amdgcn_read_exec() & __ballot(mnew > m)) {  // some lane's maximum moved
+            const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+            l *= alpha;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) o0[i] *= alpha, o1[i] *= alpha;
+            m = mnew;
+        }
+        const float nm = -mnew;
         float rs = 0.f;
         i32x8 pf;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-            float p0 = exp2f(s0[4 * g] - mnew), p1 = exp2f(s0[4 * g + 1] - mnew);
-            float p2 = exp2f(s0[4 * g + 2] - mnew), p3 = exp2f(s0[4 * g + 3] - mnew);
-            float p4 = exp2f(s1[4 * g] - mnew), p5 = exp2f(s1[4 * g + 1] - mnew);
-            float p6 = exp2f(s1[4 * g + 2] - mnew), p7 = exp2f(s1[4 * g + 3] - mnew);
+            const float p0 = __builtin_amdgcn_exp2f(fmaf(s0[4 * g], sscale, nm));
+            const float p1 = __builtin_amdgcn_exp2f(fmaf(s0[4 * g + 1], sscale, nm));
+            const float p2 = __builtin_amdgcn_exp2f(fmaf(s0[4 * g + 2], sscale, nm));
+            const float p3 = __builtin_amdgcn_exp2f(fmaf(s0[4 * g + 3], sscale, nm));
+            const float p4 = __builtin_amdgcn_exp2f(fmaf(s1[4 * g], sscale, nm));
+            const float p5 = __builtin_amdgcn_exp2f(fmaf(s1[4 * g + 1], sscale, nm));
+            const float p6 = __builtin_amdgcn_exp2f(fmaf(s1[4 * g + 2], sscale, nm));
+            const float p7 = __builtin_amdgcn_exp2f(fmaf(s1[4 * g + 3], sscale, nm));
             rs += (p0 + p1) + (p2 + p3) + (p4 + p5) + (p6 + p7);
             pf[g] = pack4_fp8_unit(p0, p1, p2, p3);      // bytes j = 4g .. 4g+3   (t = 0)
             pf[4 + g] = pack4_fp8_unit(p4, p5, p6, p7);  // bytes j = 16 + 4g ..   (t = 1)
         }
-        l = l * alpha + rs;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o0[i] *= alpha, o1[i] *= alpha;
+        l += rs;
         // O^T += V^T P^T: A = V^T rows d (0-31 / 32-63), permuted key slots
         const i32x8 va = *(const i32x8*)(vs + r * 64 + 32 * half);
         const i32x8 vb = *(const i32x8*)(vs + (32 + r) * 64 + 32 * half);
         o0 = mfma_fp8(va, pf, o0);
         o1 = mfma_fp8(vb, pf, o1);
         __syncthreads();  // everyone is done with sm[buf] and the next unit's tile is stored
-    }
+    };
+    const int nfull = N / 64;  // units with 64 valid keys; a ragged last unit is peeled
+    for (int u = 0; u < nfull; ++u) unit(u, std::false_type{});
+    if (nfull < nunit) unit(nfull, std::true_type{});
     l += __shfl_xor(l, 32, 64);
     if (q >= N) return;
     const float inv = dv / l;
