@@ -2063,6 +2063,19 @@ void bwd_launch(const void* qkv, const void* o, const void* dout, const float* l
 
 }  // namespace
 
+// query 0 (the CLS row) of the forward by the split-key row pass + merge (o row 0 and lse[0]
+// of every (image, head)); used by the fp8 forward's CLS split (attention_fp8.hip)
+void attn_row0_fwd(int dt, const void* qkv, void* o, float* lse, int B, int N, int H, hipStream_t st) {
+    const int nsplit = (N + R0_CHUNK - 1) / R0_CHUNK;
+    if (dt == DCLIP_BF16) {
+        attn_row0_part_kernel<bf16><<<B * H * nsplit, 256, 0, st>>>((const bf16*)qkv, (bf16*)o, N, H, nsplit);
+        attn_row0_merge_kernel<bf16><<<B * H, 64, 0, st>>>((bf16*)o, lse, N, H, nsplit);
+    } else {
+        attn_row0_part_kernel<f16><<<B * H * nsplit, 256, 0, st>>>((const f16*)qkv, (f16*)o, N, H, nsplit);
+        attn_row0_merge_kernel<f16><<<B * H, 64, 0, st>>>((f16*)o, lse, N, H, nsplit);
+    }
+}
+
 extern "C" int dclip_attn_fwd(int dt, const void* qkv, void* o, float* lse, int B, int N, int H, int D,
                               float scale, void* stream) {
     DCLIP_HOST_CHECK(D == HD, "dclip_attn_fwd: head_dim must be 64 (got %d)", D);

@@ -99,6 +99,34 @@ __global__ void __launch_bounds__(256) fp8_amax_kernel(const T* __restrict__ qkv
     for (int i = threadIdx.x; i < 3 * H; i += 256) atomicMax(&amax[b * 3 * H + i], red[i]);
 }
 
+// the same with one thread per (8-column chunk, token parity): blockDim = 2 * ncol8 (<= 1024),
+// every thread walks 32 of the 64 tokens with 8 loads in flight (the loop above keeps one
+// load in flight per thread and leaves 256 - ncol8 % 256 threads idle on its last pass)
+template <typename T>
+__global__ void __launch_bounds__(1024) fp8_amax2_kernel(const T* __restrict__ qkv, int* __restrict__ amax, int N,
+                                                         int H) {
+    __shared__ int red[3 * 64];
+    const int C = H * 64, ncol8 = 3 * C / 8;
+    const int b = blockIdx.y, t0 = blockIdx.x * 64;
+    const int c8 = threadIdx.x % ncol8, par = threadIdx.x / ncol8;
+    for (int i = threadIdx.x; i < 3 * H; i += blockDim.x) red[i] = 0;
+    __syncthreads();
+    const int ntok = min(64, N - t0);
+    const T* p = qkv + ((int64_t)b * N + t0) * 3 * C + c8 * 8;
+    float m = 0.f;
+#pragma unroll 8
+    for (int t = par; t < ntok; t += 2) {
+        const uint4 raw = *(const uint4*)(p + (int64_t)t * 3 * C);
+        const T* e = (const T*)&raw;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) m = fmaxf(m, fabsf((float)e[k]));
+    }
+    const int col = c8 * 8, which = col / C, h = (col % C) / 64;
+    atomicMax(&red[which * H + h], __float_as_int(m));
+    __syncthreads();
+    for (int i = threadIdx.x; i < 3 * H; i += blockDim.x) atomicMax(&amax[b * 3 * H + i], red[i]);
+}
+
 // ---------------------------------------------------------------------------- 2. pack
 // grid (Npad / 64, H, B), 256 threads: one 64-token unit of one head
 template <typename T>
@@ -175,12 +203,12 @@ template <typename T>
 __global__ void __launch_bounds__(512) attn_fp8_kernel(const uint8_t* __restrict__ q8, const uint8_t* __restrict__ k8,
                                                        const uint8_t* __restrict__ vt8, const int* __restrict__ amax,
                                                        T* __restrict__ o, float* __restrict__ lse, int N, int H,
-                                                       int Npad) {
+                                                       int Npad, int q0) {
     __shared__ __attribute__((aligned(16))) uint8_t sm[2][2][64 * 64];  // [buf][K | V^T][64 rows x 64 B]
     const int h = blockIdx.y, b = blockIdx.z;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int r = lane & 31, half = lane >> 5;
-    const int q = blockIdx.x * 256 + wave * 32 + r;  // this lane's query (column of S^T)
+    const int q = q0 + blockIdx.x * 256 + wave * 32 + r;  // this lane's query (column of S^T)
     const int64_t hb = (int64_t)b * H + h;
     const float* am = (const float*)amax + b * 3 * H;
     const float dq = am[h] > 0.f ? am[h] / FP8_MAX : 1.f;
@@ -329,15 +357,26 @@ extern "C" int dclip_attn_fwd_fp8(int dt, const void* qkv, void* o, float* lse, 
         dclip_set_error("dclip_attn_fwd_fp8: memset failed");
         return DCLIP_ERR_HIP;
     }
-    const dim3 ga((N + 63) / 64, B), gp(npad / 64, H, B), gf((N + 255) / 256, H, B);
+    // CLS split (N = 1 + 256k, the benchmark's 8193): query 0 by the bf16 row pass of the
+    // 16-bit forward, queries 1..N-1 as full 256-query blocks — no near-empty last block
+    // (at N = 8193 that block held 1 query and cost a full key sweep: 33 blocks -> 32, and
+    // B*H*32 workgroups fill whole rounds of 2 workgroups per CU)
+    const bool cls = N >= 257 && (N - 1) % 256 == 0;
+    const int q0 = cls ? 1 : 0;
+    const dim3 ga((N + 63) / 64, B), gp(npad / 64, H, B), gf((N - q0 + 255) / 256, H, B);
+    if (cls) attn_row0_fwd(dt, qkv, o, lse, B, N, H, st);
+    const int ncol8 = 3 * H * 64 / 8;
+    const bool amax2 = 2 * ncol8 <= 1024 && (2 * ncol8) % 64 == 0;
     if (dt == DCLIP_BF16) {
-        fp8_amax_kernel<bf16><<<ga, 256, 0, st>>>((const bf16*)qkv, amax, N, H);
+        if (amax2) fp8_amax2_kernel<bf16><<<ga, 2 * ncol8, 0, st>>>((const bf16*)qkv, amax, N, H);
+        else fp8_amax_kernel<bf16><<<ga, 256, 0, st>>>((const bf16*)qkv, amax, N, H);
         fp8_pack_kernel<bf16><<<gp, 256, 0, st>>>((const bf16*)qkv, amax, q8, k8, vt8, N, H, npad);
-        attn_fp8_kernel<bf16><<<gf, 512, 0, st>>>(q8, k8, vt8, amax, (bf16*)o, lse, N, H, npad);
+        attn_fp8_kernel<bf16><<<gf, 512, 0, st>>>(q8, k8, vt8, amax, (bf16*)o, lse, N, H, npad, q0);
     } else {
-        fp8_amax_kernel<f16><<<ga, 256, 0, st>>>((const f16*)qkv, amax, N, H);
+        if (amax2) fp8_amax2_kernel<f16><<<ga, 2 * ncol8, 0, st>>>((const f16*)qkv, amax, N, H);
+        else fp8_amax_kernel<f16><<<ga, 256, 0, st>>>((const f16*)qkv, amax, N, H);
         fp8_pack_kernel<f16><<<gp, 256, 0, st>>>((const f16*)qkv, amax, q8, k8, vt8, N, H, npad);
-        attn_fp8_kernel<f16><<<gf, 512, 0, st>>>(q8, k8, vt8, amax, (f16*)o, lse, N, H, npad);
+        attn_fp8_kernel<f16><<<gf, 512, 0, st>>>(q8, k8, vt8, amax, (f16*)o, lse, N, H, npad, q0);
     }
     DCLIP_LAUNCH_CHECK();
     return 0;

@@ -121,3 +121,6 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
     const int xcd = bid % 8, loc = bid / 8;
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
+
+// query 0 (CLS row) of the 16-bit forward: split-key row pass + merge (attention.hip)
+void attn_row0_fwd(int dt, const void* qkv, void* o, float* lse, int B, int N, int H, hipStream_t st);

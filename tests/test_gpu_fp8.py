@@ -88,6 +88,23 @@ def exact(qkv, B, N, H, rows=None):
     return (p @ v).permute(0, 2, 1, 3).reshape(B, q.shape[2], C)
 
 
+def cls_split(N):
+    """N = 1 + 256k: dclip_attn_fwd_fp8 computes query 0 (the CLS row) with the 16-bit
+    split-key row pass of the bf16 forward, so that row is held to the EXACT attention (16-bit
+    output rounding) instead of the fp8 emulation."""
+    return N >= 257 and (N - 1) % 256 == 0
+
+
+def check_row0_exact(o, lse, qkv, B, N, H):
+    """o, lse: the kernel's row 0 (B, C) / (B, H) on the host in float64."""
+    q, k, v = qkv.double().cpu().view(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    s = q[:, :, :1] @ k.transpose(-1, -2)  # (B, H, 1, N), log2 domain
+    lref = torch.logsumexp(s * math.log(2.0), -1)[..., 0] / math.log(2.0)
+    oref = (torch.softmax(s * math.log(2.0), -1) @ v)[:, :, 0].reshape(B, -1)
+    assert rel_err(o, oref) < 1e-2, rel_err(o, oref)
+    assert ((lse - lref).abs() <= 1e-3 + 1e-3 * lref.abs()).all(), float((lse - lref).abs().max())
+
+
 def check_emulation(o, lse, ref, lref):
     assert rel_err(o, ref) < 2e-2, rel_err(o, ref)
     rows = ((o - ref).norm(dim=-1) / ref.norm(dim=-1).clamp(min=1e-30))
@@ -107,11 +124,15 @@ def test_attn_fp8_matches_emulation_and_exact(N, dt):
     B, H = 2, 3
     qkv = make_qkv(B, N, H, dt)
     o, lse = ops.attn_fwd_fp8(qkv, B, N, H)
-    rows = torch.arange(N)
+    r0 = 1 if cls_split(N) else 0
+    if r0:
+        o0, l0 = pick(o, lse, B, N, H, torch.arange(1))
+        check_row0_exact(o0[:, 0], l0[:, :, 0], qkv, B, N, H)
+    rows = torch.arange(r0, N)
     o, lse = pick(o, lse, B, N, H, rows)
-    ref, lref = emulate(qkv, B, N, H)
+    ref, lref = emulate(qkv, B, N, H, rows)
     check_emulation(o, lse, ref, lref)
-    e = rel_err(o, exact(qkv, B, N, H))
+    e = rel_err(o, exact(qkv, B, N, H, rows))
     assert e < 1e-1, e
 
 
@@ -127,7 +148,10 @@ def test_attn_fp8_full_length_heads_and_batch():
     qkv = qkv.view(B * N, -1).to(torch.bfloat16)
     o, lse = ops.attn_fwd_fp8(qkv, B, N, H)
     assert torch.isfinite(o).all()
-    rows = torch.cat([torch.arange(0, 70), torch.randperm(N - 140)[:300] + 70, torch.arange(N - 70, N)])
+    assert cls_split(N)
+    o0, l0 = pick(o, lse, B, N, H, torch.arange(1))
+    check_row0_exact(o0[:, 0], l0[:, :, 0], qkv, B, N, H)
+    rows = torch.cat([torch.arange(1, 70), torch.randperm(N - 140)[:300] + 70, torch.arange(N - 70, N)])
     o, lse = pick(o, lse, B, N, H, rows)
     ref, lref = emulate(qkv, B, N, H, rows)
     ex = exact(qkv, B, N, H, rows)
