@@ -7,14 +7,15 @@ TAG=${1:-r01}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-step() { local name=$1; shift; "$@"; local rc=$?; echo "[$name] exit $rc" | tee -a $OUT/steps.log; [ $rc -eq 0 ] || exit $rc; }
-step bench timeout -k 10 420 python bench.py --steps 10 --warmup 3 > $OUT/bench.log 2>&1
+# step <name> <log> <command...>: runs the command with its output in <log>, stops on failure
+step() { local name=$1 log=$2; shift 2; "$@" > "$log" 2>&1; local rc=$?; echo "[$name] exit $rc" | tee -a $OUT/steps.log; [ $rc -eq 0 ] || exit $rc; }
+step bench $OUT/bench.log timeout -k 10 420 python bench.py --steps 10 --warmup 3
 tail -1 $OUT/bench.log
-step infer timeout -k 10 300 python bench.py --infer --steps 10 --warmup 3 > $OUT/bench_infer.log 2>&1
+step infer $OUT/bench_infer.log timeout -k 10 300 python bench.py --infer --steps 10 --warmup 3
 tail -1 $OUT/bench_infer.log
-step infer_fp8 timeout -k 10 300 python bench.py --attn-fp8 --steps 10 --warmup 3 > $OUT/bench_infer_fp8.log 2>&1
+step infer_fp8 $OUT/bench_infer_fp8.log timeout -k 10 300 python bench.py --attn-fp8 --steps 10 --warmup 3
 tail -1 $OUT/bench_infer_fp8.log
-step prof timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
-  python bench.py --steps 3 --warmup 2 --no-mode-r --cpu-baseline off > $OUT/bench_prof.log 2>&1
-step prof_fp8 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_fp8 -o run --output-format csv -- \
-  python bench.py --attn-fp8 --steps 3 --warmup 2 > $OUT/bench_prof_fp8.log 2>&1
+step prof $OUT/bench_prof.log timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
+  python bench.py --steps 3 --warmup 2 --no-mode-r --cpu-baseline off
+step prof_fp8 $OUT/bench_prof_fp8.log timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_fp8 -o run --output-format csv -- \
+  python bench.py --attn-fp8 --steps 3 --warmup 2
