@@ -244,6 +244,8 @@ def main():
             cpu = {"value": None, "error": repr(e)[:300]}
 
     if rank == 0:
+        # N = 1 + 256k runs the CLS-split attention kernels (attention.hip bwd2_launch / fwd2)
+        cls_split = N >= 257 and (N - 1) % 256 == 0
         line = {
             "metric": "images/sec (%s) %s DenseCLIP @%dx%d" % (
                 "fwd, inference" if args.infer else "fwd+bwd",
@@ -266,13 +268,16 @@ def main():
                        "per_gpu_batch": B, "global_batch": B * world, "tokens_per_image": N,
                        "parallelism": f"dp{world}", "mode": args.mode,
                        "head_loss": "fused resize+CE/SILog" if FUSED_HEAD_LOSS else "materialised resize"},
-            "roofline": {"kernel": "attn_fp8_kernel (+ amax / pack)" if args.attn_fp8 else "attn_fwd_kernel<bf16>",
+            "roofline": {"kernel": ("attn_fp8_kernel (+ amax / pack%s)" % (" / row-0 pass" if cls_split else "")
+                                    if args.attn_fp8 else
+                                    "attn_fwd2_kernel<bf16> (+ row-0 pass)" if cls_split else "attn_fwd_kernel<bf16>"),
                          "bound": "mfma",
                          "achieved": round(achieved, 2) if achieved else None, "peak": peak_attn,
                          "unit": "TFLOP/s", "frac": round(achieved / peak_attn, 4) if achieved else None,
                          "traffic": traffic, "flops_per_launch": fl, "launches": n_att,
                          "ms_per_launch": round(mean_att, 4) if n_att else None},
-            "roofline_attn_bwd": {"kernel": "attn_bwd_dq2_kernel + attn_bwd_dkdv2_kernel (+ row-0 passes)",
+            "roofline_attn_bwd": {"kernel": "attn_bwd_dq2_kernel + attn_bwd_dkdv2_kernel (+ row-0 passes)" if cls_split
+                                  else "attn_bwd_dq_kernel + attn_bwd_dkdv_kernel",
                                   "bound": "mfma", "achieved": round(ach_b, 2) if ach_b else None,
                                   "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                                   "frac": round(ach_b / PEAK_BF16_TFLOPS, 4) if ach_b else None,

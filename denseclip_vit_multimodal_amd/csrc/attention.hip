@@ -2022,8 +2022,12 @@ bool bwd2_launch(const void* qkv, const void* o, const void* dout, const float* 
     attn_bwd_row0_dkdv_part<T><<<B * H * nsplit, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, ws0, N, H,
                                                               nsplit);
     attn_bwd_row0_dkdv_merge<T><<<B * H, 64, 0, st>>>(ws0, (T*)dqkv, N, H, nsplit, 1.0f / LOG2E);
-    attn_bwd_dkdv2_kernel<T, 4><<<B * H * ((N - 1) / 128), 256, 0, st>>>(
-        (const T*)qkv, (const T*)dout, lse, delta, nstat, nstat + (int64_t)B * H * N, (T*)dqkv, N, H, 1.0f / LOG2E);
+    if (dclip_option(DCLIP_OPT_ATTN_DKDV_WAVES) == 8)  // 256 keys per workgroup (one Q / dO slice per 256 keys)
+        attn_bwd_dkdv2_kernel<T, 8><<<B * H * ((N - 1) / 256), 512, 0, st>>>(
+            (const T*)qkv, (const T*)dout, lse, delta, nstat, nstat + (int64_t)B * H * N, (T*)dqkv, N, H, 1.0f / LOG2E);
+    else
+        attn_bwd_dkdv2_kernel<T, 4><<<B * H * ((N - 1) / 128), 256, 0, st>>>(
+            (const T*)qkv, (const T*)dout, lse, delta, nstat, nstat + (int64_t)B * H * N, (T*)dqkv, N, H, 1.0f / LOG2E);
     return true;
 }
 
