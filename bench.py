@@ -208,9 +208,15 @@ def main():
     achieved = fl / (mean_att * 1e-3) / 1e12 if n_att else None
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "attn_fwd_pmc.json")
-    if os.path.exists(pmc) and args.arch == "vitb16" and not args.infer:
+    probe_shape = args.arch == "vitb16" and B == 8 and (H, W) == (1024, 2048)  # the PMC runs' shape
+    if os.path.exists(pmc) and probe_shape and not args.attn_fp8:
         with open(pmc) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
+    traffic_b = None
+    pmc_b = os.path.join(ROOT, "profiles", "attn_bwd_pmc.json")
+    if os.path.exists(pmc_b) and probe_shape and not args.infer:
+        with open(pmc_b) as f:
+            traffic_b = json.load(f).get("hbm_bytes_per_launch")
     kernels = {k: {"launches": v[0], "ms_total": round(v[1], 3), "ms_mean": round(v[2], 4)} for k, v in summ.items()}
     # the attention backward (row-0 passes + dQ pass + dK/dV pass per launch): useful work = the
     # 5 N^2-matmuls of flash backward (2.5x the forward's), same HIP-event timing
@@ -281,6 +287,7 @@ def main():
                                   "bound": "mfma", "achieved": round(ach_b, 2) if ach_b else None,
                                   "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                                   "frac": round(ach_b / PEAK_BF16_TFLOPS, 4) if ach_b else None,
+                                  "traffic": traffic_b,
                                   "flops_per_launch": fl_b, "launches": n_ab,
                                   "ms_per_launch": round(mean_ab, 4) if n_ab else None},
             "model_mfma": {"flops_per_image": model_fl, "peak_tflops": PEAK_BF16_TFLOPS, "achieved_tflops": round(value / world * model_fl / 1e12, 1),
