@@ -48,6 +48,11 @@ _SIGS = {
     "dclip_bilinear_fwd": [_c_void_p, _i32, _c_void_p, _i32, _i64, _i32, _i32, _i32, _i32, _c_void_p],
     "dclip_bilinear_bwd": [_c_void_p, _i32, _c_void_p, _c_void_p, _i64, _i32, _i32, _i32, _i32, _c_void_p],
     "dclip_cast": [_c_void_p, _i32, _c_void_p, _i32, _i64, _f32, _c_void_p],
+    "dclip_bn_workspace": [_i64, _i32],
+    "dclip_bn_fwd": [_i32, _c_void_p, _i64, _i32, _c_void_p, _c_void_p, _f32, _f32, _c_void_p, _c_void_p, _c_void_p,
+                     _c_void_p, _c_void_p, _c_void_p, _c_void_p],
+    "dclip_bn_bwd": [_i32, _c_void_p, _c_void_p, _i64, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                     _c_void_p, _c_void_p, _c_void_p],
     "dclip_conv3x3": [_i32, _i32, _c_void_p, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _c_void_p, _i32, _c_void_p,
                       _i32, _i64, _i32, _i32, _i32, _c_void_p],
     "dclip_upsample_ce": [_i32, _c_void_p, _i32, _i32, _i32, _i32, _c_void_p, _i32, _i32, _i32, _i32, _c_void_p,
@@ -96,6 +101,7 @@ def load(path=None):
         lib.dclip_abi_version.restype = ctypes.c_int
         lib.dclip_abi_version.argtypes = []
         lib.dclip_attn_bwd_workspace.restype = ctypes.c_int64  # a size, not a status
+        lib.dclip_bn_workspace.restype = ctypes.c_int64
         lib.dclip_attn_fwd_fp8_workspace.restype = ctypes.c_int64
         # kernel-variant knobs for A/B runs: DCLIP_OPTIONS="id=value,..." (DCLIP_OPT_* ids of dclip.h)
         for kv in filter(None, os.environ.get("DCLIP_OPTIONS", "").split(",")):

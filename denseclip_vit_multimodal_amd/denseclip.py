@@ -240,6 +240,12 @@ class DenseCLIP(nn.Module):
         captured once into a HIP graph and REPLAYED every step (recomputed, not cached), which
         removes the per-kernel launch gaps; any trainable text parameter, or a parameter
         re-allocated since the capture, falls back to eager execution / a new capture."""
+        device = torch.device(device)
+        if device.type == "cuda" and device.index is None:
+            # "cuda" and "cuda:0" compare unequal: without this the token ids were re-uploaded on
+            # every call, freeing the tensor a captured graph reads (a replay then gathered
+            # through a recycled block: test_text_path_graph_replay_matches_eager faulted)
+            device = torch.device("cuda", torch.cuda.current_device())
         if getattr(self, "_texts_dev", None) is None or self._texts_dev.device != device:
             self._texts_dev = self.texts.to(device)
         texts = self._texts_dev
@@ -249,7 +255,8 @@ class DenseCLIP(nn.Module):
         frozen = not any(p.requires_grad for p in params)
         if not (self.graph_text and frozen and device.type == "cuda"):
             return self._text_forward(texts).expand(B, -1, -1)
-        key = (device, tuple(p.data_ptr() for p in params), torch.is_autocast_enabled())
+        # every device buffer the graph reads is in the key: a re-allocated one forces a new capture
+        key = (device, texts.data_ptr(), tuple(p.data_ptr() for p in params), torch.is_autocast_enabled())
         g = getattr(self, "_text_graph", None)
         if g is None or g[0] != key:
             side = torch.cuda.Stream(device=device)

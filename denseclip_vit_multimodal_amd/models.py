@@ -18,13 +18,23 @@ logger = logging.getLogger(__name__)
 
 
 class BatchNorm2d(nn.BatchNorm2d):
-    """nn.BatchNorm2d (same parameters, buffers and state-dict keys) whose GPU forward runs
+    """nn.BatchNorm2d (same parameters, buffers and state-dict keys).  Train mode on 16-bit
+    channels-last maps runs the HIP batch-norm kernels (ops.BatchNormFn); everything else runs
     torch's native kernels instead of MIOpen: MIOpen's batch-norm segfaults on the host for a
     bf16 channels-last (1, 128, 73, 146) map in train mode — the ViT-L/14 neck at 1024x2048 —
     while fp32, NCHW, other sizes and the native kernels are fine (tools/bn_probe.py,
     gpurun_out/bn_probe.log)."""
 
     def forward(self, x):
+        f32 = all(t is None or t.dtype == torch.float32
+                  for t in (self.weight, self.bias, self.running_mean, self.running_var))
+        if self.training and self.track_running_stats and self.momentum is not None and f32 and ops.bn_supported(x):
+            # batch statistics on the HIP kernels (torch's native channels-last kernels run at
+            # ~0.12 TB/s on the neck maps): dclip_bn_fwd / dclip_bn_bwd
+            if self.num_batches_tracked is not None:
+                self.num_batches_tracked.add_(1)
+            return ops.BatchNormFn.apply(x, self.weight, self.bias, self.running_mean, self.running_var,
+                                         self.momentum, self.eps)
         if x.is_cuda:
             with torch.backends.cudnn.flags(enabled=False):
                 return super().forward(x)

@@ -559,6 +559,54 @@ class ReadoutFn(torch.autograd.Function):
         return dx, dw, db, None
 
 
+def bn_supported(x):
+    """Train-mode BatchNorm on the HIP kernels: 16-bit channels-last maps, C / 8 a power of two
+    <= 256 (the neck's 128 / 256 channels, the heads' in // 4)."""
+    if not (x.is_cuda and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float16)):
+        return False
+    C = x.shape[1]
+    t = C // 8
+    return C % 8 == 0 and 1 <= t <= 256 and (t & (t - 1)) == 0 and x.numel() > 0 and \
+        x.is_contiguous(memory_format=torch.channels_last)
+
+
+class BatchNormFn(torch.autograd.Function):
+    """nn.BatchNorm2d in train mode (batch statistics; the running statistics updated in place
+    like torch's) on a channels-last map viewed as (B*H*W, C): dclip_bn_fwd / dclip_bn_bwd
+    (reference models.py:13-20 ConvModule norm, heads' FCNHead norm)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps):
+        B, C, H, W = x.shape
+        rows = B * H * W
+        ws = torch.empty(N.lib().dclip_bn_workspace(rows, C), dtype=torch.float32, device=x.device)
+        mean = torch.empty(C, dtype=torch.float32, device=x.device)
+        rstd = torch.empty_like(mean)
+        y = torch.empty_like(x, memory_format=torch.channels_last)
+        w = weight.detach() if weight is not None else None
+        b = bias.detach() if bias is not None else None
+        _check(w, b, running_mean, running_var, strided=(x,))
+        N.call("dclip_bn_fwd", _dt(x), _p(x), rows, C, _p(w), _p(b), float(eps), float(momentum),
+               _p(running_mean), _p(running_var), _p(ws), _p(mean), _p(rstd), _p(y), _stream())
+        ctx.save_for_backward(x, w, mean, rstd)
+        ctx.has_w = (weight is not None, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, mean, rstd = ctx.saved_tensors
+        B, C, H, W = x.shape
+        rows = B * H * W
+        dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last)
+        ws = torch.empty(N.lib().dclip_bn_workspace(rows, C), dtype=torch.float32, device=x.device)
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        dw = torch.empty(C, dtype=torch.float32, device=x.device) if ctx.has_w[0] else None
+        db = torch.empty(C, dtype=torch.float32, device=x.device) if ctx.has_w[1] else None
+        N.call("dclip_bn_bwd", _dt(x), _p(dy), _p(x), rows, C, _p(w), _p(mean), _p(rstd), _p(ws), _p(dx), _p(dw),
+               _p(db), _stream())
+        return dx, dw, db, None, None, None, None
+
+
 class UpsampleFn(torch.autograd.Function):
     """F.interpolate(mode='bilinear', align_corners=False) to (Ho, Wo), fp32 output
     (reference denseclip.py:847, 860, 899, 909)."""

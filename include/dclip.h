@@ -273,6 +273,21 @@ int dclip_cityscapes_prepare(const uint8_t* img, const uint8_t* ids, const uint1
  * scale keeps fp16 gradients out of the subnormal range (see dclip_gemm's alpha).     */
 int dclip_cast(const void* in, int in_dt, void* out, int out_dt, int64_t n, float scale, void* stream);
 
+/* Train-mode BatchNorm2d on a channels-last 16-bit map viewed as (rows = B*H*W, C), C / 8 a
+ * power of two <= 256 (replaces nn.BatchNorm2d in the neck's ConvModules, models.py:13-20, and
+ * the FCN heads; torch.nn.functional.batch_norm semantics: biased batch variance for the
+ * normalisation, unbiased for running_var, running = (1 - momentum) running + momentum batch).
+ * w, b, running_mean / running_var may be NULL.  ws: dclip_bn_workspace(rows, C) floats.
+ * Forward writes mean / rstd (f32, C) for the backward; the backward writes dx (dt) and, when
+ * non-null, dw / db (f32, C). */
+int64_t dclip_bn_workspace(int64_t rows, int C);
+int dclip_bn_fwd(int dt, const void* x, int64_t rows, int C, const float* w, const float* b, float eps,
+                 float momentum, float* running_mean, float* running_var, float* ws, float* mean,
+                 float* rstd, void* y, void* stream);
+int dclip_bn_bwd(int dt, const void* dy, const void* x, int64_t rows, int C, const float* w,
+                 const float* mean, const float* rstd, float* ws, void* dx, float* dw, float* db,
+                 void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -653,3 +653,50 @@ def test_upsample_silog_vs_reference(hw, HW, with_mask):
     # per-pixel gradient 2d/T - 2 lambda S/T^2 cancels where d ~ lambda S/T: both fp32
     # evaluations (torch's and ours) carry a few 1e-4 of relative error at 16.8M pixels
     assert rel_err(pred.grad, pr.grad) < 1e-3
+
+
+# ----------------------------------------------------------------------------- batch norm
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("B,C,H,W,shift", [(8, 128, 16, 32, 0.0), (2, 256, 5, 7, 3.0), (1, 64, 1, 3, 0.0),
+                                           (3, 8, 9, 13, -2.0)])
+def test_batchnorm_train_vs_torch(dt, B, C, H, W, shift):
+    """Train-mode BatchNorm2d on the HIP kernels (models.BatchNorm2d -> ops.BatchNormFn) vs
+    torch's fp32 F.batch_norm on the same 16-bit-rounded map: output, running statistics
+    (unbiased variance, momentum 0.1, num_batches_tracked), dx / dweight / dbias.  `shift`
+    offsets the map's mean (the shifted statistics must not cancel)."""
+    from denseclip_vit_multimodal_amd.models import BatchNorm2d
+    O = ops()
+    torch.manual_seed(0)
+    x = (torch.randn(B, C, H, W, device=DEV) * 2 + shift).to(dt).contiguous(memory_format=torch.channels_last)
+    bn = BatchNorm2d(C).to(DEV).train()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+        bn.running_var.uniform_(0.5, 2.0)
+    ref_rm, ref_rv = bn.running_mean.clone(), bn.running_var.clone()
+    assert O.bn_supported(x)
+    xg = x.detach().requires_grad_(True)
+    y = bn(xg)
+    assert y.dtype == dt and y.is_contiguous(memory_format=torch.channels_last)
+    xr = x.detach().float().requires_grad_(True)
+    wr = bn.weight.detach().clone().requires_grad_(True)
+    br = bn.bias.detach().clone().requires_grad_(True)
+    yr = F.batch_norm(xr, ref_rm, ref_rv, wr, br, training=True, momentum=0.1, eps=bn.eps)
+    tol = 8e-3 if dt == torch.bfloat16 else 1e-3  # the 16-bit output rounding
+    assert rel_err(y.float(), yr) < tol
+    assert rel_err(bn.running_mean, ref_rm) < 1e-4 and rel_err(bn.running_var, ref_rv) < 1e-4
+    assert int(bn.num_batches_tracked) == 1
+    g = torch.randn(B, C, H, W, device=DEV).to(dt).contiguous(memory_format=torch.channels_last)
+    y.backward(g)
+    yr.backward(g.float())
+    assert rel_err(xg.grad.float(), xr.grad) < 2 * tol
+    assert rel_err(bn.weight.grad, wr.grad) < 1e-4
+    assert rel_err(bn.bias.grad, br.grad) < 1e-5
+
+
+def test_batchnorm_eval_and_nchw_use_torch():
+    """Eval mode (running statistics) and NCHW / fp32 maps keep torch's kernels."""
+    O = ops()
+    x = torch.randn(2, 64, 4, 4, device=DEV).to(torch.bfloat16)
+    assert not O.bn_supported(x)  # NCHW
+    assert not O.bn_supported(x.float().contiguous(memory_format=torch.channels_last))
