@@ -494,6 +494,55 @@ extern "C" int dclip_bilinear_bwd(const void* dout, int dout_dt, float* din, flo
     return 0;
 }
 
+// sum = a + b (b's CLS rows, row % ntok == 0, read as 0) and lp = (TO)(sum * scale), 8 columns
+// per thread with 16-byte accesses; cols % 8 == 0.  sum may alias a.
+template <typename TB, typename TO>
+__global__ void add_readout_cast_kernel(const float* a, const TB* __restrict__ b, float* sum, TO* __restrict__ lp,
+                                        int64_t rows, int cols, int ntok, float scale) {
+    const int c8 = cols / 8;
+    const int64_t n8 = rows * c8;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t row = i / c8;
+        const int64_t off = i * 8;
+        f32x4 x0 = *(const f32x4*)(a + off), x1 = *(const f32x4*)(a + off + 4);
+        if (row % ntok != 0) {
+            if constexpr (sizeof(TB) == 4) {
+                const f32x4 y0 = *(const f32x4*)(b + off), y1 = *(const f32x4*)(b + off + 4);
+                x0 += y0;
+                x1 += y1;
+            } else {
+                typedef TB tb8 __attribute__((ext_vector_type(8)));
+                const tb8 y = *(const tb8*)(b + off);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) x0[e] += (float)y[e], x1[e] += (float)y[4 + e];
+            }
+        }
+        *(f32x4*)(sum + off) = x0;
+        *(f32x4*)(sum + off + 4) = x1;
+        typedef TO to8 __attribute__((ext_vector_type(8)));
+        to8 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (TO)(x0[e] * scale), o[4 + e] = (TO)(x1[e] * scale);
+        *(to8*)(lp + off) = o;
+    }
+}
+
+extern "C" int dclip_add_readout_cast(const float* a, const void* b, int b_dt, float* sum, void* lp, int lp_dt,
+                                      int64_t rows, int cols, int ntok, float scale, void* stream) {
+    DCLIP_HOST_CHECK(cols % 8 == 0 && ntok > 0, "dclip_add_readout_cast: cols must be a multiple of 8");
+    DCLIP_HOST_CHECK(lp_dt == DCLIP_BF16 || lp_dt == DCLIP_F16, "dclip_add_readout_cast: lp must be bf16/f16");
+    DCLIP_HOST_CHECK(((uintptr_t)a | (uintptr_t)b | (uintptr_t)sum | (uintptr_t)lp) % 16 == 0,
+                     "dclip_add_readout_cast: unaligned buffers");
+    if (rows == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    const unsigned g = grid_for(rows * (cols / 8), 8192);
+    DISPATCH_DT(b_dt, TB, DISPATCH_DT(lp_dt, TO,
+        if constexpr (sizeof(TO) == 2)
+            add_readout_cast_kernel<TB, TO><<<g, 256, 0, st>>>(a, (const TB*)b, sum, (TO*)lp, rows, cols, ntok, scale)));
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
+
 extern "C" int dclip_cast(const void* in, int in_dt, void* out, int out_dt, int64_t n, float scale, void* stream) {
     if (n == 0) return 0;
     hipStream_t st = (hipStream_t)stream;

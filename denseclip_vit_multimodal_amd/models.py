@@ -289,12 +289,15 @@ class CLIPVisionTransformer(nn.Module):
         for i, blk in enumerate(self.transformer.resblocks):
             if i > last:
                 break  # later blocks feed nothing the reference returns
+            if i in self.out_indices and i != self.layers - 1:
+                # read-out without ln_post: produced by the block itself, so its gradient is
+                # folded into the block's backward (ops.BlockFn, meta[5])
+                tok, fmap = ops.BlockFn.apply(tok, meta + ((gh, gw, x.dtype),), *blk.hip_params())
+                outs.append(fmap)
+                continue
             tok = ops.BlockFn.apply(tok, meta, *blk.hip_params())
-            if i in self.out_indices:
-                if i == self.layers - 1:
-                    outs.append(ops.ReadoutFn.apply(tok, self.ln_post.weight, self.ln_post.bias, rmeta))
-                else:
-                    outs.append(ops.ReadoutFn.apply(tok, None, None, rmeta))
+            if i in self.out_indices:  # the last layer: ln_post (models.py:576)
+                outs.append(ops.ReadoutFn.apply(tok, self.ln_post.weight, self.ln_post.bias, rmeta))
         return outs
 
 

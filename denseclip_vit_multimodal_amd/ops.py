@@ -432,11 +432,18 @@ class BlockFn(torch.autograd.Function):
         x = x + out_proj(attn(qkv(ln_1(x))))
         x = x + c_proj(quick_gelu(c_fc(ln_2(x))))
     LN -> GEMM(+bias) -> fused attention -> GEMM(+bias+residual) -> LN -> GEMM(+bias+QuickGELU)
-    -> GEMM(+bias+residual): 7 kernels, no elementwise passes."""
+    -> GEMM(+bias+residual): 7 kernels, no elementwise passes.
+
+    meta[5] (optional) = (gh, gw, map dtype): the block also returns the per-layer read-out map
+    of its output (models.py:577-597 without ln_post; the layout of ReadoutFn), so the backward
+    receives the map's gradient beside the residual one and folds it into the cast that feeds
+    its first GEMM (dclip_add_readout_cast) instead of autograd summing two fp32 token
+    gradients."""
 
     @staticmethod
     def forward(ctx, x, meta, ln1w, ln1b, w_in, b_in, w_out, b_out, ln2w, ln2b, w1, b1, w2, b2):
-        B, Ntok, H, cdt, fp8 = meta
+        B, Ntok, H, cdt, fp8 = meta[:5]
+        ro = meta[5] if len(meta) > 5 else None
         C = x.shape[1]
         scale = (C // H) ** -0.5
         xh1, mu1, rs1 = layernorm_fwd(x, ln1w.detach(), ln1b.detach(), cdt)
@@ -450,25 +457,50 @@ class BlockFn(torch.autograd.Function):
         ctx.save_for_backward(x, mu1, rs1, xh1, qkv, o, lse, xm, mu2, rs2, xh2, z, h,
                               ln1w, w_in, w_out, ln2w, w1, w2)
         ctx.meta = meta
-        return xo
+        if ro is None:
+            return xo
+        gh, gw, mdt = ro
+        ctx.set_materialize_grads(False)  # an unused map (or block output) brings None, not zeros
+        buf = xo.clone() if mdt == torch.float32 else cast(xo, mdt)
+        return xo, buf.as_strided((B, C, gh, gw), (Ntok * C, 1, gw * C, C), C)
 
     @staticmethod
-    def backward(ctx, dxo):
+    def backward(ctx, dxo, dmap=None):
         (x, mu1, rs1, xh1, qkv, o, lse, xm, mu2, rs2, xh2, z, h,
          ln1w, w_in, w_out, ln2w, w1, w2) = ctx.saved_tensors
-        B, Ntok, H, cdt, fp8 = ctx.meta
+        B, Ntok, H, cdt, fp8 = ctx.meta[:5]
         if fp8:
             raise RuntimeError("fp8 attention is forward-only (inference); train with attn_fp8=False")
         C = x.shape[1]
         scale = (C // H) ** -0.5
         need = ctx.needs_input_grad
-        dxo = dxo.contiguous()
         wg = any(need[2:])
+        dy = None
+        if dxo is None:
+            dxo = torch.zeros(B * Ntok, C, dtype=torch.float32, device=x.device)
+        dxo = dxo.contiguous()
+        if dmap is not None:  # the read-out map's gradient joins the block output's
+            gh, gw, _ = ctx.meta[5]
+            base = _readout_grad_buffer(dmap, B, Ntok, gh, gw, C)
+            if base is not None and cdt == torch.bfloat16:
+                # one pass: dxo + map gradient (CLS rows masked) in fp32, and its bf16 copy
+                tot = torch.empty_like(dxo)
+                dy = torch.empty(dxo.shape, dtype=cdt, device=dxo.device)
+                N.call("dclip_add_readout_cast", _p(dxo), _p(base), _dt(base), _p(tot), _p(dy), _dt(dy),
+                       B * Ntok, C, Ntok, 1.0, _stream())
+                dxo = tot
+            elif base is not None:
+                dr = base.float() if base.dtype != torch.float32 else base.clone()
+                dr.view(B, Ntok, C)[:, 0].zero_()
+                dxo = dxo + dr
+            else:
+                dxo = dxo + _readout_grad_dense(dmap, B, Ntok, gh, gw, C)
 
         # ---- MLP: xo = xm + h W2^T + b2,  h = qgelu(z),  z = xh2 W1^T + b1
         # (s1, s2: power-of-two gradient scales, 1.0 unless fp16 — see grad_scale)
         s1 = grad_scale(dxo, cdt)
-        dy = cast(dxo, cdt, s1)
+        if dy is None:
+            dy = cast(dxo, cdt, s1)
         dz = gemm(dy, WEIGHTS.get(w2, cdt, transposed=True), N.EPI_GELU_BWD, aux=z)
         dW2 = db2 = dW1 = db1 = None
         if wg:
@@ -510,6 +542,24 @@ class BlockFn(torch.autograd.Function):
                 g(7, dbo), g(8, dln2w), g(9, dln2b), g(10, dW1), g(11, db1), g(12, dW2), g(13, db2))
 
 
+def _readout_grad_buffer(dmap, B, Ntok, gh, gw, C):
+    """The read-out map's gradient as a (B*Ntok, C) token buffer whose CLS rows are NOT zeroed
+    (callers mask them), when it already has the token-buffer layout (Conv3x3Fn's input
+    gradient: zero copy); None otherwise."""
+    if dmap.stride() == (Ntok * C, 1, gw * C, C) and dmap.storage_offset() >= C and \
+            dmap.untyped_storage().nbytes() >= (dmap.storage_offset() - C + B * Ntok * C) * dmap.element_size():
+        STATS["readout_zero_copy"] = STATS.get("readout_zero_copy", 0) + 1
+        return dmap.as_strided((B * Ntok, C), (C, 1), dmap.storage_offset() - C)
+    return None
+
+
+def _readout_grad_dense(dmap, B, Ntok, gh, gw, C):
+    """The read-out map's gradient scattered into a fresh fp32 (B*Ntok, C) token gradient."""
+    dy = torch.zeros(B * Ntok, C, dtype=torch.float32, device=dmap.device)
+    dy.view(B, Ntok, C)[:, 1:].copy_(dmap.permute(0, 2, 3, 1).reshape(B, gh * gw, C))
+    return dy
+
+
 class ReadoutFn(torch.autograd.Function):
     """Per-layer dense read-out (reference models.py:568-582): optional ln_post (only for the
     last block, models.py:574-576), drop CLS, (B, N, C) -> (B, C, H, W).
@@ -540,16 +590,12 @@ class ReadoutFn(torch.autograd.Function):
         x, mean, rstd, ln_w = ctx.saved_tensors
         B, Ntok, gh, gw, _ = ctx.meta
         C = dmap.shape[1]
-        if dmap.stride() == (Ntok * C, 1, gw * C, C) and dmap.storage_offset() >= C and \
-                dmap.untyped_storage().nbytes() >= (dmap.storage_offset() - C + B * Ntok * C) * dmap.element_size():
-            # token-buffer layout (Conv3x3Fn's input gradient): take the buffer as it is
-            STATS["readout_zero_copy"] = STATS.get("readout_zero_copy", 0) + 1
-            base = dmap.as_strided((B * Ntok, C), (C, 1), dmap.storage_offset() - C)
+        base = _readout_grad_buffer(dmap, B, Ntok, gh, gw, C)
+        if base is not None:  # token-buffer layout (Conv3x3Fn's input gradient): take the buffer as it is
             dy = base.float() if base.dtype != torch.float32 else base.clone()
             dy.view(B, Ntok, C)[:, 0].zero_()
         else:
-            dy = torch.zeros(B * Ntok, C, dtype=torch.float32, device=dmap.device)
-            dy.view(B, Ntok, C)[:, 1:].copy_(dmap.permute(0, 2, 3, 1).reshape(B, gh * gw, C))
+            dy = _readout_grad_dense(dmap, B, Ntok, gh, gw, C)
         if not ctx.has_ln:
             return dy, None, None, None
         dx = torch.empty_like(dy)

@@ -272,6 +272,12 @@ int dclip_cityscapes_prepare(const uint8_t* img, const uint8_t* ids, const uint1
 /* Element-wise dtype conversion of n elements: out = (out_dt)(in * scale).  A power-of-two
  * scale keeps fp16 gradients out of the subnormal range (see dclip_gemm's alpha).     */
 int dclip_cast(const void* in, int in_dt, void* out, int out_dt, int64_t n, float scale, void* stream);
+/* Read-out gradient folded into a block's incoming gradient (replaces the autograd sum of the
+ * two uses of a block output, models.py:565 -> 577-597, plus the backward's cast): sum = a + b
+ * with b's CLS rows (row % ntok == 0) read as 0, lp = (lp_dt)(sum * scale).  a, sum: f32
+ * (rows, cols); b: (rows, cols) token buffer, f32/bf16/f16; cols % 8 == 0; sum may alias a. */
+int dclip_add_readout_cast(const float* a, const void* b, int b_dt, float* sum, void* lp, int lp_dt,
+                           int64_t rows, int cols, int ntok, float scale, void* stream);
 
 /* Train-mode BatchNorm2d on a channels-last 16-bit map viewed as (rows = B*H*W, C), C / 8 a
  * power of two <= 256 (replaces nn.BatchNorm2d in the neck's ConvModules, models.py:13-20, and

@@ -572,6 +572,62 @@ def test_conv3x3_dgrad_token_layout_and_readout():
     assert rel_err(tok.grad, tr.grad) < 1.5e-2
 
 
+@pytest.mark.parametrize("bdt", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("rows,cols,ntok", [(2 * 61, 128, 61), (3 * 5, 768, 5), (1, 8, 1)])
+def test_add_readout_cast(bdt, rows, cols, ntok):
+    """dclip_add_readout_cast: sum = a + b with b's CLS rows (row % ntok == 0) ignored, and the
+    bf16 copy of the sum; in place (sum aliasing a) too."""
+    from denseclip_vit_multimodal_amd import _native as N
+    O = ops()
+    a = torch.randn(rows, cols, device=DEV)
+    b = torch.randn(rows, cols, device=DEV).to(bdt)
+    keep = (torch.arange(rows, device=DEV) % ntok != 0)[:, None]
+    ref = torch.where(keep, a + b.float(), a)
+    for inplace in (False, True):
+        x = a.clone()
+        out = x if inplace else torch.empty_like(a)
+        lp = torch.empty(rows, cols, dtype=torch.bfloat16, device=DEV)
+        N.call("dclip_add_readout_cast", O._p(x), O._p(b), O._dt(b), O._p(out), O._p(lp), O._dt(lp), rows, cols,
+               ntok, 1.0, O._stream())
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)  # one fp32 add per element, as torch does it
+        assert torch.equal(lp, ref.to(torch.bfloat16))
+
+
+def test_block_readout_fused_backward_matches_separate():
+    """A block that returns its own read-out map (BlockFn meta[5]) gives the same gradients as
+    BlockFn followed by ReadoutFn (the autograd sum of the two token gradients)."""
+    O = ops()
+    from denseclip_vit_multimodal_amd.models import CLIPVisionTransformer
+    torch.manual_seed(0)
+    B, H, W, C, heads = 2, 4, 6, 128, 2
+    Nt = 1 + H * W
+    bb = CLIPVisionTransformer(input_resolution=32, patch_size=16, width=C, layers=1, heads=heads,
+                               out_indices=[0]).to(DEV)
+    blk = bb.transformer.resblocks[0]
+    x = torch.randn(B * Nt, C, device=DEV)
+    w = torch.randn(64, C, 3, 3, device=DEV) * 0.05
+    g = torch.randn(B, 64, H, W, device=DEV)
+    gx = torch.randn(B * Nt, C, device=DEV) * 1e-2
+    meta = (B, Nt, heads, torch.bfloat16, False)
+    grads = []
+    for fused in (False, True):
+        xi = x.clone().requires_grad_(True)
+        if fused:
+            tok, m = O.BlockFn.apply(xi, meta + ((H, W, torch.bfloat16),), *blk.hip_params())
+        else:
+            tok = O.BlockFn.apply(xi, meta, *blk.hip_params())
+            m = O.ReadoutFn.apply(tok, None, None, (B, Nt, H, W, torch.bfloat16))
+        y = O.Conv3x3Fn.apply(m, w, torch.bfloat16)
+        ((y.float() * g).sum() + (tok * gx).sum()).backward()
+        grads.append([xi.grad] + [p.grad.clone() for p in blk.hip_params() if p.grad is not None])
+        for p in blk.parameters():
+            p.grad = None
+    assert len(grads[0]) == len(grads[1])
+    for a, b in zip(*grads):
+        assert rel_err(b, a) < 1e-5, rel_err(b, a)
+
+
 @pytest.mark.parametrize("B,Cin,H,W,Cout", [(2, 1536, 8, 16, 256), (1, 64, 3, 5, 64)])
 def test_conv1x1_fn_vs_torch(B, Cin, H, W, Cout):
     O = ops()
