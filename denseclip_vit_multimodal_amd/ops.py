@@ -175,7 +175,7 @@ def _tn_plan(M, N, K):
     return sp.value, kp.value
 
 
-def weight_grad(dy, x, want_bias=True, alpha=1.0):
+def weight_grad(dy, x, want_bias=True, alpha=1.0, db=None):
     """dW = alpha dy^T x (N x K, fp32) and db = alpha colsum(dy) for dy (M, N), x (M, K)
     (compute dtype).
 
@@ -186,7 +186,10 @@ def weight_grad(dy, x, want_bias=True, alpha=1.0):
     M, Nn = dy.shape
     K = x.shape[1]
     splits, k_pad = _tn_plan(Nn, K, M)
-    db = torch.zeros(Nn, dtype=torch.float32, device=dy.device) if want_bias else None
+    if want_bias and db is None:  # db: a caller-zeroed (Nn,) f32 buffer, or allocated here
+        db = torch.zeros(Nn, dtype=torch.float32, device=dy.device)
+    elif not want_bias:
+        db = None
     dW = torch.empty(Nn, K, dtype=torch.float32, device=dy.device)
     ws = torch.empty(splits, Nn, K, dtype=torch.float32, device=dy.device)
     e0 = _tic()
@@ -475,6 +478,12 @@ class BlockFn(torch.autograd.Function):
         scale = (C // H) ** -0.5
         need = ctx.needs_input_grad
         wg = any(need[2:])
+        # every zero-initialised small gradient of the block from ONE zeroed arena (one fill
+        # launch instead of eight): LN weights / biases (4C), biases of c_proj (C), c_fc (4C),
+        # out_proj (C), in_proj (3C)
+        arena = torch.zeros(13 * C, dtype=torch.float32, device=x.device)
+        dln1w, dln1b, dln2w, dln2b = (arena[i * C:(i + 1) * C] for i in range(4))
+        zb2, zb1, zbo, zbi = arena[4 * C:5 * C], arena[5 * C:9 * C], arena[9 * C:10 * C], arena[10 * C:13 * C]
         dy = None
         if dxo is None:
             dxo = torch.zeros(B * Ntok, C, dtype=torch.float32, device=x.device)
@@ -504,13 +513,11 @@ class BlockFn(torch.autograd.Function):
         dz = gemm(dy, WEIGHTS.get(w2, cdt, transposed=True), N.EPI_GELU_BWD, aux=z)
         dW2 = db2 = dW1 = db1 = None
         if wg:
-            dW2, db2 = weight_grad(dy, h, alpha=1.0 / s1)
+            dW2, db2 = weight_grad(dy, h, alpha=1.0 / s1, db=zb2)
         dxh2 = gemm(dz, WEIGHTS.get(w1, cdt, transposed=True), out_dtype=torch.float32, alpha=1.0 / s1)
         if wg:
-            dW1, db1 = weight_grad(dz, xh2, alpha=1.0 / s1)
+            dW1, db1 = weight_grad(dz, xh2, alpha=1.0 / s1, db=zb1)
         del dz
-        dln2w = torch.zeros(C, dtype=torch.float32, device=x.device)
-        dln2b = torch.zeros(C, dtype=torch.float32, device=x.device)
         dxm = torch.empty_like(dxo)
         if cdt == torch.bfloat16:  # no gradient scaling: the attention branch's operand comes out of the LN pass
             dyo = torch.empty(dxo.shape, dtype=cdt, device=dxo.device)
@@ -526,16 +533,14 @@ class BlockFn(torch.autograd.Function):
         do = gemm(dyo, WEIGHTS.get(w_out, cdt, transposed=True))
         dWo = dbo = dWi = dbi = None
         if wg:
-            dWo, dbo = weight_grad(dyo, o, alpha=1.0 / s2)
+            dWo, dbo = weight_grad(dyo, o, alpha=1.0 / s2, db=zbo)
         del dyo
         dqkv = attn_bwd(qkv, o, do, lse, B, Ntok, H, scale)  # linear in dO: carries s2
         del do
         dxh1 = gemm(dqkv, WEIGHTS.get(w_in, cdt, transposed=True), out_dtype=torch.float32, alpha=1.0 / s2)
         if wg:
-            dWi, dbi = weight_grad(dqkv, xh1, alpha=1.0 / s2)
+            dWi, dbi = weight_grad(dqkv, xh1, alpha=1.0 / s2, db=zbi)
         del dqkv
-        dln1w = torch.zeros(C, dtype=torch.float32, device=x.device)
-        dln1b = torch.zeros(C, dtype=torch.float32, device=x.device)
         layernorm_bwd(dxh1, x, ln1w.detach(), mu1, rs1, dxm, 1, dln1w, dln1b)
         g = lambda i, t: t if need[i] else None  # noqa: E731
         return (dxm if need[0] else None, None, g(2, dln1w), g(3, dln1b), g(4, dWi), g(5, dbi), g(6, dWo),
