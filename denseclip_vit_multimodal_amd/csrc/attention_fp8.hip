@@ -198,9 +198,9 @@ __global__ void __launch_bounds__(256) fp8_pack_kernel(const T* __restrict__ qkv
 }
 
 // ---------------------------------------------------------------------------- 3. attention
-// grid (ceil(N / 256), H, B), 512 threads (8 waves x 32 queries)
-template <typename T>
-__global__ void __launch_bounds__(512) attn_fp8_kernel(const uint8_t* __restrict__ q8, const uint8_t* __restrict__ k8,
+// grid (ceil(N / (32 NW)), H, B), 64 NW threads (NW waves x 32 queries)
+template <typename T, int NW>
+__global__ void __launch_bounds__(64 * NW) attn_fp8_kernel(const uint8_t* __restrict__ q8, const uint8_t* __restrict__ k8,
                                                        const uint8_t* __restrict__ vt8, const int* __restrict__ amax,
                                                        T* __restrict__ o, float* __restrict__ lse, int N, int H,
                                                        int Npad, int q0) {
@@ -208,7 +208,7 @@ __global__ void __launch_bounds__(512) attn_fp8_kernel(const uint8_t* __restrict
     const int h = blockIdx.y, b = blockIdx.z;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int r = lane & 31, half = lane >> 5;
-    const int q = q0 + blockIdx.x * 256 + wave * 32 + r;  // this lane's query (column of S^T)
+    const int q = q0 + blockIdx.x * (32 * NW) + wave * 32 + r;  // this lane's query (column of S^T)
     const int64_t hb = (int64_t)b * H + h;
     const float* am = (const float*)amax + b * 3 * H;
     const float dq = am[h] > 0.f ? am[h] / FP8_MAX : 1.f;
@@ -220,18 +220,24 @@ __global__ void __launch_bounds__(512) attn_fp8_kernel(const uint8_t* __restrict
     const uint8_t* qrow = q8 + (hb * Npad + min(q, Npad - 1)) * 64 + 32 * half;
     const i32x8 qf = *(const i32x8*)qrow;
 
-    // cooperative tile loads: threads 0-255 the K tile (4 KB contiguous), 256-511 the V^T tile
-    const uint8_t* ksrc = k8 + hb * Npad * 64 + tid * 16;
-    const int vd = (tid - 256) >> 2, vpart = (tid & 3) * 16;
-    const uint8_t* vsrc = vt8 + (hb * 64 + (vd & 63)) * Npad + vpart;
+    // cooperative tile loads of a unit's K tile (4 KB contiguous) and V^T tile (64 rows x 64 B):
+    // NW = 8: threads 0-255 K, 256-511 V^T, 16 B each; NW = 4: every thread 16 B of both
+    static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+    const int t256 = tid & 255;
+    const uint8_t* ksrc = k8 + hb * Npad * 64 + t256 * 16;
+    const int vd = t256 >> 2, vpart = (tid & 3) * 16;
+    const uint8_t* vsrc = vt8 + (hb * 64 + vd) * Npad + vpart;
     const int nunit = Npad / 64;
-    auto load_unit = [&](int u) -> i32x4 {
-        if (tid < 256) return *(const i32x4*)(ksrc + (int64_t)u * 4096);
-        return *(const i32x4*)(vsrc + u * 64);
+    struct Pre { i32x4 k, v; };
+    auto load_unit = [&](int u) -> Pre {
+        Pre p;
+        if (NW == 4 || tid < 256) p.k = *(const i32x4*)(ksrc + (int64_t)u * 4096);
+        if (NW == 4 || tid >= 256) p.v = *(const i32x4*)(vsrc + u * 64);
+        return p;
     };
-    auto store_unit = [&](int buf, i32x4 v) {
-        if (tid < 256) *(i32x4*)(&sm[buf][0][tid * 16]) = v;
-        else *(i32x4*)(&sm[buf][1][vd * 64 + vpart]) = v;
+    auto store_unit = [&](int buf, const Pre& p) {
+        if (NW == 4 || tid < 256) *(i32x4*)(&sm[buf][0][t256 * 16]) = p.k;
+        if (NW == 4 || tid >= 256) *(i32x4*)(&sm[buf][1][vd * 64 + vpart]) = p.v;
     };
 
     f32x16 o0, o1;
@@ -239,7 +245,7 @@ __global__ void __launch_bounds__(512) attn_fp8_kernel(const uint8_t* __restrict
     for (int i = 0; i < 16; ++i) o0[i] = 0.f, o1[i] = 0.f;
     float m = -INFINITY, l = 0.f;
 
-    i32x4 pre = load_unit(0);
+    Pre pre = load_unit(0);
     store_unit(0, pre);
     if (nunit > 1) pre = load_unit(1);
     __syncthreads();
@@ -363,7 +369,9 @@ extern "C" int dclip_attn_fwd_fp8(int dt, const void* qkv, void* o, float* lse, 
     // B*H*32 workgroups fill whole rounds of 2 workgroups per CU)
     const bool cls = N >= 257 && (N - 1) % 256 == 0;
     const int q0 = cls ? 1 : 0;
-    const dim3 ga((N + 63) / 64, B), gp(npad / 64, H, B), gf((N - q0 + 255) / 256, H, B);
+    // 4-wave workgroups (128 queries; DCLIP_OPT_ATTN_FWD_WAVES 4) or 8-wave (256 queries)
+    const int fnw = dclip_option(DCLIP_OPT_ATTN_FWD_WAVES) == 4 ? 4 : 8;
+    const dim3 ga((N + 63) / 64, B), gp(npad / 64, H, B), gf((N - q0 + 32 * fnw - 1) / (32 * fnw), H, B);
     if (cls) attn_row0_fwd(dt, qkv, o, lse, B, N, H, st);
     const int ncol8 = 3 * H * 64 / 8;
     const bool amax2 = 2 * ncol8 <= 1024 && (2 * ncol8) % 64 == 0;
@@ -371,12 +379,14 @@ extern "C" int dclip_attn_fwd_fp8(int dt, const void* qkv, void* o, float* lse, 
         if (amax2) fp8_amax2_kernel<bf16><<<ga, 2 * ncol8, 0, st>>>((const bf16*)qkv, amax, N, H);
         else fp8_amax_kernel<bf16><<<ga, 256, 0, st>>>((const bf16*)qkv, amax, N, H);
         fp8_pack_kernel<bf16><<<gp, 256, 0, st>>>((const bf16*)qkv, amax, q8, k8, vt8, N, H, npad);
-        attn_fp8_kernel<bf16><<<gf, 512, 0, st>>>(q8, k8, vt8, amax, (bf16*)o, lse, N, H, npad, q0);
+        if (fnw == 4) attn_fp8_kernel<bf16, 4><<<gf, 256, 0, st>>>(q8, k8, vt8, amax, (bf16*)o, lse, N, H, npad, q0);
+        else attn_fp8_kernel<bf16, 8><<<gf, 512, 0, st>>>(q8, k8, vt8, amax, (bf16*)o, lse, N, H, npad, q0);
     } else {
         if (amax2) fp8_amax2_kernel<f16><<<ga, 2 * ncol8, 0, st>>>((const f16*)qkv, amax, N, H);
         else fp8_amax_kernel<f16><<<ga, 256, 0, st>>>((const f16*)qkv, amax, N, H);
         fp8_pack_kernel<f16><<<gp, 256, 0, st>>>((const f16*)qkv, amax, q8, k8, vt8, N, H, npad);
-        attn_fp8_kernel<f16><<<gf, 512, 0, st>>>(q8, k8, vt8, amax, (f16*)o, lse, N, H, npad, q0);
+        if (fnw == 4) attn_fp8_kernel<f16, 4><<<gf, 256, 0, st>>>(q8, k8, vt8, amax, (f16*)o, lse, N, H, npad, q0);
+        else attn_fp8_kernel<f16, 8><<<gf, 512, 0, st>>>(q8, k8, vt8, amax, (f16*)o, lse, N, H, npad, q0);
     }
     DCLIP_LAUNCH_CHECK();
     return 0;
