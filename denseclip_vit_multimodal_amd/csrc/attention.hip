@@ -2017,8 +2017,12 @@ bool bwd2_launch(const void* qkv, const void* o, const void* dout, const float* 
                                                             nsplit);
     attn_bwd_row0_dq_merge<T><<<B * H, 64, 0, st>>>((const T*)o, (const T*)dout, ws0, delta, (T*)dqkv, N, H, nsplit,
                                                     scale);
-    attn_bwd_dq2_kernel<T, 8><<<B * H * ((N - 1) / 256), 512, 0, st>>>((const T*)qkv, (const T*)o, (const T*)dout, lse,
-                                                                      delta, nstat, (T*)dqkv, N, H, scale);
+    if (dclip_option(DCLIP_OPT_ATTN_DQ_WAVES) == 4)  // 128 queries per workgroup, two workgroups per CU
+        attn_bwd_dq2_kernel<T, 4><<<B * H * ((N - 1) / 128), 256, 0, st>>>(
+            (const T*)qkv, (const T*)o, (const T*)dout, lse, delta, nstat, (T*)dqkv, N, H, scale);
+    else
+        attn_bwd_dq2_kernel<T, 8><<<B * H * ((N - 1) / 256), 512, 0, st>>>(
+            (const T*)qkv, (const T*)o, (const T*)dout, lse, delta, nstat, (T*)dqkv, N, H, scale);
     attn_bwd_row0_dkdv_part<T><<<B * H * nsplit, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, ws0, N, H,
                                                               nsplit);
     attn_bwd_row0_dkdv_merge<T><<<B * H, 64, 0, st>>>(ws0, (T*)dqkv, N, H, nsplit, 1.0f / LOG2E);
