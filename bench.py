@@ -60,9 +60,16 @@ def parse():
     ap.add_argument("--infer", action="store_true",
                     help="inference forward only (eval mode, seg + depth at full resolution, no grad)")
     ap.add_argument("--attn-fp8", action="store_true",
-                    help="attention on the e4m3 MFMA kernel (BASELINE configs[4]; inference only, implies --infer)")
+                    help="attention forward on the e4m3 MFMA kernel (BASELINE configs[4]); training runs the 16-bit "
+                         "flash backward on its (o, lse)")
     ap.add_argument("--unfused-head-loss", action="store_true",
                     help="materialise the resized logits/depth and use F.cross_entropy + SILogLoss")
+    ap.add_argument("--dtype", choices=["bf16", "fp16"], default="bf16",
+                    help="image / compute dtype of the ViT and neck operands (fp32 accumulation either way)")
+    ap.add_argument("--ddp", action="store_true",
+                    help="process group (RCCL) + DDP even at world size 1 (torchrun --nproc-per-node 1)")
+    ap.add_argument("--grad-dtype", choices=["fp32", "bf16"], default="fp32",
+                    help="dtype of the DDP gradient all-reduce buckets (bf16: DDP's compression hook)")
     return ap.parse_args()
 
 
@@ -109,22 +116,23 @@ def run_steps(model, opt, batch, steps, silog):
     return loss
 
 
-def timed(model, opt, batch, steps, warmup, silog, world):
+def timed(model, opt, batch, steps, warmup, silog, world, dist_on=None):
     from denseclip_vit_multimodal_amd import ops
+    dist_on = world > 1 if dist_on is None else dist_on
     run_steps(model, opt, batch, warmup, silog)
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     ops.TIMING = {}
     t0 = time.perf_counter()
     loss = run_steps(model, opt, batch, steps, silog)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     dt = time.perf_counter() - t0
     summary = ops.timing_summary()
     ops.TIMING = None
-    if world > 1:
+    if dist_on:
         t = torch.tensor([dt], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t)
@@ -148,8 +156,6 @@ def cpu_baseline(H, W, threads):
     g = torch.Generator().manual_seed(1235)
     seg = torch.randint(0, 19, (1, H, W), generator=g)
     t0 = time.perf_counter()
-    with torch.no_grad():
-        pass
     out = O.denseclip_forward(x, p, class_tokens(), CITYSCAPES_CFG, training=True)
     loss = F.cross_entropy(out["seg"], seg, ignore_index=255)
     loss.backward()
@@ -163,15 +169,15 @@ def cpu_baseline(H, W, threads):
 def main():
     global FUSED_HEAD_LOSS
     args = parse()
-    args.infer = args.infer or args.attn_fp8
     FUSED_HEAD_LOSS = not args.unfused_head_loss
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    dist_on = world > 1 or args.ddp
+    if dist_on:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group("nccl")  # RCCL on ROCm (reference utils.py:106)
     dev = torch.device("cuda", local)
     torch.manual_seed(0)
     from denseclip_vit_multimodal_amd.losses import SILogLoss
@@ -179,28 +185,29 @@ def main():
 
     from denseclip_vit_multimodal_amd.train import synth_batch, wrap_ddp, make_optimizer
     B, H, W = args.batch, args.height, args.width
-    batch = synth_batch(B, H, W, dev, rank)
+    img_dtype = torch.float16 if args.dtype == "fp16" else torch.bfloat16
+    batch = synth_batch(B, H, W, dev, rank, image_dtype=img_dtype)
 
     def setup(mode):
         model = make_model(dev, mode, args.arch)
+        model.backbone.attn_fp8 = args.attn_fp8
         if args.infer:  # replicas: no gradients, no collective
             model.eval()
-            model.backbone.attn_fp8 = args.attn_fp8
             return model, None
         model.train()
-        if world > 1:
-            model = wrap_ddp(model, dev)
+        if dist_on:
+            model = wrap_ddp(model, dev, torch.bfloat16 if args.grad_dtype == "bf16" else None)
         opt = make_optimizer([p for p in model.parameters() if p.requires_grad])
         return model, opt
 
     model, opt = setup(args.mode)
-    dt, summ, loss = timed(model, opt, batch, args.steps, args.warmup, silog, world)
+    dt, summ, loss = timed(model, opt, batch, args.steps, args.warmup, silog, world, dist_on)
     value = world * B * args.steps / dt
     bb = ARCHS[args.arch] or dict(patch_size=16, heads=12)
     N = (H // bb["patch_size"]) * (W // bb["patch_size"]) + 1
     heads = bb["heads"]
 
-    # roofline of the dominant kernel: the fused attention forward (one kernel per launch)
+    # attention forward roofline (one dclip_attn_fwd launch per layer)
     akey = "attn_fwd_fp8" if args.attn_fp8 else "attn_fwd"
     peak_attn = PEAK_FP8_TFLOPS if args.attn_fp8 else PEAK_BF16_TFLOPS
     n_att, tot_att, mean_att = summ.get(akey, (0, 0.0, float("nan")))
@@ -236,7 +243,7 @@ def main():
         del model, opt
         torch.cuda.empty_cache()
         model, opt = setup("R")
-        dtr, _, _ = timed(model, opt, batch, max(3, args.steps // 2), 2, silog, world)
+        dtr, _, _ = timed(model, opt, batch, max(3, args.steps // 2), 2, silog, world, dist_on)
         mode_r = {"value": round(world * B * max(3, args.steps // 2) / dtr, 4), "unit": "images/sec",
                   "ms_per_step": round(dtr / max(3, args.steps // 2) * 1e3, 2),
                   "what": "reference regime: backbone + text encoder frozen (train_denseclip.py:1040-1044)"}
@@ -252,6 +259,23 @@ def main():
     if rank == 0:
         # N = 1 + 256k runs the CLS-split attention kernels (attention.hip bwd2_launch / fwd2)
         cls_split = N >= 257 and (N - 1) % 256 == 0
+        rf_fwd = {"kernel": ("attn_fp8_kernel (+ amax / pack%s)" % (" / row-0 pass" if cls_split else "")
+                             if args.attn_fp8 else
+                             "attn_fwd2_kernel (+ row-0 pass)" if cls_split else "attn_fwd_kernel"),
+                  "bound": "mfma",
+                  "achieved": round(achieved, 2) if achieved else None, "peak": peak_attn,
+                  "unit": "TFLOP/s", "frac": round(achieved / peak_attn, 4) if achieved else None,
+                  "traffic": traffic, "flops_per_launch": fl, "launches": n_att,
+                  "ms_per_launch": round(mean_att, 4) if n_att else None}
+        # the dominant op of a train step is the attention backward (5 N^2-matmuls
+        # per launch, 2.5x the forward's): it is the headline roofline whenever it ran
+        rf_bwd = None
+        if n_ab:
+            rf_bwd = {"kernel": "attn_bwd_dq2_kernel + attn_bwd_dkdv2_kernel (+ row-0 passes)" if cls_split
+                      else "attn_bwd_dq_kernel + attn_bwd_dkdv_kernel",
+                      "bound": "mfma", "achieved": round(ach_b, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                      "frac": round(ach_b / PEAK_BF16_TFLOPS, 4), "traffic": traffic_b,
+                      "flops_per_launch": fl_b, "launches": n_ab, "ms_per_launch": round(mean_ab, 4)}
         line = {
             "metric": "images/sec (%s) %s DenseCLIP @%dx%d" % (
                 "fwd, inference" if args.infer else "fwd+bwd",
@@ -265,31 +289,18 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16 (attention e4m3)" if args.attn_fp8 else "bf16",
+            "dtype": args.dtype + (" (attention e4m3)" if args.attn_fp8 else ""),
             "data": "synthetic (randn images, random labels/depth; random-init weights)",
             "config": {"workload": "DenseCLIP %s seg+depth %s, %dx%d" % (
                            {"vitb16": "ViT-B/16", "vitl14": "ViT-L/14"}[args.arch],
-                           "inference forward" + (" (fp8 attention)" if args.attn_fp8 else "") if args.infer
-                           else "train step (mode %s)" % args.mode, H, W),
+                           ("inference forward" if args.infer else "train step (mode %s)" % args.mode)
+                           + (" (fp8 attention forward)" if args.attn_fp8 else ""), H, W),
                        "per_gpu_batch": B, "global_batch": B * world, "tokens_per_image": N,
-                       "parallelism": f"dp{world}", "mode": args.mode,
+                       "parallelism": f"dp{world}", "mode": args.mode, "ddp": dist_on,
+                       "grad_allreduce_dtype": args.grad_dtype if dist_on else None,
                        "head_loss": "fused resize+CE/SILog" if FUSED_HEAD_LOSS else "materialised resize"},
-            "roofline": {"kernel": ("attn_fp8_kernel (+ amax / pack%s)" % (" / row-0 pass" if cls_split else "")
-                                    if args.attn_fp8 else
-                                    "attn_fwd2_kernel<bf16> (+ row-0 pass)" if cls_split else "attn_fwd_kernel<bf16>"),
-                         "bound": "mfma",
-                         "achieved": round(achieved, 2) if achieved else None, "peak": peak_attn,
-                         "unit": "TFLOP/s", "frac": round(achieved / peak_attn, 4) if achieved else None,
-                         "traffic": traffic, "flops_per_launch": fl, "launches": n_att,
-                         "ms_per_launch": round(mean_att, 4) if n_att else None},
-            "roofline_attn_bwd": {"kernel": "attn_bwd_dq2_kernel + attn_bwd_dkdv2_kernel (+ row-0 passes)" if cls_split
-                                  else "attn_bwd_dq_kernel + attn_bwd_dkdv_kernel",
-                                  "bound": "mfma", "achieved": round(ach_b, 2) if ach_b else None,
-                                  "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                                  "frac": round(ach_b / PEAK_BF16_TFLOPS, 4) if ach_b else None,
-                                  "traffic": traffic_b,
-                                  "flops_per_launch": fl_b, "launches": n_ab,
-                                  "ms_per_launch": round(mean_ab, 4) if n_ab else None},
+            "roofline": rf_bwd if rf_bwd is not None else rf_fwd,
+            "roofline_attn_fwd": rf_fwd,
             "model_mfma": {"flops_per_image": model_fl, "peak_tflops": PEAK_BF16_TFLOPS, "achieved_tflops": round(value / world * model_fl / 1e12, 1),
                            "frac": round(value / world * model_fl / 1e12 / PEAK_BF16_TFLOPS, 4)} if model_fl else None,
             "kernels": kernels,
@@ -298,7 +309,7 @@ def main():
             "loss": round(loss, 4),
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

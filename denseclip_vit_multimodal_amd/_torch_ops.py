@@ -1,0 +1,170 @@
+"""torch.ops.dclip.*: the TORCH_LIBRARY custom ops of libdclip_torch.so (csrc/torch_ops.cpp, an
+adapter over the C ABI of include/dclip.h) and their fake (meta) implementations, so the ops
+trace under torch.compile / torch.export / FakeTensorMode and pass torch.library.opcheck.
+
+There is no CPU kernel: a CPU tensor reaching an op raises (NotImplementedError from the
+dispatcher for the CPU key), and a missing library raises at import.
+"""
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DCLIP_TORCH_LIB", os.path.join(_HERE, "libdclip_torch.so"))
+
+_loaded = False
+
+
+def load():
+    """Load libdclip_torch.so into the torch dispatcher once (it links libdclip.so)."""
+    global _loaded
+    if _loaded:
+        return torch.ops.dclip
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libdclip_torch.so not found at {LIB_PATH}: build it with "
+                           "`make -C denseclip_vit_multimodal_amd/csrc` (the HIP path has no CPU fallback)")
+    from . import _native
+    _native.load()  # same libdclip.so instance (DCLIP_OPTIONS are applied there)
+    torch.ops.load_library(LIB_PATH)
+    _register_fakes()
+    _loaded = True
+    return torch.ops.dclip
+
+
+def _e(*shape, like, dtype=None):
+    return like.new_empty(shape, dtype=dtype if dtype is not None else like.dtype)
+
+
+def _register_fakes():
+    reg = torch.library.register_fake
+    f32 = torch.float32
+
+    @reg("dclip::layernorm_fwd")
+    def _(x, w, b, out_dtype, eps):
+        r, c = x.shape
+        return _e(r, c, like=x, dtype=out_dtype), _e(r, like=x, dtype=f32), _e(r, like=x, dtype=f32)
+
+    @reg("dclip::layernorm_bwd")
+    def _(dy, x, w, mean, rstd, res, dw, db):
+        return _e(*x.shape, like=x, dtype=f32)
+
+    @reg("dclip::layernorm_bwd_lp")
+    def _(dy, x, w, mean, rstd, res, dw, db, lp_dtype):
+        return _e(*x.shape, like=x, dtype=f32), _e(*x.shape, like=x, dtype=lp_dtype)
+
+    @reg("dclip::gemm")
+    def _(A, B, epi, bias, aux, out_dtype, alpha):
+        return _e(A.shape[0], B.shape[0], like=A, dtype=out_dtype)
+
+    @reg("dclip::gemm_gelu")
+    def _(A, B, bias):
+        return _e(A.shape[0], B.shape[0], like=A), _e(A.shape[0], B.shape[0], like=A)
+
+    @reg("dclip::weight_grad")
+    def _(dy, x, alpha, db):
+        return _e(dy.shape[1], x.shape[1], like=dy, dtype=f32)
+
+    @reg("dclip::gemm_tn")
+    def _(A, B):
+        return _e(A.shape[1], B.shape[1], like=A, dtype=f32)
+
+    @reg("dclip::cast")
+    def _(x, dtype, scale):
+        return _e(*x.shape, like=x, dtype=dtype)
+
+    @reg("dclip::transpose2d")
+    def _(x, dtype):
+        return _e(x.shape[1], x.shape[0], like=x, dtype=dtype)
+
+    @reg("dclip::add_readout_cast")
+    def _(a, b, ntok, lp_dtype, scale):
+        return _e(*a.shape, like=a), _e(*a.shape, like=a, dtype=lp_dtype)
+
+    @reg("dclip::attn_fwd")
+    def _(qkv, B, N, H, scale):
+        return _e(B * N, 64 * H, like=qkv), _e(B * H * N, like=qkv, dtype=f32)
+
+    @reg("dclip::attn_fwd_fp8")
+    def _(qkv, B, N, H):
+        return _e(B * N, 64 * H, like=qkv), _e(B * H * N, like=qkv, dtype=f32)
+
+    @reg("dclip::attn_bwd")
+    def _(qkv, o, dout, lse, B, N, H, scale):
+        return torch.empty_like(qkv)
+
+    @reg("dclip::im2col")
+    def _(img, p, dtype):
+        B, Cin, Hi, Wi = img.shape
+        return _e(B * (Hi // p) * (Wi // p), -(-Cin * p * p // 64) * 64, like=img, dtype=dtype)
+
+    @reg("dclip::tokens_fwd")
+    def _(emb, cls, pos, B, P):
+        return _e(B * (P + 1), emb.shape[1], like=emb, dtype=f32)
+
+    @reg("dclip::tokens_bwd")
+    def _(dx, dtype, scale, B, P):
+        C = dx.shape[1]
+        return _e(B * P, C, like=dx, dtype=dtype), _e(C, like=dx, dtype=f32), _e(P + 1, C, like=dx, dtype=f32)
+
+    @reg("dclip::pos_interp")
+    def _(pos, g, H, W):
+        return _e(H * W + 1, pos.shape[1], like=pos)
+
+    @reg("dclip::pos_interp_bwd")
+    def _(dout, g, H, W):
+        return _e(g * g + 1, dout.shape[1], like=dout)
+
+    @reg("dclip::channel_mean")
+    def _(x, B):
+        return _e(B, x.shape[1], like=x, dtype=f32)
+
+    @reg("dclip::score_map")
+    def _(v, text, B, HW, eps):
+        return _e(B, text.shape[1], HW, like=v, dtype=f32)
+
+    @reg("dclip::bilinear")
+    def _(x, Ho, Wo, dtype):
+        return _e(x.shape[0], x.shape[1], Ho, Wo, like=x, dtype=dtype)
+
+    @reg("dclip::bilinear_bwd")
+    def _(dout, Hi, Wi):
+        return _e(dout.shape[0], dout.shape[1], Hi, Wi, like=dout, dtype=f32)
+
+    @reg("dclip::bn_fwd")
+    def _(x, w, b, running_mean, running_var, momentum, eps):
+        C = x.shape[1]
+        return (torch.empty_like(x, memory_format=torch.channels_last), _e(C, like=x, dtype=f32),
+                _e(C, like=x, dtype=f32))
+
+    @reg("dclip::bn_bwd")
+    def _(dy, x, w, mean, rstd, want_w, want_b):
+        C = x.shape[1]
+        return (torch.empty_like(x, memory_format=torch.channels_last), _e(C if want_w else 0, like=x, dtype=f32),
+                _e(C if want_b else 0, like=x, dtype=f32))
+
+    @reg("dclip::conv3x3")
+    def _(mode, X, x_bstride, x_off, x_ld, B, H, W, Cin, Wt, Nout, out, out_ld, out_gap, out_off, accumulate):
+        return None
+
+    @reg("dclip::conv3x3_wgrad")
+    def _(dY, ldy, Nout, X, x_bstride, x_off, x_ld, B, H, W, Cin, splits):
+        return _e(Nout, 9 * Cin, like=X, dtype=f32)
+
+    @reg("dclip::upsample_ce")
+    def _(logits, labels, ignore_index):
+        return (_e(1, like=logits, dtype=torch.float64), _e(1, like=logits, dtype=torch.int32),
+                _e(*logits.shape, like=logits, dtype=f32))
+
+    @reg("dclip::upsample_silog_sums")
+    def _(pred, target, mask, eps):
+        return _e(3, like=pred, dtype=torch.float64)
+
+    @reg("dclip::upsample_silog_grad")
+    def _(pred, target, mask, sums, eps, lambd):
+        return _e(*pred.shape, like=pred, dtype=f32)
+
+    @reg("dclip::cityscapes_prepare")
+    def _(img, ids, disp, crop, h, w, mean, std, bf, depth_max, out_dtype):
+        B = img.shape[0]
+        return (_e(B, 3, h, w, like=img, dtype=out_dtype), _e(B, h, w, like=img, dtype=torch.int64),
+                _e(B, 1, h, w, like=img, dtype=f32), _e(B, 1, h, w, like=img, dtype=torch.uint8))

@@ -1,0 +1,558 @@
+// TORCH_LIBRARY(dclip) — the PyTorch-ROCm custom-op surface of the DenseCLIP ViT hot path
+// (SURVEY §8(b) "Native ABI"): at::Tensor in, at::Tensor out, outputs allocated through the
+// caching allocator, every launch on the current HIP stream of the input's device, errors as
+// TORCH_CHECK (RuntimeError in Python; the reference's blanket try/except -> None of
+// denseclip.py:733-752 is deliberately not reproduced).  Each op is a thin adapter over one
+// entry point of the C ABI in include/dclip.h (libdclip.so), which cites the reference call it
+// replaces.  No op synchronises with the host, so any op sequence can be captured in a
+// hipGraph (torch.cuda.graph).  Fake (meta) implementations and autograd live in Python
+// (denseclip_vit_multimodal_amd/ops.py: torch.library.register_fake, autograd.Function).
+#include <ATen/ATen.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include "../../include/dclip.h"
+
+namespace {
+
+using at::Tensor;
+
+int dt_code(at::ScalarType t) {
+    switch (t) {
+        case at::kFloat: return DCLIP_F32;
+        case at::kHalf: return DCLIP_F16;
+        case at::kBFloat16: return DCLIP_BF16;
+        default: TORCH_CHECK(false, "dclip: unsupported dtype ", t);
+    }
+    return -1;
+}
+
+void* stream_of(const Tensor& t) { return (void*)c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
+
+void check_gpu(const Tensor& t, const char* what, bool contiguous = true) {
+    TORCH_CHECK(t.defined(), "dclip: ", what, " is undefined");
+    TORCH_CHECK(t.is_cuda(), "dclip: ", what, " must be a GPU tensor (the MI355X path has no CPU fallback)");
+    if (contiguous) TORCH_CHECK(t.is_contiguous(), "dclip: ", what, " must be contiguous");
+}
+
+void check_opt(const c10::optional<Tensor>& t, const char* what) {
+    if (t.has_value() && t->defined()) check_gpu(*t, what);
+}
+
+template <typename T>
+T* ptr(const Tensor& t) { return t.defined() ? (T*)t.data_ptr() : nullptr; }
+
+template <typename T>
+T* optr(const c10::optional<Tensor>& t) { return t.has_value() && t->defined() ? (T*)t->data_ptr() : nullptr; }
+
+#define DCLIP_CALL(expr)                                                                    \
+    do {                                                                                    \
+        const int rc_ = (expr);                                                             \
+        TORCH_CHECK(rc_ == 0, "dclip: ", #expr " failed (", rc_, "): ", dclip_last_error()); \
+    } while (0)
+
+at::TensorOptions like(const Tensor& t, at::ScalarType dt) { return t.options().dtype(dt); }
+
+// ----------------------------------------------------------------------------- LayerNorm
+std::tuple<Tensor, Tensor, Tensor> layernorm_fwd(const Tensor& x, const Tensor& w, const Tensor& b,
+                                                 at::ScalarType out_dtype, double eps) {
+    check_gpu(x, "x"); check_gpu(w, "w"); check_gpu(b, "b");
+    TORCH_CHECK(x.dim() == 2 && w.scalar_type() == at::kFloat && b.scalar_type() == at::kFloat,
+                "layernorm_fwd: x (rows, cols), fp32 affine");
+    c10::DeviceGuard g(x.device());
+    const int64_t rows = x.size(0), cols = x.size(1);
+    Tensor y = at::empty({rows, cols}, like(x, out_dtype));
+    Tensor mean = at::empty({rows}, like(x, at::kFloat)), rstd = at::empty({rows}, like(x, at::kFloat));
+    DCLIP_CALL(dclip_layernorm_fwd(x.data_ptr(), dt_code(x.scalar_type()), ptr<float>(w), ptr<float>(b), y.data_ptr(),
+                                   dt_code(out_dtype), ptr<float>(mean), ptr<float>(rstd), rows, cols, (float)eps,
+                                   stream_of(x)));
+    return {y, mean, rstd};
+}
+
+// dx = res + LN^T(dy) (res optional); dw / db accumulated in place
+Tensor layernorm_bwd(const Tensor& dy, const Tensor& x, const Tensor& w, const Tensor& mean, const Tensor& rstd,
+                     const c10::optional<Tensor>& res, Tensor& dw, Tensor& db) {
+    check_gpu(dy, "dy"); check_gpu(x, "x"); check_gpu(w, "w"); check_gpu(mean, "mean"); check_gpu(rstd, "rstd");
+    check_opt(res, "res"); check_gpu(dw, "dw"); check_gpu(db, "db");
+    c10::DeviceGuard g(x.device());
+    Tensor dx = at::empty(x.sizes(), like(x, at::kFloat));
+    DCLIP_CALL(dclip_layernorm_bwd_res(dy.data_ptr(), dt_code(dy.scalar_type()), x.data_ptr(), dt_code(x.scalar_type()),
+                                       ptr<float>(w), ptr<float>(mean), ptr<float>(rstd), optr<float>(res), ptr<float>(dx),
+                                       nullptr, 0, ptr<float>(dw), ptr<float>(db), x.size(0), x.size(1), stream_of(x)));
+    return dx;
+}
+
+// the same plus lp = (lp_dtype) dx, the next GEMM's 16-bit operand
+std::tuple<Tensor, Tensor> layernorm_bwd_lp(const Tensor& dy, const Tensor& x, const Tensor& w, const Tensor& mean,
+                                            const Tensor& rstd, const c10::optional<Tensor>& res, Tensor& dw,
+                                            Tensor& db, at::ScalarType lp_dtype) {
+    check_gpu(dy, "dy"); check_gpu(x, "x"); check_gpu(w, "w"); check_gpu(mean, "mean"); check_gpu(rstd, "rstd");
+    check_opt(res, "res"); check_gpu(dw, "dw"); check_gpu(db, "db");
+    c10::DeviceGuard g(x.device());
+    Tensor dx = at::empty(x.sizes(), like(x, at::kFloat));
+    Tensor lp = at::empty(x.sizes(), like(x, lp_dtype));
+    DCLIP_CALL(dclip_layernorm_bwd_res(dy.data_ptr(), dt_code(dy.scalar_type()), x.data_ptr(), dt_code(x.scalar_type()),
+                                       ptr<float>(w), ptr<float>(mean), ptr<float>(rstd), optr<float>(res), ptr<float>(dx),
+                                       lp.data_ptr(), dt_code(lp_dtype), ptr<float>(dw), ptr<float>(db), x.size(0),
+                                       x.size(1), stream_of(x)));
+    return {dx, lp};
+}
+
+// ----------------------------------------------------------------------------- GEMM
+void gemm_checks(const Tensor& A, const Tensor& B) {
+    TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "gemm: A (M, K), B (N, K)");
+    TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1, "gemm: operands must be k-contiguous");
+    TORCH_CHECK(A.is_cuda() && B.is_cuda(), "gemm: GPU tensors only");
+    TORCH_CHECK(A.scalar_type() == B.scalar_type(), "gemm: A and B dtypes differ");
+}
+
+// out[m][n] = alpha * sum_k A[m][k] B[n][k] (+ epilogue epi != GELU)
+Tensor gemm(const Tensor& A, const Tensor& B, int64_t epi, const c10::optional<Tensor>& bias,
+            const c10::optional<Tensor>& aux, at::ScalarType out_dtype, double alpha) {
+    gemm_checks(A, B);
+    TORCH_CHECK(epi != DCLIP_EPI_GELU && epi != DCLIP_EPI_SPLITK, "gemm: use gemm_gelu / weight_grad for this epilogue");
+    check_opt(bias, "bias");
+    c10::DeviceGuard g(A.device());
+    const int64_t M = A.size(0), N = B.size(0), K = A.size(1);
+    Tensor out = at::empty({M, N}, like(A, out_dtype));
+    const bool has_aux = aux.has_value() && aux->defined();
+    if (has_aux) TORCH_CHECK(aux->is_cuda() && aux->stride(-1) == 1, "gemm: aux must be a row-major GPU tensor");
+    DCLIP_CALL(dclip_gemm((int)epi, dt_code(A.scalar_type()), A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), M, N,
+                          K, 1, (float)alpha, optr<float>(bias), has_aux ? aux->data_ptr() : nullptr,
+                          has_aux ? dt_code(aux->scalar_type()) : 0, has_aux && aux->dim() == 2 ? aux->stride(0) : 0,
+                          out.data_ptr(), dt_code(out_dtype), out.stride(0), nullptr, 0, stream_of(A)));
+    return out;
+}
+
+// z = A B^T + bias, h = quick_gelu(z)  (c_fc + QuickGELU, models.py:277-281, 252-254)
+std::tuple<Tensor, Tensor> gemm_gelu(const Tensor& A, const Tensor& B, const c10::optional<Tensor>& bias) {
+    gemm_checks(A, B);
+    check_opt(bias, "bias");
+    c10::DeviceGuard g(A.device());
+    const int64_t M = A.size(0), N = B.size(0), K = A.size(1);
+    Tensor z = at::empty({M, N}, A.options()), h = at::empty({M, N}, A.options());
+    DCLIP_CALL(dclip_gemm(DCLIP_EPI_GELU, dt_code(A.scalar_type()), A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0),
+                          M, N, K, 1, 1.0f, optr<float>(bias), nullptr, 0, 0, z.data_ptr(), dt_code(A.scalar_type()),
+                          z.stride(0), h.data_ptr(), h.stride(0), stream_of(A)));
+    return {z, h};
+}
+
+// dW = alpha dy^T x (f32) and, when db is given, db += alpha colsum(dy)
+Tensor weight_grad(const Tensor& dy, const Tensor& x, double alpha, c10::optional<Tensor> db) {
+    check_gpu(dy, "dy"); check_gpu(x, "x");
+    TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0), "weight_grad: dy (M, N), x (M, K)");
+    check_opt(db, "db");
+    c10::DeviceGuard g(dy.device());
+    const int64_t M = dy.size(0), N = dy.size(1), K = x.size(1);
+    int splits = 0;
+    int64_t k_pad = 0;
+    DCLIP_CALL(dclip_gemm_tn_plan(N, K, M, &splits, &k_pad));
+    Tensor dW = at::empty({N, K}, like(dy, at::kFloat));
+    Tensor ws = at::empty({(int64_t)splits * N * K}, like(dy, at::kFloat));
+    DCLIP_CALL(dclip_gemm_tn(DCLIP_EPI_SPLITK, dt_code(dy.scalar_type()), dy.data_ptr(), dy.stride(0), x.data_ptr(),
+                             x.stride(0), N, K, M, k_pad, splits, (float)alpha, nullptr, ws.data_ptr(), dW.data_ptr(), K,
+                             optr<float>(db), stream_of(dy)));
+    return dW;
+}
+
+// out[m][n] = sum_k A[k][m] B[k][n] (f32)
+Tensor gemm_tn(const Tensor& A, const Tensor& B) {
+    check_gpu(A, "A"); check_gpu(B, "B");
+    TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(0) == B.size(0), "gemm_tn: A (K, M), B (K, N)");
+    c10::DeviceGuard g(A.device());
+    const int64_t K = A.size(0), M = A.size(1), N = B.size(1);
+    Tensor out = at::empty({M, N}, like(A, at::kFloat));
+    DCLIP_CALL(dclip_gemm_tn(DCLIP_EPI_STORE, dt_code(A.scalar_type()), A.data_ptr(), A.stride(0), B.data_ptr(),
+                             B.stride(0), M, N, K, (K + 63) / 64 * 64, 1, 1.0f, nullptr, nullptr, out.data_ptr(), N,
+                             nullptr, stream_of(A)));
+    return out;
+}
+
+// ----------------------------------------------------------------------------- element-wise
+Tensor cast(const Tensor& x, at::ScalarType dtype, double scale) {
+    check_gpu(x, "x");
+    c10::DeviceGuard g(x.device());
+    Tensor y = at::empty(x.sizes(), like(x, dtype));
+    DCLIP_CALL(dclip_cast(x.data_ptr(), dt_code(x.scalar_type()), y.data_ptr(), dt_code(dtype), x.numel(), (float)scale,
+                          stream_of(x)));
+    return y;
+}
+
+// 2-D transpose (rows, cols) -> (cols, rows) in dtype
+Tensor transpose2d(const Tensor& x, at::ScalarType dtype) {
+    check_gpu(x, "x");
+    TORCH_CHECK(x.dim() == 2, "transpose2d: 2-D input");
+    c10::DeviceGuard g(x.device());
+    const int64_t rows = x.size(0), cols = x.size(1);
+    Tensor out = at::empty({cols, rows}, like(x, dtype));
+    DCLIP_CALL(dclip_transpose(x.data_ptr(), dt_code(x.scalar_type()), 0, cols, 0, out.data_ptr(), dt_code(dtype),
+                               cols * rows, rows, 1, rows, rows, cols, 0, nullptr, stream_of(x)));
+    return out;
+}
+
+std::tuple<Tensor, Tensor> add_readout_cast(const Tensor& a, const Tensor& b, int64_t ntok, at::ScalarType lp_dtype,
+                                            double scale) {
+    check_gpu(a, "a"); check_gpu(b, "b", false);
+    TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && b.stride(1) == 1 && b.stride(0) == a.size(1) && a.sizes() == b.sizes(),
+                "add_readout_cast: a, b (rows, cols) row-major");
+    c10::DeviceGuard g(a.device());
+    Tensor sum = at::empty(a.sizes(), a.options());
+    Tensor lp = at::empty(a.sizes(), like(a, lp_dtype));
+    DCLIP_CALL(dclip_add_readout_cast(ptr<float>(a), b.data_ptr(), dt_code(b.scalar_type()), ptr<float>(sum), lp.data_ptr(),
+                                      dt_code(lp_dtype), a.size(0), (int)a.size(1), (int)ntok, (float)scale, stream_of(a)));
+    return {sum, lp};
+}
+
+// ----------------------------------------------------------------------------- attention
+std::tuple<Tensor, Tensor> attn_fwd(const Tensor& qkv, int64_t B, int64_t N, int64_t H, double scale) {
+    check_gpu(qkv, "qkv");
+    TORCH_CHECK(qkv.dim() == 2 && qkv.size(0) == B * N && qkv.size(1) == 3 * 64 * H, "attn_fwd: qkv (B*N, 3*H*64)");
+    c10::DeviceGuard g(qkv.device());
+    Tensor o = at::empty({B * N, 64 * H}, qkv.options());
+    Tensor lse = at::empty({B * H * N}, like(qkv, at::kFloat));
+    DCLIP_CALL(dclip_attn_fwd(dt_code(qkv.scalar_type()), qkv.data_ptr(), o.data_ptr(), ptr<float>(lse), (int)B, (int)N,
+                              (int)H, 64, (float)scale, stream_of(qkv)));
+    return {o, lse};
+}
+
+std::tuple<Tensor, Tensor> attn_fwd_fp8(const Tensor& qkv, int64_t B, int64_t N, int64_t H) {
+    check_gpu(qkv, "qkv");
+    TORCH_CHECK(qkv.dim() == 2 && qkv.size(0) == B * N && qkv.size(1) == 3 * 64 * H, "attn_fwd_fp8: qkv (B*N, 3*H*64)");
+    c10::DeviceGuard g(qkv.device());
+    Tensor o = at::empty({B * N, 64 * H}, qkv.options());
+    Tensor lse = at::empty({B * H * N}, like(qkv, at::kFloat));
+    Tensor ws = at::empty({dclip_attn_fwd_fp8_workspace((int)B, (int)N, (int)H)}, like(qkv, at::kByte));
+    DCLIP_CALL(dclip_attn_fwd_fp8(dt_code(qkv.scalar_type()), qkv.data_ptr(), o.data_ptr(), ptr<float>(lse), ws.data_ptr(),
+                                  (int)B, (int)N, (int)H, 64, stream_of(qkv)));
+    return {o, lse};
+}
+
+Tensor attn_bwd(const Tensor& qkv, const Tensor& o, const Tensor& dout, const Tensor& lse, int64_t B, int64_t N,
+                int64_t H, double scale) {
+    check_gpu(qkv, "qkv"); check_gpu(o, "o"); check_gpu(dout, "dout"); check_gpu(lse, "lse");
+    TORCH_CHECK(qkv.size(0) == B * N && o.sizes() == dout.sizes() && o.size(1) == 64 * H, "attn_bwd: shapes");
+    c10::DeviceGuard g(qkv.device());
+    Tensor ws = at::empty({dclip_attn_bwd_workspace((int)B, (int)N, (int)H)}, like(qkv, at::kFloat));
+    Tensor dqkv = at::empty_like(qkv);
+    DCLIP_CALL(dclip_attn_bwd(dt_code(qkv.scalar_type()), qkv.data_ptr(), o.data_ptr(), dout.data_ptr(), ptr<float>(lse),
+                              ptr<float>(ws), dqkv.data_ptr(), (int)B, (int)N, (int)H, 64, (float)scale, stream_of(qkv)));
+    return dqkv;
+}
+
+// ----------------------------------------------------------------------------- patch embedding
+Tensor im2col(const Tensor& img, int64_t p, at::ScalarType dtype) {
+    check_gpu(img, "img");
+    TORCH_CHECK(img.dim() == 4, "im2col: img (B, Cin, H, W)");
+    c10::DeviceGuard g(img.device());
+    const int64_t B = img.size(0), Cin = img.size(1), Hin = img.size(2), Win = img.size(3);
+    const int64_t k_pad = (Cin * p * p + 63) / 64 * 64;
+    Tensor out = at::empty({B * (Hin / p) * (Win / p), k_pad}, like(img, dtype));
+    DCLIP_CALL(dclip_im2col(img.data_ptr(), dt_code(img.scalar_type()), out.data_ptr(), dt_code(dtype), k_pad, (int)B,
+                            (int)Cin, (int)Hin, (int)Win, (int)p, stream_of(img)));
+    return out;
+}
+
+Tensor tokens_fwd(const Tensor& emb, const Tensor& cls, const Tensor& pos, int64_t B, int64_t P) {
+    check_gpu(emb, "emb"); check_gpu(cls, "cls"); check_gpu(pos, "pos");
+    const int64_t C = emb.size(1);
+    TORCH_CHECK(emb.size(0) == B * P && pos.size(0) == P + 1 && cls.numel() == C, "tokens_fwd: shapes");
+    c10::DeviceGuard g(emb.device());
+    Tensor x = at::empty({B * (P + 1), C}, like(emb, at::kFloat));
+    DCLIP_CALL(dclip_tokens_fwd(emb.data_ptr(), dt_code(emb.scalar_type()), ptr<float>(cls), ptr<float>(pos), ptr<float>(x),
+                                (int)B, (int)P, (int)C, stream_of(emb)));
+    return x;
+}
+
+// (demb = scale * dx[patch rows] in dtype, dcls, dpos (P+1, C))
+std::tuple<Tensor, Tensor, Tensor> tokens_bwd(const Tensor& dx, at::ScalarType dtype, double scale, int64_t B,
+                                              int64_t P) {
+    check_gpu(dx, "dx");
+    const int64_t C = dx.size(1);
+    TORCH_CHECK(dx.size(0) == B * (P + 1), "tokens_bwd: dx (B*(P+1), C)");
+    c10::DeviceGuard g(dx.device());
+    Tensor demb = at::empty({B * P, C}, like(dx, dtype));
+    Tensor dcls = at::zeros({C}, like(dx, at::kFloat));
+    Tensor dpos = at::zeros({P + 1, C}, like(dx, at::kFloat));
+    DCLIP_CALL(dclip_tokens_bwd(ptr<float>(dx), demb.data_ptr(), dt_code(dtype), (float)scale, ptr<float>(dcls),
+                                ptr<float>(dpos), (int)B, (int)P, (int)C, stream_of(dx)));
+    return {demb, dcls, dpos};
+}
+
+Tensor pos_interp(const Tensor& pos, int64_t g, int64_t H, int64_t W) {
+    check_gpu(pos, "pos");
+    TORCH_CHECK(pos.scalar_type() == at::kFloat && pos.size(0) == g * g + 1, "pos_interp: pos (g*g+1, C) fp32");
+    c10::DeviceGuard gd(pos.device());
+    Tensor out = at::empty({H * W + 1, pos.size(1)}, pos.options());
+    DCLIP_CALL(dclip_pos_interp_fwd(ptr<float>(pos), ptr<float>(out), (int)g, (int)pos.size(1), (int)H, (int)W,
+                                    stream_of(pos)));
+    return out;
+}
+
+Tensor pos_interp_bwd(const Tensor& dout, int64_t g, int64_t H, int64_t W) {
+    check_gpu(dout, "dout");
+    TORCH_CHECK(dout.scalar_type() == at::kFloat && dout.size(0) == H * W + 1, "pos_interp_bwd: dout (H*W+1, C) fp32");
+    c10::DeviceGuard gd(dout.device());
+    Tensor dpos = at::zeros({g * g + 1, dout.size(1)}, dout.options());
+    DCLIP_CALL(dclip_pos_interp_bwd(ptr<float>(dout), ptr<float>(dpos), (int)g, (int)dout.size(1), (int)H, (int)W,
+                                    stream_of(dout)));
+    return dpos;
+}
+
+// ----------------------------------------------------------------------------- score map / resize
+Tensor channel_mean(const Tensor& x, int64_t B) {
+    check_gpu(x, "x");
+    TORCH_CHECK(x.dim() == 2 && x.size(0) % B == 0, "channel_mean: x (B*rows, C)");
+    c10::DeviceGuard g(x.device());
+    Tensor out = at::empty({B, x.size(1)}, like(x, at::kFloat));
+    DCLIP_CALL(dclip_channel_mean(x.data_ptr(), dt_code(x.scalar_type()), ptr<float>(out), (int)B, x.size(0) / B,
+                                  (int)x.size(1), stream_of(x)));
+    return out;
+}
+
+Tensor score_map(const Tensor& v, const Tensor& text, int64_t B, int64_t HW, double eps) {
+    check_gpu(v, "v"); check_gpu(text, "text");
+    TORCH_CHECK(text.scalar_type() == at::kFloat && text.dim() == 3 && text.size(2) == v.size(1), "score_map: text (B, K, C) fp32");
+    c10::DeviceGuard g(v.device());
+    const int64_t K = text.size(1), C = text.size(2);
+    Tensor out = at::empty({B, K, HW}, like(v, at::kFloat));
+    DCLIP_CALL(dclip_score_map(v.data_ptr(), dt_code(v.scalar_type()), ptr<float>(text), ptr<float>(out), (int)B, (int)HW,
+                               (int)C, (int)K, (float)eps, stream_of(v)));
+    return out;
+}
+
+Tensor bilinear(const Tensor& x, int64_t Ho, int64_t Wo, at::ScalarType dtype) {
+    check_gpu(x, "x");
+    TORCH_CHECK(x.dim() == 4, "bilinear: x (n, c, h, w)");
+    c10::DeviceGuard g(x.device());
+    Tensor out = at::empty({x.size(0), x.size(1), Ho, Wo}, like(x, dtype));
+    DCLIP_CALL(dclip_bilinear_fwd(x.data_ptr(), dt_code(x.scalar_type()), out.data_ptr(), dt_code(dtype),
+                                  x.size(0) * x.size(1), (int)x.size(2), (int)x.size(3), (int)Ho, (int)Wo, stream_of(x)));
+    return out;
+}
+
+Tensor bilinear_bwd(const Tensor& dout, int64_t Hi, int64_t Wi) {
+    check_gpu(dout, "dout");
+    TORCH_CHECK(dout.dim() == 4, "bilinear_bwd: dout (n, c, H, W)");
+    c10::DeviceGuard g(dout.device());
+    const int64_t nc = dout.size(0) * dout.size(1), Ho = dout.size(2), Wo = dout.size(3);
+    Tensor din = at::empty({dout.size(0), dout.size(1), Hi, Wi}, like(dout, at::kFloat));
+    Tensor ws = at::empty({nc * Ho * Wi}, like(dout, at::kFloat));
+    DCLIP_CALL(dclip_bilinear_bwd(dout.data_ptr(), dt_code(dout.scalar_type()), ptr<float>(din), ptr<float>(ws), nc,
+                                  (int)Hi, (int)Wi, (int)Ho, (int)Wo, stream_of(dout)));
+    return din;
+}
+
+// ----------------------------------------------------------------------------- BatchNorm (train mode)
+// x: channels-last (B, C, H, W) 16-bit map viewed as (rows, C)
+std::tuple<Tensor, Tensor, Tensor> bn_fwd(const Tensor& x, const c10::optional<Tensor>& w,
+                                          const c10::optional<Tensor>& b, c10::optional<Tensor> running_mean,
+                                          c10::optional<Tensor> running_var, double momentum, double eps) {
+    TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "bn_fwd: channels-last 4-D GPU map");
+    check_opt(w, "w"); check_opt(b, "b"); check_opt(running_mean, "running_mean"); check_opt(running_var, "running_var");
+    c10::DeviceGuard g(x.device());
+    const int64_t C = x.size(1), rows = x.numel() / C;
+    Tensor ws = at::empty({dclip_bn_workspace(rows, (int)C)}, like(x, at::kFloat));
+    Tensor mean = at::empty({C}, like(x, at::kFloat)), rstd = at::empty({C}, like(x, at::kFloat));
+    Tensor y = at::empty_like(x, at::MemoryFormat::ChannelsLast);
+    DCLIP_CALL(dclip_bn_fwd(dt_code(x.scalar_type()), x.data_ptr(), rows, (int)C, optr<float>(w), optr<float>(b), (float)eps,
+                            (float)momentum, optr<float>(running_mean), optr<float>(running_var), ptr<float>(ws),
+                            ptr<float>(mean), ptr<float>(rstd), y.data_ptr(), stream_of(x)));
+    return {y, mean, rstd};
+}
+
+std::tuple<Tensor, Tensor, Tensor> bn_bwd(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& w,
+                                          const Tensor& mean, const Tensor& rstd, bool want_w, bool want_b) {
+    TORCH_CHECK(dy.is_contiguous(at::MemoryFormat::ChannelsLast) && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "bn_bwd: channels-last maps");
+    TORCH_CHECK(dy.scalar_type() == x.scalar_type(), "bn_bwd: dy dtype must match x");
+    check_opt(w, "w"); check_gpu(mean, "mean"); check_gpu(rstd, "rstd");
+    c10::DeviceGuard g(x.device());
+    const int64_t C = x.size(1), rows = x.numel() / C;
+    Tensor ws = at::empty({dclip_bn_workspace(rows, (int)C)}, like(x, at::kFloat));
+    Tensor dx = at::empty_like(x, at::MemoryFormat::ChannelsLast);
+    Tensor dw = want_w ? at::empty({C}, like(x, at::kFloat)) : at::empty({0}, like(x, at::kFloat));
+    Tensor db = want_b ? at::empty({C}, like(x, at::kFloat)) : at::empty({0}, like(x, at::kFloat));
+    DCLIP_CALL(dclip_bn_bwd(dt_code(x.scalar_type()), dy.data_ptr(), x.data_ptr(), rows, (int)C, optr<float>(w),
+                            ptr<float>(mean), ptr<float>(rstd), ptr<float>(ws), dx.data_ptr(),
+                            want_w ? ptr<float>(dw) : nullptr, want_b ? ptr<float>(db) : nullptr, stream_of(x)));
+    return {dx, dw, db};
+}
+
+// ----------------------------------------------------------------------------- neck 3x3 conv
+// X: any GPU tensor whose data_ptr is input pixel (0, 0, 0) (a channels-last map or a token-
+// buffer view); geometry in elements as in dclip.h.  out: written (or accumulated) in place.
+void conv3x3(int64_t mode, const Tensor& X, int64_t x_bstride, int64_t x_off, int64_t x_ld, int64_t B, int64_t H,
+             int64_t W, int64_t Cin, const Tensor& Wt, int64_t Nout, Tensor& out, int64_t out_ld, int64_t out_gap,
+             int64_t out_off, int64_t accumulate) {
+    check_gpu(X, "X", false); check_gpu(Wt, "Wt"); check_gpu(out, "out", false);
+    TORCH_CHECK(X.scalar_type() == Wt.scalar_type(), "conv3x3: X and Wt dtypes differ");
+    c10::DeviceGuard g(X.device());
+    DCLIP_CALL(dclip_conv3x3((int)mode, dt_code(X.scalar_type()), X.data_ptr(), x_bstride, x_off, x_ld, (int)B, (int)H,
+                             (int)W, (int)Cin, Wt.data_ptr(), (int)Nout, out.data_ptr(), dt_code(out.scalar_type()), out_ld,
+                             (int)out_gap, (int)out_off, (int)accumulate, stream_of(X)));
+}
+
+Tensor conv3x3_wgrad(const Tensor& dY, int64_t ldy, int64_t Nout, const Tensor& X, int64_t x_bstride, int64_t x_off,
+                     int64_t x_ld, int64_t B, int64_t H, int64_t W, int64_t Cin, int64_t splits) {
+    check_gpu(dY, "dY", false); check_gpu(X, "X", false);
+    c10::DeviceGuard g(X.device());
+    Tensor dW = at::empty({Nout, 9 * Cin}, like(X, at::kFloat));
+    Tensor ws = at::empty({splits * Nout * 9 * Cin}, like(X, at::kFloat));
+    DCLIP_CALL(dclip_conv3x3_wgrad(dt_code(dY.scalar_type()), dY.data_ptr(), ldy, (int)Nout, X.data_ptr(), x_bstride,
+                                   x_off, x_ld, (int)B, (int)H, (int)W, (int)Cin, ptr<float>(dW), ws.data_ptr(),
+                                   (int)splits, stream_of(X)));
+    return dW;
+}
+
+// ----------------------------------------------------------------------------- fused head losses
+int lab_code(at::ScalarType t) {
+    switch (t) {
+        case at::kLong: return 0;
+        case at::kInt: return 1;
+        case at::kByte: return 2;
+        default: TORCH_CHECK(false, "upsample_ce: labels must be int64, int32 or uint8");
+    }
+    return -1;
+}
+
+// (loss sum f64[1], valid count i32[1], un-normalised low-res gradient f32)
+std::tuple<Tensor, Tensor, Tensor> upsample_ce(const Tensor& logits, const Tensor& labels, int64_t ignore_index) {
+    check_gpu(logits, "logits"); check_gpu(labels, "labels");
+    TORCH_CHECK(logits.dim() == 4 && labels.dim() == 3 && labels.size(0) == logits.size(0), "upsample_ce: shapes");
+    c10::DeviceGuard g(logits.device());
+    Tensor sums = at::zeros({1}, like(logits, at::kDouble));
+    Tensor cnt = at::zeros({1}, like(logits, at::kInt));
+    Tensor grad = at::zeros(logits.sizes(), like(logits, at::kFloat));
+    DCLIP_CALL(dclip_upsample_ce(dt_code(logits.scalar_type()), logits.data_ptr(), (int)logits.size(0),
+                                 (int)logits.size(1), (int)logits.size(2), (int)logits.size(3), labels.data_ptr(),
+                                 lab_code(labels.scalar_type()), (int)labels.size(1), (int)labels.size(2),
+                                 (int)ignore_index, (double*)sums.data_ptr(), (unsigned*)cnt.data_ptr(), ptr<float>(grad),
+                                 stream_of(logits)));
+    return {sums, cnt, grad};
+}
+
+// pass 0 of the SILog pair: sums f64[3] = (sum d, sum d^2, T)
+Tensor upsample_silog_sums(const Tensor& pred, const Tensor& target, const c10::optional<Tensor>& mask, double eps) {
+    check_gpu(pred, "pred"); check_gpu(target, "target"); check_opt(mask, "mask");
+    TORCH_CHECK(target.scalar_type() == at::kFloat && target.dim() == 3, "upsample_silog: target (B, H, W) fp32");
+    c10::DeviceGuard g(pred.device());
+    Tensor sums = at::zeros({3}, like(pred, at::kDouble));
+    DCLIP_CALL(dclip_upsample_silog(0, dt_code(pred.scalar_type()), pred.data_ptr(), (int)pred.size(0), (int)pred.size(2),
+                                    (int)pred.size(3), ptr<float>(target), optr<uint8_t>(mask), (int)target.size(1),
+                                    (int)target.size(2), (float)eps, 0.f, (double*)sums.data_ptr(), nullptr,
+                                    stream_of(pred)));
+    return sums;
+}
+
+// pass 1: d loss / d pred (low-res, f32) from the complete sums
+Tensor upsample_silog_grad(const Tensor& pred, const Tensor& target, const c10::optional<Tensor>& mask,
+                           const Tensor& sums, double eps, double lambd) {
+    check_gpu(pred, "pred"); check_gpu(target, "target"); check_opt(mask, "mask"); check_gpu(sums, "sums");
+    c10::DeviceGuard g(pred.device());
+    Tensor grad = at::zeros(pred.sizes(), like(pred, at::kFloat));
+    DCLIP_CALL(dclip_upsample_silog(1, dt_code(pred.scalar_type()), pred.data_ptr(), (int)pred.size(0), (int)pred.size(2),
+                                    (int)pred.size(3), ptr<float>(target), optr<uint8_t>(mask), (int)target.size(1),
+                                    (int)target.size(2), (float)eps, (float)lambd, (double*)sums.data_ptr(),
+                                    ptr<float>(grad), stream_of(pred)));
+    return grad;
+}
+
+// ----------------------------------------------------------------------------- Cityscapes batch preparation
+std::tuple<Tensor, Tensor, Tensor, Tensor> cityscapes_prepare(const Tensor& img, const Tensor& ids, const Tensor& disp,
+                                                              const Tensor& crop, int64_t h, int64_t w,
+                                                              at::ArrayRef<double> mean, at::ArrayRef<double> stdv,
+                                                              double bf, double depth_max, at::ScalarType out_dtype) {
+    check_gpu(img, "img"); check_gpu(ids, "ids"); check_gpu(disp, "disp"); check_gpu(crop, "crop");
+    TORCH_CHECK(mean.size() == 3 && stdv.size() == 3, "cityscapes_prepare: 3 means / stds");
+    TORCH_CHECK(img.dim() == 4 && img.size(3) == 3 && crop.scalar_type() == at::kInt, "cityscapes_prepare: shapes");
+    c10::DeviceGuard g(img.device());
+    const int64_t B = img.size(0), H = img.size(1), W = img.size(2);
+    Tensor out_img = at::empty({B, 3, h, w}, like(img, out_dtype));
+    Tensor seg = at::empty({B, h, w}, like(img, at::kLong));
+    Tensor depth = at::empty({B, 1, h, w}, like(img, at::kFloat));
+    Tensor mask = at::empty({B, 1, h, w}, like(img, at::kByte));
+    const float m[3] = {(float)mean[0], (float)mean[1], (float)mean[2]};
+    const float s[3] = {(float)stdv[0], (float)stdv[1], (float)stdv[2]};
+    DCLIP_CALL(dclip_cityscapes_prepare(ptr<uint8_t>(img), ptr<uint8_t>(ids), (const uint16_t*)disp.data_ptr(), (int)B,
+                                        (int)H, (int)W, ptr<int>(crop), (int)h, (int)w, m, s, (float)bf, (float)depth_max,
+                                        out_img.data_ptr(), dt_code(out_dtype), ptr<int64_t>(seg), ptr<float>(depth),
+                                        ptr<uint8_t>(mask), stream_of(img)));
+    return {out_img, seg, depth, mask};
+}
+
+}  // namespace
+
+TORCH_LIBRARY(dclip, m) {
+    m.def("layernorm_fwd(Tensor x, Tensor w, Tensor b, ScalarType out_dtype, float eps) -> (Tensor, Tensor, Tensor)");
+    m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, Tensor? res, Tensor(a!) dw, "
+          "Tensor(b!) db) -> Tensor");
+    m.def("layernorm_bwd_lp(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, Tensor? res, Tensor(a!) dw, "
+          "Tensor(b!) db, ScalarType lp_dtype) -> (Tensor, Tensor)");
+    m.def("gemm(Tensor A, Tensor B, int epi, Tensor? bias, Tensor? aux, ScalarType out_dtype, float alpha) -> Tensor");
+    m.def("gemm_gelu(Tensor A, Tensor B, Tensor? bias) -> (Tensor, Tensor)");
+    m.def("weight_grad(Tensor dy, Tensor x, float alpha, Tensor(a!)? db) -> Tensor");
+    m.def("gemm_tn(Tensor A, Tensor B) -> Tensor");
+    m.def("cast(Tensor x, ScalarType dtype, float scale) -> Tensor");
+    m.def("transpose2d(Tensor x, ScalarType dtype) -> Tensor");
+    m.def("add_readout_cast(Tensor a, Tensor b, int ntok, ScalarType lp_dtype, float scale) -> (Tensor, Tensor)");
+    m.def("attn_fwd(Tensor qkv, int B, int N, int H, float scale) -> (Tensor, Tensor)");
+    m.def("attn_fwd_fp8(Tensor qkv, int B, int N, int H) -> (Tensor, Tensor)");
+    m.def("attn_bwd(Tensor qkv, Tensor o, Tensor dout, Tensor lse, int B, int N, int H, float scale) -> Tensor");
+    m.def("im2col(Tensor img, int p, ScalarType dtype) -> Tensor");
+    m.def("tokens_fwd(Tensor emb, Tensor cls, Tensor pos, int B, int P) -> Tensor");
+    m.def("tokens_bwd(Tensor dx, ScalarType dtype, float scale, int B, int P) -> (Tensor, Tensor, Tensor)");
+    m.def("pos_interp(Tensor pos, int g, int H, int W) -> Tensor");
+    m.def("pos_interp_bwd(Tensor dout, int g, int H, int W) -> Tensor");
+    m.def("channel_mean(Tensor x, int B) -> Tensor");
+    m.def("score_map(Tensor v, Tensor text, int B, int HW, float eps) -> Tensor");
+    m.def("bilinear(Tensor x, int Ho, int Wo, ScalarType dtype) -> Tensor");
+    m.def("bilinear_bwd(Tensor dout, int Hi, int Wi) -> Tensor");
+    m.def("bn_fwd(Tensor x, Tensor? w, Tensor? b, Tensor(a!)? running_mean, Tensor(b!)? running_var, float momentum, "
+          "float eps) -> (Tensor, Tensor, Tensor)");
+    m.def("bn_bwd(Tensor dy, Tensor x, Tensor? w, Tensor mean, Tensor rstd, bool want_w, bool want_b) -> "
+          "(Tensor, Tensor, Tensor)");
+    m.def("conv3x3(int mode, Tensor X, int x_bstride, int x_off, int x_ld, int B, int H, int W, int Cin, Tensor Wt, "
+          "int Nout, Tensor(a!) out, int out_ld, int out_gap, int out_off, int accumulate) -> ()");
+    m.def("conv3x3_wgrad(Tensor dY, int ldy, int Nout, Tensor X, int x_bstride, int x_off, int x_ld, int B, int H, "
+          "int W, int Cin, int splits) -> Tensor");
+    m.def("upsample_ce(Tensor logits, Tensor labels, int ignore_index) -> (Tensor, Tensor, Tensor)");
+    m.def("upsample_silog_sums(Tensor pred, Tensor target, Tensor? mask, float eps) -> Tensor");
+    m.def("upsample_silog_grad(Tensor pred, Tensor target, Tensor? mask, Tensor sums, float eps, float lambd) -> Tensor");
+    m.def("cityscapes_prepare(Tensor img, Tensor ids, Tensor disp, Tensor crop, int h, int w, float[] mean, "
+          "float[] std, float bf, float depth_max, ScalarType out_dtype) -> (Tensor, Tensor, Tensor, Tensor)");
+}
+
+TORCH_LIBRARY_IMPL(dclip, CUDA, m) {
+    m.impl("layernorm_fwd", &layernorm_fwd);
+    m.impl("layernorm_bwd", &layernorm_bwd);
+    m.impl("layernorm_bwd_lp", &layernorm_bwd_lp);
+    m.impl("gemm", &gemm);
+    m.impl("gemm_gelu", &gemm_gelu);
+    m.impl("weight_grad", &weight_grad);
+    m.impl("gemm_tn", &gemm_tn);
+    m.impl("cast", &cast);
+    m.impl("transpose2d", &transpose2d);
+    m.impl("add_readout_cast", &add_readout_cast);
+    m.impl("attn_fwd", &attn_fwd);
+    m.impl("attn_fwd_fp8", &attn_fwd_fp8);
+    m.impl("attn_bwd", &attn_bwd);
+    m.impl("im2col", &im2col);
+    m.impl("tokens_fwd", &tokens_fwd);
+    m.impl("tokens_bwd", &tokens_bwd);
+    m.impl("pos_interp", &pos_interp);
+    m.impl("pos_interp_bwd", &pos_interp_bwd);
+    m.impl("channel_mean", &channel_mean);
+    m.impl("score_map", &score_map);
+    m.impl("bilinear", &bilinear);
+    m.impl("bilinear_bwd", &bilinear_bwd);
+    m.impl("bn_fwd", &bn_fwd);
+    m.impl("bn_bwd", &bn_bwd);
+    m.impl("conv3x3", &conv3x3);
+    m.impl("conv3x3_wgrad", &conv3x3_wgrad);
+    m.impl("upsample_ce", &upsample_ce);
+    m.impl("upsample_silog_sums", &upsample_silog_sums);
+    m.impl("upsample_silog_grad", &upsample_silog_grad);
+    m.impl("cityscapes_prepare", &cityscapes_prepare);
+}

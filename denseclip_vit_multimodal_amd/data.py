@@ -18,7 +18,7 @@ import os.path as osp
 import numpy as np
 import torch
 
-from . import _native as N
+
 
 # reference constants (datasets/cityscapes_depth_seg.py:19-23) and CLIP normalisation
 # (train_denseclip.py:113-114)
@@ -123,15 +123,7 @@ def prepare_batch(samples, crop_hw, crops, device, out_dtype=torch.bfloat16, mea
     ids = up([s[1] for s in samples])
     disp = up([s[2].view(np.int16) for s in samples])  # the uint16 bits through an int16 tensor
     cr = crops.to(dev)
-    out_img = torch.empty(B, 3, h, w, dtype=out_dtype, device=dev)
-    seg = torch.empty(B, h, w, dtype=torch.int64, device=dev)
-    depth = torch.empty(B, 1, h, w, dtype=torch.float32, device=dev)
-    mask = torch.empty(B, 1, h, w, dtype=torch.uint8, device=dev)
-    import ctypes
-    m = (ctypes.c_float * 3)(*mean)
-    sd = (ctypes.c_float * 3)(*std)
-    from .ops import _DT, _stream
-    N.call("dclip_cityscapes_prepare", img.data_ptr(), ids.data_ptr(), disp.data_ptr(), B, H, W, cr.data_ptr(),
-           h, w, ctypes.cast(m, ctypes.c_void_p), ctypes.cast(sd, ctypes.c_void_p), float(bf), float(depth_max),
-           out_img.data_ptr(), _DT[out_dtype], seg.data_ptr(), depth.data_ptr(), mask.data_ptr(), _stream())
+    from .ops import D
+    out_img, seg, depth, mask = D().cityscapes_prepare(img, ids, disp, cr, h, w, [float(v) for v in mean],
+                                                       [float(v) for v in std], float(bf), float(depth_max), out_dtype)
     return out_img, seg, depth, mask.view(torch.bool)

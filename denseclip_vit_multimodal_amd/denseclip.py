@@ -125,6 +125,10 @@ class DenseCLIP(nn.Module):
         if decode_head:
             dtype_ = decode_head.get("type")
             self.align_corners = decode_head.get("align_corners", False)
+            if self.align_corners:
+                # the resize kernels (bilinear, fused resize + CE / SILog) implement the
+                # config's align_corners=False only (denseclip.py:847, 860, 899, 909)
+                raise NotImplementedError("decode_head.align_corners=True is not supported by the HIP resize kernels")
             self.num_classes = decode_head.get("num_classes", self.num_classes)
             hin = decode_head.get("in_channels", head_in)
             if dtype_ == "FPNHead":
@@ -141,6 +145,8 @@ class DenseCLIP(nn.Module):
         self.depth_head = None
         self.with_depth_head = False
         if depth_head:
+            if depth_head.get("align_corners", False):
+                raise NotImplementedError("depth_head.align_corners=True is not supported by the HIP resize kernels")
             if depth_head.get("type") == "FCNHeadDepth":
                 ch = depth_head.get("channels", 128)
                 self.depth_head = FCNHead(depth_head.get("in_channels", head_in), ch)
@@ -252,7 +258,9 @@ class DenseCLIP(nn.Module):
         params = list(self.text_encoder.parameters())
         if self.contexts is not None:
             params.append(self.contexts)
-        frozen = not any(p.requires_grad for p in params)
+        # no autograd graph is recorded when gradients are off (the score-map branch runs under
+        # no_grad: its output is discarded, denseclip.py:747), trainable parameters or not
+        frozen = not torch.is_grad_enabled() or not any(p.requires_grad for p in params)
         if not (self.graph_text and frozen and device.type == "cuda"):
             return self._text_forward(texts).expand(B, -1, -1)
         # every device buffer the graph reads is in the key: a re-allocated one forces a new capture
@@ -284,6 +292,12 @@ class DenseCLIP(nn.Module):
         HW = h * w
         cdt = visual.dtype if visual.dtype in (torch.bfloat16, torch.float16) else \
             getattr(self.backbone, "compute_dtype", torch.bfloat16)
+        if 0 <= self.score_concat_index < len(x) and torch.is_grad_enabled() and any(
+                p.requires_grad for m in (self.vis_proj, self.global_proj, self.context_decoder) if m is not None
+                for p in m.parameters()):
+            # the score branch below is forward-only (no autograd through the HIP score map)
+            raise NotImplementedError("training through score_concat_index >= 0 (the score map feeding the "
+                                      "neck) is not supported; the ViT Cityscapes config uses -1")
         with torch.no_grad():
             # channel-last pixel rows of the last map (the read-out is a channels-last view)
             pix = visual.permute(0, 2, 3, 1).reshape(B * HW, Cv).to(cdt).contiguous()

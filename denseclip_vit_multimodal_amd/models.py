@@ -180,9 +180,9 @@ class CLIPVisionTransformer(nn.Module):
     out_index in ascending order, in x.dtype.  Runs on the HIP kernels only (x must be a
     GPU tensor).  The compute dtype of the GEMM/attention operands is bf16 for bf16 input,
     fp16 for fp16 input and `compute_dtype` (default bf16) for fp32 input; the residual
-    stream and LayerNorms are fp32 throughout.  `attn_fp8=True` (BASELINE config 5, inference
-    only) runs the attention core on the e4m3 MFMA kernel (dclip_attn_fwd_fp8); a backward
-    through it raises.
+    stream and LayerNorms are fp32 throughout.  `attn_fp8=True` (BASELINE config 5) runs the
+    attention forward on the e4m3 MFMA kernel (dclip_attn_fwd_fp8); its backward is the 16-bit
+    flash backward recomputing P against the fp8 forward's lse.
     """
 
     def __init__(self, input_resolution=224, patch_size=16, width=768, layers=12, heads=12, output_dim=768,

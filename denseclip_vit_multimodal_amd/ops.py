@@ -1,8 +1,9 @@
-"""Torch-facing wrappers of the HIP C ABI and the autograd Functions of the ViT path.
+"""Torch-facing wrappers of the dclip custom ops and the autograd Functions of the ViT path.
 
-Every op launches one or more kernels of libdclip.so on the current HIP stream of the
-current device; tensors are only plumbing (device memory + the caching allocator).
-There is no CPU fallback: a CPU tensor or a missing library raises.
+Every op is a torch.ops.dclip.* custom op (TORCH_LIBRARY in csrc/torch_ops.cpp over the C ABI
+of libdclip.so, fake implementations in _torch_ops.py) that launches one or more HIP kernels
+on the current stream of the current device; tensors are only plumbing (device memory + the
+caching allocator).  There is no CPU fallback: a CPU tensor or a missing library raises.
 
 Numerics (the contract checked by tests/test_gpu_parity.py):
   * the residual stream, LayerNorm statistics, bias/LN gradients and weight gradients are
@@ -82,58 +83,55 @@ def _check(*ts, strided=()):
 
 
 # ============================================================================ raw ops
-def layernorm_fwd(x2d, w, b, out_dtype, eps=1e-5, stats=True):
+# Each wrapper calls one torch.ops.dclip.* custom op (csrc/torch_ops.cpp, TORCH_LIBRARY over
+# the C ABI of include/dclip.h): outputs come from the caching allocator, the kernels run on
+# the current HIP stream.
+_D = None
+
+
+def D():
+    """torch.ops.dclip (loads libdclip_torch.so on first use; raises if it is missing)."""
+    global _D
+    if _D is None:
+        from . import _torch_ops
+        _D = _torch_ops.load()
+    return _D
+
+
+def layernorm_fwd(x2d, w, b, out_dtype, eps=1e-5):
+    """(y in out_dtype, mean, rstd) of LayerNorm over the last dim in fp32 (models.py:243-249)."""
     _check(x2d, w, b)
-    rows, cols = x2d.shape
-    y = torch.empty(rows, cols, dtype=out_dtype, device=x2d.device)
-    mean = torch.empty(rows, dtype=torch.float32, device=x2d.device) if stats else None
-    rstd = torch.empty(rows, dtype=torch.float32, device=x2d.device) if stats else None
-    N.call("dclip_layernorm_fwd", _p(x2d), _dt(x2d), _p(w), _p(b), _p(y), _DT[out_dtype], _p(mean), _p(rstd),
-           rows, cols, float(eps), _stream())
-    return y, mean, rstd
+    return D().layernorm_fwd(x2d, w, b, out_dtype, float(eps))
 
 
-def layernorm_bwd(dy, x, w, mean, rstd, dx, accumulate, dw=None, db=None, res=None, lp=None):
-    """dx (=, or += if accumulate) LN^T(dy); with res: dx = res + LN^T(dy) (accumulate ignored);
-    with lp: also lp = (lp.dtype) dx."""
-    _check(dy, x, w, mean, rstd, dx, dw, db, res, lp)
-    rows, cols = x.shape
-    if res is None and accumulate:
-        res = dx
-    N.call("dclip_layernorm_bwd_res", _p(dy), _dt(dy), _p(x), _dt(x), _p(w), _p(mean), _p(rstd), _p(res), _p(dx),
-           _p(lp), _dt(lp) if lp is not None else 0, _p(dw), _p(db), rows, cols, _stream())
+def layernorm_bwd(dy, x, w, mean, rstd, dw, db, res=None, lp_dtype=None):
+    """dx = res + LN^T(dy) (fp32; res optional); dw / db (fp32, zeroed by the caller) are
+    accumulated in place.  With lp_dtype also returns lp = (lp_dtype) dx, the next GEMM's operand."""
+    _check(dy, x, w, mean, rstd, dw, db, res)
+    if lp_dtype is None:
+        return D().layernorm_bwd(dy, x, w, mean, rstd, res, dw, db)
+    return D().layernorm_bwd_lp(dy, x, w, mean, rstd, res, dw, db, lp_dtype)
 
 
-def gemm(A, B, epi=N.EPI_STORE, bias=None, aux=None, out_dtype=None, out=None, out2=None, alpha=1.0):
-    """out[m][n] = alpha * sum_k A[m][k] B[n][k] (+ epilogue).  A: (M, K), B: (N, K)."""
-    _check(A, B, bias, aux, out, out2)
-    M, K = A.shape
-    Nn, K2 = B.shape
-    assert K == K2, (A.shape, B.shape)
-    if out is None:
-        odt = out_dtype or (torch.float32 if epi == N.EPI_RESIDUAL else A.dtype)
-        out = torch.empty(M, Nn, dtype=odt, device=A.device)
-    if epi == N.EPI_GELU and out2 is None:
-        out2 = torch.empty(M, Nn, dtype=A.dtype, device=A.device)
+def gemm(A, B, epi=N.EPI_STORE, bias=None, aux=None, out_dtype=None, alpha=1.0):
+    """out[m][n] = alpha * sum_k A[m][k] B[n][k] (+ epilogue).  A: (M, K), B: (N, K).
+    EPI_GELU returns (z, quick_gelu(z))."""
+    _check(A, B, bias, aux)
+    assert A.shape[1] == B.shape[1], (A.shape, B.shape)
     e0 = _tic()
-    N.call("dclip_gemm", epi, _dt(A), _p(A), A.stride(0), _p(B), B.stride(0), M, Nn, K, 1, float(alpha), _p(bias), _p(aux),
-           _dt(aux) if aux is not None else 0, aux.stride(0) if aux is not None else 0, _p(out), _dt(out),
-           out.stride(0), _p(out2), out2.stride(0) if out2 is not None else 0, _stream())
+    if epi == N.EPI_GELU:
+        out = D().gemm_gelu(A, B, bias)
+    else:
+        odt = out_dtype or (torch.float32 if epi == N.EPI_RESIDUAL else A.dtype)
+        out = D().gemm(A, B, epi, bias, aux, odt, float(alpha))
     _toc("gemm", e0)
-    return (out, out2) if epi == N.EPI_GELU else out
-
-
-def transpose(x, rows, cols, out_dtype, r0=0, batch=1, in_bstride=0, rows_pad=None, colsum=None, out=None,
-              accumulate=False):
-    """out[b][c][r] = x[b][r0 + r][c]  ->  (batch, cols, rows_pad) (2D if batch == 1 and out given 2D)."""
-    _check(x, colsum, out)
-    rows_pad = rows if rows_pad is None else rows_pad
-    if out is None:
-        out = torch.empty(batch, cols, rows_pad, dtype=out_dtype, device=x.device)
-    ld_in = x.shape[-1]
-    N.call("dclip_transpose", _p(x), _dt(x), in_bstride, ld_in, r0, _p(out), _dt(out), cols * rows_pad, rows_pad,
-           batch, rows, rows_pad, cols, int(accumulate), _p(colsum), _stream())
     return out
+
+
+def transpose2d(x, out_dtype):
+    """(rows, cols) -> (cols, rows) in out_dtype."""
+    _check(x)
+    return D().transpose2d(x, out_dtype)
 
 
 def cast(x, dtype, scale=1.0):
@@ -141,9 +139,7 @@ def cast(x, dtype, scale=1.0):
     _check(x)
     if x.dtype == dtype and scale == 1.0:
         return x
-    y = torch.empty(x.shape, dtype=dtype, device=x.device)
-    N.call("dclip_cast", _p(x), _dt(x), _p(y), _DT[dtype], x.numel(), float(scale), _stream())
-    return y
+    return D().cast(x, dtype, float(scale))
 
 
 FP16_GRAD_AMAX = 16.0
@@ -166,35 +162,20 @@ def grad_scale(g, cdt):
     return float(2.0 ** max(-60, min(60, e)))
 
 
-def _tn_plan(M, N, K):
-    """(splits, K_pad) for a TN GEMM with an M x N output over K rows (libdclip's heuristic)."""
-    import ctypes
-    sp = ctypes.c_int(0)
-    kp = ctypes.c_int64(0)
-    N_.call("dclip_gemm_tn_plan", M, N, K, ctypes.addressof(sp), ctypes.addressof(kp))
-    return sp.value, kp.value
-
-
 def weight_grad(dy, x, want_bias=True, alpha=1.0, db=None):
-    """dW = alpha dy^T x (N x K, fp32) and db = alpha colsum(dy) for dy (M, N), x (M, K)
+    """dW = alpha dy^T x (N x K, fp32) and db += alpha colsum(dy) for dy (M, N), x (M, K)
     (compute dtype).
 
     One "TN" MFMA GEMM reading both operands in their natural token-major layout (the
     reduction runs over the rows), split over the M tokens with a deterministic slab
     combine; no transposed copies."""
-    _check(dy, x)
-    M, Nn = dy.shape
-    K = x.shape[1]
-    splits, k_pad = _tn_plan(Nn, K, M)
+    _check(dy, x, db)
     if want_bias and db is None:  # db: a caller-zeroed (Nn,) f32 buffer, or allocated here
-        db = torch.zeros(Nn, dtype=torch.float32, device=dy.device)
+        db = torch.zeros(dy.shape[1], dtype=torch.float32, device=dy.device)
     elif not want_bias:
         db = None
-    dW = torch.empty(Nn, K, dtype=torch.float32, device=dy.device)
-    ws = torch.empty(splits, Nn, K, dtype=torch.float32, device=dy.device)
     e0 = _tic()
-    N.call("dclip_gemm_tn", N.EPI_SPLITK, _dt(dy), _p(dy), dy.stride(0), _p(x), x.stride(0), Nn, K, M, k_pad,
-           splits, float(alpha), None, _p(ws), _p(dW), K, _p(db), _stream())
+    dW = D().weight_grad(dy, x, float(alpha), db)
     _toc("gemm_wgrad", e0)
     return dW, db
 
@@ -202,12 +183,7 @@ def weight_grad(dy, x, want_bias=True, alpha=1.0, db=None):
 def gemm_tn(A, B):
     """out[m][n] = sum_k A[k][m] B[k][n] (f32)."""
     _check(A, B)
-    K, M = A.shape
-    Nn = B.shape[1]
-    out = torch.empty(M, Nn, dtype=torch.float32, device=A.device)
-    N.call("dclip_gemm_tn", N.EPI_STORE, _dt(A), _p(A), A.stride(0), _p(B), B.stride(0), M, Nn, K,
-           math.ceil(K / 64) * 64, 1, 1.0, None, None, _p(out), Nn, None, _stream())
-    return out
+    return D().gemm_tn(A, B)
 
 
 LOG2E = 1.4426950408889634
@@ -231,38 +207,26 @@ _QSCALE = {}
 def attn_fwd(qkv, B, Ntok, H, scale):
     """qkv with the q columns pre-multiplied by scale*log2(e) (qkv_scale_vector)."""
     _check(qkv)
-    C = qkv.shape[1] // 3
-    o = torch.empty(B * Ntok, C, dtype=qkv.dtype, device=qkv.device)
-    lse = torch.empty(B * H * Ntok, dtype=torch.float32, device=qkv.device)
     e0 = _tic()
-    N.call("dclip_attn_fwd", _dt(qkv), _p(qkv), _p(o), _p(lse), B, Ntok, H, C // H, float(scale), _stream())
+    o, lse = D().attn_fwd(qkv, B, Ntok, H, float(scale))
     _toc("attn_fwd", e0)
     return o, lse
 
 
 def attn_fwd_fp8(qkv, B, Ntok, H):
-    """fp8 (e4m3) attention forward, inference only (BASELINE config 5): the same qkv / o / lse
-    contract as attn_fwd, on the block-scaled fp8 MFMA (dclip_attn_fwd_fp8)."""
+    """fp8 (e4m3) attention forward (BASELINE config 5): the same qkv / o / lse contract as
+    attn_fwd, on the block-scaled fp8 MFMA (dclip_attn_fwd_fp8)."""
     _check(qkv)
-    C = qkv.shape[1] // 3
-    o = torch.empty(B * Ntok, C, dtype=qkv.dtype, device=qkv.device)
-    lse = torch.empty(B * H * Ntok, dtype=torch.float32, device=qkv.device)
-    ws = torch.empty(N.lib().dclip_attn_fwd_fp8_workspace(B, Ntok, H), dtype=torch.uint8, device=qkv.device)
     e0 = _tic()
-    N.call("dclip_attn_fwd_fp8", _dt(qkv), _p(qkv), _p(o), _p(lse), _p(ws), B, Ntok, H, C // H, _stream())
+    o, lse = D().attn_fwd_fp8(qkv, B, Ntok, H)
     _toc("attn_fwd_fp8", e0)
     return o, lse
 
 
 def attn_bwd(qkv, o, dout, lse, B, Ntok, H, scale):
     _check(qkv, o, dout, lse)
-    C = o.shape[1]
-    # delta (B*H*N) + the CLS-split row-0 partials (dclip_attn_bwd_workspace)
-    delta = torch.empty(N.lib().dclip_attn_bwd_workspace(B, Ntok, H), dtype=torch.float32, device=qkv.device)
-    dqkv = torch.empty_like(qkv)
     e0 = _tic()
-    N.call("dclip_attn_bwd", _dt(qkv), _p(qkv), _p(o), _p(dout), _p(lse), _p(delta), _p(dqkv), B, Ntok, H, C // H,
-           float(scale), _stream())
+    dqkv = D().attn_bwd(qkv, o, dout, lse, B, Ntok, H, float(scale))
     _toc("attn_bwd", e0)
     return dqkv
 
@@ -271,12 +235,7 @@ def im2col(img, p, out_dtype):
     """Patch rows (B*gh*gw, K_pad): K = Cin*p*p zero-padded to a multiple of 64 (the GEMM's K
     step; p = 14 gives 588 -> 640)."""
     _check(img)
-    B, Cin, Hin, Win = img.shape
-    gh, gw = Hin // p, Win // p
-    k_pad = -(-Cin * p * p // 64) * 64
-    out = torch.empty(B * gh * gw, k_pad, dtype=out_dtype, device=img.device)
-    N.call("dclip_im2col", _p(img), _dt(img), _p(out), _DT[out_dtype], k_pad, B, Cin, Hin, Win, p, _stream())
-    return out
+    return D().im2col(img, p, out_dtype)
 
 
 def _patch_weight(conv_w, cdt, k_pad):
@@ -290,84 +249,98 @@ def _patch_weight(conv_w, cdt, k_pad):
 
 def pos_interp(pos, g, H, W):
     _check(pos)
-    out = torch.empty(H * W + 1, pos.shape[1], dtype=torch.float32, device=pos.device)
-    N.call("dclip_pos_interp_fwd", _p(pos), _p(out), g, pos.shape[1], H, W, _stream())
-    return out
+    return D().pos_interp(pos, g, H, W)
 
 
-def pos_interp_bwd(dout, dpos, g, H, W):
-    _check(dout, dpos)
-    N.call("dclip_pos_interp_bwd", _p(dout), _p(dpos), g, dpos.shape[1], H, W, _stream())
+def pos_interp_bwd(dout, g, H, W):
+    _check(dout)
+    return D().pos_interp_bwd(dout, g, H, W)
 
 
 def channel_mean(x2d, B):
     _check(x2d)
-    rows = x2d.shape[0] // B
-    out = torch.empty(B, x2d.shape[1], dtype=torch.float32, device=x2d.device)
-    N.call("dclip_channel_mean", _p(x2d), _dt(x2d), _p(out), B, rows, x2d.shape[1], _stream())
-    return out
+    return D().channel_mean(x2d, B)
 
 
 def score_map(v2d, text, B, HW, eps=1e-12):
     """v2d: (B*HW, C) pixel embeddings; text (B, K, C) f32 -> (B, K, HW) f32."""
     text = text.float().contiguous()
     _check(v2d, text)
-    K, C = text.shape[1], text.shape[2]
-    out = torch.empty(B, K, HW, dtype=torch.float32, device=v2d.device)
-    N.call("dclip_score_map", _p(v2d), _dt(v2d), _p(text), _p(out), B, HW, C, K, float(eps), _stream())
-    return out
+    return D().score_map(v2d, text, B, HW, float(eps))
 
 
 def bilinear(x, Ho, Wo, out_dtype=torch.float32):
     _check(x)
-    n, c, Hi, Wi = x.shape
-    out = torch.empty(n, c, Ho, Wo, dtype=out_dtype, device=x.device)
-    N.call("dclip_bilinear_fwd", _p(x), _dt(x), _p(out), _DT[out_dtype], n * c, Hi, Wi, Ho, Wo, _stream())
-    return out
+    return D().bilinear(x, Ho, Wo, out_dtype)
 
 
 def bilinear_bwd(dout, Hi, Wi):
     dout = dout.contiguous()
     _check(dout)
-    n, c, Ho, Wo = dout.shape
-    din = torch.empty(n, c, Hi, Wi, dtype=torch.float32, device=dout.device)
-    ws = torch.empty(n * c * Ho * Wi, dtype=torch.float32, device=dout.device)
-    N.call("dclip_bilinear_bwd", _p(dout), _dt(dout), _p(din), _p(ws), n * c, Hi, Wi, Ho, Wo, _stream())
-    return din
+    return D().bilinear_bwd(dout, Hi, Wi)
 
 
 # ============================================================================ weight cache
-class _Cast:
-    """Per-parameter cache of the compute-dtype copy (and its transpose) of a master
-    fp32 weight; refreshed whenever the parameter's version counter moves."""
+# Every optimizer step (any torch.optim optimizer, fused or not) bumps this generation.  The
+# fused AdamW kernel updates parameters in place WITHOUT moving their version counters, so the
+# version alone cannot tell a cached compute-dtype copy that its master weight changed.
+_GENERATION = [0]
 
-    def __init__(self):
-        self._c = {}
+
+def _bump_generation(*_):
+    _GENERATION[0] += 1
+
+
+from torch.optim.optimizer import register_optimizer_step_post_hook  # noqa: E402
+
+register_optimizer_step_post_hook(_bump_generation)
+
+
+def invalidate_weight_cache():
+    """Force every cached compute-dtype weight copy to be rebuilt on next use (for code that
+    writes parameters through `.data` or outside torch.optim)."""
+    _bump_generation()
+
+
+class _Cast:
+    """Cache of the compute-dtype copy (and derived layouts) of fp32 master weights.
+
+    The entries live ON the parameter object (attribute `_dclip_cache`), so they die with it:
+    no entry outlives its parameter and no new parameter can inherit another's entry through
+    a recycled `id`.  An entry is valid while the parameter's version counter, storage
+    address and the optimizer-step generation are all unchanged."""
+
+    @staticmethod
+    def _lookup(p, key):
+        w = p.detach()
+        stamp = (_GENERATION[0], w._version, w.data_ptr())
+        cache = p.__dict__.get("_dclip_cache")
+        if cache is None:
+            cache = p.__dict__["_dclip_cache"] = {}
+        ent = cache.get(key)
+        if ent is not None and ent[0] == stamp:
+            return w, cache, stamp, ent[1]
+        return w, cache, stamp, None
 
     def get(self, p, dtype, transposed=False):
-        w = p.detach()
-        key = (id(p), dtype, transposed)
-        ent = self._c.get(key)
-        if ent is not None and ent[0] == w._version and ent[1] == w.data_ptr():
-            return ent[2]
+        w, cache, stamp, v = self._lookup(p, (dtype, transposed))
+        if v is not None:
+            return v
         w2 = w.reshape(w.shape[0], -1)
         if transposed:
-            v = transpose(w2.contiguous(), w2.shape[0], w2.shape[1], dtype).view(w2.shape[1], w2.shape[0])
+            v = transpose2d(w2.contiguous(), dtype)
         else:
             v = cast(w2.contiguous(), dtype)
-        self._c[key] = (w._version, w.data_ptr(), v)
+        cache[(dtype, transposed)] = (stamp, v)
         return v
-
 
     def get_with(self, p, dtype, tag, fn):
         """Cached fn(p) (a derived layout of parameter p in dtype), refreshed when p changes."""
-        w = p.detach()
-        key = (id(p), dtype, tag)
-        ent = self._c.get(key)
-        if ent is not None and ent[0] == w._version and ent[1] == w.data_ptr():
-            return ent[2]
+        w, cache, stamp, v = self._lookup(p, (dtype, tag))
+        if v is not None:
+            return v
         v = fn(w).to(dtype).contiguous()
-        self._c[key] = (w._version, w.data_ptr(), v)
+        cache[(dtype, tag)] = (stamp, v)
         return v
 
 
@@ -391,9 +364,7 @@ class PatchEmbedFn(torch.autograd.Function):
         posf = pos_interp(pos.detach().contiguous(), g, gh, gw) if interp else pos.detach().contiguous()
         patches = im2col(img.contiguous(), patch, cdt)
         emb = gemm(patches, _patch_weight(conv_w, cdt, patches.shape[1]), out_dtype=torch.float32)
-        x_pre = torch.empty(B * (P + 1), C, dtype=torch.float32, device=img.device)
-        N.call("dclip_tokens_fwd", _p(emb), N.F32, _p(cls.detach().float().contiguous()), _p(posf), _p(x_pre),
-               B, P, C, _stream())
+        x_pre = D().tokens_fwd(emb, cls.detach().float().contiguous(), posf, B, P)
         x, mean, rstd = layernorm_fwd(x_pre, ln_w.detach(), ln_b.detach(), torch.float32)
         ctx.save_for_backward(patches, x_pre, mean, rstd, ln_w)
         ctx.meta = (B, P, C, g, gh, gw, interp, cdt, tuple(conv_w.shape))
@@ -407,20 +378,12 @@ class PatchEmbedFn(torch.autograd.Function):
         need = ctx.needs_input_grad
         dlnw = torch.zeros(C, dtype=torch.float32, device=dx.device)
         dlnb = torch.zeros(C, dtype=torch.float32, device=dx.device)
-        dxp = torch.empty_like(x_pre)
-        layernorm_bwd(dx, x_pre, ln_w.detach(), mean, rstd, dxp, 0, dlnw, dlnb)
-        demb = torch.empty(B * P, C, dtype=cdt, device=dx.device)
-        dcls = torch.zeros(C, dtype=torch.float32, device=dx.device)
-        dposf = torch.zeros(P + 1, C, dtype=torch.float32, device=dx.device)
+        dxp = layernorm_bwd(dx, x_pre, ln_w.detach(), mean, rstd, dlnw, dlnb)
         s = grad_scale(dxp, cdt) if need[1] else 1.0
-        N.call("dclip_tokens_bwd", _p(dxp), _p(demb), _DT[cdt], float(s), _p(dcls), _p(dposf), B, P, C, _stream())
+        demb, dcls, dposf = D().tokens_bwd(dxp, cdt, float(s), B, P)
         dpos = None
         if need[3]:
-            if interp:
-                dpos = torch.zeros(g * g + 1, C, dtype=torch.float32, device=dx.device)
-                pos_interp_bwd(dposf, dpos, g, gh, gw)
-            else:
-                dpos = dposf
+            dpos = pos_interp_bwd(dposf, g, gh, gw) if interp else dposf
         dconv = None
         if need[1]:
             dW, _ = weight_grad(demb, patches, want_bias=False, alpha=1.0 / s)
@@ -471,9 +434,10 @@ class BlockFn(torch.autograd.Function):
     def backward(ctx, dxo, dmap=None):
         (x, mu1, rs1, xh1, qkv, o, lse, xm, mu2, rs2, xh2, z, h,
          ln1w, w_in, w_out, ln2w, w1, w2) = ctx.saved_tensors
+        # fp8 forward (BASELINE config 5): the backward is the bf16 / fp16 flash backward, P
+        # recomputed from the 16-bit q, k against the fp8 forward's own lse and delta taken from
+        # its o — the straight-through gradient of the quantised forward
         B, Ntok, H, cdt, fp8 = ctx.meta[:5]
-        if fp8:
-            raise RuntimeError("fp8 attention is forward-only (inference); train with attn_fp8=False")
         C = x.shape[1]
         scale = (C // H) ** -0.5
         need = ctx.needs_input_grad
@@ -493,11 +457,7 @@ class BlockFn(torch.autograd.Function):
             base = _readout_grad_buffer(dmap, B, Ntok, gh, gw, C)
             if base is not None and cdt == torch.bfloat16:
                 # one pass: dxo + map gradient (CLS rows masked) in fp32, and its bf16 copy
-                tot = torch.empty_like(dxo)
-                dy = torch.empty(dxo.shape, dtype=cdt, device=dxo.device)
-                N.call("dclip_add_readout_cast", _p(dxo), _p(base), _dt(base), _p(tot), _p(dy), _dt(dy),
-                       B * Ntok, C, Ntok, 1.0, _stream())
-                dxo = tot
+                dxo, dy = D().add_readout_cast(dxo, base, Ntok, cdt, 1.0)
             elif base is not None:
                 dr = base.float() if base.dtype != torch.float32 else base.clone()
                 dr.view(B, Ntok, C)[:, 0].zero_()
@@ -518,13 +478,11 @@ class BlockFn(torch.autograd.Function):
         if wg:
             dW1, db1 = weight_grad(dz, xh2, alpha=1.0 / s1, db=zb1)
         del dz
-        dxm = torch.empty_like(dxo)
         if cdt == torch.bfloat16:  # no gradient scaling: the attention branch's operand comes out of the LN pass
-            dyo = torch.empty(dxo.shape, dtype=cdt, device=dxo.device)
-            layernorm_bwd(dxh2, xm, ln2w.detach(), mu2, rs2, dxm, 0, dln2w, dln2b, res=dxo, lp=dyo)
+            dxm, dyo = layernorm_bwd(dxh2, xm, ln2w.detach(), mu2, rs2, dln2w, dln2b, res=dxo, lp_dtype=cdt)
             s2 = 1.0
         else:
-            layernorm_bwd(dxh2, xm, ln2w.detach(), mu2, rs2, dxm, 0, dln2w, dln2b, res=dxo)
+            dxm = layernorm_bwd(dxh2, xm, ln2w.detach(), mu2, rs2, dln2w, dln2b, res=dxo)
         del dxh2
         # ---- attention: xm = x + o Wout^T + bout
         if cdt != torch.bfloat16:
@@ -541,7 +499,7 @@ class BlockFn(torch.autograd.Function):
         if wg:
             dWi, dbi = weight_grad(dqkv, xh1, alpha=1.0 / s2, db=zbi)
         del dqkv
-        layernorm_bwd(dxh1, x, ln1w.detach(), mu1, rs1, dxm, 1, dln1w, dln1b)
+        dxm = layernorm_bwd(dxh1, x, ln1w.detach(), mu1, rs1, dln1w, dln1b, res=dxm)
         g = lambda i, t: t if need[i] else None  # noqa: E731
         return (dxm if need[0] else None, None, g(2, dln1w), g(3, dln1b), g(4, dWi), g(5, dbi), g(6, dWo),
                 g(7, dbo), g(8, dln2w), g(9, dln2b), g(10, dW1), g(11, db1), g(12, dW2), g(13, db2))
@@ -603,10 +561,9 @@ class ReadoutFn(torch.autograd.Function):
             dy = _readout_grad_dense(dmap, B, Ntok, gh, gw, C)
         if not ctx.has_ln:
             return dy, None, None, None
-        dx = torch.empty_like(dy)
         dw = torch.zeros(C, dtype=torch.float32, device=dy.device)
         db = torch.zeros(C, dtype=torch.float32, device=dy.device)
-        layernorm_bwd(dy, x, ln_w.detach(), mean, rstd, dx, 0, dw, db)
+        dx = layernorm_bwd(dy, x, ln_w.detach(), mean, rstd, dw, db)
         return dx, dw, db, None
 
 
@@ -628,17 +585,10 @@ class BatchNormFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps):
-        B, C, H, W = x.shape
-        rows = B * H * W
-        ws = torch.empty(N.lib().dclip_bn_workspace(rows, C), dtype=torch.float32, device=x.device)
-        mean = torch.empty(C, dtype=torch.float32, device=x.device)
-        rstd = torch.empty_like(mean)
-        y = torch.empty_like(x, memory_format=torch.channels_last)
         w = weight.detach() if weight is not None else None
         b = bias.detach() if bias is not None else None
         _check(w, b, running_mean, running_var, strided=(x,))
-        N.call("dclip_bn_fwd", _dt(x), _p(x), rows, C, _p(w), _p(b), float(eps), float(momentum),
-               _p(running_mean), _p(running_var), _p(ws), _p(mean), _p(rstd), _p(y), _stream())
+        y, mean, rstd = D().bn_fwd(x, w, b, running_mean, running_var, float(momentum), float(eps))
         ctx.save_for_backward(x, w, mean, rstd)
         ctx.has_w = (weight is not None, bias is not None)
         return y
@@ -646,16 +596,9 @@ class BatchNormFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w, mean, rstd = ctx.saved_tensors
-        B, C, H, W = x.shape
-        rows = B * H * W
         dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last)
-        ws = torch.empty(N.lib().dclip_bn_workspace(rows, C), dtype=torch.float32, device=x.device)
-        dx = torch.empty_like(x, memory_format=torch.channels_last)
-        dw = torch.empty(C, dtype=torch.float32, device=x.device) if ctx.has_w[0] else None
-        db = torch.empty(C, dtype=torch.float32, device=x.device) if ctx.has_w[1] else None
-        N.call("dclip_bn_bwd", _dt(x), _p(dy), _p(x), rows, C, _p(w), _p(mean), _p(rstd), _p(ws), _p(dx), _p(dw),
-               _p(db), _stream())
-        return dx, dw, db, None, None, None, None
+        dx, dw, db = D().bn_bwd(dy, x, w, mean, rstd, ctx.has_w[0], ctx.has_w[1])
+        return dx, dw if ctx.has_w[0] else None, db if ctx.has_w[1] else None, None, None, None, None
 
 
 class UpsampleFn(torch.autograd.Function):
@@ -706,8 +649,7 @@ def conv3x3_fwd(xmap, w_rows, cout_pad, cdt):
     xr, bs, ld = pixel_rows(xmap, cdt)
     _check(w_rows, strided=(xr,))
     out = torch.empty(B * H * W, cout_pad, dtype=cdt, device=xmap.device)
-    N.call("dclip_conv3x3", 0, _dt(w_rows), _p(xr), bs, 0, ld, B, H, W, Cin, _p(w_rows), cout_pad, _p(out), _dt(out),
-           cout_pad, 0, 0, 0, _stream())
+    D().conv3x3(0, xr, bs, 0, ld, B, H, W, Cin, w_rows, cout_pad, out, cout_pad, 0, 0, 0)
     return out, (xr, bs, ld)
 
 
@@ -759,24 +701,19 @@ class Conv3x3Fn(torch.autograd.Function):
                 # same layout as the input view: batches of bs elements, pixel rows after a gap
                 gap_rows = (bs - H * W * ld) // ld
                 buf = torch.zeros(B * bs, dtype=cdt, device=dy.device)
-                N.call("dclip_conv3x3", 1, _dt(w_t), _p(dyr), H * W * cp, 0, cp, B, H, W, cp, _p(w_t), Cin, _p(buf),
-                       _dt(buf), ld, gap_rows, gap_rows, 0, _stream())
+                D().conv3x3(1, dyr, H * W * cp, 0, cp, B, H, W, cp, w_t, Cin, buf, ld, gap_rows, gap_rows, 0)
                 dx = buf.as_strided((B, Cin, H, W), (bs, 1, W * ld, ld), gap_rows * ld)
             else:
                 buf = torch.empty(M, Cin, dtype=cdt, device=dy.device)
-                N.call("dclip_conv3x3", 1, _dt(w_t), _p(dyr), H * W * cp, 0, cp, B, H, W, cp, _p(w_t), Cin, _p(buf),
-                       _dt(buf), Cin, 0, 0, 0, _stream())
+                D().conv3x3(1, dyr, H * W * cp, 0, cp, B, H, W, cp, w_t, Cin, buf, Cin, 0, 0, 0)
                 dx = buf.as_strided((B, Cin, H, W), (H * W * Cin, 1, W * Cin, Cin))
             if in_dt != cdt:
                 dx = dx.to(in_dt)
         if ctx.needs_input_grad[1]:
             tiles = (cp + 127) // 128 * (9 * Cin // 128)
             splits = max(1, min(32, 512 // max(1, tiles), M // 4096 or 1))
-            ws = torch.empty(splits, cp, 9 * Cin, dtype=torch.float32, device=dy.device)
-            dwr = torch.empty(cp, 9 * Cin, dtype=torch.float32, device=dy.device)
             e0 = _tic()
-            N.call("dclip_conv3x3_wgrad", _dt(dyr), _p(dyr), cp, cp, _p(xr), bs, 0, ld, B, H, W, Cin, _p(dwr), _p(ws),
-                   splits, _stream())
+            dwr = D().conv3x3_wgrad(dyr, cp, cp, xr, bs, 0, ld, B, H, W, Cin, splits)
             _toc("conv_wgrad", e0)
             dw = dwr[:Cout].view(Cout, 3, 3, Cin).permute(0, 3, 1, 2).contiguous().to(weight.dtype)
         return dx, dw, None
@@ -848,17 +785,15 @@ class UpsampleCEFn(torch.autograd.Function):
         _check(lg, lab)
         if lab.dtype not in _LAB_DT:
             lab = lab.long()
-        sums = torch.zeros(1, dtype=torch.float64, device=lg.device)
-        cnt = torch.zeros(1, dtype=torch.int32, device=lg.device)
-        grad = torch.zeros(B, K, h, w, dtype=torch.float32, device=lg.device)
         e0 = _tic()
-        N.call("dclip_upsample_ce", _dt(lg), _p(lg), B, K, h, w, _p(lab), _LAB_DT[lab.dtype], H, W, int(ignore_index),
-               _p(sums), _p(cnt), _p(grad), _stream())
+        sums, cnt, grad = D().upsample_ce(lg, lab, int(ignore_index))
         _toc("upsample_ce", e0)
         n = cnt.to(torch.float64).clamp(min=1)
         ctx.save_for_backward(grad, n)
         ctx.in_dtype = logits.dtype
-        return (sums / n).to(torch.float32).reshape(())
+        # all labels ignored: NaN, like torch's CrossEntropyLoss (0 / 0); no host sync
+        mean = torch.where(cnt > 0, sums / n, torch.full_like(sums, float("nan")))
+        return mean.to(torch.float32).reshape(())
 
     @staticmethod
     def backward(ctx, g):
@@ -880,9 +815,7 @@ class UpsampleSILogFn(torch.autograd.Function):
         tg = target.detach().reshape(B, H, W).float().contiguous()
         mk = mask.reshape(B, H, W).to(torch.uint8).contiguous() if mask is not None else None
         _check(pd, tg, mk)
-        sums = torch.zeros(3, dtype=torch.float64, device=pd.device)
-        N.call("dclip_upsample_silog", 0, _dt(pd), _p(pd), B, h, w, _p(tg), _p(mk), H, W, float(eps), float(lambd),
-               _p(sums), None, _stream())
+        sums = D().upsample_silog_sums(pd, tg, mk, float(eps))
         T = sums[2].clamp(min=1)
         loss = sums[1] / T - lambd * sums[0] ** 2 / T ** 2
         loss = torch.where(sums[2] > 0, loss, torch.zeros_like(loss))
@@ -894,9 +827,5 @@ class UpsampleSILogFn(torch.autograd.Function):
     def backward(ctx, g):
         pd, tg, mk, sums = ctx.saved_tensors
         lambd, eps, in_dtype = ctx.args
-        B, _, h, w = pd.shape
-        H, W = tg.shape[-2:]
-        grad = torch.zeros(B, 1, h, w, dtype=torch.float32, device=pd.device)
-        N.call("dclip_upsample_silog", 1, _dt(pd), _p(pd), B, h, w, _p(tg), _p(mk), H, W, float(eps), float(lambd),
-               _p(sums), _p(grad), _stream())
+        grad = D().upsample_silog_grad(pd, tg, mk, sums, float(eps), float(lambd))
         return (grad * g.to(torch.float32)).to(in_dtype), None, None, None, None

@@ -19,14 +19,31 @@ import torch.nn.functional as F
 
 from .losses import SILogLoss
 
-# parameters that feed nothing differentiable in the ViT Cityscapes config: the unused
-# CLIP projection and the score-map branch, whose output is discarded (denseclip.py:747)
+# parameters that receive no gradient in the ViT Cityscapes config: the unused CLIP
+# projection and the score-map branch, whose output is discarded (denseclip.py:747).  They stay
+# trainable — the reference's AdamW param list holds them (train_denseclip.py:1040-1044, 1061),
+# so optimizer states interoperate — and are kept out of the DDP gradient reduction instead.
 _DEAD = ("backbone.proj", "contexts", "gamma")
 _DEAD_PREFIX = ("vis_proj.", "global_proj.")
 
 
+def _score_branch_live(model):
+    m = _unwrap(model)
+    return 0 <= getattr(m, "score_concat_index", -1) < len(getattr(m.backbone, "out_indices", []))
+
+
+def gradless_parameter_names(model):
+    """Trainable parameter names that get no gradient (DDP must not wait for them)."""
+    if _score_branch_live(model):
+        return []
+    return [n for n, p in _unwrap(model).named_parameters()
+            if p.requires_grad and (n in _DEAD or n.startswith(_DEAD_PREFIX))]
+
+
 def freeze_for_mode(model, mode):
-    """requires_grad per the reference freeze rule; returns the trainable parameters."""
+    """requires_grad per the reference freeze rule (train_denseclip.py:1040-1044: backbone.* and
+    text_encoder.* frozen; mode F also trains the backbone); returns the trainable parameters
+    in named_parameters order — the reference optimizer's param list."""
     if mode not in ("F", "R"):
         raise ValueError(f"mode must be 'F' or 'R' (got {mode!r})")
     params = []
@@ -34,8 +51,6 @@ def freeze_for_mode(model, mode):
         frozen = name.startswith("text_encoder.")
         if mode == "R":
             frozen = frozen or name.startswith("backbone.")
-        if name in _DEAD or name.startswith(_DEAD_PREFIX):
-            frozen = True
         p.requires_grad_(not frozen)
         if not frozen:
             params.append(p)
@@ -56,32 +71,63 @@ def synth_batch(B, H, W, device, rank=0, image_dtype=torch.bfloat16, num_classes
     return img, seg.to(device), depth.to(device), mask.to(device)
 
 
-def loss_fn(out, seg, depth, mask, silog=None):
-    """CE(ignore 255) + 0.1 * SILog (train_denseclip.py:1265-1314).  With a model in
+def loss_config(cfg):
+    """(seg weight, silog weight, SILogLoss) from a trainer YAML (train_denseclip.py:1088-1095,
+    1311-1312: training.loss_weights.{seg, silog}, training.silog_loss.{lambda, eps})."""
+    tr = (cfg or {}).get("training", {}) or {}
+    # the reference's defaults: the whole dict {'seg': 1.0, 'silog': 0.1} when absent, 1.0 for a
+    # key missing from a given dict (train_denseclip.py:1094-1095, 1311-1312)
+    w = tr.get("loss_weights", {"seg": 1.0, "silog": 0.1}) or {}
+    sl = tr.get("silog_loss", {}) or {}
+    return (float(w.get("seg", 1.0)), float(w.get("silog", 1.0)),
+            SILogLoss(lambd=float(sl.get("lambda", 0.5)), eps=float(sl.get("eps", 1e-6))))
+
+
+def loss_fn(out, seg, depth, mask, silog=None, seg_weight=1.0, silog_weight=0.1):
+    """seg_weight * CE(ignore 255) + silog_weight * SILog (train_denseclip.py:1265-1314; the
+    weights and the SILog parameters come from the config, `loss_config`).  With a model in
     fused_head_loss mode the outputs are the heads' low-res maps and the resize + loss run
-    as one fused kernel each (identical loss and gradients)."""
+    as one fused kernel each (identical loss and gradients).  A batch whose labels are all
+    ignored gives a NaN CE, as torch's CrossEntropyLoss does (the reference trainer then
+    skips the step, train_denseclip.py:1323)."""
     silog = silog or SILogLoss()
     if out.get("main_output_lowres") is not None:
         from . import ops
-        loss = ops.UpsampleCEFn.apply(out["main_output_lowres"], seg, 255)
+        loss = seg_weight * ops.UpsampleCEFn.apply(out["main_output_lowres"], seg, 255)
         if out.get("depth_output_lowres") is not None:
-            loss = loss + 0.1 * ops.UpsampleSILogFn.apply(out["depth_output_lowres"], depth, mask, silog.lambd,
-                                                          silog.eps)
+            loss = loss + silog_weight * ops.UpsampleSILogFn.apply(out["depth_output_lowres"], depth, mask,
+                                                                   silog.lambd, silog.eps)
         return loss
-    loss = F.cross_entropy(out["main_output"], seg, ignore_index=255)
+    loss = seg_weight * F.cross_entropy(out["main_output"], seg, ignore_index=255)
     if out.get("depth_output") is not None:
-        loss = loss + 0.1 * silog(out["depth_output"], depth, mask)
+        loss = loss + silog_weight * silog(out["depth_output"], depth, mask)
     return loss
 
 
-def wrap_ddp(model, device=None):
+def wrap_ddp(model, device=None, grad_dtype=None):
     """DDP over the default process group (RCCL on GPUs, gloo on CPU).  100 MB buckets:
     fewer, larger all-reduces suit xGMI's per-link ring bandwidth; the buckets are views of
-    the gradients (no copy)."""
+    the gradients (no copy).  Trainable parameters that get no gradient in this config
+    (`gradless_parameter_names`) are left out of the reduction rather than searched for every
+    step (find_unused_parameters).  grad_dtype=torch.bfloat16 all-reduces the buckets in bf16
+    (half the xGMI bytes; the sum is rounded to 8 mantissa bits) via DDP's compression hook."""
     from torch.nn.parallel import DistributedDataParallel as DDP
+    ignore = set(gradless_parameter_names(model))
+    if ignore:
+        # DDP matches both the named_parameters() name ("gamma") and f"{module_name}.{param_name}"
+        # (".gamma" for a top-level parameter) in different places: give both forms
+        fq = [f"{mn}.{pn}" for mn, mod in model.named_modules() for pn, _ in mod.named_parameters(recurse=False)
+              if (f"{mn}.{pn}" if mn else pn) in ignore]
+        DDP._set_params_and_buffers_to_ignore_for_model(model, sorted(ignore | set(fq)))
     ids = [device.index] if device is not None and device.type == "cuda" else None
-    return DDP(model, device_ids=ids, bucket_cap_mb=100, gradient_as_bucket_view=True,
-               find_unused_parameters=False)
+    ddp = DDP(model, device_ids=ids, bucket_cap_mb=100, gradient_as_bucket_view=True,
+              find_unused_parameters=False)
+    if grad_dtype == torch.bfloat16:
+        from torch.distributed.algorithms.ddp_comm_hooks import default_hooks
+        ddp.register_comm_hook(None, default_hooks.bf16_compress_hook)
+    elif grad_dtype not in (None, torch.float32):
+        raise ValueError(f"unsupported gradient all-reduce dtype {grad_dtype}")
+    return ddp
 
 
 def make_optimizer(params, fused=None):
@@ -90,12 +136,12 @@ def make_optimizer(params, fused=None):
     return torch.optim.AdamW(params, lr=2e-5, weight_decay=0.01, fused=fused)
 
 
-def train_step(model, opt, batch, silog=None):
+def train_step(model, opt, batch, silog=None, seg_weight=1.0, silog_weight=0.1):
     """One step: forward (DenseCLIP.forward train branch), loss, backward (DDP all-reduce
     overlapped with it), AdamW.  Returns the loss tensor (no host sync)."""
     img, seg, depth, mask = batch
     out = model(img, gt_semantic_seg=seg, gt_depth=depth, return_loss=True)
-    loss = loss_fn(out, seg, depth, mask, silog)
+    loss = loss_fn(out, seg, depth, mask, silog, seg_weight, silog_weight)
     opt.zero_grad(set_to_none=True)
     loss.backward()
     opt.step()

@@ -129,3 +129,79 @@ def test_checkpoint_roundtrip_reference_format(tmp_path):
     msg = load_weights(ddp_style, m3)
     assert not msg.missing_keys and not msg.unexpected_keys
     assert all(torch.equal(a, b) for a, b in zip(m.state_dict().values(), m3.state_dict().values()))
+
+
+def test_optimizer_param_list_matches_reference_rule(tmp_path):
+    """freeze_for_mode('R') keeps the reference's AdamW param list (train_denseclip.py:1040-1061:
+    every parameter but backbone.* / text_encoder.*, named_parameters order), so an optimizer
+    state saved with the reference's list resumes here and vice versa."""
+    from denseclip_vit_multimodal_amd import DenseCLIP
+    from denseclip_vit_multimodal_amd.train import freeze_for_mode, make_optimizer, save_checkpoint, resume
+    torch.manual_seed(0)
+    m = DenseCLIP(class_names=CITYSCAPES_CLASSES, **TINY_CFG)
+    ref_list = [p for n, p in m.named_parameters() if not n.startswith(("backbone.", "text_encoder."))]
+    ours = freeze_for_mode(m, "R")
+    assert len(ours) == len(ref_list) and all(a is b for a, b in zip(ours, ref_list))
+    names = [n for n, p in m.named_parameters() if p.requires_grad]
+    assert "contexts" in names and "gamma" in names and any(n.startswith("vis_proj.") for n in names)
+    # a reference-built optimizer (its own param list) saved, then resumed into ours
+    ref_opt = torch.optim.AdamW(ref_list, lr=2e-5, weight_decay=0.01)
+    for p in ref_list:
+        p.grad = torch.randn_like(p) * 1e-3
+    ref_opt.step()
+    path = str(tmp_path / "latest.pth")
+    save_checkpoint(path, m, ref_opt, epoch=0)
+    m2 = DenseCLIP(class_names=CITYSCAPES_CLASSES, **TINY_CFG)
+    opt2 = make_optimizer(freeze_for_mode(m2, "R"), fused=False)
+    assert resume(path, m2, opt2) == 1
+    s1, s2 = ref_opt.state_dict(), opt2.state_dict()
+    assert len(s1["param_groups"][0]["params"]) == len(s2["param_groups"][0]["params"])
+    for i in s1["state"]:
+        assert torch.equal(s1["state"][i]["exp_avg"], s2["state"][i]["exp_avg"])
+
+
+def test_ddp_ignores_gradless_parameters():
+    """The score-map parameters get no gradient in the Cityscapes config (denseclip.py:747):
+    they are trainable (reference param list) but left out of the DDP reduction."""
+    from denseclip_vit_multimodal_amd import DenseCLIP
+    from denseclip_vit_multimodal_amd.train import freeze_for_mode, gradless_parameter_names
+    m = DenseCLIP(class_names=CITYSCAPES_CLASSES, **TINY_CFG)
+    freeze_for_mode(m, "F")
+    ign = set(gradless_parameter_names(m))
+    assert {"contexts", "gamma", "backbone.proj", "vis_proj.weight", "global_proj.bias"} <= ign
+    assert not any(n.startswith(("neck.", "decode_head.", "backbone.transformer")) for n in ign)
+
+
+def test_weight_cache_follows_optimizer_steps():
+    """ADVICE r1: torch's fused AdamW updates parameters without moving their version counters;
+    the compute-dtype cache must still see every step (optimizer-step generation), and it
+    lives on the parameter (no id reuse across models)."""
+    from denseclip_vit_multimodal_amd import ops
+    p = torch.nn.Parameter(torch.randn(8, 4))
+    v1 = ops.WEIGHTS.get_with(p, torch.bfloat16, "t", lambda w: w * 1)
+    assert ops.WEIGHTS.get_with(p, torch.bfloat16, "t", lambda w: w * 1) is v1  # cached
+    for fused in (True, False):
+        opt = torch.optim.AdamW([p], lr=0.1, fused=fused)
+        p.grad = torch.ones_like(p)
+        opt.step()
+        v2 = ops.WEIGHTS.get_with(p, torch.bfloat16, "t", lambda w: w * 1)
+        assert torch.equal(v2, p.detach().to(torch.bfloat16)) and not torch.equal(v2, v1)
+        v1 = v2
+    q = torch.nn.Parameter(torch.randn(8, 4))
+    assert ops.WEIGHTS.get_with(q, torch.bfloat16, "t", lambda w: w * 1) is not v1
+
+
+def test_loss_config_follows_reference_defaults():
+    from denseclip_vit_multimodal_amd.train import loss_config
+    sw, lw, sl = loss_config({"training": {}})
+    assert (sw, lw, sl.lambd, sl.eps) == (1.0, 0.1, 0.5, 1e-6)
+    sw, lw, sl = loss_config({"training": {"loss_weights": {"seg": 2.0}, "silog_loss": {"lambda": 0.85}}})
+    assert (sw, lw, sl.lambd) == (2.0, 1.0, 0.85)
+
+
+def test_align_corners_true_is_refused():
+    from denseclip_vit_multimodal_amd import DenseCLIP
+    cfg = dict(TINY_CFG)
+    cfg["decode_head"] = dict(cfg["decode_head"], align_corners=True)
+    with pytest.raises(NotImplementedError):
+        DenseCLIP(class_names=CITYSCAPES_CLASSES, **cfg)

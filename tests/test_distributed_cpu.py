@@ -44,7 +44,8 @@ def _model():
     m = DenseCLIP(class_names=CITYSCAPES_CLASSES, **TINY_CFG)
     trainable = freeze_for_mode(m, "R")
     names = {n for n, p in m.named_parameters() if p.requires_grad}
-    assert names and all(n.startswith(("neck.", "decode_head.", "depth_head.")) for n in names)
+    # the reference rule (train_denseclip.py:1040-1044): everything but backbone.* / text_encoder.*
+    assert names == {n for n, _ in m.named_parameters() if not n.startswith(("backbone.", "text_encoder."))}
     assert len(trainable) == len(names)
     h = _HeadsOnly(m)
     h.eval()  # BN batch statistics are per-rank in the reference too; eval keeps the check exact
@@ -130,3 +131,26 @@ def test_rank_shards_are_distinct():
     seg = a[1]
     frac_ignore = float((seg == 255).float().mean())
     assert 0.05 < frac_ignore < 0.15 and int(seg[seg != 255].max()) < 19
+
+
+def test_wrap_ddp_leaves_gradless_parameters_out(tmp_path):
+    """wrap_ddp on the whole DenseCLIP (gloo, world size 1): the trainable parameters that get no
+    gradient in this config (score branch, unused CLIP projection; top-level ones included —
+    DDP names them '.gamma') are not in the reducer, everything else trainable is."""
+    import torch.distributed as dist
+    from denseclip_vit_multimodal_amd import DenseCLIP
+    from denseclip_vit_multimodal_amd.train import freeze_for_mode, gradless_parameter_names, wrap_ddp
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        m = DenseCLIP(class_names=CITYSCAPES_CLASSES, **TINY_CFG)
+        freeze_for_mode(m, "F")
+        dead = set(gradless_parameter_names(m))
+        assert {"gamma", "contexts", "backbone.proj"} <= dead
+        ddp = wrap_ddp(m)
+        managed = {id(p) for p in ddp._module_parameters}
+        for n, p in m.named_parameters():
+            assert (id(p) in managed) == (n not in dead), n
+    finally:
+        dist.destroy_process_group()

@@ -58,10 +58,9 @@ def test_layernorm_bwd(cols, dydt, acc, rows):
     ref.backward(dy.float())
     _, mu, rs = O.layernorm_fwd(x.detach(), w.detach(), b.detach(), torch.float32)
     prev = torch.randn(rows, cols, device=DEV)
-    dx = prev.clone()
     dw = torch.zeros(cols, device=DEV)
     db = torch.zeros(cols, device=DEV)
-    O.layernorm_bwd(dy, x.detach(), w.detach(), mu, rs, dx, acc, dw, db)
+    dx = O.layernorm_bwd(dy, x.detach(), w.detach(), mu, rs, dw, db, res=prev if acc else None)
     assert rel_err(dx - prev if acc else dx, x.grad) < 1e-5
     assert rel_err(dw, w.grad) < 1e-5
     assert rel_err(db, b.grad) < 1e-5
@@ -80,13 +79,22 @@ def test_layernorm_bwd_res(cols, lpdt):
     F.layer_norm(x, (cols,), w, None, 1e-5).backward(dy.float())
     _, mu, rs = O.layernorm_fwd(x.detach(), w, torch.zeros_like(w), torch.float32)
     res = torch.randn(rows, cols, device=DEV)
-    dx = torch.full((rows, cols), float("nan"), device=DEV)
-    lp = torch.empty(rows, cols, device=DEV, dtype=lpdt) if lpdt else None
     dw = torch.zeros(cols, device=DEV)
-    O.layernorm_bwd(dy, x.detach(), w, mu, rs, dx, 0, dw, None, res=res, lp=lp)
-    assert rel_err(dx, res + x.grad) < 1e-5
-    if lp is not None:
+    db = torch.zeros(cols, device=DEV)
+    if lpdt is None:
+        dx = O.layernorm_bwd(dy, x.detach(), w, mu, rs, dw, db, res=res)
+    else:
+        dx, lp = O.layernorm_bwd(dy, x.detach(), w, mu, rs, dw, db, res=res, lp_dtype=lpdt)
         assert torch.equal(lp, dx.to(lpdt))
+    assert rel_err(dx, res + x.grad) < 1e-5
+    # the C ABI also takes res aliasing dx (in place), as the op layer's callers once did
+    from denseclip_vit_multimodal_amd import _native as Nat
+    dx2 = res.clone()
+    Nat.call("dclip_layernorm_bwd_res", dy.data_ptr(), Nat.BF16, x.data_ptr(), Nat.F32, w.data_ptr(), mu.data_ptr(),
+             rs.data_ptr(), dx2.data_ptr(), dx2.data_ptr(), None, 0, dw.data_ptr(), None, rows, cols,
+             torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert rel_err(dx2, res + x.grad) < 1e-5
 
 
 # ----------------------------------------------------------------------------- GEMM
@@ -164,9 +172,12 @@ def test_gemm_gelu_and_residual(M, N, K, gemm_tile):
     res = torch.randn(M, N, device=DEV)
     out = O.gemm(A, B, Nat.EPI_RESIDUAL, bias=bias, aux=res)
     assert rel_err(out, res + zr) < 1e-5
-    # in place (aux aliases C)
+    # in place through the C ABI (aux aliases C)
     res2 = res.clone()
-    O.gemm(A, B, Nat.EPI_RESIDUAL, bias=bias, aux=res2, out=res2)
+    Nat.call("dclip_gemm", Nat.EPI_RESIDUAL, Nat.BF16, A.data_ptr(), K, B.data_ptr(), K, M, N, K, 1, 1.0,
+             bias.data_ptr(), res2.data_ptr(), Nat.F32, N, res2.data_ptr(), Nat.F32, N, None, 0,
+             torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
     assert rel_err(res2, res + zr) < 1e-5
     g = torch.randn(M, N, device=DEV).to(dt)
     Bt = torch.randn(N, N, device=DEV).to(dt)  # dh = g @ Bt^T
@@ -472,8 +483,7 @@ def test_pos_interp_fwd_bwd():
     assert rel_err(out, ref) < 1e-6
     gout = torch.randn_like(ref)
     ref.backward(gout)
-    dpos = torch.zeros_like(pos)
-    O.pos_interp_bwd(gout, dpos, g, H, W)
+    dpos = O.pos_interp_bwd(gout, g, H, W)
     assert rel_err(dpos, pos.grad) < 1e-5
 
 
@@ -491,10 +501,15 @@ def test_bilinear_fwd_bwd(hw, out):
 
 
 def test_transpose_colsum_pad():
+    """dclip_transpose through the C ABI (padded rows, fused column sums) and the 2-D op."""
+    from denseclip_vit_multimodal_amd import _native as Nat
     O = ops()
     x = torch.randn(300, 72, device=DEV).to(torch.bfloat16)
     cs = torch.zeros(72, device=DEV)
-    t = O.transpose(x, 300, 72, torch.bfloat16, rows_pad=384, colsum=cs).view(72, 384)
+    t = torch.empty(72, 384, dtype=torch.bfloat16, device=DEV)
+    Nat.call("dclip_transpose", x.data_ptr(), Nat.BF16, 0, 72, 0, t.data_ptr(), Nat.BF16, 72 * 384, 384, 1, 300, 384,
+             72, 0, cs.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    assert torch.equal(O.transpose2d(x, torch.bfloat16), x.t())
     assert torch.equal(t[:, :300], x.t())
     assert torch.count_nonzero(t[:, 300:]) == 0
     assert rel_err(cs, x.float().sum(0)) < 1e-6
@@ -583,6 +598,8 @@ def test_add_readout_cast(bdt, rows, cols, ntok):
     b = torch.randn(rows, cols, device=DEV).to(bdt)
     keep = (torch.arange(rows, device=DEV) % ntok != 0)[:, None]
     ref = torch.where(keep, a + b.float(), a)
+    sm, lp = O.D().add_readout_cast(a, b, ntok, torch.bfloat16, 1.0)  # the torch op
+    assert torch.equal(sm, ref) and torch.equal(lp, ref.to(torch.bfloat16))
     for inplace in (False, True):
         x = a.clone()
         out = x if inplace else torch.empty_like(a)

@@ -1,0 +1,123 @@
+"""torch.ops.dclip.* on the GPU: torch.library.opcheck (schema / mutation annotations, fake vs
+real shapes and strides, AOT dispatch with dynamic shapes) on the ViT block's ops, and a whole
+ViT block (forward and backward) captured in a HIP graph with torch.cuda.graph and replayed."""
+import pytest
+import torch
+
+from helpers import rel_err
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True)
+def _need(hip):
+    torch.manual_seed(0)
+
+
+def D():
+    from denseclip_vit_multimodal_amd import ops
+    return ops.D()
+
+
+def _opcheck(op, args):
+    torch.library.opcheck(op, args, test_utils=("test_schema", "test_faketensor", "test_aot_dispatch_dynamic"))
+
+
+def test_opcheck_layernorm():
+    x = torch.randn(300, 768, device=DEV)
+    w = torch.randn(768, device=DEV)
+    b = torch.randn(768, device=DEV)
+    _opcheck(D().layernorm_fwd, (x, w, b, torch.bfloat16, 1e-5))
+    _, mu, rs = D().layernorm_fwd(x, w, b, torch.float32, 1e-5)
+    dy = torch.randn(300, 768, device=DEV).to(torch.bfloat16)
+    _opcheck(D().layernorm_bwd, (dy, x, w, mu, rs, None, torch.zeros(768, device=DEV), torch.zeros(768, device=DEV)))
+    _opcheck(D().layernorm_bwd_lp, (dy, x, w, mu, rs, x.clone(), torch.zeros(768, device=DEV),
+                                    torch.zeros(768, device=DEV), torch.bfloat16))
+
+
+def test_opcheck_gemm_family():
+    A = torch.randn(520, 768, device=DEV).to(torch.bfloat16)
+    B = torch.randn(256, 768, device=DEV).to(torch.bfloat16)
+    bias = torch.randn(256, device=DEV)
+    _opcheck(D().gemm, (A, B, 0, bias, None, torch.float32, 1.0))
+    _opcheck(D().gemm, (A, B, 2, bias, torch.randn(520, 256, device=DEV), torch.float32, 1.0))
+    _opcheck(D().gemm_gelu, (A, B, bias))
+    dy = torch.randn(520, 256, device=DEV).to(torch.bfloat16)
+    _opcheck(D().weight_grad, (dy, A, 1.0, torch.zeros(256, device=DEV)))
+    _opcheck(D().cast, (torch.randn(77, 64, device=DEV), torch.bfloat16, 4.0))
+    _opcheck(D().transpose2d, (torch.randn(72, 136, device=DEV), torch.bfloat16))
+
+
+def test_opcheck_attention():
+    from test_gpu_kernels import prescale
+    B, N, H = 2, 257, 2
+    qkv, _ = prescale(torch.randn(B * N, 3 * 64 * H, device=DEV).to(torch.bfloat16), H)
+    _opcheck(D().attn_fwd, (qkv, B, N, H, 0.125))
+    o, lse = D().attn_fwd(qkv, B, N, H, 0.125)
+    _opcheck(D().attn_bwd, (qkv, o, torch.randn_like(o), lse, B, N, H, 0.125))
+    _opcheck(D().attn_fwd_fp8, (qkv, B, N, H))
+
+
+def test_opcheck_resize_and_bn():
+    x = torch.randn(2, 19, 8, 16, device=DEV)
+    _opcheck(D().bilinear, (x, 64, 128, torch.float32))
+    _opcheck(D().bilinear_bwd, (torch.randn(2, 19, 64, 128, device=DEV), 8, 16))
+    m = torch.randn(2, 128, 6, 10, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    _opcheck(D().bn_fwd, (m, torch.rand(128, device=DEV), torch.randn(128, device=DEV), torch.zeros(128, device=DEV),
+                          torch.ones(128, device=DEV), 0.1, 1e-5))
+
+
+def _block(C=768, H=12):
+    from denseclip_vit_multimodal_amd.models import ResidualAttentionBlock
+    blk = ResidualAttentionBlock(C, H).to(DEV)
+    with torch.no_grad():
+        for p in blk.parameters():
+            if p.dim() > 1:
+                p.normal_(0, C ** -0.5)
+            else:
+                p.normal_(0, 0.1)
+    return blk
+
+
+def test_vit_block_hip_graph_capture_fwd_bwd():
+    """One ViT-B block (B = 2, N = 1025, bf16 operands) forward + backward captured with
+    torch.cuda.graph: the replay reproduces the eager output and input gradient bit for bit, the
+    parameter gradients to fp32 atomic-order noise (the ops are stream-ordered and never
+    synchronise with the host)."""
+    from denseclip_vit_multimodal_amd import ops
+    blk = _block()
+    B, N, H, C = 2, 1025, 12, 768
+    meta = (B, N, H, torch.bfloat16, False)
+    x = torch.randn(B * N, C, device=DEV).requires_grad_(True)
+    gy = torch.randn(B * N, C, device=DEV)
+
+    def step():
+        y = ops.BlockFn.apply(x, meta, *blk.hip_params())
+        y.backward(gy)
+        return y
+
+    # eager reference (and warm-up: allocator, cached weight casts) on a side stream
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            x.grad = None
+            blk.zero_grad(set_to_none=True)
+            y_ref = step().detach().clone()
+    torch.cuda.current_stream().wait_stream(s)
+    gx_ref = x.grad.clone()
+    gw_ref = {n: p.grad.clone() for n, p in blk.named_parameters() if p.grad is not None}
+    x.grad = None
+    blk.zero_grad(set_to_none=True)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        y_static = step()
+    for _ in range(2):  # grads are graph outputs (re-written, not accumulated, by each replay)
+        g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(y_static, y_ref)
+    assert torch.equal(x.grad, gx_ref)
+    for n, p in blk.named_parameters():
+        if n in gw_ref:  # LayerNorm weight / bias gradients are summed with float atomics (order varies)
+            assert rel_err(p.grad, gw_ref[n]) < 1e-5, (n, rel_err(p.grad, gw_ref[n]))
