@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("DCLIP_LIB", os.path.join(_HERE, "libdclip.so"))
 F32, F16, BF16 = 0, 1, 2
 EPI_STORE, EPI_GELU, EPI_RESIDUAL, EPI_GELU_BWD, EPI_SPLITK, EPI_STORE_SCALED = 0, 1, 2, 3, 4, 5
 OPT_ATTN_FWD_WAVES, OPT_ATTN_DQ_WAVES, OPT_ATTN_DKDV_WAVES, OPT_GEMM_TILE, OPT_GEMM_TN_TILE = 0, 1, 2, 3, 4
-OPT_ATTN_DKDV_QS, OPT_ATTN_FWD_KERNEL, OPT_ATTN_BWD_KERNEL = 5, 6, 7
+OPT_ATTN_DKDV_QS, OPT_ATTN_FWD_KERNEL, OPT_ATTN_BWD_KERNEL, OPT_ATTN_BWD_BLOCK = 5, 6, 7, 8
 
 _c_void_p = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -43,8 +43,10 @@ _SIGS = {
     "dclip_pos_interp_bwd": [_c_void_p, _c_void_p, _i32, _i32, _i32, _i32, _c_void_p],
     "dclip_transpose": [_c_void_p, _i32, _i64, _i64, _i64, _c_void_p, _i32, _i64, _i64, _i32, _i64, _i64, _i64,
                         _i32, _c_void_p, _c_void_p],
-    "dclip_channel_mean": [_c_void_p, _i32, _c_void_p, _i32, _i64, _i32, _c_void_p],
-    "dclip_score_map": [_c_void_p, _i32, _c_void_p, _c_void_p, _i32, _i32, _i32, _i32, _f32, _c_void_p],
+    "dclip_row_mean_workspace": [_i32, _i64, _i32],
+    "dclip_row_mean": [_c_void_p, _i32, _i64, _i64, _i64, _i32, _i64, _i32, _c_void_p, _c_void_p, _c_void_p],
+    "dclip_score_map": [_c_void_p, _i32, _i64, _i64, _i64, _c_void_p, _c_void_p, _i32, _i32, _i32, _i32, _f32,
+                        _c_void_p],
     "dclip_bilinear_fwd": [_c_void_p, _i32, _c_void_p, _i32, _i64, _i32, _i32, _i32, _i32, _c_void_p],
     "dclip_bilinear_bwd": [_c_void_p, _i32, _c_void_p, _c_void_p, _i64, _i32, _i32, _i32, _i32, _c_void_p],
     "dclip_cast": [_c_void_p, _i32, _c_void_p, _i32, _i64, _f32, _c_void_p],
@@ -105,6 +107,7 @@ def load(path=None):
         lib.dclip_attn_bwd_workspace.restype = ctypes.c_int64  # a size, not a status
         lib.dclip_bn_workspace.restype = ctypes.c_int64
         lib.dclip_attn_fwd_fp8_workspace.restype = ctypes.c_int64
+        lib.dclip_row_mean_workspace.restype = ctypes.c_int64
         # kernel-variant knobs for A/B runs: DCLIP_OPTIONS="id=value,..." (DCLIP_OPT_* ids of dclip.h)
         for kv in filter(None, os.environ.get("DCLIP_OPTIONS", "").split(",")):
             k, v = kv.split("=")

@@ -114,12 +114,12 @@ def _register_fakes():
     def _(dout, g, H, W):
         return _e(g * g + 1, dout.shape[1], like=dout)
 
-    @reg("dclip::channel_mean")
-    def _(x, B):
-        return _e(B, x.shape[1], like=x, dtype=f32)
+    @reg("dclip::row_mean")
+    def _(x, bstride, row_off, ld, B, rows, C):
+        return _e(B, C, like=x, dtype=f32)
 
     @reg("dclip::score_map")
-    def _(v, text, B, HW, eps):
+    def _(v, bstride, row_off, ld, text, B, HW, eps):
         return _e(B, text.shape[1], HW, like=v, dtype=f32)
 
     @reg("dclip::bilinear")

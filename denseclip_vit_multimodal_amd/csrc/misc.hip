@@ -272,60 +272,116 @@ __global__ __launch_bounds__(256) void transpose_kernel(const TI* __restrict__ i
     }
 }
 
-// ---------------------------------------------------------------------------- channel mean
+// ---------------------------------------------------------------------------- row mean
+// F.adaptive_avg_pool2d(x, 1) of a pixel-row map (denseclip.py:596) read in place from a strided
+// row layout (the ViT token buffer: batch stride N*C, row offset 1 skips CLS).  Stage 1: one
+// workgroup per (image, chunk of rows) streams its rows with 16-byte loads (a 768-channel row =
+// 96 lanes, 256 / 96 rows in flight per pass) and writes the chunk's column sums; stage 2 sums
+// the chunks in a fixed order (deterministic) and divides.
+constexpr int RM_CHUNK = 64;  // rows per workgroup
+
 template <typename TI>
-__global__ __launch_bounds__(256) void channel_mean_kernel(const TI* __restrict__ in, float* __restrict__ out,
-                                                           int64_t rows, int C) {
-    __shared__ float red[4][64];
-    const int b = blockIdx.y;
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int ty = threadIdx.x >> 6;
+__global__ __launch_bounds__(256) void row_mean_part_kernel(const TI* __restrict__ x, int64_t bstride, int64_t row_off,
+                                                            int64_t ld, int64_t rows, int C, float* __restrict__ ws) {
+    __shared__ float red[2048 / 8 * 8];
+    const int b = blockIdx.y, ch = blockIdx.x, S = gridDim.x;
+    const int nc8 = C / 8, nrp = 256 / nc8;
+    const int t = threadIdx.x, cc = t % nc8, rp = t / nc8;
+    const int64_t r0 = (int64_t)ch * RM_CHUNK;
+    const int64_t r1 = r0 + RM_CHUNK < rows ? r0 + RM_CHUNK : rows;
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (rp < nrp) {
+        const TI* base = x + (int64_t)b * bstride + row_off * ld + cc * 8;
+#pragma unroll 4
+        for (int64_t r = r0 + rp; r < r1; r += nrp) {
+            typedef TI t8 __attribute__((ext_vector_type(8)));
+            const t8 v = *(const t8*)(base + r * ld);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a[e] += (float)v[e];
+        }
+    }
+    // reduce the nrp row phases of each column chunk through LDS (phase 0 keeps, the others add)
+    for (int p = 1; p < nrp; ++p) {
+        if (rp == p)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) red[cc * 8 + e] = a[e];
+        __syncthreads();
+        if (rp == 0)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a[e] += red[cc * 8 + e];
+        __syncthreads();
+    }
+    if (rp == 0) {
+        float* o = ws + ((int64_t)b * S + ch) * C + cc * 8;
+        *(f32x4*)o = f32x4{a[0], a[1], a[2], a[3]};
+        *(f32x4*)(o + 4) = f32x4{a[4], a[5], a[6], a[7]};
+    }
+}
+
+__global__ __launch_bounds__(256) void row_mean_final_kernel(const float* __restrict__ ws, int S, int C, int64_t rows,
+                                                             int B, float* __restrict__ out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= B * C) return;
+    const int b = i / C, c = i % C;
     float s = 0.f;
-    if (c < C)
-        for (int64_t r = ty; r < rows; r += 4) s += (float)in[((int64_t)b * rows + r) * C + c];
-    red[ty][threadIdx.x & 63] = s;
-    __syncthreads();
-    if (ty == 0 && c < C) out[(int64_t)b * C + c] = (red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
-                                                     red[3][threadIdx.x]) / (float)rows;
+    for (int k = 0; k < S; ++k) s += ws[((int64_t)b * S + k) * C + c];
+    out[i] = s / (float)rows;
 }
 
 // ---------------------------------------------------------------------------- score map
-// one wave per pixel; text rows normalised once per block into LDS
+// s[b][k][p] = <v_p / max(|v_p|, eps), t_k / max(|t_k|, eps)> (F.normalize x2 + einsum
+// 'bchw,bkc->bkhw', denseclip.py:672-675) as a batched [K x C] . [C x 32-pixel] MFMA product:
+// A = the normalised class embeddings (K <= 32 rows, 16-bit, LDS, rows padded by 16 B so the
+// row-fragment reads are bank-conflict free), B = 32 pixel rows of v read in place (strided rows:
+// the vis_proj GEMM's output over the token buffer, CLS rows skipped), D[class][pixel] with the
+// pixel on the lane, so the pixel norm (accumulated from the same B fragments) is lane-local.
 template <typename TV>
-__global__ __launch_bounds__(256) void score_map_kernel(const TV* __restrict__ v, const float* __restrict__ t,
+__global__ __launch_bounds__(256) void score_map_kernel(const TV* __restrict__ v, int64_t bstride, int64_t row_off,
+                                                        int64_t ld, const float* __restrict__ t,
                                                         float* __restrict__ score, int HW, int C, int K, float eps) {
-    extern __shared__ float tn[];  // K * C
+    typedef typename Mfma<TV>::frag frag;
+    extern __shared__ __attribute__((aligned(16))) char smem[];  // [32][C + 8] TV
+    TV* tn = (TV*)smem;
+    const int pitch = C + 8;
     const int b = blockIdx.y;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // normalise text embeddings of batch b (F.normalize, p=2, dim=2, eps)
-    for (int k = wave; k < K; k += 4) {
-        const float* tr = t + ((int64_t)b * K + k) * C;
-        float ss = 0.f;
-        for (int c = lane; c < C; c += 64) ss += tr[c] * tr[c];
-        ss = wave_sum(ss);
-        const float inv = 1.f / fmaxf(sqrtf(ss), eps);
-        for (int c = lane; c < C; c += 64) tn[k * C + c] = tr[c] * inv;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l32 = lane & 31, h = lane >> 5;
+    for (int k = wave; k < 32; k += 4) {
+        if (k < K) {
+            const float* tr = t + ((int64_t)b * K + k) * C;
+            float ss = 0.f;
+            for (int c = lane; c < C; c += 64) ss += tr[c] * tr[c];
+            const float inv = 1.f / fmaxf(sqrtf(wave_sum(ss)), eps);
+            for (int c = lane; c < C; c += 64) tn[k * pitch + c] = (TV)(tr[c] * inv);
+        } else {
+            for (int c = lane; c < C; c += 64) tn[k * pitch + c] = (TV)0.f;
+        }
     }
     __syncthreads();
-    for (int p = blockIdx.x * 4 + wave; p < HW; p += gridDim.x * 4) {
-        const TV* vr = v + ((int64_t)b * HW + p) * C;
+    const int nsteps = C / 16;
+    for (int p0 = (blockIdx.x * 4 + wave) * 32; p0 < HW; p0 += gridDim.x * 128) {
+        const int p = p0 + l32;
+        const int pc = p < HW ? p : HW - 1;
+        const TV* row = v + (int64_t)b * bstride + (row_off + pc) * ld + 8 * h;
+        const TV* arow = tn + l32 * pitch + 8 * h;
+        f32x16 acc;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[e] = 0.f;
         float ss = 0.f;
-        float dots[32];
+#pragma unroll 8
+        for (int s = 0; s < nsteps; ++s) {
+            const frag bf = *(const frag*)(row + 16 * s);
+            const frag af = *(const frag*)(arow + 16 * s);
 #pragma unroll
-        for (int k = 0; k < 32; ++k) dots[k] = 0.f;
-        for (int c = lane; c < C; c += 64) {
-            const float x = (float)vr[c];
-            ss += x * x;
-#pragma unroll
-            for (int k = 0; k < 32; ++k)
-                if (k < K) dots[k] += x * tn[k * C + c];
+            for (int j = 0; j < 8; ++j) ss += (float)bf[j] * (float)bf[j];
+            acc = Mfma<TV>::mma(af, bf, acc);
         }
-        const float inv = 1.f / fmaxf(sqrtf(wave_sum(ss)), eps);
+        ss += __shfl_xor(ss, 32, 64);  // the other half-wave holds the pixel's other 8-column chunks
+        const float inv = 1.f / fmaxf(sqrtf(ss), eps);
+        if (p < HW) {
 #pragma unroll
-        for (int k = 0; k < 32; ++k) {
-            if (k < K) {
-                const float d = wave_sum(dots[k]);
-                if (lane == 0) score[((int64_t)b * K + k) * HW + p] = d * inv;
+            for (int r = 0; r < 16; ++r) {
+                const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (k < K) score[((int64_t)b * K + k) * HW + p] = acc[r] * inv;
             }
         }
     }
@@ -447,25 +503,44 @@ extern "C" int dclip_transpose(const void* in, int in_dt, int64_t in_bstride, in
     return 0;
 }
 
-extern "C" int dclip_channel_mean(const void* in, int in_dt, float* out, int B, int64_t rows, int C, void* stream) {
-    DCLIP_HOST_CHECK(rows > 0 && C > 0 && B > 0, "dclip_channel_mean: empty input");
-    dim3 grid((C + 63) / 64, B);
+extern "C" int64_t dclip_row_mean_workspace(int B, int64_t rows, int C) {
+    return (int64_t)B * ((rows + RM_CHUNK - 1) / RM_CHUNK) * C;
+}
+
+extern "C" int dclip_row_mean(const void* x, int x_dt, int64_t bstride, int64_t row_off, int64_t ld, int B, int64_t rows,
+                              int C, float* ws, float* out, void* stream) {
+    DCLIP_HOST_CHECK(rows > 0 && C > 0 && B > 0, "dclip_row_mean: empty input");
+    DCLIP_HOST_CHECK(x_dt != DCLIP_F32, "dclip_row_mean: 16-bit input");
+    DCLIP_HOST_CHECK(C % 8 == 0 && C <= 2048 && ld % 8 == 0 && bstride % 8 == 0 && ((uintptr_t)x % 16) == 0,
+                     "dclip_row_mean: C %% 8 == 0, C <= 2048, 16-byte aligned rows");
+    const int S = (int)((rows + RM_CHUNK - 1) / RM_CHUNK);
     hipStream_t st = (hipStream_t)stream;
-    DISPATCH_DT(in_dt, TI, channel_mean_kernel<TI><<<grid, 256, 0, st>>>((const TI*)in, out, rows, C));
+    if (x_dt == DCLIP_BF16)
+        row_mean_part_kernel<bf16><<<dim3(S, B), 256, 0, st>>>((const bf16*)x, bstride, row_off, ld, rows, C, ws);
+    else
+        row_mean_part_kernel<f16><<<dim3(S, B), 256, 0, st>>>((const f16*)x, bstride, row_off, ld, rows, C, ws);
+    row_mean_final_kernel<<<(B * C + 255) / 256, 256, 0, st>>>(ws, S, C, rows, B, out);
     DCLIP_LAUNCH_CHECK();
     return 0;
 }
 
-extern "C" int dclip_score_map(const void* v, int v_dt, const float* t, float* score, int B, int HW, int C, int K,
-                               float eps, void* stream) {
+extern "C" int dclip_score_map(const void* v, int v_dt, int64_t bstride, int64_t row_off, int64_t ld, const float* t,
+                               float* score, int B, int HW, int C, int K, float eps, void* stream) {
     DCLIP_HOST_CHECK(K > 0 && K <= 32, "dclip_score_map: K must be in [1, 32] (got %d)", K);
-    DCLIP_HOST_CHECK((size_t)K * C * 4 <= 64 * 1024, "dclip_score_map: K*C too large for LDS");
-    int bx = (HW + 3) / 4;
-    if (bx > 1024) bx = 1024;
-    dim3 grid(bx, B);
+    DCLIP_HOST_CHECK(v_dt == DCLIP_BF16 || v_dt == DCLIP_F16, "dclip_score_map: v must be f16/bf16");
+    DCLIP_HOST_CHECK(C % 16 == 0 && C <= 2048 && ld % 8 == 0 && bstride % 8 == 0 && ((uintptr_t)v % 16) == 0,
+                     "dclip_score_map: C %% 16 == 0, C <= 2048, 16-byte aligned rows");
+    DCLIP_HOST_CHECK(B > 0 && HW > 0, "dclip_score_map: empty input");
+    int bx = (HW + 127) / 128;
+    if (bx > 256) bx = 256;
+    const size_t lds = (size_t)32 * (C + 8) * 2;
     hipStream_t st = (hipStream_t)stream;
-    DISPATCH_DT(v_dt, TV,
-        score_map_kernel<TV><<<grid, 256, (size_t)K * C * 4, st>>>((const TV*)v, t, score, HW, C, K, eps));
+    if (v_dt == DCLIP_BF16)
+        score_map_kernel<bf16><<<dim3(bx, B), 256, lds, st>>>((const bf16*)v, bstride, row_off, ld, t, score, HW, C, K,
+                                                              eps);
+    else
+        score_map_kernel<f16><<<dim3(bx, B), 256, lds, st>>>((const f16*)v, bstride, row_off, ld, t, score, HW, C, K,
+                                                             eps);
     DCLIP_LAUNCH_CHECK();
     return 0;
 }

@@ -300,24 +300,34 @@ Tensor pos_interp_bwd(const Tensor& dout, int64_t g, int64_t H, int64_t W) {
 }
 
 // ----------------------------------------------------------------------------- score map / resize
-Tensor channel_mean(const Tensor& x, int64_t B) {
-    check_gpu(x, "x");
-    TORCH_CHECK(x.dim() == 2 && x.size(0) % B == 0, "channel_mean: x (B*rows, C)");
+// strided pixel rows (dclip.h): row r of image b at x + b*bstride + (row_off + r)*ld (elements)
+void check_rows(const Tensor& x, int64_t bstride, int64_t row_off, int64_t ld, int64_t B, int64_t rows, int64_t C) {
+    TORCH_CHECK(x.is_cuda() && x.stride(-1) == 1, "dclip: pixel rows must be a GPU tensor with unit column stride");
+    const int64_t last = (B - 1) * bstride + (row_off + rows - 1) * ld + C;  // one past the last element read
+    TORCH_CHECK(x.storage_offset() + last <= (int64_t)(x.storage().nbytes() / x.element_size()),
+                "dclip: the strided rows run past the tensor's storage");
+}
+
+Tensor row_mean(const Tensor& x, int64_t bstride, int64_t row_off, int64_t ld, int64_t B, int64_t rows, int64_t C) {
+    check_rows(x, bstride, row_off, ld, B, rows, C);
     c10::DeviceGuard g(x.device());
-    Tensor out = at::empty({B, x.size(1)}, like(x, at::kFloat));
-    DCLIP_CALL(dclip_channel_mean(x.data_ptr(), dt_code(x.scalar_type()), ptr<float>(out), (int)B, x.size(0) / B,
-                                  (int)x.size(1), stream_of(x)));
+    Tensor ws = at::empty({dclip_row_mean_workspace((int)B, rows, (int)C)}, like(x, at::kFloat));
+    Tensor out = at::empty({B, C}, like(x, at::kFloat));
+    DCLIP_CALL(dclip_row_mean(x.data_ptr(), dt_code(x.scalar_type()), bstride, row_off, ld, (int)B, rows, (int)C,
+                              ptr<float>(ws), ptr<float>(out), stream_of(x)));
     return out;
 }
 
-Tensor score_map(const Tensor& v, const Tensor& text, int64_t B, int64_t HW, double eps) {
-    check_gpu(v, "v"); check_gpu(text, "text");
-    TORCH_CHECK(text.scalar_type() == at::kFloat && text.dim() == 3 && text.size(2) == v.size(1), "score_map: text (B, K, C) fp32");
-    c10::DeviceGuard g(v.device());
+Tensor score_map(const Tensor& v, int64_t bstride, int64_t row_off, int64_t ld, const Tensor& text, int64_t B,
+                 int64_t HW, double eps) {
+    check_gpu(text, "text");
+    TORCH_CHECK(text.scalar_type() == at::kFloat && text.dim() == 3 && text.size(0) == B, "score_map: text (B, K, C) fp32");
     const int64_t K = text.size(1), C = text.size(2);
+    check_rows(v, bstride, row_off, ld, B, HW, C);
+    c10::DeviceGuard g(v.device());
     Tensor out = at::empty({B, K, HW}, like(v, at::kFloat));
-    DCLIP_CALL(dclip_score_map(v.data_ptr(), dt_code(v.scalar_type()), ptr<float>(text), ptr<float>(out), (int)B, (int)HW,
-                               (int)C, (int)K, (float)eps, stream_of(v)));
+    DCLIP_CALL(dclip_score_map(v.data_ptr(), dt_code(v.scalar_type()), bstride, row_off, ld, ptr<float>(text),
+                               ptr<float>(out), (int)B, (int)HW, (int)C, (int)K, (float)eps, stream_of(v)));
     return out;
 }
 
@@ -505,8 +515,8 @@ TORCH_LIBRARY(dclip, m) {
     m.def("tokens_bwd(Tensor dx, ScalarType dtype, float scale, int B, int P) -> (Tensor, Tensor, Tensor)");
     m.def("pos_interp(Tensor pos, int g, int H, int W) -> Tensor");
     m.def("pos_interp_bwd(Tensor dout, int g, int H, int W) -> Tensor");
-    m.def("channel_mean(Tensor x, int B) -> Tensor");
-    m.def("score_map(Tensor v, Tensor text, int B, int HW, float eps) -> Tensor");
+    m.def("row_mean(Tensor x, int bstride, int row_off, int ld, int B, int rows, int C) -> Tensor");
+    m.def("score_map(Tensor v, int bstride, int row_off, int ld, Tensor text, int B, int HW, float eps) -> Tensor");
     m.def("bilinear(Tensor x, int Ho, int Wo, ScalarType dtype) -> Tensor");
     m.def("bilinear_bwd(Tensor dout, int Hi, int Wi) -> Tensor");
     m.def("bn_fwd(Tensor x, Tensor? w, Tensor? b, Tensor(a!)? running_mean, Tensor(b!)? running_var, float momentum, "
@@ -543,7 +553,7 @@ TORCH_LIBRARY_IMPL(dclip, CUDA, m) {
     m.impl("tokens_bwd", &tokens_bwd);
     m.impl("pos_interp", &pos_interp);
     m.impl("pos_interp_bwd", &pos_interp_bwd);
-    m.impl("channel_mean", &channel_mean);
+    m.impl("row_mean", &row_mean);
     m.impl("score_map", &score_map);
     m.impl("bilinear", &bilinear);
     m.impl("bilinear_bwd", &bilinear_bwd);

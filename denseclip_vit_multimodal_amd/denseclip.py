@@ -5,9 +5,9 @@ Differences from the reference, all deliberate:
   * errors RAISE (the reference catches everything in forward and returns None outputs,
     denseclip.py:733-752, which hides kernel failures);
   * no defensive `.clone()` of the 12 feature maps (denseclip.py:586, 743);
-  * the score map (denseclip.py:670-675) is computed on the HIP kernels from the
-    channel-last view of the last map: vis_proj as an MFMA GEMM and one fused
-    normalise-and-contract kernel.  It is returned by `_process_features` and, exactly as
+  * the score map (denseclip.py:670-675) is computed on the HIP kernels from the token buffer
+    behind the last map (read in place): the pooling as a strided row mean, vis_proj as an MFMA
+    GEMM and the normalise-and-contract as a batched [K x C] . [C x pixels] MFMA product.  It is returned by `_process_features` and, exactly as
     in the reference, not used by the heads (denseclip.py:747);
   * the final logits/depth resize is the HIP bilinear kernel (fp32 output).
 """
@@ -299,29 +299,37 @@ class DenseCLIP(nn.Module):
             raise NotImplementedError("training through score_concat_index >= 0 (the score map feeding the "
                                       "neck) is not supported; the ViT Cityscapes config uses -1")
         with torch.no_grad():
-            # channel-last pixel rows of the last map (the read-out is a channels-last view)
-            pix = visual.permute(0, 2, 3, 1).reshape(B * HW, Cv).to(cdt).contiguous()
-            g = ops.channel_mean(pix, B)                                   # adaptive_avg_pool2d
+            # pixel rows of the last map read in place: the read-out map is a channels-last view
+            # of a (B*N, C) token buffer (CLS rows in between, ops.ReadoutFn), so the pooling, the
+            # vis_proj GEMM and the score map run on that buffer with a batch stride and a row
+            # offset — no NHWC copy of the map.  Any other map layout gets one NHWC copy.
+            tok = ops.token_rows(visual)
+            if tok is not None and tok.dtype == cdt:
+                rows, Nr, off = tok, HW + 1, 1
+            else:
+                rows, Nr, off = visual.permute(0, 2, 3, 1).reshape(B * HW, Cv).to(cdt).contiguous(), HW, 0
+            g = ops.row_mean(rows, B, HW, row_off=off, bstride=Nr * Cv)    # adaptive_avg_pool2d
             if self.global_proj is not None:
                 g = ops.gemm(ops.cast(g, cdt), ops.WEIGHTS.get(self.global_proj.weight, cdt),
                              bias=self.global_proj.bias.detach(), out_dtype=torch.float32)
-            if self.vis_proj is not None:
-                v = ops.gemm(pix, ops.WEIGHTS.get(self.vis_proj.weight, cdt), bias=self.vis_proj.bias.detach())
+            if self.vis_proj is not None:  # 1x1 conv over every row (the B CLS rows ride along)
+                v = ops.gemm(rows, ops.WEIGHTS.get(self.vis_proj.weight, cdt), bias=self.vis_proj.bias.detach())
             else:
-                v = pix
+                v = rows
+            Ct = v.shape[1]
             text = self._text_embeddings(B, visual.device)
             if self.context_decoder is not None:
-                Ct = v.shape[1]
+                vpix = v.view(B, Nr, Ct)[:, off:].float()
                 if self.context_feature == "attention":
-                    ctx = torch.cat([g.unsqueeze(1), v.view(B, HW, Ct).float()], dim=1)
+                    ctx = torch.cat([g.unsqueeze(1), vpix], dim=1)
                 elif self.context_feature == "backbone":
-                    ctx = v.view(B, HW, Ct).float()
+                    ctx = vpix
                 else:
                     raise ValueError(f"Invalid context_feature type: {self.context_feature}")
                 text = text + self.gamma * self.context_decoder(text, ctx)
-            if v.shape[1] != text.shape[2]:
-                raise ValueError(f"Visual dim after proj ({v.shape[1]}) != Text dim ({text.shape[2]}).")
-            score = ops.score_map(v, text, B, HW).view(B, -1, h, w)
+            if Ct != text.shape[2]:
+                raise ValueError(f"Visual dim after proj ({Ct}) != Text dim ({text.shape[2]}).")
+            score = ops.score_map(v, text, B, HW, row_off=off, bstride=Nr * Ct).view(B, -1, h, w)
         feats = list(x)
         if 0 <= self.score_concat_index < len(feats):
             tgt = feats[self.score_concat_index]

@@ -257,16 +257,22 @@ def pos_interp_bwd(dout, g, H, W):
     return D().pos_interp_bwd(dout, g, H, W)
 
 
-def channel_mean(x2d, B):
-    _check(x2d)
-    return D().channel_mean(x2d, B)
+def row_mean(x, B, rows, row_off=0, bstride=None):
+    """(B, C) f32 mean over `rows` pixel rows per image of a row-major (.., C) tensor whose image b
+    starts at row b*bstride/C + row_off (a ViT token buffer: bstride N*C, row_off 1)."""
+    C = x.shape[-1]
+    bstride = rows * C if bstride is None else bstride
+    return D().row_mean(x, bstride, row_off, C, B, rows, C)
 
 
-def score_map(v2d, text, B, HW, eps=1e-12):
-    """v2d: (B*HW, C) pixel embeddings; text (B, K, C) f32 -> (B, K, HW) f32."""
+def score_map(v, text, B, HW, row_off=0, bstride=None, eps=1e-12):
+    """v: pixel embedding rows (.., C) (image b's pixel p at row b*bstride/C + row_off + p);
+    text (B, K, C) f32 -> (B, K, HW) f32."""
     text = text.float().contiguous()
-    _check(v2d, text)
-    return D().score_map(v2d, text, B, HW, float(eps))
+    _check(text)
+    C = v.shape[-1]
+    bstride = HW * C if bstride is None else bstride
+    return D().score_map(v, bstride, row_off, C, text, B, HW, float(eps))
 
 
 def bilinear(x, Ho, Wo, out_dtype=torch.float32):
@@ -503,6 +509,19 @@ class BlockFn(torch.autograd.Function):
         g = lambda i, t: t if need[i] else None  # noqa: E731
         return (dxm if need[0] else None, None, g(2, dln1w), g(3, dln1b), g(4, dWi), g(5, dbi), g(6, dWo),
                 g(7, dbo), g(8, dln2w), g(9, dln2b), g(10, dW1), g(11, db1), g(12, dW2), g(13, db2))
+
+
+def token_rows(m):
+    """The (B*N, C) token buffer behind a read-out map (the channels-last view ReadoutFn /
+    BlockFn return: strides (N*C, 1, W*C, C), offset C past the buffer start), or None."""
+    if m.dim() != 4 or not m.is_cuda:
+        return None
+    B, C, gh, gw = m.shape
+    Ntok = gh * gw + 1
+    if m.stride() == (Ntok * C, 1, gw * C, C) and m.storage_offset() >= C and \
+            m.untyped_storage().nbytes() >= (m.storage_offset() - C + B * Ntok * C) * m.element_size():
+        return m.as_strided((B * Ntok, C), (C, 1), m.storage_offset() - C)
+    return None
 
 
 def _readout_grad_buffer(dmap, B, Ntok, gh, gw, C):

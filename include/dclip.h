@@ -27,7 +27,7 @@
  *   dclip_transpose            per-layer read-out NLC->NCHW models.py:568-582 (and its
  *                              gradient), NCHW->NHWC for vis_proj, GEMM operand
  *                              transposes with fused bias-gradient column sums
- *   dclip_channel_mean         F.adaptive_avg_pool2d(...,(1,1)) denseclip.py:596
+ *   dclip_row_mean             F.adaptive_avg_pool2d(...,(1,1)) denseclip.py:596
  *   dclip_score_map            F.normalize x2 + einsum('bchw,bkc->bkhw')
  *                              denseclip.py:672-675
  *   dclip_bilinear_fwd/bwd     F.interpolate(bilinear, align_corners=False)
@@ -77,7 +77,8 @@ int dclip_abi_version(void);
 #define DCLIP_OPT_ATTN_DKDV_QS 5     /* dK/dV pass query rows per barrier: 64 (default) or 128 */
 #define DCLIP_OPT_ATTN_BWD_KERNEL 7  /* 0 (default): CLS-split passes when N-1 is a multiple of 256; 1: generic */
 #define DCLIP_OPT_ATTN_FWD_KERNEL 6  /* 0 (default): CLS-split kernel when N-1 is a multiple of the query block; 1: generic */
-#define DCLIP_OPT_COUNT 8
+#define DCLIP_OPT_ATTN_BWD_BLOCK 8   /* 0 (default): register-blocked CLS-split backward passes (64 rows per wave); 1: 32 rows per wave */
+#define DCLIP_OPT_COUNT 9
 int dclip_set_option(int id, int value);
 
 /* LayerNorm over the last dim (cols), eps, affine w/b (fp32).  y = (x-mu)*rstd*w+b.
@@ -197,14 +198,22 @@ int dclip_transpose(const void* in, int in_dt, int64_t in_bstride, int64_t in_ld
                     int batch, int64_t rows, int64_t rows_pad, int64_t cols,
                     int accumulate, float* colsum, void* stream);
 
-/* out[b][c] = mean over r < rows of in[b*rows + r][c]  (in: (B*rows, C) in_dt)        */
-int dclip_channel_mean(const void* in, int in_dt, float* out, int B, int64_t rows, int C,
-                       void* stream);
+/* Strided pixel rows: row r (< rows) of image b is X + b*bstride + (row_off + r)*ld (elements; a ViT
+ * token buffer (B*N, C) has bstride N*C, row_off 1 (skips CLS), ld C).  16-bit X, 16-byte aligned rows.
+ *
+ * out[b][c] (f32) = mean over r < rows of row r of image b  (F.adaptive_avg_pool2d(x, (1, 1)),
+ * denseclip.py:596); ws: dclip_row_mean_workspace(B, rows, C) floats (fixed-order chunk sums).
+ * C % 8 == 0, C <= 2048.                                                                       */
+int64_t dclip_row_mean_workspace(int B, int64_t rows, int C);
+int dclip_row_mean(const void* x, int x_dt, int64_t bstride, int64_t row_off, int64_t ld, int B, int64_t rows,
+                   int C, float* ws, float* out, void* stream);
 
-/* Pixel-text score map.  v: (B*HW, C) v_dt (pixel embeddings, channel-contiguous),
- * t: f32 (B, K, C).  score f32 (B, K, HW) = <v/max(|v|,eps), t/max(|t|,eps)>.        */
-int dclip_score_map(const void* v, int v_dt, const float* t, float* score,
-                    int B, int HW, int C, int K, float eps, void* stream);
+/* Pixel-text score map (F.normalize x2 + einsum('bchw,bkc->bkhw'), denseclip.py:672-675) as a
+ * batched MFMA product.  v: strided pixel rows as above (HW rows per image, v_dt F16/BF16),
+ * t: f32 (B, K, C).  score f32 (B, K, HW) = <v/max(|v|,eps), t/max(|t|,eps)>.  K <= 32,
+ * C % 16 == 0, C <= 2048.                                                                      */
+int dclip_score_map(const void* v, int v_dt, int64_t bstride, int64_t row_off, int64_t ld, const float* t,
+                    float* score, int B, int HW, int C, int K, float eps, void* stream);
 
 /* Bilinear resize, align_corners=False, of NC planes (NC, Hi, Wi) -> (NC, Ho, Wo).   */
 int dclip_bilinear_fwd(const void* in, int in_dt, void* out, int out_dt,

@@ -515,18 +515,35 @@ def test_transpose_colsum_pad():
     assert rel_err(cs, x.float().sum(0)) < 1e-6
 
 
-def test_score_map_and_channel_mean():
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("B,HW,C,K,tok", [(2, 333, 512, 19, False), (3, 8192, 512, 19, True), (1, 40, 1024, 32, True),
+                                          (2, 31, 64, 1, False)])
+def test_score_map_and_row_mean(dt, B, HW, C, K, tok):
+    """The MFMA score map and the strided row mean on plain pixel rows and on token-buffer rows
+    (CLS row first in every image) against fp32 torch on the same 16-bit values."""
     O = ops()
-    B, HW, C, K = 2, 333, 512, 19
+    off = 1 if tok else 0
+    Nr = HW + off
+    buf = torch.randn(B * Nr, C, device=DEV).to(dt)
+    v = buf.view(B, Nr, C)[:, off:].float()
+    t = torch.randn(B, K, C, device=DEV)
+    s = O.score_map(buf, t, B, HW, row_off=off, bstride=Nr * C)
+    ref = torch.einsum("bpc,bkc->bkp", F.normalize(v, dim=2), F.normalize(t, dim=2))
+    # T-hat is rounded to the operand dtype for the MFMA: ~2^-9 (bf16) / 2^-11 (fp16) per element
+    assert rel_err(s, ref) < (4e-3 if dt == torch.bfloat16 else 1e-3)
+    m = O.row_mean(buf, B, HW, row_off=off, bstride=Nr * C)
+    assert rel_err(m, v.mean(1)) < 1e-5
+
+
+def test_score_map_eps_and_zero_rows():
+    """F.normalize's eps: an all-zero pixel row scores 0 (not NaN)."""
+    O = ops()
+    B, HW, C, K = 1, 64, 512, 19
     v = torch.randn(B * HW, C, device=DEV).to(torch.bfloat16)
+    v[5] = 0
     t = torch.randn(B, K, C, device=DEV)
     s = O.score_map(v, t, B, HW)
-    vn = F.normalize(v.float().view(B, HW, C), dim=2)
-    tn = F.normalize(t, dim=2)
-    ref = torch.einsum("bpc,bkc->bkp", vn, tn)
-    assert rel_err(s, ref) < 1e-5
-    m = O.channel_mean(v, B)
-    assert rel_err(m, v.float().view(B, HW, C).mean(1)) < 1e-6
+    assert torch.isfinite(s).all() and torch.count_nonzero(s[0, :, 5]) == 0
 
 
 # ----------------------------------------------------------------------------- neck convs

@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
     lib = N.load()
     for name in declared_symbols():
         assert hasattr(lib, name), name
-    assert lib.dclip_abi_version() == 1
+    assert lib.dclip_abi_version() == 2
 
 
 def test_no_oracle_in_product_package():
@@ -47,7 +47,8 @@ def test_no_oracle_in_product_package():
      "multiple of 64*splits"),
     (lambda L: L.dclip_attn_fwd(2, None, None, None, 1, 8, 2, 32, 1.0, None), "head_dim must be 64"),
     (lambda L: L.dclip_layernorm_fwd(None, 0, None, None, None, 0, None, None, 4, 4098, 1e-5, None), "cols"),
-    (lambda L: L.dclip_score_map(None, 0, None, None, 1, 4, 512, 40, 1e-12, None), "K must be"),
+    (lambda L: L.dclip_score_map(None, 2, 0, 0, 512, None, None, 1, 4, 512, 40, 1e-12, None), "K must be"),
+    (lambda L: L.dclip_row_mean(None, 2, 0, 0, 100, 1, 4, 100, None, None, None), "C % 8"),
     (lambda L: L.dclip_im2col(None, 0, None, 0, 768, 1, 3, 8, 8, 16, None), "smaller than one patch"),
 ])
 def test_argument_errors_are_reported(call, needle):
