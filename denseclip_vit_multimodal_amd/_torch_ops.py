@@ -76,6 +76,10 @@ def _register_fakes():
     def _(x, dtype):
         return _e(x.shape[1], x.shape[0], like=x, dtype=dtype)
 
+    @reg("dclip::transpose_batched")
+    def _(x, B, rows, cols, ld_in, rows_pad, dtype):
+        return _e(B, cols, rows_pad, like=x, dtype=dtype)
+
     @reg("dclip::add_readout_cast")
     def _(a, b, ntok, lp_dtype, scale):
         return _e(*a.shape, like=a), _e(*a.shape, like=a, dtype=lp_dtype)
@@ -131,16 +135,25 @@ def _register_fakes():
         return _e(dout.shape[0], dout.shape[1], Hi, Wi, like=dout, dtype=f32)
 
     @reg("dclip::bn_fwd")
-    def _(x, w, b, running_mean, running_var, momentum, eps):
+    def _(x, w, b, running_mean, running_var, momentum, eps, relu):
         C = x.shape[1]
         return (torch.empty_like(x, memory_format=torch.channels_last), _e(C, like=x, dtype=f32),
                 _e(C, like=x, dtype=f32))
 
     @reg("dclip::bn_bwd")
-    def _(dy, x, w, mean, rstd, want_w, want_b):
+    def _(dy, x, w, b, mean, rstd, relu, want_w, want_b):
         C = x.shape[1]
         return (torch.empty_like(x, memory_format=torch.channels_last), _e(C if want_w else 0, like=x, dtype=f32),
                 _e(C if want_b else 0, like=x, dtype=f32))
+
+    @reg("dclip::bn_fwd_rows")
+    def _(x, w, b, running_mean, running_var, momentum, eps, relu, y):
+        return _e(x.shape[1], like=x, dtype=f32), _e(x.shape[1], like=x, dtype=f32)
+
+    @reg("dclip::bn_bwd_rows")
+    def _(dy, x, w, b, mean, rstd, relu, want_w, want_b, dx):
+        C = x.shape[1]
+        return _e(C if want_w else 0, like=x, dtype=f32), _e(C if want_b else 0, like=x, dtype=f32)
 
     @reg("dclip::conv3x3")
     def _(mode, X, x_bstride, x_off, x_ld, B, H, W, Cin, Wt, Nout, out, out_ld, out_gap, out_off, accumulate):

@@ -1960,256 +1960,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv2_kernel(const T
     store_row_t21<T>(rk + C, c.dv, 1.0f, c.h);
 }
 
-// ---------------------------------------------------------------------------- dK/dV pass, register-blocked
-// The CLS-split dK/dV pass with TWO 32-key blocks per wave (64 keys, 4 waves = 256 keys per
-// workgroup, one wave per SIMD): every Q / dO fragment read from LDS — the row fragments of the
-// S and dP chains and the transposed fragments of the dV / dK products — feeds both key blocks,
-// halving LDS instructions per MFMA (0.75 instead of 1.5) and giving each wave two independent
-// MFMA chains per phase.  dK^T / dV^T of the 64 keys stay in 128 accumulator registers; the ring,
-// the LDS-DMA staging and the query-0 fold are those of attn_bwd_dkdv2_kernel.
-template <typename T>
-struct Dkv3Ctx : Dkv2Ctx<T, 4> {
-    typedef typename Mfma<T>::frag frag;
-    frag kf1[4], vf1[4];  // the wave's second key block (kf / vf of the base: the first)
-    f32x16 dk1[2], dv1[2];
-};
-
-// dV^T += dO^T P ; dK^T += Q^T dS for one key block from its S / dP accumulators (consumed)
-template <typename T>
-__device__ __forceinline__ void dkv3_update(f32x16& sacc, f32x16& pacc, const typename Mfma<T>::frag (&gt)[2][2],
-                                            const typename Mfma<T>::frag (&qt)[2][2], f32x16 (&dv)[2],
-                                            f32x16 (&dk)[2]) {
-    typedef typename Mfma<T>::frag frag;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const float p = __builtin_amdgcn_exp2f(sacc[r]);
-        sacc[r] = p;
-        pacc[r] = p * pacc[r] * DsScale<T>::v;
-    }
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-        const frag pf = pack_frag<T>(sacc, s);
-        const frag sf = pack_frag<T>(pacc, s);
-#pragma unroll
-        for (int db = 0; db < 2; ++db) {
-            dv[db] = Mfma<T>::mma(gt[s][db], pf, dv[db]);
-            dk[db] = Mfma<T>::mma(qt[s][db], sf, dk[db]);
-        }
-    }
-}
-
-template <typename T, int Q>
-__device__ __forceinline__ void dkv3_step(Dkv3Ctx<T>& c, int t) {
-    typedef typename Mfma<T>::frag frag;
-    typedef Dkv2Ctx<T, 4> X;
-    wait_vmcnt<2 * (X::PIECES + 1)>();  // own pieces of slice t landed (slices t+1, t+2 in flight)
-    __builtin_amdgcn_s_barrier();       // everyone's; everyone done with step t-1
-    dkv2_issue<T, 4>(c, t + 3 < c.nt ? t + 3 : c.nt - 1, (Q + 3) & 3);
-    const char* base = c.smem + Q * X::SLOT;
-    const float* Lsl = (const float*)(base + 16384);
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-        const char* Qt = base + sub * 32 * 128;
-        const char* Gt = base + 8192 + sub * 32 * 128;
-        const float* Ls = Lsl + sub * 32;
-        const float* Ds = Lsl + 64 + sub * 32;
-        frag qa[4], ga[4];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            qa[s] = row_frag<T>(Qt, c.l32, 2 * s + c.h);
-            ga[s] = row_frag<T>(Gt, c.l32, 2 * s + c.h);
-        }
-        f32x16 s0, p0, s1, p1;  // start from -L[q] / -delta[q] per row (negated by the dQ pass)
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-            const f32x4 Lv = *(const f32x4*)(Ls + 8 * g4 + 4 * c.h);
-            const f32x4 Dv = *(const f32x4*)(Ds + 8 * g4 + 4 * c.h);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                s0[4 * g4 + e] = Lv[e];
-                p0[4 * g4 + e] = Dv[e];
-            }
-        }
-        s1 = s0;
-        p1 = p0;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            s0 = Mfma<T>::mma(qa[s], c.kf[s], s0);
-            p0 = Mfma<T>::mma(ga[s], c.vf[s], p0);
-        }
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            s1 = Mfma<T>::mma(qa[s], c.kf1[s], s1);
-            p1 = Mfma<T>::mma(ga[s], c.vf1[s], p1);
-        }
-        frag gt[2][2], qt[2][2];
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-            for (int db = 0; db < 2; ++db) {
-                gt[s][db] = tr_frag<T>(Gt, 0, s, db, c.lane);
-                qt[s][db] = tr_frag<T>(Qt, 0, s, db, c.lane);
-            }
-        dkv3_update<T>(s0, p0, gt, qt, c.dv, c.dk);
-        dkv3_update<T>(s1, p1, gt, qt, c.dv1, c.dk1);
-    }
-}
-
-template <typename T>
-__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv3_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
-                                                                const float* __restrict__ lse,
-                                                                const float* __restrict__ delta,
-                                                                const float* __restrict__ nlse,
-                                                                const float* __restrict__ ndelta,
-                                                                T* __restrict__ dqkv, int N, int H, float dk_scale) {
-    constexpr int NW = 4, KB = 256;
-    typedef Dkv2Ctx<T, NW> X;
-    typedef typename Mfma<T>::frag frag;
-    __shared__ __attribute__((aligned(16))) char smem[4 * X::SLOT];
-    Dkv3Ctx<T> c;
-    c.smem = smem;
-    c.lane = threadIdx.x & 63;
-    c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    c.h = c.lane >> 5;
-    c.l32 = c.lane & 31;
-    const int nkb = (N - 1) / KB;
-    const int tile = xcd_remap(blockIdx.x, gridDim.x);
-    const int kblk = tile % nkb, bh = tile / nkb, b = bh / H, hd = bh % H;
-    const int C = H * HD;
-    const int64_t ld = 3 * (int64_t)C;
-    const T* Bb = qkv + (int64_t)b * N * ld;
-    const T* dOb = dout + (int64_t)b * N * C;
-    c.ldq = (uint32_t)(ld * sizeof(T));
-    c.ldg = (uint32_t)(C * sizeof(T));
-    c.nt = (N - 1) / 64;
-    const int key0 = 1 + kblk * KB + c.wave * 64 + c.l32;  // first key block; the second is key0 + 32
-    frag q0[4], g0[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        c.kf[s] = *(const frag*)(Bb + (int64_t)key0 * ld + C + hd * HD + (2 * s + c.h) * 8);
-        c.vf[s] = *(const frag*)(Bb + (int64_t)key0 * ld + 2 * C + hd * HD + (2 * s + c.h) * 8);
-        c.kf1[s] = *(const frag*)(Bb + (int64_t)(key0 + 32) * ld + C + hd * HD + (2 * s + c.h) * 8);
-        c.vf1[s] = *(const frag*)(Bb + (int64_t)(key0 + 32) * ld + 2 * C + hd * HD + (2 * s + c.h) * 8);
-        q0[s] = *(const frag*)(Bb + hd * HD + (2 * s + c.h) * 8);
-        g0[s] = *(const frag*)(dOb + hd * HD + (2 * s + c.h) * 8);
-    }
-    typedef T t4 __attribute__((ext_vector_type(4)));
-    t4 q0d[2][4], g0d[2][4];  // query 0's q and dO at this lane's accumulator rows d
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            q0d[db][g] = *(const t4*)(Bb + hd * HD + db * 32 + 8 * g + 4 * c.h);
-            g0d[db][g] = *(const t4*)(dOb + hd * HD + db * 32 + 8 * g + 4 * c.h);
-        }
-    const float L0 = lse[(int64_t)bh * N], d0 = delta[(int64_t)bh * N];
-
-    c.rs = make_rsrc(Bb, (uint32_t)N * c.ldq);
-    c.rg = make_rsrc(dOb, (uint32_t)N * c.ldg);
-    c.rl = make_rsrc(nlse + (int64_t)bh * N, (uint32_t)N * 4);
-    c.rd = make_rsrc(ndelta + (int64_t)bh * N, (uint32_t)N * 4);
-    const bool q_wave = c.wave * X::PIECES < 8;
-    c.rmine = q_wave ? c.rs : c.rg;
-    c.ldmine = q_wave ? c.ldq : c.ldg;
-#pragma unroll
-    for (int i = 0; i < X::PIECES; ++i) {
-        const int piece = c.wave * X::PIECES + i;
-        const int r = (piece & 7) * 8 + (c.lane >> 3);
-        const uint32_t chunk = (uint32_t)(((c.lane & 7) ^ xsw(r)) * 16);
-        c.voff[i] = piece < 8 ? (uint32_t)r * c.ldq + chunk + (uint32_t)(hd * HD * sizeof(T))
-                              : (uint32_t)r * c.ldg + chunk + (uint32_t)(hd * HD * sizeof(T));
-    }
-    dkv2_issue<T, NW>(c, 0, 0);
-    dkv2_issue<T, NW>(c, c.nt > 1 ? 1 : 0, 1);
-    dkv2_issue<T, NW>(c, c.nt > 2 ? 2 : c.nt - 1, 2);
-
-    // query 0 (CLS) folded in for both key blocks: P = exp2(q0 . k - L0), dS = P (dO0 . v - delta0)
-    float sp0 = 0.f, pp0 = 0.f, sp1 = 0.f, pp1 = 0.f;
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            sp0 += (float)q0[s][j] * (float)c.kf[s][j];
-            pp0 += (float)g0[s][j] * (float)c.vf[s][j];
-            sp1 += (float)q0[s][j] * (float)c.kf1[s][j];
-            pp1 += (float)g0[s][j] * (float)c.vf1[s][j];
-        }
-    const float pa = __builtin_amdgcn_exp2f(xhalf_sum(sp0) - L0);
-    const float da = pa * (xhalf_sum(pp0) - d0) * DsScale<T>::v;
-    const float pb = __builtin_amdgcn_exp2f(xhalf_sum(sp1) - L0);
-    const float dbv = pb * (xhalf_sum(pp1) - d0) * DsScale<T>::v;
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                c.dv[db][4 * g + e] = pa * (float)g0d[db][g][e];
-                c.dk[db][4 * g + e] = da * (float)q0d[db][g][e];
-                c.dv1[db][4 * g + e] = pb * (float)g0d[db][g][e];
-                c.dk1[db][4 * g + e] = dbv * (float)q0d[db][g][e];
-            }
-
-    for (int t = 0; t < c.nt; t += 4) {  // nt = (N-1)/64 is a multiple of 4: one loop exit
-        dkv3_step<T, 0>(c, t);
-        dkv3_step<T, 1>(c, t + 1);
-        dkv3_step<T, 2>(c, t + 2);
-        dkv3_step<T, 3>(c, t + 3);
-    }
-    wait_vmcnt<0>();
-    T* rk = dqkv + ((int64_t)b * N + key0) * ld + C + hd * HD;
-    store_row_t21<T>(rk, c.dk, dk_scale / DsScale<T>::v, c.h);
-    store_row_t21<T>(rk + C, c.dv, 1.0f, c.h);
-    store_row_t21<T>(rk + 32 * ld, c.dk1, dk_scale / DsScale<T>::v, c.h);
-    store_row_t21<T>(rk + 32 * ld + C, c.dv1, 1.0f, c.h);
-}
-
-// ---------------------------------------------------------------------------- dK/dV pass, register-blocked + pipelined
-// attn_bwd_dkdv3_kernel's blocking (two 32-key blocks per wave, one wave per SIMD) with the
-// sub-slice loop software-pipelined one 32-query sub-slice ahead: the S / dP chains of the next
-// sub-slice (16 MFMAs, independent of everything in flight) are issued while the VALU turns the
-// current sub-slice's accumulators into P / dS operands (exp2, multiply, pack), and the dV / dK
-// products of key block 0 run beside the exp of key block 1.  Two sets of S / dP accumulators
-// (A: the sub-slice being finished, B: the one being computed) alternate.  The ring is read one
-// slice ahead (slice t+1's first sub-slice inside step t), so each step waits for slice t+1.
-template <typename T>
-__device__ __forceinline__ void dkv4_sdp(const Dkv3Ctx<T>& c, const char* base, int sub, f32x16& s0, f32x16& p0,
-                                         f32x16& s1, f32x16& p1) {
-    typedef typename Mfma<T>::frag frag;
-    const char* Qt = base + sub * 32 * 128;
-    const char* Gt = base + 8192 + sub * 32 * 128;
-    const float* Ls = (const float*)(base + 16384) + sub * 32;
-    const float* Ds = Ls + 64;
-    frag qa[4], ga[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        qa[s] = row_frag<T>(Qt, c.l32, 2 * s + c.h);
-        ga[s] = row_frag<T>(Gt, c.l32, 2 * s + c.h);
-    }
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-        const f32x4 Lv = *(const f32x4*)(Ls + 8 * g4 + 4 * c.h);
-        const f32x4 Dv = *(const f32x4*)(Ds + 8 * g4 + 4 * c.h);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            s0[4 * g4 + e] = Lv[e];
-            p0[4 * g4 + e] = Dv[e];
-            s1[4 * g4 + e] = Lv[e];
-            p1[4 * g4 + e] = Dv[e];
-        }
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        s0 = Mfma<T>::mma(qa[s], c.kf[s], s0);
-        p0 = Mfma<T>::mma(ga[s], c.vf[s], p0);
-        s1 = Mfma<T>::mma(qa[s], c.kf1[s], s1);
-        p1 = Mfma<T>::mma(ga[s], c.vf1[s], p1);
-    }
-}
-
+// ---------------------------------------------------------------------------- dK/dV pass helpers
 // P = exp2(S - L), dS = P (dP - delta) as 16-bit B operands (the accumulators are consumed)
 template <typename T>
-__device__ __forceinline__ void dkv4_pack(f32x16& s, f32x16& p, typename Mfma<T>::frag (&pf)[2],
+__device__ __forceinline__ void dkv_pack(f32x16& s, f32x16& p, typename Mfma<T>::frag (&pf)[2],
                                           typename Mfma<T>::frag (&sf)[2]) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -2225,7 +1979,7 @@ __device__ __forceinline__ void dkv4_pack(f32x16& s, f32x16& p, typename Mfma<T>
 }
 
 template <typename T>
-__device__ __forceinline__ void dkv4_mm(const typename Mfma<T>::frag (&gt)[2][2], const typename Mfma<T>::frag (&qt)[2][2],
+__device__ __forceinline__ void dkv_mm(const typename Mfma<T>::frag (&gt)[2][2], const typename Mfma<T>::frag (&qt)[2][2],
                                         const typename Mfma<T>::frag (&pf)[2], const typename Mfma<T>::frag (&sf)[2],
                                         f32x16 (&dv)[2], f32x16 (&dk)[2]) {
 #pragma unroll
@@ -2237,165 +1991,18 @@ __device__ __forceinline__ void dkv4_mm(const typename Mfma<T>::frag (&gt)[2][2]
         }
 }
 
-// finish sub-slice (image base, sub) from accumulators (a0, b0, a1, b1): pack kb0, dV/dK kb0 beside
-// the pack of kb1, dV/dK kb1
-template <typename T>
-__device__ __forceinline__ void dkv4_finish(Dkv3Ctx<T>& c, const char* base, int sub, f32x16& a0, f32x16& b0,
-                                            f32x16& a1, f32x16& b1) {
-    typedef typename Mfma<T>::frag frag;
-    const char* Qt = base + sub * 32 * 128;
-    const char* Gt = base + 8192 + sub * 32 * 128;
-    frag gt[2][2], qt[2][2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int db = 0; db < 2; ++db) {
-            gt[s][db] = tr_frag<T>(Gt, 0, s, db, c.lane);
-            qt[s][db] = tr_frag<T>(Qt, 0, s, db, c.lane);
-        }
-    frag pf0[2], sf0[2], pf1[2], sf1[2];
-    dkv4_pack<T>(a0, b0, pf0, sf0);
-    dkv4_mm<T>(gt, qt, pf0, sf0, c.dv, c.dk);
-    dkv4_pack<T>(a1, b1, pf1, sf1);
-    dkv4_mm<T>(gt, qt, pf1, sf1, c.dv1, c.dk1);
-}
-
-// step t (slot Q = t % 4); on entry (sA0, pA0, sA1, pA1) = S / dP of sub-slice (t, 0), on exit
-// those of (t+1, 0)
-template <typename T, int Q>
-__device__ __forceinline__ void dkv4_step(Dkv3Ctx<T>& c, int t, f32x16& sA0, f32x16& pA0, f32x16& sA1, f32x16& pA1) {
-    typedef Dkv2Ctx<T, 4> X;
-    wait_vmcnt<X::PIECES + 1>();    // own pieces of slice t+1 landed (slice t+2 in flight)
-    __builtin_amdgcn_s_barrier();  // everyone's; everyone done with step t-1 (slot (t+3) % 4 free)
-    dkv2_issue<T, 4>(c, t + 3 < c.nt ? t + 3 : c.nt - 1, (Q + 3) & 3);
-    const char* cur = c.smem + Q * X::SLOT;
-    const char* nxt = c.smem + ((Q + 1) & 3) * X::SLOT;
-    f32x16 sB0, pB0, sB1, pB1;
-    dkv4_sdp<T>(c, cur, 1, sB0, pB0, sB1, pB1);    // (t, 1) on the matrix pipe ...
-    dkv4_finish<T>(c, cur, 0, sA0, pA0, sA1, pA1);  // ... beside the finish of (t, 0)
-    dkv4_sdp<T>(c, nxt, 0, sA0, pA0, sA1, pA1);    // (t+1, 0) ...
-    dkv4_finish<T>(c, cur, 1, sB0, pB0, sB1, pB1);  // ... beside the finish of (t, 1)
-}
-
-template <typename T>
-__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv4_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
-                                                                const float* __restrict__ lse,
-                                                                const float* __restrict__ delta,
-                                                                const float* __restrict__ nlse,
-                                                                const float* __restrict__ ndelta,
-                                                                T* __restrict__ dqkv, int N, int H, float dk_scale) {
-    constexpr int NW = 4, KB = 256;
-    typedef Dkv2Ctx<T, NW> X;
-    typedef typename Mfma<T>::frag frag;
-    __shared__ __attribute__((aligned(16))) char smem[4 * X::SLOT];
-    Dkv3Ctx<T> c;
-    c.smem = smem;
-    c.lane = threadIdx.x & 63;
-    c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    c.h = c.lane >> 5;
-    c.l32 = c.lane & 31;
-    const int nkb = (N - 1) / KB;
-    const int tile = xcd_remap(blockIdx.x, gridDim.x);
-    const int kblk = tile % nkb, bh = tile / nkb, b = bh / H, hd = bh % H;
-    const int C = H * HD;
-    const int64_t ld = 3 * (int64_t)C;
-    const T* Bb = qkv + (int64_t)b * N * ld;
-    const T* dOb = dout + (int64_t)b * N * C;
-    c.ldq = (uint32_t)(ld * sizeof(T));
-    c.ldg = (uint32_t)(C * sizeof(T));
-    c.nt = (N - 1) / 64;
-    const int key0 = 1 + kblk * KB + c.wave * 64 + c.l32;  // first key block; the second is key0 + 32
-    frag q0[4], g0[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        c.kf[s] = *(const frag*)(Bb + (int64_t)key0 * ld + C + hd * HD + (2 * s + c.h) * 8);
-        c.vf[s] = *(const frag*)(Bb + (int64_t)key0 * ld + 2 * C + hd * HD + (2 * s + c.h) * 8);
-        c.kf1[s] = *(const frag*)(Bb + (int64_t)(key0 + 32) * ld + C + hd * HD + (2 * s + c.h) * 8);
-        c.vf1[s] = *(const frag*)(Bb + (int64_t)(key0 + 32) * ld + 2 * C + hd * HD + (2 * s + c.h) * 8);
-        q0[s] = *(const frag*)(Bb + hd * HD + (2 * s + c.h) * 8);
-        g0[s] = *(const frag*)(dOb + hd * HD + (2 * s + c.h) * 8);
-    }
-    typedef T t4 __attribute__((ext_vector_type(4)));
-    t4 q0d[2][4], g0d[2][4];
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            q0d[db][g] = *(const t4*)(Bb + hd * HD + db * 32 + 8 * g + 4 * c.h);
-            g0d[db][g] = *(const t4*)(dOb + hd * HD + db * 32 + 8 * g + 4 * c.h);
-        }
-    const float L0 = lse[(int64_t)bh * N], d0 = delta[(int64_t)bh * N];
-
-    c.rs = make_rsrc(Bb, (uint32_t)N * c.ldq);
-    c.rg = make_rsrc(dOb, (uint32_t)N * c.ldg);
-    c.rl = make_rsrc(nlse + (int64_t)bh * N, (uint32_t)N * 4);
-    c.rd = make_rsrc(ndelta + (int64_t)bh * N, (uint32_t)N * 4);
-    const bool q_wave = c.wave * X::PIECES < 8;
-    c.rmine = q_wave ? c.rs : c.rg;
-    c.ldmine = q_wave ? c.ldq : c.ldg;
-#pragma unroll
-    for (int i = 0; i < X::PIECES; ++i) {
-        const int piece = c.wave * X::PIECES + i;
-        const int r = (piece & 7) * 8 + (c.lane >> 3);
-        const uint32_t chunk = (uint32_t)(((c.lane & 7) ^ xsw(r)) * 16);
-        c.voff[i] = piece < 8 ? (uint32_t)r * c.ldq + chunk + (uint32_t)(hd * HD * sizeof(T))
-                              : (uint32_t)r * c.ldg + chunk + (uint32_t)(hd * HD * sizeof(T));
-    }
-    dkv2_issue<T, NW>(c, 0, 0);
-    dkv2_issue<T, NW>(c, c.nt > 1 ? 1 : 0, 1);
-    dkv2_issue<T, NW>(c, c.nt > 2 ? 2 : c.nt - 1, 2);
-
-    float sp0 = 0.f, pp0 = 0.f, sp1 = 0.f, pp1 = 0.f;
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            sp0 += (float)q0[s][j] * (float)c.kf[s][j];
-            pp0 += (float)g0[s][j] * (float)c.vf[s][j];
-            sp1 += (float)q0[s][j] * (float)c.kf1[s][j];
-            pp1 += (float)g0[s][j] * (float)c.vf1[s][j];
-        }
-    const float pa = __builtin_amdgcn_exp2f(xhalf_sum(sp0) - L0);
-    const float da = pa * (xhalf_sum(pp0) - d0) * DsScale<T>::v;
-    const float pb = __builtin_amdgcn_exp2f(xhalf_sum(sp1) - L0);
-    const float dbv = pb * (xhalf_sum(pp1) - d0) * DsScale<T>::v;
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                c.dv[db][4 * g + e] = pa * (float)g0d[db][g][e];
-                c.dk[db][4 * g + e] = da * (float)q0d[db][g][e];
-                c.dv1[db][4 * g + e] = pb * (float)g0d[db][g][e];
-                c.dk1[db][4 * g + e] = dbv * (float)q0d[db][g][e];
-            }
-
-    wait_vmcnt<2 * (X::PIECES + 1)>();  // slice 0 landed (slices 1, 2 in flight)
-    __builtin_amdgcn_s_barrier();
-    f32x16 sA0, pA0, sA1, pA1;
-    dkv4_sdp<T>(c, smem, 0, sA0, pA0, sA1, pA1);
-    for (int t = 0; t < c.nt; t += 4) {  // nt = (N-1)/64 is a multiple of 4: one loop exit
-        dkv4_step<T, 0>(c, t, sA0, pA0, sA1, pA1);
-        dkv4_step<T, 1>(c, t + 1, sA0, pA0, sA1, pA1);
-        dkv4_step<T, 2>(c, t + 2, sA0, pA0, sA1, pA1);
-        dkv4_step<T, 3>(c, t + 3, sA0, pA0, sA1, pA1);
-    }
-    wait_vmcnt<0>();
-    T* rk = dqkv + ((int64_t)b * N + key0) * ld + C + hd * HD;
-    store_row_t21<T>(rk, c.dk, dk_scale / DsScale<T>::v, c.h);
-    store_row_t21<T>(rk + C, c.dv, 1.0f, c.h);
-    store_row_t21<T>(rk + 32 * ld, c.dk1, dk_scale / DsScale<T>::v, c.h);
-    store_row_t21<T>(rk + 32 * ld + C, c.dv1, 1.0f, c.h);
-}
-
 // ---------------------------------------------------------------------------- dK/dV pass, pipelined (32 keys per wave)
 // attn_bwd_dkdv2_kernel (32 keys per wave, 4 waves, two workgroups = two waves per SIMD, so the
 // compiler keeps every accumulator in arch VGPRs: no v_accvgpr copies around the softmax VALU)
-// with dkdv4's sub-slice software pipeline: the S / dP chains of the next 32-query sub-slice
-// are issued before the exp / pack of the current one, so each wave always has independent
-// MFMA work queued behind its VALU.  Peak liveness ~220 VGPRs (K / V 32, dK / dV 64, two S / dP
-// sets 64, Q / dO fragments 32, packed P / dS 16).
+// with the sub-slice loop software-pipelined one 32-query sub-slice ahead: the S / dP chains of
+// the next sub-slice are issued before the exp / pack of the current one, so each wave always
+// has independent MFMA work queued behind its VALU.  The ring is read one slice ahead (slice
+// t+1's first sub-slice inside step t), so each step waits for slice t+1.  Peak liveness ~220
+// VGPRs (K / V 32, dK / dV 64, two S / dP sets 64, Q / dO fragments 32, packed P / dS 16).
+// Measured against the unpipelined pass: 2.74 vs 2.98 ms per launch in one process
+// (profiles/r02i).  Blocking two key blocks per wave (one wave per SIMD, Q / dO fragments shared
+// by both) did NOT pay: above 256 registers hipcc puts every MFMA accumulator in AGPRs, and the
+// softmax's v_accvgpr copies doubled the VALU count (2.98-3.50 ms, profiles/r02g).
 template <typename T>
 __device__ __forceinline__ void dkv5_sdp(const Dkv2Ctx<T, 4>& c, const char* base, int sub, f32x16& s0, f32x16& p0) {
     typedef typename Mfma<T>::frag frag;
@@ -2440,8 +2047,8 @@ __device__ __forceinline__ void dkv5_finish(Dkv2Ctx<T, 4>& c, const char* base, 
             qt[s][db] = tr_frag<T>(Qt, 0, s, db, c.lane);
         }
     frag pf[2], sf[2];
-    dkv4_pack<T>(a0, b0, pf, sf);
-    dkv4_mm<T>(gt, qt, pf, sf, c.dv, c.dk);
+    dkv_pack<T>(a0, b0, pf, sf);
+    dkv_mm<T>(gt, qt, pf, sf, c.dv, c.dk);
 }
 
 template <typename T, int Q>
@@ -2627,14 +2234,8 @@ bool bwd2_launch(const void* qkv, const void* o, const void* dout, const float* 
     attn_bwd_row0_dkdv_part<T><<<B * H * nsplit, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, ws0, N, H,
                                                               nsplit);
     attn_bwd_row0_dkdv_merge<T><<<B * H, 64, 0, st>>>(ws0, (T*)dqkv, N, H, nsplit, 1.0f / LOG2E);
-    if (dclip_option(DCLIP_OPT_ATTN_BWD_BLOCK) == 0)  // register-blocked + pipelined: 64 keys per wave
-        attn_bwd_dkdv4_kernel<T><<<B * H * ((N - 1) / 256), 256, 0, st>>>(
-            (const T*)qkv, (const T*)dout, lse, delta, nstat, nstat + (int64_t)B * H * N, (T*)dqkv, N, H, 1.0f / LOG2E);
-    else if (dclip_option(DCLIP_OPT_ATTN_BWD_BLOCK) == 3)  // pipelined, 32 keys per wave, 2 waves per SIMD
+    if (dclip_option(DCLIP_OPT_ATTN_BWD_BLOCK) == 0)  // default: pipelined, 32 keys per wave, 2 waves per SIMD
         attn_bwd_dkdv5_kernel<T><<<B * H * ((N - 1) / 128), 256, 0, st>>>(
-            (const T*)qkv, (const T*)dout, lse, delta, nstat, nstat + (int64_t)B * H * N, (T*)dqkv, N, H, 1.0f / LOG2E);
-    else if (dclip_option(DCLIP_OPT_ATTN_BWD_BLOCK) == 2)  // register-blocked: 64 keys per wave, 256 per workgroup
-        attn_bwd_dkdv3_kernel<T><<<B * H * ((N - 1) / 256), 256, 0, st>>>(
             (const T*)qkv, (const T*)dout, lse, delta, nstat, nstat + (int64_t)B * H * N, (T*)dqkv, N, H, 1.0f / LOG2E);
     else if (dclip_option(DCLIP_OPT_ATTN_DKDV_WAVES) == 8)  // 256 keys per workgroup (one Q / dO slice per 256 keys)
         attn_bwd_dkdv2_kernel<T, 8><<<B * H * ((N - 1) / 256), 512, 0, st>>>(

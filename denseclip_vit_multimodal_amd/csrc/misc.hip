@@ -653,46 +653,63 @@ __device__ __forceinline__ void load8(const T* p, float* v) {
     for (int e = 0; e < 8; ++e) v[e] = (float)r[e];
 }
 
-// MODE 0: s += x - x0, q += (x - x0)^2 ;  MODE 1: s += dy, q += dy * (x - mean)
-template <typename T, int MODE>
+// the forward's per-channel affine of BN (scale = w rstd, shift = b - mean scale) for 8 channels
+__device__ __forceinline__ void bn_affine8(const float* w, const float* b, const float* mean, const float* rstd, int c0,
+                                           float* sc, float* sh) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        sc[e] = (w ? w[c0 + e] : 1.f) * rstd[c0 + e];
+        sh[e] = (b ? b[c0 + e] : 0.f) - mean[c0 + e] * sc[e];
+    }
+}
+
+// MODE 0: s += x - x0, q += (x - x0)^2 ;  MODE 1: s += dy, q += dy * (x - mean), with dy masked by
+// the fused ReLU's derivative (x sc + sh > 0) when RELU.  Rows of ld elements; threads past the
+// last whole row of a pass (C / 8 not dividing 256) idle.
+template <typename T, int MODE, bool RELU>
 __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ a, const T* __restrict__ x,
-                                                       const float* __restrict__ mean, int64_t rows, int C,
-                                                       float* __restrict__ part) {
+                                                       const float* __restrict__ w, const float* __restrict__ b,
+                                                       const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                       int64_t rows, int C, int64_t ld, float* __restrict__ part) {
     __shared__ float red[2 * 2048];
     const int tpr = C / 8, rpb = 256 / tpr;
     const int c8 = threadIdx.x % tpr, rr = threadIdx.x / tpr;
-    float s[8], q[8], ref[8];
+    float s[8], q[8], ref[8], sc[8], sh[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) s[e] = q[e] = 0.f;
-    if (MODE == 0) load8(a + c8 * 8, ref);
-    else
+    if (rr < rpb) {
+        if (MODE == 0) load8(a + c8 * 8, ref);
+        else
 #pragma unroll
-        for (int e = 0; e < 8; ++e) ref[e] = mean[c8 * 8 + e];
+            for (int e = 0; e < 8; ++e) ref[e] = mean[c8 * 8 + e];
+        if (RELU) bn_affine8(w, b, mean, rstd, c8 * 8, sc, sh);
 #pragma unroll 4
-    for (int64_t r = (int64_t)blockIdx.x * rpb + rr; r < rows; r += (int64_t)gridDim.x * rpb) {
-        float v[8];
-        load8(a + r * C + c8 * 8, v);
-        if (MODE == 0) {
+        for (int64_t r = (int64_t)blockIdx.x * rpb + rr; r < rows; r += (int64_t)gridDim.x * rpb) {
+            float v[8];
+            load8(a + r * ld + c8 * 8, v);
+            if (MODE == 0) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const float d = v[e] - ref[e];
-                s[e] += d;
-                q[e] += d * d;
-            }
-        } else {
-            float xv[8];
-            load8(x + r * C + c8 * 8, xv);
+                for (int e = 0; e < 8; ++e) {
+                    const float d = v[e] - ref[e];
+                    s[e] += d;
+                    q[e] += d * d;
+                }
+            } else {
+                float xv[8];
+                load8(x + r * ld + c8 * 8, xv);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                s[e] += v[e];
-                q[e] += v[e] * (xv[e] - ref[e]);
+                for (int e = 0; e < 8; ++e) {
+                    const float g = (!RELU || xv[e] * sc[e] + sh[e] > 0.f) ? v[e] : 0.f;
+                    s[e] += g;
+                    q[e] += g * (xv[e] - ref[e]);
+                }
             }
         }
-    }
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        red[rr * C + c8 * 8 + e] = s[e];
-        red[2048 + rr * C + c8 * 8 + e] = q[e];
+        for (int e = 0; e < 8; ++e) {
+            red[rr * C + c8 * 8 + e] = s[e];
+            red[2048 + rr * C + c8 * 8 + e] = q[e];
+        }
     }
     __syncthreads();
     for (int c = threadIdx.x; c < C; c += 256) {
@@ -779,90 +796,122 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk,
     k[2 * C + c] = -k1 * (S / n) - k2 * mean[c];
 }
 
-// y = (T)(x * s1[c] + s2[c])   (forward: s1 = scale, s2 = shift)
-// y = (T)(a * k1[c] + x * k2[c] + k3[c])   (backward: a = dy)
-template <typename T, bool BWD>
+// y = (T)(x * s1[c] + s2[c])   (forward: s1 = scale, s2 = shift; RELU: max(0, .))
+// y = (T)(a * k1[c] + x * k2[c] + k3[c])   (backward: a = dy, masked by the ReLU derivative when RELU;
+// k[3C..5C) = the forward's scale / shift)
+template <typename T, bool BWD, bool RELU>
 __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ a, const T* __restrict__ x,
-                                                       const float* __restrict__ k, int64_t rows, int C,
+                                                       const float* __restrict__ k, int64_t rows, int C, int64_t ld,
                                                        T* __restrict__ y) {
     const int c8n = C / 8;
     const int64_t n8 = rows * c8n;
     typedef T t8 __attribute__((ext_vector_type(8)));
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
         const int c0 = (int)(i % c8n) * 8;
+        const int64_t off = (i / c8n) * ld + c0;
         float v[8];
-        load8(a + i * 8, v);
+        load8(a + off, v);
         t8 o;
         if (BWD) {
             float xv[8];
-            load8(x + i * 8, xv);
+            load8(x + off, xv);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] = (T)(v[e] * k[c0 + e] + xv[e] * k[C + c0 + e] + k[2 * C + c0 + e]);
+            for (int e = 0; e < 8; ++e) {
+                const float g = (!RELU || xv[e] * k[3 * C + c0 + e] + k[4 * C + c0 + e] > 0.f) ? v[e] : 0.f;
+                o[e] = (T)(g * k[c0 + e] + xv[e] * k[C + c0 + e] + k[2 * C + c0 + e]);
+            }
         } else {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] = (T)(v[e] * k[c0 + e] + k[C + c0 + e]);
+            for (int e = 0; e < 8; ++e) {
+                const float t = v[e] * k[c0 + e] + k[C + c0 + e];
+                o[e] = (T)(RELU ? fmaxf(t, 0.f) : t);
+            }
         }
-        *(t8*)(y + i * 8) = o;
+        *(t8*)(y + off) = o;
     }
 }
 
-bool bn_shape_ok(int64_t rows, int C) {
+// the forward's scale / shift for the backward's ReLU mask, into k[3C..5C)
+__global__ void bn_mask_affine_kernel(const float* __restrict__ w, const float* __restrict__ b,
+                                      const float* __restrict__ mean, const float* __restrict__ rstd, int C,
+                                      float* __restrict__ k) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= C) return;
+    const float sc = (w ? w[c] : 1.f) * rstd[c];
+    k[3 * C + c] = sc;
+    k[4 * C + c] = (b ? b[c] : 0.f) - mean[c] * sc;
+}
+
+bool bn_shape_ok(int64_t rows, int C, int64_t ld) {
     const int tpr = C / 8;
-    return rows > 0 && C % 8 == 0 && tpr >= 1 && tpr <= 256 && (256 % tpr) == 0;
+    return rows > 0 && C % 8 == 0 && tpr >= 1 && tpr <= 256 && ld >= C && ld % 8 == 0;
 }
 
 }  // namespace
 
 extern "C" int64_t dclip_bn_workspace(int64_t rows, int C) {
-    // partials (nblk x 2C) + scale/shift or the backward coefficients (3C)
-    return (int64_t)BN_NBLK_MAX * 2 * C + 3 * (int64_t)C;
+    (void)rows;
+    return (int64_t)BN_NBLK_MAX * 2 * C + 5 * (int64_t)C;
 }
 
-extern "C" int dclip_bn_fwd(int dt, const void* x, int64_t rows, int C, const float* w, const float* b, float eps,
-                            float momentum, float* running_mean, float* running_var, float* ws, float* mean,
-                            float* rstd, void* y, void* stream) {
+extern "C" int dclip_bn_fwd(int dt, const void* x, int64_t rows, int C, int64_t ld, const float* w, const float* b,
+                            float eps, float momentum, float* running_mean, float* running_var, float* ws, float* mean,
+                            float* rstd, void* y, int relu, void* stream) {
     DCLIP_HOST_CHECK(dt == DCLIP_BF16 || dt == DCLIP_F16, "dclip_bn_fwd: dtype must be bf16/f16");
-    DCLIP_HOST_CHECK(bn_shape_ok(rows, C), "dclip_bn_fwd: need rows > 0 and C / 8 a power of two <= 256 (C = %d)", C);
+    DCLIP_HOST_CHECK(bn_shape_ok(rows, C, ld), "dclip_bn_fwd: need rows > 0, C %% 8 == 0, C <= 2048, ld >= C, "
+                     "ld %% 8 == 0 (C = %d)", C);
     DCLIP_HOST_CHECK(((uintptr_t)x % 16) == 0 && ((uintptr_t)y % 16) == 0, "dclip_bn_fwd: unaligned buffers");
     hipStream_t st = (hipStream_t)stream;
     const int nblk = bn_nblk(rows, C);
     float* ss = ws + (int64_t)BN_NBLK_MAX * 2 * C;
     const unsigned ga = grid_for(rows * (C / 8), 8192);
+#define BN_FWD(T)                                                                                                      \
+    bn_stats_kernel<T, 0, false><<<nblk, 256, 0, st>>>((const T*)x, nullptr, nullptr, nullptr, nullptr, nullptr, rows, \
+                                                       C, ld, ws);                                                     \
+    bn_fwd_finalize_kernel<T><<<(C + 7) / 8, 256, 0, st>>>(ws, nblk, (const T*)x, rows, C, w, b, eps, momentum,        \
+                                                           running_mean, running_var, mean, rstd, ss);                 \
+    if (relu) bn_apply_kernel<T, false, true><<<ga, 256, 0, st>>>((const T*)x, nullptr, ss, rows, C, ld, (T*)y);       \
+    else bn_apply_kernel<T, false, false><<<ga, 256, 0, st>>>((const T*)x, nullptr, ss, rows, C, ld, (T*)y);
     if (dt == DCLIP_BF16) {
-        bn_stats_kernel<bf16, 0><<<nblk, 256, 0, st>>>((const bf16*)x, nullptr, nullptr, rows, C, ws);
-        bn_fwd_finalize_kernel<bf16><<<(C + 7) / 8, 256, 0, st>>>(ws, nblk, (const bf16*)x, rows, C, w, b, eps,
-                                                                      momentum, running_mean, running_var, mean, rstd, ss);
-        bn_apply_kernel<bf16, false><<<ga, 256, 0, st>>>((const bf16*)x, nullptr, ss, rows, C, (bf16*)y);
+        BN_FWD(bf16)
     } else {
-        bn_stats_kernel<f16, 0><<<nblk, 256, 0, st>>>((const f16*)x, nullptr, nullptr, rows, C, ws);
-        bn_fwd_finalize_kernel<f16><<<(C + 7) / 8, 256, 0, st>>>(ws, nblk, (const f16*)x, rows, C, w, b, eps,
-                                                                     momentum, running_mean, running_var, mean, rstd, ss);
-        bn_apply_kernel<f16, false><<<ga, 256, 0, st>>>((const f16*)x, nullptr, ss, rows, C, (f16*)y);
+        BN_FWD(f16)
     }
+#undef BN_FWD
     DCLIP_LAUNCH_CHECK();
     return 0;
 }
 
-extern "C" int dclip_bn_bwd(int dt, const void* dy, const void* x, int64_t rows, int C, const float* w,
-                            const float* mean, const float* rstd, float* ws, void* dx, float* dw, float* db,
-                            void* stream) {
+extern "C" int dclip_bn_bwd(int dt, const void* dy, const void* x, int64_t rows, int C, int64_t ld, const float* w,
+                            const float* b, const float* mean, const float* rstd, float* ws, void* dx, float* dw,
+                            float* db, int relu, void* stream) {
     DCLIP_HOST_CHECK(dt == DCLIP_BF16 || dt == DCLIP_F16, "dclip_bn_bwd: dtype must be bf16/f16");
-    DCLIP_HOST_CHECK(bn_shape_ok(rows, C), "dclip_bn_bwd: need rows > 0 and C / 8 a power of two <= 256 (C = %d)", C);
+    DCLIP_HOST_CHECK(bn_shape_ok(rows, C, ld), "dclip_bn_bwd: need rows > 0, C %% 8 == 0, C <= 2048, ld >= C, "
+                     "ld %% 8 == 0 (C = %d)", C);
     DCLIP_HOST_CHECK(((uintptr_t)dy % 16) == 0 && ((uintptr_t)x % 16) == 0 && ((uintptr_t)dx % 16) == 0,
                      "dclip_bn_bwd: unaligned buffers");
     hipStream_t st = (hipStream_t)stream;
     const int nblk = bn_nblk(rows, C);
     float* k = ws + (int64_t)BN_NBLK_MAX * 2 * C;
     const unsigned ga = grid_for(rows * (C / 8), 8192);
-    if (dt == DCLIP_BF16) {
-        bn_stats_kernel<bf16, 1><<<nblk, 256, 0, st>>>((const bf16*)dy, (const bf16*)x, mean, rows, C, ws);
-        bn_bwd_finalize_kernel<<<(C + 7) / 8, 256, 0, st>>>(ws, nblk, rows, C, w, mean, rstd, dw, db, k);
-        bn_apply_kernel<bf16, true><<<ga, 256, 0, st>>>((const bf16*)dy, (const bf16*)x, k, rows, C, (bf16*)dx);
-    } else {
-        bn_stats_kernel<f16, 1><<<nblk, 256, 0, st>>>((const f16*)dy, (const f16*)x, mean, rows, C, ws);
-        bn_bwd_finalize_kernel<<<(C + 7) / 8, 256, 0, st>>>(ws, nblk, rows, C, w, mean, rstd, dw, db, k);
-        bn_apply_kernel<f16, true><<<ga, 256, 0, st>>>((const f16*)dy, (const f16*)x, k, rows, C, (f16*)dx);
+    if (relu) bn_mask_affine_kernel<<<(C + 255) / 256, 256, 0, st>>>(w, b, mean, rstd, C, k);
+#define BN_BWD(T)                                                                                                      \
+    if (relu) {                                                                                                        \
+        bn_stats_kernel<T, 1, true><<<nblk, 256, 0, st>>>((const T*)dy, (const T*)x, w, b, mean, rstd, rows, C, ld, ws); \
+        bn_bwd_finalize_kernel<<<(C + 7) / 8, 256, 0, st>>>(ws, nblk, rows, C, w, mean, rstd, dw, db, k);               \
+        bn_apply_kernel<T, true, true><<<ga, 256, 0, st>>>((const T*)dy, (const T*)x, k, rows, C, ld, (T*)dx);          \
+    } else {                                                                                                           \
+        bn_stats_kernel<T, 1, false><<<nblk, 256, 0, st>>>((const T*)dy, (const T*)x, w, b, mean, rstd, rows, C, ld,   \
+                                                           ws);                                                        \
+        bn_bwd_finalize_kernel<<<(C + 7) / 8, 256, 0, st>>>(ws, nblk, rows, C, w, mean, rstd, dw, db, k);               \
+        bn_apply_kernel<T, true, false><<<ga, 256, 0, st>>>((const T*)dy, (const T*)x, k, rows, C, ld, (T*)dx);         \
     }
+    if (dt == DCLIP_BF16) {
+        BN_BWD(bf16)
+    } else {
+        BN_BWD(f16)
+    }
+#undef BN_BWD
     DCLIP_LAUNCH_CHECK();
     return 0;
 }

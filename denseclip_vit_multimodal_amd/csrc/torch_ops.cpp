@@ -191,6 +191,20 @@ Tensor transpose2d(const Tensor& x, at::ScalarType dtype) {
     return out;
 }
 
+// out[b][c][r] = x[b][r][c] for r < rows, c < cols (x rows of ld_in elements, batch stride
+// rows*ld_in); r in [rows, rows_pad) written as zeros: (B, cols, rows_pad) in dtype
+Tensor transpose_batched(const Tensor& x, int64_t B, int64_t rows, int64_t cols, int64_t ld_in, int64_t rows_pad,
+                         at::ScalarType dtype) {
+    check_gpu(x, "x");
+    TORCH_CHECK(x.numel() >= B * rows * ld_in && cols <= ld_in && rows_pad >= rows, "transpose_batched: shapes");
+    c10::DeviceGuard g(x.device());
+    Tensor out = at::empty({B, cols, rows_pad}, like(x, dtype));
+    DCLIP_CALL(dclip_transpose(x.data_ptr(), dt_code(x.scalar_type()), rows * ld_in, ld_in, 0, out.data_ptr(),
+                               dt_code(dtype), cols * rows_pad, rows_pad, (int)B, rows, rows_pad, cols, 0, nullptr,
+                               stream_of(x)));
+    return out;
+}
+
 std::tuple<Tensor, Tensor> add_readout_cast(const Tensor& a, const Tensor& b, int64_t ntok, at::ScalarType lp_dtype,
                                             double scale) {
     check_gpu(a, "a"); check_gpu(b, "b", false);
@@ -353,41 +367,88 @@ Tensor bilinear_bwd(const Tensor& dout, int64_t Hi, int64_t Wi) {
     return din;
 }
 
-// ----------------------------------------------------------------------------- BatchNorm (train mode)
-// x: channels-last (B, C, H, W) 16-bit map viewed as (rows, C)
-std::tuple<Tensor, Tensor, Tensor> bn_fwd(const Tensor& x, const c10::optional<Tensor>& w,
-                                          const c10::optional<Tensor>& b, c10::optional<Tensor> running_mean,
-                                          c10::optional<Tensor> running_var, double momentum, double eps) {
-    TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
-                "bn_fwd: channels-last 4-D GPU map");
+// ----------------------------------------------------------------------------- BatchNorm (+ ReLU), train mode
+// rows view of a map: a channels-last 4-D tensor (pitch C) or a 2-D (rows, C) view with unit column
+// stride (a channel slice of a wider buffer: pitch = stride(0))
+struct Rows {
+    int64_t rows, C, ld;
+};
+
+Rows rows_of(const Tensor& x) {
+    TORCH_CHECK(x.is_cuda(), "dclip: BatchNorm input must be a GPU tensor");
+    if (x.dim() == 4) {
+        TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "dclip: BatchNorm map must be channels-last");
+        return {x.numel() / x.size(1), x.size(1), x.size(1)};
+    }
+    TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "dclip: BatchNorm rows must be 2-D with unit column stride");
+    return {x.size(0), x.size(1), x.stride(0)};
+}
+
+std::tuple<Tensor, Tensor> bn_fwd_into(const Tensor& x, const c10::optional<Tensor>& w, const c10::optional<Tensor>& b,
+                                       const c10::optional<Tensor>& running_mean, const c10::optional<Tensor>& running_var,
+                                       double momentum, double eps, bool relu, const Tensor& y) {
+    const Rows r = rows_of(x), ry = rows_of(y);
+    TORCH_CHECK(r.rows == ry.rows && r.C == ry.C && r.ld == ry.ld && x.scalar_type() == y.scalar_type(),
+                "dclip: BatchNorm output must match the input's rows, channels and pitch");
     check_opt(w, "w"); check_opt(b, "b"); check_opt(running_mean, "running_mean"); check_opt(running_var, "running_var");
     c10::DeviceGuard g(x.device());
-    const int64_t C = x.size(1), rows = x.numel() / C;
-    Tensor ws = at::empty({dclip_bn_workspace(rows, (int)C)}, like(x, at::kFloat));
-    Tensor mean = at::empty({C}, like(x, at::kFloat)), rstd = at::empty({C}, like(x, at::kFloat));
+    Tensor ws = at::empty({dclip_bn_workspace(r.rows, (int)r.C)}, like(x, at::kFloat));
+    Tensor mean = at::empty({r.C}, like(x, at::kFloat)), rstd = at::empty({r.C}, like(x, at::kFloat));
+    DCLIP_CALL(dclip_bn_fwd(dt_code(x.scalar_type()), x.data_ptr(), r.rows, (int)r.C, r.ld, optr<float>(w), optr<float>(b),
+                            (float)eps, (float)momentum, optr<float>(running_mean), optr<float>(running_var),
+                            ptr<float>(ws), ptr<float>(mean), ptr<float>(rstd), y.data_ptr(), relu ? 1 : 0, stream_of(x)));
+    return {mean, rstd};
+}
+
+std::tuple<Tensor, Tensor, Tensor> bn_fwd(const Tensor& x, const c10::optional<Tensor>& w,
+                                          const c10::optional<Tensor>& b, const c10::optional<Tensor>& running_mean,
+                                          const c10::optional<Tensor>& running_var, double momentum, double eps,
+                                          bool relu) {
+    TORCH_CHECK(x.dim() == 4, "bn_fwd: a channels-last 4-D map");
     Tensor y = at::empty_like(x, at::MemoryFormat::ChannelsLast);
-    DCLIP_CALL(dclip_bn_fwd(dt_code(x.scalar_type()), x.data_ptr(), rows, (int)C, optr<float>(w), optr<float>(b), (float)eps,
-                            (float)momentum, optr<float>(running_mean), optr<float>(running_var), ptr<float>(ws),
-                            ptr<float>(mean), ptr<float>(rstd), y.data_ptr(), stream_of(x)));
-    return {y, mean, rstd};
+    auto ms = bn_fwd_into(x, w, b, running_mean, running_var, momentum, eps, relu, y);
+    return {y, std::get<0>(ms), std::get<1>(ms)};
+}
+
+// (rows view) y written in place into the caller's buffer
+std::tuple<Tensor, Tensor> bn_fwd_rows(const Tensor& x, const c10::optional<Tensor>& w, const c10::optional<Tensor>& b,
+                                       c10::optional<Tensor> running_mean, c10::optional<Tensor> running_var,
+                                       double momentum, double eps, bool relu, Tensor& y) {
+    return bn_fwd_into(x, w, b, running_mean, running_var, momentum, eps, relu, y);
+}
+
+std::tuple<Tensor, Tensor> bn_bwd_into(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& w,
+                                       const c10::optional<Tensor>& b, const Tensor& mean, const Tensor& rstd, bool relu,
+                                       bool want_w, bool want_b, const Tensor& dx) {
+    const Rows r = rows_of(x), rd = rows_of(dy), rdx = rows_of(dx);
+    TORCH_CHECK(rd.rows == r.rows && rd.C == r.C && rd.ld == r.ld && rdx.ld == r.ld && rdx.rows == r.rows,
+                "dclip: BatchNorm backward tensors must share rows, channels and pitch");
+    TORCH_CHECK(dy.scalar_type() == x.scalar_type() && dx.scalar_type() == x.scalar_type(), "bn_bwd: dtypes must match");
+    check_opt(w, "w"); check_opt(b, "b"); check_gpu(mean, "mean"); check_gpu(rstd, "rstd");
+    c10::DeviceGuard g(x.device());
+    Tensor ws = at::empty({dclip_bn_workspace(r.rows, (int)r.C)}, like(x, at::kFloat));
+    Tensor dw = want_w ? at::empty({r.C}, like(x, at::kFloat)) : at::empty({0}, like(x, at::kFloat));
+    Tensor db = want_b ? at::empty({r.C}, like(x, at::kFloat)) : at::empty({0}, like(x, at::kFloat));
+    DCLIP_CALL(dclip_bn_bwd(dt_code(x.scalar_type()), dy.data_ptr(), x.data_ptr(), r.rows, (int)r.C, r.ld, optr<float>(w),
+                            optr<float>(b), ptr<float>(mean), ptr<float>(rstd), ptr<float>(ws), dx.data_ptr(),
+                            want_w ? ptr<float>(dw) : nullptr, want_b ? ptr<float>(db) : nullptr, relu ? 1 : 0,
+                            stream_of(x)));
+    return {dw, db};
 }
 
 std::tuple<Tensor, Tensor, Tensor> bn_bwd(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& w,
-                                          const Tensor& mean, const Tensor& rstd, bool want_w, bool want_b) {
-    TORCH_CHECK(dy.is_contiguous(at::MemoryFormat::ChannelsLast) && x.is_contiguous(at::MemoryFormat::ChannelsLast),
-                "bn_bwd: channels-last maps");
-    TORCH_CHECK(dy.scalar_type() == x.scalar_type(), "bn_bwd: dy dtype must match x");
-    check_opt(w, "w"); check_gpu(mean, "mean"); check_gpu(rstd, "rstd");
-    c10::DeviceGuard g(x.device());
-    const int64_t C = x.size(1), rows = x.numel() / C;
-    Tensor ws = at::empty({dclip_bn_workspace(rows, (int)C)}, like(x, at::kFloat));
+                                          const c10::optional<Tensor>& b, const Tensor& mean, const Tensor& rstd,
+                                          bool relu, bool want_w, bool want_b) {
+    TORCH_CHECK(x.dim() == 4, "bn_bwd: a channels-last 4-D map");
     Tensor dx = at::empty_like(x, at::MemoryFormat::ChannelsLast);
-    Tensor dw = want_w ? at::empty({C}, like(x, at::kFloat)) : at::empty({0}, like(x, at::kFloat));
-    Tensor db = want_b ? at::empty({C}, like(x, at::kFloat)) : at::empty({0}, like(x, at::kFloat));
-    DCLIP_CALL(dclip_bn_bwd(dt_code(x.scalar_type()), dy.data_ptr(), x.data_ptr(), rows, (int)C, optr<float>(w),
-                            ptr<float>(mean), ptr<float>(rstd), ptr<float>(ws), dx.data_ptr(),
-                            want_w ? ptr<float>(dw) : nullptr, want_b ? ptr<float>(db) : nullptr, stream_of(x)));
-    return {dx, dw, db};
+    auto g = bn_bwd_into(dy, x, w, b, mean, rstd, relu, want_w, want_b, dx);
+    return {dx, std::get<0>(g), std::get<1>(g)};
+}
+
+std::tuple<Tensor, Tensor> bn_bwd_rows(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& w,
+                                       const c10::optional<Tensor>& b, const Tensor& mean, const Tensor& rstd, bool relu,
+                                       bool want_w, bool want_b, Tensor& dx) {
+    return bn_bwd_into(dy, x, w, b, mean, rstd, relu, want_w, want_b, dx);
 }
 
 // ----------------------------------------------------------------------------- neck 3x3 conv
@@ -506,6 +567,7 @@ TORCH_LIBRARY(dclip, m) {
     m.def("gemm_tn(Tensor A, Tensor B) -> Tensor");
     m.def("cast(Tensor x, ScalarType dtype, float scale) -> Tensor");
     m.def("transpose2d(Tensor x, ScalarType dtype) -> Tensor");
+    m.def("transpose_batched(Tensor x, int B, int rows, int cols, int ld_in, int rows_pad, ScalarType dtype) -> Tensor");
     m.def("add_readout_cast(Tensor a, Tensor b, int ntok, ScalarType lp_dtype, float scale) -> (Tensor, Tensor)");
     m.def("attn_fwd(Tensor qkv, int B, int N, int H, float scale) -> (Tensor, Tensor)");
     m.def("attn_fwd_fp8(Tensor qkv, int B, int N, int H) -> (Tensor, Tensor)");
@@ -520,9 +582,13 @@ TORCH_LIBRARY(dclip, m) {
     m.def("bilinear(Tensor x, int Ho, int Wo, ScalarType dtype) -> Tensor");
     m.def("bilinear_bwd(Tensor dout, int Hi, int Wi) -> Tensor");
     m.def("bn_fwd(Tensor x, Tensor? w, Tensor? b, Tensor(a!)? running_mean, Tensor(b!)? running_var, float momentum, "
-          "float eps) -> (Tensor, Tensor, Tensor)");
-    m.def("bn_bwd(Tensor dy, Tensor x, Tensor? w, Tensor mean, Tensor rstd, bool want_w, bool want_b) -> "
-          "(Tensor, Tensor, Tensor)");
+          "float eps, bool relu) -> (Tensor, Tensor, Tensor)");
+    m.def("bn_bwd(Tensor dy, Tensor x, Tensor? w, Tensor? b, Tensor mean, Tensor rstd, bool relu, bool want_w, "
+          "bool want_b) -> (Tensor, Tensor, Tensor)");
+    m.def("bn_fwd_rows(Tensor x, Tensor? w, Tensor? b, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
+          "float momentum, float eps, bool relu, Tensor(c!) y) -> (Tensor, Tensor)");
+    m.def("bn_bwd_rows(Tensor dy, Tensor x, Tensor? w, Tensor? b, Tensor mean, Tensor rstd, bool relu, bool want_w, "
+          "bool want_b, Tensor(a!) dx) -> (Tensor, Tensor)");
     m.def("conv3x3(int mode, Tensor X, int x_bstride, int x_off, int x_ld, int B, int H, int W, int Cin, Tensor Wt, "
           "int Nout, Tensor(a!) out, int out_ld, int out_gap, int out_off, int accumulate) -> ()");
     m.def("conv3x3_wgrad(Tensor dY, int ldy, int Nout, Tensor X, int x_bstride, int x_off, int x_ld, int B, int H, "
@@ -544,6 +610,7 @@ TORCH_LIBRARY_IMPL(dclip, CUDA, m) {
     m.impl("gemm_tn", &gemm_tn);
     m.impl("cast", &cast);
     m.impl("transpose2d", &transpose2d);
+    m.impl("transpose_batched", &transpose_batched);
     m.impl("add_readout_cast", &add_readout_cast);
     m.impl("attn_fwd", &attn_fwd);
     m.impl("attn_fwd_fp8", &attn_fwd_fp8);
@@ -559,6 +626,8 @@ TORCH_LIBRARY_IMPL(dclip, CUDA, m) {
     m.impl("bilinear_bwd", &bilinear_bwd);
     m.impl("bn_fwd", &bn_fwd);
     m.impl("bn_bwd", &bn_bwd);
+    m.impl("bn_fwd_rows", &bn_fwd_rows);
+    m.impl("bn_bwd_rows", &bn_bwd_rows);
     m.impl("conv3x3", &conv3x3);
     m.impl("conv3x3_wgrad", &conv3x3_wgrad);
     m.impl("upsample_ce", &upsample_ce);

@@ -3,13 +3,18 @@ builds for 'FPNHead' / 'FCNHeadDepth', denseclip.py:22-23, 305-309, 343-349)."""
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import ops
 from .models import BatchNorm2d, Registry
 
 
 class FCNHead(nn.Sequential):
     """torchvision.models.segmentation.fcn.FCNHead: conv3x3(in -> in/4, no bias), BN, ReLU,
     Dropout(0.1), conv1x1(in/4 -> channels).  DenseCLIP then assigns a `.classifier`
-    conv, which nn.Sequential appends to the module sequence (so it runs last)."""
+    conv, which nn.Sequential appends to the module sequence (so it runs last).
+
+    On a 16-bit GPU map the forward runs on the HIP kernels (ops.fcn_head): the 3x3 conv as an
+    implicit GEMM, BN + ReLU fused, and the two trailing 1x1 convs merged into one GEMM
+    (ops.MergedPointwiseFn) — same parameters, same function."""
 
     def __init__(self, in_channels, channels):
         inter = in_channels // 4
@@ -20,6 +25,11 @@ class FCNHead(nn.Sequential):
             nn.Dropout(0.1),
             nn.Conv2d(inter, channels, 1),
         )
+
+    def forward(self, x):
+        if ops.fcn_head_hip_ok(self, x):
+            return ops.fcn_head(self, x)
+        return super().forward(x)
 
 
 class ConvModule(nn.Module):

@@ -26,15 +26,10 @@ class BatchNorm2d(nn.BatchNorm2d):
     gpurun_out/bn_probe.log)."""
 
     def forward(self, x):
-        f32 = all(t is None or t.dtype == torch.float32
-                  for t in (self.weight, self.bias, self.running_mean, self.running_var))
-        if self.training and self.track_running_stats and self.momentum is not None and f32 and ops.bn_supported(x):
+        if ops.bn_hip_ok(self, x):
             # batch statistics on the HIP kernels (torch's native channels-last kernels run at
             # ~0.12 TB/s on the neck maps): dclip_bn_fwd / dclip_bn_bwd
-            if self.num_batches_tracked is not None:
-                self.num_batches_tracked.add_(1)
-            return ops.BatchNormFn.apply(x, self.weight, self.bias, self.running_mean, self.running_var,
-                                         self.momentum, self.eps)
+            return ops.bn_train(self, x)
         if x.is_cuda:
             with torch.backends.cudnn.flags(enabled=False):
                 return super().forward(x)
@@ -448,6 +443,8 @@ class ViTFeatureFusionNeck(nn.Module):
             y = ops.Conv1x1Fn.apply(x, conv.weight, conv.bias, x.dtype)
         else:
             y = conv(x)
+        if ops.bn_hip_ok(bn, y):
+            return ops.bn_train(bn, y, relu=True)  # BN + ReLU in one pass each way
         return act(bn(y))
 
     def forward(self, features):
@@ -456,8 +453,16 @@ class ViTFeatureFusionNeck(nn.Module):
         if not features[0].is_cuda:
             feats = [layer(f) for layer, f in zip(self.process_layers, features)]
             return [self.fusion_layer(torch.cat(feats, dim=1))]
-        feats = [self._conv_bn_relu(layer, f) for layer, f in zip(self.process_layers, features)]
-        cat = torch.cat(feats, dim=1)  # channels-last in, channels-last out
+        if ops.neck_levels_hip_ok(self.process_layers, features):
+            # train mode: the 12 ConvModules write their slices of one concatenated buffer
+            # (no torch.cat), BN + ReLU fused (ops.NeckLevelsFn)
+            layers = list(self.process_layers)
+            cat = ops.NeckLevelsFn.apply((tuple(layer[1] for layer in layers), features[0].dtype), *features,
+                                         *[layer[0].weight for layer in layers], *[layer[1].weight for layer in layers],
+                                         *[layer[1].bias for layer in layers])
+        else:
+            feats = [self._conv_bn_relu(layer, f) for layer, f in zip(self.process_layers, features)]
+            cat = torch.cat(feats, dim=1)  # channels-last in, channels-last out
         return [self._conv_bn_relu(self.fusion_layer, cat)]
 
 

@@ -587,37 +587,50 @@ class ReadoutFn(torch.autograd.Function):
 
 
 def bn_supported(x):
-    """Train-mode BatchNorm on the HIP kernels: 16-bit channels-last maps, C / 8 a power of two
-    <= 256 (the neck's 128 / 256 channels, the heads' in // 4)."""
+    """Train-mode BatchNorm on the HIP kernels: 16-bit channels-last maps, C % 8 == 0, C <= 2048."""
     if not (x.is_cuda and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float16)):
         return False
     C = x.shape[1]
-    t = C // 8
-    return C % 8 == 0 and 1 <= t <= 256 and (t & (t - 1)) == 0 and x.numel() > 0 and \
-        x.is_contiguous(memory_format=torch.channels_last)
+    return C % 8 == 0 and 8 <= C <= 2048 and x.numel() > 0 and x.is_contiguous(memory_format=torch.channels_last)
 
 
 class BatchNormFn(torch.autograd.Function):
     """nn.BatchNorm2d in train mode (batch statistics; the running statistics updated in place
-    like torch's) on a channels-last map viewed as (B*H*W, C): dclip_bn_fwd / dclip_bn_bwd
-    (reference models.py:13-20 ConvModule norm, heads' FCNHead norm)."""
+    like torch's), optionally followed by the ReLU of a ConvModule / FCNHead (fused: the backward
+    recomputes the mask from x), on a channels-last map viewed as (B*H*W, C): dclip_bn_fwd /
+    dclip_bn_bwd (reference models.py:13-20 ConvModule norm + act, heads' FCNHead norm + ReLU)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps):
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu=False):
         w = weight.detach() if weight is not None else None
         b = bias.detach() if bias is not None else None
         _check(w, b, running_mean, running_var, strided=(x,))
-        y, mean, rstd = D().bn_fwd(x, w, b, running_mean, running_var, float(momentum), float(eps))
-        ctx.save_for_backward(x, w, mean, rstd)
+        y, mean, rstd = D().bn_fwd(x, w, b, running_mean, running_var, float(momentum), float(eps), bool(relu))
+        ctx.save_for_backward(x, w, b, mean, rstd)
         ctx.has_w = (weight is not None, bias is not None)
+        ctx.relu = bool(relu)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, w, mean, rstd = ctx.saved_tensors
+        x, w, b, mean, rstd = ctx.saved_tensors
         dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last)
-        dx, dw, db = D().bn_bwd(dy, x, w, mean, rstd, ctx.has_w[0], ctx.has_w[1])
-        return dx, dw if ctx.has_w[0] else None, db if ctx.has_w[1] else None, None, None, None, None
+        dx, dw, db = D().bn_bwd(dy, x, w, b, mean, rstd, ctx.relu, ctx.has_w[0], ctx.has_w[1])
+        return dx, dw if ctx.has_w[0] else None, db if ctx.has_w[1] else None, None, None, None, None, None
+
+
+def bn_train(bn, x, relu=False):
+    """`bn` (an nn.BatchNorm2d in train mode) on x via BatchNormFn, then the fused ReLU; the
+    module's num_batches_tracked advances as torch's does.  Caller checks bn_supported(x)."""
+    if bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
+    return BatchNormFn.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum, bn.eps, relu)
+
+
+def bn_hip_ok(bn, x):
+    """Whether `bn` in its current mode runs on the HIP batch-norm kernels for input x."""
+    f32 = all(t is None or t.dtype == torch.float32 for t in (bn.weight, bn.bias, bn.running_mean, bn.running_var))
+    return bn.training and bn.track_running_stats and bn.momentum is not None and f32 and bn_supported(x)
 
 
 class UpsampleFn(torch.autograd.Function):
@@ -738,6 +751,136 @@ class Conv3x3Fn(torch.autograd.Function):
         return dx, dw, None
 
 
+def _conv3x3_rows(weight, cdt):
+    """(Cout, Cin, 3, 3) -> cached (cp, 9*Cin) rows in (ky, kx, ci) order, zero rows past Cout."""
+    Cout, Cin = weight.shape[:2]
+    cp = _pad64(Cout)
+
+    def rows(w):
+        r = w.permute(0, 2, 3, 1).reshape(Cout, 9 * Cin)
+        return torch.cat([r, r.new_zeros(cp - Cout, 9 * Cin)]) if cp > Cout else r
+    return WEIGHTS.get_with(weight, cdt, "conv3x3_rows", rows)
+
+
+def _conv3x3_dgrad_rows(weight, cdt):
+    """(Cout, Cin, 3, 3) -> cached (Cin, 9*cp): [ci][tap][co], zero columns past Cout."""
+    Cout, Cin = weight.shape[:2]
+    cp = _pad64(Cout)
+
+    def trows(w):
+        t = w.permute(1, 2, 3, 0)
+        if cp > Cout:
+            t = torch.cat([t, t.new_zeros(Cin, 3, 3, cp - Cout)], dim=3)
+        return t.reshape(Cin, 9 * cp)
+    return WEIGHTS.get_with(weight, cdt, "conv3x3_dgrad", trows)
+
+
+class NeckLevelsFn(torch.autograd.Function):
+    """The fusion neck's per-level ConvModules + concatenation (reference models.py:741-765:
+    12 x [3x3 conv C -> Ci, BN, ReLU], torch.cat over channels) in train mode, without the
+    concatenation copy: level l's implicit-GEMM conv writes its Ci channels straight into columns
+    [l*Ci, (l+1)*Ci) of one (B*H*W, L*Ci) pre-activation buffer, and its BN + ReLU (batch
+    statistics, fused) writes the same columns of the concatenated output, which the 1x1 fusion
+    conv reads as it is.  The backward runs the same way on column slices: fused BN + ReLU
+    backward per level into a dgrad buffer whose slices feed each level's dgrad / wgrad convs.
+    Inputs: L maps (channels-last views, e.g. token-buffer read-outs), then per level the conv
+    weight, BN weight, BN bias; the BN modules are in meta (running statistics updated in place)."""
+
+    @staticmethod
+    def forward(ctx, meta, *args):
+        bns, cdt = meta
+        L = len(bns)
+        maps = args[:L]
+        convw = args[L:2 * L]
+        bnw = args[2 * L:3 * L]
+        bnb = args[3 * L:4 * L]
+        B, Cin, H, W = maps[0].shape
+        Ci = convw[0].shape[0]
+        M, LC = B * H * W, L * Ci
+        pre = torch.empty(M, LC, dtype=cdt, device=maps[0].device)
+        out = torch.empty(M, LC, dtype=cdt, device=maps[0].device)
+        geo, stats = [], []
+        for l in range(L):
+            xr, bs, ld = pixel_rows(maps[l], cdt)
+            D().conv3x3(0, xr, bs, 0, ld, B, H, W, Cin, _conv3x3_rows(convw[l], cdt), Ci, pre[:, l * Ci:], LC, 0, 0, 0)
+            bn = bns[l]
+            if bn.num_batches_tracked is not None:
+                bn.num_batches_tracked.add_(1)
+            mean, rstd = D().bn_fwd_rows(pre[:, l * Ci:(l + 1) * Ci], bnw[l].detach(), bnb[l].detach(), bn.running_mean,
+                                         bn.running_var, float(bn.momentum), float(bn.eps), True,
+                                         out[:, l * Ci:(l + 1) * Ci])
+            geo.append((xr, bs, ld))
+            stats += [mean, rstd]
+        ctx.save_for_backward(pre, *[g[0] for g in geo], *convw, *bnw, *bnb, *stats)
+        ctx.meta = (L, B, Cin, H, W, Ci, cdt, [(g[1], g[2]) for g in geo], [m.dtype for m in maps],
+                    [tuple(m.stride()) for m in maps], [g[0] is m for g, m in zip(geo, maps)])
+        return out.as_strided((B, LC, H, W), (H * W * LC, 1, W * LC, LC))
+
+    @staticmethod
+    def backward(ctx, dout):
+        L, B, Cin, H, W, Ci, cdt, bsld, in_dts, in_strides, in_place = ctx.meta
+        saved = ctx.saved_tensors
+        pre = saved[0]
+        xrs = saved[1:1 + L]
+        convw = saved[1 + L:1 + 2 * L]
+        bnw = saved[1 + 2 * L:1 + 3 * L]
+        bnb = saved[1 + 3 * L:1 + 4 * L]
+        stats = saved[1 + 4 * L:]
+        M, LC = B * H * W, L * Ci
+        d = dout.to(cdt).permute(0, 2, 3, 1).reshape(M, LC)
+        if not d.is_contiguous():
+            d = d.contiguous()
+        dpre = torch.empty(M, LC, dtype=cdt, device=d.device)
+        need = ctx.needs_input_grad  # (meta, maps..., convw..., bnw..., bnb...)
+        dmaps, dconv, dbnw, dbnb = [None] * L, [None] * L, [None] * L, [None] * L
+        tiles = (Ci + 127) // 128 * (9 * Cin // 128)
+        splits = max(1, min(32, 512 // max(1, tiles), M // 4096 or 1))
+        for l in range(L):
+            sl = slice(l * Ci, (l + 1) * Ci)
+            dbnw[l], dbnb[l] = D().bn_bwd_rows(d[:, sl], pre[:, sl], bnw[l].detach(), bnb[l].detach(), stats[2 * l],
+                                               stats[2 * l + 1], True, True, True, dpre[:, sl])
+            bs, ld = bsld[l]
+            if need[1 + l]:  # input gradient: the dgrad conv, in the input's own layout when it is a token view
+                w_t = _conv3x3_dgrad_rows(convw[l], cdt)
+                if in_place[l] and in_strides[l][0] == bs:
+                    gap_rows = (bs - H * W * ld) // ld
+                    buf = torch.zeros(B * bs, dtype=cdt, device=d.device)
+                    D().conv3x3(1, dpre[:, l * Ci:], H * W * LC, 0, LC, B, H, W, Ci, w_t, Cin, buf, ld, gap_rows,
+                                gap_rows, 0)
+                    dm = buf.as_strided((B, Cin, H, W), (bs, 1, W * ld, ld), gap_rows * ld)
+                else:
+                    buf = torch.empty(M, Cin, dtype=cdt, device=d.device)
+                    D().conv3x3(1, dpre[:, l * Ci:], H * W * LC, 0, LC, B, H, W, Ci, w_t, Cin, buf, Cin, 0, 0, 0)
+                    dm = buf.as_strided((B, Cin, H, W), (H * W * Cin, 1, W * Cin, Cin))
+                dmaps[l] = dm if in_dts[l] == cdt else dm.to(in_dts[l])
+            if need[1 + L + l]:
+                e0 = _tic()
+                dwr = D().conv3x3_wgrad(dpre[:, l * Ci:], LC, Ci, xrs[l], bs, 0, ld, B, H, W, Cin, splits)
+                _toc("conv_wgrad", e0)
+                dconv[l] = dwr[:Ci].view(Ci, 3, 3, Cin).permute(0, 3, 1, 2).contiguous().to(convw[l].dtype)
+        return (None, *dmaps, *dconv, *dbnw, *dbnb)
+
+
+def neck_levels_hip_ok(layers, feats):
+    """Every level a 3x3 ConvModule with a train-mode BN the HIP kernels take, 16-bit GPU maps
+    of one shape, Cin % 128 == 0, Ci % 8 == 0 and Ci <= 2048 / levels."""
+    if not feats or not all(f.is_cuda and f.dim() == 4 and f.dtype in (torch.bfloat16, torch.float16) for f in feats):
+        return False
+    if len({(tuple(f.shape), f.dtype) for f in feats}) != 1:
+        return False
+    Ci = layers[0][0].weight.shape[0]
+    for layer in layers:
+        conv, bn = layer[0], layer[1]
+        if conv.kernel_size != (3, 3) or conv.bias is not None or conv.weight.shape[0] != Ci or \
+                not conv3x3_supported(feats[0], conv.weight):
+            return False
+        f32 = all(t is not None and t.dtype == torch.float32 for t in (bn.weight, bn.bias, bn.running_mean,
+                                                                       bn.running_var))
+        if not (bn.training and bn.track_running_stats and bn.momentum is not None and f32):
+            return False
+    return Ci % 64 == 0 and len(layers) * Ci <= 2048
+
+
 def conv3x3_supported(xmap, weight):
     return (xmap.is_cuda and xmap.dim() == 4 and weight.shape[2:] == (3, 3) and xmap.shape[1] % 128 == 0
             and weight.shape[1] == xmap.shape[1])
@@ -783,6 +926,91 @@ class Conv1x1Fn(torch.autograd.Function):
 def conv1x1_supported(xmap, weight):
     return (xmap.is_cuda and xmap.dim() == 4 and weight.shape[2:] == (1, 1) and xmap.shape[1] % 64 == 0
             and weight.shape[0] % 64 == 0)  # K of the forward and of the input-gradient GEMM
+
+
+# ============================================================================ FCN heads
+class MergedPointwiseFn(torch.autograd.Function):
+    """The FCN head's tail — 1x1 conv (Cin -> C1, bias) then the classifier 1x1 conv (C1 -> K,
+    bias) (torchvision FCNHead + DenseCLIP's classifier, reference denseclip.py:305-309,
+    343-349) — as ONE MFMA GEMM with the merged weight Wc W1 (K x Cin) and bias Wc b1 + bc: the
+    (B, C1, H, W) intermediate never exists.  The backward needs it only through
+    dWc = dY^T h = (dY^T X) W1^T + colsum(dY) b1^T, so it runs two K-row GEMMs on the pixel rows
+    (dX, and dY^T X by the TN weight-gradient GEMM) and tiny K x Cin products.  Output: NCHW
+    (B, K, H, W) in the compute dtype (the head's logits)."""
+
+    @staticmethod
+    def forward(ctx, y, w1, b1, wc, bc, cdt):
+        B, Cin, H, W = y.shape
+        C1, K = w1.shape[0], wc.shape[0]
+        Kp = _pad64(K)
+        with torch.autocast("cuda", enabled=False):
+            W1m = w1.detach().reshape(C1, Cin).float()
+            Wcm = wc.detach().reshape(K, C1).float()
+            Wm = Wcm @ W1m
+            bm = Wcm @ b1.detach().float() + bc.detach().float()
+        Wp = torch.zeros(Kp, Cin, dtype=cdt, device=y.device)
+        Wp[:K] = Wm
+        bp = torch.zeros(Kp, dtype=torch.float32, device=y.device)
+        bp[:K] = bm
+        y2 = y.to(cdt).permute(0, 2, 3, 1).reshape(B * H * W, Cin)
+        if not y2.is_contiguous():
+            y2 = y2.contiguous()
+        rows = gemm(y2, Wp, bias=bp)  # (B*H*W, Kp)
+        out = D().transpose_batched(rows, B, H * W, K, Kp, H * W, cdt)  # (B, K, H*W)
+        ctx.save_for_backward(y2, w1, b1, wc, Wp)
+        ctx.meta = (B, Cin, H, W, C1, K, Kp, y.dtype, cdt)
+        return out.view(B, K, H, W)
+
+    @staticmethod
+    def backward(ctx, dout):
+        y2, w1, b1, wc, Wp = ctx.saved_tensors
+        B, Cin, H, W, C1, K, Kp, in_dt, cdt = ctx.meta
+        dY = D().transpose_batched(dout.contiguous(), B, K, H * W, H * W, Kp, cdt).view(B * H * W, Kp)
+        need = ctx.needs_input_grad
+        dy = None
+        if need[0]:
+            dX = gemm(dY, transpose2d(Wp, cdt))  # (B*H*W, Cin)
+            dy = dX.as_strided((B, Cin, H, W), (H * W * Cin, 1, W * Cin, Cin))
+            if in_dt != cdt:
+                dy = dy.to(in_dt)
+        dw1 = db1 = dwc = dbc = None
+        if any(need[1:5]):
+            G, cs = weight_grad(dY, y2)  # (Kp, Cin) = dY^T X, colsum(dY)
+            with torch.autocast("cuda", enabled=False):
+                G, cs = G[:K], cs[:K]
+                W1m = w1.detach().reshape(C1, Cin).float()
+                Wcm = wc.detach().reshape(K, C1).float()
+                dwc = (G @ W1m.t() + cs[:, None] * b1.detach().float()[None, :]).reshape(wc.shape).to(wc.dtype)
+                dw1 = (Wcm.t() @ G).reshape(w1.shape).to(w1.dtype)
+                db1 = (Wcm.t() @ cs).to(b1.dtype)
+                dbc = cs.to(wc.dtype)
+        return dy, dw1, db1, dwc, dbc, None
+
+
+def fcn_head_hip_ok(head, x):
+    """FCNHead + classifier in the layout DenseCLIP builds (conv3x3 no-bias, BN, ReLU, Dropout,
+    conv1x1 + bias, classifier conv1x1 + bias) on a 16-bit GPU map."""
+    if len(head) != 6 or not (x.is_cuda and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float16)):
+        return False
+    c3, _, _, _, c1, cl = head
+    return (c3.kernel_size == (3, 3) and c3.padding == (1, 1) and c3.stride == (1, 1) and c3.bias is None
+            and c1.kernel_size == (1, 1) and cl.kernel_size == (1, 1) and c1.bias is not None and cl.bias is not None
+            and c1.stride == (1, 1) and cl.stride == (1, 1) and c1.weight.shape[1] % 64 == 0
+            and conv3x3_supported(x, c3.weight) and c1.groups == 1 and cl.groups == 1)
+
+
+def fcn_head(head, x):
+    """FCNHead forward on the HIP kernels: implicit-GEMM 3x3 conv, BN + ReLU (batch statistics
+    in train mode; torch's eval BN otherwise), Dropout (torch), merged 1x1 tail."""
+    c3, bn, relu, drop, c1, cl = head
+    cdt = x.dtype
+    y = Conv3x3Fn.apply(x, c3.weight, cdt)
+    if bn_hip_ok(bn, y):
+        y = bn_train(bn, y, relu=True)
+    else:
+        y = relu(bn(y))
+    y = drop(y)
+    return MergedPointwiseFn.apply(y, c1.weight, c1.bias, cl.weight, cl.bias, cdt)
 
 
 # ============================================================================ fused head losses

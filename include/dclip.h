@@ -77,7 +77,7 @@ int dclip_abi_version(void);
 #define DCLIP_OPT_ATTN_DKDV_QS 5     /* dK/dV pass query rows per barrier: 64 (default) or 128 */
 #define DCLIP_OPT_ATTN_BWD_KERNEL 7  /* 0 (default): CLS-split passes when N-1 is a multiple of 256; 1: generic */
 #define DCLIP_OPT_ATTN_FWD_KERNEL 6  /* 0 (default): CLS-split kernel when N-1 is a multiple of the query block; 1: generic */
-#define DCLIP_OPT_ATTN_BWD_BLOCK 8   /* 0 (default): register-blocked CLS-split backward passes (64 rows per wave); 1: 32 rows per wave */
+#define DCLIP_OPT_ATTN_BWD_BLOCK 8   /* 0 (default): software-pipelined CLS-split dK/dV pass; 1: the unpipelined one */
 #define DCLIP_OPT_COUNT 9
 int dclip_set_option(int id, int value);
 
@@ -288,20 +288,23 @@ int dclip_cast(const void* in, int in_dt, void* out, int out_dt, int64_t n, floa
 int dclip_add_readout_cast(const float* a, const void* b, int b_dt, float* sum, void* lp, int lp_dt,
                            int64_t rows, int cols, int ntok, float scale, void* stream);
 
-/* Train-mode BatchNorm2d on a channels-last 16-bit map viewed as (rows = B*H*W, C), C / 8 a
- * power of two <= 256 (replaces nn.BatchNorm2d in the neck's ConvModules, models.py:13-20, and
- * the FCN heads; torch.nn.functional.batch_norm semantics: biased batch variance for the
- * normalisation, unbiased for running_var, running = (1 - momentum) running + momentum batch).
- * w, b, running_mean / running_var may be NULL.  ws: dclip_bn_workspace(rows, C) floats.
- * Forward writes mean / rstd (f32, C) for the backward; the backward writes dx (dt) and, when
- * non-null, dw / db (f32, C). */
+/* Train-mode BatchNorm2d (+ optionally the ReLU after it) on a channels-last 16-bit map viewed as
+ * rows (B*H*W) of C channels at a row pitch of ld elements (ld = C for a whole map; larger for a
+ * channel slice of a wider buffer, e.g. one level of the neck's concatenation).  Replaces
+ * nn.BatchNorm2d + nn.ReLU in the neck's ConvModules (models.py:13-20) and the FCN heads;
+ * torch.nn.functional.batch_norm semantics: biased batch variance for the normalisation,
+ * unbiased for running_var, running = (1 - momentum) running + momentum batch.  C % 8 == 0,
+ * C <= 2048, ld % 8 == 0.  w, b, running_mean / running_var may be NULL.  ws:
+ * dclip_bn_workspace(rows, C) floats.  Forward: y = [relu](bn(x)) (same pitch as x), mean /
+ * rstd (f32, C) for the backward.  Backward (relu: dy masked where bn(x) <= 0, recomputed from x):
+ * dx (dt, same pitch) and, when non-null, dw / db (f32, C). */
 int64_t dclip_bn_workspace(int64_t rows, int C);
-int dclip_bn_fwd(int dt, const void* x, int64_t rows, int C, const float* w, const float* b, float eps,
-                 float momentum, float* running_mean, float* running_var, float* ws, float* mean,
-                 float* rstd, void* y, void* stream);
-int dclip_bn_bwd(int dt, const void* dy, const void* x, int64_t rows, int C, const float* w,
-                 const float* mean, const float* rstd, float* ws, void* dx, float* dw, float* db,
-                 void* stream);
+int dclip_bn_fwd(int dt, const void* x, int64_t rows, int C, int64_t ld, const float* w, const float* b,
+                 float eps, float momentum, float* running_mean, float* running_var, float* ws, float* mean,
+                 float* rstd, void* y, int relu, void* stream);
+int dclip_bn_bwd(int dt, const void* dy, const void* x, int64_t rows, int C, int64_t ld, const float* w,
+                 const float* b, const float* mean, const float* rstd, float* ws, void* dx, float* dw,
+                 float* db, int relu, void* stream);
 
 #ifdef __cplusplus
 }

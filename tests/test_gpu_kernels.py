@@ -790,3 +790,103 @@ def test_batchnorm_eval_and_nchw_use_torch():
     x = torch.randn(2, 64, 4, 4, device=DEV).to(torch.bfloat16)
     assert not O.bn_supported(x)  # NCHW
     assert not O.bn_supported(x.float().contiguous(memory_format=torch.channels_last))
+
+
+# ----------------------------------------------------------------------------- BN + ReLU, heads, neck
+@pytest.mark.parametrize("C,ld", [(64, 64), (128, 1536), (1536, 1536), (256, 264)])
+@pytest.mark.parametrize("relu", [False, True])
+def test_bn_rows_fused_relu(C, ld, relu):
+    """Train-mode BatchNorm (+ ReLU) on a channel slice of a wider row buffer (the neck's
+    concatenation) vs F.batch_norm (+ relu) in fp32 on the same 16-bit values: output, running
+    statistics, input / weight / bias gradients."""
+    O = ops()
+    rows = 3000
+    buf = torch.randn(rows, ld, device=DEV).to(torch.bfloat16) * 2 + 0.5
+    x = buf[:, :C]
+    w = torch.rand(C, device=DEV) + 0.5
+    b = torch.randn(C, device=DEV)
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    out = torch.full((rows, ld), float("nan"), device=DEV).to(torch.bfloat16)
+    mean, rstd = O.D().bn_fwd_rows(x, w, b, rm, rv, 0.1, 1e-5, relu, out[:, :C])
+    xr = x.float().clone().requires_grad_(True)
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    rm2, rv2 = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    ref = F.batch_norm(xr, rm2, rv2, wr, br, training=True, momentum=0.1, eps=1e-5)
+    if relu:
+        ref = F.relu(ref)
+    assert rel_err(out[:, :C].float(), ref) < 1e-2
+    assert rel_err(rm, rm2) < 1e-5 and rel_err(rv, rv2) < 1e-5
+    g = torch.randn(rows, ld, device=DEV).to(torch.bfloat16)
+    ref.backward(g[:, :C].float())
+    dx = torch.empty(rows, ld, device=DEV, dtype=torch.bfloat16)
+    dw, db = O.D().bn_bwd_rows(g[:, :C], x, w, b, mean, rstd, relu, True, True, dx[:, :C])
+    assert rel_err(dx[:, :C].float(), xr.grad) < 2e-2
+    assert rel_err(dw, wr.grad) < 1e-2 and rel_err(db, br.grad) < 1e-2
+
+
+@pytest.mark.parametrize("K,C1", [(19, 256), (1, 128)])
+def test_fcn_head_hip_matches_sequential(K, C1):
+    """FCNHead + classifier (train-mode BN, dropout off) on the HIP path — implicit-GEMM 3x3 conv,
+    fused BN + ReLU, merged 1x1 tail — vs the same module's plain torch forward in fp32 on the same
+    bf16 input: logits and every parameter gradient."""
+    from denseclip_vit_multimodal_amd.heads import FCNHead
+    torch.manual_seed(1)
+    head = FCNHead(256, C1)
+    head.classifier = torch.nn.Conv2d(C1, K, 1)
+    for m in head.modules():
+        if isinstance(m, torch.nn.Conv2d):
+            torch.nn.init.normal_(m.weight, 0, m.weight[0].numel() ** -0.5)
+            if m.bias is not None:
+                torch.nn.init.normal_(m.bias, 0, 0.1)
+    head = head.to(DEV).train()
+    head[3].p = 0.0
+    import copy
+    ref = copy.deepcopy(head)
+    x = torch.randn(2, 256, 12, 20, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    from denseclip_vit_multimodal_amd import ops as O
+    assert O.fcn_head_hip_ok(head, x)
+    y = head(x)
+    xr = x.detach().float().requires_grad_(True)
+    yr = torch.nn.Sequential.forward(ref, xr)
+    assert y.shape == yr.shape == (2, K, 12, 20)
+    assert rel_err(y.float(), yr) < 2e-2
+    g = torch.randn_like(yr)
+    y.float().backward(g)
+    yr.backward(g)
+    assert rel_err(x.grad.float(), xr.grad) < 3e-2
+    for (n, p), (_, pr) in zip(head.named_parameters(), ref.named_parameters()):
+        assert rel_err(p.grad, pr.grad) < 3e-2, n
+    assert rel_err(head[1].running_mean, ref[1].running_mean) < 1e-2
+
+
+def test_neck_levels_fn_matches_per_level_path():
+    """The concat-free neck (NeckLevelsFn: 12 implicit-GEMM convs writing slices of one buffer,
+    fused BN + ReLU on the slices) vs the per-level ConvModules + torch.cat, both train mode, on
+    token-buffer read-out views: fused output and the gradients of maps and parameters."""
+    import copy
+    from denseclip_vit_multimodal_amd.models import ViTFeatureFusionNeck
+    from denseclip_vit_multimodal_amd import ops as O
+    torch.manual_seed(2)
+    L, B, C, H, W = 4, 2, 256, 8, 12
+    neck = ViTFeatureFusionNeck([C] * L, 256, 128).to(DEV).train()
+    ref = copy.deepcopy(neck)
+    Nt = 1 + H * W
+    bufs = [torch.randn(B * Nt, C, device=DEV).to(torch.bfloat16).requires_grad_(True) for _ in range(L)]
+    maps = [b.as_strided((B, C, H, W), (Nt * C, 1, W * C, C), C) for b in bufs]
+    assert O.neck_levels_hip_ok(neck.process_layers, maps)
+    out = neck(maps)[0]
+    bufs_r = [b.detach().clone().requires_grad_(True) for b in bufs]
+    maps_r = [b.as_strided((B, C, H, W), (Nt * C, 1, W * C, C), C) for b in bufs_r]
+    feats = [ref._conv_bn_relu(layer, f) for layer, f in zip(ref.process_layers, maps_r)]
+    out_r = ref._conv_bn_relu(ref.fusion_layer, torch.cat(feats, dim=1))
+    assert rel_err(out.float(), out_r.float()) < 1e-2
+    g = torch.randn(out.shape, device=DEV)
+    (out.float() * g).sum().backward()
+    (out_r.float() * g).sum().backward()
+    for b, br in zip(bufs, bufs_r):
+        assert rel_err(b.grad.float(), br.grad.float()) < 2e-2
+    for (n, p), (_, pr) in zip(neck.named_parameters(), ref.named_parameters()):
+        assert rel_err(p.grad, pr.grad) < 2e-2, n
+    for (n, bu), (_, br) in zip(neck.named_buffers(), ref.named_buffers()):
+        assert rel_err(bu.float(), br.float()) < 1e-4, n
