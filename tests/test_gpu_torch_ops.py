@@ -65,7 +65,10 @@ def test_opcheck_resize_and_bn():
     _opcheck(D().bilinear_bwd, (torch.randn(2, 19, 64, 128, device=DEV), 8, 16))
     m = torch.randn(2, 128, 6, 10, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     _opcheck(D().bn_fwd, (m, torch.rand(128, device=DEV), torch.randn(128, device=DEV), torch.zeros(128, device=DEV),
-                          torch.ones(128, device=DEV), 0.1, 1e-5))
+                          torch.ones(128, device=DEV), 0.1, 1e-5, True))
+    buf = torch.randn(300, 1536, device=DEV).to(torch.bfloat16)
+    _opcheck(D().bn_fwd_rows, (buf[:, 128:256], torch.rand(128, device=DEV), torch.randn(128, device=DEV), None, None,
+                               0.1, 1e-5, True, torch.empty(300, 1536, device=DEV, dtype=torch.bfloat16)[:, 128:256]))
 
 
 def _block(C=768, H=12):
