@@ -30,15 +30,18 @@ _SIGS = {
     "dclip_layernorm_bwd_res": [_c_void_p, _i32, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                                 _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _i64, _i64, _c_void_p],
     "dclip_gemm": [_i32, _i32, _c_void_p, _i64, _c_void_p, _i64, _i64, _i64, _i64, _i32, _f32, _c_void_p, _c_void_p,
+                   _c_void_p,
                    _i32, _i64, _c_void_p, _i32, _i64, _c_void_p, _i64, _c_void_p],
     "dclip_gemm_tn": [_i32, _i32, _c_void_p, _i64, _c_void_p, _i64, _i64, _i64, _i64, _i64, _i32, _f32, _c_void_p,
+                      _c_void_p,
                       _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p],
     "dclip_attn_fwd": [_i32, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i32, _i32, _f32, _c_void_p],
     "dclip_attn_bwd": [_i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i32,
                        _i32, _f32, _c_void_p],
     "dclip_im2col": [_c_void_p, _i32, _c_void_p, _i32, _i64, _i32, _i32, _i32, _i32, _i32, _c_void_p],
     "dclip_tokens_fwd": [_c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p],
-    "dclip_tokens_bwd": [_c_void_p, _c_void_p, _i32, _f32, _c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p],
+    "dclip_tokens_bwd": [_c_void_p, _c_void_p, _i32, _f32, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i32,
+                         _c_void_p],
     "dclip_pos_interp_fwd": [_c_void_p, _c_void_p, _i32, _i32, _i32, _i32, _c_void_p],
     "dclip_pos_interp_bwd": [_c_void_p, _c_void_p, _i32, _i32, _i32, _i32, _c_void_p],
     "dclip_transpose": [_c_void_p, _i32, _i64, _i64, _i64, _c_void_p, _i32, _i64, _i64, _i32, _i64, _i64, _i64,
@@ -49,7 +52,8 @@ _SIGS = {
                         _c_void_p],
     "dclip_bilinear_fwd": [_c_void_p, _i32, _c_void_p, _i32, _i64, _i32, _i32, _i32, _i32, _c_void_p],
     "dclip_bilinear_bwd": [_c_void_p, _i32, _c_void_p, _c_void_p, _i64, _i32, _i32, _i32, _i32, _c_void_p],
-    "dclip_cast": [_c_void_p, _i32, _c_void_p, _i32, _i64, _f32, _c_void_p],
+    "dclip_cast": [_c_void_p, _i32, _c_void_p, _i32, _i64, _f32, _c_void_p, _c_void_p],
+    "dclip_grad_scale": [_c_void_p, _i64, _f32, _c_void_p, _c_void_p],
     "dclip_add_readout_cast": [_c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _i32, _i64, _i32, _i32, _f32,
                                _c_void_p],
     "dclip_bn_workspace": [_i64, _i32],

@@ -53,7 +53,7 @@ def _register_fakes():
         return _e(*x.shape, like=x, dtype=f32), _e(*x.shape, like=x, dtype=lp_dtype)
 
     @reg("dclip::gemm")
-    def _(A, B, epi, bias, aux, out_dtype, alpha):
+    def _(A, B, epi, bias, aux, out_dtype, alpha, scale=None):
         return _e(A.shape[0], B.shape[0], like=A, dtype=out_dtype)
 
     @reg("dclip::gemm_gelu")
@@ -61,7 +61,7 @@ def _register_fakes():
         return _e(A.shape[0], B.shape[0], like=A), _e(A.shape[0], B.shape[0], like=A)
 
     @reg("dclip::weight_grad")
-    def _(dy, x, alpha, db):
+    def _(dy, x, alpha, db, scale=None):
         return _e(dy.shape[1], x.shape[1], like=dy, dtype=f32)
 
     @reg("dclip::gemm_tn")
@@ -69,8 +69,12 @@ def _register_fakes():
         return _e(A.shape[1], B.shape[1], like=A, dtype=f32)
 
     @reg("dclip::cast")
-    def _(x, dtype, scale):
+    def _(x, dtype, scale, scale_t=None):
         return _e(*x.shape, like=x, dtype=dtype)
+
+    @reg("dclip::grad_scale")
+    def _(g, target):
+        return _e(4, like=g, dtype=f32)
 
     @reg("dclip::transpose2d")
     def _(x, dtype):
@@ -106,7 +110,7 @@ def _register_fakes():
         return _e(B * (P + 1), emb.shape[1], like=emb, dtype=f32)
 
     @reg("dclip::tokens_bwd")
-    def _(dx, dtype, scale, B, P):
+    def _(dx, dtype, scale, B, P, scale_t=None):
         C = dx.shape[1]
         return _e(B * P, C, like=dx, dtype=dtype), _e(C, like=dx, dtype=f32), _e(P + 1, C, like=dx, dtype=f32)
 

@@ -114,6 +114,15 @@ __device__ __forceinline__ float quick_gelu_grad(float z) {
     return s + 1.702f * z * s * (1.0f - s);
 }
 
+// GEMM output scale: v, times *p when p is set (a device-resident factor such as the 1/s of a
+// dclip_grad_scale pair, read once per workgroup — no host round trip for fp16 gradients)
+struct Alpha {
+    float v;
+    const float* p;
+    __host__ __device__ Alpha(float v_ = 1.f, const float* p_ = nullptr) : v(v_), p(p_) {}
+    __device__ __forceinline__ float get() const { return p ? v * *p : v; }
+};
+
 // bijective XCD-aware remap of a linear block id (8 XCDs, round-robin dispatch):
 // consecutive logical tiles land on the same XCD so they share its L2.
 __device__ __forceinline__ int xcd_remap(int bid, int nblk) {

@@ -184,7 +184,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(
     const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
     int M, int N, int k_chunk, int tiles_m, int tiles_n,
     const float* __restrict__ bias, const void* __restrict__ aux, int64_t ld_aux,
-    void* __restrict__ C, int64_t ldc, void* __restrict__ C2, int64_t ldc2, int64_t slab, float alpha) {
+    void* __restrict__ C, int64_t ldc, void* __restrict__ C2, int64_t ldc2, int64_t slab, Alpha alpha_arg) {
+    const float alpha = alpha_arg.get();
     __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -397,7 +398,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_nt_big_kernel(
     const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
     int M, int N, int k_chunk, int tiles_m, int tiles_n,
     const float* __restrict__ bias, const void* __restrict__ aux, int64_t ld_aux,
-    void* __restrict__ C, int64_t ldc, void* __restrict__ C2, int64_t ldc2, int64_t slab, float alpha) {
+    void* __restrict__ C, int64_t ldc, void* __restrict__ C2, int64_t ldc2, int64_t slab, Alpha alpha_arg) {
+    const float alpha = alpha_arg.get();
     typedef BigCfg<BM, BN, WM, WN, STAGES, BKT> Cfg;
     typedef typename Mfma<T>::frag frag;
     __shared__ __attribute__((aligned(16))) char smem[Cfg::SMEM];
@@ -500,7 +502,8 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pp_kernel(
     const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
     int M, int N, int k_chunk, int tiles_m, int tiles_n,
     const float* __restrict__ bias, const void* __restrict__ aux, int64_t ld_aux,
-    void* __restrict__ C, int64_t ldc, void* __restrict__ C2, int64_t ldc2, int64_t slab, float alpha) {
+    void* __restrict__ C, int64_t ldc, void* __restrict__ C2, int64_t ldc2, int64_t slab, Alpha alpha_arg) {
+    const float alpha = alpha_arg.get();
     typedef BigCfg<256, 256, 2, 4, 2, 64> Cfg;
     typedef typename Mfma<T>::frag frag;
     constexpr int HALF = 32768;
@@ -602,7 +605,8 @@ template <typename T, int EPI, typename OutT>
 __global__ __launch_bounds__(512, 1) void gemm_nt_pers_kernel(
     const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb, int K, int tiles_m, int tiles_n,
     const float* __restrict__ bias, const void* __restrict__ aux, int64_t ld_aux, void* __restrict__ C, int64_t ldc,
-    void* __restrict__ C2, int64_t ldc2, float alpha) {
+    void* __restrict__ C2, int64_t ldc2, Alpha alpha_arg) {
+    const float alpha = alpha_arg.get();
     typedef BigCfg<256, 256, 2, 4, 2, 64> Cfg;
     typedef typename Mfma<T>::frag frag;
     __shared__ __attribute__((aligned(16))) char smem[Cfg::SMEM];
@@ -766,7 +770,8 @@ template <typename T, int EPI, typename OutT>
 __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(
     const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
     int M, int N, int Kreal, int k_chunk, int tiles_m, int tiles_n, const float* __restrict__ bias,
-    void* __restrict__ C, int64_t ldc, int64_t slab, float alpha) {
+    void* __restrict__ C, int64_t ldc, int64_t slab, Alpha alpha_arg) {
+    const float alpha = alpha_arg.get();
     __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -880,7 +885,8 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(const T* __restrict
                                                              const T* __restrict__ B, int64_t ldb, int M, int N,
                                                              int Kreal, int k_chunk, int tiles_m, int tiles_n,
                                                              void* __restrict__ C, int64_t ldc, int64_t slab,
-                                                             float alpha) {
+                                                             Alpha alpha_arg) {
+    const float alpha = alpha_arg.get();
     typedef BigCfg<256, 256, 2, 4, 2> Cfg;
     typedef typename Mfma<T>::frag frag;
     constexpr int STAGE = 2 * 64 * 512;  // A | B
@@ -949,7 +955,8 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(const T* __restrict
 // (32 row lanes), reduces its 32 partial sums per column in LDS, one atomic per column.
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ x, int64_t ld, int64_t rows, int cols,
-                                                     int64_t rows_per_block, float alpha, float* __restrict__ out) {
+                                                     int64_t rows_per_block, Alpha alpha_arg, float* __restrict__ out) {
+    const float alpha = alpha_arg.get();
     __shared__ float red[32][65];
     const int cx = threadIdx.x & 7, ry = threadIdx.x >> 3;
     const int c0 = blockIdx.x * 64 + cx * 8;
@@ -1286,7 +1293,7 @@ __global__ void tail_combine_kernel(const float* __restrict__ ws, int splits, in
 template <typename T, int EPI, typename OutT, int TBM, int TBN, int WM, int WN, int STAGES, int BKT = 64,
           bool PP = false>
 void launch_big(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
-                int splits, float alpha, const float* bias, const void* aux, int64_t ld_aux, void* C, int64_t ldc,
+                int splits, Alpha alpha, const float* bias, const void* aux, int64_t ld_aux, void* C, int64_t ldc,
                 void* C2, int64_t ldc2, hipStream_t st) {
     int tiles_m = (int)((M + TBM - 1) / TBM);
     const int tiles_n = (int)((N + TBN - 1) / TBN);
@@ -1351,7 +1358,7 @@ int cu_count() {
 
 template <typename T, int EPI, typename OutT>
 bool launch_pers(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
-                 float alpha, const float* bias, const void* aux, int64_t ld_aux, void* C, int64_t ldc, void* C2,
+                 Alpha alpha, const float* bias, const void* aux, int64_t ld_aux, void* C, int64_t ldc, void* C2,
                  int64_t ldc2, hipStream_t st) {
     if constexpr (EPI == DCLIP_EPI_SPLITK) {
         return false;
@@ -1406,7 +1413,7 @@ inline int gemm_tile_choice(int64_t M, int64_t N) {
 
 template <typename T, int EPI, typename OutT>
 int launch(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
-           int splits, float alpha, const float* bias, const void* aux, int64_t ld_aux, void* C, int64_t ldc,
+           int splits, Alpha alpha, const float* bias, const void* aux, int64_t ld_aux, void* C, int64_t ldc,
            void* C2, int64_t ldc2, hipStream_t st) {
     const int choice = gemm_tile_choice(M, N);
     if (choice == 2) {
@@ -1448,7 +1455,7 @@ int launch(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, in
 
 template <typename T>
 int dispatch(int epi, int c_dt, const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M,
-             int64_t N, int64_t K, int splits, float alpha, const float* bias, const void* aux, int64_t ld_aux,
+             int64_t N, int64_t K, int splits, Alpha alpha, const float* bias, const void* aux, int64_t ld_aux,
              void* C, int64_t ldc, void* C2, int64_t ldc2, hipStream_t st) {
     switch (epi) {
         case DCLIP_EPI_STORE:
@@ -1482,9 +1489,10 @@ int dispatch(int epi, int c_dt, const void* A, int64_t lda, const void* B, int64
 }  // namespace
 
 extern "C" int dclip_gemm(int epilogue, int ab_dt, const void* A, int64_t lda, const void* B,
-                          int64_t ldb, int64_t M, int64_t N, int64_t K, int splits, float alpha,
+                          int64_t ldb, int64_t M, int64_t N, int64_t K, int splits, float alpha_v, const float* alpha_ptr,
                           const float* bias, const void* aux, int aux_dt, int64_t ld_aux, void* C,
                           int c_dt, int64_t ldc, void* C2, int64_t ldc2, void* stream) {
+    const Alpha alpha(alpha_v, alpha_ptr);
     DCLIP_HOST_CHECK(ab_dt == DCLIP_BF16 || ab_dt == DCLIP_F16, "dclip_gemm: operands must be f16/bf16");
     DCLIP_HOST_CHECK(M > 0 && N > 0 && K > 0, "dclip_gemm: empty problem M=%lld N=%lld K=%lld",
                      (long long)M, (long long)N, (long long)K);
@@ -1558,8 +1566,9 @@ extern "C" int dclip_gemm_tn_plan(int64_t M, int64_t N, int64_t K, int* splits_o
 }
 
 extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda, const void* B, int64_t ldb,
-                             int64_t M, int64_t N, int64_t K, int64_t K_pad, int splits, float alpha, const float* bias,
+                             int64_t M, int64_t N, int64_t K, int64_t K_pad, int splits, float alpha_v, const float* alpha_ptr, const float* bias,
                              void* ws, void* C, int64_t ldc, float* colsum_a, void* stream) {
+    const Alpha alpha(alpha_v, alpha_ptr);
     DCLIP_HOST_CHECK(ab_dt == DCLIP_BF16 || ab_dt == DCLIP_F16, "dclip_gemm_tn: operands must be f16/bf16");
     DCLIP_HOST_CHECK(M > 0 && N > 0 && K > 0 && M % 8 == 0 && N % 8 == 0,
                      "dclip_gemm_tn: M, N must be positive multiples of 8 (M=%lld N=%lld)", (long long)M, (long long)N);

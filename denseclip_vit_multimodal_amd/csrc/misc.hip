@@ -79,9 +79,10 @@ __global__ void tokens_fwd_kernel(const TP* __restrict__ patch, const float* __r
 }
 
 template <typename TP>
-__global__ void tokens_bwd_kernel(const float* __restrict__ dx, TP* __restrict__ dpatch, float dpatch_scale,
+__global__ void tokens_bwd_kernel(const float* __restrict__ dx, TP* __restrict__ dpatch, Alpha dpatch_scale_arg,
                                   float* __restrict__ dcls, float* __restrict__ dpos, int B, int P, int C,
                                   int64_t total4) {
+    const float dpatch_scale = dpatch_scale_arg.get();
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over (P+1) * C/4
     if (i >= total4) return;
     const int c4 = C / 4;
@@ -387,9 +388,67 @@ __global__ __launch_bounds__(256) void score_map_kernel(const TV* __restrict__ v
     }
 }
 
+// ---------------------------------------------------------------------------- gradient scale
+// Power-of-two scale of an fp32 gradient for its fp16 cast, on the device (no host read):
+//   ws[0] = s = 2^clamp(floor(log2(target / amax|g|)), -60, 60), ws[1] = 1/s  (s = 1 when amax is
+//   0 or not finite); ws[2] = running amax bits, ws[3] = finished-workgroup count (both zero on
+//   entry, zero again on exit: the last workgroup to finish computes s and resets them).
+// |g| as uint32 bits orders like the float (non-negative), NaN / inf sort above every finite value.
+__global__ __launch_bounds__(256) void grad_scale_kernel(const float* __restrict__ g, int64_t n, float target,
+                                                         float* __restrict__ ws) {
+    uint32_t m = 0;
+    const int64_t n4 = n / 4;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+        const f32x4 v = *(const f32x4*)(g + 4 * i);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) m = max(m, __float_as_uint(v[e]) & 0x7fffffffu);
+    }
+    if (blockIdx.x == 0)
+        for (int64_t i = 4 * n4 + threadIdx.x; i < n; i += blockDim.x) m = max(m, __float_as_uint(g[i]) & 0x7fffffffu);
+    for (int o = 32; o >= 1; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+    __shared__ uint32_t red[4];
+    __shared__ bool last;
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        m = max(max(red[0], red[1]), max(red[2], red[3]));
+        uint32_t* wsu = (uint32_t*)ws;
+        atomicMax(wsu + 2, m);
+        __threadfence();
+        last = atomicAdd(wsu + 3, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last && threadIdx.x == 0) {
+        __threadfence();
+        uint32_t* wsu = (uint32_t*)ws;
+        const uint32_t bits = atomicMax(wsu + 2, 0u);
+        int e = 0;
+        if (bits != 0 && bits < 0x7f800000u) {
+            const double l = floor(log2((double)target / (double)__uint_as_float(bits)));
+            e = (int)fmin(60.0, fmax(-60.0, l));
+        }
+        ws[0] = ldexpf(1.f, e);
+        ws[1] = ldexpf(1.f, -e);
+        atomicExch(wsu + 2, 0u);
+        atomicExch(wsu + 3, 0u);
+    }
+}
+
+extern "C" int dclip_grad_scale(const float* g, int64_t n, float target, float* ws, void* stream) {
+    DCLIP_HOST_CHECK(n >= 0 && ws != nullptr && target > 0.f, "dclip_grad_scale: bad arguments");
+    DCLIP_HOST_CHECK(((uintptr_t)g % 16) == 0, "dclip_grad_scale: g must be 16-byte aligned");
+    hipStream_t st = (hipStream_t)stream;
+    int64_t blocks = (n / 4 + 255) / 256;
+    blocks = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks);
+    grad_scale_kernel<<<(unsigned)blocks, 256, 0, st>>>(g, n, target, ws);
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
+
 // ---------------------------------------------------------------------------- cast
 template <typename TI, typename TO>
-__global__ void cast_kernel(const TI* __restrict__ in, TO* __restrict__ out, int64_t n, float scale) {
+__global__ void cast_kernel(const TI* __restrict__ in, TO* __restrict__ out, int64_t n, Alpha scale_arg) {
+    const float scale = scale_arg.get();
     for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n;
          i += (int64_t)gridDim.x * blockDim.x * 4) {
         if (i + 3 < n) {
@@ -454,8 +513,10 @@ extern "C" int dclip_tokens_fwd(const void* patch, int patch_dt, const float* cl
     return 0;
 }
 
-extern "C" int dclip_tokens_bwd(const float* dx, void* dpatch, int dpatch_dt, float dpatch_scale, float* dcls,
-                                float* dpos, int B, int P, int C, void* stream) {
+extern "C" int dclip_tokens_bwd(const float* dx, void* dpatch, int dpatch_dt, float dpatch_scale_v,
+                                const float* dpatch_scale_ptr, float* dcls, float* dpos, int B, int P, int C,
+                                void* stream) {
+    const Alpha dpatch_scale(dpatch_scale_v, dpatch_scale_ptr);
     DCLIP_HOST_CHECK(C % 4 == 0, "dclip_tokens_bwd: C %% 4 != 0");
     const int64_t total4 = (int64_t)(P + 1) * C / 4;
     hipStream_t st = (hipStream_t)stream;
@@ -618,8 +679,10 @@ extern "C" int dclip_add_readout_cast(const float* a, const void* b, int b_dt, f
     return 0;
 }
 
-extern "C" int dclip_cast(const void* in, int in_dt, void* out, int out_dt, int64_t n, float scale, void* stream) {
+extern "C" int dclip_cast(const void* in, int in_dt, void* out, int out_dt, int64_t n, float scale_v,
+                          const float* scale_ptr, void* stream) {
     if (n == 0) return 0;
+    const Alpha scale(scale_v, scale_ptr);
     hipStream_t st = (hipStream_t)stream;
     DISPATCH_DT(in_dt, TI, DISPATCH_DT(out_dt, TO,
         cast_kernel<TI, TO><<<grid_for((n + 3) / 4), 256, 0, st>>>((const TI*)in, (TO*)out, n, scale)));

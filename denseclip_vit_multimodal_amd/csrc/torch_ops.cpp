@@ -46,6 +46,14 @@ T* ptr(const Tensor& t) { return t.defined() ? (T*)t.data_ptr() : nullptr; }
 template <typename T>
 T* optr(const c10::optional<Tensor>& t) { return t.has_value() && t->defined() ? (T*)t->data_ptr() : nullptr; }
 
+// entry i of a grad_scale() buffer (s, 1/s, 0, 0) on the op's device, or null without one
+const float* scale_entry(const c10::optional<Tensor>& t, int i) {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->numel() == 4 && t->is_contiguous(),
+                "scale must be a grad_scale() result: 4 contiguous f32 on the GPU");
+    return (const float*)t->data_ptr() + i;
+}
+
 #define DCLIP_CALL(expr)                                                                    \
     do {                                                                                    \
         const int rc_ = (expr);                                                             \
@@ -109,7 +117,8 @@ void gemm_checks(const Tensor& A, const Tensor& B) {
 
 // out[m][n] = alpha * sum_k A[m][k] B[n][k] (+ epilogue epi != GELU)
 Tensor gemm(const Tensor& A, const Tensor& B, int64_t epi, const c10::optional<Tensor>& bias,
-            const c10::optional<Tensor>& aux, at::ScalarType out_dtype, double alpha) {
+            const c10::optional<Tensor>& aux, at::ScalarType out_dtype, double alpha,
+            const c10::optional<Tensor>& scale) {
     gemm_checks(A, B);
     TORCH_CHECK(epi != DCLIP_EPI_GELU && epi != DCLIP_EPI_SPLITK, "gemm: use gemm_gelu / weight_grad for this epilogue");
     check_opt(bias, "bias");
@@ -119,7 +128,8 @@ Tensor gemm(const Tensor& A, const Tensor& B, int64_t epi, const c10::optional<T
     const bool has_aux = aux.has_value() && aux->defined();
     if (has_aux) TORCH_CHECK(aux->is_cuda() && aux->stride(-1) == 1, "gemm: aux must be a row-major GPU tensor");
     DCLIP_CALL(dclip_gemm((int)epi, dt_code(A.scalar_type()), A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), M, N,
-                          K, 1, (float)alpha, optr<float>(bias), has_aux ? aux->data_ptr() : nullptr,
+                          K, 1, (float)alpha, scale_entry(scale, 1), optr<float>(bias),
+                          has_aux ? aux->data_ptr() : nullptr,
                           has_aux ? dt_code(aux->scalar_type()) : 0, has_aux && aux->dim() == 2 ? aux->stride(0) : 0,
                           out.data_ptr(), dt_code(out_dtype), out.stride(0), nullptr, 0, stream_of(A)));
     return out;
@@ -133,13 +143,14 @@ std::tuple<Tensor, Tensor> gemm_gelu(const Tensor& A, const Tensor& B, const c10
     const int64_t M = A.size(0), N = B.size(0), K = A.size(1);
     Tensor z = at::empty({M, N}, A.options()), h = at::empty({M, N}, A.options());
     DCLIP_CALL(dclip_gemm(DCLIP_EPI_GELU, dt_code(A.scalar_type()), A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0),
-                          M, N, K, 1, 1.0f, optr<float>(bias), nullptr, 0, 0, z.data_ptr(), dt_code(A.scalar_type()),
+                          M, N, K, 1, 1.0f, nullptr, optr<float>(bias), nullptr, 0, 0, z.data_ptr(), dt_code(A.scalar_type()),
                           z.stride(0), h.data_ptr(), h.stride(0), stream_of(A)));
     return {z, h};
 }
 
 // dW = alpha dy^T x (f32) and, when db is given, db += alpha colsum(dy)
-Tensor weight_grad(const Tensor& dy, const Tensor& x, double alpha, c10::optional<Tensor> db) {
+Tensor weight_grad(const Tensor& dy, const Tensor& x, double alpha, c10::optional<Tensor> db,
+                   const c10::optional<Tensor>& scale) {
     check_gpu(dy, "dy"); check_gpu(x, "x");
     TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0), "weight_grad: dy (M, N), x (M, K)");
     check_opt(db, "db");
@@ -151,7 +162,8 @@ Tensor weight_grad(const Tensor& dy, const Tensor& x, double alpha, c10::optiona
     Tensor dW = at::empty({N, K}, like(dy, at::kFloat));
     Tensor ws = at::empty({(int64_t)splits * N * K}, like(dy, at::kFloat));
     DCLIP_CALL(dclip_gemm_tn(DCLIP_EPI_SPLITK, dt_code(dy.scalar_type()), dy.data_ptr(), dy.stride(0), x.data_ptr(),
-                             x.stride(0), N, K, M, k_pad, splits, (float)alpha, nullptr, ws.data_ptr(), dW.data_ptr(), K,
+                             x.stride(0), N, K, M, k_pad, splits, (float)alpha, scale_entry(scale, 1), nullptr, ws.data_ptr(),
+                             dW.data_ptr(), K,
                              optr<float>(db), stream_of(dy)));
     return dW;
 }
@@ -164,18 +176,28 @@ Tensor gemm_tn(const Tensor& A, const Tensor& B) {
     const int64_t K = A.size(0), M = A.size(1), N = B.size(1);
     Tensor out = at::empty({M, N}, like(A, at::kFloat));
     DCLIP_CALL(dclip_gemm_tn(DCLIP_EPI_STORE, dt_code(A.scalar_type()), A.data_ptr(), A.stride(0), B.data_ptr(),
-                             B.stride(0), M, N, K, (K + 63) / 64 * 64, 1, 1.0f, nullptr, nullptr, out.data_ptr(), N,
+                             B.stride(0), M, N, K, (K + 63) / 64 * 64, 1, 1.0f, nullptr, nullptr, nullptr, out.data_ptr(), N,
                              nullptr, stream_of(A)));
     return out;
 }
 
 // ----------------------------------------------------------------------------- element-wise
-Tensor cast(const Tensor& x, at::ScalarType dtype, double scale) {
+// (s, 1/s, 0, 0) f32 on the device: the power-of-two fp16 scale of the gradient g (dclip_grad_scale)
+Tensor grad_scale(const Tensor& g, double target) {
+    check_gpu(g, "g");
+    TORCH_CHECK(g.scalar_type() == at::kFloat && g.is_contiguous(), "grad_scale: g must be contiguous f32");
+    c10::DeviceGuard gd(g.device());
+    Tensor ws = at::zeros({4}, g.options());
+    DCLIP_CALL(dclip_grad_scale(ptr<float>(g), g.numel(), (float)target, ptr<float>(ws), stream_of(g)));
+    return ws;
+}
+
+Tensor cast(const Tensor& x, at::ScalarType dtype, double scale, const c10::optional<Tensor>& scale_t) {
     check_gpu(x, "x");
     c10::DeviceGuard g(x.device());
     Tensor y = at::empty(x.sizes(), like(x, dtype));
     DCLIP_CALL(dclip_cast(x.data_ptr(), dt_code(x.scalar_type()), y.data_ptr(), dt_code(dtype), x.numel(), (float)scale,
-                          stream_of(x)));
+                          scale_entry(scale_t, 0), stream_of(x)));
     return y;
 }
 
@@ -280,7 +302,7 @@ Tensor tokens_fwd(const Tensor& emb, const Tensor& cls, const Tensor& pos, int64
 
 // (demb = scale * dx[patch rows] in dtype, dcls, dpos (P+1, C))
 std::tuple<Tensor, Tensor, Tensor> tokens_bwd(const Tensor& dx, at::ScalarType dtype, double scale, int64_t B,
-                                              int64_t P) {
+                                              int64_t P, const c10::optional<Tensor>& scale_t) {
     check_gpu(dx, "dx");
     const int64_t C = dx.size(1);
     TORCH_CHECK(dx.size(0) == B * (P + 1), "tokens_bwd: dx (B*(P+1), C)");
@@ -288,7 +310,8 @@ std::tuple<Tensor, Tensor, Tensor> tokens_bwd(const Tensor& dx, at::ScalarType d
     Tensor demb = at::empty({B * P, C}, like(dx, dtype));
     Tensor dcls = at::zeros({C}, like(dx, at::kFloat));
     Tensor dpos = at::zeros({P + 1, C}, like(dx, at::kFloat));
-    DCLIP_CALL(dclip_tokens_bwd(ptr<float>(dx), demb.data_ptr(), dt_code(dtype), (float)scale, ptr<float>(dcls),
+    DCLIP_CALL(dclip_tokens_bwd(ptr<float>(dx), demb.data_ptr(), dt_code(dtype), (float)scale,
+                                scale_entry(scale_t, 0), ptr<float>(dcls),
                                 ptr<float>(dpos), (int)B, (int)P, (int)C, stream_of(dx)));
     return {demb, dcls, dpos};
 }
@@ -561,11 +584,13 @@ TORCH_LIBRARY(dclip, m) {
           "Tensor(b!) db) -> Tensor");
     m.def("layernorm_bwd_lp(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, Tensor? res, Tensor(a!) dw, "
           "Tensor(b!) db, ScalarType lp_dtype) -> (Tensor, Tensor)");
-    m.def("gemm(Tensor A, Tensor B, int epi, Tensor? bias, Tensor? aux, ScalarType out_dtype, float alpha) -> Tensor");
+    m.def("gemm(Tensor A, Tensor B, int epi, Tensor? bias, Tensor? aux, ScalarType out_dtype, float alpha, "
+          "Tensor? scale=None) -> Tensor");
     m.def("gemm_gelu(Tensor A, Tensor B, Tensor? bias) -> (Tensor, Tensor)");
-    m.def("weight_grad(Tensor dy, Tensor x, float alpha, Tensor(a!)? db) -> Tensor");
+    m.def("weight_grad(Tensor dy, Tensor x, float alpha, Tensor(a!)? db, Tensor? scale=None) -> Tensor");
     m.def("gemm_tn(Tensor A, Tensor B) -> Tensor");
-    m.def("cast(Tensor x, ScalarType dtype, float scale) -> Tensor");
+    m.def("cast(Tensor x, ScalarType dtype, float scale, Tensor? scale_t=None) -> Tensor");
+    m.def("grad_scale(Tensor g, float target) -> Tensor");
     m.def("transpose2d(Tensor x, ScalarType dtype) -> Tensor");
     m.def("transpose_batched(Tensor x, int B, int rows, int cols, int ld_in, int rows_pad, ScalarType dtype) -> Tensor");
     m.def("add_readout_cast(Tensor a, Tensor b, int ntok, ScalarType lp_dtype, float scale) -> (Tensor, Tensor)");
@@ -574,7 +599,8 @@ TORCH_LIBRARY(dclip, m) {
     m.def("attn_bwd(Tensor qkv, Tensor o, Tensor dout, Tensor lse, int B, int N, int H, float scale) -> Tensor");
     m.def("im2col(Tensor img, int p, ScalarType dtype) -> Tensor");
     m.def("tokens_fwd(Tensor emb, Tensor cls, Tensor pos, int B, int P) -> Tensor");
-    m.def("tokens_bwd(Tensor dx, ScalarType dtype, float scale, int B, int P) -> (Tensor, Tensor, Tensor)");
+    m.def("tokens_bwd(Tensor dx, ScalarType dtype, float scale, int B, int P, Tensor? scale_t=None) -> "
+          "(Tensor, Tensor, Tensor)");
     m.def("pos_interp(Tensor pos, int g, int H, int W) -> Tensor");
     m.def("pos_interp_bwd(Tensor dout, int g, int H, int W) -> Tensor");
     m.def("row_mean(Tensor x, int bstride, int row_off, int ld, int B, int rows, int C) -> Tensor");
@@ -609,6 +635,7 @@ TORCH_LIBRARY_IMPL(dclip, CUDA, m) {
     m.impl("weight_grad", &weight_grad);
     m.impl("gemm_tn", &gemm_tn);
     m.impl("cast", &cast);
+    m.impl("grad_scale", &grad_scale);
     m.impl("transpose2d", &transpose2d);
     m.impl("transpose_batched", &transpose_batched);
     m.impl("add_readout_cast", &add_readout_cast);

@@ -113,17 +113,18 @@ def layernorm_bwd(dy, x, w, mean, rstd, dw, db, res=None, lp_dtype=None):
     return D().layernorm_bwd_lp(dy, x, w, mean, rstd, res, dw, db, lp_dtype)
 
 
-def gemm(A, B, epi=N.EPI_STORE, bias=None, aux=None, out_dtype=None, alpha=1.0):
+def gemm(A, B, epi=N.EPI_STORE, bias=None, aux=None, out_dtype=None, alpha=1.0, scale=None):
     """out[m][n] = alpha * sum_k A[m][k] B[n][k] (+ epilogue).  A: (M, K), B: (N, K).
-    EPI_GELU returns (z, quick_gelu(z))."""
-    _check(A, B, bias, aux)
+    EPI_GELU returns (z, quick_gelu(z)).  scale: a grad_scale() buffer whose 1/s also
+    multiplies the result (read on the device)."""
+    _check(A, B, bias, aux, scale)
     assert A.shape[1] == B.shape[1], (A.shape, B.shape)
     e0 = _tic()
     if epi == N.EPI_GELU:
         out = D().gemm_gelu(A, B, bias)
     else:
         odt = out_dtype or (torch.float32 if epi == N.EPI_RESIDUAL else A.dtype)
-        out = D().gemm(A, B, epi, bias, aux, odt, float(alpha))
+        out = D().gemm(A, B, epi, bias, aux, odt, float(alpha), scale)
     _toc("gemm", e0)
     return out
 
@@ -134,48 +135,47 @@ def transpose2d(x, out_dtype):
     return D().transpose2d(x, out_dtype)
 
 
-def cast(x, dtype, scale=1.0):
-    """(dtype)(x * scale)."""
-    _check(x)
-    if x.dtype == dtype and scale == 1.0:
+def cast(x, dtype, scale=1.0, scale_t=None):
+    """(dtype)(x * scale), times s of the grad_scale() buffer scale_t when given."""
+    _check(x, scale_t)
+    if x.dtype == dtype and scale == 1.0 and scale_t is None:
         return x
-    return D().cast(x, dtype, float(scale))
+    return D().cast(x, dtype, float(scale), scale_t)
 
 
 FP16_GRAD_AMAX = 16.0
 
 
 def grad_scale(g, cdt):
-    """Power-of-two scale for casting the fp32 gradient g to the compute dtype.
+    """Power-of-two scale for casting the fp32 gradient g to the compute dtype, ON THE DEVICE.
 
-    bf16 has the fp32 exponent range: 1.0, no host round trip.  fp16 does not: the
-    gradients of a segmentation loss averaged over ~10^5-10^7 pixels sit at 1e-5..1e-9,
-    in (or below) fp16's subnormal range, so they are scaled to amax ~ FP16_GRAD_AMAX
-    before the cast and every fp32 result computed from them is unscaled by the GEMM's
-    alpha (one device->host read of amax per backward block, fp16 mode only)."""
+    bf16 has the fp32 exponent range: None (no scaling).  fp16 does not: the gradients of a
+    segmentation loss averaged over ~10^5-10^7 pixels sit at 1e-5..1e-9, in (or below) fp16's
+    subnormal range, so they are scaled by s = 2^floor(log2(FP16_GRAD_AMAX / max|g|)) before
+    the cast and every fp32 result computed from them is unscaled by 1/s in the GEMM epilogue.
+    Returns the (s, 1/s, 0, 0) f32 buffer dclip_grad_scale writes; cast / tokens_bwd read s from
+    it and gemm / weight_grad read 1/s, all on the stream: no device->host round trip."""
     if cdt != torch.float16:
-        return 1.0
-    amax = float(g.detach().abs().amax())
-    if not math.isfinite(amax) or amax == 0.0:
-        return 1.0
-    e = math.floor(math.log2(FP16_GRAD_AMAX / amax))
-    return float(2.0 ** max(-60, min(60, e)))
+        return None
+    g = g.detach()
+    _check(g)
+    return D().grad_scale(g if g.is_contiguous() else g.contiguous(), FP16_GRAD_AMAX)
 
 
-def weight_grad(dy, x, want_bias=True, alpha=1.0, db=None):
+def weight_grad(dy, x, want_bias=True, alpha=1.0, db=None, scale=None):
     """dW = alpha dy^T x (N x K, fp32) and db += alpha colsum(dy) for dy (M, N), x (M, K)
-    (compute dtype).
+    (compute dtype); scale: a grad_scale() buffer whose 1/s also multiplies both.
 
     One "TN" MFMA GEMM reading both operands in their natural token-major layout (the
     reduction runs over the rows), split over the M tokens with a deterministic slab
     combine; no transposed copies."""
-    _check(dy, x, db)
+    _check(dy, x, db, scale)
     if want_bias and db is None:  # db: a caller-zeroed (Nn,) f32 buffer, or allocated here
         db = torch.zeros(dy.shape[1], dtype=torch.float32, device=dy.device)
     elif not want_bias:
         db = None
     e0 = _tic()
-    dW = D().weight_grad(dy, x, float(alpha), db)
+    dW = D().weight_grad(dy, x, float(alpha), db, scale)
     _toc("gemm_wgrad", e0)
     return dW, db
 
@@ -385,14 +385,14 @@ class PatchEmbedFn(torch.autograd.Function):
         dlnw = torch.zeros(C, dtype=torch.float32, device=dx.device)
         dlnb = torch.zeros(C, dtype=torch.float32, device=dx.device)
         dxp = layernorm_bwd(dx, x_pre, ln_w.detach(), mean, rstd, dlnw, dlnb)
-        s = grad_scale(dxp, cdt) if need[1] else 1.0
-        demb, dcls, dposf = D().tokens_bwd(dxp, cdt, float(s), B, P)
+        s = grad_scale(dxp, cdt) if need[1] else None
+        demb, dcls, dposf = D().tokens_bwd(dxp, cdt, 1.0, B, P, s)
         dpos = None
         if need[3]:
             dpos = pos_interp_bwd(dposf, g, gh, gw) if interp else dposf
         dconv = None
         if need[1]:
-            dW, _ = weight_grad(demb, patches, want_bias=False, alpha=1.0 / s)
+            dW, _ = weight_grad(demb, patches, want_bias=False, scale=s)
             K = math.prod(wshape[1:])
             dconv = (dW if dW.shape[1] == K else dW[:, :K]).reshape(wshape)
         return (None, dconv, dcls if need[2] else None, dpos, dlnw if need[4] else None,
@@ -472,38 +472,38 @@ class BlockFn(torch.autograd.Function):
                 dxo = dxo + _readout_grad_dense(dmap, B, Ntok, gh, gw, C)
 
         # ---- MLP: xo = xm + h W2^T + b2,  h = qgelu(z),  z = xh2 W1^T + b1
-        # (s1, s2: power-of-two gradient scales, 1.0 unless fp16 — see grad_scale)
+        # (s1, s2: device-side power-of-two gradient scales, None unless fp16 — see grad_scale)
         s1 = grad_scale(dxo, cdt)
         if dy is None:
-            dy = cast(dxo, cdt, s1)
+            dy = cast(dxo, cdt, scale_t=s1)
         dz = gemm(dy, WEIGHTS.get(w2, cdt, transposed=True), N.EPI_GELU_BWD, aux=z)
         dW2 = db2 = dW1 = db1 = None
         if wg:
-            dW2, db2 = weight_grad(dy, h, alpha=1.0 / s1, db=zb2)
-        dxh2 = gemm(dz, WEIGHTS.get(w1, cdt, transposed=True), out_dtype=torch.float32, alpha=1.0 / s1)
+            dW2, db2 = weight_grad(dy, h, db=zb2, scale=s1)
+        dxh2 = gemm(dz, WEIGHTS.get(w1, cdt, transposed=True), out_dtype=torch.float32, scale=s1)
         if wg:
-            dW1, db1 = weight_grad(dz, xh2, alpha=1.0 / s1, db=zb1)
+            dW1, db1 = weight_grad(dz, xh2, db=zb1, scale=s1)
         del dz
         if cdt == torch.bfloat16:  # no gradient scaling: the attention branch's operand comes out of the LN pass
             dxm, dyo = layernorm_bwd(dxh2, xm, ln2w.detach(), mu2, rs2, dln2w, dln2b, res=dxo, lp_dtype=cdt)
-            s2 = 1.0
+            s2 = None
         else:
             dxm = layernorm_bwd(dxh2, xm, ln2w.detach(), mu2, rs2, dln2w, dln2b, res=dxo)
         del dxh2
         # ---- attention: xm = x + o Wout^T + bout
         if cdt != torch.bfloat16:
             s2 = grad_scale(dxm, cdt)
-            dyo = cast(dxm, cdt, s2)
+            dyo = cast(dxm, cdt, scale_t=s2)
         do = gemm(dyo, WEIGHTS.get(w_out, cdt, transposed=True))
         dWo = dbo = dWi = dbi = None
         if wg:
-            dWo, dbo = weight_grad(dyo, o, alpha=1.0 / s2, db=zbo)
+            dWo, dbo = weight_grad(dyo, o, db=zbo, scale=s2)
         del dyo
         dqkv = attn_bwd(qkv, o, do, lse, B, Ntok, H, scale)  # linear in dO: carries s2
         del do
-        dxh1 = gemm(dqkv, WEIGHTS.get(w_in, cdt, transposed=True), out_dtype=torch.float32, alpha=1.0 / s2)
+        dxh1 = gemm(dqkv, WEIGHTS.get(w_in, cdt, transposed=True), out_dtype=torch.float32, scale=s2)
         if wg:
-            dWi, dbi = weight_grad(dqkv, xh1, alpha=1.0 / s2, db=zbi)
+            dWi, dbi = weight_grad(dqkv, xh1, db=zbi, scale=s2)
         del dqkv
         dxm = layernorm_bwd(dxh1, x, ln1w.detach(), mu1, rs1, dln1w, dln1b, res=dxm)
         g = lambda i, t: t if need[i] else None  # noqa: E731

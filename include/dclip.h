@@ -106,11 +106,13 @@ int dclip_layernorm_bwd_res(const void* dy, int dy_dt, const void* x, int x_dt,
 /* C[m][n] = alpha * sum_k A[m][k] * B[n][k]  ("NT": both operands k-contiguous, ab_dt in
  * {F16, BF16}), m < M, n < N, k < K (K % 64 == 0, lda/ldb % 8 == 0), then the
  * epilogue.  bias: f32[N] or null.  aux: epilogue side input (see DCLIP_EPI_*).
- * alpha undoes a gradient scale carried by an operand (fp16 backward; 1 otherwise).
+ * alpha undoes a gradient scale carried by an operand (fp16 backward; 1 otherwise); when
+ * alpha_ptr is non-null the factor is alpha * *alpha_ptr, read on the device (the 1/s entry
+ * of a dclip_grad_scale pair: no host round trip).
  * splits > 1 (EPI_SPLITK only) splits K into `splits` equal 64-multiple chunks.      */
 int dclip_gemm(int epilogue, int ab_dt,
                const void* A, int64_t lda, const void* B, int64_t ldb,
-               int64_t M, int64_t N, int64_t K, int splits, float alpha,
+               int64_t M, int64_t N, int64_t K, int splits, float alpha, const float* alpha_ptr,
                const float* bias, const void* aux, int aux_dt, int64_t ld_aux,
                void* C, int c_dt, int64_t ldc, void* C2, int64_t ldc2, void* stream);
 
@@ -120,13 +122,15 @@ int dclip_gemm(int epilogue, int ab_dt,
  * K_pad / splits (K_pad >= K, multiple of 64*splits; rows >= K contribute zero).
  * epilogue STORE (f32 C, splits == 1) or SPLITK (f32 slabs in ws, splits*M*N, then a
  * combine that adds bias[n] when non-null).  colsum_a (f32, M), when non-null, receives
- * += alpha * the column sums of A over the K rows (the bias gradient of dY).          */
+ * += alpha * the column sums of A over the K rows (the bias gradient of dY).  alpha_ptr
+ * as in dclip_gemm.                                                                   */
 /* The K-split plan dclip_gemm_tn runs best with for an M x N output over K rows
  * (splits, and K_pad = K rounded up to 64*splits); host-side only, no GPU work.      */
 int dclip_gemm_tn_plan(int64_t M, int64_t N, int64_t K, int* splits, int64_t* K_pad);
 
 int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda, const void* B, int64_t ldb,
-                  int64_t M, int64_t N, int64_t K, int64_t K_pad, int splits, float alpha, const float* bias,
+                  int64_t M, int64_t N, int64_t K, int64_t K_pad, int splits, float alpha,
+                  const float* alpha_ptr, const float* bias,
                   void* ws, void* C, int64_t ldc, float* colsum_a, void* stream);
 
 /* Fused multi-head attention over a packed QKV buffer.
@@ -176,10 +180,12 @@ int dclip_im2col(const void* img, int img_dt, void* out, int out_dt, int64_t ldo
 int dclip_tokens_fwd(const void* patch, int patch_dt, const float* cls, const float* pos,
                      float* x, int B, int P, int C, void* stream);
 
-/* Token assembly backward: dpatch[b*P+i] = dpatch_scale * dx[b][1+i] (dpatch_dt);
+/* Token assembly backward: dpatch[b*P+i] = dpatch_scale * dx[b][1+i] (dpatch_dt; times
+ * *dpatch_scale_ptr when non-null, read on the device);
  * dcls += sum_b dx[b][0]; dpos[t] += sum_b dx[b][t]  (dcls/dpos f32, accumulated)   */
-int dclip_tokens_bwd(const float* dx, void* dpatch, int dpatch_dt, float dpatch_scale, float* dcls,
-                     float* dpos, int B, int P, int C, void* stream);
+int dclip_tokens_bwd(const float* dx, void* dpatch, int dpatch_dt, float dpatch_scale,
+                     const float* dpatch_scale_ptr, float* dcls, float* dpos, int B, int P, int C,
+                     void* stream);
 
 /* Bilinear (align_corners=False) resize of the g x g patch grid of pos (g*g+1, C)
  * to H x W; out (H*W+1, C), row 0 = pos row 0.                                       */
@@ -278,9 +284,19 @@ int dclip_cityscapes_prepare(const uint8_t* img, const uint8_t* ids, const uint1
                              float depth_max, void* out_img, int out_dt, int64_t* out_seg, float* out_depth,
                              uint8_t* out_mask, void* stream);
 
-/* Element-wise dtype conversion of n elements: out = (out_dt)(in * scale).  A power-of-two
- * scale keeps fp16 gradients out of the subnormal range (see dclip_gemm's alpha).     */
-int dclip_cast(const void* in, int in_dt, void* out, int out_dt, int64_t n, float scale, void* stream);
+/* Element-wise dtype conversion of n elements: out = (out_dt)(in * scale), times *scale_ptr
+ * when non-null (read on the device).  A power-of-two scale keeps fp16 gradients out of the
+ * subnormal range (see dclip_grad_scale and dclip_gemm's alpha).                      */
+int dclip_cast(const void* in, int in_dt, void* out, int out_dt, int64_t n, float scale,
+               const float* scale_ptr, void* stream);
+
+/* Power-of-two scale for the fp16 cast of an f32 gradient g (n elements, 16-byte aligned),
+ * computed on the device: ws[0] = s = 2^clamp(floor(log2(target / max|g|)), -60, 60),
+ * ws[1] = 1/s (s = 1 when max|g| is 0 or not finite).  ws: 4 floats, ws[2..3] zero on entry
+ * (left zero on exit, so one buffer serves successive calls on a stream).  Pass ws to
+ * dclip_cast / dclip_tokens_bwd as scale_ptr and ws + 1 to dclip_gemm / dclip_gemm_tn as
+ * alpha_ptr.  (No reference counterpart: the reference trains in fp32.)              */
+int dclip_grad_scale(const float* g, int64_t n, float target, float* ws, void* stream);
 /* Read-out gradient folded into a block's incoming gradient (replaces the autograd sum of the
  * two uses of a block output, models.py:565 -> 577-597, plus the backward's cast): sum = a + b
  * with b's CLS rows (row % ntok == 0) read as 0, lp = (lp_dt)(sum * scale).  a, sum: f32

@@ -1,0 +1,118 @@
+"""fp16 training path: the power-of-two gradient scale is computed ON THE DEVICE
+(dclip_grad_scale) and read by the cast / token / GEMM kernels through a pointer, so an fp16
+backward makes no device->host round trip.  The scaled ops must equal the
+same ops with the scale passed as a host float (bit-exact: a power-of-two factor)."""
+import math
+
+import pytest
+import torch
+
+from helpers import CITYSCAPES_CFG, CITYSCAPES_CLASSES, images, rel_err, spec_state_dict
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True)
+def _need(hip):
+    pass
+
+
+def host_scale(g, target=16.0):
+    """The formula dclip_grad_scale restates (include/dclip.h)."""
+    amax = float(g.abs().amax())
+    if not math.isfinite(amax) or amax == 0.0:
+        return 1.0
+    return 2.0 ** max(-60, min(60, math.floor(math.log2(target / amax))))
+
+
+@pytest.mark.parametrize("mag,n", [(1e-7, 1 << 20), (3.0, 4099), (1e-30, 77), (1e30, 1000), (1e-9, 8 * 8193 * 768)])
+def test_grad_scale_matches_host_formula(mag, n):
+    from denseclip_vit_multimodal_amd import ops
+    g = torch.randn(n, device=DEV) * mag
+    g[-1] = 40 * mag  # the maximum in the ragged tail (n % 4 != 0 for two cases)
+    ws = ops.grad_scale(g, torch.float16).cpu()
+    s = host_scale(g)
+    assert ws.tolist() == [s, 1.0 / s, 0.0, 0.0]
+    assert ops.grad_scale(g, torch.bfloat16) is None  # bf16 has the fp32 exponent range
+
+
+@pytest.mark.parametrize("bad", [0.0, float("inf"), float("nan")])
+def test_grad_scale_degenerate_is_one(bad):
+    from denseclip_vit_multimodal_amd import ops
+    g = torch.zeros(1000, device=DEV) if bad == 0.0 else torch.randn(1000, device=DEV)
+    g[123] = bad
+    assert ops.grad_scale(g, torch.float16).cpu().tolist() == [1.0, 1.0, 0.0, 0.0]
+
+
+@pytest.mark.parametrize("M,N,K", [(200, 256, 128), (4100, 768, 768), (16392, 3072, 768)])
+def test_scaled_ops_equal_host_alpha(M, N, K):
+    """gemm / weight_grad / cast / tokens_bwd with the device scale == the host-float path (the
+    three shapes take the 128x128, 256x256 grid and persistent + M-tail GEMM kernels)."""
+    from denseclip_vit_multimodal_amd import ops
+    torch.manual_seed(0)
+    g = torch.randn(M, K, device=DEV) * 3e-8
+    ws = ops.grad_scale(g, torch.float16)
+    s = host_scale(g)
+    a_dev = ops.cast(g, torch.float16, scale_t=ws)
+    a_host = ops.cast(g, torch.float16, s)
+    assert torch.equal(a_dev, a_host)
+    assert a_dev.abs().amax().item() > 4.0  # scaled up out of the fp16 subnormal range
+    B = torch.randn(N, K, device=DEV).half()
+    assert torch.equal(ops.gemm(a_dev, B, out_dtype=torch.float32, scale=ws),
+                       ops.gemm(a_dev, B, out_dtype=torch.float32, alpha=1.0 / s))
+    x = torch.randn(M, N, device=DEV).half()
+    dw_dev, db_dev = ops.weight_grad(a_dev, x, scale=ws)
+    dw_host, db_host = ops.weight_grad(a_dev, x, alpha=1.0 / s)
+    assert torch.equal(dw_dev, dw_host)
+    assert rel_err(db_dev, db_host) < 1e-6  # column sums: atomics, order-dependent rounding
+    ref = g.double().t() @ x.double()
+    assert rel_err(dw_dev, ref) < 2e-3
+
+
+def test_tokens_bwd_device_scale():
+    from denseclip_vit_multimodal_amd import ops
+    B, P, C = 2, 64, 768
+    dx = torch.randn(B * (P + 1), C, device=DEV) * 1e-8
+    ws = ops.grad_scale(dx, torch.float16)
+    s = host_scale(dx)
+    d_dev = ops.D().tokens_bwd(dx, torch.float16, 1.0, B, P, ws)
+    d_host = ops.D().tokens_bwd(dx, torch.float16, s, B, P)
+    for a, b in zip(d_dev, d_host):
+        assert torch.equal(a, b)
+
+
+def _model(cdt):
+    from denseclip_vit_multimodal_amd import DenseCLIP
+    m = DenseCLIP(class_names=CITYSCAPES_CLASSES, **CITYSCAPES_CFG)
+    m.load_state_dict(spec_state_dict("cityscapes"))
+    m.backbone.compute_dtype = cdt
+    return m.to(DEV)
+
+
+def test_fp16_backbone_backward_makes_no_host_sync():
+    """ViT-B/16 fwd+bwd in fp16 (the gradient-scaled path through all 12 BlockFn and the
+    patch embedding) under torch's sync debug mode "error": any device->host read raises."""
+    m = _model(torch.float16)
+    bb = m.backbone.train()
+    x = images(1, 128, 256).to(DEV).half()
+    gen = torch.Generator().manual_seed(5)
+    ws = None
+    for it in range(2):  # the second pass runs with every cache / allocation warm
+        maps = bb(x)
+        if ws is None:
+            ws = [(torch.randn(mp.shape, generator=gen) * 1e-6).to(DEV) for mp in maps]
+        torch.cuda.synchronize()
+        if it == 1:
+            torch.cuda.set_sync_debug_mode("error")
+        try:
+            loss = sum((mp.float() * w).sum() for mp, w in zip(maps, ws))
+            loss.backward()
+        finally:
+            torch.cuda.set_sync_debug_mode(0)
+        torch.cuda.synchronize()
+    for name, p in bb.named_parameters():
+        if p.grad is not None:
+            assert torch.isfinite(p.grad).all(), name
+    w = bb.transformer.resblocks[0].attn.in_proj_weight.grad
+    assert w is not None and w.abs().sum() > 0

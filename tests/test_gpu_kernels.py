@@ -174,7 +174,7 @@ def test_gemm_gelu_and_residual(M, N, K, gemm_tile):
     assert rel_err(out, res + zr) < 1e-5
     # in place through the C ABI (aux aliases C)
     res2 = res.clone()
-    Nat.call("dclip_gemm", Nat.EPI_RESIDUAL, Nat.BF16, A.data_ptr(), K, B.data_ptr(), K, M, N, K, 1, 1.0,
+    Nat.call("dclip_gemm", Nat.EPI_RESIDUAL, Nat.BF16, A.data_ptr(), K, B.data_ptr(), K, M, N, K, 1, 1.0, None,
              bias.data_ptr(), res2.data_ptr(), Nat.F32, N, res2.data_ptr(), Nat.F32, N, None, 0,
              torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()

@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
     lib = N.load()
     for name in declared_symbols():
         assert hasattr(lib, name), name
-    assert lib.dclip_abi_version() == 2
+    assert lib.dclip_abi_version() == 3
 
 
 def test_no_oracle_in_product_package():
@@ -39,11 +39,11 @@ def test_no_oracle_in_product_package():
 
 
 @pytest.mark.parametrize("call,needle", [
-    (lambda L: L.dclip_gemm(0, 0, None, 64, None, 64, 64, 64, 64, 1, 1.0, None, None, 0, 0, None, 0, 64, None, 0, None),
+    (lambda L: L.dclip_gemm(0, 0, None, 64, None, 64, 64, 64, 64, 1, 1.0, None, None, None, 0, 0, None, 0, 64, None, 0, None),
      "f16/bf16"),
-    (lambda L: L.dclip_gemm(0, 2, None, 64, None, 64, 64, 64, 100, 1, 1.0, None, None, 0, 0, None, 2, 64, None, 0, None),
+    (lambda L: L.dclip_gemm(0, 2, None, 64, None, 64, 64, 64, 100, 1, 1.0, None, None, None, 0, 0, None, 2, 64, None, 0, None),
      "multiple of 64"),
-    (lambda L: L.dclip_gemm(4, 2, None, 64, None, 64, 64, 64, 64, 2, 1.0, None, None, 0, 0, None, 0, 64, None, 0, None),
+    (lambda L: L.dclip_gemm(4, 2, None, 64, None, 64, 64, 64, 64, 2, 1.0, None, None, None, 0, 0, None, 0, 64, None, 0, None),
      "multiple of 64*splits"),
     (lambda L: L.dclip_attn_fwd(2, None, None, None, 1, 8, 2, 32, 1.0, None), "head_dim must be 64"),
     (lambda L: L.dclip_layernorm_fwd(None, 0, None, None, None, 0, None, None, 4, 4098, 1e-5, None), "cols"),
