@@ -266,6 +266,9 @@ if __name__ == "__main__":
         gen_manifest()
         gen_tiny_ctx()
         sys.exit(0)
+    if sys.argv[1:] == ["cfg1"]:
+        gen_full("vitb16_2x512x1024", 2, 512, 1024, keep_full_maps=(0, 11))
+        sys.exit(0)
     if sys.argv[1:] == ["vitl14"]:
         gen_manifest()
         gen_vitl14()
@@ -275,5 +278,5 @@ if __name__ == "__main__":
     gen_tiny()
     gen_tiny_ctx()
     gen_full("vitb16_1x128x256", 1, 128, 256)
-    gen_full("vitb16_2x512x1024", 2, 512, 1024, keep_full_maps=())
+    gen_full("vitb16_2x512x1024", 2, 512, 1024, keep_full_maps=(0, 11))
     gen_vitl14()
