@@ -72,6 +72,10 @@ def _register_fakes():
     def _(x, dtype, scale, scale_t=None):
         return _e(*x.shape, like=x, dtype=dtype)
 
+    @reg("dclip::row_scale_add")
+    def _(x, y, s):
+        return torch.empty_like(y)
+
     @reg("dclip::grad_scale")
     def _(g, target):
         return _e(4, like=g, dtype=f32)

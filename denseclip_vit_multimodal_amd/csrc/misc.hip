@@ -445,6 +445,36 @@ extern "C" int dclip_grad_scale(const float* g, int64_t n, float target, float* 
     return 0;
 }
 
+// ---------------------------------------------------------------------------- stochastic depth
+// out[r][c] = (x ? x[r][c] : 0) + s[r % ntok] * y[r][c]: a residual branch scaled by a per-TOKEN
+// keep mask (timm drop_path on the reference's LND layout draws one value per token position,
+// shared by the batch: models.py:257-268, 291-294), and the same scaling for its gradient.
+__global__ void row_scale_add_kernel(const float* __restrict__ x, const float* __restrict__ y,
+                                     const float* __restrict__ s, float* __restrict__ out, int64_t rows, int cols,
+                                     int ntok) {
+    const int c4 = cols / 4;
+    const int64_t total = rows * c4;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / c4;
+        const float sc = s[r % ntok];
+        f32x4 v = *(const f32x4*)(y + 4 * i) * sc;
+        if (x) v += *(const f32x4*)(x + 4 * i);
+        *(f32x4*)(out + 4 * i) = v;
+    }
+}
+
+extern "C" int dclip_row_scale_add(const float* x, const float* y, const float* s, int ntok, float* out, int64_t rows,
+                                   int cols, void* stream) {
+    DCLIP_HOST_CHECK(y && s && out && ntok > 0 && rows >= 0 && cols % 4 == 0 && rows % ntok == 0,
+                     "dclip_row_scale_add: bad arguments (cols %% 4 == 0, rows a multiple of ntok)");
+    if (rows == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t blocks = (rows * (cols / 4) + 255) / 256;
+    row_scale_add_kernel<<<(unsigned)(blocks < 65536 ? blocks : 65536), 256, 0, st>>>(x, y, s, out, rows, cols, ntok);
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
+
 // ---------------------------------------------------------------------------- cast
 template <typename TI, typename TO>
 __global__ void cast_kernel(const TI* __restrict__ in, TO* __restrict__ out, int64_t n, Alpha scale_arg) {

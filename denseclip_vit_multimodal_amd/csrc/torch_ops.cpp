@@ -240,6 +240,20 @@ std::tuple<Tensor, Tensor> add_readout_cast(const Tensor& a, const Tensor& b, in
     return {sum, lp};
 }
 
+// (x ? x : 0) + s[row % ntok] * y, f32 (rows, cols): a drop_path-scaled residual branch
+Tensor row_scale_add(const c10::optional<Tensor>& x, const Tensor& y, const Tensor& s) {
+    check_gpu(y, "y"); check_gpu(s, "s"); check_opt(x, "x");
+    TORCH_CHECK(y.scalar_type() == at::kFloat && s.scalar_type() == at::kFloat && y.dim() == 2,
+                "row_scale_add: y (rows, cols) f32, s (ntok,) f32");
+    const bool has_x = x.has_value() && x->defined();
+    if (has_x) TORCH_CHECK(x->scalar_type() == at::kFloat && x->sizes() == y.sizes(), "row_scale_add: x like y");
+    c10::DeviceGuard g(y.device());
+    Tensor out = at::empty(y.sizes(), y.options());
+    DCLIP_CALL(dclip_row_scale_add(has_x ? ptr<float>(*x) : nullptr, ptr<float>(y), ptr<float>(s), (int)s.numel(),
+                                   ptr<float>(out), y.size(0), (int)y.size(1), stream_of(y)));
+    return out;
+}
+
 // ----------------------------------------------------------------------------- attention
 std::tuple<Tensor, Tensor> attn_fwd(const Tensor& qkv, int64_t B, int64_t N, int64_t H, double scale) {
     check_gpu(qkv, "qkv");
@@ -591,6 +605,7 @@ TORCH_LIBRARY(dclip, m) {
     m.def("gemm_tn(Tensor A, Tensor B) -> Tensor");
     m.def("cast(Tensor x, ScalarType dtype, float scale, Tensor? scale_t=None) -> Tensor");
     m.def("grad_scale(Tensor g, float target) -> Tensor");
+    m.def("row_scale_add(Tensor? x, Tensor y, Tensor s) -> Tensor");
     m.def("transpose2d(Tensor x, ScalarType dtype) -> Tensor");
     m.def("transpose_batched(Tensor x, int B, int rows, int cols, int ld_in, int rows_pad, ScalarType dtype) -> Tensor");
     m.def("add_readout_cast(Tensor a, Tensor b, int ntok, ScalarType lp_dtype, float scale) -> (Tensor, Tensor)");
@@ -636,6 +651,7 @@ TORCH_LIBRARY_IMPL(dclip, CUDA, m) {
     m.impl("gemm_tn", &gemm_tn);
     m.impl("cast", &cast);
     m.impl("grad_scale", &grad_scale);
+    m.impl("row_scale_add", &row_scale_add);
     m.impl("transpose2d", &transpose2d);
     m.impl("transpose_batched", &transpose_batched);
     m.impl("add_readout_cast", &add_readout_cast);

@@ -291,7 +291,7 @@ class DenseCLIP(nn.Module):
         B, Cv, h, w = visual.shape
         HW = h * w
         cdt = visual.dtype if visual.dtype in (torch.bfloat16, torch.float16) else \
-            getattr(self.backbone, "compute_dtype", torch.bfloat16)
+            getattr(self.backbone, "compute_dtype", torch.float16)
         if 0 <= self.score_concat_index < len(x) and torch.is_grad_enabled() and any(
                 p.requires_grad for m in (self.vis_proj, self.global_proj, self.context_decoder) if m is not None
                 for p in m.parameters()):

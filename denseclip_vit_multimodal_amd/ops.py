@@ -257,6 +257,13 @@ def pos_interp_bwd(dout, g, H, W):
     return D().pos_interp_bwd(dout, g, H, W)
 
 
+def row_scale_add(x, y, s):
+    """(x or 0) + s[row % len(s)] * y for f32 (rows, C) token buffers: a residual branch under a
+    per-token stochastic-depth mask (see BlockFn meta[6])."""
+    _check(x, y, s)
+    return D().row_scale_add(x, y, s)
+
+
 def row_mean(x, B, rows, row_off=0, bstride=None):
     """(B, C) f32 mean over `rows` pixel rows per image of a row-major (.., C) tensor whose image b
     starts at row b*bstride/C + row_off (a ViT token buffer: bstride N*C, row_off 1)."""
@@ -406,26 +413,40 @@ class BlockFn(torch.autograd.Function):
     LN -> GEMM(+bias) -> fused attention -> GEMM(+bias+residual) -> LN -> GEMM(+bias+QuickGELU)
     -> GEMM(+bias+residual): 7 kernels, no elementwise passes.
 
-    meta[5] (optional) = (gh, gw, map dtype): the block also returns the per-layer read-out map
-    of its output (models.py:577-597 without ln_post; the layout of ReadoutFn), so the backward
-    receives the map's gradient beside the residual one and folds it into the cast that feeds
-    its first GEMM (dclip_add_readout_cast) instead of autograd summing two fp32 token
-    gradients."""
+    meta[5] (optional, may be None) = (gh, gw, map dtype): the block also returns the per-layer
+    read-out map of its output (models.py:577-597 without ln_post; the layout of ReadoutFn), so the
+    backward receives the map's gradient beside the residual one and folds it into the cast that
+    feeds its first GEMM (dclip_add_readout_cast) instead of autograd summing two fp32 token
+    gradients.
+
+    meta[6] (optional) = (m1, m2): stochastic depth in training (reference models.py:257-268,
+    291-294): f32 (Ntok,) keep masks already divided by the keep probability, one value per token
+    POSITION (timm's drop_path on the reference's LND layout); the attention / MLP branch is
+    added as x + m[token] * branch (dclip_row_scale_add) instead of through the fused residual
+    epilogue, and its gradient is scaled the same way."""
 
     @staticmethod
     def forward(ctx, x, meta, ln1w, ln1b, w_in, b_in, w_out, b_out, ln2w, ln2b, w1, b1, w2, b2):
         B, Ntok, H, cdt, fp8 = meta[:5]
         ro = meta[5] if len(meta) > 5 else None
+        dp = meta[6] if len(meta) > 6 else None
         C = x.shape[1]
         scale = (C // H) ** -0.5
         xh1, mu1, rs1 = layernorm_fwd(x, ln1w.detach(), ln1b.detach(), cdt)
         qkv = gemm(xh1, WEIGHTS.get(w_in, cdt), N.EPI_STORE_SCALED, bias=b_in.detach(),
                    aux=qkv_scale_vector(C, H, x.device))
         o, lse = attn_fwd_fp8(qkv, B, Ntok, H) if fp8 else attn_fwd(qkv, B, Ntok, H, scale)
-        xm = gemm(o, WEIGHTS.get(w_out, cdt), N.EPI_RESIDUAL, bias=b_out.detach(), aux=x)
+        if dp is None:
+            xm = gemm(o, WEIGHTS.get(w_out, cdt), N.EPI_RESIDUAL, bias=b_out.detach(), aux=x)
+        else:
+            xm = row_scale_add(x, gemm(o, WEIGHTS.get(w_out, cdt), bias=b_out.detach(), out_dtype=torch.float32),
+                               dp[0])
         xh2, mu2, rs2 = layernorm_fwd(xm, ln2w.detach(), ln2b.detach(), cdt)
         z, h = gemm(xh2, WEIGHTS.get(w1, cdt), N.EPI_GELU, bias=b1.detach())
-        xo = gemm(h, WEIGHTS.get(w2, cdt), N.EPI_RESIDUAL, bias=b2.detach(), aux=xm)
+        if dp is None:
+            xo = gemm(h, WEIGHTS.get(w2, cdt), N.EPI_RESIDUAL, bias=b2.detach(), aux=xm)
+        else:
+            xo = row_scale_add(xm, gemm(h, WEIGHTS.get(w2, cdt), bias=b2.detach(), out_dtype=torch.float32), dp[1])
         ctx.save_for_backward(x, mu1, rs1, xh1, qkv, o, lse, xm, mu2, rs2, xh2, z, h,
                               ln1w, w_in, w_out, ln2w, w1, w2)
         ctx.meta = meta
@@ -444,6 +465,7 @@ class BlockFn(torch.autograd.Function):
         # recomputed from the 16-bit q, k against the fp8 forward's own lse and delta taken from
         # its o — the straight-through gradient of the quantised forward
         B, Ntok, H, cdt, fp8 = ctx.meta[:5]
+        dp = ctx.meta[6] if len(ctx.meta) > 6 else None
         C = x.shape[1]
         scale = (C // H) ** -0.5
         need = ctx.needs_input_grad
@@ -461,7 +483,7 @@ class BlockFn(torch.autograd.Function):
         if dmap is not None:  # the read-out map's gradient joins the block output's
             gh, gw, _ = ctx.meta[5]
             base = _readout_grad_buffer(dmap, B, Ntok, gh, gw, C)
-            if base is not None and cdt == torch.bfloat16:
+            if base is not None and cdt == torch.bfloat16 and dp is None:
                 # one pass: dxo + map gradient (CLS rows masked) in fp32, and its bf16 copy
                 dxo, dy = D().add_readout_cast(dxo, base, Ntok, cdt, 1.0)
             elif base is not None:
@@ -473,9 +495,11 @@ class BlockFn(torch.autograd.Function):
 
         # ---- MLP: xo = xm + h W2^T + b2,  h = qgelu(z),  z = xh2 W1^T + b1
         # (s1, s2: device-side power-of-two gradient scales, None unless fp16 — see grad_scale)
-        s1 = grad_scale(dxo, cdt)
+        dbr = dxo if dp is None else row_scale_add(None, dxo, dp[1])  # the MLP branch's gradient
+        s1 = grad_scale(dbr, cdt)
         if dy is None:
-            dy = cast(dxo, cdt, scale_t=s1)
+            dy = cast(dbr, cdt, scale_t=s1)
+        del dbr
         dz = gemm(dy, WEIGHTS.get(w2, cdt, transposed=True), N.EPI_GELU_BWD, aux=z)
         dW2 = db2 = dW1 = db1 = None
         if wg:
@@ -484,16 +508,18 @@ class BlockFn(torch.autograd.Function):
         if wg:
             dW1, db1 = weight_grad(dz, xh2, db=zb1, scale=s1)
         del dz
-        if cdt == torch.bfloat16:  # no gradient scaling: the attention branch's operand comes out of the LN pass
+        if cdt == torch.bfloat16 and dp is None:  # no gradient scaling: the attention branch's operand comes out of the LN pass
             dxm, dyo = layernorm_bwd(dxh2, xm, ln2w.detach(), mu2, rs2, dln2w, dln2b, res=dxo, lp_dtype=cdt)
             s2 = None
         else:
             dxm = layernorm_bwd(dxh2, xm, ln2w.detach(), mu2, rs2, dln2w, dln2b, res=dxo)
         del dxh2
         # ---- attention: xm = x + o Wout^T + bout
-        if cdt != torch.bfloat16:
-            s2 = grad_scale(dxm, cdt)
-            dyo = cast(dxm, cdt, scale_t=s2)
+        if cdt != torch.bfloat16 or dp is not None:
+            dab = dxm if dp is None else row_scale_add(None, dxm, dp[0])  # the attention branch's gradient
+            s2 = grad_scale(dab, cdt)
+            dyo = cast(dab, cdt, scale_t=s2)
+            del dab
         do = gemm(dyo, WEIGHTS.get(w_out, cdt, transposed=True))
         dWo = dbo = dWi = dbi = None
         if wg:

@@ -290,6 +290,12 @@ int dclip_cityscapes_prepare(const uint8_t* img, const uint8_t* ids, const uint1
 int dclip_cast(const void* in, int in_dt, void* out, int out_dt, int64_t n, float scale,
                const float* scale_ptr, void* stream);
 
+/* Stochastic depth (drop_path, reference models.py:257-268, 291-294 on the LND layout: one keep
+ * value per token position): out[r][c] = (x ? x[r][c] : 0) + s[r % ntok] * y[r][c], f32
+ * (rows, cols) row-major, rows a multiple of ntok, cols % 4 == 0; out may alias x or y. */
+int dclip_row_scale_add(const float* x, const float* y, const float* s, int ntok, float* out, int64_t rows,
+                        int cols, void* stream);
+
 /* Power-of-two scale for the fp16 cast of an f32 gradient g (n elements, 16-byte aligned),
  * computed on the device: ws[0] = s = 2^clamp(floor(log2(target / max|g|)), -60, 60),
  * ws[1] = 1/s (s = 1 when max|g| is 0 or not finite).  ws: 4 floats, ws[2..3] zero on entry
