@@ -54,6 +54,9 @@ _SIGS = {
     "dclip_bilinear_bwd": [_c_void_p, _i32, _c_void_p, _c_void_p, _i64, _i32, _i32, _i32, _i32, _c_void_p],
     "dclip_cast": [_c_void_p, _i32, _c_void_p, _i32, _i64, _f32, _c_void_p, _c_void_p],
     "dclip_grad_scale": [_c_void_p, _i64, _f32, _c_void_p, _c_void_p],
+    "dclip_cityscapes_augment": [_c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p, _i32, _i32,
+                                 _c_void_p, _c_void_p, _f32, _f32, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p,
+                                 _c_void_p],
     "dclip_row_scale_add": [_c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _i64, _i32, _c_void_p],
     "dclip_add_readout_cast": [_c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _i32, _i64, _i32, _i32, _f32,
                                _c_void_p],

@@ -575,6 +575,10 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> cityscapes_prepare(const Tensor& img,
     check_gpu(img, "img"); check_gpu(ids, "ids"); check_gpu(disp, "disp"); check_gpu(crop, "crop");
     TORCH_CHECK(mean.size() == 3 && stdv.size() == 3, "cityscapes_prepare: 3 means / stds");
     TORCH_CHECK(img.dim() == 4 && img.size(3) == 3 && crop.scalar_type() == at::kInt, "cityscapes_prepare: shapes");
+    // crop (B, 3) = window + flip; crop (B, 7) = the RandomScale / PadIfNeeded parameters in front
+    const bool aug = crop.dim() == 2 && crop.size(1) == 7;
+    TORCH_CHECK(crop.dim() == 2 && (crop.size(1) == 3 || aug) && crop.size(0) == img.size(0),
+                "cityscapes_prepare: crop (B, 3) or params (B, 7) int32");
     c10::DeviceGuard g(img.device());
     const int64_t B = img.size(0), H = img.size(1), W = img.size(2);
     Tensor out_img = at::empty({B, 3, h, w}, like(img, out_dtype));
@@ -583,10 +587,10 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> cityscapes_prepare(const Tensor& img,
     Tensor mask = at::empty({B, 1, h, w}, like(img, at::kByte));
     const float m[3] = {(float)mean[0], (float)mean[1], (float)mean[2]};
     const float s[3] = {(float)stdv[0], (float)stdv[1], (float)stdv[2]};
-    DCLIP_CALL(dclip_cityscapes_prepare(ptr<uint8_t>(img), ptr<uint8_t>(ids), (const uint16_t*)disp.data_ptr(), (int)B,
-                                        (int)H, (int)W, ptr<int>(crop), (int)h, (int)w, m, s, (float)bf, (float)depth_max,
-                                        out_img.data_ptr(), dt_code(out_dtype), ptr<int64_t>(seg), ptr<float>(depth),
-                                        ptr<uint8_t>(mask), stream_of(img)));
+    auto fn = aug ? &dclip_cityscapes_augment : &dclip_cityscapes_prepare;
+    DCLIP_CALL(fn(ptr<uint8_t>(img), ptr<uint8_t>(ids), (const uint16_t*)disp.data_ptr(), (int)B, (int)H, (int)W,
+                  ptr<int>(crop), (int)h, (int)w, m, s, (float)bf, (float)depth_max, out_img.data_ptr(),
+                  dt_code(out_dtype), ptr<int64_t>(seg), ptr<float>(depth), ptr<uint8_t>(mask), stream_of(img)));
     return {out_img, seg, depth, mask};
 }
 

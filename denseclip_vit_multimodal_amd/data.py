@@ -5,12 +5,19 @@ remaps label ids, turns the uint16 disparity into metric depth and runs the trai
 albumentations pipeline on the CPU, then ships f32 / int64 tensors (25 bytes per pixel).
 Here the CPU only scans and decodes (`CityscapesDepthSegDataset`, same file layout, names and
 errors as the reference); `prepare_batch` uploads the decoded uint8 / uint16 planes (6 bytes
-per pixel) and one HIP kernel (`dclip_cityscapes_prepare`) does the label remap, the
-disparity -> depth conversion, the random crop + horizontal flip and the normalisation, writing
-the batch in the layout `train.train_step` takes.
+per pixel) and one HIP kernel does the label remap, the disparity -> depth conversion, the
+trainer's spatial augmentation and the normalisation, writing the batch in the layout
+`train.train_step` takes:
+  * `dclip_cityscapes_augment` (params from `random_scale_crops`): the whole train pipeline of
+    train_denseclip.py:138-149, RandomScale(0.5..2.0) -> PadIfNeeded -> RandomCrop ->
+    HorizontalFlip -> Normalize, with cv2's 8-bit INTER_CUBIC for the image (the reference's
+    interpolation=Image.BILINEAR is the integer 2, which cv2 reads as INTER_CUBIC) and
+    INTER_NEAREST for the label ids / disparity, restated from OpenCV's resize (cv2 is not
+    installed here: that restatement is parity-unpinned against cv2 itself, see DESIGN.md);
+  * `dclip_cityscapes_prepare` (crops from `random_crops`): crop + flip only (no rescale).
 
-Not reproduced: albumentations' RandomScale / PadIfNeeded / ColorJitter (cv2 resampling
-arithmetic is not restated here); `prepare_batch` crops windows inside the image.
+Not reproduced: ColorJitter, which the reference enables only with `color_jitter: true` (off in
+the Cityscapes configs).
 """
 import os
 import os.path as osp
@@ -94,19 +101,51 @@ def random_crops(B, H, W, h, w, generator=None, flip_p=0.5):
     return torch.stack([y0, x0, flip], 1).to(torch.int32)
 
 
+def random_scale_crops(B, H, W, h, w, scale_range=(0.5, 2.0), rng=None, flip_p=0.5):
+    """RandomScale + PadIfNeeded + RandomCrop + HorizontalFlip parameters per image, int32 (B, 7) =
+    (Hs, Ws, pad_top, pad_left, y0, x0, flip), drawn like albumentations (train_denseclip.py:
+    138-149): scale ~ U(scale_range), (Hs, Ws) = (int(H s), int(W s)); centred padding up to
+    the crop, top = int(pad / 2); y0 = int((Hp - h + 1) u), x0 likewise; flip with flip_p.
+    rng: a `random.Random` (albumentations draws from Python's `random`)."""
+    import random
+    r = rng if rng is not None else random
+    out = []
+    for _ in range(B):
+        s = r.uniform(scale_range[0], scale_range[1])
+        Hs, Ws = int(H * s), int(W * s)
+        ph, pw = max(0, h - Hs), max(0, w - Ws)
+        pt, pl = int(ph / 2.0), int(pw / 2.0)
+        Hp, Wp = Hs + ph, Ws + pw
+        y0 = int((Hp - h + 1) * r.random())
+        x0 = int((Wp - w + 1) * r.random())
+        out.append((Hs, Ws, pt, pl, y0, x0, int(r.random() < flip_p)))
+    return torch.tensor(out, dtype=torch.int32)
+
+
 def prepare_batch(samples, crop_hw, crops, device, out_dtype=torch.bfloat16, mean=CLIP_MEAN, std=CLIP_STD,
                   depth_max=80.0, bf=BASELINE_FOCAL_LENGTH):
     """samples: list of (img uint8 HxWx3, ids uint8 HxW, disp uint16 HxW) of one size;
-    crops: int32 (B, 3) (y0, x0, flip).  Returns (img (B,3,h,w) out_dtype, seg int64 (B,h,w),
-    depth f32 (B,1,h,w), mask bool (B,1,h,w)) on `device`, ready for train.train_step."""
+    crops: int32 (B, 3) (y0, x0, flip) — a window of the image (`random_crops`) — or (B, 7)
+    (Hs, Ws, pad_top, pad_left, y0, x0, flip) — the rescaled / padded pipeline
+    (`random_scale_crops`).  Returns (img (B,3,h,w) out_dtype, seg int64 (B,h,w), depth f32
+    (B,1,h,w), mask bool (B,1,h,w)) on `device`, ready for train.train_step."""
     if not samples:
         raise ValueError("empty batch")
     H, W = samples[0][1].shape
     h, w = crop_hw
     B = len(samples)
-    crops = torch.as_tensor(crops, dtype=torch.int32).reshape(B, 3)
-    if ((crops[:, 0] < 0) | (crops[:, 0] + h > H) | (crops[:, 1] < 0) | (crops[:, 1] + w > W)).any():
-        raise ValueError(f"crop windows must lie inside the {H}x{W} images (got {crops.tolist()})")
+    crops = torch.as_tensor(crops, dtype=torch.int32)
+    if crops.dim() == 2 and crops.shape == (B, 7):
+        Hs, Ws, pt, pl, y0, x0 = (crops[:, i] for i in range(6))
+        bad = (Hs < 1) | (Ws < 1) | (pt < 0) | (pl < 0) | (y0 < 0) | (x0 < 0) | \
+              (y0 + h > torch.maximum(Hs + pt, torch.full_like(Hs, h))) | \
+              (x0 + w > torch.maximum(Ws + pl, torch.full_like(Ws, w)))
+        if bad.any():
+            raise ValueError(f"bad scale / pad / crop parameters {crops.tolist()} for a {h}x{w} crop")
+    else:
+        crops = crops.reshape(B, 3)
+        if ((crops[:, 0] < 0) | (crops[:, 0] + h > H) | (crops[:, 1] < 0) | (crops[:, 1] + w > W)).any():
+            raise ValueError(f"crop windows must lie inside the {H}x{W} images (got {crops.tolist()})")
     for s in samples:
         if s[0].shape != (H, W, 3) or s[1].shape != (H, W) or s[2].shape != (H, W):
             raise ValueError("all samples of a batch must share one image size")

@@ -284,6 +284,20 @@ int dclip_cityscapes_prepare(const uint8_t* img, const uint8_t* ids, const uint1
                              float depth_max, void* out_img, int out_dt, int64_t* out_seg, float* out_depth,
                              uint8_t* out_mask, void* stream);
 
+/* dclip_cityscapes_prepare with the trainer's whole spatial pipeline in front of the crop
+ * (train_denseclip.py:138-149): RandomScale -> PadIfNeeded -> RandomCrop -> HorizontalFlip.
+ * params int32 (B, 7) on the device = (Hs, Ws, pad_top, pad_left, y0, x0, flip) per image: the
+ * image is resized to Hs x Ws (cv2 INTER_CUBIC on uint8, the flag the reference's
+ * interpolation=Image.BILINEAR (= 2) selects; label ids and disparity INTER_NEAREST), padded by
+ * pad_top / pad_left (image 0, seg 255, depth 255 -> mask 1, as PadIfNeeded(value=0,
+ * mask_value=255) followed by the reference's depth > 0 validity), and the h x w window at
+ * (y0, x0) of the padded image is taken (mirrored when flip).  Same outputs as
+ * dclip_cityscapes_prepare; identity params (H, W, 0, 0, y0, x0, flip) give its result.   */
+int dclip_cityscapes_augment(const uint8_t* img, const uint8_t* ids, const uint16_t* disp, int B, int H, int W,
+                             const int* params, int h, int w, const float* mean, const float* stdv, float bf,
+                             float depth_max, void* out_img, int out_dt, int64_t* out_seg, float* out_depth,
+                             uint8_t* out_mask, void* stream);
+
 /* Element-wise dtype conversion of n elements: out = (out_dt)(in * scale), times *scale_ptr
  * when non-null (read on the device).  A power-of-two scale keeps fp16 gradients out of the
  * subnormal range (see dclip_grad_scale and dclip_gemm's alpha).                      */

@@ -61,3 +61,88 @@ def prepare(samples, crop_hw, crops, mean, std, bf=500.0, depth_max=80.0):
         depths.append(depth[None])
         masks.append((depth > 0)[None])
     return np.stack(imgs), np.stack(segs), np.stack(depths), np.stack(masks)
+
+
+# ---------------------------------------------------------------------------- RandomScale + PadIfNeeded
+# train_denseclip.py:138-149.  cv2 is not installed here: the resize below restates OpenCV's generic
+# 8-bit resize path (modules/imgproc/src/resize.cpp: interpolateCubic, fixed-point HResizeCubic /
+# VResizeCubic, resizeNN) — parity against cv2 itself is UNPINNED; tests/test_data_cpu.py holds it
+# within 1 LSB of torch's float bicubic (same A = -0.75 kernel, half-pixel centres, clamped borders).
+def _cubic_coeffs(fx):
+    """interpolateCubic(fx) (A = -0.75, f32 op by op) rounded to 11-bit fixed point (int32 (n, 4))."""
+    f32 = np.float32
+    x = fx.astype(f32)
+    A = f32(-0.75)
+    one = f32(1)
+    c0 = ((A * (x + one) - f32(5) * A) * (x + one) + f32(8) * A) * (x + one) - f32(4) * A
+    c1 = ((A + f32(2)) * x - (A + f32(3))) * x * x + one
+    c2 = ((A + f32(2)) * (one - x) - (A + f32(3))) * (one - x) * (one - x) + one
+    c3 = one - c0 - c1 - c2
+    c = np.stack([c0, c1, c2, c3], -1) * f32(2048)
+    return np.clip(np.rint(c), -32768, 32767).astype(np.int64)
+
+
+def _cubic_src(n_dst, n_src):
+    """sx = floor(fx), frac, fx = (float)((d + 0.5) * scale - 0.5), scale = 1 / (dst / src)."""
+    scale = 1.0 / (float(n_dst) / float(n_src))
+    fx = ((np.arange(n_dst, dtype=np.float64) + 0.5) * scale - 0.5).astype(np.float32)
+    sx = np.floor(fx).astype(np.int64)
+    return sx, fx - sx.astype(np.float32)
+
+
+def resize_cubic_u8(img, Hs, Ws):
+    """cv2.resize(img (H, W, 3) uint8, (Ws, Hs), INTER_CUBIC) restated (see above)."""
+    H, W = img.shape[:2]
+    sx, fx = _cubic_src(Ws, W)
+    sy, fy = _cubic_src(Hs, H)
+    ax, by = _cubic_coeffs(fx), _cubic_coeffs(fy)
+    cols = np.clip(sx[:, None] - 1 + np.arange(4), 0, W - 1)  # (Ws, 4)
+    rows = np.clip(sy[:, None] - 1 + np.arange(4), 0, H - 1)  # (Hs, 4)
+    src = img.astype(np.int64)
+    hv = (src[:, cols, :] * ax[None, :, :, None]).sum(2)       # (H, Ws, 3) horizontal pass, int
+    v = (hv[rows, :, :] * by[:, :, None, None]).sum(1)          # (Hs, Ws, 3)
+    return np.clip((v + (1 << 21)) >> 22, 0, 255).astype(np.uint8)
+
+
+def resize_nearest(a, Hs, Ws):
+    """cv2.resize(a, (Ws, Hs), INTER_NEAREST): index min(floor(d * src / dst), src - 1)."""
+    H, W = a.shape[:2]
+    ix = np.minimum(np.floor(np.arange(Ws) * (1.0 / (float(Ws) / W))).astype(np.int64), W - 1)
+    iy = np.minimum(np.floor(np.arange(Hs) * (1.0 / (float(Hs) / H))).astype(np.int64), H - 1)
+    return a[iy][:, ix]
+
+
+def scale_pad_params(H, W, h, w, scale, h_start, w_start, flip):
+    """albumentations RandomScale (int(H s), int(W s)), PadIfNeeded (centred: top = int(pad / 2)),
+    RandomCrop (y0 = int((Hp - h + 1) * h_start)) -> (Hs, Ws, pad_top, pad_left, y0, x0, flip)."""
+    Hs, Ws = int(H * scale), int(W * scale)
+    ph, pw = max(0, h - Hs), max(0, w - Ws)
+    pt, pl = int(ph / 2.0), int(pw / 2.0)
+    Hp, Wp = Hs + ph, Ws + pw
+    return (Hs, Ws, pt, pl, int((Hp - h + 1) * h_start), int((Wp - w + 1) * w_start), int(bool(flip)))
+
+
+def prepare_augmented(samples, crop_hw, params, mean, std, bf=500.0, depth_max=80.0):
+    """dclip_cityscapes_augment: per sample resize (image cubic, label ids / disparity nearest),
+    pad (image 0, seg 255, depth 255.0), crop, mirror, then the prepare() outputs."""
+    h, w = crop_hw
+    imgs, segs, depths, masks = [], [], [], []
+    for (img, ids, disp), (Hs, Ws, pt, pl, y0, x0, flip) in zip(samples, params):
+        H, W = ids.shape
+        im = img if (Hs, Ws) == (H, W) else resize_cubic_u8(img, Hs, Ws)
+        lab = map_labels(resize_nearest(ids, Hs, Ws))
+        dep, _ = disparity_to_depth(resize_nearest(disp, Hs, Ws), bf, depth_max)
+        Hp, Wp = max(Hs + pt, y0 + h), max(Ws + pl, x0 + w)  # a canvas holding the image and the window
+        pim = np.zeros((Hp, Wp, 3), np.uint8)
+        plab = np.full((Hp, Wp), 255, np.uint8)
+        pdep = np.full((Hp, Wp), 255.0, np.float32)
+        pim[pt:pt + Hs, pl:pl + Ws], plab[pt:pt + Hs, pl:pl + Ws], pdep[pt:pt + Hs, pl:pl + Ws] = im, lab, dep
+        win = (slice(y0, y0 + h), slice(x0, x0 + w))
+        im, lab, dep = pim[win], plab[win], pdep[win]
+        if flip:
+            im, lab, dep = im[:, ::-1], lab[:, ::-1], dep[:, ::-1]
+        imgs.append(normalize(im, mean, std).transpose(2, 0, 1))
+        segs.append(lab.astype(np.int64))
+        depths.append(dep[None])
+        masks.append((dep > 0)[None])
+    return np.stack(imgs), np.stack(segs), np.stack(depths), np.stack(masks)

@@ -77,3 +77,43 @@ def test_random_crops_and_cpu_refusal():
         prepare_batch([s], (4, 4), [[0, 0, 0]], "cpu")
     with pytest.raises(ValueError, match="inside"):
         prepare_batch([s], (4, 4), [[6, 0, 0]], "cpu")
+
+
+@pytest.mark.parametrize("H,W,Hs,Ws", [(48, 96, 73, 150), (48, 96, 24, 48), (64, 128, 50, 97), (32, 64, 64, 128)])
+def test_cubic_restatement_within_one_lsb_of_torch_bicubic(H, W, Hs, Ws):
+    """The oracle's cv2 INTER_CUBIC restatement (fixed point) against torch's float bicubic with the
+    same kernel (A = -0.75), centres and clamped borders: the fixed-point rounding moves at most
+    1 of 255 (cv2 itself is not installed: this is the available pin)."""
+    import torch.nn.functional as F
+    from oracle import data_oracle as D
+    img = np.random.default_rng(0).integers(0, 256, (H, W, 3), dtype=np.uint8)
+    ours = D.resize_cubic_u8(img, Hs, Ws).astype(np.int64)
+    t = torch.from_numpy(img).permute(2, 0, 1)[None].double()
+    ref = F.interpolate(t, size=(Hs, Ws), mode="bicubic", align_corners=False)[0].permute(1, 2, 0)
+    ref = ref.clamp(0, 255).round().numpy().astype(np.int64)
+    assert np.abs(ours - ref).max() <= 1
+    # 2x upscale: exact; identity size: the input
+    if (Hs, Ws) == (2 * H, 2 * W):
+        assert np.array_equal(ours, ref)
+    assert np.array_equal(D.resize_cubic_u8(img, H, W), img)
+
+
+def test_nearest_restatement_and_scale_params():
+    from oracle import data_oracle as D
+    from denseclip_vit_multimodal_amd.data import random_scale_crops
+    a = np.arange(6 * 8).reshape(6, 8)
+    assert np.array_equal(D.resize_nearest(a, 12, 16), np.repeat(np.repeat(a, 2, 0), 2, 1))
+    assert np.array_equal(D.resize_nearest(a, 3, 4), a[::2, ::2])
+    import random
+    p = random_scale_crops(64, 1024, 2048, 512, 1024, rng=random.Random(0))
+    assert p.shape == (64, 7) and p.dtype == torch.int32
+    Hs, Ws, pt, pl, y0, x0, fl = (p[:, i] for i in range(7))
+    assert ((Hs >= 512) & (Hs <= 2048) & (Ws >= 1024) & (Ws <= 4096)).all()
+    assert (pt == 0).all() and (pl == 0).all()  # scale >= 0.5 never needs padding at this crop
+    assert ((y0 >= 0) & (y0 + 512 <= Hs) & (x0 >= 0) & (x0 + 1024 <= Ws)).all()
+    assert set(fl.tolist()) == {0, 1}
+    # a crop larger than the scaled image: centred padding, as PadIfNeeded
+    q = random_scale_crops(8, 100, 200, 150, 300, scale_range=(0.5, 0.6), rng=random.Random(1))
+    for Hs, Ws, pt, pl, y0, x0, _ in q.tolist():
+        assert pt == (150 - Hs) // 2 and pl == (300 - Ws) // 2 and y0 == 0 and x0 == 0
+    assert D.scale_pad_params(100, 200, 150, 300, 0.5, 0.0, 0.999, 1) == (50, 100, 50, 100, 0, 0, 1)

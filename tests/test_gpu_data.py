@@ -72,3 +72,46 @@ def test_prepared_batch_trains():
                           out_dtype=torch.bfloat16)
     loss = train_step(m, opt, batch)
     assert torch.isfinite(loss)
+
+
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+def test_augment_scale_pad_crop_matches_oracle(out_dtype):
+    """dclip_cityscapes_augment (RandomScale + PadIfNeeded + RandomCrop + HorizontalFlip) bit-exact
+    against the oracle's restatement: up- and down-scales, a padded case, a flipped case and the
+    identity (which must equal dclip_cityscapes_prepare)."""
+    import random
+    from denseclip_vit_multimodal_amd.data import prepare_batch, random_scale_crops, CLIP_MEAN, CLIP_STD
+    B, H, W, h, w = 6, 64, 160, 48, 96
+    samples = _samples(B, H, W)
+    p = random_scale_crops(B, H, W, h, w, rng=random.Random(4))
+    p[0] = torch.tensor([H, W, 0, 0, 3, 7, 1], dtype=torch.int32)                       # identity scale
+    p[1] = torch.tensor([40, 60, 4, 18, 0, 0, 0], dtype=torch.int32)                     # padded both ways
+    p[2] = torch.tensor([int(H * 1.7), int(W * 1.7), 0, 0, 50, 100, 1], dtype=torch.int32)  # up, flipped
+    p[3] = torch.tensor([int(H * 0.8), int(W * 0.8), 0, 0, 2, 20, 0], dtype=torch.int32)    # down
+    img, seg, depth, mask = prepare_batch(samples, (h, w), p, "cuda", out_dtype=out_dtype)
+    ri, rs, rd, rm = D.prepare_augmented(samples, (h, w), p.tolist(), CLIP_MEAN, CLIP_STD)
+    assert torch.equal(img.cpu(), torch.from_numpy(np.ascontiguousarray(ri)).to(out_dtype))
+    assert torch.equal(seg.cpu(), torch.from_numpy(rs))
+    assert torch.equal(depth.cpu().view(torch.int32), torch.from_numpy(np.ascontiguousarray(rd)).view(torch.int32))
+    assert torch.equal(mask.cpu(), torch.from_numpy(rm))
+    assert (seg[1] == 255).any() and (depth[1] == 255.0).any()  # the padded border
+    # identity parameters = the crop-only kernel
+    i2, s2, d2, m2 = prepare_batch(samples[:1], (h, w), [[3, 7, 1]], "cuda", out_dtype=out_dtype)
+    assert torch.equal(i2, img[:1]) and torch.equal(s2, seg[:1]) and torch.equal(d2, depth[:1])
+
+
+def test_augment_full_resolution_batch():
+    """The Cityscapes train shape: 8 images 1024x2048 rescaled by U(0.5, 2) and cropped to 512x1024."""
+    import random
+    from denseclip_vit_multimodal_amd.data import prepare_batch, random_scale_crops
+    B, H, W = 8, 1024, 2048
+    rng = np.random.default_rng(1)
+    s = [(rng.integers(0, 256, (H, W, 3), dtype=np.uint8), rng.integers(0, 34, (H, W), dtype=np.uint8),
+          rng.integers(0, 3000, (H, W)).astype(np.uint16)) for _ in range(B)]
+    p = random_scale_crops(B, H, W, 512, 1024, rng=random.Random(0))
+    img, seg, depth, mask = prepare_batch(s, (512, 1024), p, "cuda")
+    assert img.shape == (B, 3, 512, 1024) and torch.isfinite(img.float()).all()
+    ri, rs, rd, rm = D.prepare_augmented(s[:1], (512, 1024), p[:1].tolist(), (0.48145466, 0.4578275, 0.40821073),
+                                         (0.26862954, 0.26130258, 0.27577711))
+    assert torch.equal(seg[:1].cpu(), torch.from_numpy(rs))
+    assert torch.equal(img[:1].float().cpu(), torch.from_numpy(np.ascontiguousarray(ri)).to(torch.bfloat16).float())
