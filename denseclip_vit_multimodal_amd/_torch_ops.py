@@ -72,6 +72,10 @@ def _register_fakes():
     def _(x, dtype, scale, scale_t=None):
         return _e(*x.shape, like=x, dtype=dtype)
 
+    @reg("dclip::bn_eval")
+    def _(x, w, b, running_mean, running_var, eps, relu):
+        return torch.empty_like(x, memory_format=torch.channels_last)
+
     @reg("dclip::row_scale_add")
     def _(x, y, s):
         return torch.empty_like(y)

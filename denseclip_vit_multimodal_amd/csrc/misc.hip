@@ -935,6 +935,17 @@ __global__ void bn_mask_affine_kernel(const float* __restrict__ w, const float* 
     k[4 * C + c] = (b ? b[c] : 0.f) - mean[c] * sc;
 }
 
+// eval mode: scale = w / sqrt(running_var + eps), shift = b - running_mean * scale into ss[0..2C)
+__global__ void bn_eval_affine_kernel(const float* __restrict__ w, const float* __restrict__ b,
+                                      const float* __restrict__ rmean, const float* __restrict__ rvar, float eps,
+                                      int C, float* __restrict__ ss) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= C) return;
+    const float sc = (w ? w[c] : 1.f) / sqrtf(rvar[c] + eps);
+    ss[c] = sc;
+    ss[C + c] = (b ? b[c] : 0.f) - rmean[c] * sc;
+}
+
 bool bn_shape_ok(int64_t rows, int C, int64_t ld) {
     const int tpr = C / 8;
     return rows > 0 && C % 8 == 0 && tpr >= 1 && tpr <= 256 && ld >= C && ld % 8 == 0;
@@ -971,6 +982,31 @@ extern "C" int dclip_bn_fwd(int dt, const void* x, int64_t rows, int C, int64_t 
         BN_FWD(f16)
     }
 #undef BN_FWD
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int dclip_bn_eval(int dt, const void* x, int64_t rows, int C, int64_t ld, const float* w, const float* b,
+                             float eps, const float* running_mean, const float* running_var, float* ws, void* y,
+                             int relu, void* stream) {
+    DCLIP_HOST_CHECK(dt == DCLIP_BF16 || dt == DCLIP_F16, "dclip_bn_eval: dtype must be bf16/f16");
+    DCLIP_HOST_CHECK(bn_shape_ok(rows, C, ld), "dclip_bn_eval: need rows > 0, C %% 8 == 0, C <= 2048, ld >= C, "
+                     "ld %% 8 == 0 (C = %d)", C);
+    DCLIP_HOST_CHECK(running_mean && running_var && ws, "dclip_bn_eval: running statistics and workspace required");
+    DCLIP_HOST_CHECK(((uintptr_t)x % 16) == 0 && ((uintptr_t)y % 16) == 0, "dclip_bn_eval: unaligned buffers");
+    hipStream_t st = (hipStream_t)stream;
+    float* ss = ws + (int64_t)BN_NBLK_MAX * 2 * C;
+    const unsigned ga = grid_for(rows * (C / 8), 8192);
+    bn_eval_affine_kernel<<<(C + 255) / 256, 256, 0, st>>>(w, b, running_mean, running_var, eps, C, ss);
+#define BN_EVAL(T)                                                                                                 \
+    if (relu) bn_apply_kernel<T, false, true><<<ga, 256, 0, st>>>((const T*)x, nullptr, ss, rows, C, ld, (T*)y);   \
+    else bn_apply_kernel<T, false, false><<<ga, 256, 0, st>>>((const T*)x, nullptr, ss, rows, C, ld, (T*)y);
+    if (dt == DCLIP_BF16) {
+        BN_EVAL(bf16)
+    } else {
+        BN_EVAL(f16)
+    }
+#undef BN_EVAL
     DCLIP_LAUNCH_CHECK();
     return 0;
 }

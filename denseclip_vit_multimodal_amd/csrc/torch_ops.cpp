@@ -447,6 +447,21 @@ std::tuple<Tensor, Tensor, Tensor> bn_fwd(const Tensor& x, const c10::optional<T
     return {y, std::get<0>(ms), std::get<1>(ms)};
 }
 
+// eval mode (running statistics), channels-last map in, channels-last map out
+Tensor bn_eval(const Tensor& x, const c10::optional<Tensor>& w, const c10::optional<Tensor>& b,
+               const Tensor& running_mean, const Tensor& running_var, double eps, bool relu) {
+    TORCH_CHECK(x.dim() == 4, "bn_eval: a channels-last 4-D map");
+    const Rows r = rows_of(x);
+    check_opt(w, "w"); check_opt(b, "b"); check_gpu(running_mean, "running_mean"); check_gpu(running_var, "running_var");
+    c10::DeviceGuard g(x.device());
+    Tensor y = at::empty_like(x, at::MemoryFormat::ChannelsLast);
+    Tensor ws = at::empty({dclip_bn_workspace(r.rows, (int)r.C)}, like(x, at::kFloat));
+    DCLIP_CALL(dclip_bn_eval(dt_code(x.scalar_type()), x.data_ptr(), r.rows, (int)r.C, r.ld, optr<float>(w),
+                             optr<float>(b), (float)eps, ptr<float>(running_mean), ptr<float>(running_var),
+                             ptr<float>(ws), y.data_ptr(), relu ? 1 : 0, stream_of(x)));
+    return y;
+}
+
 // (rows view) y written in place into the caller's buffer
 std::tuple<Tensor, Tensor> bn_fwd_rows(const Tensor& x, const c10::optional<Tensor>& w, const c10::optional<Tensor>& b,
                                        c10::optional<Tensor> running_mean, c10::optional<Tensor> running_var,
@@ -610,6 +625,7 @@ TORCH_LIBRARY(dclip, m) {
     m.def("cast(Tensor x, ScalarType dtype, float scale, Tensor? scale_t=None) -> Tensor");
     m.def("grad_scale(Tensor g, float target) -> Tensor");
     m.def("row_scale_add(Tensor? x, Tensor y, Tensor s) -> Tensor");
+    m.def("bn_eval(Tensor x, Tensor? w, Tensor? b, Tensor running_mean, Tensor running_var, float eps, bool relu) -> Tensor");
     m.def("transpose2d(Tensor x, ScalarType dtype) -> Tensor");
     m.def("transpose_batched(Tensor x, int B, int rows, int cols, int ld_in, int rows_pad, ScalarType dtype) -> Tensor");
     m.def("add_readout_cast(Tensor a, Tensor b, int ntok, ScalarType lp_dtype, float scale) -> (Tensor, Tensor)");
@@ -656,6 +672,7 @@ TORCH_LIBRARY_IMPL(dclip, CUDA, m) {
     m.impl("cast", &cast);
     m.impl("grad_scale", &grad_scale);
     m.impl("row_scale_add", &row_scale_add);
+    m.impl("bn_eval", &bn_eval);
     m.impl("transpose2d", &transpose2d);
     m.impl("transpose_batched", &transpose_batched);
     m.impl("add_readout_cast", &add_readout_cast);

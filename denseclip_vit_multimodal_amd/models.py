@@ -18,9 +18,9 @@ logger = logging.getLogger(__name__)
 
 
 class BatchNorm2d(nn.BatchNorm2d):
-    """nn.BatchNorm2d (same parameters, buffers and state-dict keys).  Train mode on 16-bit
-    channels-last maps runs the HIP batch-norm kernels (ops.BatchNormFn); everything else runs
-    torch's native kernels instead of MIOpen: MIOpen's batch-norm segfaults on the host for a
+    """nn.BatchNorm2d (same parameters, buffers and state-dict keys).  16-bit channels-last maps
+    run the HIP batch-norm kernels: train mode through ops.BatchNormFn, eval mode (no gradient)
+    through dclip_bn_eval; everything else runs torch's native kernels instead of MIOpen: MIOpen's batch-norm segfaults on the host for a
     bf16 channels-last (1, 128, 73, 146) map in train mode — the ViT-L/14 neck at 1024x2048 —
     while fp32, NCHW, other sizes and the native kernels are fine (tools/bn_probe.py,
     gpurun_out/bn_probe.log)."""
@@ -30,6 +30,8 @@ class BatchNorm2d(nn.BatchNorm2d):
             # batch statistics on the HIP kernels (torch's native channels-last kernels run at
             # ~0.12 TB/s on the neck maps): dclip_bn_fwd / dclip_bn_bwd
             return ops.bn_train(self, x)
+        if ops.bn_eval_ok(self, x):  # running statistics, no gradient: dclip_bn_eval
+            return ops.bn_eval(self, x)
         if x.is_cuda:
             with torch.backends.cudnn.flags(enabled=False):
                 return super().forward(x)
@@ -470,6 +472,8 @@ class ViTFeatureFusionNeck(nn.Module):
             y = conv(x)
         if ops.bn_hip_ok(bn, y):
             return ops.bn_train(bn, y, relu=True)  # BN + ReLU in one pass each way
+        if ops.bn_eval_ok(bn, y):
+            return ops.bn_eval(bn, y, relu=True)   # eval: running statistics, ReLU fused
         return act(bn(y))
 
     def forward(self, features):

@@ -653,6 +653,24 @@ def bn_train(bn, x, relu=False):
     return BatchNormFn.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum, bn.eps, relu)
 
 
+def bn_eval(bn, x, relu=False):
+    """`bn` (an nn.BatchNorm2d in eval mode with running statistics) on x via dclip_bn_eval, with
+    the following ReLU fused when relu.  No autograd (eval).  Caller checks bn_eval_ok."""
+    w = bn.weight.detach() if bn.weight is not None else None
+    b = bn.bias.detach() if bn.bias is not None else None
+    _check(w, b, bn.running_mean, bn.running_var, strided=(x,))
+    return D().bn_eval(x, w, b, bn.running_mean, bn.running_var, float(bn.eps), bool(relu))
+
+
+def bn_eval_ok(bn, x):
+    """Whether eval-mode `bn` runs on dclip_bn_eval for x (no gradient needed through it)."""
+    f32 = all(t is None or t.dtype == torch.float32 for t in (bn.weight, bn.bias, bn.running_mean, bn.running_var))
+    needs_grad = torch.is_grad_enabled() and (x.requires_grad or any(
+        p is not None and p.requires_grad for p in (bn.weight, bn.bias)))
+    return (not bn.training and bn.track_running_stats and bn.running_mean is not None and f32
+            and not needs_grad and bn_supported(x))
+
+
 def bn_hip_ok(bn, x):
     """Whether `bn` in its current mode runs on the HIP batch-norm kernels for input x."""
     f32 = all(t is None or t.dtype == torch.float32 for t in (bn.weight, bn.bias, bn.running_mean, bn.running_var))
@@ -1033,6 +1051,8 @@ def fcn_head(head, x):
     y = Conv3x3Fn.apply(x, c3.weight, cdt)
     if bn_hip_ok(bn, y):
         y = bn_train(bn, y, relu=True)
+    elif bn_eval_ok(bn, y):
+        y = bn_eval(bn, y, relu=True)
     else:
         y = relu(bn(y))
     y = drop(y)

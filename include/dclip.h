@@ -304,6 +304,13 @@ int dclip_cityscapes_augment(const uint8_t* img, const uint8_t* ids, const uint1
 int dclip_cast(const void* in, int in_dt, void* out, int out_dt, int64_t n, float scale,
                const float* scale_ptr, void* stream);
 
+/* Eval-mode BatchNorm2d (+ ReLU when relu != 0) from the running statistics, on the same rows
+ * as dclip_bn_fwd: y = x * w / sqrt(running_var + eps) + (b - running_mean * that scale), f32
+ * arithmetic, 16-bit I/O.  ws: dclip_bn_workspace(rows, C) floats.  (nn.BatchNorm2d.eval() of
+ * the neck's ConvModules and the FCN heads, models.py:13-20.)                            */
+int dclip_bn_eval(int dt, const void* x, int64_t rows, int C, int64_t ld, const float* w, const float* b, float eps,
+                  const float* running_mean, const float* running_var, float* ws, void* y, int relu, void* stream);
+
 /* Stochastic depth (drop_path, reference models.py:257-268, 291-294 on the LND layout: one keep
  * value per token position): out[r][c] = (x ? x[r][c] : 0) + s[r % ntok] * y[r][c], f32
  * (rows, cols) row-major, rows a multiple of ntok, cols % 4 == 0; out may alias x or y. */

@@ -785,11 +785,45 @@ def test_batchnorm_train_vs_torch(dt, B, C, H, W, shift):
 
 
 def test_batchnorm_eval_and_nchw_use_torch():
-    """Eval mode (running statistics) and NCHW / fp32 maps keep torch's kernels."""
+    """NCHW / fp32 maps keep torch's kernels."""
     O = ops()
     x = torch.randn(2, 64, 4, 4, device=DEV).to(torch.bfloat16)
     assert not O.bn_supported(x)  # NCHW
     assert not O.bn_supported(x.float().contiguous(memory_format=torch.channels_last))
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("shape,relu", [((2, 64, 9, 13), False), ((1, 128, 73, 146), True), ((2, 256, 64, 128), True)])
+def test_batchnorm_eval_hip_vs_torch(dt, shape, relu):
+    """Eval-mode BatchNorm2d (+ fused ReLU) from the running statistics on dclip_bn_eval vs
+    F.batch_norm in fp32 on the same 16-bit values (the (1, 128, 73, 146) bf16 map is the one
+    MIOpen's batch norm faulted on in round 1)."""
+    from denseclip_vit_multimodal_amd.models import BatchNorm2d
+    O = ops()
+    torch.manual_seed(0)
+    B, C, H, W = shape
+    bn = BatchNorm2d(C).to(DEV).eval()
+    with torch.no_grad():
+        bn.running_mean.normal_(0, 0.5)
+        bn.running_var.uniform_(0.2, 2.0)
+        bn.weight.normal_(1, 0.2)
+        bn.bias.normal_(0, 0.2)
+    x = (torch.randn(shape, device=DEV) * 1.5 + 0.3).to(dt).contiguous(memory_format=torch.channels_last)
+    assert O.bn_eval_ok(bn, x) or torch.is_grad_enabled()
+    with torch.no_grad():
+        assert O.bn_eval_ok(bn, x)
+        y = O.bn_eval(bn, x, relu=relu)
+        via_module = bn(x)
+    ref = torch.nn.functional.batch_norm(x.float(), bn.running_mean, bn.running_var, bn.weight, bn.bias, False,
+                                         0.0, bn.eps)
+    if relu:
+        ref = ref.clamp_min(0)
+    assert y.dtype == dt and y.is_contiguous(memory_format=torch.channels_last)
+    tol = 4e-3 if dt == torch.bfloat16 else 5e-4
+    assert rel_err(y.float(), ref) < tol
+    ref_noact = torch.nn.functional.batch_norm(x.float(), bn.running_mean, bn.running_var, bn.weight, bn.bias,
+                                               False, 0.0, bn.eps)
+    assert rel_err(via_module.float(), ref_noact) < tol
 
 
 # ----------------------------------------------------------------------------- BN + ReLU, heads, neck

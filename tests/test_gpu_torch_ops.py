@@ -69,6 +69,12 @@ def test_opcheck_resize_and_bn():
     buf = torch.randn(300, 1536, device=DEV).to(torch.bfloat16)
     _opcheck(D().bn_fwd_rows, (buf[:, 128:256], torch.rand(128, device=DEV), torch.randn(128, device=DEV), None, None,
                                0.1, 1e-5, True, torch.empty(300, 1536, device=DEV, dtype=torch.bfloat16)[:, 128:256]))
+    _opcheck(D().bn_eval, (m, torch.rand(128, device=DEV), torch.randn(128, device=DEV), torch.randn(128, device=DEV),
+                           torch.rand(128, device=DEV) + 0.5, 1e-5, True))
+    g = torch.randn(4096, device=DEV) * 1e-7
+    _opcheck(D().grad_scale, (g, 16.0))
+    _opcheck(D().row_scale_add, (torch.randn(258, 64, device=DEV), torch.randn(258, 64, device=DEV),
+                                 torch.rand(129, device=DEV)))
 
 
 def _block(C=768, H=12):
