@@ -862,13 +862,14 @@ __device__ __forceinline__ typename Mfma<T>::frag tn_frag(const char* img, int k
     return __builtin_bit_cast(typename Mfma<T>::frag, v);
 }
 
-// 64 rows x 256 columns (clamped: rows to krows - 1, columns to cols - 8) -> [64][512 B] image
-template <typename T>
+// BKT rows x 256 columns (clamped: rows to krows - 1, columns to cols - 8) -> [BKT][512 B] image
+template <typename T, int BKT = 64>
 __device__ __forceinline__ void stage_tn_big(const T* __restrict__ X, int64_t ldx, int k0, int krows, int col0,
                                              int cols, char* lds, int wave, int lane) {
+    constexpr int PW = BKT / 16;  // 1-KiB pieces (2 rows) per wave
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int piece = wave * 4 + i;  // 32 pieces of 2 rows
+    for (int i = 0; i < PW; ++i) {
+        const int piece = wave * PW + i;  // BKT / 2 pieces of 2 rows
         const int r = piece * 2 + (lane >> 5);
         const int c = (lane & 31) ^ (2 * tn_sw(r));
         int gr = k0 + r;
@@ -880,7 +881,9 @@ __device__ __forceinline__ void stage_tn_big(const T* __restrict__ X, int64_t ld
     }
 }
 
-template <typename T, int EPI>
+// BKT-row K-steps in a STAGES-deep ring; a counted vmcnt keeps STAGES - 2 younger K-steps in
+// flight across each barrier (BKT 64 / 2 stages: the original one-step-ahead loop).
+template <typename T, int EPI, int BKT = 64, int STAGES = 2>
 __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(const T* __restrict__ A, int64_t lda,
                                                              const T* __restrict__ B, int64_t ldb, int M, int N,
                                                              int Kreal, int k_chunk, int tiles_m, int tiles_n,
@@ -889,8 +892,9 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(const T* __restrict
     const float alpha = alpha_arg.get();
     typedef BigCfg<256, 256, 2, 4, 2> Cfg;
     typedef typename Mfma<T>::frag frag;
-    constexpr int STAGE = 2 * 64 * 512;  // A | B
-    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE > Cfg::EP_BYTES ? 2 * STAGE : Cfg::EP_BYTES];
+    constexpr int STAGE = 2 * BKT * 512;  // A | B
+    constexpr int G = 2 * (BKT / 16);     // LDS-DMA instructions per thread per K-step
+    __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE > Cfg::EP_BYTES ? STAGES * STAGE : Cfg::EP_BYTES];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int wm = wave / 4, wn = wave % 4;
@@ -900,8 +904,8 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(const T* __restrict
     const int m0 = (t / tiles_n) * 256;
     const int n0 = (t % tiles_n) * 256;
     const int kbeg = blockIdx.y * k_chunk;
-    int nk = k_chunk / BK;
-    if (kbeg + nk * BK > Kreal) nk = (Kreal - kbeg + BK - 1) / BK;  // fully padded tiles skipped
+    int nk = k_chunk / BKT;
+    if (kbeg + nk * BKT > Kreal) nk = (Kreal - kbeg + BKT - 1) / BKT;  // fully padded tiles skipped
     nk = nk < 0 ? 0 : nk;
 
     f32x4 acc[Cfg::NB][Cfg::MB];
@@ -912,21 +916,25 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(const T* __restrict
 
     auto stage = [&](int kt, int slot) {
         char* base = smem + slot * STAGE;
-        stage_tn_big<T>(A, lda, kbeg + kt * BK, Kreal, m0, M, base, wave, lane);
-        stage_tn_big<T>(B, ldb, kbeg + kt * BK, Kreal, n0, N, base + 64 * 512, wave, lane);
+        stage_tn_big<T, BKT>(A, lda, kbeg + kt * BKT, Kreal, m0, M, base, wave, lane);
+        stage_tn_big<T, BKT>(B, ldb, kbeg + kt * BKT, Kreal, n0, N, base + BKT * 512, wave, lane);
     };
-    if (nk > 0) stage(0, 0);
-    for (int kt = 0; kt < nk; ++kt) {
-        wait_vmcnt<0>();
-        __builtin_amdgcn_s_barrier();  // tile kt visible to every wave; slot of tile kt-1 free
-        __builtin_amdgcn_sched_barrier(0);
-        if (kt + 1 < nk) stage(kt + 1, (kt + 1) & 1);
-        const char* At = smem + (kt & 1) * STAGE;
-        const char* Bt = At + 64 * 512;
-        const int k0 = kbeg + kt * BK;
-        const bool ragged = k0 + BK > Kreal;
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
+    for (int s = 0; s < STAGES - 1; ++s)
+        if (s < nk) stage(s, s);
+    for (int kt = 0; kt < nk; ++kt) {
+        // K-step kt landed when at most min(STAGES - 2, nk - 1 - kt) younger K-steps are in flight
+        if (kt + STAGES - 2 <= nk - 1) wait_vmcnt<G * (STAGES - 2)>();
+        else wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();  // K-step kt visible to every wave; the slot of kt - 1 free
+        __builtin_amdgcn_sched_barrier(0);
+        if (kt + STAGES - 1 < nk) stage(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+        const char* At = smem + (kt % STAGES) * STAGE;
+        const char* Bt = At + BKT * 512;
+        const int k0 = kbeg + kt * BKT;
+        const bool ragged = k0 + BKT > Kreal;
+#pragma unroll
+        for (int ks = 0; ks < BKT / 32; ++ks) {
             frag fb[Cfg::NB], fa[Cfg::MB];
 #pragma unroll
             for (int i = 0; i < Cfg::NB; ++i) fb[i] = tn_frag<T>(Bt, ks, wn * Cfg::WTN + i * 16, lane);
@@ -1595,11 +1603,18 @@ extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda
     gemm_tn_kernel<T, EPI, float><<<grid, 256, 0, st>>>((const T*)A, lda, (const T*)B, ldb, (int)M, (int)N,   \
                                                         (int)K, k_chunk, tiles_m, tiles_n, nullptr, OUT,        \
                                                         EPI == DCLIP_EPI_SPLITK ? N : ldc, (int64_t)M * N, alpha)
-    const bool big = dclip_option(DCLIP_OPT_GEMM_TN_TILE) != 1 && M >= 256 && N >= 256;
-#define TN_BIG(T, EPI, OUT)                                                                                    \
-    gemm_tn_big_kernel<T, EPI><<<dim3(tm2 * tn2, splits), 512, 0, st>>>(                                       \
+    const int tn_opt = dclip_option(DCLIP_OPT_GEMM_TN_TILE);
+    const bool big = tn_opt != 1 && M >= 256 && N >= 256;
+#define TN_BIG_V(T, EPI, OUT, BKT, STG)                                                                        \
+    gemm_tn_big_kernel<T, EPI, BKT, STG><<<dim3(tm2 * tn2, splits), 512, 0, st>>>(                             \
         (const T*)A, lda, (const T*)B, ldb, (int)M, (int)N, (int)K, k_chunk, tm2, tn2, OUT,                     \
         EPI == DCLIP_EPI_SPLITK ? N : ldc, (int64_t)M * N, alpha)
+#define TN_BIG(T, EPI, OUT)                                                                                    \
+    do {                                                                                                       \
+        if (tn_opt == 2) TN_BIG_V(T, EPI, OUT, 32, 4);                                                         \
+        else if (tn_opt == 3) TN_BIG_V(T, EPI, OUT, 32, 5);                                                    \
+        else TN_BIG_V(T, EPI, OUT, 64, 2);                                                                     \
+    } while (0)
     const int tm2 = (int)((M + 255) / 256), tn2 = (int)((N + 255) / 256);
     if (epilogue == DCLIP_EPI_STORE) {
         DCLIP_HOST_CHECK(bias == nullptr, "dclip_gemm_tn: bias only with SPLITK");
@@ -1626,6 +1641,7 @@ extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda
     }
 #undef TN_LAUNCH
 #undef TN_BIG
+#undef TN_BIG_V
     DCLIP_LAUNCH_CHECK();
     return 0;
 }

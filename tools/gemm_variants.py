@@ -79,7 +79,9 @@ for name, fn, fl in cases:
         row += f" | tile{t} {ms * 1e3:7.1f} us {fl / ms / 1e9:7.1f} TF/s"
     print(row, flush=True)
 
-# ---- weight gradients (TN): 128x128 vs 256x256 kernel
+# ---- weight gradients (TN): DCLIP_OPT_GEMM_TN_TILE variants (1 128x128, 0 256x256 BK64 x2,
+# 2 256x256 BK32 x4, 3 256x256 BK32 x5), checked against the 128x128 kernel
+TN_TILES = [int(v) for v in os.environ.get("TN_TILES", "1,0,2,3").split(",")]
 tn = []
 for name, n, k in [("dW qkv", 3 * C, C), ("dW out_proj", C, C), ("dW c_fc", 4 * C, C), ("dW c_proj", C, 4 * C)]:
     dy = torch.randn(M, n, device="cuda").to(bf)
@@ -88,21 +90,22 @@ for name, n, k in [("dW qkv", 3 * C, C), ("dW out_proj", C, C), ("dW c_fc", 4 * 
 for name, fn, fl in tn:
     N.call("dclip_set_option", N.OPT_GEMM_TN_TILE, 1)
     ref = fn()
-    N.call("dclip_set_option", N.OPT_GEMM_TN_TILE, 0)
-    y = fn()
-    err = float((y - ref).norm() / ref.norm())
-    if err > 1e-4:
-        print(f"MISMATCH {name}: rel err {err:.2e}", flush=True)
-tt = {(c[0], t): [] for c in tn for t in (1, 0)}
+    for t in TN_TILES:
+        N.call("dclip_set_option", N.OPT_GEMM_TN_TILE, t)
+        y = fn()
+        err = float((y - ref).norm() / ref.norm())
+        if err > 1e-4:
+            print(f"MISMATCH {name} tn {t}: rel err {err:.2e}", flush=True)
+tt = {(c[0], t): [] for c in tn for t in TN_TILES}
 for r in range(rounds):
     for name, fn, fl in tn:
-        for t in (1, 0):
+        for t in TN_TILES:
             N.call("dclip_set_option", N.OPT_GEMM_TN_TILE, t)
             tt[(name, t)].append(ev(fn))
 N.call("dclip_set_option", N.OPT_GEMM_TN_TILE, 0)
 for name, fn, fl in tn:
     row = f"{name:20s}"
-    for t in (1, 0):
+    for t in TN_TILES:
         ms = sorted(tt[(name, t)])[rounds // 2]
-        row += f" | tn{'128' if t == 1 else '256'} {ms * 1e3:7.1f} us {fl / ms / 1e9:7.1f} TF/s"
+        row += f" | tn{t} {ms * 1e3:7.1f} us {fl / ms / 1e9:7.1f} TF/s"
     print(row, flush=True)
