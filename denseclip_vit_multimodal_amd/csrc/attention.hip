@@ -363,11 +363,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_kernel(const T* __re
 // recomputed from K(t), still in its slot, the reference moves to the tile's row max and O,
 // l and S(t+1) are rescaled — BEFORE P(t) enters O or l.  Without a firing every P <= 2^12
 // (representable in fp16; the relative rounding of 16-bit P does not depend on its size).
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-
-__device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
-}
 
 template <typename T, int NW>
 struct Fwd2Ctx {

@@ -120,6 +120,13 @@ __device__ __forceinline__ float quick_gelu_grad(float z) {
     return s + 1.702f * z * s * (1.0f - s);
 }
 
+// buffer resource over [p, p + bytes): buffer loads past the end read 0 (LDS-DMA staging)
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
 // GEMM output scale: v, times *p when p is set (a device-resident factor such as the 1/s of a
 // dclip_grad_scale pair, read once per workgroup — no host round trip for fp16 gradients)
 struct Alpha {

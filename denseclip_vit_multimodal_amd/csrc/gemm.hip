@@ -883,6 +883,23 @@ __device__ __forceinline__ void stage_tn_big(const T* __restrict__ X, int64_t ld
 
 // BKT-row K-steps in a STAGES-deep ring; a counted vmcnt keeps STAGES - 2 younger K-steps in
 // flight across each barrier (BKT 64 / 2 stages: the original one-step-ahead loop).
+// one K-step's LDS-DMA: this thread's PW pieces of A and of B (byte offsets va / vb + the step's
+// row offset ka / kb), as buffer loads (rows past the buffers' ends read 0)
+template <int PW, int BKT>
+__device__ __forceinline__ void tn_stage_buf(const void* A, uint32_t abytes, const void* B, uint32_t bbytes, char* base,
+                                             const uint32_t (&va)[PW], const uint32_t (&vb)[PW], uint32_t ka,
+                                             uint32_t kb, int wave) {
+#if defined(__HIP_DEVICE_COMPILE__)  // the buffer-resource type exists only for the device target
+    const rsrc_t ra = make_rsrc(A, abytes), rb = make_rsrc(B, bbytes);
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, LDS_PTR(base + (wave * PW + i) * 1024), 16, va[i] + ka, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, LDS_PTR(base + BKT * 512 + (wave * PW + i) * 1024), 16, vb[i] + kb,
+                                                 0, 0, 0);
+    }
+#endif
+}
+
 template <typename T, int EPI, int BKT = 64, int STAGES = 2>
 __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(const T* __restrict__ A, int64_t lda,
                                                              const T* __restrict__ B, int64_t ldb, int M, int N,
@@ -900,10 +917,17 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(const T* __restrict
     const int wm = wave / 4, wn = wave % 4;
     const int lq = lane >> 4;
 
-    const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+    // one-dimensional grid over (K split, tile), split-major, in XCD-contiguous ranges: the
+    // workgroups that share a split's token rows (every tile of it reads the same K range of both
+    // operands) run on one XCD and meet in its L2 (a (tiles, splits) grid spread each split over
+    // all eight XCDs: 46 % L2 hits)
+    const int ntile = tiles_m * tiles_n;
+    const int lin = xcd_remap(blockIdx.x, gridDim.x);
+    const int split = lin / ntile;
+    const int t = lin - split * ntile;
     const int m0 = (t / tiles_n) * 256;
     const int n0 = (t % tiles_n) * 256;
-    const int kbeg = blockIdx.y * k_chunk;
+    const int kbeg = split * k_chunk;
     int nk = k_chunk / BKT;
     if (kbeg + nk * BKT > Kreal) nk = (Kreal - kbeg + BKT - 1) / BKT;  // fully padded tiles skipped
     nk = nk < 0 ? 0 : nk;
@@ -914,48 +938,71 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(const T* __restrict
 #pragma unroll
         for (int j = 0; j < Cfg::MB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    auto stage = [&](int kt, int slot) {
-        char* base = smem + slot * STAGE;
-        stage_tn_big<T, BKT>(A, lda, kbeg + kt * BKT, Kreal, m0, M, base, wave, lane);
-        stage_tn_big<T, BKT>(B, ldb, kbeg + kt * BKT, Kreal, n0, N, base + BKT * 512, wave, lane);
-    };
+    // LDS-DMA sources as buffer loads: a per-lane byte offset of each of this thread's pieces,
+    // fixed for the launch, plus the K-step's row offset (one add per piece; the address
+    // arithmetic of a pointer per piece cost ~11 VALU instructions, 3 of them 64-bit multiplies,
+    // per load, all of them between the barrier and the first MFMA).  Rows past Kreal fall
+    // outside the buffer and read 0.
+    constexpr int PW = BKT / 16;
+    const uint32_t abytes = (uint32_t)((int64_t)Kreal * lda * sizeof(T));
+    const uint32_t bbytes = (uint32_t)((int64_t)Kreal * ldb * sizeof(T));
+    uint32_t va[PW], vb[PW];
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+        const int r = (wave * PW + i) * 2 + (lane >> 5);
+        const int c = (lane & 31) ^ (2 * tn_sw(r));
+        const int gca = m0 + c * 8 + 8 <= M ? m0 + c * 8 : M - 8;
+        const int gcb = n0 + c * 8 + 8 <= N ? n0 + c * 8 : N - 8;
+        va[i] = (uint32_t)(((int64_t)r * lda + gca) * sizeof(T));
+        vb[i] = (uint32_t)(((int64_t)r * ldb + gcb) * sizeof(T));
+    }
+    // (the buffer resources live only inside tn_stage_buf, compiled for the device alone: a template
+    // kernel body holding the device-only resource type makes hipcc drop the kernel's host stub)
+#define TN_STAGE(KT, SLOT)                                                                                          \
+    tn_stage_buf<PW, BKT>(A, abytes, B, bbytes, smem + (SLOT) * STAGE, va, vb,                                      \
+                          (uint32_t)((int64_t)(kbeg + (KT) * BKT) * lda * sizeof(T)),                               \
+                          (uint32_t)((int64_t)(kbeg + (KT) * BKT) * ldb * sizeof(T)), wave)
 #pragma unroll
     for (int s = 0; s < STAGES - 1; ++s)
-        if (s < nk) stage(s, s);
-    for (int kt = 0; kt < nk; ++kt) {
-        // K-step kt landed when at most min(STAGES - 2, nk - 1 - kt) younger K-steps are in flight
-        if (kt + STAGES - 2 <= nk - 1) wait_vmcnt<G * (STAGES - 2)>();
-        else wait_vmcnt<0>();
-        __builtin_amdgcn_s_barrier();  // K-step kt visible to every wave; the slot of kt - 1 free
-        __builtin_amdgcn_sched_barrier(0);
-        if (kt + STAGES - 1 < nk) stage(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
-        const char* At = smem + (kt % STAGES) * STAGE;
-        const char* Bt = At + BKT * 512;
-        const int k0 = kbeg + kt * BKT;
-        const bool ragged = k0 + BKT > Kreal;
-#pragma unroll
-        for (int ks = 0; ks < BKT / 32; ++ks) {
-            frag fb[Cfg::NB], fa[Cfg::MB];
-#pragma unroll
-            for (int i = 0; i < Cfg::NB; ++i) fb[i] = tn_frag<T>(Bt, ks, wn * Cfg::WTN + i * 16, lane);
-#pragma unroll
-            for (int j = 0; j < Cfg::MB; ++j) fa[j] = tn_frag<T>(At, ks, wm * Cfg::WTM + j * 16, lane);
-            if (ragged) {  // token rows past Kreal were clamped duplicates: zero them (A side)
-#pragma unroll
-                for (int j = 0; j < Cfg::MB; ++j)
-#pragma unroll
-                    for (int e = 0; e < 8; ++e)
-                        if (k0 + ks * 32 + 8 * lq + e >= Kreal) fa[j][e] = (T)0.f;
-            }
-#pragma unroll
-            for (int j = 0; j < Cfg::MB; ++j)
-#pragma unroll
-                for (int i = 0; i < Cfg::NB; ++i) acc[i][j] = Mfma16<T>::mma(fb[i], fa[j], acc[i][j]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
+        if (s < nk) TN_STAGE(s, s);
+    // one K-step; RAGGED (only the last step of the last split can be) masks the token rows past
+    // Kreal.  The ragged step is peeled off the loop so the steady-state body has no branch between
+    // its fragment reads and its MFMAs.
+#define TN_KSTEP(KT, RAGGED)                                                                                        \
+    do {                                                                                                            \
+        const int kt_ = (KT);                                                                                       \
+        if (kt_ + STAGES - 2 <= nk - 1) wait_vmcnt<G * (STAGES - 2)>();                                             \
+        else wait_vmcnt<0>();                                                                                       \
+        __builtin_amdgcn_s_barrier(); /* K-step kt visible to every wave; the slot of kt - 1 free */               \
+        __builtin_amdgcn_sched_barrier(0);                                                                          \
+        if (kt_ + STAGES - 1 < nk) TN_STAGE(kt_ + STAGES - 1, (kt_ + STAGES - 1) % STAGES);                         \
+        const char* At = smem + (kt_ % STAGES) * STAGE;                                                             \
+        const char* Bt = At + BKT * 512;                                                                            \
+        const int k0 = kbeg + kt_ * BKT;                                                                            \
+        _Pragma("unroll") for (int ks = 0; ks < BKT / 32; ++ks) {                                                   \
+            frag fb[Cfg::NB], fa[Cfg::MB];                                                                          \
+            _Pragma("unroll") for (int i = 0; i < Cfg::NB; ++i) fb[i] = tn_frag<T>(Bt, ks, wn * Cfg::WTN + i * 16, lane); \
+            _Pragma("unroll") for (int j = 0; j < Cfg::MB; ++j) fa[j] = tn_frag<T>(At, ks, wm * Cfg::WTM + j * 16, lane); \
+            if (RAGGED) {                                                                                           \
+                _Pragma("unroll") for (int j = 0; j < Cfg::MB; ++j)                                                 \
+                    _Pragma("unroll") for (int e = 0; e < 8; ++e)                                                   \
+                        if (k0 + ks * 32 + 8 * lq + e >= Kreal) fa[j][e] = (T)0.f;                                  \
+            }                                                                                                       \
+            _Pragma("unroll") for (int j = 0; j < Cfg::MB; ++j)                                                     \
+                _Pragma("unroll") for (int i = 0; i < Cfg::NB; ++i) acc[i][j] = Mfma16<T>::mma(fb[i], fa[j], acc[i][j]); \
+        }                                                                                                           \
+        __builtin_amdgcn_sched_barrier(0);                                                                          \
+    } while (0)
+    const bool last_ragged = nk > 0 && kbeg + nk * BKT > Kreal;
+    const int nfull = last_ragged ? nk - 1 : nk;
+    for (int kt = 0; kt < nfull; ++kt) TN_KSTEP(kt, false);
+    if (last_ragged) TN_KSTEP(nk - 1, true);
+#undef TN_KSTEP
+#undef TN_STAGE
+    // the split's slab (blockIdx.y is 0 on this grid, so the epilogue's own slab offset vanishes)
+    float* Cs = (float*)C + (EPI == DCLIP_EPI_SPLITK ? (int64_t)split * slab : 0);
     big_epilogue<T, EPI, float, Cfg>(acc, smem, M, N, m0 + wm * Cfg::WTM, n0 + wn * Cfg::WTN, nullptr, nullptr, 0,
-                                     C, ldc, nullptr, 0, slab, alpha);
+                                     Cs, ldc, nullptr, 0, slab, alpha);
 }
 
 // per-column sums of a row-major (rows x cols) matrix, accumulated into out (f32):
@@ -1589,6 +1636,8 @@ extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda
     DCLIP_HOST_CHECK(epilogue == DCLIP_EPI_STORE ? splits == 1 : ws != nullptr,
                      "dclip_gemm_tn: STORE needs splits == 1; SPLITK needs a workspace of splits*M*N f32");
     DCLIP_HOST_CHECK(ldc % 4 == 0, "dclip_gemm_tn: ldc %% 4 != 0");
+    DCLIP_HOST_CHECK(K * lda * 2 < (1ll << 32) && K * ldb * 2 < (1ll << 32),
+                     "dclip_gemm_tn: operands must stay below 4 GiB (buffer-load staging)");
     hipStream_t st = (hipStream_t)stream;
     const int tiles_m = (int)((M + BM - 1) / BM), tiles_n = (int)((N + BN - 1) / BN);
     const int k_chunk = (int)(K_pad / splits);
@@ -1606,7 +1655,7 @@ extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda
     const int tn_opt = dclip_option(DCLIP_OPT_GEMM_TN_TILE);
     const bool big = tn_opt != 1 && M >= 256 && N >= 256;
 #define TN_BIG_V(T, EPI, OUT, BKT, STG)                                                                        \
-    gemm_tn_big_kernel<T, EPI, BKT, STG><<<dim3(tm2 * tn2, splits), 512, 0, st>>>(                             \
+    gemm_tn_big_kernel<T, EPI, BKT, STG><<<dim3(tm2 * tn2 * splits), 512, 0, st>>>(                            \
         (const T*)A, lda, (const T*)B, ldb, (int)M, (int)N, (int)K, k_chunk, tm2, tn2, OUT,                     \
         EPI == DCLIP_EPI_SPLITK ? N : ldc, (int64_t)M * N, alpha)
 #define TN_BIG(T, EPI, OUT)                                                                                    \
