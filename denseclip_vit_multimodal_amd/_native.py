@@ -57,6 +57,8 @@ _SIGS = {
     "dclip_cityscapes_augment": [_c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p, _i32, _i32,
                                  _c_void_p, _c_void_p, _f32, _f32, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p,
                                  _c_void_p],
+    "dclip_color_jitter": [_c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p],
+    "dclip_normalize_u8": [_c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p],
     "dclip_bn_eval": [_i32, _c_void_p, _i64, _i32, _i64, _c_void_p, _c_void_p, _f32, _c_void_p, _c_void_p,
                       _c_void_p, _c_void_p, _i32, _c_void_p],
     "dclip_row_scale_add": [_c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _i64, _i32, _c_void_p],

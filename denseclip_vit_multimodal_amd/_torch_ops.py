@@ -189,7 +189,7 @@ def _register_fakes():
         return _e(*pred.shape, like=pred, dtype=f32)
 
     @reg("dclip::cityscapes_prepare")
-    def _(img, ids, disp, crop, h, w, mean, std, bf, depth_max, out_dtype):
+    def _(img, ids, disp, crop, h, w, mean, std, bf, depth_max, out_dtype, jitter=None):
         B = img.shape[0]
         return (_e(B, 3, h, w, like=img, dtype=out_dtype), _e(B, h, w, like=img, dtype=torch.int64),
                 _e(B, 1, h, w, like=img, dtype=f32), _e(B, 1, h, w, like=img, dtype=torch.uint8))

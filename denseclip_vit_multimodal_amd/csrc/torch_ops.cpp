@@ -586,7 +586,8 @@ Tensor upsample_silog_grad(const Tensor& pred, const Tensor& target, const c10::
 std::tuple<Tensor, Tensor, Tensor, Tensor> cityscapes_prepare(const Tensor& img, const Tensor& ids, const Tensor& disp,
                                                               const Tensor& crop, int64_t h, int64_t w,
                                                               at::ArrayRef<double> mean, at::ArrayRef<double> stdv,
-                                                              double bf, double depth_max, at::ScalarType out_dtype) {
+                                                              double bf, double depth_max, at::ScalarType out_dtype,
+                                                              const c10::optional<Tensor>& jitter) {
     check_gpu(img, "img"); check_gpu(ids, "ids"); check_gpu(disp, "disp"); check_gpu(crop, "crop");
     TORCH_CHECK(mean.size() == 3 && stdv.size() == 3, "cityscapes_prepare: 3 means / stds");
     TORCH_CHECK(img.dim() == 4 && img.size(3) == 3 && crop.scalar_type() == at::kInt, "cityscapes_prepare: shapes");
@@ -602,6 +603,26 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> cityscapes_prepare(const Tensor& img,
     Tensor mask = at::empty({B, 1, h, w}, like(img, at::kByte));
     const float m[3] = {(float)mean[0], (float)mean[1], (float)mean[2]};
     const float s[3] = {(float)stdv[0], (float)stdv[1], (float)stdv[2]};
+    const bool jit = jitter.has_value() && jitter->defined();
+    if (jit) {
+        // ColorJitter sits between the spatial transforms and Normalize: the crop as uint8 HWC, the
+        // jitter in place, then the normalisation
+        TORCH_CHECK(aug, "cityscapes_prepare: ColorJitter needs the (B, 7) scale / pad / crop parameters");
+        TORCH_CHECK(jitter->is_cuda() && jitter->scalar_type() == at::kDouble && jitter->dim() == 2 &&
+                        jitter->size(0) == B && jitter->size(1) == 8 && jitter->is_contiguous(),
+                    "cityscapes_prepare: jitter must be (B, 8) float64 on the GPU");
+        Tensor u8 = at::empty({B, h, w, 3}, like(img, at::kByte));
+        Tensor ws = at::empty({B}, like(img, at::kLong));
+        DCLIP_CALL(dclip_cityscapes_augment(ptr<uint8_t>(img), ptr<uint8_t>(ids), (const uint16_t*)disp.data_ptr(),
+                                            (int)B, (int)H, (int)W, ptr<int>(crop), (int)h, (int)w, m, s, (float)bf,
+                                            (float)depth_max, u8.data_ptr(), DCLIP_U8, ptr<int64_t>(seg),
+                                            ptr<float>(depth), ptr<uint8_t>(mask), stream_of(img)));
+        DCLIP_CALL(dclip_color_jitter(ptr<uint8_t>(u8), (int)B, (int)h, (int)w, (const double*)jitter->data_ptr(),
+                                      (unsigned long long*)ws.data_ptr(), stream_of(img)));
+        DCLIP_CALL(dclip_normalize_u8(ptr<uint8_t>(u8), (int)B, (int)h, (int)w, m, s, out_img.data_ptr(),
+                                      dt_code(out_dtype), stream_of(img)));
+        return {out_img, seg, depth, mask};
+    }
     auto fn = aug ? &dclip_cityscapes_augment : &dclip_cityscapes_prepare;
     DCLIP_CALL(fn(ptr<uint8_t>(img), ptr<uint8_t>(ids), (const uint16_t*)disp.data_ptr(), (int)B, (int)H, (int)W,
                   ptr<int>(crop), (int)h, (int)w, m, s, (float)bf, (float)depth_max, out_img.data_ptr(),
@@ -658,7 +679,8 @@ TORCH_LIBRARY(dclip, m) {
     m.def("upsample_silog_sums(Tensor pred, Tensor target, Tensor? mask, float eps) -> Tensor");
     m.def("upsample_silog_grad(Tensor pred, Tensor target, Tensor? mask, Tensor sums, float eps, float lambd) -> Tensor");
     m.def("cityscapes_prepare(Tensor img, Tensor ids, Tensor disp, Tensor crop, int h, int w, float[] mean, "
-          "float[] std, float bf, float depth_max, ScalarType out_dtype) -> (Tensor, Tensor, Tensor, Tensor)");
+          "float[] std, float bf, float depth_max, ScalarType out_dtype, Tensor? jitter=None) -> "
+          "(Tensor, Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(dclip, CUDA, m) {

@@ -16,8 +16,8 @@ trainer's spatial augmentation and the normalisation, writing the batch in the l
     installed here: that restatement is parity-unpinned against cv2 itself, see DESIGN.md);
   * `dclip_cityscapes_prepare` (crops from `random_crops`): crop + flip only (no rescale).
 
-Not reproduced: ColorJitter, which the reference enables only with `color_jitter: true` (off in
-the Cityscapes configs).
+  * ColorJitter (the reference's `color_jitter: true`, off in the Cityscapes configs): params from
+    `color_jitter_params`, `dclip_color_jitter` between the spatial transforms and Normalize.
 """
 import os
 import os.path as osp
@@ -122,13 +122,35 @@ def random_scale_crops(B, H, W, h, w, scale_range=(0.5, 2.0), rng=None, flip_p=0
     return torch.tensor(out, dtype=torch.int32)
 
 
+def color_jitter_params(B, rng=None, brightness=0.4, contrast=0.4, saturation=0.4, hue=0.1, p=0.8):
+    """ColorJitter(brightness, contrast, saturation, hue, p) parameters per image as albumentations
+    draws them (train_denseclip.py:152-155): with probability p, factors U(1 - b, 1 + b) (clipped at
+    0) for brightness / contrast / saturation, U(-hue, hue) for hue, and a random order of the four;
+    otherwise the identity (1, 1, 1, 0).  float64 (B, 8): factors, then the order (0 brightness,
+    1 contrast, 2 saturation, 3 hue).  rng: a `random.Random`."""
+    import random
+    r = rng if rng is not None else random
+    out = []
+    for _ in range(B):
+        if r.random() < p:
+            f = [r.uniform(max(0.0, 1 - brightness), 1 + brightness), r.uniform(max(0.0, 1 - contrast), 1 + contrast),
+                 r.uniform(max(0.0, 1 - saturation), 1 + saturation), r.uniform(-hue, hue)]
+            order = [0, 1, 2, 3]
+            r.shuffle(order)
+        else:
+            f, order = [1.0, 1.0, 1.0, 0.0], [0, 1, 2, 3]
+        out.append(f + [float(o) for o in order])
+    return torch.tensor(out, dtype=torch.float64)
+
+
 def prepare_batch(samples, crop_hw, crops, device, out_dtype=torch.bfloat16, mean=CLIP_MEAN, std=CLIP_STD,
-                  depth_max=80.0, bf=BASELINE_FOCAL_LENGTH):
+                  depth_max=80.0, bf=BASELINE_FOCAL_LENGTH, jitter=None):
     """samples: list of (img uint8 HxWx3, ids uint8 HxW, disp uint16 HxW) of one size;
     crops: int32 (B, 3) (y0, x0, flip) — a window of the image (`random_crops`) — or (B, 7)
     (Hs, Ws, pad_top, pad_left, y0, x0, flip) — the rescaled / padded pipeline
     (`random_scale_crops`).  Returns (img (B,3,h,w) out_dtype, seg int64 (B,h,w), depth f32
-    (B,1,h,w), mask bool (B,1,h,w)) on `device`, ready for train.train_step."""
+    (B,1,h,w), mask bool (B,1,h,w)) on `device`, ready for train.train_step.  jitter: (B, 8) from
+    `color_jitter_params` (needs the (B, 7) parameters) applies ColorJitter before Normalize."""
     if not samples:
         raise ValueError("empty batch")
     H, W = samples[0][1].shape
@@ -163,6 +185,10 @@ def prepare_batch(samples, crop_hw, crops, device, out_dtype=torch.bfloat16, mea
     disp = up([s[2].view(np.int16) for s in samples])  # the uint16 bits through an int16 tensor
     cr = crops.to(dev)
     from .ops import D
+    jt = None
+    if jitter is not None:
+        jt = torch.as_tensor(jitter, dtype=torch.float64).reshape(B, 8).to(dev)
     out_img, seg, depth, mask = D().cityscapes_prepare(img, ids, disp, cr, h, w, [float(v) for v in mean],
-                                                       [float(v) for v in std], float(bf), float(depth_max), out_dtype)
+                                                       [float(v) for v in std], float(bf), float(depth_max), out_dtype,
+                                                       jt)
     return out_img, seg, depth, mask.view(torch.bool)

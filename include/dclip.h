@@ -47,6 +47,7 @@ extern "C" {
 #define DCLIP_F32 0
 #define DCLIP_F16 1
 #define DCLIP_BF16 2
+#define DCLIP_U8 3    /* dclip_cityscapes_augment only: the uint8 HWC crop, before ColorJitter / Normalize */
 
 #define DCLIP_OK 0
 #define DCLIP_ERR_ARG (-1)
@@ -297,6 +298,20 @@ int dclip_cityscapes_augment(const uint8_t* img, const uint8_t* ids, const uint1
                              const int* params, int h, int w, const float* mean, const float* stdv, float bf,
                              float depth_max, void* out_img, int out_dt, int64_t* out_seg, float* out_depth,
                              uint8_t* out_mask, void* stream);
+
+/* ColorJitter (albumentations, train_denseclip.py:152-155; `color_jitter: true`) in place on a
+ * uint8 HWC batch img (B, h, w, 3) RGB: params (B, 8) f64 on the device = brightness, contrast,
+ * saturation, hue factors and the order of the four (0 brightness, 1 contrast, 2 saturation,
+ * 3 hue) per image; identity factors (1, 1, 1, 0) leave an image untouched.  uint8 arithmetic of
+ * albumentations' *_torchvision functions and OpenCV's 8-bit RGB<->GRAY / HSV conversions.
+ * ws: B uint64 (per-image gray sums for the contrast mean).                             */
+int dclip_color_jitter(uint8_t* img, int B, int h, int w, const double* params, unsigned long long* ws,
+                       void* stream);
+
+/* Normalize + ToTensorV2 of a uint8 HWC batch (B, h, w, 3): out (B, 3, h, w) out_dt =
+ * (x - 255 mean) * (1 / (255 std)) (mean, stdv: 3 host floats).                           */
+int dclip_normalize_u8(const uint8_t* img, int B, int h, int w, const float* mean, const float* stdv, void* out,
+                       int out_dt, void* stream);
 
 /* Element-wise dtype conversion of n elements: out = (out_dt)(in * scale), times *scale_ptr
  * when non-null (read on the device).  A power-of-two scale keeps fp16 gradients out of the

@@ -146,3 +146,92 @@ def prepare_augmented(samples, crop_hw, params, mean, std, bf=500.0, depth_max=8
         depths.append(dep[None])
         masks.append((dep > 0)[None])
     return np.stack(imgs), np.stack(segs), np.stack(depths), np.stack(masks)
+
+
+# ---------------------------------------------------------------------------- ColorJitter
+# albumentations ColorJitter on uint8 RGB (train_denseclip.py:152-155): the *_torchvision uint8
+# functions and OpenCV's 8-bit RGB2GRAY / RGB2HSV / HSV2RGB, restated from their published code
+# (neither is installed here: parity against them is UNPINNED; the GPU kernel is held to this).
+def _gray_u8(img):
+    x = img.astype(np.int64)
+    return (x[..., 0] * 4899 + x[..., 1] * 9617 + x[..., 2] * 1868 + 8192) >> 14
+
+
+def _rgb2hsv_u8(img):
+    x = img.astype(np.int64)
+    r, g, b = x[..., 0], x[..., 1], x[..., 2]
+    v = np.maximum(np.maximum(b, g), r)
+    vmin = np.minimum(np.minimum(b, g), r)
+    diff = v - vmin
+    i = np.arange(256, dtype=np.float64)
+    with np.errstate(divide="ignore"):
+        sdiv = np.where(i > 0, np.rint((255 << 12) / i), 0).astype(np.int64)
+        hdiv = np.where(i > 0, np.rint((180 << 12) / (6.0 * i)), 0).astype(np.int64)
+    s = (diff * sdiv[v] + (1 << 11)) >> 12
+    vr = np.where(v == r, -1, 0)
+    vg = np.where(v == g, -1, 0)
+    h = (vr & (g - b)) + (~vr & ((vg & (b - r + 2 * diff)) + ((~vg) & (r - g + 4 * diff))))
+    h = (h * hdiv[diff] + (1 << 11)) >> 12
+    h = np.where(h < 0, h + 180, h)
+    return np.minimum(h, 255), s, v
+
+
+def _hsv2rgb_u8(h, s, v):
+    f32 = np.float32
+    hf = h.astype(f32)
+    sf = s.astype(f32) * f32(1.0 / 255.0)
+    vf = v.astype(f32) * f32(1.0 / 255.0)
+    hh = hf * (f32(6.0) / f32(180.0))
+    hh = np.where(hh >= f32(6), hh - f32(6), hh)
+    sector = np.floor(hh).astype(np.int64)
+    hh = hh - sector.astype(f32)
+    bad = (sector < 0) | (sector >= 6)
+    sector = np.where(bad, 0, sector)
+    hh = np.where(bad, f32(0), hh)
+    one = f32(1)
+    tab = np.stack([vf, vf * (one - sf), vf * (one - sf * hh), vf * (one - sf * (one - hh))], -1)
+    sd = np.array([[1, 3, 0], [1, 0, 2], [3, 0, 1], [0, 2, 1], [0, 1, 3], [2, 1, 0]])
+    idx = sd[sector]                                    # (..., 3): b, g, r table slots
+    bgr = np.take_along_axis(tab, idx, -1)
+    gray = sf == 0
+    bgr = np.where(gray[..., None], vf[..., None], bgr)
+    rgb = bgr[..., ::-1] * f32(255)
+    return np.clip(np.rint(rgb), 0, 255).astype(np.uint8)
+
+
+def color_jitter(img, params):
+    """One image (h, w, 3) uint8 through the jitter ops in params' order (see
+    data.color_jitter_params)."""
+    img = img.copy()
+    fac, order = params[:4], [int(o) for o in params[4:]]
+    for op in order:
+        f = float(fac[op])
+        if (op == 3 and f == 0.0) or (op != 3 and f == 1.0):
+            continue
+        if op in (0, 1):
+            lut = np.arange(0, 256) * f
+            if op == 1:
+                lut = lut + _gray_u8(img).mean() * (1 - f)
+            img = np.clip(lut, 0, 255).astype(np.uint8)[img]
+        elif op == 2:
+            g = _gray_u8(img).astype(np.float32)[..., None]
+            t = img.astype(np.float32) * np.float32(f) + g * np.float32(1 - f) + np.float32(0)
+            img = np.clip(np.rint(t), 0, 255).astype(np.uint8)
+        else:
+            h, s, v = _rgb2hsv_u8(img)
+            lut = np.mod(np.arange(0, 256, dtype=np.int16) + 180 * f, 180).astype(np.uint8)
+            img = _hsv2rgb_u8(lut[h].astype(np.int64), s, v)
+    return img
+
+
+def prepare_augmented_jitter(samples, crop_hw, params, jitter, mean, std, bf=500.0, depth_max=80.0):
+    """prepare_augmented with ColorJitter on the uint8 crop before Normalize."""
+    h, w = crop_hw
+    imgs, segs, depths, masks = prepare_augmented(samples, crop_hw, params, (0.0, 0.0, 0.0), (1 / 255.0,) * 3, bf,
+                                                  depth_max)
+    out = []
+    for b in range(len(samples)):
+        # undo the identity normalisation above exactly: it wrote (x - 0) * (1 / (255 / 255)) = x
+        u8 = np.rint(imgs[b].transpose(1, 2, 0)).astype(np.uint8)
+        out.append(normalize(color_jitter(u8, jitter[b]), mean, std).transpose(2, 0, 1))
+    return np.stack(out), segs, depths, masks

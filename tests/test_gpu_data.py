@@ -115,3 +115,33 @@ def test_augment_full_resolution_batch():
                                          (0.26862954, 0.26130258, 0.27577711))
     assert torch.equal(seg[:1].cpu(), torch.from_numpy(rs))
     assert torch.equal(img[:1].float().cpu(), torch.from_numpy(np.ascontiguousarray(ri)).to(torch.bfloat16).float())
+
+
+def test_color_jitter_matches_oracle():
+    """ColorJitter (brightness / contrast / saturation / hue in a random order per image, the
+    identity for a not-applied image) on the GPU bit-exact against the oracle's restatement of
+    albumentations' uint8 functions and OpenCV's 8-bit colour conversions (cv2 itself absent:
+    parity against it unpinned), inside the full augmented batch preparation."""
+    import random
+    from denseclip_vit_multimodal_amd.data import (prepare_batch, random_scale_crops, color_jitter_params,
+                                                   CLIP_MEAN, CLIP_STD)
+    B, H, W, h, w = 6, 64, 160, 48, 96
+    samples = _samples(B, H, W, seed=9)
+    # saturated colours, greys and black / white pixels beside the random ones
+    for s_ in samples:
+        s_[0][:4, :4] = [[255, 0, 0], [0, 255, 0], [0, 0, 255], [128, 128, 128]]
+        s_[0][4:8, :4] = [[0, 0, 0], [255, 255, 255], [255, 255, 0], [1, 2, 3]]
+    p = random_scale_crops(B, H, W, h, w, rng=random.Random(2))
+    p[0] = torch.tensor([H, W, 0, 0, 0, 0, 0], dtype=torch.int32)
+    jit = color_jitter_params(B, rng=random.Random(3), p=1.0)
+    jit[1] = torch.tensor([1.0, 1.0, 1.0, 0.0, 0, 1, 2, 3], dtype=torch.float64)      # not applied
+    jit[2] = torch.tensor([1.37, 0.61, 1.39, -0.099, 3, 2, 1, 0], dtype=torch.float64)
+    for out_dtype in (torch.float32, torch.bfloat16):
+        img, seg, depth, mask = prepare_batch(samples, (h, w), p, "cuda", out_dtype=out_dtype, jitter=jit)
+        ri, rs, rd, rm = D.prepare_augmented_jitter(samples, (h, w), p.tolist(), jit.tolist(), CLIP_MEAN, CLIP_STD)
+        assert torch.equal(img.cpu(), torch.from_numpy(np.ascontiguousarray(ri)).to(out_dtype))
+        assert torch.equal(seg.cpu(), torch.from_numpy(rs))
+    # the not-applied image equals the jitter-free pipeline
+    i0, *_ = prepare_batch(samples, (h, w), p, "cuda", out_dtype=torch.float32)
+    assert torch.equal(img.float()[1], i0.to(img.dtype).float()[1])
+    assert not torch.equal(img[2], i0.to(img.dtype)[2])
