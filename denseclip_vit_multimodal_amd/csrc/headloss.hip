@@ -209,13 +209,166 @@ __global__ __launch_bounds__(NTH) void band_loss_kernel(const TL* __restrict__ l
     }
 }
 
+// Cross-entropy with the gradient folded per LOW-RES column: thread (jj, xs) of the 32 x 8 grid owns
+// every 8th high-res column x whose left interpolation column is j0 = jc + jj, runs all the band's
+// rows for it, and keeps the four folded sums (left / right column x upper / lower row) of its
+// columns in registers; only those go to LDS (8 threads per column instead of one atomic set per
+// high-res column: the per-column LDS atomics of band_loss_kernel, 16-way on the same addresses,
+// were its cost).  Same arithmetic per pixel as band_loss_kernel MODE 0.
+template <typename TL, int K>
+__global__ __launch_bounds__(NTH) void band_ce_kernel(const TL* __restrict__ low, int h, int w, int H, int W,
+                                                      int chunks, const void* __restrict__ lab, int lab_dt,
+                                                      int ignore, double* __restrict__ sums,
+                                                      unsigned* __restrict__ count, float* __restrict__ grad) {
+    static_assert(NTH == JW * 8, "32 low-res columns x 8 column slices");
+    __shared__ float low_s[2][JW + 1][K];
+    __shared__ float acc_s[2][JW + 1][K];
+    __shared__ double red_s[NTH / 64][2];
+    const int tid = threadIdx.x;
+    const int ch = blockIdx.x % chunks;
+    const int i = (blockIdx.x / chunks) % h;
+    const int b = blockIdx.x / (chunks * h);
+    const int jc = ch * JW;
+    const int i1 = i + (i < h - 1 ? 1 : 0);
+    const int ncol = (jc + JW + 1 <= w ? JW + 1 : w - jc);
+    for (int e = tid; e < 2 * (JW + 1) * K; e += NTH) {
+        const int r = e / ((JW + 1) * K), jj = (e / K) % (JW + 1), k = e % K;
+        const int row = r ? i1 : i;
+        low_s[r][jj][k] = jj < ncol ? ld(low + (((int64_t)b * K + k) * h + row) * w + jc + jj) : 0.f;
+        acc_s[r][jj][k] = 0.f;
+    }
+    __syncthreads();
+    const int jj = tid >> 3, xs = tid & 7;
+    const int j0 = jc + jj;
+    int ylo, yhi, xlo, xhi;
+    band_range(i, h, H, &ylo, &yhi);
+    double lsum = 0.0;
+    unsigned lcnt = 0;
+    float g[4][K];  // folded gradient: [left / right column][upper / lower row] as 0: l-u, 1: r-u, 2: l-b, 3: r-b
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int k = 0; k < K; ++k) g[q][k] = 0.f;
+    if (j0 < w) {
+        band_range(j0, w, W, &xlo, &xhi);
+        for (int x = xlo + xs; x <= xhi; x += 8) {
+            const Lerp X = lerp_index(x, w, W);
+            if (X.i0 != j0) continue;
+            const int j1 = X.i1 - jc;
+            float ut[K], ub[K], at[K], ab[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                ut[k] = X.l0 * low_s[0][jj][k] + X.l1 * low_s[0][j1][k];
+                ub[k] = X.l0 * low_s[1][jj][k] + X.l1 * low_s[1][j1][k];
+                at[k] = 0.f;
+                ab[k] = 0.f;
+            }
+            // the column's labels 8 rows at a time, all loads in flight together (one dependent
+            // global load per pixel left this kernel latency-bound)
+            for (int y0 = ylo; y0 <= yhi; y0 += 8) {
+            int tl[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int y = y0 + u;
+                tl[u] = y <= yhi ? load_label(lab, lab_dt, ((int64_t)b * H + y) * W + x) : ignore;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int y = y0 + u;
+                if (y > yhi) continue;
+                const Lerp Y = lerp_index(y, h, H);
+                if (Y.i0 != i) continue;
+                const int t = tl[u];
+                if (t == ignore || t < 0 || t >= K) continue;
+                float v[K];
+#pragma unroll
+                for (int k = 0; k < K; ++k) v[k] = Y.l0 * ut[k] + Y.l1 * ub[k];
+                float m = v[0], vt = 0.f;
+#pragma unroll
+                for (int k = 1; k < K; ++k) m = fmaxf(m, v[k]);
+#pragma unroll
+                for (int k = 0; k < K; ++k) vt = k == t ? v[k] : vt;
+                float s = 0.f;
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    v[k] = __expf(v[k] - m);
+                    s += v[k];
+                }
+                lsum += (double)(__logf(s) - (vt - m));  // -log softmax[t]
+                ++lcnt;
+                const float inv = 1.0f / s;
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const float d = v[k] * inv - (k == t ? 1.f : 0.f);
+                    at[k] += Y.l0 * d;
+                    ab[k] += Y.l1 * d;
+                }
+            }
+            }
+            if (j1 == jj) {  // clamped right edge: both weights on one column
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    g[0][k] += at[k];
+                    g[2][k] += ab[k];
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    g[0][k] += X.l0 * at[k];
+                    g[1][k] += X.l1 * at[k];
+                    g[2][k] += X.l0 * ab[k];
+                    g[3][k] += X.l1 * ab[k];
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (g[0][k] != 0.f) atomicAdd(&acc_s[0][jj][k], g[0][k]);
+            if (g[1][k] != 0.f) atomicAdd(&acc_s[0][jj + 1][k], g[1][k]);
+            if (g[2][k] != 0.f) atomicAdd(&acc_s[1][jj][k], g[2][k]);
+            if (g[3][k] != 0.f) atomicAdd(&acc_s[1][jj + 1][k], g[3][k]);
+        }
+    }
+    double a = lsum, c = (double)lcnt;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        a += __shfl_xor(a, o, 64);
+        c += __shfl_xor(c, o, 64);
+    }
+    if ((tid & 63) == 0) {
+        red_s[tid >> 6][0] = a;
+        red_s[tid >> 6][1] = c;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double sa = 0.0, sc = 0.0;
+        for (int wv = 0; wv < NTH / 64; ++wv) {
+            sa += red_s[wv][0];
+            sc += red_s[wv][1];
+        }
+        atomicAdd(sums, sa);
+        atomicAdd(count, (unsigned)sc);
+    }
+    for (int e = tid; e < 2 * (JW + 1) * K; e += NTH) {
+        const int r = e / ((JW + 1) * K), jx = (e / K) % (JW + 1), k = e % K;
+        if (jx >= ncol || (r == 1 && i1 == i)) continue;
+        const float v = acc_s[r][jx][k] + (r == 0 && i1 == i ? acc_s[1][jx][k] : 0.f);
+        if (v != 0.f) atomicAdd(grad + (((int64_t)b * K + k) * h + (r ? i1 : i)) * w + jc + jx, v);
+    }
+}
+
 template <typename TL, int K, int MODE>
 void launch_band(const void* low, int B, int h, int w, int H, int W, const void* lab, int lab_dt, int ignore,
                  const float* gt, const uint8_t* mask, float eps, float lambd, double* sums, unsigned* count,
                  float* grad, hipStream_t st) {
     const int chunks = (w + JW - 1) / JW;
-    band_loss_kernel<TL, K, MODE><<<B * h * chunks, NTH, 0, st>>>((const TL*)low, h, w, H, W, chunks, lab, lab_dt,
-                                                                  ignore, gt, mask, eps, lambd, sums, count, grad);
+    if constexpr (MODE == 0)
+        band_ce_kernel<TL, K><<<B * h * chunks, NTH, 0, st>>>((const TL*)low, h, w, H, W, chunks, lab, lab_dt, ignore,
+                                                              sums, count, grad);
+    else
+        band_loss_kernel<TL, K, MODE><<<B * h * chunks, NTH, 0, st>>>((const TL*)low, h, w, H, W, chunks, lab,
+                                                                      lab_dt, ignore, gt, mask, eps, lambd, sums,
+                                                                      count, grad);
 }
 
 }  // namespace
