@@ -388,6 +388,37 @@ __device__ __forceinline__ void stage_rows(const T* __restrict__ X, int64_t ldx,
     }
 }
 
+// stage_rows as buffer loads: per-lane byte offsets of this thread's pieces (rows row0.., clamped
+// to rows - 1, swizzled chunk) computed once per tile by rows_voff, plus the K-step's byte offset:
+// one add per load instead of the ~11 address instructions (3 of them 64-bit multiplies) of
+// stage_rows, which sat between every K-step's barrier and its first MFMA
+template <typename T, int ROWS_INST, int BKT>
+__device__ __forceinline__ void rows_voff(int64_t ldx, int row0, int rows, int wave, int lane,
+                                          uint32_t (&voff)[ROWS_INST]) {
+    constexpr int CPR = BKT / 8;
+#pragma unroll
+    for (int i = 0; i < ROWS_INST; ++i) {
+        const int inst = wave * ROWS_INST + i;
+        const int r = inst * (64 / CPR) + lane / CPR;
+        const int c = (lane % CPR) ^ big_sw<BKT>(r);
+        int gr = row0 + r;
+        gr = gr < rows ? gr : rows - 1;
+        voff[i] = (uint32_t)((gr * ldx + c * 8) * (int64_t)sizeof(T));
+    }
+}
+
+template <typename T, int ROWS_INST>
+__device__ __forceinline__ void stage_rows_buf(const T* X, uint32_t bytes, const uint32_t (&voff)[ROWS_INST],
+                                               uint32_t kbyte, char* lds, int wave) {
+#if defined(__HIP_DEVICE_COMPILE__)  // the buffer-resource type exists only for the device target
+    const rsrc_t rs = make_rsrc(X, bytes);
+#pragma unroll
+    for (int i = 0; i < ROWS_INST; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(lds + (wave * ROWS_INST + i) * 1024), 16, voff[i] + kbyte,
+                                                 0, 0, 0);
+#endif
+}
+
 template <typename T, int BKT>
 __device__ __forceinline__ typename Mfma<T>::frag big_frag(const char* img, int r, int chunk) {
     return *(const typename Mfma<T>::frag*)(img + r * (2 * BKT) + ((chunk ^ big_sw<BKT>(r)) << 4));
@@ -620,15 +651,21 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pers_kernel(
     const int nk = K / 64;
     const int M = tiles_m * 256, N = tiles_n * 256;
 
-    auto stage = [&](int m0, int n0, int kt, int slot) {
-        char* base = smem + slot * Cfg::STAGE_BYTES;
-        stage_rows<T, Cfg::A_INST, 64>(A, lda, m0, M, kt * 64, base, wave, lane);
-        stage_rows<T, Cfg::B_INST, 64>(B, ldb, n0, N, kt * 64, base + Cfg::A_BYTES, wave, lane);
-    };
+    // buffer-load staging (stage_rows_buf): offsets per tile, one add per load per K-step
+    const uint32_t abytes = (uint32_t)((int64_t)M * lda * sizeof(T)), bbytes = (uint32_t)((int64_t)N * ldb * sizeof(T));
+    uint32_t va[Cfg::A_INST], vb[Cfg::B_INST], van[Cfg::A_INST], vbn[Cfg::B_INST];
+#define PERS_STAGE(VA, VB, KT, SLOT)                                                                                 \
+    do {                                                                                                             \
+        char* base_ = smem + (SLOT) * Cfg::STAGE_BYTES;                                                              \
+        stage_rows_buf<T, Cfg::A_INST>(A, abytes, VA, (uint32_t)((KT) * 64 * sizeof(T)), base_, wave);               \
+        stage_rows_buf<T, Cfg::B_INST>(B, bbytes, VB, (uint32_t)((KT) * 64 * sizeof(T)), base_ + Cfg::A_BYTES, wave); \
+    } while (0)
     int u = r;
     if (u >= ntiles) return;
     int m0 = (u / tiles_n) * 256, n0 = (u % tiles_n) * 256;
-    stage(m0, n0, 0, 0);
+    rows_voff<T, Cfg::A_INST, 64>(lda, m0, M, wave, lane, va);
+    rows_voff<T, Cfg::B_INST, 64>(ldb, n0, N, wave, lane, vb);
+    PERS_STAGE(va, vb, 0, 0);
     int slot = 0;
     bool first = true;
     while (true) {
@@ -639,15 +676,19 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pers_kernel(
             for (int j = 0; j < Cfg::MB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         const int un = u + G;
         const int nm0 = (un / tiles_n) * 256, nn0 = (un % tiles_n) * 256;
+        if (un < ntiles) {  // the next tile's offsets (its first K-step is staged by this tile's last)
+            rows_voff<T, Cfg::A_INST, 64>(lda, nm0, M, wave, lane, van);
+            rows_voff<T, Cfg::B_INST, 64>(ldb, nn0, N, wave, lane, vbn);
+        }
         for (int kt = 0; kt < nk; ++kt) {
             if (kt == 0 && !first) wait_vmcnt<PERS_EPI_MIN>();  // this K-step's loads, not the epilogue's stores
             else wait_vmcnt<0>();
             __builtin_amdgcn_s_barrier();  // K-step kt visible to every wave; the other slot free
             __builtin_amdgcn_sched_barrier(0);
             if (kt + 1 < nk) {
-                stage(m0, n0, kt + 1, slot ^ 1);
+                PERS_STAGE(va, vb, kt + 1, slot ^ 1);
             } else if (un < ntiles) {
-                stage(nm0, nn0, 0, slot ^ 1);
+                PERS_STAGE(van, vbn, 0, slot ^ 1);
             }
             const char* At = smem + slot * Cfg::STAGE_BYTES;
             const char* Bt = At + Cfg::A_BYTES;
@@ -722,8 +763,13 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pers_kernel(
         u = un;
         m0 = nm0;
         n0 = nn0;
+#pragma unroll
+        for (int i = 0; i < Cfg::A_INST; ++i) va[i] = van[i];
+#pragma unroll
+        for (int i = 0; i < Cfg::B_INST; ++i) vb[i] = vbn[i];
         first = false;
     }
+#undef PERS_STAGE
 }
 
 // ---------------------------------------------------------------------------- "TN"
@@ -1421,6 +1467,8 @@ bool launch_pers(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t
         const int64_t Mfull = (M / 256) * 256, tail = M - Mfull;
         const int G = cu_count();
         if (N % 256 != 0 || tail > 64 || (Mfull / 256) * (N / 256) < 2 * G) return false;
+        // buffer-load staging addresses each operand with 32-bit byte offsets
+        if (Mfull * lda * (int64_t)sizeof(T) >= (1ll << 32) || N * ldb * (int64_t)sizeof(T) >= (1ll << 32)) return false;
         if (EPI == DCLIP_EPI_STORE_SCALED || (bias != nullptr && EPI != DCLIP_EPI_GELU_BWD)) {
             // 16-byte per-column vector loads
             if (((uintptr_t)(EPI == DCLIP_EPI_STORE_SCALED ? aux : bias) % 16) != 0) return false;
