@@ -1192,12 +1192,38 @@ __device__ __forceinline__ void stage_conv_rows(const T* __restrict__ X, const T
     }
 }
 
+// stage_conv_rows as buffer loads from X (xbytes bytes from X): a pixel row's byte offset per lane
+// (R.base), the tap's shift added per K-step; an out-of-image tap gets an offset past the buffer,
+// which reads 0 (no zero row, no 64-bit address arithmetic per load)
+template <typename T, int ROWS_INST, int BKT>
+__device__ __forceinline__ void stage_conv_rows_buf(const T* X, uint32_t xbytes, const ConvRows<ROWS_INST, BKT>& R,
+                                                    const PixGeo g, int Cin, int dir, int k0, char* lds, int wave,
+                                                    int lane) {
+#if defined(__HIP_DEVICE_COMPILE__)  // the buffer-resource type exists only for the device target
+    constexpr int CPR = BKT / 8;
+    const rsrc_t rs = make_rsrc(X, xbytes);
+    const int tap = k0 / Cin, ci = k0 - tap * Cin;  // wave-uniform
+    const int dy = (tap / 3 - 1) * dir, dx = (tap % 3 - 1) * dir;
+    const int shift = (int)((((int64_t)dy * g.W + dx) * g.ld + ci) * (int64_t)sizeof(T));
+#pragma unroll
+    for (int i = 0; i < ROWS_INST; ++i) {
+        const int inst = wave * ROWS_INST + i;
+        const int r = inst * (64 / CPR) + lane / CPR;
+        const int c = (lane % CPR) ^ big_sw<BKT>(r);
+        const int yy = R.y[i] + dy, xx = R.x[i] + dx;
+        const bool ok = yy >= 0 && yy < g.H && xx >= 0 && xx < g.W;
+        const uint32_t voff = ok ? (uint32_t)((int64_t)R.base[i] * (int64_t)sizeof(T) + shift + c * 16) : 0xFFFFFFF0u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(lds + inst * 1024), 16, voff, 0, 0, 0);
+    }
+#endif
+}
+
 // out (row-mapped, see big_epilogue) = implicit-GEMM conv; B: weights [Nout][9 * Cin] in (tap, ci) order
 template <typename T, int EPI, typename OutT, int BM, int BN, int WM, int WN, int STAGES>
 __global__ __launch_bounds__(64 * WM * WN, 1) void conv_nt_kernel(
     const T* __restrict__ X, const T* __restrict__ zero, PixGeo g, int Cin, int dir, const T* __restrict__ Bw,
     int64_t ldb, int M, int N, int tiles_m, int tiles_n, const void* __restrict__ aux, int64_t ld_aux,
-    void* __restrict__ C, int64_t ldc, int map_hw, int map_gap, int map_off) {
+    void* __restrict__ C, int64_t ldc, int map_hw, int map_gap, int map_off, uint32_t xbytes) {
     constexpr int BKT = 64;
     typedef BigCfg<BM, BN, WM, WN, STAGES, BKT> Cfg;
     typedef typename Mfma<T>::frag frag;
@@ -1220,10 +1246,15 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_nt_kernel(
 #pragma unroll
         for (int j = 0; j < Cfg::MB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    // buffer-load staging when the input fits 32-bit byte offsets (xbytes > 0); weights always
+    uint32_t vb[Cfg::B_INST];
+    rows_voff<T, Cfg::B_INST, BKT>(ldb, n0, N, wave, lane, vb);
+    const uint32_t bbytes = (uint32_t)((int64_t)N * ldb * sizeof(T));
     auto stage = [&](int kt, int slot) {
         char* base = smem + slot * Cfg::STAGE_BYTES;
-        stage_conv_rows<T, Cfg::A_INST, BKT>(X, zero, R, g, Cin, dir, kt * BKT, base, wave, lane);
-        stage_rows<T, Cfg::B_INST, BKT>(Bw, ldb, n0, N, kt * BKT, base + Cfg::A_BYTES, wave, lane);
+        if (xbytes) stage_conv_rows_buf<T, Cfg::A_INST, BKT>(X, xbytes, R, g, Cin, dir, kt * BKT, base, wave, lane);
+        else stage_conv_rows<T, Cfg::A_INST, BKT>(X, zero, R, g, Cin, dir, kt * BKT, base, wave, lane);
+        stage_rows_buf<T, Cfg::B_INST>(Bw, bbytes, vb, (uint32_t)(kt * BKT * sizeof(T)), base + Cfg::A_BYTES, wave);
     };
 #pragma unroll
     for (int s = 0; s < STAGES - 1; ++s)
@@ -1766,10 +1797,14 @@ extern "C" int dclip_conv3x3(int mode, int ab_dt, const void* X, int64_t x_bstri
     constexpr int TBM = 256, TBN = 128;
     const int tiles_m = (M + TBM - 1) / TBM, tiles_n = (Nout + TBN - 1) / TBN;
     const int map_hw = out_gap ? H * W : 0;
+    // the input's extent in bytes for the buffer-load staging (0: too large for 32-bit offsets ->
+    // pointer staging with the zero row)
+    const int64_t xext = ((int64_t)(B - 1) * x_bstride + x_off + (int64_t)H * W * x_ld) * 2;
+    const uint32_t xbytes = xext < (1ll << 32) - 4096 ? (uint32_t)xext : 0u;
 #define CONV_LAUNCH(T, EPI, OUTT)                                                                                    \
     conv_nt_kernel<T, EPI, OUTT, TBM, TBN, 4, 2, 3><<<tiles_m * tiles_n, 512, 0, st>>>(                             \
         (const T*)X, (const T*)zero, g, Cin, dir, (const T*)Wt, 9 * (int64_t)Cin, M, Nout, tiles_m, tiles_n, out,    \
-        out_ld, out, out_ld, map_hw, out_gap, out_off)
+        out_ld, out, out_ld, map_hw, out_gap, out_off, xbytes)
     if (ab_dt == DCLIP_BF16) {
         if (accumulate) CONV_LAUNCH(bf16, DCLIP_EPI_RESIDUAL, float);
         else if (out_dt == DCLIP_F32) CONV_LAUNCH(bf16, DCLIP_EPI_STORE, float);
