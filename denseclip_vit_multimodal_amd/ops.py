@@ -776,7 +776,9 @@ class Conv3x3Fn(torch.autograd.Function):
             if in_place and in_strides[0] == bs:
                 # same layout as the input view: batches of bs elements, pixel rows after a gap
                 gap_rows = (bs - H * W * ld) // ld
-                buf = torch.zeros(B * bs, dtype=cdt, device=dy.device)
+                # the gap (CLS) rows stay unwritten: every reader of this token-layout gradient skips
+                # or overwrites them (dclip_add_readout_cast, BlockFn / ReadoutFn's CLS masking)
+                buf = torch.empty(B * bs, dtype=cdt, device=dy.device)
                 D().conv3x3(1, dyr, H * W * cp, 0, cp, B, H, W, cp, w_t, Cin, buf, ld, gap_rows, gap_rows, 0)
                 dx = buf.as_strided((B, Cin, H, W), (bs, 1, W * ld, ld), gap_rows * ld)
             else:
@@ -888,7 +890,7 @@ class NeckLevelsFn(torch.autograd.Function):
                 w_t = _conv3x3_dgrad_rows(convw[l], cdt)
                 if in_place[l] and in_strides[l][0] == bs:
                     gap_rows = (bs - H * W * ld) // ld
-                    buf = torch.zeros(B * bs, dtype=cdt, device=d.device)
+                    buf = torch.empty(B * bs, dtype=cdt, device=d.device)  # CLS rows unread (see Conv3x3Fn)
                     D().conv3x3(1, dpre[:, l * Ci:], H * W * LC, 0, LC, B, H, W, Ci, w_t, Cin, buf, ld, gap_rows,
                                 gap_rows, 0)
                     dm = buf.as_strided((B, Cin, H, W), (bs, 1, W * ld, ld), gap_rows * ld)
