@@ -70,6 +70,22 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
+// c + the sum of an 8-element fragment (four v_dot2c_f32 against packed ones)
+__device__ __forceinline__ float frag_sum8(bf16x8 v, float c) {
+    typedef bf16 b2 __attribute__((ext_vector_type(2)));
+    const b2 one = {(bf16)1.f, (bf16)1.f};
+#pragma unroll
+    for (int p = 0; p < 4; ++p) c = __builtin_amdgcn_fdot2_f32_bf16(b2{v[2 * p], v[2 * p + 1]}, one, c, false);
+    return c;
+}
+__device__ __forceinline__ float frag_sum8(f16x8 v, float c) {
+    typedef f16 h2 __attribute__((ext_vector_type(2)));
+    const h2 one = {(f16)1.f, (f16)1.f};
+#pragma unroll
+    for (int p = 0; p < 4; ++p) c = __builtin_amdgcn_fdot2(h2{v[2 * p], v[2 * p + 1]}, one, c, false);
+    return c;
+}
+
 // ----------------------------------------------------------------------------- MFMA
 template <typename T> struct Mfma;
 template <> struct Mfma<bf16> {

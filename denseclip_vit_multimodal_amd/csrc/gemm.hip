@@ -946,12 +946,16 @@ __device__ __forceinline__ void tn_stage_buf(const void* A, uint32_t abytes, con
 #endif
 }
 
-template <typename T, int EPI, int BKT = 64, int STAGES = 2>
+// CS: also accumulate the column sums of A over the K range (alpha * sum_k A[k][m] into colsum,
+// the bias gradient when A is dY): the tiles in column 0 of the tile grid own them, and of their
+// waves the ones with wn == 0 (the other three hold the same A fragments) add their fragments
+// with v_dot2c beside the MFMAs -- no separate pass re-reading A from HBM.
+template <typename T, int EPI, int BKT = 64, int STAGES = 2, bool CS = false>
 __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(const T* __restrict__ A, int64_t lda,
                                                              const T* __restrict__ B, int64_t ldb, int M, int N,
                                                              int Kreal, int k_chunk, int tiles_m, int tiles_n,
                                                              void* __restrict__ C, int64_t ldc, int64_t slab,
-                                                             Alpha alpha_arg) {
+                                                             Alpha alpha_arg, float* __restrict__ colsum) {
     const float alpha = alpha_arg.get();
     typedef BigCfg<256, 256, 2, 4, 2> Cfg;
     typedef typename Mfma<T>::frag frag;
@@ -959,7 +963,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(const T* __restrict
     constexpr int G = 2 * (BKT / 16);     // LDS-DMA instructions per thread per K-step
     __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE > Cfg::EP_BYTES ? STAGES * STAGE : Cfg::EP_BYTES];
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wm = wave / 4, wn = wave % 4;
     const int lq = lane >> 4;
 
@@ -983,6 +987,10 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(const T* __restrict
     for (int i = 0; i < Cfg::NB; ++i)
 #pragma unroll
         for (int j = 0; j < Cfg::MB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bool do_cs = CS && t % tiles_n == 0 && wn == 0;  // wave-uniform
+    float cs[Cfg::MB];
+#pragma unroll
+    for (int j = 0; j < Cfg::MB; ++j) cs[j] = 0.f;
 
     // LDS-DMA sources as buffer loads: a per-lane byte offset of each of this thread's pieces,
     // fixed for the launch, plus the K-step's row offset (one add per piece; the address
@@ -1034,6 +1042,9 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(const T* __restrict
                     _Pragma("unroll") for (int e = 0; e < 8; ++e)                                                   \
                         if (k0 + ks * 32 + 8 * lq + e >= Kreal) fa[j][e] = (T)0.f;                                  \
             }                                                                                                       \
+            if (CS && do_cs) {                                                                                      \
+                _Pragma("unroll") for (int j = 0; j < Cfg::MB; ++j) cs[j] = frag_sum8(fa[j], cs[j]);               \
+            }                                                                                                       \
             _Pragma("unroll") for (int j = 0; j < Cfg::MB; ++j)                                                     \
                 _Pragma("unroll") for (int i = 0; i < Cfg::NB; ++i) acc[i][j] = Mfma16<T>::mma(fb[i], fa[j], acc[i][j]); \
         }                                                                                                           \
@@ -1045,6 +1056,16 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(const T* __restrict
     if (last_ragged) TN_KSTEP(nk - 1, true);
 #undef TN_KSTEP
 #undef TN_STAGE
+    if (CS && do_cs) {  // fragment lane l: column (l & 15), tokens 8 (l >> 4) .. +7 of each 32-row step
+#pragma unroll
+        for (int j = 0; j < Cfg::MB; ++j) {
+            float v = cs[j];
+            v += __shfl_xor(v, 16, 64);
+            v += __shfl_xor(v, 32, 64);
+            const int col = m0 + wm * Cfg::WTM + j * 16 + (lane & 15);
+            if (lq == 0 && col < M) atomicAdd(colsum + col, v * alpha);  // columns past M: clamped copies
+        }
+    }
     // the split's slab (blockIdx.y is 0 on this grid, so the epilogue's own slab offset vanishes)
     float* Cs = (float*)C + (EPI == DCLIP_EPI_SPLITK ? (int64_t)split * slab : 0);
     big_epilogue<T, EPI, float, Cfg>(acc, smem, M, N, m0 + wm * Cfg::WTM, n0 + wn * Cfg::WTN, nullptr, nullptr, 0,
@@ -1721,7 +1742,11 @@ extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda
     const int tiles_m = (int)((M + BM - 1) / BM), tiles_n = (int)((N + BN - 1) / BN);
     const int k_chunk = (int)(K_pad / splits);
     dim3 grid(tiles_m * tiles_n, splits);
-    if (colsum_a) {
+    const int tn_opt = dclip_option(DCLIP_OPT_GEMM_TN_TILE);
+    const bool big = tn_opt != 1 && M >= 256 && N >= 256;
+    // the big kernel sums A's columns itself (DCLIP_OPT_GEMM_TN_COLSUM 1: the separate pass)
+    const bool fused_cs = colsum_a && big && dclip_option(DCLIP_OPT_GEMM_TN_COLSUM) != 1;
+    if (colsum_a && !fused_cs) {
         const int64_t rpb = 2048;
         dim3 cg((unsigned)((M + 63) / 64), (unsigned)((K + rpb - 1) / rpb));
         if (ab_dt == DCLIP_BF16) colsum_kernel<bf16><<<cg, 256, 0, st>>>((const bf16*)A, lda, K, (int)M, rpb, alpha, colsum_a);
@@ -1731,17 +1756,16 @@ extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda
     gemm_tn_kernel<T, EPI, float><<<grid, 256, 0, st>>>((const T*)A, lda, (const T*)B, ldb, (int)M, (int)N,   \
                                                         (int)K, k_chunk, tiles_m, tiles_n, nullptr, OUT,        \
                                                         EPI == DCLIP_EPI_SPLITK ? N : ldc, (int64_t)M * N, alpha)
-    const int tn_opt = dclip_option(DCLIP_OPT_GEMM_TN_TILE);
-    const bool big = tn_opt != 1 && M >= 256 && N >= 256;
-#define TN_BIG_V(T, EPI, OUT, BKT, STG)                                                                        \
-    gemm_tn_big_kernel<T, EPI, BKT, STG><<<dim3(tm2 * tn2 * splits), 512, 0, st>>>(                            \
+#define TN_BIG_V(T, EPI, OUT, BKT, STG, CS)                                                                    \
+    gemm_tn_big_kernel<T, EPI, BKT, STG, CS><<<dim3(tm2 * tn2 * splits), 512, 0, st>>>(                        \
         (const T*)A, lda, (const T*)B, ldb, (int)M, (int)N, (int)K, k_chunk, tm2, tn2, OUT,                     \
-        EPI == DCLIP_EPI_SPLITK ? N : ldc, (int64_t)M * N, alpha)
+        EPI == DCLIP_EPI_SPLITK ? N : ldc, (int64_t)M * N, alpha, colsum_a)
 #define TN_BIG(T, EPI, OUT)                                                                                    \
     do {                                                                                                       \
-        if (tn_opt == 2) TN_BIG_V(T, EPI, OUT, 32, 4);                                                         \
-        else if (tn_opt == 3) TN_BIG_V(T, EPI, OUT, 32, 5);                                                    \
-        else TN_BIG_V(T, EPI, OUT, 64, 2);                                                                     \
+        if (tn_opt == 2) TN_BIG_V(T, EPI, OUT, 32, 4, false);                                                  \
+        else if (tn_opt == 3) TN_BIG_V(T, EPI, OUT, 32, 5, false);                                             \
+        else if (fused_cs) TN_BIG_V(T, EPI, OUT, 64, 2, true);                                                 \
+        else TN_BIG_V(T, EPI, OUT, 64, 2, false);                                                              \
     } while (0)
     const int tm2 = (int)((M + 255) / 256), tn2 = (int)((N + 255) / 256);
     if (epilogue == DCLIP_EPI_STORE) {

@@ -79,7 +79,8 @@ int dclip_abi_version(void);
 #define DCLIP_OPT_ATTN_BWD_KERNEL 7  /* 0 (default): CLS-split passes when N-1 is a multiple of 256; 1: generic */
 #define DCLIP_OPT_ATTN_FWD_KERNEL 6  /* 0 (default): CLS-split kernel when N-1 is a multiple of the query block; 1: generic */
 #define DCLIP_OPT_ATTN_BWD_BLOCK 8   /* 0 (default): software-pipelined CLS-split dK/dV pass; 1: the unpipelined one */
-#define DCLIP_OPT_COUNT 9
+#define DCLIP_OPT_GEMM_TN_COLSUM 9   /* 0 (default): the 256x256 weight-gradient kernel sums dY's columns (bias gradient) itself; 1: a separate pass */
+#define DCLIP_OPT_COUNT 10
 int dclip_set_option(int id, int value);
 
 /* LayerNorm over the last dim (cols), eps, affine w/b (fp32).  y = (x-mu)*rstd*w+b.

@@ -208,6 +208,27 @@ def test_weight_grad_splitk(M, N, K, tn_tile):
     assert rel_err(db, dy.float().sum(0)) < 1e-5
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,N,K", [(65544, 768, 768), (5000, 2304, 768), (300, 264, 520), (4100, 3072, 768)])
+def test_weight_grad_fused_bias_sum(M, N, K, dt):
+    """The 256x256 TN kernel's folded column sums (bias gradient) == the separate colsum pass
+    (DCLIP_OPT_GEMM_TN_COLSUM 1) and torch, with a host alpha; dW is unaffected by the fold."""
+    from denseclip_vit_multimodal_amd import _native as NT
+    O = ops()
+    torch.manual_seed(1)
+    dy = (torch.randn(M, N, device=DEV) + 0.3).to(dt)
+    x = torch.randn(M, K, device=DEV).to(dt)
+    dW, db = O.weight_grad(dy, x, alpha=0.5)
+    NT.call("dclip_set_option", NT.OPT_GEMM_TN_COLSUM, 1)
+    try:
+        dW1, db1 = O.weight_grad(dy, x, alpha=0.5)
+    finally:
+        NT.call("dclip_set_option", NT.OPT_GEMM_TN_COLSUM, 0)
+    assert torch.equal(dW, dW1)
+    assert rel_err(db, db1) < 1e-6
+    assert rel_err(db, 0.5 * dy.double().sum(0)) < 1e-6
+
+
 @pytest.mark.parametrize("tn_tile", [0, 1], indirect=True)
 @pytest.mark.parametrize("K,M,N", [(64, 128, 128), (100, 136, 72), (1000, 256, 384), (8193, 768, 768), (70, 264, 520)])
 def test_gemm_tn(K, M, N, tn_tile):
