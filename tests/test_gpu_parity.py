@@ -317,6 +317,35 @@ def test_text_path_graph_replay_matches_eager():
     assert m._text_graph is graph_before  # eager path taken: no new capture, no replay needed
 
 
+def test_text_prelaunch_on_side_stream_matches_in_line():
+    """The forward replays the captured text graph on a side stream before the backbone
+    (DenseCLIP._text_prelaunch) and the score branch waits for it: the same class embeddings and
+    score map as the golden reference, the pending replay is consumed, and an in-place context
+    update between forwards is seen by the prelaunched replay."""
+    g = golden("tiny_ctx_eval")
+    m = build("tiny_ctx", TINY_CTX_CFG, torch.float16)
+    for p in list(m.text_encoder.parameters()) + [m.contexts]:
+        p.requires_grad_(False)
+    cap = capture(m)
+    x = g["input"].to(DEV)
+    with torch.no_grad():
+        m(x, return_loss=False)  # captures the graph in line
+        assert m._text_graph is not None
+        t1 = cap["text"].clone()
+        m(x, return_loss=False)  # prelaunched replay
+        assert getattr(m, "_text_pending", None) is None
+        assert torch.equal(cap["text"], t1)
+        assert rel_err(cap["text"].cpu(), g["text"]) < 1e-3
+        assert rel_err(cap["score"].cpu(), g["score"]) < 1e-3
+        m.contexts.add_(0.25)
+        m(x, return_loss=False)
+        t3 = cap["text"].clone()
+        m.graph_text = False
+        m(x, return_loss=False)
+    assert not torch.equal(t3, t1)
+    assert rel_err(t3, cap["text"]) < 1e-3
+
+
 @pytest.mark.parametrize("graph_text", [False, True])
 def test_tiny_context_decoder_vs_reference(graph_text):
     """The ContextDecoder branch on the GPU (text path and decoder in torch, ViT / projections /
