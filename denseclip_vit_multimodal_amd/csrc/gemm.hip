@@ -310,7 +310,7 @@ struct BigCfg {
     static constexpr int SMEM = STAGES * STAGE_BYTES > EP_BYTES ? STAGES * STAGE_BYTES : EP_BYTES;
     static_assert(BM % (RPI * NW) == 0 && BN % (RPI * NW) == 0, "staging split");
     static_assert(BKT == 64 || BKT == 32, "k per stage");
-    static_assert(WTM % 32 == 0 && WTN % 16 == 0 && WTN <= 64, "wave tile");
+    static_assert(WTM % 32 == 0 && WTN % 16 == 0 && WTN <= 128, "wave tile");
 };
 
 // Epilogue of the large-tile kernels: 32-row slices of the wave's WTM x WTN tile go through
@@ -416,6 +416,30 @@ __device__ __forceinline__ void stage_rows_buf(const T* X, uint32_t bytes, const
     for (int i = 0; i < ROWS_INST; ++i)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(lds + (wave * ROWS_INST + i) * 1024), 16, voff[i] + kbyte,
                                                  0, 0, 0);
+#endif
+}
+
+// stage_rows_buf with the per-tile and per-piece parts of the source offset in the SCALAR
+// offset: piece i of wave w covers rows 8 (w RI + i) .. + 7 of the tile; lane l reads row
+// l / 8 of it, chunk (l % 8) ^ big_sw(row), and for BKT 64 and an even RI that swizzle depends
+// on the piece only through its parity.  Two offset VGPRs per operand, none per tile.
+template <int ROWS_INST>
+__device__ __forceinline__ void rows_voff2(uint32_t ldbytes, int lane, uint32_t (&v2)[2]) {
+    static_assert(ROWS_INST % 2 == 0, "piece parity");
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+        v2[p] = (uint32_t)(lane >> 3) * ldbytes + (uint32_t)(((lane & 7) ^ ((4 * p + (lane >> 4)) & 7)) << 4);
+}
+
+template <typename T, int ROWS_INST>
+__device__ __forceinline__ void stage_rows_sbuf(const T* X, uint32_t bytes, const uint32_t (&v2)[2], uint32_t s0,
+                                                uint32_t s8, char* lds, int wave) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const rsrc_t rs = make_rsrc(X, bytes);
+#pragma unroll
+    for (int i = 0; i < ROWS_INST; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(lds + (wave * ROWS_INST + i) * 1024), 16, v2[i & 1],
+                                                 s0 + (uint32_t)i * s8, 0, 0);
 #endif
 }
 
@@ -632,18 +656,79 @@ __device__ __forceinline__ void store4_out(OutT* p, const f32x4& v) {
     }
 }
 
-template <typename T, int EPI, typename OutT>
-__global__ __launch_bounds__(512, 1) void gemm_nt_pers_kernel(
+// epilogue of the persistent kernels, from the accumulators straight to global memory:
+// acc[i][j] = C[mw + 16 j + l16][nw + 16 i + 4 lq + e]
+template <typename T, int EPI, typename OutT, typename Cfg>
+__device__ __forceinline__ void pers_epilogue(const f32x4 (&acc)[Cfg::NB][Cfg::MB], int mw, int nw, int l16, int lq,
+                                              float alpha, const float* __restrict__ bias,
+                                              const void* __restrict__ aux, int64_t ld_aux, void* __restrict__ C,
+                                              int64_t ldc, void* __restrict__ C2, int64_t ldc2) {
+    // column pairs outer (their bias / scale vectors loaded once, 16 registers live), rows inner
+#pragma unroll
+    for (int i = 0; i < Cfg::NB; i += 2) {
+        f32x4 bv[2], sv[2];  // per-column constants of this lane's columns of blocks i, i + 1
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int col = nw + 16 * (i + h) + 4 * lq;
+            bv[h] = (bias != nullptr && EPI != DCLIP_EPI_GELU_BWD) ? *(const f32x4*)(bias + col)
+                                                                  : f32x4{0.f, 0.f, 0.f, 0.f};
+            if constexpr (EPI == DCLIP_EPI_STORE_SCALED) sv[h] = *(const f32x4*)((const float*)aux + col);
+        }
+#pragma unroll
+        for (int j = 0; j < Cfg::MB; ++j) {
+            const int64_t row = mw + 16 * j + l16;
+            const int col = nw + 16 * i + 4 * lq;
+            f32x4 v[2] = {acc[i][j] * alpha + bv[0], acc[i + 1][j] * alpha + bv[1]};
+            if constexpr (EPI == DCLIP_EPI_RESIDUAL || sizeof(OutT) == 4) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    if constexpr (EPI == DCLIP_EPI_RESIDUAL)
+                        v[h] += *(const f32x4*)((const float*)aux + row * ld_aux + col + 16 * h);
+                    store4_out<OutT>((OutT*)C + row * ldc + col + 16 * h, v[h]);
+                }
+            } else if constexpr (EPI == DCLIP_EPI_STORE) {
+                store_pair16<OutT>((OutT*)C + row * ldc, col, v[0], v[1], lq);
+            } else if constexpr (EPI == DCLIP_EPI_STORE_SCALED) {
+                store_pair16<OutT>((OutT*)C + row * ldc, col, v[0] * sv[0], v[1] * sv[1], lq);
+            } else if constexpr (EPI == DCLIP_EPI_GELU) {
+                f32x4 g[2];
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        v[h][e] = (float)(OutT)v[h][e];  // the activation sees the rounded pre-activation
+                        g[h][e] = quick_gelu(v[h][e]);
+                    }
+                store_pair16<OutT>((OutT*)C + row * ldc, col, v[0], v[1], lq);
+                store_pair16<OutT>((OutT*)C2 + row * ldc2, col, g[0], g[1], lq);
+            } else if constexpr (EPI == DCLIP_EPI_GELU_BWD) {
+                typedef T t4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const t4 z = *(const t4*)((const T*)aux + row * ld_aux + col + 16 * h);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[h][e] *= quick_gelu_grad((float)z[e]);
+                }
+                store_pair16<OutT>((OutT*)C + row * ldc, col, v[0], v[1], lq);
+            }
+        }
+    }
+}
+
+// NW = 8: 2 x 4 waves of 128 x 64 (two waves per SIMD); NW = 4: 2 x 2 waves of 128 x 128 (one
+// wave per SIMD, the accumulators in AGPRs: 2/3 of the fragment reads per MFMA)
+template <typename T, int EPI, typename OutT, int NW = 8>
+__global__ __launch_bounds__(64 * NW, 1) void gemm_nt_pers_kernel(
     const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb, int K, int tiles_m, int tiles_n,
     const float* __restrict__ bias, const void* __restrict__ aux, int64_t ld_aux, void* __restrict__ C, int64_t ldc,
     void* __restrict__ C2, int64_t ldc2, Alpha alpha_arg) {
     const float alpha = alpha_arg.get();
-    typedef BigCfg<256, 256, 2, 4, 2, 64> Cfg;
+    typedef BigCfg<256, 256, 2, NW / 2, 2, 64> Cfg;
     typedef typename Mfma<T>::frag frag;
     __shared__ __attribute__((aligned(16))) char smem[Cfg::SMEM];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wm = wave >> 2, wn = wave & 3;
+    const int wm = wave / (NW / 2), wn = wave % (NW / 2);
     const int l16 = lane & 15, lq = lane >> 4;
     const int ntiles = tiles_m * tiles_n;
     const int G = gridDim.x;
@@ -651,21 +736,25 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pers_kernel(
     const int nk = K / 64;
     const int M = tiles_m * 256, N = tiles_n * 256;
 
-    // buffer-load staging (stage_rows_buf): offsets per tile, one add per load per K-step
+    // buffer-load staging (stage_rows_sbuf): two per-lane offsets per operand, the rest scalar
     const uint32_t abytes = (uint32_t)((int64_t)M * lda * sizeof(T)), bbytes = (uint32_t)((int64_t)N * ldb * sizeof(T));
-    uint32_t va[Cfg::A_INST], vb[Cfg::B_INST], van[Cfg::A_INST], vbn[Cfg::B_INST];
-#define PERS_STAGE(VA, VB, KT, SLOT)                                                                                 \
+    const uint32_t lda_b = (uint32_t)(lda * sizeof(T)), ldb_b = (uint32_t)(ldb * sizeof(T));
+    uint32_t va[2], vb[2];
+    rows_voff2<Cfg::A_INST>(lda_b, lane, va);
+    rows_voff2<Cfg::B_INST>(ldb_b, lane, vb);
+#define PERS_STAGE(M0, N0, KT, SLOT)                                                                                 \
     do {                                                                                                             \
         char* base_ = smem + (SLOT) * Cfg::STAGE_BYTES;                                                              \
-        stage_rows_buf<T, Cfg::A_INST>(A, abytes, VA, (uint32_t)((KT) * 64 * sizeof(T)), base_, wave);               \
-        stage_rows_buf<T, Cfg::B_INST>(B, bbytes, VB, (uint32_t)((KT) * 64 * sizeof(T)), base_ + Cfg::A_BYTES, wave); \
+        const uint32_t kb_ = (uint32_t)((KT) * 64 * sizeof(T));                                                      \
+        stage_rows_sbuf<T, Cfg::A_INST>(A, abytes, va, (uint32_t)((M0) + 8 * wave * Cfg::A_INST) * lda_b + kb_,     \
+                                        8 * lda_b, base_, wave);                                                     \
+        stage_rows_sbuf<T, Cfg::B_INST>(B, bbytes, vb, (uint32_t)((N0) + 8 * wave * Cfg::B_INST) * ldb_b + kb_,     \
+                                        8 * ldb_b, base_ + Cfg::A_BYTES, wave);                                      \
     } while (0)
     int u = r;
     if (u >= ntiles) return;
     int m0 = (u / tiles_n) * 256, n0 = (u % tiles_n) * 256;
-    rows_voff<T, Cfg::A_INST, 64>(lda, m0, M, wave, lane, va);
-    rows_voff<T, Cfg::B_INST, 64>(ldb, n0, N, wave, lane, vb);
-    PERS_STAGE(va, vb, 0, 0);
+    PERS_STAGE(m0, n0, 0, 0);
     int slot = 0;
     bool first = true;
     while (true) {
@@ -676,19 +765,15 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pers_kernel(
             for (int j = 0; j < Cfg::MB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         const int un = u + G;
         const int nm0 = (un / tiles_n) * 256, nn0 = (un % tiles_n) * 256;
-        if (un < ntiles) {  // the next tile's offsets (its first K-step is staged by this tile's last)
-            rows_voff<T, Cfg::A_INST, 64>(lda, nm0, M, wave, lane, van);
-            rows_voff<T, Cfg::B_INST, 64>(ldb, nn0, N, wave, lane, vbn);
-        }
         for (int kt = 0; kt < nk; ++kt) {
             if (kt == 0 && !first) wait_vmcnt<PERS_EPI_MIN>();  // this K-step's loads, not the epilogue's stores
             else wait_vmcnt<0>();
             __builtin_amdgcn_s_barrier();  // K-step kt visible to every wave; the other slot free
             __builtin_amdgcn_sched_barrier(0);
             if (kt + 1 < nk) {
-                PERS_STAGE(va, vb, kt + 1, slot ^ 1);
-            } else if (un < ntiles) {
-                PERS_STAGE(van, vbn, 0, slot ^ 1);
+                PERS_STAGE(m0, n0, kt + 1, slot ^ 1);
+            } else if (un < ntiles) {  // the next tile's first K-step
+                PERS_STAGE(nm0, nn0, 0, slot ^ 1);
             }
             const char* At = smem + slot * Cfg::STAGE_BYTES;
             const char* Bt = At + Cfg::A_BYTES;
@@ -708,68 +793,157 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_pers_kernel(
             __builtin_amdgcn_sched_barrier(0);
             slot ^= 1;
         }
-        // epilogue: acc[i][j] = C[mw + 16 j + l16][nw + 16 i + 4 lq + e]
-        const int mw = m0 + wm * 128, nw = n0 + wn * 64;
-        f32x4 bv[Cfg::NB], sv[Cfg::NB];  // per-column constants of this lane's 16 columns
-#pragma unroll
-        for (int i = 0; i < Cfg::NB; ++i) {
-            const int col = nw + 16 * i + 4 * lq;
-            bv[i] = (bias != nullptr && EPI != DCLIP_EPI_GELU_BWD) ? *(const f32x4*)(bias + col)
-                                                                  : f32x4{0.f, 0.f, 0.f, 0.f};
-            if constexpr (EPI == DCLIP_EPI_STORE_SCALED) sv[i] = *(const f32x4*)((const float*)aux + col);
-        }
-#pragma unroll
-        for (int j = 0; j < Cfg::MB; ++j) {
-            const int64_t row = mw + 16 * j + l16;
-#pragma unroll
-            for (int i = 0; i < Cfg::NB; i += 2) {
-                const int col = nw + 16 * i + 4 * lq;
-                f32x4 v[2] = {acc[i][j] * alpha + bv[i], acc[i + 1][j] * alpha + bv[i + 1]};
-                if constexpr (EPI == DCLIP_EPI_RESIDUAL || sizeof(OutT) == 4) {
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        if constexpr (EPI == DCLIP_EPI_RESIDUAL)
-                            v[h] += *(const f32x4*)((const float*)aux + row * ld_aux + col + 16 * h);
-                        store4_out<OutT>((OutT*)C + row * ldc + col + 16 * h, v[h]);
-                    }
-                } else if constexpr (EPI == DCLIP_EPI_STORE) {
-                    store_pair16<OutT>((OutT*)C + row * ldc, col, v[0], v[1], lq);
-                } else if constexpr (EPI == DCLIP_EPI_STORE_SCALED) {
-                    store_pair16<OutT>((OutT*)C + row * ldc, col, v[0] * sv[i], v[1] * sv[i + 1], lq);
-                } else if constexpr (EPI == DCLIP_EPI_GELU) {
-                    f32x4 g[2];
-#pragma unroll
-                    for (int h = 0; h < 2; ++h)
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            v[h][e] = (float)(OutT)v[h][e];  // the activation sees the rounded pre-activation
-                            g[h][e] = quick_gelu(v[h][e]);
-                        }
-                    store_pair16<OutT>((OutT*)C + row * ldc, col, v[0], v[1], lq);
-                    store_pair16<OutT>((OutT*)C2 + row * ldc2, col, g[0], g[1], lq);
-                } else if constexpr (EPI == DCLIP_EPI_GELU_BWD) {
-                    typedef T t4 __attribute__((ext_vector_type(4)));
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const t4 z = *(const t4*)((const T*)aux + row * ld_aux + col + 16 * h);
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) v[h][e] *= quick_gelu_grad((float)z[e]);
-                    }
-                    store_pair16<OutT>((OutT*)C + row * ldc, col, v[0], v[1], lq);
-                }
-            }
-        }
+        pers_epilogue<T, EPI, OutT, Cfg>(acc, m0 + wm * 128, n0 + wn * Cfg::WTN, l16, lq, alpha, bias, aux, ld_aux, C, ldc,
+                                         C2, ldc2);
         if (un >= ntiles) break;
         u = un;
         m0 = nm0;
         n0 = nn0;
-#pragma unroll
-        for (int i = 0; i < Cfg::A_INST; ++i) va[i] = van[i];
-#pragma unroll
-        for (int i = 0; i < Cfg::B_INST; ++i) vb[i] = vbn[i];
         first = false;
     }
 #undef PERS_STAGE
+}
+
+// ---------------------------------------------------------------------------- persistent, pipelined fragments
+// gemm_nt_pers_kernel with the LDS fragment reads software-pipelined across the MFMA stream:
+// the K-stream is cut into 32-deep phases (two per 64-deep K-step) and two fragment register
+// sets alternate, so the reads of phase p+1 are issued between the MFMAs of phase p
+// (sched_group_barrier interleave) instead of just in time behind an lgkmcnt wait.  One
+// barrier per K-step sits between its two phases: by then every wave holds both phases of the
+// step in registers (slot free for the step two ahead) and the next step has landed.
+// Needs K >= 128 (the DMA for step g + 2 may already belong to the next tile).
+template <typename T, int NB, int MB>
+__device__ __forceinline__ void pipe_frags(typename Mfma<T>::frag (&fb)[NB], typename Mfma<T>::frag (&fa)[MB],
+                                           const char* At, const char* Bt, int arow, int brow, int ch) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) fb[i] = big_frag<T, 64>(Bt, brow + i * 16, ch);
+#pragma unroll
+    for (int j = 0; j < MB; ++j) fa[j] = big_frag<T, 64>(At, arow + j * 16, ch);
+}
+
+template <typename T, int NB, int MB>
+__device__ __forceinline__ void pipe_mfma(f32x4 (&acc)[NB][MB], const typename Mfma<T>::frag (&fb)[NB],
+                                          const typename Mfma<T>::frag (&fa)[MB]) {
+#pragma unroll
+    for (int j = 0; j < MB; ++j)
+#pragma unroll
+        for (int i = 0; i < NB; ++i) acc[i][j] = Mfma16<T>::mma(fb[i], fa[j], acc[i][j]);
+}
+
+// MB*NB MFMAs with the phase's MB+NB fragment reads spread between them
+template <int NB, int MB>
+__device__ __forceinline__ void pipe_interleave() {
+    constexpr int D = NB + MB, F = NB * MB, PER = F / D;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        __builtin_amdgcn_sched_group_barrier(0x008, PER, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);    // DS read
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, F - PER * D, 0);
+}
+
+template <typename T, int EPI, typename OutT, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void gemm_nt_pipe_kernel(
+    const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb, int K, int tiles_m, int tiles_n,
+    const float* __restrict__ bias, const void* __restrict__ aux, int64_t ld_aux, void* __restrict__ C, int64_t ldc,
+    void* __restrict__ C2, int64_t ldc2, Alpha alpha_arg) {
+    const float alpha = alpha_arg.get();
+    typedef BigCfg<256, 256, 2, NW / 2, 2, 64> Cfg;
+    constexpr int NB = Cfg::NB, MB = Cfg::MB;
+    typedef typename Mfma<T>::frag frag;
+    __shared__ __attribute__((aligned(16))) char smem[Cfg::SMEM];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave / (NW / 2), wn = wave % (NW / 2);
+    const int l16 = lane & 15, lq = lane >> 4;
+    const int ntiles = tiles_m * tiles_n;
+    const int G = gridDim.x;
+    const int nk = K / 64;
+    const int M = tiles_m * 256, N = tiles_n * 256;
+    const int arow = wm * Cfg::WTM + l16, brow = wn * Cfg::WTN + l16;
+    const uint32_t abytes = (uint32_t)((int64_t)M * lda * sizeof(T)), bbytes = (uint32_t)((int64_t)N * ldb * sizeof(T));
+    const uint32_t lda_b = (uint32_t)(lda * sizeof(T)), ldb_b = (uint32_t)(ldb * sizeof(T));
+    uint32_t va[2], vb[2];
+    rows_voff2<Cfg::A_INST>(lda_b, lane, va);
+    rows_voff2<Cfg::B_INST>(ldb_b, lane, vb);
+#define stage(M0_, N0_, KT_, SLOT_)                                                                                    \
+    do {                                                                                                               \
+        char* base_ = smem + (SLOT_) * Cfg::STAGE_BYTES;                                                               \
+        const uint32_t kb_ = (uint32_t)((KT_) * 64 * sizeof(T));                                                       \
+        stage_rows_sbuf<T, Cfg::A_INST>(A, abytes, va, (uint32_t)((M0_) + 8 * wave * Cfg::A_INST) * lda_b + kb_,       \
+                                        8 * lda_b, base_, wave);                                                       \
+        stage_rows_sbuf<T, Cfg::B_INST>(B, bbytes, vb, (uint32_t)((N0_) + 8 * wave * Cfg::B_INST) * ldb_b + kb_,       \
+                                        8 * ldb_b, base_ + Cfg::A_BYTES, wave);                                        \
+    } while (0)
+    int u = xcd_remap(blockIdx.x, G);  // the G tiles of a round in XCD-contiguous ranges
+    if (u >= ntiles) return;
+    int m0 = (u / tiles_n) * 256, n0 = (u % tiles_n) * 256;
+    stage(m0, n0, 0, 0);
+    stage(m0, n0, 1, 1);
+    wait_vmcnt<Cfg::G>();  // step 0 landed (step 1 in flight)
+    __builtin_amdgcn_s_barrier();
+    frag fb0[NB], fa0[MB], fb1[NB], fa1[MB];
+    pipe_frags<T, NB, MB>(fb0, fa0, smem, smem + Cfg::A_BYTES, arow, brow, lq);
+    int slot = 0;
+    bool first = true;
+    while (true) {
+        f32x4 acc[NB][MB];
+#pragma unroll
+        for (int i = 0; i < NB; ++i)
+#pragma unroll
+            for (int j = 0; j < MB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int un = u + G;
+        const bool more = un < ntiles;
+        const int nm0 = (un / tiles_n) * 256, nn0 = (un % tiles_n) * 256;
+        // one 64-deep K-step (a macro: a lambda over these register arrays sends them to scratch);
+        // VMWAIT: the DMA of step g + 1 is the youngest load, or (first step of a tile after the
+        // first) older than the previous tile's epilogue stores, which are counted out, not drained
+#define PIPE_STEP(KT, VMWAIT)                                                                                          \
+    do {                                                                                                               \
+        const int kt_ = (KT);                                                                                          \
+        const char* At = smem + slot * Cfg::STAGE_BYTES;                                                               \
+        const char* An = smem + (slot ^ 1) * Cfg::STAGE_BYTES;                                                         \
+        /* phase (kt, 0): MFMAs on set 0, reads of (kt, 1) into set 1 */                                               \
+        __builtin_amdgcn_sched_barrier(0);                                                                             \
+        pipe_frags<T, NB, MB>(fb1, fa1, At, At + Cfg::A_BYTES, arow, brow, 4 + lq);                                    \
+        pipe_mfma<T, NB, MB>(acc, fb0, fa0);                                                                           \
+        pipe_interleave<NB, MB>();                                                                                     \
+        __builtin_amdgcn_sched_barrier(0);                                                                             \
+        wait_vmcnt<VMWAIT>();                                                                                          \
+        __builtin_amdgcn_s_waitcnt(0xc07f); /* lgkmcnt(0): this wave is done reading slot `slot` */                    \
+        __builtin_amdgcn_s_barrier();                                                                                  \
+        /* set 1 pinned behind the barrier (the MFMA builtins are pure: without this the compiler */                   \
+        /* hoists phase (kt, 1) above it and leaves the reads below with nothing beside them) */                       \
+        for (int i = 0; i < NB; ++i) asm volatile("" : "+v"(fb1[i]));                                                  \
+        for (int j = 0; j < MB; ++j) asm volatile("" : "+v"(fa1[j]));                                                  \
+        __builtin_amdgcn_sched_barrier(0);                                                                             \
+        /* step g + 2 into the slot just read (branch-free: past the last tile a harmless re-load of */                \
+        /* this tile's step 0 into a slot nobody reads again) */                                                       \
+        const bool in_tile = kt_ + 2 < nk;                                                                             \
+        stage(in_tile ? m0 : (more ? nm0 : m0), in_tile ? n0 : (more ? nn0 : n0),                                      \
+              in_tile ? kt_ + 2 : (more ? kt_ + 2 - nk : 0), slot);                                                    \
+        /* phase (kt, 1): MFMAs on set 1, reads of (kt + 1, 0) (or the next tile's first) into set 0 */                \
+        __builtin_amdgcn_sched_barrier(0);                                                                             \
+        pipe_frags<T, NB, MB>(fb0, fa0, An, An + Cfg::A_BYTES, arow, brow, lq);                                        \
+        pipe_mfma<T, NB, MB>(acc, fb1, fa1);                                                                           \
+        pipe_interleave<NB, MB>();                                                                                     \
+        __builtin_amdgcn_sched_barrier(0);                                                                             \
+        slot ^= 1;                                                                                                     \
+    } while (0)
+        if (first) PIPE_STEP(0, 0);
+        else PIPE_STEP(0, PERS_EPI_MIN);
+        for (int kt = 1; kt < nk; ++kt) PIPE_STEP(kt, 0);
+#undef PIPE_STEP
+        pers_epilogue<T, EPI, OutT, Cfg>(acc, m0 + wm * 128, n0 + wn * Cfg::WTN, l16, lq, alpha, bias, aux, ld_aux, C,
+                                         ldc, C2, ldc2);
+        if (!more) break;
+        u = un;
+        m0 = nm0;
+        n0 = nn0;
+        first = false;
+    }
+    wait_vmcnt<0>();
+#undef stage
 }
 
 // ---------------------------------------------------------------------------- "TN"
@@ -1509,7 +1683,7 @@ int cu_count() {
     return n[dev];
 }
 
-template <typename T, int EPI, typename OutT>
+template <typename T, int EPI, typename OutT, int NW = 8, bool PIPE = false>
 bool launch_pers(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
                  Alpha alpha, const float* bias, const void* aux, int64_t ld_aux, void* C, int64_t ldc, void* C2,
                  int64_t ldc2, hipStream_t st) {
@@ -1519,6 +1693,7 @@ bool launch_pers(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t
         const int64_t Mfull = (M / 256) * 256, tail = M - Mfull;
         const int G = cu_count();
         if (N % 256 != 0 || tail > 64 || (Mfull / 256) * (N / 256) < 2 * G) return false;
+        if (PIPE && K < 128) return false;
         // buffer-load staging addresses each operand with 32-bit byte offsets
         if (Mfull * lda * (int64_t)sizeof(T) >= (1ll << 32) || N * ldb * (int64_t)sizeof(T) >= (1ll << 32)) return false;
         if (EPI == DCLIP_EPI_STORE_SCALED || (bias != nullptr && EPI != DCLIP_EPI_GELU_BWD)) {
@@ -1548,9 +1723,14 @@ bool launch_pers(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t
             tail_combine_kernel<T, EPI, OutT><<<(threads + 255) / 256, 256, 0, st>>>(
                 ws, ts, (int)tail, (int)N, Mfull, bias, aux, ld_aux, C, ldc, C2, ldc2);
         }
-        gemm_nt_pers_kernel<T, EPI, OutT><<<G, 512, 0, st>>>((const T*)A, lda, (const T*)B, ldb, (int)K,
-                                                             (int)(Mfull / 256), (int)(N / 256), bias, aux, ld_aux,
-                                                             C, ldc, C2, ldc2, alpha);
+        if constexpr (PIPE)
+            gemm_nt_pipe_kernel<T, EPI, OutT, NW><<<G, 64 * NW, 0, st>>>((const T*)A, lda, (const T*)B, ldb, (int)K,
+                                                                         (int)(Mfull / 256), (int)(N / 256), bias, aux,
+                                                                         ld_aux, C, ldc, C2, ldc2, alpha);
+        else
+            gemm_nt_pers_kernel<T, EPI, OutT, NW><<<G, 64 * NW, 0, st>>>((const T*)A, lda, (const T*)B, ldb, (int)K,
+                                                                         (int)(Mfull / 256), (int)(N / 256), bias, aux,
+                                                                         ld_aux, C, ldc, C2, ldc2, alpha);
         return true;
     }
 }
@@ -1558,7 +1738,9 @@ bool launch_pers(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t
 // tile configuration: DCLIP_OPT_GEMM_TILE 1 = 128x128 (4 waves, 2 workgroups/CU), 2 = 256x256
 // (8 waves, 2-stage ring of 64-deep k-tiles), 3 = 256x128 (8 waves, 3-stage ring),
 // 4 = 256x256 with a 4-stage ring of 32-deep k-tiles, 5 = 256x256 ping-pong (gemm_nt_pp_kernel),
-// 6 = persistent 256x256 (gemm_nt_pers_kernel) where the shape allows it, 0 = automatic
+// 6 = persistent 256x256 (gemm_nt_pers_kernel) where the shape allows it, 7 = the same with 4
+// waves of 128x128, 8 / 9 = the persistent kernel with pipelined fragment reads
+// (gemm_nt_pipe_kernel) with 8 / 4 waves, 0 = automatic
 inline int gemm_tile_choice(int64_t M, int64_t N) {
     const int opt = dclip_option(DCLIP_OPT_GEMM_TILE);
     if (opt != 0) return opt;
@@ -1584,7 +1766,16 @@ int launch(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, in
     if (choice == 6 && splits == 1 &&
         launch_pers<T, EPI, OutT>(A, lda, B, ldb, M, N, K, alpha, bias, aux, ld_aux, C, ldc, C2, ldc2, st))
         return 0;
-    if (choice == 6) {
+    if (choice == 7 && splits == 1 &&
+        launch_pers<T, EPI, OutT, 4>(A, lda, B, ldb, M, N, K, alpha, bias, aux, ld_aux, C, ldc, C2, ldc2, st))
+        return 0;
+    if (choice == 8 && splits == 1 &&
+        launch_pers<T, EPI, OutT, 8, true>(A, lda, B, ldb, M, N, K, alpha, bias, aux, ld_aux, C, ldc, C2, ldc2, st))
+        return 0;
+    if (choice == 9 && splits == 1 &&
+        launch_pers<T, EPI, OutT, 4, true>(A, lda, B, ldb, M, N, K, alpha, bias, aux, ld_aux, C, ldc, C2, ldc2, st))
+        return 0;
+    if (choice >= 6) {
         launch_big<T, EPI, OutT, 256, 256, 2, 4, 2>(A, lda, B, ldb, M, N, K, splits, alpha, bias, aux, ld_aux, C,
                                                     ldc, C2, ldc2, st);
         return 0;

@@ -100,7 +100,7 @@ def test_layernorm_bwd_res(cols, lpdt):
 # ----------------------------------------------------------------------------- GEMM
 SHAPES = [(128, 128, 64), (300, 200, 192), (65, 64, 128), (1000, 2304, 768), (4097, 768, 3072), (8, 512, 768),
           (65544, 768, 1536)]  # the last: M = 256k + 8 takes the M-tail split-K path on the big tiles
-TILES = [1, 2, 3, 4, 5, 6]  # DCLIP_OPT_GEMM_TILE: 128x128, 256x256, 256x128, 256x256 k32, ping-pong, persistent
+TILES = [1, 2, 3, 4, 5, 6, 7, 8, 9]  # DCLIP_OPT_GEMM_TILE: 128x128, 256x256, 256x128, 256x256 k32, ping-pong, persistent (8 / 4 waves; pipelined 8 / 4)
 
 
 @pytest.fixture

@@ -1,0 +1,60 @@
+"""Timing diagnostic: attention fwd / bwd launches at the bench shape (B=8, N=8193, H=12, bf16)
+with the library given on the command line (libdclip.so or the WRONG-results
+libdclip_diag.so whose 32x32x16 MFMAs are replaced by pairs of 16x16x32), per-launch HIP-event
+times.  Run the two libraries in separate processes, alternately.
+
+  python tools/mfma_shape_diag.py path/to/lib.so [reps]
+"""
+import ctypes
+import sys
+
+import torch
+
+lib = ctypes.CDLL(sys.argv[1])
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+B, N, H, D = 8, 8193, 12, 64
+C = H * D
+torch.manual_seed(0)
+qkv = (torch.randn(B * N, 3 * C, device="cuda") * 0.5).to(torch.bfloat16)
+qkv[:, :C] *= 0.125 * 1.4426950408889634
+dout = torch.randn(B * N, C, device="cuda").to(torch.bfloat16)
+o = torch.empty(B * N, C, device="cuda", dtype=torch.bfloat16)
+lse = torch.empty(B * H * N, device="cuda", dtype=torch.float32)
+lib.dclip_attn_bwd_workspace.restype = ctypes.c_int64
+ws = torch.empty(lib.dclip_attn_bwd_workspace(B, N, H), device="cuda", dtype=torch.float32)
+dqkv = torch.empty_like(qkv)
+st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+P = ctypes.c_void_p
+
+
+def fwd():
+    rc = lib.dclip_attn_fwd(2, P(qkv.data_ptr()), P(o.data_ptr()), P(lse.data_ptr()), B, N, H, D,
+                            ctypes.c_float(0.125), st)
+    assert rc == 0, rc
+
+
+def bwd():
+    rc = lib.dclip_attn_bwd(2, P(qkv.data_ptr()), P(o.data_ptr()), P(dout.data_ptr()), P(lse.data_ptr()),
+                            P(ws.data_ptr()), P(dqkv.data_ptr()), B, N, H, D, ctypes.c_float(0.125), st)
+    assert rc == 0, rc
+
+
+def timed(fn):
+    fn()
+    ts = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+fwd()
+tf = timed(fwd)
+tb = timed(bwd)
+print(f"{sys.argv[1].split('/')[-1]}: fwd {tf:.3f} ms  bwd {tb:.3f} ms  "
+      f"finite o {bool(torch.isfinite(o.float()).all())} dqkv {bool(torch.isfinite(dqkv.float()).all())}", flush=True)
