@@ -658,21 +658,37 @@ __device__ __forceinline__ void store4_out(OutT* p, const f32x4& v) {
 
 // epilogue of the persistent kernels, from the accumulators straight to global memory:
 // acc[i][j] = C[mw + 16 j + l16][nw + 16 i + 4 lq + e]
+// the per-column constants (bias, QKV scale) of a wave's columns, loaded when its tile starts so
+// that their latency hides behind the K-loop instead of stalling the epilogue
+template <int EPI, int NB>
+struct PersCols {
+    f32x4 bv[NB], sv[NB];
+};
+
+template <int EPI, int NB>
+__device__ __forceinline__ void pers_cols(PersCols<EPI, NB>& pc, const float* __restrict__ bias,
+                                          const void* __restrict__ aux, int nw, int lq) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        const int col = nw + 16 * i + 4 * lq;
+        pc.bv[i] = (bias != nullptr && EPI != DCLIP_EPI_GELU_BWD) ? *(const f32x4*)(bias + col)
+                                                                 : f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (EPI == DCLIP_EPI_STORE_SCALED) pc.sv[i] = *(const f32x4*)((const float*)aux + col);
+    }
+}
+
 template <typename T, int EPI, typename OutT, typename Cfg>
-__device__ __forceinline__ void pers_epilogue(const f32x4 (&acc)[Cfg::NB][Cfg::MB], int mw, int nw, int l16, int lq,
-                                              float alpha, const float* __restrict__ bias,
+__device__ __forceinline__ void pers_epilogue(const f32x4 (&acc)[Cfg::NB][Cfg::MB], const PersCols<EPI, Cfg::NB>& pc,
+                                              int mw, int nw, int l16, int lq, float alpha,
                                               const void* __restrict__ aux, int64_t ld_aux, void* __restrict__ C,
                                               int64_t ldc, void* __restrict__ C2, int64_t ldc2) {
-    // column pairs outer (their bias / scale vectors loaded once, 16 registers live), rows inner
 #pragma unroll
     for (int i = 0; i < Cfg::NB; i += 2) {
-        f32x4 bv[2], sv[2];  // per-column constants of this lane's columns of blocks i, i + 1
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int col = nw + 16 * (i + h) + 4 * lq;
-            bv[h] = (bias != nullptr && EPI != DCLIP_EPI_GELU_BWD) ? *(const f32x4*)(bias + col)
-                                                                  : f32x4{0.f, 0.f, 0.f, 0.f};
-            if constexpr (EPI == DCLIP_EPI_STORE_SCALED) sv[h] = *(const f32x4*)((const float*)aux + col);
+        const f32x4 bv[2] = {pc.bv[i], pc.bv[i + 1]};
+        f32x4 sv[2];
+        if constexpr (EPI == DCLIP_EPI_STORE_SCALED) {
+            sv[0] = pc.sv[i];
+            sv[1] = pc.sv[i + 1];
         }
 #pragma unroll
         for (int j = 0; j < Cfg::MB; ++j) {
@@ -763,6 +779,8 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_nt_pers_kernel(
         for (int i = 0; i < Cfg::NB; ++i)
 #pragma unroll
             for (int j = 0; j < Cfg::MB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        PersCols<EPI, Cfg::NB> pc;
+        pers_cols<EPI, Cfg::NB>(pc, bias, aux, n0 + wn * Cfg::WTN, lq);
         const int un = u + G;
         const int nm0 = (un / tiles_n) * 256, nn0 = (un % tiles_n) * 256;
         for (int kt = 0; kt < nk; ++kt) {
@@ -793,7 +811,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_nt_pers_kernel(
             __builtin_amdgcn_sched_barrier(0);
             slot ^= 1;
         }
-        pers_epilogue<T, EPI, OutT, Cfg>(acc, m0 + wm * 128, n0 + wn * Cfg::WTN, l16, lq, alpha, bias, aux, ld_aux, C, ldc,
+        pers_epilogue<T, EPI, OutT, Cfg>(acc, pc, m0 + wm * 128, n0 + wn * Cfg::WTN, l16, lq, alpha, aux, ld_aux, C, ldc,
                                          C2, ldc2);
         if (un >= ntiles) break;
         u = un;
@@ -892,6 +910,8 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_nt_pipe_kernel(
         for (int i = 0; i < NB; ++i)
 #pragma unroll
             for (int j = 0; j < MB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        PersCols<EPI, Cfg::NB> pc;
+        pers_cols<EPI, Cfg::NB>(pc, bias, aux, n0 + wn * Cfg::WTN, lq);
         const int un = u + G;
         const bool more = un < ntiles;
         const int nm0 = (un / tiles_n) * 256, nn0 = (un % tiles_n) * 256;
@@ -934,7 +954,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_nt_pipe_kernel(
         else PIPE_STEP(0, PERS_EPI_MIN);
         for (int kt = 1; kt < nk; ++kt) PIPE_STEP(kt, 0);
 #undef PIPE_STEP
-        pers_epilogue<T, EPI, OutT, Cfg>(acc, m0 + wm * 128, n0 + wn * Cfg::WTN, l16, lq, alpha, bias, aux, ld_aux, C,
+        pers_epilogue<T, EPI, OutT, Cfg>(acc, pc, m0 + wm * 128, n0 + wn * Cfg::WTN, l16, lq, alpha, aux, ld_aux, C,
                                          ldc, C2, ldc2);
         if (!more) break;
         u = un;

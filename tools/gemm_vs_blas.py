@@ -1,4 +1,4 @@
-"""Our MFMA GEMMs (default tile choice) vs torch.mm (hipBLASLt) on the ViT-B/16 token GEMMs at
+"""Our MFMA GEMMs (default tile choice; NT with a bias epilogue) vs torch.mm / addmm (hipBLASLt) on the ViT-B/16 token GEMMs at
 the bench shape (M = 8 x 8193), random bf16 data, interleaved rounds.  Forward/dX GEMMs are
 "NT" (out = A B^T); weight gradients are "TN" (dW = dY^T X, fp32 out).
 
@@ -34,8 +34,9 @@ for name, n, k in [("qkv", 3 * C, C), ("out_proj", C, C), ("c_fc", 4 * C, C), ("
                    ("dX in_proj", C, 3 * C), ("dX c_fc", C, 4 * C), ("dX c_proj", 4 * C, C)]:
     a = torch.randn(M, k, device="cuda").to(bf)
     w = (torch.randn(n, k, device="cuda") * k ** -0.5).to(bf)
-    cases.append((f"NT {name:11s} N={n:5d} K={k:5d}", lambda a=a, w=w: O.gemm(a, w), lambda a=a, w=w: torch.mm(a, w.t()),
-                  2.0 * M * n * k))
+    b = torch.randn(n, device="cuda")  # every token GEMM of the model carries a bias
+    cases.append((f"NT {name:11s} N={n:5d} K={k:5d}", lambda a=a, w=w, b=b: O.gemm(a, w, bias=b),
+                  lambda a=a, w=w, b=b: torch.addmm(b.to(bf), a, w.t()), 2.0 * M * n * k))
 for name, n, k in [("in_proj", 3 * C, C), ("out_proj", C, C), ("c_fc", 4 * C, C), ("c_proj", C, 4 * C)]:
     dy = torch.randn(M, n, device="cuda").to(bf)
     x = torch.randn(M, k, device="cuda").to(bf)

@@ -1,0 +1,157 @@
+// Clock probe: does the MFMA shape change the clock the chip holds under an attention-like
+// load?  Two kernels with the same FLOPs, operand bytes and VALU work per iteration, one on
+// v_mfma_f32_32x32x16_bf16 (as the attention kernels), one on v_mfma_f32_16x16x32_bf16:
+//   S = K Q^T chain over 4 (or 2) K-steps from zero, P = exp2(S * c - 1), row sums += P,
+//   P packed to bf16 and fed as the B operand of O += V P.  Operands are re-read from LDS
+//   (random bf16) every iteration.  The in-kernel clock is stamped with s_memtime /
+//   s_memrealtime around the loop (diagnostic buffer only; no output value depends on it).
+//   hipcc -O3 --offload-arch=gfx950 tools/mfma_clock.hip -o tools/mfma_clock
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bf16x8 lds8(const char* p) { return *(const bf16x8*)p; }
+
+template <int SHAPE>
+__global__ __launch_bounds__(256, 2) void probe(const __bf16* __restrict__ src, float* __restrict__ out,
+                                                unsigned long long* __restrict__ stamps, int iters) {
+    __shared__ __attribute__((aligned(16))) char sm[32768];
+    const int lane = threadIdx.x & 63;
+    for (int i = threadIdx.x; i < 32768 / 16; i += 256) ((bf16x8*)sm)[i] = ((const bf16x8*)src)[i];
+    __syncthreads();
+    float rs = 0.f;
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    if constexpr (SHAPE == 32) {
+        f32x16 o[2] = {};
+        for (int it = 0; it < iters; ++it) {
+            const char* base = sm + ((it * 4096) & 16383) + lane * 16;
+            f32x16 s[2];
+            for (int kb = 0; kb < 2; ++kb) {
+                s[kb] = f32x16{};
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds8(base + 1024 * k + 512 * kb),
+                                                                    lds8(base + 8192 + 1024 * k), s[kb], 0, 0, 0);
+            }
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float p = __builtin_amdgcn_exp2f(s[kb][r] * 0.01f - 1.f);
+                    s[kb][r] = p;
+                    rs += p;
+                }
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    bf16x8 pf;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) pf[j] = (__bf16)s[kb][8 * h + j];
+#pragma unroll
+                    for (int db = 0; db < 2; ++db)
+                        o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds8(base + 16384 + 2048 * kb + 1024 * h + 512 * db),
+                                                                        pf, o[db], 0, 0, 0);
+                }
+        }
+        for (int db = 0; db < 2; ++db)
+            for (int r = 0; r < 16; ++r) rs += o[db][r];
+    } else {
+        f32x4 o[8] = {};
+        for (int it = 0; it < iters; ++it) {
+            const char* base = sm + ((it * 4096) & 16383) + lane * 16;
+            f32x4 s[8];  // same 2048 scores per wave: 8 blocks of 16 x 16
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                s[b] = f32x4{};
+#pragma unroll
+                for (int k = 0; k < 2; ++k)
+                    s[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(base + 1024 * k + 256 * (b & 3)),
+                                                                   lds8(base + 8192 + 1024 * k + 512 * (b >> 2)), s[b], 0, 0, 0);
+            }
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float p = __builtin_amdgcn_exp2f(s[b][r] * 0.01f - 1.f);
+                    s[b][r] = p;
+                    rs += p;
+                }
+#pragma unroll
+            for (int b = 0; b < 8; b += 2) {
+                bf16x8 pf;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    pf[j] = (__bf16)s[b][j];
+                    pf[4 + j] = (__bf16)s[b + 1][j];
+                }
+#pragma unroll
+                for (int db = 0; db < 4; ++db)
+                    o[2 * (b >> 2) + (db & 1) + 0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        lds8(base + 16384 + 1024 * (b >> 1) + 256 * db), pf, o[2 * (b >> 2) + (db & 1)], 0, 0, 0);
+            }
+        }
+        for (int i = 0; i < 8; ++i)
+            for (int r = 0; r < 4; ++r) rs += o[i][r];
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    out[blockIdx.x * 256 + threadIdx.x] = rs;
+    if (threadIdx.x == 0) {
+        stamps[2 * blockIdx.x] = t1 - t0;
+        stamps[2 * blockIdx.x + 1] = r1 - r0;
+    }
+}
+
+template <int SHAPE>
+void run(const __bf16* src, float* out, unsigned long long* st, int iters, int blocks) {
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    for (int rep = 0; rep < 3; ++rep) {
+        hipEventRecord(e0);
+        probe<SHAPE><<<blocks, 256>>>(src, out, st, iters);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms = 0;
+        hipEventElapsedTime(&ms, e0, e1);
+        unsigned long long* h = (unsigned long long*)malloc(16 * blocks);
+        hipMemcpy(h, st, 16 * blocks, hipMemcpyDeviceToHost);
+        double clk = 0;
+        for (int b = 0; b < blocks; ++b) clk += (double)h[2 * b] / (double)h[2 * b + 1] * 100.0;  // MHz
+        free(h);
+        // FLOP per iteration per wave: 16 (32x32x16) MFMAs = 32 (16x16x32) = 524288
+        const double flop = 524288.0 * 4 * blocks * (double)iters;
+        printf("mfma %dx%d: %.3f ms  %.1f TFLOP/s  in-kernel clock %.0f MHz\n", SHAPE, SHAPE, ms, flop / ms / 1e9,
+               clk / blocks);
+    }
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+}
+
+int main(int argc, char** argv) {
+    const int iters = argc > 1 ? atoi(argv[1]) : 20000;
+    const int blocks = 512;  // 256 CUs x 2 workgroups of 4 waves = 2 waves per SIMD
+    __bf16* src;
+    float* out;
+    unsigned long long* st;
+    hipMalloc(&src, 32768);
+    hipMalloc(&out, blocks * 256 * 4);
+    hipMalloc(&st, blocks * 16);
+    __bf16* h = (__bf16*)malloc(32768);
+    srand(1);
+    for (int i = 0; i < 16384; ++i) h[i] = (__bf16)((rand() / (float)RAND_MAX - 0.5f) * 4.f);
+    hipMemcpy(src, h, 32768, hipMemcpyHostToDevice);
+    for (int round = 0; round < 2; ++round) {
+        run<32>(src, out, st, iters, blocks);
+        run<16>(src, out, st, iters, blocks);
+    }
+    hipFree(src);
+    hipFree(out);
+    hipFree(st);
+    free(h);
+    return 0;
+}
