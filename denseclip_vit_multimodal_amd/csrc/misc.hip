@@ -277,13 +277,16 @@ __global__ __launch_bounds__(256) void transpose_kernel(const TI* __restrict__ i
 // F.adaptive_avg_pool2d(x, 1) of a pixel-row map (denseclip.py:596) read in place from a strided
 // row layout (the ViT token buffer: batch stride N*C, row offset 1 skips CLS).  Stage 1: one
 // workgroup per (image, chunk of rows) streams its rows with 16-byte loads (a 768-channel row =
-// 96 lanes, 256 / 96 rows in flight per pass) and writes the chunk's column sums; stage 2 sums
-// the chunks in a fixed order (deterministic) and divides.
-constexpr int RM_CHUNK = 64;  // rows per workgroup
+// 96 lanes, 256 / 96 rows per pass), RM_BATCH rows per thread loaded before any is summed so
+// that ~24 KiB per workgroup are in flight (HBM rate, not load latency), and writes the chunk's
+// column sums; stage 2 sums the chunks in a fixed order (deterministic) and divides.
+constexpr int RM_CHUNK = 128;  // rows per workgroup
+constexpr int RM_BATCH = 8;    // loads in flight per thread
 
 template <typename TI>
 __global__ __launch_bounds__(256) void row_mean_part_kernel(const TI* __restrict__ x, int64_t bstride, int64_t row_off,
                                                             int64_t ld, int64_t rows, int C, float* __restrict__ ws) {
+    typedef TI t8 __attribute__((ext_vector_type(8)));
     __shared__ float red[2048 / 8 * 8];
     const int b = blockIdx.y, ch = blockIdx.x, S = gridDim.x;
     const int nc8 = C / 8, nrp = 256 / nc8;
@@ -293,12 +296,17 @@ __global__ __launch_bounds__(256) void row_mean_part_kernel(const TI* __restrict
     float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (rp < nrp) {
         const TI* base = x + (int64_t)b * bstride + row_off * ld + cc * 8;
-#pragma unroll 4
-        for (int64_t r = r0 + rp; r < r1; r += nrp) {
-            typedef TI t8 __attribute__((ext_vector_type(8)));
-            const t8 v = *(const t8*)(base + r * ld);
+        for (int64_t r = r0 + rp; r < r1; r += RM_BATCH * nrp) {
+            t8 v[RM_BATCH];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) a[e] += (float)v[e];
+            for (int i = 0; i < RM_BATCH; ++i) {
+                const int64_t ri = r + (int64_t)i * nrp;
+                v[i] = ri < r1 ? *(const t8*)(base + ri * ld) : t8{};
+            }
+#pragma unroll
+            for (int i = 0; i < RM_BATCH; ++i)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) a[e] += (float)v[i][e];
         }
     }
     // reduce the nrp row phases of each column chunk through LDS (phase 0 keeps, the others add)
@@ -346,35 +354,70 @@ __global__ __launch_bounds__(256) void score_map_kernel(const TV* __restrict__ v
     const int pitch = C + 8;
     const int b = blockIdx.y;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l32 = lane & 31, h = lane >> 5;
-    for (int k = wave; k < 32; k += 4) {
-        if (k < K) {
-            const float* tr = t + ((int64_t)b * K + k) * C;
-            float ss = 0.f;
-            for (int c = lane; c < C; c += 64) ss += tr[c] * tr[c];
-            const float inv = 1.f / fmaxf(sqrtf(wave_sum(ss)), eps);
-            for (int c = lane; c < C; c += 64) tn[k * pitch + c] = (TV)(tr[c] * inv);
+    // class-embedding norms, then the normalised 16-bit rows: two sweeps of independent 16-byte
+    // loads over the K x C block (the second from cache) instead of one dependent load -> wave
+    // reduction -> reload chain per row
+    __shared__ float nrm[32];
+    if (threadIdx.x < 32) nrm[threadIdx.x] = 0.f;
+    __syncthreads();
+    const f32x4* tb = (const f32x4*)(t + (int64_t)b * K * C);
+    const int n4 = K * C / 4, c4 = C / 4;
+    for (int i = threadIdx.x; i < n4; i += 256) {
+        const f32x4 x = tb[i];
+        float ss = x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3];
+        const int k = i / c4;
+        const int base = i - lane;  // this wave's first chunk (every lane of the wave is active: n4 % 4 == 0)
+        if (base + 63 < n4 && base / c4 == (base + 63) / c4) {  // the wave's 64 chunks lie in one row
+            ss = wave_sum(ss);
+            if (lane == 0) atomicAdd(&nrm[k], ss);
         } else {
-            for (int c = lane; c < C; c += 64) tn[k * pitch + c] = (TV)0.f;
+            atomicAdd(&nrm[k], ss);
         }
     }
     __syncthreads();
-    const int nsteps = C / 16;
-    for (int p0 = (blockIdx.x * 4 + wave) * 32; p0 < HW; p0 += gridDim.x * 128) {
-        const int p = p0 + l32;
-        const int pc = p < HW ? p : HW - 1;
-        const TV* row = v + (int64_t)b * bstride + (row_off + pc) * ld + 8 * h;
-        const TV* arow = tn + l32 * pitch + 8 * h;
-        f32x16 acc;
+    for (int i = threadIdx.x; i < 32 * c4; i += 256) {
+        const int k = i / c4, c = 4 * (i - k * c4);
+        f32x4 x = {0.f, 0.f, 0.f, 0.f};
+        if (k < K) x = tb[i] * (1.f / fmaxf(sqrtf(nrm[k]), eps));
+        typedef TV t4 __attribute__((ext_vector_type(4)));
+        *(t4*)(tn + k * pitch + c) = t4{(TV)x[0], (TV)x[1], (TV)x[2], (TV)x[3]};
+    }
+    __syncthreads();
+    // one 32-pixel group per workgroup, its channels split over the 4 waves (16-channel MFMA steps
+    // [w S / 4, (w + 1) S / 4)): 4x the loads in flight of one wave sweeping all C, then the
+    // partial products and norms summed through LDS in a fixed order
+    float* red = (float*)(smem + (size_t)32 * pitch * sizeof(TV));  // [3][17][64]
+    const int nsteps = C / 16, s0 = wave * nsteps / 4, s1 = (wave + 1) * nsteps / 4;
+    const int p = blockIdx.x * 32 + l32;
+    const int pc = p < HW ? p : HW - 1;
+    const TV* row = v + (int64_t)b * bstride + (row_off + pc) * ld + 8 * h;
+    const TV* arow = tn + l32 * pitch + 8 * h;
+    f32x16 acc;
 #pragma unroll
-        for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-        float ss = 0.f;
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    float ss = 0.f;
 #pragma unroll 8
-        for (int s = 0; s < nsteps; ++s) {
-            const frag bf = *(const frag*)(row + 16 * s);
-            const frag af = *(const frag*)(arow + 16 * s);
+    for (int s = s0; s < s1; ++s) {
+        const frag bf = *(const frag*)(row + 16 * s);
+        const frag af = *(const frag*)(arow + 16 * s);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) ss += (float)bf[j] * (float)bf[j];
-            acc = Mfma<TV>::mma(af, bf, acc);
+        for (int j = 0; j < 8; ++j) ss += (float)bf[j] * (float)bf[j];
+        acc = Mfma<TV>::mma(af, bf, acc);
+    }
+    if (wave > 0) {
+        float* r = red + (wave - 1) * 17 * 64;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) r[e * 64 + lane] = acc[e];
+        r[16 * 64 + lane] = ss;
+    }
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+        for (int w = 0; w < 3; ++w) {
+            const float* r = red + w * 17 * 64;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[e] += r[e * 64 + lane];
+            ss += r[16 * 64 + lane];
         }
         ss += __shfl_xor(ss, 32, 64);  // the other half-wave holds the pixel's other 8-column chunks
         const float inv = 1.f / fmaxf(sqrtf(ss), eps);
@@ -622,9 +665,8 @@ extern "C" int dclip_score_map(const void* v, int v_dt, int64_t bstride, int64_t
     DCLIP_HOST_CHECK(C % 16 == 0 && C <= 2048 && ld % 8 == 0 && bstride % 8 == 0 && ((uintptr_t)v % 16) == 0,
                      "dclip_score_map: C %% 16 == 0, C <= 2048, 16-byte aligned rows");
     DCLIP_HOST_CHECK(B > 0 && HW > 0, "dclip_score_map: empty input");
-    int bx = (HW + 127) / 128;
-    if (bx > 256) bx = 256;
-    const size_t lds = (size_t)32 * (C + 8) * 2;
+    const int bx = (HW + 31) / 32;
+    const size_t lds = (size_t)32 * (C + 8) * 2 + 3 * 17 * 64 * sizeof(float);
     hipStream_t st = (hipStream_t)stream;
     if (v_dt == DCLIP_BF16)
         score_map_kernel<bf16><<<dim3(bx, B), 256, lds, st>>>((const bf16*)v, bstride, row_off, ld, t, score, HW, C, K,
