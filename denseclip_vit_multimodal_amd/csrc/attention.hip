@@ -255,7 +255,13 @@ __device__ __forceinline__ void fwd_step(FwdCtx<T, NT>& c, int t, f32x16 (&sc)[2
 #pragma unroll
             for (int r = 0; r < 16; ++r) c.o[db][r] *= alpha;
         c.m += shift;
-        c.negm = splat16(-c.m);
+        const float nm = -c.m;  // into negm's own registers (see fwd2_step)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            float x = c.negm[r];
+            asm volatile("v_mov_b32 %0, %1" : "+v"(x) : "v"(nm));
+            c.negm[r] = x;
+        }
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -442,9 +448,15 @@ __device__ __forceinline__ void fwd2_step(Fwd2Ctx<T, NW>& c, int t, f32x16 (&sc)
     exp_tile(sc, rsp);
     const float tot = (rsp[0] + rsp[1]) + (rsp[2] + rsp[3]);
     if (__any(!(tot <= LIM))) {  // rare: move the reference to the tile's row max and redo P(t)
-        f32x16 sr[2];
-        s_tile<T>(sr, Ks + Q * 8192, c.qf, c.negm, c.l32, c.h);
-        const float shift = fmaxf(tile_rowmax2(sr), 0.f);
+        // S(t) recomputed from a zero accumulator and the reference applied afterwards: feeding
+        // c.negm to the MFMAs here let the compiler overwrite its registers in this path, and
+        // the common path then copied all 16 of them (8 v_mov_b64 per tile) to join the two
+        s_tile<T>(sc, Ks + Q * 8192, c.qf, zero16(), c.l32, c.h);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sc[kb][r] -= c.m;
+        const float shift = fmaxf(tile_rowmax2(sc), 0.f);
         const float alpha = __builtin_amdgcn_exp2f(-shift);
 #pragma unroll
         for (int j = 0; j < 4; ++j) c.l4[j] *= alpha;
@@ -453,13 +465,21 @@ __device__ __forceinline__ void fwd2_step(Fwd2Ctx<T, NW>& c, int t, f32x16 (&sc)
 #pragma unroll
             for (int r = 0; r < 16; ++r) c.o[db][r] *= alpha;
         c.m += shift;
-        c.negm = splat16(-c.m);
+        // new reference written into negm's own registers (tied asm operands): a fresh splat
+        // lands in other registers and every common-path step then copies 16 of them to join
+        const float nm = -c.m;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            float x = c.negm[r];
+            asm volatile("v_mov_b32 %0, %1" : "+v"(x) : "v"(nm));
+            c.negm[r] = x;
+        }
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 sn[kb][r] -= shift;
-                sc[kb][r] = sr[kb][r] - shift;
+                sc[kb][r] -= shift;
             }
         exp_tile(sc, rsp);
     }
