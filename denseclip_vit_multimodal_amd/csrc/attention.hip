@@ -104,6 +104,18 @@ __device__ __forceinline__ f32x16 splat16(float v) {
 template <typename T> struct DsScale { static constexpr float v = 1.0f; };
 template <> struct DsScale<f16> { static constexpr float v = 16.0f; };
 
+// frag *= DsScale (a power of two: exact unless the value overflows, which the gradient scaling
+// of the callers rules out).  The CLS-split backward passes apply the fp16 dS pre-scale this way,
+// to the register-resident dO (dQ pass) / V (dK/dV pass) fragments once per workgroup, with the
+// matching -DsScale * delta seeds, instead of one multiply per dS element.
+template <typename T>
+__device__ __forceinline__ void frag_ds_scale(typename Mfma<T>::frag& f) {
+    if constexpr (DsScale<T>::v != 1.0f) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = (T)((float)f[j] * DsScale<T>::v);
+    }
+}
+
 // accumulator register r -> row offset within a 32x32 tile (column = lane & 31)
 __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
@@ -1307,7 +1319,7 @@ __device__ __forceinline__ void dq2_ds(Dq2Ctx<T, NW>& c, const char* Kt, int kb,
 #pragma unroll
         for (int db = 0; db < 2; ++db) kt[s][db] = tr_frag<T>(Kt, kb, s, db, c.lane);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) sacc[r] = __builtin_amdgcn_exp2f(sacc[r]) * pacc[r] * DsScale<T>::v;
+    for (int r = 0; r < 16; ++r) sacc[r] = __builtin_amdgcn_exp2f(sacc[r]) * pacc[r];  // pacc: DsScale (dP - delta)
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
         const frag sf = pack_frag<T>(sacc, s);
@@ -1406,10 +1418,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq2_kernel(const T* 
         delta[(int64_t)bh * N + q] = dl;
         // negated copies for the dK/dV pass, whose S / dP chains start from -L / -delta
         nstat[(int64_t)bh * N + q] = -L;
-        nstat[(int64_t)gridDim.x / nq * N + (int64_t)bh * N + q] = -dl;
+        nstat[(int64_t)gridDim.x / nq * N + (int64_t)bh * N + q] = -dl * DsScale<T>::v;
     }
     c.negL = -L;
-    c.negD = -dl;
+    c.negD = -dl * DsScale<T>::v;
     const float p0 = __builtin_amdgcn_exp2f(xhalf_sum(spart) - L);
     const float ds0 = p0 * (xhalf_sum(ppart) - dl) * DsScale<T>::v;
 #pragma unroll
@@ -1418,6 +1430,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq2_kernel(const T* 
         for (int g = 0; g < 4; ++g)
 #pragma unroll
             for (int e = 0; e < 4; ++e) c.dq[db][4 * g + e] = ds0 * (float)k0d[db][g][e];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) frag_ds_scale<T>(c.gf[s]);  // dP chains now give DsScale dP
 
     wait_vmcnt<2 * PIECES>();  // tiles 0 and 1 landed (tile 2 in flight)
     __builtin_amdgcn_s_barrier();
@@ -1857,7 +1871,7 @@ __device__ __forceinline__ void dkv2_step(Dkv2Ctx<T, NW>& c, int t) {
         for (int r = 0; r < 16; ++r) {
             const float p = __builtin_amdgcn_exp2f(sacc[r]);
             sacc[r] = p;
-            pacc[r] = p * pacc[r] * DsScale<T>::v;
+            pacc[r] = p * pacc[r];  // pacc: DsScale (dP - delta)
         }
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
@@ -1962,6 +1976,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv2_kernel(const T
                 c.dv[db][4 * g + e] = p0 * (float)g0d[db][g][e];
                 c.dk[db][4 * g + e] = ds0 * (float)q0d[db][g][e];
             }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) frag_ds_scale<T>(c.vf[s]);  // dP chains now give DsScale dP (seeds: -DsScale delta)
 
     for (int t = 0; t < c.nt; t += 4) {  // nt = (N-1)/64 is a multiple of 4: one loop exit
         dkv2_step<T, NW, 0>(c, t);
@@ -1984,7 +2000,7 @@ __device__ __forceinline__ void dkv_pack(f32x16& s, f32x16& p, typename Mfma<T>:
     for (int r = 0; r < 16; ++r) {
         const float e = __builtin_amdgcn_exp2f(s[r]);
         s[r] = e;
-        p[r] = e * p[r] * DsScale<T>::v;
+        p[r] = e * p[r];  // p: DsScale (dP - delta)
     }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -2166,6 +2182,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv5_kernel(const T* __restr
                 c.dv[db][4 * g + e] = p0 * (float)g0d[db][g][e];
                 c.dk[db][4 * g + e] = ds0 * (float)q0d[db][g][e];
             }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) frag_ds_scale<T>(c.vf[s]);  // dP chains now give DsScale dP (seeds: -DsScale delta)
 
     wait_vmcnt<2 * (X::PIECES + 1)>();  // slice 0 landed (slices 1, 2 in flight)
     __builtin_amdgcn_s_barrier();
