@@ -682,17 +682,18 @@ __device__ __forceinline__ void pers_epilogue(const f32x4 (&acc)[Cfg::NB][Cfg::M
                                               int mw, int nw, int l16, int lq, float alpha,
                                               const void* __restrict__ aux, int64_t ld_aux, void* __restrict__ C,
                                               int64_t ldc, void* __restrict__ C2, int64_t ldc2) {
+    // rows outer, column pairs inner (a row's segments stored back to back)
 #pragma unroll
-    for (int i = 0; i < Cfg::NB; i += 2) {
-        const f32x4 bv[2] = {pc.bv[i], pc.bv[i + 1]};
-        f32x4 sv[2];
-        if constexpr (EPI == DCLIP_EPI_STORE_SCALED) {
-            sv[0] = pc.sv[i];
-            sv[1] = pc.sv[i + 1];
-        }
+    for (int j = 0; j < Cfg::MB; ++j) {
+        const int64_t row = mw + 16 * j + l16;
 #pragma unroll
-        for (int j = 0; j < Cfg::MB; ++j) {
-            const int64_t row = mw + 16 * j + l16;
+        for (int i = 0; i < Cfg::NB; i += 2) {
+            const f32x4 bv[2] = {pc.bv[i], pc.bv[i + 1]};
+            f32x4 sv[2];
+            if constexpr (EPI == DCLIP_EPI_STORE_SCALED) {
+                sv[0] = pc.sv[i];
+                sv[1] = pc.sv[i + 1];
+            }
             const int col = nw + 16 * i + 4 * lq;
             f32x4 v[2] = {acc[i][j] * alpha + bv[0], acc[i + 1][j] * alpha + bv[1]};
             if constexpr (EPI == DCLIP_EPI_RESIDUAL || sizeof(OutT) == 4) {
