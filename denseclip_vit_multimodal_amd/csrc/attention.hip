@@ -391,6 +391,7 @@ struct Fwd2Ctx {
     uint32_t voffK[PIECES], voffV[PIECES];
     uint32_t ldb;  // row pitch (bytes)
     int nt, l32, h, lane, wave;
+    int rem;       // keys in the last tile (64 unless N - 1 is ragged)
     frag qf[4];
     f32x16 o[2];
     f32x16 negm;
@@ -416,6 +417,15 @@ __device__ __forceinline__ void fwd2_issue(Fwd2Ctx<T, NW>& c, int t, int slot) {
                                                  c.voffV[i], soff, 0, 0);
     }
 #endif
+}
+
+// scores of the keys past N in a ragged last tile to -inf (P = 0): key kb * 32 + acc_row(r, h)
+__device__ __forceinline__ void mask_tail(f32x16 (&s)[2], int rem, int h) {
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            if (kb * 32 + acc_row(r, h) >= rem) s[kb][r] = -INFINITY;
 }
 
 __device__ __forceinline__ float tile_rowmax2(const f32x16 (&sacc)[2]) {
@@ -514,6 +524,79 @@ __device__ __forceinline__ void fwd2_step(Fwd2Ctx<T, NW>& c, int t, f32x16 (&sc)
     }
 }
 
+// A ragged N - 1 (rem < 64 keys in the last tile): that tile is loaded ONCE, in the prologue,
+// into its own K / V slots past the rings (whole offsets in the per-lane voffset, rows past N at
+// 0xFFFFFFF0, past the descriptor's range, so they land as zeros), and processed after the loop
+// by fwd2_tail: S recomputed from the slot, the keys past N masked to -inf, the same reference
+// check, P V.  The steady-state steps stay exactly the non-ragged ones.
+template <typename T, int NW>
+__device__ __forceinline__ void fwd2_issue_tail(Fwd2Ctx<T, NW>& c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t base = (uint32_t)(1 + 64 * (c.nt - 1)) * c.ldb;
+#pragma unroll
+    for (int i = 0; i < Fwd2Ctx<T, NW>::PIECES; ++i) {
+        const int piece = c.wave + i * NW;
+        const bool ok = piece * 8 + (c.lane >> 3) < c.rem;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rs, LDS_PTR(c.smem + 8 * 8192 + piece * 1024), 16,
+                                                 ok ? c.voffK[i] + base : 0xFFFFFFF0u, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rs, LDS_PTR(c.smem + 9 * 8192 + piece * 1024), 16,
+                                                 ok ? c.voffV[i] + base : 0xFFFFFFF0u, 0, 0, 0);
+    }
+#endif
+}
+
+template <typename T, int NW>
+__device__ __forceinline__ void fwd2_tail(Fwd2Ctx<T, NW>& c) {
+    typedef typename Mfma<T>::frag frag;
+    constexpr float LIM = 4096.0f;
+    const char* Kt = c.smem + 8 * 8192;
+    const char* Vt = c.smem + 9 * 8192;
+    f32x16 sc[2];
+    s_tile<T>(sc, Kt, c.qf, c.negm, c.l32, c.h);
+    mask_tail(sc, c.rem, c.h);
+    float rsp[4];
+    exp_tile(sc, rsp);
+    const float tot = (rsp[0] + rsp[1]) + (rsp[2] + rsp[3]);
+    if (__any(!(tot <= LIM))) {
+        s_tile<T>(sc, Kt, c.qf, zero16(), c.l32, c.h);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sc[kb][r] -= c.m;
+        mask_tail(sc, c.rem, c.h);
+        const float shift = fmaxf(tile_rowmax2(sc), 0.f);
+        const float alpha = __builtin_amdgcn_exp2f(-shift);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c.l4[j] *= alpha;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) c.o[db][r] *= alpha;
+        c.m += shift;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sc[kb][r] -= shift;
+        exp_tile(sc, rsp);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c.l4[j] += rsp[j];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+        frag vf[2][2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int db = 0; db < 2; ++db) vf[s][db] = tr_frag<T>(Vt, kb, s, db, c.lane);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const frag pf = pack_frag<T>(sc[kb], s);
+#pragma unroll
+            for (int db = 0; db < 2; ++db) c.o[db] = Mfma<T>::mma(vf[s][db], pf, c.o[db]);
+        }
+    }
+}
+
 // 16-B stores of one output row held as the O^T accumulator layout (T21): lane h of a row
 // holds columns 8G + 4h .. 8G + 4h + 3 of every 8-column group G; one permlane32 swap per
 // dword pairs groups (G, G+1) into 16 contiguous bytes per lane.
@@ -549,24 +632,26 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd2_kernel(const T* __r
                                                                     float* __restrict__ lse, int N, int H) {
     constexpr int QB = 32 * NW;
     typedef typename Mfma<T>::frag frag;
-    __shared__ __attribute__((aligned(16))) char smem[8 * 8192];
+    __shared__ __attribute__((aligned(16))) char smem[10 * 8192];  // K ring, V ring, ragged-tail K / V
     Fwd2Ctx<T, NW> c;
     c.smem = smem;
     c.lane = threadIdx.x & 63;
     c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (scalar) for the DMA
     c.h = c.lane >> 5;
     c.l32 = c.lane & 31;
-    const int nq = (N - 1) / QB;
+    const int nq = (N - 1 + QB - 1) / QB;  // the last query block partial when N - 1 is ragged
     const int tile = xcd_remap(blockIdx.x, gridDim.x);
     const int qblk = tile % nq, bh = tile / nq, b = bh / H, hd = bh % H;
     const int C = H * HD;
     const int64_t ld = 3 * (int64_t)C;
     const T* Bb = qkv + (int64_t)b * N * ld;  // this batch's rows
     c.ldb = (uint32_t)(ld * sizeof(T));
-    c.nt = (N - 1) / 64;
+    c.nt = (N - 1 + 63) / 64;
+    c.rem = N - 1 - 64 * (c.nt - 1);
     // queries first: their register loads must not queue behind the DMA in vmcnt order
     const int q = 1 + qblk * QB + c.wave * 32 + c.l32;
-    const T* Qrow = Bb + (int64_t)q * ld + hd * HD;
+    const bool qok = q < N;  // rows past N (ragged last block) compute on row N - 1, store nothing
+    const T* Qrow = Bb + (int64_t)(qok ? q : N - 1) * ld + hd * HD;
 #pragma unroll
     for (int s = 0; s < 4; ++s) c.qf[s] = *(const frag*)(Qrow + (2 * s + c.h) * 8);
     const T* K0 = Bb + C + hd * HD;  // key 0 (CLS)
@@ -589,6 +674,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd2_kernel(const T* __r
         c.voffK[i] = base + (uint32_t)((C + hd * HD) * sizeof(T));
         c.voffV[i] = base + (uint32_t)((2 * C + hd * HD) * sizeof(T));
     }
+    const bool ragged = c.rem < 64;
+    if (ragged) fwd2_issue_tail<T, NW>(c);  // oldest loads: every later wait covers them
+    const int ntf = ragged ? c.nt - 1 : c.nt;  // full tiles, swept by the steady-state steps
+    c.nt = ntf;  // the steps' issue clamp and loop bound see the full tiles only
     fwd2_issue<T, NW>(c, 0, 0);
     fwd2_issue<T, NW>(c, c.nt > 1 ? 1 : 0, 1);
     fwd2_issue<T, NW>(c, c.nt > 2 ? 2 : c.nt - 1, 2);
@@ -633,12 +722,15 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd2_kernel(const T* __r
         if (t >= c.nt) break;
         fwd2_step<T, NW, 3>(c, t++, sB, sA);
     }
+    if (ragged) fwd2_tail<T, NW>(c);
     __builtin_amdgcn_s_setprio(0);
     wait_vmcnt<0>();  // no LDS-DMA may still be landing when the workgroup retires
 
     const float lt = xhalf_sum((c.l4[0] + c.l4[1]) + (c.l4[2] + c.l4[3]));
-    store_row_t21<T>(out + ((int64_t)b * N + q) * C + hd * HD, c.o, 1.0f / lt, c.h);
-    if (c.h == 0) lse[(int64_t)bh * N + q] = c.m + __log2f(lt);
+    if (qok) {  // both half-waves of a row agree (the swap inside pairs lanes l, l ^ 32)
+        store_row_t21<T>(out + ((int64_t)b * N + q) * C + hd * HD, c.o, 1.0f / lt, c.h);
+        if (c.h == 0) lse[(int64_t)bh * N + q] = c.m + __log2f(lt);
+    }
 }
 
 // ---------------------------------------------------------------------------- pipelined variant
@@ -1270,15 +1362,31 @@ struct Dq2Ctx {
     uint32_t voffK[PIECES], voffV[PIECES];
     uint32_t ldb;
     int nt, lane, l32, h, wave;
+    int rem;  // keys in the last tile (64 unless N - 1 is ragged)
     frag qf[4], gf[4];
     float negL, negD;
     f32x16 dq[2];
 };
 
+// a ragged last tile as in fwd2_issue (keys past N land as zero rows: their dS multiplies a zero
+// K row, so they add nothing to dQ)
 template <typename T, int NW>
 __device__ __forceinline__ void dq2_issue(Dq2Ctx<T, NW>& c, int t, int slot) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const uint32_t soff = (uint32_t)(1 + 64 * t) * c.ldb;
+    const bool ragged = t == c.nt - 1 && c.rem < 64;  // wave-uniform
+    if (__builtin_expect(ragged, 0)) {
+#pragma unroll
+        for (int i = 0; i < Dq2Ctx<T, NW>::PIECES; ++i) {
+            const int piece = c.wave + NW * i;
+            const bool ok = piece * 8 + (c.lane >> 3) < c.rem;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rs, LDS_PTR(c.smem + slot * 16384 + piece * 1024), 16,
+                                                     ok ? c.voffK[i] + soff : 0xFFFFFFF0u, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rs, LDS_PTR(c.smem + slot * 16384 + 8192 + piece * 1024), 16,
+                                                     ok ? c.voffV[i] + soff : 0xFFFFFFF0u, 0, 0, 0);
+        }
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < Dq2Ctx<T, NW>::PIECES; ++i) {
         const int piece = c.wave + NW * i;
@@ -1361,23 +1469,26 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq2_kernel(const T* 
     c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (scalar) for the DMA
     c.h = c.lane >> 5;
     c.l32 = c.lane & 31;
-    const int nq = (N - 1) / QB;
+    const int nq = (N - 1 + QB - 1) / QB;  // the last query block partial when N - 1 is ragged
     const int tile = xcd_remap(blockIdx.x, gridDim.x);
     const int qblk = tile % nq, bh = tile / nq, b = bh / H, hd = bh % H;
     const int C = H * HD;
     const int64_t ld = 3 * (int64_t)C;
     const T* Bb = qkv + (int64_t)b * N * ld;
     c.ldb = (uint32_t)(ld * sizeof(T));
-    c.nt = (N - 1) / 64;
+    c.nt = (N - 1 + 63) / 64;
+    c.rem = N - 1 - 64 * (c.nt - 1);
     const int q = 1 + qblk * QB + c.wave * 32 + c.l32;
+    const bool qok = q < N;  // rows past N compute on row N - 1 and store nothing
+    const int qc = qok ? q : N - 1;
     // register loads first (their waits must not queue behind the DMA)
     const T* dOb = dout + (int64_t)b * N * C + hd * HD;
-    const T* Orow = o + ((int64_t)b * N + q) * C + hd * HD;
+    const T* Orow = o + ((int64_t)b * N + qc) * C + hd * HD;
     frag of[4], k0[4], v0[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-        c.qf[s] = *(const frag*)(Bb + (int64_t)q * ld + hd * HD + (2 * s + c.h) * 8);
-        c.gf[s] = *(const frag*)(dOb + (int64_t)q * C + (2 * s + c.h) * 8);
+        c.qf[s] = *(const frag*)(Bb + (int64_t)qc * ld + hd * HD + (2 * s + c.h) * 8);
+        c.gf[s] = *(const frag*)(dOb + (int64_t)qc * C + (2 * s + c.h) * 8);
         of[s] = *(const frag*)(Orow + (2 * s + c.h) * 8);
         k0[s] = *(const frag*)(Bb + C + hd * HD + (2 * s + c.h) * 8);
         v0[s] = *(const frag*)(Bb + 2 * C + hd * HD + (2 * s + c.h) * 8);
@@ -1388,7 +1499,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq2_kernel(const T* 
     for (int db = 0; db < 2; ++db)
 #pragma unroll
         for (int g = 0; g < 4; ++g) k0d[db][g] = *(const t4*)(Bb + C + hd * HD + db * 32 + 8 * g + 4 * c.h);
-    const float L = lse[(int64_t)bh * N + q];
+    const float L = lse[(int64_t)bh * N + qc];
 
     c.rs = make_rsrc(Bb, (uint32_t)N * c.ldb);
 #pragma unroll
@@ -1414,7 +1525,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq2_kernel(const T* 
             ppart += (float)c.gf[s][j] * (float)v0[s][j];
         }
     const float dl = xhalf_sum(dpart);
-    if (c.h == 0) {
+    if (c.h == 0 && qok) {
         delta[(int64_t)bh * N + q] = dl;
         // negated copies for the dK/dV pass, whose S / dP chains start from -L / -delta
         nstat[(int64_t)bh * N + q] = -L;
@@ -1437,14 +1548,20 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq2_kernel(const T* 
     __builtin_amdgcn_s_barrier();
     f32x16 sA, pA, sB, pB;
     dq2_sdp<T, NW>(c, smem, 0, sA, pA);
-    for (int t = 0; t < c.nt; t += 4) {  // nt = (N-1)/64 is a multiple of 4: one loop exit
+    // unrolled by four (ring slots are immediates), then up to three single steps for a ragged
+    // tile count (a loop with an exit after every step spilled ~90 VGPRs to scratch)
+    int t = 0;
+    for (; t + 4 <= c.nt; t += 4) {
         dq2_step<T, NW, 0>(c, t, sA, pA, sB, pB);
         dq2_step<T, NW, 1>(c, t + 1, sA, pA, sB, pB);
         dq2_step<T, NW, 2>(c, t + 2, sA, pA, sB, pB);
         dq2_step<T, NW, 3>(c, t + 3, sA, pA, sB, pB);
     }
+    if (t < c.nt) dq2_step<T, NW, 0>(c, t++, sA, pA, sB, pB);
+    if (t < c.nt) dq2_step<T, NW, 1>(c, t++, sA, pA, sB, pB);
+    if (t < c.nt) dq2_step<T, NW, 2>(c, t++, sA, pA, sB, pB);
     wait_vmcnt<0>();
-    store_row_t21<T>(dqkv + ((int64_t)b * N + q) * ld + hd * HD, c.dq, scale / DsScale<T>::v, c.h);
+    if (qok) store_row_t21<T>(dqkv + ((int64_t)b * N + q) * ld + hd * HD, c.dq, scale / DsScale<T>::v, c.h);
 }
 
 // ---------------------------------------------------------------------------- row 0 of the backward
@@ -1794,6 +1911,7 @@ struct Dkv2Ctx {
     uint32_t voff[PIECES];
     uint32_t ldq, ldg, ldmine;  // row pitches (bytes)
     int nt, lane, l32, h, wave;
+    int rem;  // queries in the last slice (64 unless N - 1 is ragged)
     frag kf[4], vf[4];
     f32x16 dk[2], dv[2];
 };
@@ -1806,19 +1924,37 @@ __device__ __forceinline__ void dkv2_issue(Dkv2Ctx<T, NW>& c, int t, int slot) {
     const int r0 = 1 + 64 * t;
     // a wave's pieces are all Q (waves 0 .. NW/2-1) or all dO: its source resource and row
     // pitch were chosen once at setup, so the issue is one straight-line block (no branches
-    // splitting the step's schedule)
+    // splitting the step's schedule).  A ragged last slice (rem < 64 queries) goes with the
+    // whole offset in the voffset and the rows past N at 0xFFFFFFF0 (zeros, as in fwd2_issue):
+    // a zero Q / dO row and zero statistics give dS = 0 and zero dV / dK terms.
+    const bool ragged = t == c.nt - 1 && c.rem < 64;  // wave-uniform
     const uint32_t soff = (uint32_t)r0 * c.ldmine;
+    const int part = c.wave % (NW / 2);
+    const bool is_l = c.wave < NW / 2;
+    const uint32_t idx = (uint32_t)(part * X::SPW + c.lane);  // this lane's statistic in the slice
+    if (__builtin_expect(ragged, 0)) {
+#pragma unroll
+        for (int i = 0; i < X::PIECES; ++i) {
+            const int piece = c.wave * X::PIECES + i;
+            const bool ok = (piece & 7) * 8 + (c.lane >> 3) < c.rem;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rmine, LDS_PTR(base + piece * 1024), 16,
+                                                     ok ? c.voff[i] + soff : 0xFFFFFFF0u, 0, 0, 0);
+        }
+        if (c.lane < X::SPW)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(is_l ? c.rl : c.rd,
+                                                     LDS_PTR(base + 16384 + (is_l ? 0 : 256) + part * X::SPW * 4), 4,
+                                                     (int)idx < c.rem ? (idx + (uint32_t)r0) * 4 : 0xFFFFFFF0u, 0, 0, 0);
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < X::PIECES; ++i)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rmine, LDS_PTR(base + (c.wave * X::PIECES + i) * 1024), 16,
                                                  c.voff[i], soff, 0, 0);
     // statistics: waves 0 .. NW/2-1 load L, the others delta, SPW values each
-    const int part = c.wave % (NW / 2);
-    const bool is_l = c.wave < NW / 2;
     if (c.lane < X::SPW)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(is_l ? c.rl : c.rd,
                                                  LDS_PTR(base + 16384 + (is_l ? 0 : 256) + part * X::SPW * 4), 4,
-                                                 (uint32_t)(part * X::SPW + c.lane) * 4, (uint32_t)r0 * 4, 0, 0);
+                                                 idx * 4, (uint32_t)r0 * 4, 0, 0);
 #endif
 }
 
@@ -1914,7 +2050,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv2_kernel(const T
     const T* dOb = dout + (int64_t)b * N * C;
     c.ldq = (uint32_t)(ld * sizeof(T));
     c.ldg = (uint32_t)(C * sizeof(T));
-    c.nt = (N - 1) / 64;
+    c.nt = (N - 1) / 64;  // launched for N - 1 a multiple of 256 only
+    c.rem = 64;
     const int key = 1 + kblk * KB + c.wave * 32 + c.l32;
     // register loads first
     frag q0[4], g0[4];
@@ -2114,7 +2251,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv5_kernel(const T* __restr
     c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     c.h = c.lane >> 5;
     c.l32 = c.lane & 31;
-    const int nkb = (N - 1) / KB;
+    const int nkb = (N - 1 + KB - 1) / KB;  // the last key block partial when N - 1 is ragged
     const int tile = xcd_remap(blockIdx.x, gridDim.x);
     const int kblk = tile % nkb, bh = tile / nkb, b = bh / H, hd = bh % H;
     const int C = H * HD;
@@ -2123,13 +2260,16 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv5_kernel(const T* __restr
     const T* dOb = dout + (int64_t)b * N * C;
     c.ldq = (uint32_t)(ld * sizeof(T));
     c.ldg = (uint32_t)(C * sizeof(T));
-    c.nt = (N - 1) / 64;
+    c.nt = (N - 1 + 63) / 64;
+    c.rem = N - 1 - 64 * (c.nt - 1);
     const int key = 1 + kblk * KB + c.wave * 32 + c.l32;
+    const bool kok = key < N;  // keys past N compute on key N - 1 and store nothing
+    const int kc = kok ? key : N - 1;
     frag q0[4], g0[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-        c.kf[s] = *(const frag*)(Bb + (int64_t)key * ld + C + hd * HD + (2 * s + c.h) * 8);
-        c.vf[s] = *(const frag*)(Bb + (int64_t)key * ld + 2 * C + hd * HD + (2 * s + c.h) * 8);
+        c.kf[s] = *(const frag*)(Bb + (int64_t)kc * ld + C + hd * HD + (2 * s + c.h) * 8);
+        c.vf[s] = *(const frag*)(Bb + (int64_t)kc * ld + 2 * C + hd * HD + (2 * s + c.h) * 8);
         q0[s] = *(const frag*)(Bb + hd * HD + (2 * s + c.h) * 8);
         g0[s] = *(const frag*)(dOb + hd * HD + (2 * s + c.h) * 8);
     }
@@ -2189,16 +2329,22 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv5_kernel(const T* __restr
     __builtin_amdgcn_s_barrier();
     f32x16 sA, pA;
     dkv5_sdp<T>(c, smem, 0, sA, pA);
-    for (int t = 0; t < c.nt; t += 4) {
+    int t = 0;  // unrolled by four, then up to three single steps (see attn_bwd_dq2_kernel)
+    for (; t + 4 <= c.nt; t += 4) {
         dkv5_step<T, 0>(c, t, sA, pA);
         dkv5_step<T, 1>(c, t + 1, sA, pA);
         dkv5_step<T, 2>(c, t + 2, sA, pA);
         dkv5_step<T, 3>(c, t + 3, sA, pA);
     }
+    if (t < c.nt) dkv5_step<T, 0>(c, t++, sA, pA);
+    if (t < c.nt) dkv5_step<T, 1>(c, t++, sA, pA);
+    if (t < c.nt) dkv5_step<T, 2>(c, t++, sA, pA);
     wait_vmcnt<0>();
-    T* rk = dqkv + ((int64_t)b * N + key) * ld + C + hd * HD;
-    store_row_t21<T>(rk, c.dk, dk_scale / DsScale<T>::v, c.h);
-    store_row_t21<T>(rk + C, c.dv, 1.0f, c.h);
+    if (kok) {  // both half-waves of a key agree
+        T* rk = dqkv + ((int64_t)b * N + key) * ld + C + hd * HD;
+        store_row_t21<T>(rk, c.dk, dk_scale / DsScale<T>::v, c.h);
+        store_row_t21<T>(rk + C, c.dv, 1.0f, c.h);
+    }
 }
 
 // ---------------------------------------------------------------------------- launch
@@ -2208,15 +2354,15 @@ void fwd_launch_nw(const void* qkv, void* o, float* lse, int B, int N, int H, hi
     attn_fwd_kernel<T, NW><<<grid, 64 * NW, 0, st>>>((const T*)qkv, (T*)o, lse, N, H);
 }
 
-// CLS-split path (attn_fwd2_kernel) when N - 1 is a multiple of the query block
+// CLS-split path (attn_fwd2_kernel) for N - 1 >= the query block (ragged N - 1 included)
 template <typename T, int NW>
 bool fwd2_launch_nw(const void* qkv, void* o, float* lse, int B, int N, int H, hipStream_t st) {
     constexpr int QB = 32 * NW;
-    if (N < 1 + QB || (N - 1) % QB != 0) return false;
+    if (N < 1 + QB) return false;  // any N - 1 >= QB (a ragged tail: masked last key tile, partial last block)
     const int nsplit = (N + R0_CHUNK - 1) / R0_CHUNK;
     attn_row0_part_kernel<T><<<B * H * nsplit, 256, 0, st>>>((const T*)qkv, (T*)o, N, H, nsplit);
     attn_row0_merge_kernel<T><<<B * H, 64, 0, st>>>((T*)o, lse, N, H, nsplit);
-    const dim3 grid(B * H * ((N - 1) / QB));
+    const dim3 grid(B * H * ((N - 1 + QB - 1) / QB));
     attn_fwd2_kernel<T, NW><<<grid, 64 * NW, 0, st>>>((const T*)qkv, (T*)o, lse, N, H);
     return true;
 }
@@ -2246,11 +2392,16 @@ void fwd_launch(const void* qkv, void* o, float* lse, int B, int N, int H, hipSt
     else fwd_launch_nw<T, 8>(qkv, o, lse, B, N, H, st);
 }
 
-// CLS-split backward when N - 1 is a multiple of 256 (dQ blocks of 256, dK/dV blocks of 128)
+// CLS-split backward for N >= 257 (dQ blocks of 256, dK/dV blocks of 128; a ragged N - 1 takes
+// partial last blocks and zero-filled tails)
 template <typename T>
 bool bwd2_launch(const void* qkv, const void* o, const void* dout, const float* lse, float* delta, void* dqkv, int B,
                  int N, int H, float scale, hipStream_t st) {
-    if (N < 257 || (N - 1) % 256 != 0 || dclip_option(DCLIP_OPT_ATTN_BWD_KERNEL) == 1) return false;
+    if (N < 257 || dclip_option(DCLIP_OPT_ATTN_BWD_KERNEL) == 1) return false;
+    // a ragged N - 1 (partial last query / key blocks, masked tails) in the default passes only
+    const bool ragged = (N - 1) % 256 != 0;
+    if (ragged && (dclip_option(DCLIP_OPT_ATTN_DQ_WAVES) == 4 || dclip_option(DCLIP_OPT_ATTN_BWD_BLOCK) != 0))
+        return false;
     const int nsplit = (N + R0_CHUNK - 1) / R0_CHUNK;
     float* ws0 = delta + (int64_t)B * H * N;
     float* nstat = ws0 + (int64_t)B * H * ((N + 63) / 64) * 192;  // [-lse | -delta], B*H*N each
@@ -2262,13 +2413,13 @@ bool bwd2_launch(const void* qkv, const void* o, const void* dout, const float* 
         attn_bwd_dq2_kernel<T, 4><<<B * H * ((N - 1) / 128), 256, 0, st>>>(
             (const T*)qkv, (const T*)o, (const T*)dout, lse, delta, nstat, (T*)dqkv, N, H, scale);
     else
-        attn_bwd_dq2_kernel<T, 8><<<B * H * ((N - 1) / 256), 512, 0, st>>>(
+        attn_bwd_dq2_kernel<T, 8><<<B * H * ((N - 1 + 255) / 256), 512, 0, st>>>(
             (const T*)qkv, (const T*)o, (const T*)dout, lse, delta, nstat, (T*)dqkv, N, H, scale);
     attn_bwd_row0_dkdv_part<T><<<B * H * nsplit, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, ws0, N, H,
                                                               nsplit);
     attn_bwd_row0_dkdv_merge<T><<<B * H, 64, 0, st>>>(ws0, (T*)dqkv, N, H, nsplit, 1.0f / LOG2E);
     if (dclip_option(DCLIP_OPT_ATTN_BWD_BLOCK) == 0)  // default: pipelined, 32 keys per wave, 2 waves per SIMD
-        attn_bwd_dkdv5_kernel<T><<<B * H * ((N - 1) / 128), 256, 0, st>>>(
+        attn_bwd_dkdv5_kernel<T><<<B * H * ((N - 1 + 127) / 128), 256, 0, st>>>(
             (const T*)qkv, (const T*)dout, lse, delta, nstat, nstat + (int64_t)B * H * N, (T*)dqkv, N, H, 1.0f / LOG2E);
     else if (dclip_option(DCLIP_OPT_ATTN_DKDV_WAVES) == 8)  // 256 keys per workgroup (one Q / dO slice per 256 keys)
         attn_bwd_dkdv2_kernel<T, 8><<<B * H * ((N - 1) / 256), 512, 0, st>>>(

@@ -440,6 +440,26 @@ def _attn_bwd_check(B, H, N, dt, spike=None):
     return errs
 
 
+@pytest.mark.parametrize("B,H,N", [(2, 2, 258), (2, 2, 290), (2, 3, 803), (3, 2, 1345), (1, 1, 10659)])
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+def test_attention_cls_split_ragged(B, H, N, dt):
+    """CLS-split passes at a ragged N - 1 (not a multiple of 64 / 256): the last key tile masked
+    (forward) or zero-filled (backward), partial last query / key blocks.  N = 10659 is ViT-L/14
+    at 1024x2048 (1 + 73 * 146, BASELINE config [3]); forward, lse and every gradient against fp32
+    autograd, the CLS row included."""
+    O = ops()
+    C = 64 * H
+    qkv, qref = prescale((torch.randn(B * N, 3 * C, device=DEV) * 1.5).to(dt), H)
+    o, lse = O.attn_fwd(qkv, B, N, H, 64 ** -0.5)
+    ref = attn_ref(qref, B, N, H)
+    assert rel_err(o.float(), ref) < TOL[dt]
+    q, k, _ = qref.view(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    lref = torch.logsumexp((q @ k.transpose(-1, -2)) * 64 ** -0.5, -1) / math.log(2)
+    assert (lse.view(B, H, N) - lref).abs().max() < 1e-2
+    errs = _attn_bwd_check(B, H, N, dt)
+    assert max(errs) < 4 * TOL[dt], errs
+
+
 @pytest.mark.parametrize("bwd_kernel", [0, 1], indirect=True)
 @pytest.mark.parametrize("N", [257, 513, 2049])
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
