@@ -257,9 +257,11 @@ def main():
             cpu = {"value": None, "error": repr(e)[:300]}
 
     if rank == 0:
-        # N = 1 + 256k runs the CLS-split attention kernels (attention.hip bwd2_launch / fwd2)
-        cls_split = N >= 257 and (N - 1) % 256 == 0
-        rf_fwd = {"kernel": ("attn_fp8_kernel (+ amax / pack%s)" % (" / row-0 pass" if cls_split else "")
+        # N >= 257 runs the CLS-split attention kernels (attention.hip bwd2_launch / fwd2, a ragged
+        # N - 1 included); the fp8 forward splits CLS for N = 1 + 256k only
+        cls_split = N >= 257
+        fp8_split = N >= 257 and (N - 1) % 256 == 0
+        rf_fwd = {"kernel": ("attn_fp8_kernel (+ amax / pack%s)" % (" / row-0 pass" if fp8_split else "")
                              if args.attn_fp8 else
                              "attn_fwd2_kernel (+ row-0 pass)" if cls_split else "attn_fwd_kernel"),
                   "bound": "mfma",
