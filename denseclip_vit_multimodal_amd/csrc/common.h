@@ -88,29 +88,12 @@ __device__ __forceinline__ float frag_sum8(f16x8 v, float c) {
 
 // ----------------------------------------------------------------------------- MFMA
 template <typename T> struct Mfma;
-#ifdef DCLIP_MFMA16_DIAG
-// timing diagnostic only (libdclip_diag.so, WRONG results): each 32x32x16 replaced by two
-// 16x16x32 on the same operands (same operand bytes, same matrix-pipe cycles) so that a
-// kernel's instruction mix stays and only the MFMA shape changes
-template <> struct Mfma<bf16> {
-    typedef bf16x8 frag;
-    static __device__ __forceinline__ f32x16 mma(frag a, frag b, f32x16 c) {
-        f32x4 c0 = {c[0], c[1], c[2], c[3]}, c1 = {c[4], c[5], c[6], c[7]};
-        c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c0, 0, 0, 0);
-        c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, c1, 0, 0, 0);
-        c[0] = c0[0]; c[1] = c0[1]; c[2] = c0[2]; c[3] = c0[3];
-        c[4] = c1[0]; c[5] = c1[1]; c[6] = c1[2]; c[7] = c1[3];
-        return c;
-    }
-};
-#else
 template <> struct Mfma<bf16> {
     typedef bf16x8 frag;
     static __device__ __forceinline__ f32x16 mma(frag a, frag b, f32x16 c) {
         return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
     }
 };
-#endif
 template <> struct Mfma<f16> {
     typedef f16x8 frag;
     static __device__ __forceinline__ f32x16 mma(frag a, frag b, f32x16 c) {

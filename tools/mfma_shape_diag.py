@@ -1,9 +1,9 @@
-"""Timing diagnostic: attention fwd / bwd launches at the bench shape (B=8, N=8193, H=12, bf16)
-with the library given on the command line (libdclip.so or the WRONG-results
-libdclip_diag.so whose 32x32x16 MFMAs are replaced by pairs of 16x16x32), per-launch HIP-event
-times.  Run the two libraries in separate processes, alternately.
+"""A/B timing of the attention kernels: fwd / bwd launches at the bench shape (B=8, N=8193, H=12)
+through the C ABI of the library given on the command line, per-launch HIP-event medians and a
+bitwise fingerprint of dQKV (two builds that should agree bit for bit print the same number).
+Run the libraries in separate processes, alternately (tools/gpu_r04j.sh).
 
-  python tools/mfma_shape_diag.py path/to/lib.so [reps]
+  python tools/mfma_shape_diag.py path/to/lib.so [reps] [dtype code: 2 bf16 (default), 1 fp16]
 """
 import ctypes
 import sys
