@@ -556,6 +556,16 @@ def test_transpose_colsum_pad():
     assert rel_err(cs, x.float().sum(0)) < 1e-6
 
 
+@pytest.mark.parametrize("shape", [(64, 64), (768, 3072), (2304, 768), (3072, 768), (192, 72)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_transpose_f32_weights(shape, dt):
+    """fp32 -> 16-bit transposed weight copies: the 64-multiple fast kernel (and the generic one
+    for (192, 72)) round exactly as torch's cast."""
+    O = ops()
+    x = torch.randn(*shape, device=DEV) * 3.0
+    assert torch.equal(O.transpose2d(x, dt), x.t().to(dt))
+
+
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("B,HW,C,K,tok", [(2, 333, 512, 19, False), (3, 8192, 512, 19, True), (1, 40, 1024, 32, True),
                                           (2, 31, 64, 1, False)])
