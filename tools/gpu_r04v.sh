@@ -1,6 +1,6 @@
 #!/bin/bash
 # final binary: the whole GPU suite, smoke(), and the default bench invocation
-OUT=gpurun_out/r04v; mkdir -p $OUT
+OUT=gpurun_out/${TAG:-r04v}; mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -30 $OUT/pytest_gpu.log; exit 1; }
 tail -2 $OUT/pytest_gpu.log
