@@ -11,8 +11,11 @@ fine-tune) trains the ViT too, so its backward kernels run; mode R is the refere
 trainer's regime (backbone + text encoder frozen, train_denseclip.py:1040-1044) and is
 measured as well and reported beside the headline.
 
-rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (the fused attention
-forward), timed with HIP events on its launch stream over the timed region;
+rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel of a train step (the
+attention backward: dQ + dK/dV passes; `roofline_attn_fwd` for the forward), timed with HIP
+events on its launch stream over the timed region; `fp16` repeats the mode-F step with fp32
+images and the fp16 compute dtype (the reference trainer's input, the dtype that holds the
+north-star 1e-3: the HIP neck / heads run in fp16 with device-side gradient scales);
 `cpu_baseline` times the CPU oracle (the reference algorithm restated in torch fp32,
 including the same SDPA op the reference calls) on a bounded sample on the host cores.
 """
@@ -53,6 +56,7 @@ def parse():
     ap.add_argument("--width", type=int, default=2048)
     ap.add_argument("--mode", choices=["F", "R"], default="F")
     ap.add_argument("--no-mode-r", action="store_true", help="skip the extra mode-R measurement")
+    ap.add_argument("--no-fp16", action="store_true", help="skip the extra fp16 (fp32-image) mode-F measurement")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--arch", choices=sorted(ARCHS), default="vitb16",
@@ -188,9 +192,11 @@ def main():
     img_dtype = torch.float16 if args.dtype == "fp16" else torch.bfloat16
     batch = synth_batch(B, H, W, dev, rank, image_dtype=img_dtype)
 
-    def setup(mode):
+    def setup(mode, compute_dtype=None):
         model = make_model(dev, mode, args.arch)
         model.backbone.attn_fp8 = args.attn_fp8
+        if compute_dtype is not None:
+            model.backbone.compute_dtype = compute_dtype
         if args.infer:  # replicas: no gradients, no collective
             model.eval()
             return model, None
@@ -247,6 +253,28 @@ def main():
         mode_r = {"value": round(world * B * max(3, args.steps // 2) / dtr, 4), "unit": "images/sec",
                   "ms_per_step": round(dtr / max(3, args.steps // 2) * 1e3, 2),
                   "what": "reference regime: backbone + text encoder frozen (train_denseclip.py:1040-1044)"}
+
+    fp16 = None
+    if args.mode == "F" and not args.no_fp16 and not args.infer and args.dtype == "bf16" and not args.attn_fp8:
+        # the 1e-3 dtype: fp32 images (what the reference trainer feeds), fp16 compute
+        del model, opt
+        torch.cuda.empty_cache()
+        model, opt = setup("F", torch.float16)
+        batch16 = synth_batch(B, H, W, dev, rank, image_dtype=torch.float32)
+        k16 = max(3, args.steps // 2)
+        dt16, s16, loss16 = timed(model, opt, batch16, k16, 2, silog, world, dist_on)
+        del batch16
+
+        def rf(key, flops):
+            n, _, mean = s16.get(key, (0, 0.0, float("nan")))
+            if not n:
+                return None
+            a = flops / (mean * 1e-3) / 1e12
+            return {"achieved": round(a, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(a / PEAK_BF16_TFLOPS, 4), "ms_per_launch": round(mean, 4), "launches": n}
+        fp16 = {"value": round(world * B * k16 / dt16, 4), "unit": "images/sec", "ms_per_step": round(dt16 / k16 * 1e3, 2),
+                "what": "mode F with fp32 images and fp16 compute (neck / heads on the HIP kernels in fp16)",
+                "loss": round(loss16, 4), "roofline_attn_bwd": rf("attn_bwd", fl_b), "roofline_attn_fwd": rf("attn_fwd", fl)}
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline == "auto" and args.arch == "vitb16" and not args.infer:
@@ -307,6 +335,7 @@ def main():
                            "frac": round(value / world * model_fl / 1e12 / PEAK_BF16_TFLOPS, 4)} if model_fl else None,
             "kernels": kernels,
             "mode_R": mode_r,
+            "fp16": fp16,
             "cpu_baseline": cpu,
             "loss": round(loss, 4),
         }

@@ -24,6 +24,12 @@ def load():
         raise RuntimeError(f"libdclip_torch.so not found at {LIB_PATH}: build it with "
                            "`make -C denseclip_vit_multimodal_amd/csrc` (the HIP path has no CPU fallback)")
     from . import _native
+    # libdclip_torch.so binds the libdclip.so next to it (rpath $ORIGIN): a DCLIP_LIB pointing at
+    # another build would be configured (dclip_set_option) while every op ran the other one
+    bound = os.path.realpath(os.path.join(os.path.dirname(LIB_PATH), "libdclip.so"))
+    if os.path.realpath(_native.LIB_PATH) != bound:
+        raise RuntimeError(f"DCLIP_LIB ({_native.LIB_PATH}) is not the libdclip.so that {LIB_PATH} binds ({bound}); "
+                           "build a matching adapter and point DCLIP_TORCH_LIB at it")
     _native.load()  # same libdclip.so instance (DCLIP_OPTIONS are applied there)
     torch.ops.load_library(LIB_PATH)
     _register_fakes()

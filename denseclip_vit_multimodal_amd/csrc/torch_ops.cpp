@@ -40,6 +40,14 @@ void check_opt(const c10::optional<Tensor>& t, const char* what) {
     if (t.has_value() && t->defined()) check_gpu(*t, what);
 }
 
+// an optional per-column / per-channel f32 vector the kernels index [0, n): GPU, contiguous, f32, n elements
+void check_vec(const c10::optional<Tensor>& t, int64_t n, const char* what) {
+    if (!t.has_value() || !t->defined()) return;
+    check_gpu(*t, what);
+    TORCH_CHECK(t->scalar_type() == at::kFloat, "dclip: ", what, " must be float32 (got ", t->scalar_type(), ")");
+    TORCH_CHECK(t->numel() == n, "dclip: ", what, " must have ", n, " elements (got ", t->numel(), ")");
+}
+
 template <typename T>
 T* ptr(const Tensor& t) { return t.defined() ? (T*)t.data_ptr() : nullptr; }
 
@@ -66,8 +74,8 @@ at::TensorOptions like(const Tensor& t, at::ScalarType dt) { return t.options().
 std::tuple<Tensor, Tensor, Tensor> layernorm_fwd(const Tensor& x, const Tensor& w, const Tensor& b,
                                                  at::ScalarType out_dtype, double eps) {
     check_gpu(x, "x"); check_gpu(w, "w"); check_gpu(b, "b");
-    TORCH_CHECK(x.dim() == 2 && w.scalar_type() == at::kFloat && b.scalar_type() == at::kFloat,
-                "layernorm_fwd: x (rows, cols), fp32 affine");
+    TORCH_CHECK(x.dim() == 2, "layernorm_fwd: x (rows, cols)");
+    check_vec(w, x.size(1), "LayerNorm weight"); check_vec(b, x.size(1), "LayerNorm bias");
     c10::DeviceGuard g(x.device());
     const int64_t rows = x.size(0), cols = x.size(1);
     Tensor y = at::empty({rows, cols}, like(x, out_dtype));
@@ -82,7 +90,10 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_fwd(const Tensor& x, const Tensor& 
 Tensor layernorm_bwd(const Tensor& dy, const Tensor& x, const Tensor& w, const Tensor& mean, const Tensor& rstd,
                      const c10::optional<Tensor>& res, Tensor& dw, Tensor& db) {
     check_gpu(dy, "dy"); check_gpu(x, "x"); check_gpu(w, "w"); check_gpu(mean, "mean"); check_gpu(rstd, "rstd");
-    check_opt(res, "res"); check_gpu(dw, "dw"); check_gpu(db, "db");
+    check_opt(res, "res");
+    TORCH_CHECK(x.dim() == 2 && dy.sizes() == x.sizes(), "layernorm_bwd: dy and x (rows, cols)");
+    check_vec(w, x.size(1), "LayerNorm weight"); check_vec(dw, x.size(1), "dw"); check_vec(db, x.size(1), "db");
+    check_vec(mean, x.size(0), "mean"); check_vec(rstd, x.size(0), "rstd");
     c10::DeviceGuard g(x.device());
     Tensor dx = at::empty(x.sizes(), like(x, at::kFloat));
     DCLIP_CALL(dclip_layernorm_bwd_res(dy.data_ptr(), dt_code(dy.scalar_type()), x.data_ptr(), dt_code(x.scalar_type()),
@@ -96,7 +107,10 @@ std::tuple<Tensor, Tensor> layernorm_bwd_lp(const Tensor& dy, const Tensor& x, c
                                             const Tensor& rstd, const c10::optional<Tensor>& res, Tensor& dw,
                                             Tensor& db, at::ScalarType lp_dtype) {
     check_gpu(dy, "dy"); check_gpu(x, "x"); check_gpu(w, "w"); check_gpu(mean, "mean"); check_gpu(rstd, "rstd");
-    check_opt(res, "res"); check_gpu(dw, "dw"); check_gpu(db, "db");
+    check_opt(res, "res");
+    TORCH_CHECK(x.dim() == 2 && dy.sizes() == x.sizes(), "layernorm_bwd: dy and x (rows, cols)");
+    check_vec(w, x.size(1), "LayerNorm weight"); check_vec(dw, x.size(1), "dw"); check_vec(db, x.size(1), "db");
+    check_vec(mean, x.size(0), "mean"); check_vec(rstd, x.size(0), "rstd");
     c10::DeviceGuard g(x.device());
     Tensor dx = at::empty(x.sizes(), like(x, at::kFloat));
     Tensor lp = at::empty(x.sizes(), like(x, lp_dtype));
@@ -121,12 +135,25 @@ Tensor gemm(const Tensor& A, const Tensor& B, int64_t epi, const c10::optional<T
             const c10::optional<Tensor>& scale) {
     gemm_checks(A, B);
     TORCH_CHECK(epi != DCLIP_EPI_GELU && epi != DCLIP_EPI_SPLITK, "gemm: use gemm_gelu / weight_grad for this epilogue");
-    check_opt(bias, "bias");
+    TORCH_CHECK(epi >= DCLIP_EPI_STORE && epi <= DCLIP_EPI_STORE_SCALED, "gemm: unknown epilogue ", epi);
     c10::DeviceGuard g(A.device());
     const int64_t M = A.size(0), N = B.size(0), K = A.size(1);
-    Tensor out = at::empty({M, N}, like(A, out_dtype));
+    check_vec(bias, N, "gemm bias");
     const bool has_aux = aux.has_value() && aux->defined();
     if (has_aux) TORCH_CHECK(aux->is_cuda() && aux->stride(-1) == 1, "gemm: aux must be a row-major GPU tensor");
+    if (epi == DCLIP_EPI_RESIDUAL || epi == DCLIP_EPI_GELU_BWD) {
+        // the residual (f32) / the saved pre-activation z (A's dtype), read at [m][n]
+        TORCH_CHECK(has_aux && aux->dim() == 2 && aux->size(0) == M && aux->size(1) == N,
+                    "gemm: this epilogue needs aux of shape (M, N) = (", M, ", ", N, ")");
+        TORCH_CHECK(epi != DCLIP_EPI_RESIDUAL || (aux->scalar_type() == at::kFloat && out_dtype == at::kFloat),
+                    "gemm: the residual epilogue reads and writes float32");
+        TORCH_CHECK(epi != DCLIP_EPI_GELU_BWD || aux->scalar_type() == A.scalar_type(),
+                    "gemm: the QuickGELU' epilogue's aux (z) must have A's dtype");
+    } else if (epi == DCLIP_EPI_STORE_SCALED) {
+        TORCH_CHECK(has_aux, "gemm: the scaled epilogue needs the per-column scale aux");
+        check_vec(aux, N, "gemm per-column scale (aux)");
+    }
+    Tensor out = at::empty({M, N}, like(A, out_dtype));
     DCLIP_CALL(dclip_gemm((int)epi, dt_code(A.scalar_type()), A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), M, N,
                           K, 1, (float)alpha, scale_entry(scale, 1), optr<float>(bias),
                           has_aux ? aux->data_ptr() : nullptr,
@@ -138,9 +165,9 @@ Tensor gemm(const Tensor& A, const Tensor& B, int64_t epi, const c10::optional<T
 // z = A B^T + bias, h = quick_gelu(z)  (c_fc + QuickGELU, models.py:277-281, 252-254)
 std::tuple<Tensor, Tensor> gemm_gelu(const Tensor& A, const Tensor& B, const c10::optional<Tensor>& bias) {
     gemm_checks(A, B);
-    check_opt(bias, "bias");
     c10::DeviceGuard g(A.device());
     const int64_t M = A.size(0), N = B.size(0), K = A.size(1);
+    check_vec(bias, N, "gemm_gelu bias");
     Tensor z = at::empty({M, N}, A.options()), h = at::empty({M, N}, A.options());
     DCLIP_CALL(dclip_gemm(DCLIP_EPI_GELU, dt_code(A.scalar_type()), A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0),
                           M, N, K, 1, 1.0f, nullptr, optr<float>(bias), nullptr, 0, 0, z.data_ptr(), dt_code(A.scalar_type()),
@@ -153,9 +180,11 @@ Tensor weight_grad(const Tensor& dy, const Tensor& x, double alpha, c10::optiona
                    const c10::optional<Tensor>& scale) {
     check_gpu(dy, "dy"); check_gpu(x, "x");
     TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0), "weight_grad: dy (M, N), x (M, K)");
-    check_opt(db, "db");
+    TORCH_CHECK(dy.scalar_type() == x.scalar_type(), "weight_grad: dy and x dtypes differ (", dy.scalar_type(), " vs ",
+                x.scalar_type(), ")");
     c10::DeviceGuard g(dy.device());
     const int64_t M = dy.size(0), N = dy.size(1), K = x.size(1);
+    check_vec(db, N, "weight_grad db");
     int splits = 0;
     int64_t k_pad = 0;
     DCLIP_CALL(dclip_gemm_tn_plan(N, K, M, &splits, &k_pad));
@@ -427,7 +456,8 @@ std::tuple<Tensor, Tensor> bn_fwd_into(const Tensor& x, const c10::optional<Tens
     const Rows r = rows_of(x), ry = rows_of(y);
     TORCH_CHECK(r.rows == ry.rows && r.C == ry.C && r.ld == ry.ld && x.scalar_type() == y.scalar_type(),
                 "dclip: BatchNorm output must match the input's rows, channels and pitch");
-    check_opt(w, "w"); check_opt(b, "b"); check_opt(running_mean, "running_mean"); check_opt(running_var, "running_var");
+    check_vec(w, r.C, "BatchNorm weight"); check_vec(b, r.C, "BatchNorm bias");
+    check_vec(running_mean, r.C, "running_mean"); check_vec(running_var, r.C, "running_var");
     c10::DeviceGuard g(x.device());
     Tensor ws = at::empty({dclip_bn_workspace(r.rows, (int)r.C)}, like(x, at::kFloat));
     Tensor mean = at::empty({r.C}, like(x, at::kFloat)), rstd = at::empty({r.C}, like(x, at::kFloat));
@@ -452,7 +482,8 @@ Tensor bn_eval(const Tensor& x, const c10::optional<Tensor>& w, const c10::optio
                const Tensor& running_mean, const Tensor& running_var, double eps, bool relu) {
     TORCH_CHECK(x.dim() == 4, "bn_eval: a channels-last 4-D map");
     const Rows r = rows_of(x);
-    check_opt(w, "w"); check_opt(b, "b"); check_gpu(running_mean, "running_mean"); check_gpu(running_var, "running_var");
+    check_vec(w, r.C, "BatchNorm weight"); check_vec(b, r.C, "BatchNorm bias");
+    check_vec(running_mean, r.C, "running_mean"); check_vec(running_var, r.C, "running_var");
     c10::DeviceGuard g(x.device());
     Tensor y = at::empty_like(x, at::MemoryFormat::ChannelsLast);
     Tensor ws = at::empty({dclip_bn_workspace(r.rows, (int)r.C)}, like(x, at::kFloat));
@@ -476,7 +507,8 @@ std::tuple<Tensor, Tensor> bn_bwd_into(const Tensor& dy, const Tensor& x, const 
     TORCH_CHECK(rd.rows == r.rows && rd.C == r.C && rd.ld == r.ld && rdx.ld == r.ld && rdx.rows == r.rows,
                 "dclip: BatchNorm backward tensors must share rows, channels and pitch");
     TORCH_CHECK(dy.scalar_type() == x.scalar_type() && dx.scalar_type() == x.scalar_type(), "bn_bwd: dtypes must match");
-    check_opt(w, "w"); check_opt(b, "b"); check_gpu(mean, "mean"); check_gpu(rstd, "rstd");
+    check_vec(w, r.C, "BatchNorm weight"); check_vec(b, r.C, "BatchNorm bias");
+    check_vec(mean, r.C, "mean"); check_vec(rstd, r.C, "rstd");
     c10::DeviceGuard g(x.device());
     Tensor ws = at::empty({dclip_bn_workspace(r.rows, (int)r.C)}, like(x, at::kFloat));
     Tensor dw = want_w ? at::empty({r.C}, like(x, at::kFloat)) : at::empty({0}, like(x, at::kFloat));

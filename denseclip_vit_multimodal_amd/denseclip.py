@@ -48,6 +48,10 @@ class DenseCLIP(nn.Module):
         # False (default): the reference contract — upsampled 'main_output' / 'depth_output'.
         self.fused_head_loss = False
         self.graph_text = True  # replay the frozen text path from a HIP graph (see _text_embeddings)
+        # fp32 images (the reference trainer's input): run the neck and heads on the HIP kernels in
+        # the backbone's 16-bit compute dtype (outputs returned in fp32) whenever their widths
+        # allow it (ops.neck_heads_hip_capable); False keeps them in fp32 torch (for A/B tests)
+        self.hip_heads = True
 
         # ---- backbone (denseclip.py:111-126)
         bcfg = dict(backbone)
@@ -331,12 +335,10 @@ class DenseCLIP(nn.Module):
         HW = h * w
         cdt = visual.dtype if visual.dtype in (torch.bfloat16, torch.float16) else \
             getattr(self.backbone, "compute_dtype", torch.float16)
-        if 0 <= self.score_concat_index < len(x) and torch.is_grad_enabled() and any(
-                p.requires_grad for m in (self.vis_proj, self.global_proj, self.context_decoder) if m is not None
-                for p in m.parameters()):
-            # the score branch below is forward-only (no autograd through the HIP score map)
-            raise NotImplementedError("training through score_concat_index >= 0 (the score map feeding the "
-                                      "neck) is not supported; the ViT Cityscapes config uses -1")
+        # the score branch is forward-only, as in the reference: with score_concat_index >= 0 the
+        # reference concatenates the score map onto a CLONE of the maps and the forward passes
+        # the unmodified maps to the neck (denseclip.py:586, 684-694, 747), so nothing trainable
+        # is reached through it (its parameters are kept out of DDP: train.gradless_parameter_names)
         with torch.no_grad():
             # pixel rows of the last map read in place: the read-out map is a channels-last view
             # of a (B*N, C) token buffer (CLS rows in between, ops.ReadoutFn), so the pooling, the
@@ -371,9 +373,10 @@ class DenseCLIP(nn.Module):
             score = ops.score_map(v, text, B, HW, row_off=off, bstride=Nr * Ct).view(B, -1, h, w)
         feats = list(x)
         if 0 <= self.score_concat_index < len(feats):
-            tgt = feats[self.score_concat_index]
-            sc = ops.upsample(score, tgt.shape[2:]).to(tgt.dtype)
-            feats[self.score_concat_index] = torch.cat([tgt, sc], dim=1)
+            with torch.no_grad():
+                tgt = feats[self.score_concat_index]
+                sc = ops.upsample(score, tgt.shape[2:]).to(tgt.dtype)
+                feats[self.score_concat_index] = torch.cat([tgt, sc], dim=1)
         return text, feats, score, list(x)
 
     def _heads(self, x_maps):
@@ -386,20 +389,56 @@ class DenseCLIP(nn.Module):
         depth = self.depth_head(inp) if self.with_depth_head else None
         return seg, depth
 
+    def _hip_heads_dtype(self, img):
+        """The 16-bit dtype the neck / heads run in for this input on the fp32-image path, or None
+        (16-bit images already give 16-bit maps; CPU tensors, fp32 compute or widths without a HIP
+        kernel keep the fp32 torch neck / heads)."""
+        if not (self.hip_heads and img.is_cuda and img.dtype == torch.float32
+                and isinstance(self.backbone, CLIPVisionTransformer)):
+            return None
+        cdt = self.backbone.compute_dtype
+        if cdt not in (torch.float16, torch.bfloat16) or not ops.neck_heads_hip_capable(self):
+            return None
+        return cdt
+
+    def _forward_hip_heads(self, img, cdt):
+        """fp32 images with the neck and heads on the HIP kernels: the backbone returns its maps in
+        the compute dtype (channels-last token-buffer views the implicit-GEMM convs read in place),
+        the neck / heads run in it, and their low-res outputs come back in fp32 through
+        ops.HeadsOutFn (whose backward applies the fp16 gradient scale, ops.HeadScale)."""
+        hs = ops.HeadScale(img.device, cdt)
+        with ops.head_scale(hs):
+            feats = self.backbone(img, map_dtype=cdt)
+            if not isinstance(feats, (list, tuple)) or not feats:
+                raise RuntimeError("backbone returned no feature maps")
+            feats = list(feats)
+            self._process_features(feats)  # score branch: computed and discarded (denseclip.py:747)
+            with torch.autocast("cuda", dtype=cdt):
+                seg, depth = self._heads(feats)
+        outs = [t for t in (seg, depth) if t is not None]
+        res = list(ops.HeadsOutFn.apply(hs, *outs)) if outs else []
+        seg = res.pop(0) if seg is not None else None
+        depth = res.pop(0) if depth is not None else None
+        return seg, depth
+
     def forward(self, img, img_metas=None, gt_semantic_seg=None, return_loss=True, **kwargs):
         """denseclip.py:702-916.  Train: {'main_output','depth_output','aux_losses'};
         eval: {'seg','depth'} resized to the image."""
         if img.is_cuda:
             self._text_prelaunch(img.device)
-        feats = self.extract_feat(img)
-        text, _, score, _ = self._process_features(feats)
-        maps = feats
-        param = next(self.neck.parameters()) if self.neck is not None else None
-        if param is not None and maps[0].dtype != param.dtype and maps[0].is_cuda:
-            with torch.autocast("cuda", dtype=maps[0].dtype):
-                seg, depth = self._heads(maps)
+        hcdt = self._hip_heads_dtype(img)
+        if hcdt is not None:
+            seg, depth = self._forward_hip_heads(img, hcdt)
         else:
-            seg, depth = self._heads(maps)
+            feats = self.extract_feat(img)
+            self._process_features(feats)  # score branch: computed and discarded (denseclip.py:747)
+            maps = feats
+            param = next(self.neck.parameters()) if self.neck is not None else None
+            if param is not None and maps[0].dtype != param.dtype and maps[0].is_cuda:
+                with torch.autocast("cuda", dtype=maps[0].dtype):
+                    seg, depth = self._heads(maps)
+            else:
+                seg, depth = self._heads(maps)
         if return_loss and self.training and self.fused_head_loss:
             # low-res head outputs for train.loss_fn's fused upsample + CE / SILog kernels
             # (same loss and gradients; the 1024x2048 logits are never materialised)

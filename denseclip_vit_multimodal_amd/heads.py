@@ -29,6 +29,7 @@ class FCNHead(nn.Sequential):
     def forward(self, x):
         if ops.fcn_head_hip_ok(self, x):
             return ops.fcn_head(self, x)
+        ops.note_torch_fallback()
         return super().forward(x)
 
 

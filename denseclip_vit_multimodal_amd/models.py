@@ -32,6 +32,7 @@ class BatchNorm2d(nn.BatchNorm2d):
             return ops.bn_train(self, x)
         if ops.bn_eval_ok(self, x):  # running statistics, no gradient: dclip_bn_eval
             return ops.bn_eval(self, x)
+        ops.note_torch_fallback()
         if x.is_cuda:
             with torch.backends.cudnn.flags(enabled=False):
                 return super().forward(x)
@@ -271,7 +272,10 @@ class CLIPVisionTransformer(nn.Module):
             return x.dtype
         return self.compute_dtype
 
-    def forward(self, x):
+    def forward(self, x, map_dtype=None):
+        """map_dtype (extension; default x.dtype, the reference contract): dtype of the returned
+        maps.  DenseCLIP passes the compute dtype for fp32 images so the HIP neck and heads read
+        the read-out token buffers in place (their outputs are returned in fp32)."""
         if not x.is_cuda:
             raise RuntimeError("CLIPVisionTransformer runs on the MI355X HIP kernels only (got a CPU tensor)")
         if self.width != self.heads * 64:
@@ -286,7 +290,9 @@ class CLIPVisionTransformer(nn.Module):
                                      self.ln_pre.weight, self.ln_pre.bias, p, cdt)
         outs = []
         meta = (B, Ntok, self.heads, cdt, self.attn_fp8)
-        rmeta = (B, Ntok, gh, gw, x.dtype)
+        mdt = map_dtype or x.dtype
+        hsb = ops._head_scale_buf()  # the 16-bit heads' gradient scale (DenseCLIP, fp16, fp32 images)
+        rmeta = (B, Ntok, gh, gw, mdt, hsb)
         last = max(self.out_indices) if self.out_indices else -1
         for i, blk in enumerate(self.transformer.resblocks):
             if i > last:
@@ -295,7 +301,7 @@ class CLIPVisionTransformer(nn.Module):
             if i in self.out_indices and i != self.layers - 1:
                 # read-out without ln_post: produced by the block itself, so its gradient is
                 # folded into the block's backward (ops.BlockFn, meta[5])
-                bmeta = meta + ((gh, gw, x.dtype),) + ((dp,) if dp is not None else ())
+                bmeta = meta + ((gh, gw, mdt, hsb),) + ((dp,) if dp is not None else ())
                 tok, fmap = ops.BlockFn.apply(tok, bmeta, *blk.hip_params())
                 outs.append(fmap)
                 continue
@@ -469,11 +475,13 @@ class ViTFeatureFusionNeck(nn.Module):
                 and ops.conv1x1_supported(x, conv.weight):
             y = ops.Conv1x1Fn.apply(x, conv.weight, conv.bias, x.dtype)
         else:
+            ops.note_torch_fallback()
             y = conv(x)
         if ops.bn_hip_ok(bn, y):
             return ops.bn_train(bn, y, relu=True)  # BN + ReLU in one pass each way
         if ops.bn_eval_ok(bn, y):
             return ops.bn_eval(bn, y, relu=True)   # eval: running statistics, ReLU fused
+        ops.note_torch_fallback()
         return act(bn(y))
 
     def forward(self, features):

@@ -43,6 +43,10 @@ TIMING = None
 STATS = {}  # path counters (tests check which path ran)
 
 
+def _stat(name):
+    STATS[name] = STATS.get(name, 0) + 1
+
+
 def _tic():
     if TIMING is None:
         return None
@@ -294,25 +298,30 @@ def bilinear_bwd(dout, Hi, Wi):
 
 
 # ============================================================================ weight cache
-# Every optimizer step (any torch.optim optimizer, fused or not) bumps this generation.  The
-# fused AdamW kernel updates parameters in place WITHOUT moving their version counters, so the
-# version alone cannot tell a cached compute-dtype copy that its master weight changed.
-_GENERATION = [0]
+# Every optimizer step (any torch.optim optimizer, fused or not) stamps the parameters IT holds
+# with a new step number.  The fused AdamW kernel updates parameters in place WITHOUT moving their
+# version counters, so the version alone cannot tell a cached compute-dtype copy that its master
+# weight changed; frozen parameters (mode R's backbone) keep their stamp and their cached copies.
+_GENERATION = [0]   # bumped by invalidate_weight_cache(): every entry is stale
+_STEP = [0]
 
 
-def _bump_generation(*_):
-    _GENERATION[0] += 1
+def _stamp_stepped_params(opt, *_):
+    _STEP[0] += 1
+    for group in opt.param_groups:
+        for p in group["params"]:
+            p.__dict__["_dclip_step"] = _STEP[0]
 
 
 from torch.optim.optimizer import register_optimizer_step_post_hook  # noqa: E402
 
-register_optimizer_step_post_hook(_bump_generation)
+register_optimizer_step_post_hook(_stamp_stepped_params)
 
 
 def invalidate_weight_cache():
     """Force every cached compute-dtype weight copy to be rebuilt on next use (for code that
     writes parameters through `.data` or outside torch.optim)."""
-    _bump_generation()
+    _GENERATION[0] += 1
 
 
 class _Cast:
@@ -321,12 +330,12 @@ class _Cast:
     The entries live ON the parameter object (attribute `_dclip_cache`), so they die with it:
     no entry outlives its parameter and no new parameter can inherit another's entry through
     a recycled `id`.  An entry is valid while the parameter's version counter, storage
-    address and the optimizer-step generation are all unchanged."""
+    address, the last optimizer step that held it and the global generation are all unchanged."""
 
     @staticmethod
     def _lookup(p, key):
         w = p.detach()
-        stamp = (_GENERATION[0], w._version, w.data_ptr())
+        stamp = (_GENERATION[0], p.__dict__.get("_dclip_step", 0), w._version, w.data_ptr())
         cache = p.__dict__.get("_dclip_cache")
         if cache is None:
             cache = p.__dict__["_dclip_cache"] = {}
@@ -452,7 +461,7 @@ class BlockFn(torch.autograd.Function):
         ctx.meta = meta
         if ro is None:
             return xo
-        gh, gw, mdt = ro
+        gh, gw, mdt = ro[:3]
         ctx.set_materialize_grads(False)  # an unused map (or block output) brings None, not zeros
         buf = xo.clone() if mdt == torch.float32 else cast(xo, mdt)
         return xo, buf.as_strided((B, C, gh, gw), (Ntok * C, 1, gw * C, C), C)
@@ -481,17 +490,18 @@ class BlockFn(torch.autograd.Function):
             dxo = torch.zeros(B * Ntok, C, dtype=torch.float32, device=x.device)
         dxo = dxo.contiguous()
         if dmap is not None:  # the read-out map's gradient joins the block output's
-            gh, gw, _ = ctx.meta[5]
+            gh, gw = ctx.meta[5][:2]
+            hsb = ctx.meta[5][3] if len(ctx.meta[5]) > 3 else None  # HeadScale buffer (fp16 heads)
             base = _readout_grad_buffer(dmap, B, Ntok, gh, gw, C)
-            if base is not None and cdt == torch.bfloat16 and dp is None:
+            if base is not None and cdt == torch.bfloat16 and dp is None and hsb is None:
                 # one pass: dxo + map gradient (CLS rows masked) in fp32, and its bf16 copy
                 dxo, dy = D().add_readout_cast(dxo, base, Ntok, cdt, 1.0)
             elif base is not None:
                 dr = base.float() if base.dtype != torch.float32 else base.clone()
                 dr.view(B, Ntok, C)[:, 0].zero_()
-                dxo = dxo + dr
+                dxo = dxo + _unscale_(dr, hsb)
             else:
-                dxo = dxo + _readout_grad_dense(dmap, B, Ntok, gh, gw, C)
+                dxo = dxo + _unscale_(_readout_grad_dense(dmap, B, Ntok, gh, gw, C), hsb)
 
         # ---- MLP: xo = xm + h W2^T + b2,  h = qgelu(z),  z = xh2 W1^T + b1
         # (s1, s2: device-side power-of-two gradient scales, None unless fp16 — see grad_scale)
@@ -556,7 +566,7 @@ def _readout_grad_buffer(dmap, B, Ntok, gh, gw, C):
     gradient: zero copy); None otherwise."""
     if dmap.stride() == (Ntok * C, 1, gw * C, C) and dmap.storage_offset() >= C and \
             dmap.untyped_storage().nbytes() >= (dmap.storage_offset() - C + B * Ntok * C) * dmap.element_size():
-        STATS["readout_zero_copy"] = STATS.get("readout_zero_copy", 0) + 1
+        _stat("readout_zero_copy")
         return dmap.as_strided((B * Ntok, C), (C, 1), dmap.storage_offset() - C)
     return None
 
@@ -579,7 +589,7 @@ class ReadoutFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, ln_w, ln_b, meta):
-        B, Ntok, gh, gw, out_dtype = meta
+        B, Ntok, gh, gw, out_dtype = meta[:5]
         C = x.shape[1]
         mean = rstd = None
         if ln_w is not None:
@@ -596,7 +606,8 @@ class ReadoutFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dmap):
         x, mean, rstd, ln_w = ctx.saved_tensors
-        B, Ntok, gh, gw, _ = ctx.meta
+        B, Ntok, gh, gw, _ = ctx.meta[:5]
+        hsb = ctx.meta[5] if len(ctx.meta) > 5 else None  # HeadScale buffer (fp16 heads)
         C = dmap.shape[1]
         base = _readout_grad_buffer(dmap, B, Ntok, gh, gw, C)
         if base is not None:  # token-buffer layout (Conv3x3Fn's input gradient): take the buffer as it is
@@ -604,6 +615,7 @@ class ReadoutFn(torch.autograd.Function):
             dy.view(B, Ntok, C)[:, 0].zero_()
         else:
             dy = _readout_grad_dense(dmap, B, Ntok, gh, gw, C)
+        _unscale_(dy, hsb)
         if not ctx.has_ln:
             return dy, None, None, None
         dw = torch.zeros(C, dtype=torch.float32, device=dy.device)
@@ -635,6 +647,8 @@ class BatchNormFn(torch.autograd.Function):
         ctx.save_for_backward(x, w, b, mean, rstd)
         ctx.has_w = (weight is not None, bias is not None)
         ctx.relu = bool(relu)
+        ctx.hsb = _head_scale_buf()
+        _stat("bn_train")
         return y
 
     @staticmethod
@@ -642,7 +656,9 @@ class BatchNormFn(torch.autograd.Function):
         x, w, b, mean, rstd = ctx.saved_tensors
         dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last)
         dx, dw, db = D().bn_bwd(dy, x, w, b, mean, rstd, ctx.relu, ctx.has_w[0], ctx.has_w[1])
-        return dx, dw if ctx.has_w[0] else None, db if ctx.has_w[1] else None, None, None, None, None, None
+        dw = _unscale_(dw, ctx.hsb) if ctx.has_w[0] else None
+        db = _unscale_(db, ctx.hsb) if ctx.has_w[1] else None
+        return dx, dw, db, None, None, None, None, None
 
 
 def bn_train(bn, x, relu=False):
@@ -659,6 +675,7 @@ def bn_eval(bn, x, relu=False):
     w = bn.weight.detach() if bn.weight is not None else None
     b = bn.bias.detach() if bn.bias is not None else None
     _check(w, b, bn.running_mean, bn.running_var, strided=(x,))
+    _stat("bn_eval")
     return D().bn_eval(x, w, b, bn.running_mean, bn.running_var, float(bn.eps), bool(relu))
 
 
@@ -697,6 +714,146 @@ class UpsampleFn(torch.autograd.Function):
 def upsample(x, size):
     Ho, Wo = int(size[0]), int(size[1])
     return UpsampleFn.apply(x, Ho, Wo)
+
+
+# ============================================================================ 16-bit neck / heads for fp32 images
+class HeadScale:
+    """Gradient scale of one forward's 16-bit neck / heads / read-out backward (fp32 images, the
+    reference trainer's input, run through the HIP neck and heads in the backbone's compute dtype).
+
+    The segmentation-loss gradients reaching the heads are ~1e-5..1e-8 per low-res logit: in or
+    below fp16's subnormal range.  HeadsOutFn's backward therefore casts them to fp16 with a
+    device-side power-of-two scale s (grad_scale; written into `buf` = (s, 1/s, 0, 0), no host
+    sync) and every fp32 result computed from them downstream — the neck / head weight and BN
+    gradients, the read-out maps' gradients entering the ViT backward — is multiplied by 1/s
+    from `buf` by the op that produces it.  bf16 has the fp32 exponent range: no scaling.
+
+    `torch_fallback` is set when any neck / head op ran on torch instead of a scale-aware HIP
+    op with gradients on; HeadsOutFn then leaves s = 1 (the torch op's parameter gradients could
+    not be unscaled)."""
+
+    def __init__(self, device, cdt):
+        self.cdt = cdt
+        self.buf = torch.tensor([1.0, 1.0, 0.0, 0.0], dtype=torch.float32, device=device) \
+            if cdt == torch.float16 and torch.is_grad_enabled() else None
+        self.torch_fallback = False
+
+
+_HEAD_SCALE = [None]
+
+
+class head_scale:
+    """Context manager: the neck / head / read-out autograd Functions created inside it capture
+    `hs.buf` and unscale their fp32 gradients by its 1/s."""
+
+    def __init__(self, hs):
+        self.hs = hs
+
+    def __enter__(self):
+        self.prev = _HEAD_SCALE[0]
+        _HEAD_SCALE[0] = self.hs
+        return self.hs
+
+    def __exit__(self, *exc):
+        _HEAD_SCALE[0] = self.prev
+
+
+def _head_scale_buf():
+    hs = _HEAD_SCALE[0]
+    return hs.buf if hs is not None else None
+
+
+def note_torch_fallback():
+    """A neck / head op ran on torch kernels (called by the fallback branches)."""
+    hs = _HEAD_SCALE[0]
+    if hs is not None and torch.is_grad_enabled():
+        hs.torch_fallback = True
+
+
+def _unscale_(t, buf):
+    """t *= 1/s of a HeadScale buffer (in place, on the device); t may be None."""
+    if t is not None and buf is not None:
+        t.mul_(buf[1])
+    return t
+
+
+class HeadsOutFn(torch.autograd.Function):
+    """The heads' 16-bit low-res outputs as fp32 (what the reference returns for fp32 images);
+    backward: the fp32 gradients cast back to the compute dtype, for fp16 with the shared
+    power-of-two scale of HeadScale (one s for both heads: their input gradients sum in the
+    neck)."""
+
+    @staticmethod
+    def forward(ctx, hs, *outs):
+        ctx.hs = hs
+        return tuple(o.float() for o in outs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        hs = ctx.hs
+        cdt = hs.cdt
+        if hs.buf is None or hs.torch_fallback:
+            return (None,) + tuple(None if g is None else g.to(cdt) for g in gs)
+        gs = [None if g is None else g.contiguous() for g in gs]
+        bufs = [grad_scale(g, cdt) for g in gs if g is not None]
+        if not bufs:
+            return (None,) + tuple(None for _ in gs)
+        sb = bufs[0]
+        for b in bufs[1:]:  # the smaller scale of the two (the larger max |g|)
+            sb = torch.where(b[0] < sb[0], b, sb)
+        hs.buf.copy_(sb)
+        _stat("head_grad_scale")
+        return (None,) + tuple(None if g is None else cast(g, cdt, scale_t=hs.buf) for g in gs)
+
+
+def _divides(a, b):
+    return b > 0 and a % b == 0
+
+
+def neck_heads_hip_capable(model):
+    """Whether every neck / head op of `model` (a DenseCLIP) has a HIP kernel for 16-bit maps at
+    its widths (decided from the module shapes before the backbone runs): the per-level 3x3
+    convs (Cin % 128, Cout % 64, concatenated width <= 2048), the 1x1 fusion conv (Cin, Cout %
+    64), the BN widths (% 8, <= 2048) and the FCN heads (3x3 Cin % 128, 1x1 Cin % 64)."""
+    def bn_ok(bn):
+        return (isinstance(bn, torch.nn.BatchNorm2d) and _divides(bn.num_features, 8) and bn.num_features <= 2048
+                and bn.affine and bn.track_running_stats)
+
+    def conv3_ok(conv, cin):
+        return (conv.kernel_size == (3, 3) and conv.padding == (1, 1) and conv.stride == (1, 1) and conv.bias is None
+                and conv.groups == 1 and conv.dilation == (1, 1) and _divides(cin, 128) and conv.in_channels == cin)
+
+    width = getattr(model.backbone, "width", None)
+    if width is None:
+        return False
+    head_in = width
+    neck = model.neck
+    if neck is not None:
+        layers = list(neck.process_layers)
+        if not layers:
+            return False
+        Ci = layers[0][0].out_channels
+        for layer in layers:
+            if not (conv3_ok(layer[0], width) and layer[0].out_channels == Ci and bn_ok(layer[1])):
+                return False
+        if not (_divides(Ci, 64) and len(layers) * Ci <= 2048):
+            return False
+        fconv, fbn = neck.fusion_layer[0], neck.fusion_layer[1]
+        if not (fconv.kernel_size == (1, 1) and fconv.stride == (1, 1) and fconv.groups == 1
+                and _divides(fconv.in_channels, 64) and _divides(fconv.out_channels, 64) and bn_ok(fbn)):
+            return False
+        head_in = fconv.out_channels
+    for head in (model.decode_head, model.depth_head):
+        if head is None:
+            continue
+        if len(head) != 6:
+            return False
+        c3, bn, _, _, c1, cl = head
+        if not (conv3_ok(c3, head_in) and bn_ok(bn) and c1.kernel_size == (1, 1) and cl.kernel_size == (1, 1)
+                and c1.bias is not None and cl.bias is not None and c1.stride == (1, 1) and cl.stride == (1, 1)
+                and c1.groups == 1 and cl.groups == 1 and _divides(c1.in_channels, 64)):
+            return False
+    return model.decode_head is not None or model.depth_head is not None
 
 
 # ============================================================================ neck convs
@@ -753,6 +910,8 @@ class Conv3x3Fn(torch.autograd.Function):
         ctx.geo = (B, Cin, H, W, Cout, cp, bs, ld, xmap.dtype, tuple(xmap.stride()), xmap.storage_offset() -
                    (xr.storage_offset() if xr is xmap else 0), xr is xmap)
         ctx.cdt = cdt
+        ctx.hsb = _head_scale_buf()
+        _stat("conv3x3")
         y = out.as_strided((B, Cout, H, W), (H * W * cp, 1, W * cp, cp))
         return y
 
@@ -793,7 +952,8 @@ class Conv3x3Fn(torch.autograd.Function):
             e0 = _tic()
             dwr = D().conv3x3_wgrad(dyr, cp, cp, xr, bs, 0, ld, B, H, W, Cin, splits)
             _toc("conv_wgrad", e0)
-            dw = dwr[:Cout].view(Cout, 3, 3, Cin).permute(0, 3, 1, 2).contiguous().to(weight.dtype)
+            dw = _unscale_(dwr[:Cout].view(Cout, 3, 3, Cin).permute(0, 3, 1, 2).contiguous().to(weight.dtype),
+                           ctx.hsb)
         return dx, dw, None
 
 
@@ -860,6 +1020,8 @@ class NeckLevelsFn(torch.autograd.Function):
         ctx.save_for_backward(pre, *[g[0] for g in geo], *convw, *bnw, *bnb, *stats)
         ctx.meta = (L, B, Cin, H, W, Ci, cdt, [(g[1], g[2]) for g in geo], [m.dtype for m in maps],
                     [tuple(m.stride()) for m in maps], [g[0] is m for g, m in zip(geo, maps)])
+        ctx.hsb = _head_scale_buf()
+        _stat("neck_levels")
         return out.as_strided((B, LC, H, W), (H * W * LC, 1, W * LC, LC))
 
     @staticmethod
@@ -885,6 +1047,8 @@ class NeckLevelsFn(torch.autograd.Function):
             sl = slice(l * Ci, (l + 1) * Ci)
             dbnw[l], dbnb[l] = D().bn_bwd_rows(d[:, sl], pre[:, sl], bnw[l].detach(), bnb[l].detach(), stats[2 * l],
                                                stats[2 * l + 1], True, True, True, dpre[:, sl])
+            _unscale_(dbnw[l], ctx.hsb)
+            _unscale_(dbnb[l], ctx.hsb)
             bs, ld = bsld[l]
             if need[1 + l]:  # input gradient: the dgrad conv, in the input's own layout when it is a token view
                 w_t = _conv3x3_dgrad_rows(convw[l], cdt)
@@ -903,7 +1067,8 @@ class NeckLevelsFn(torch.autograd.Function):
                 e0 = _tic()
                 dwr = D().conv3x3_wgrad(dpre[:, l * Ci:], LC, Ci, xrs[l], bs, 0, ld, B, H, W, Cin, splits)
                 _toc("conv_wgrad", e0)
-                dconv[l] = dwr[:Ci].view(Ci, 3, 3, Cin).permute(0, 3, 1, 2).contiguous().to(convw[l].dtype)
+                dconv[l] = _unscale_(dwr[:Ci].view(Ci, 3, 3, Cin).permute(0, 3, 1, 2).contiguous().to(convw[l].dtype),
+                                     ctx.hsb)
         return (None, *dmaps, *dconv, *dbnw, *dbnb)
 
 
@@ -947,6 +1112,8 @@ class Conv1x1Fn(torch.autograd.Function):
         ctx.save_for_backward(x2, weight)
         ctx.meta = (B, Cin, H, W, Cout, bias is not None, xmap.dtype)
         ctx.cdt = cdt
+        ctx.hsb = _head_scale_buf()
+        _stat("conv1x1")
         return out.as_strided((B, Cout, H, W), (H * W * Cout, 1, W * Cout, Cout))
 
     @staticmethod
@@ -963,7 +1130,7 @@ class Conv1x1Fn(torch.autograd.Function):
             if in_dt != cdt:
                 dx = dx.to(in_dt)
         if ctx.needs_input_grad[1] or (has_b and ctx.needs_input_grad[2]):
-            dWm, dbm = weight_grad(d2, x2, want_bias=has_b)
+            dWm, dbm = weight_grad(d2, x2, want_bias=has_b, scale=ctx.hsb)
             dw = dWm.view_as(weight).to(weight.dtype)
             db = dbm
         return dx, dw, db, None
@@ -1005,6 +1172,8 @@ class MergedPointwiseFn(torch.autograd.Function):
         out = D().transpose_batched(rows, B, H * W, K, Kp, H * W, cdt)  # (B, K, H*W)
         ctx.save_for_backward(y2, w1, b1, wc, Wp)
         ctx.meta = (B, Cin, H, W, C1, K, Kp, y.dtype, cdt)
+        ctx.hsb = _head_scale_buf()
+        _stat("merged_pointwise")
         return out.view(B, K, H, W)
 
     @staticmethod
@@ -1021,7 +1190,7 @@ class MergedPointwiseFn(torch.autograd.Function):
                 dy = dy.to(in_dt)
         dw1 = db1 = dwc = dbc = None
         if any(need[1:5]):
-            G, cs = weight_grad(dY, y2)  # (Kp, Cin) = dY^T X, colsum(dY)
+            G, cs = weight_grad(dY, y2, scale=ctx.hsb)  # (Kp, Cin) = dY^T X, colsum(dY), unscaled
             with torch.autocast("cuda", enabled=False):
                 G, cs = G[:K], cs[:K]
                 W1m = w1.detach().reshape(C1, Cin).float()
@@ -1050,12 +1219,14 @@ def fcn_head(head, x):
     in train mode; torch's eval BN otherwise), Dropout (torch), merged 1x1 tail."""
     c3, bn, relu, drop, c1, cl = head
     cdt = x.dtype
+    _stat("fcn_head")
     y = Conv3x3Fn.apply(x, c3.weight, cdt)
     if bn_hip_ok(bn, y):
         y = bn_train(bn, y, relu=True)
     elif bn_eval_ok(bn, y):
         y = bn_eval(bn, y, relu=True)
     else:
+        note_torch_fallback()
         y = relu(bn(y))
     y = drop(y)
     return MergedPointwiseFn.apply(y, c1.weight, c1.bias, cl.weight, cl.bias, cdt)

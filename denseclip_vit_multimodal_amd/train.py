@@ -19,23 +19,19 @@ import torch.nn.functional as F
 
 from .losses import SILogLoss
 
-# parameters that receive no gradient in the ViT Cityscapes config: the unused CLIP
-# projection and the score-map branch, whose output is discarded (denseclip.py:747).  They stay
-# trainable — the reference's AdamW param list holds them (train_denseclip.py:1040-1044, 1061),
-# so optimizer states interoperate — and are kept out of the DDP gradient reduction instead.
+# parameters that never receive a gradient: the unused CLIP projection and everything the
+# score-map branch touches — the learnable text contexts, gamma, vis_proj / global_proj and the
+# ContextDecoder.  That branch runs under no_grad and its output is discarded for every
+# score_concat_index (the reference concatenates the score map onto a clone of the maps that the
+# forward never passes on, denseclip.py:586, 684-694, 747).  They stay trainable — the
+# reference's AdamW param list holds them (train_denseclip.py:1040-1044, 1061), so optimizer
+# states interoperate — and are kept out of the DDP gradient reduction instead.
 _DEAD = ("backbone.proj", "contexts", "gamma")
-_DEAD_PREFIX = ("vis_proj.", "global_proj.")
-
-
-def _score_branch_live(model):
-    m = _unwrap(model)
-    return 0 <= getattr(m, "score_concat_index", -1) < len(getattr(m.backbone, "out_indices", []))
+_DEAD_PREFIX = ("vis_proj.", "global_proj.", "context_decoder.")
 
 
 def gradless_parameter_names(model):
     """Trainable parameter names that get no gradient (DDP must not wait for them)."""
-    if _score_branch_live(model):
-        return []
     return [n for n, p in _unwrap(model).named_parameters()
             if p.requires_grad and (n in _DEAD or n.startswith(_DEAD_PREFIX))]
 
@@ -136,15 +132,39 @@ def make_optimizer(params, fused=None):
     return torch.optim.AdamW(params, lr=2e-5, weight_decay=0.01, fused=fused)
 
 
+def step_unless_nonfinite(opt, loss):
+    """opt.step(), skipped when the loss is NaN / Inf — the reference trainer skips such a step
+    (train_denseclip.py:1323; e.g. a batch whose labels are all ignored gives a NaN CE).
+
+    Fused torch optimizers take the decision ON THE DEVICE through their `found_inf` input (the
+    AdamW kernel leaves parameters, moments and the step count untouched when it is non-zero): no
+    host sync.  Under torch.distributed the flag is MAX-reduced first, so every rank skips
+    together and the replicas stay identical.  Non-fused optimizers check on the host."""
+    if not all(g.get("fused") for g in opt.param_groups):
+        if bool(torch.isfinite(loss.detach()).all()):
+            opt.step()
+        return
+    flag = (~torch.isfinite(loss.detach().reshape(-1)[0])).to(torch.float32)  # 0-dim, like GradScaler's
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+    opt.found_inf = flag
+    try:
+        opt.step()
+    finally:
+        del opt.found_inf
+
+
 def train_step(model, opt, batch, silog=None, seg_weight=1.0, silog_weight=0.1):
     """One step: forward (DenseCLIP.forward train branch), loss, backward (DDP all-reduce
-    overlapped with it), AdamW.  Returns the loss tensor (no host sync)."""
+    overlapped with it), AdamW (skipped for a non-finite loss, step_unless_nonfinite).  Returns
+    the loss tensor (no host sync)."""
     img, seg, depth, mask = batch
     out = model(img, gt_semantic_seg=seg, gt_depth=depth, return_loss=True)
     loss = loss_fn(out, seg, depth, mask, silog, seg_weight, silog_weight)
     opt.zero_grad(set_to_none=True)
     loss.backward()
-    opt.step()
+    step_unless_nonfinite(opt, loss)
     return loss.detach()
 
 

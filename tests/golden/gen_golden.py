@@ -6,6 +6,7 @@ GPU box):
     python tests/golden/gen_golden.py            # writes tests/golden/*.safetensors
     python tests/golden/gen_golden.py ctx        # only the ContextDecoder fixture (+ manifest)
     python tests/golden/gen_golden.py vitl14     # only the ViT-L/14 fixture (+ manifest)
+    python tests/golden/gen_golden.py mid        # only the MID_CFG fixtures (+ manifest)
 
 The reference package imports `timm`, `ftfy` and `torchvision`, none of which are
 installed here.  The shims below are written into a temporary directory at run
@@ -39,7 +40,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 from weights_spec import fill_state_dict  # noqa: E402
 from model_configs import (TINY_CFG, TINY_CTX_CFG, CTX_GAMMA, CITYSCAPES_CFG, CITYSCAPES_CLASSES,  # noqa: E402
-                           VITL14_CFG)
+                           VITL14_CFG, MID_CFG)
 
 REF_SEG = "/root/reference/segmentation"
 
@@ -138,6 +139,64 @@ def sample_idx(numel, k, seed):
 def images(b, h, w, seed=1234):
     g = torch.Generator().manual_seed(seed)
     return torch.randn(b, 3, h, w, generator=g)
+
+
+def train_step_fixture(cfg, b, h, w):
+    """One seeded train step of the reference (dropout disabled -> deterministic; BN in train
+    mode uses batch statistics, as in the reference trainer): inputs, targets, loss, the
+    train-mode low-res head outputs, every gradient's norm and 64 sampled elements."""
+    model = build_reference(cfg)
+    model.train()
+    for mod in model.modules():
+        if isinstance(mod, nn.Dropout):
+            mod.eval()
+    for p in model.parameters():
+        p.requires_grad_(True)
+    cap = capture(model)
+    xb = images(b, h, w, seed=1234)
+    g = torch.Generator().manual_seed(1235)
+    seg_t = torch.randint(0, 19, (b, h, w), generator=g)
+    seg_t[torch.rand(b, h, w, generator=g) < 0.1] = 255
+    g = torch.Generator().manual_seed(1236)
+    depth_t = 1 + 79 * torch.rand(b, 1, h, w, generator=g)
+    depth_m = torch.rand(b, 1, h, w, generator=g) >= 0.2
+    out = model(xb, gt_semantic_seg=seg_t, gt_depth=depth_t, return_loss=True)
+    sys.path.insert(0, REF_SEG)
+    from denseclip.losses import SILogLoss
+    ce = F.cross_entropy(out["main_output"], seg_t, ignore_index=255)
+    silog = SILogLoss(lambd=0.5, eps=1e-6)(out["depth_output"], depth_t, depth_m)
+    loss = 1.0 * ce + 0.1 * silog
+    loss.backward()
+    tr = {"input": xb, "seg_t": seg_t, "depth_t": depth_t, "depth_m": depth_m.to(torch.uint8),
+          "loss": torch.stack([loss.detach(), ce.detach(), silog.detach()]),
+          "seg_low": cap["seg_low"], "depth_low": cap["depth_low"]}
+    for name, p in model.named_parameters():
+        if p.grad is None:
+            continue
+        gr = p.grad.detach().flatten()
+        idx = sample_idx(gr.numel(), min(64, gr.numel()), seed=7)
+        tr[f"gnorm/{name}"] = gr.double().norm().reshape(1)
+        tr[f"gidx/{name}"] = idx
+        tr[f"gval/{name}"] = gr[idx]
+    return tr, loss
+
+
+def gen_mid():
+    """MID_CFG (HIP-kernel widths for every neck / head op): an eval forward at 1 x 128x256
+    (maps, score map, low-res and resized head outputs) and one train step at 2 x 128x256."""
+    model = build_reference(MID_CFG).eval()
+    cap = capture(model)
+    x = images(1, 128, 256, seed=1234)
+    with torch.no_grad():
+        out = model(x, return_loss=False)
+    t = {"input": x, "seg": out["seg"], "depth": out["depth"], "score": cap["score"],
+         "text": cap["text"], "seg_low": cap["seg_low"], "depth_low": cap["depth_low"]}
+    for i, mp in enumerate(cap["maps"]):
+        t[f"map{i}"] = mp
+    save_file({k: v.contiguous() for k, v in t.items()}, os.path.join(HERE, "mid_eval.safetensors"))
+    tr, loss = train_step_fixture(MID_CFG, 2, 128, 256)
+    save_file({k: v.contiguous() for k, v in tr.items()}, os.path.join(HERE, "mid_train.safetensors"))
+    print("mid: loss", loss.item())
 
 
 def gen_tiny():
@@ -251,7 +310,7 @@ def gen_manifest():
     import json
     man = {}
     for name, cfg in (("tiny", TINY_CFG), ("tiny_ctx", TINY_CTX_CFG), ("cityscapes", CITYSCAPES_CFG),
-                      ("vitl14", VITL14_CFG)):
+                      ("vitl14", VITL14_CFG), ("mid", MID_CFG)):
         from denseclip import DenseCLIP
         sd = DenseCLIP(class_names=CITYSCAPES_CLASSES, **dict(cfg)).state_dict()
         man[name] = {k: [list(v.shape), str(v.dtype)] for k, v in sd.items()}
@@ -273,10 +332,15 @@ if __name__ == "__main__":
         gen_manifest()
         gen_vitl14()
         sys.exit(0)
+    if sys.argv[1:] == ["mid"]:
+        gen_manifest()
+        gen_mid()
+        sys.exit(0)
     gen_tokens()
     gen_manifest()
     gen_tiny()
     gen_tiny_ctx()
+    gen_mid()
     gen_full("vitb16_1x128x256", 1, 128, 256)
     gen_full("vitb16_2x512x1024", 2, 512, 1024, keep_full_maps=(0, 11))
     gen_vitl14()

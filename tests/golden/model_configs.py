@@ -76,3 +76,17 @@ CTX_GAMMA = 0.5
 VITL14_CFG = dict(CITYSCAPES_CFG,
                   backbone=dict(type='CLIPVisionTransformer', patch_size=14, width=1024, layers=24, heads=16,
                                 input_resolution=224, output_dim=1024, out_indices=[5, 11, 17, 23]))
+
+# TINY_CFG at widths every neck / head op of the HIP path takes (ops.neck_heads_hip_capable):
+# backbone width 128 (3x3 conv Cin % 128 == 0), 2 levels x 64 -> fusion 128 -> 256, decode head
+# 256 -> 64 -> 256 -> 19, depth head 256 -> 64 -> 64 -> 1.  score_concat_index 1 (>= 0): the
+# reference concatenates the score map onto a clone it then discards (denseclip.py:684-694, 747),
+# so training through this config is pinned too.
+MID_CFG = dict(TINY_CFG,
+               backbone=dict(type='CLIPVisionTransformer', patch_size=16, width=128, layers=2, heads=2,
+                             input_resolution=32, output_dim=128, out_indices=[0, 1]),
+               decode_head=dict(type='FPNHead', in_channels=256, channels=256, num_classes=19,
+                                align_corners=False),
+               depth_head=dict(type='FCNHeadDepth', in_channels=256, channels=64, align_corners=False),
+               neck=dict(type='ViTFeatureFusionNeck', inter_channels=64, out_channels=256),
+               score_concat_index=1)

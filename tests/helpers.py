@@ -15,7 +15,7 @@ for p in (ROOT, GOLDEN):
 
 from weights_spec import value_for  # noqa: E402
 from model_configs import (TINY_CFG, TINY_CTX_CFG, CTX_GAMMA, CITYSCAPES_CFG, CITYSCAPES_CLASSES,  # noqa: E402,F401
-                           VITL14_CFG)
+                           VITL14_CFG, MID_CFG)
 
 
 def manifest(name):

@@ -205,3 +205,54 @@ def test_align_corners_true_is_refused():
     cfg["decode_head"] = dict(cfg["decode_head"], align_corners=True)
     with pytest.raises(NotImplementedError):
         DenseCLIP(class_names=CITYSCAPES_CLASSES, **cfg)
+
+
+class _LossModel(torch.nn.Module):
+    """A stand-in for DenseCLIP's train forward (the HIP model needs a GPU): 1x1-conv logits."""
+
+    def __init__(self):
+        super().__init__()
+        self.conv = torch.nn.Conv2d(3, 19, 1)
+
+    def forward(self, img, gt_semantic_seg=None, gt_depth=None, return_loss=True):
+        return {"main_output": self.conv(img), "depth_output": None, "aux_losses": {}}
+
+
+def test_nonfinite_loss_skips_the_optimizer_step():
+    """ADVICE r2 / reference train_denseclip.py:1323: a batch whose labels are all ignored gives a
+    NaN CE; the fused AdamW step is skipped on the device (parameters, moments and step count
+    untouched, no host sync), and the next finite batch steps normally."""
+    from denseclip_vit_multimodal_amd.train import train_step
+    torch.manual_seed(0)
+    m = _LossModel()
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-2, weight_decay=0.01, fused=True)
+    img = torch.randn(2, 3, 8, 8)
+    seg = torch.randint(0, 19, (2, 8, 8))
+    train_step(m, opt, (img, seg, None, None))  # moments exist
+    w0 = m.conv.weight.detach().clone()
+    st0 = {k: v.clone() for k, v in opt.state[m.conv.weight].items()}
+    loss = train_step(m, opt, (img, torch.full_like(seg, 255), None, None))
+    assert torch.isnan(loss)
+    assert torch.equal(m.conv.weight, w0)
+    for k, v in opt.state[m.conv.weight].items():
+        assert torch.equal(v, st0[k]), k
+    assert not hasattr(opt, "found_inf")
+    train_step(m, opt, (img, seg, None, None))
+    assert not torch.equal(m.conv.weight, w0) and float(opt.state[m.conv.weight]["step"]) == 2.0
+
+
+def test_frozen_weights_keep_their_cache():
+    """an optimizer step invalidates the cached compute-dtype copies of the parameters
+    that optimizer holds only (mode R's frozen backbone keeps its casts)."""
+    from denseclip_vit_multimodal_amd import ops
+    p = torch.nn.Parameter(torch.randn(8, 4))
+    frozen = torch.nn.Parameter(torch.randn(8, 4))
+    vf = ops.WEIGHTS.get_with(frozen, torch.bfloat16, "t", lambda w: w * 1)
+    opt = torch.optim.AdamW([p], lr=0.1)
+    p.grad = torch.ones_like(p)
+    vp = ops.WEIGHTS.get_with(p, torch.bfloat16, "t", lambda w: w * 1)
+    opt.step()
+    assert ops.WEIGHTS.get_with(frozen, torch.bfloat16, "t", lambda w: w * 1) is vf
+    assert ops.WEIGHTS.get_with(p, torch.bfloat16, "t", lambda w: w * 1) is not vp
+    ops.invalidate_weight_cache()
+    assert ops.WEIGHTS.get_with(frozen, torch.bfloat16, "t", lambda w: w * 1) is not vf

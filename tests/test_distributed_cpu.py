@@ -17,7 +17,7 @@ import torch.multiprocessing as mp
 import torch.nn as nn
 import torch.nn.functional as F
 
-from helpers import TINY_CFG, CITYSCAPES_CLASSES, rel_err
+from helpers import TINY_CFG, TINY_CTX_CFG, CITYSCAPES_CLASSES, rel_err
 
 
 class _HeadsOnly(nn.Module):
@@ -133,10 +133,14 @@ def test_rank_shards_are_distinct():
     assert 0.05 < frac_ignore < 0.15 and int(seg[seg != 255].max()) < 19
 
 
-def test_wrap_ddp_leaves_gradless_parameters_out(tmp_path):
+@pytest.mark.parametrize("cfg", [TINY_CFG, TINY_CTX_CFG, dict(TINY_CTX_CFG, score_concat_index=2)],
+                         ids=["tiny", "ctx", "ctx_concat2"])
+def test_wrap_ddp_leaves_gradless_parameters_out(tmp_path, cfg):
     """wrap_ddp on the whole DenseCLIP (gloo, world size 1): the trainable parameters that get no
-    gradient in this config (score branch, unused CLIP projection; top-level ones included —
-    DDP names them '.gamma') are not in the reducer, everything else trainable is."""
+    gradient (the no_grad score branch — contexts, gamma, projections, ContextDecoder — for any
+    score_concat_index, and the unused CLIP projection; top-level ones included — DDP names them
+    '.gamma') are not in the reducer, everything else trainable is.  The two-step DDP run of such a
+    config is tests/test_gpu_dropin_heads.py::test_score_concat_and_context_decoder_train_under_ddp."""
     import torch.distributed as dist
     from denseclip_vit_multimodal_amd import DenseCLIP
     from denseclip_vit_multimodal_amd.train import freeze_for_mode, gradless_parameter_names, wrap_ddp
@@ -144,10 +148,12 @@ def test_wrap_ddp_leaves_gradless_parameters_out(tmp_path):
     os.environ["MASTER_PORT"] = str(_free_port())
     dist.init_process_group("gloo", rank=0, world_size=1)
     try:
-        m = DenseCLIP(class_names=CITYSCAPES_CLASSES, **TINY_CFG)
+        m = DenseCLIP(class_names=CITYSCAPES_CLASSES, **cfg)
         freeze_for_mode(m, "F")
         dead = set(gradless_parameter_names(m))
         assert {"gamma", "contexts", "backbone.proj"} <= dead
+        cd = {n for n, _ in m.named_parameters() if n.startswith("context_decoder.")}
+        assert cd <= dead and (cd or cfg.get("context_decoder") is None)
         ddp = wrap_ddp(m)
         managed = {id(p) for p in ddp._module_parameters}
         for n, p in m.named_parameters():

@@ -130,3 +130,41 @@ def test_vit_block_hip_graph_capture_fwd_bwd():
     for n, p in blk.named_parameters():
         if n in gw_ref:  # LayerNorm weight / bias gradients are summed with float atomics (order varies)
             assert rel_err(p.grad, gw_ref[n]) < 1e-5, (n, rel_err(p.grad, gw_ref[n]))
+
+
+def test_custom_ops_reject_bad_dtypes_and_sizes():
+    """the ops check the f32 vectors and side inputs the kernels index by the GEMM / BN
+    widths — a half-precision bias, a mis-sized aux or db, mismatched weight-gradient operands or
+    16-bit running statistics raise instead of reading or writing past a buffer."""
+    bf = torch.bfloat16
+    A = torch.randn(256, 128, device=DEV).to(bf)
+    B = torch.randn(64, 128, device=DEV).to(bf)
+    good = torch.randn(64, device=DEV)
+    with pytest.raises(RuntimeError, match="float32"):
+        D().gemm(A, B, 0, good.half(), None, bf, 1.0)
+    with pytest.raises(RuntimeError, match="elements"):
+        D().gemm(A, B, 0, torch.randn(63, device=DEV), None, bf, 1.0)
+    with pytest.raises(RuntimeError, match=r"\(M, N\)"):
+        D().gemm(A, B, 2, good, torch.randn(256, 32, device=DEV), torch.float32, 1.0)
+    with pytest.raises(RuntimeError, match=r"\(M, N\)"):
+        D().gemm(A, B, 3, None, None, bf, 1.0)
+    with pytest.raises(RuntimeError, match="scale"):
+        D().gemm(A, B, 5, good, torch.randn(32, device=DEV), bf, 1.0)
+    with pytest.raises(RuntimeError, match="elements"):
+        D().gemm_gelu(A, B, torch.randn(65, device=DEV))
+    dy = torch.randn(256, 64, device=DEV)
+    with pytest.raises(RuntimeError, match="dtypes differ"):
+        D().weight_grad(dy.half(), A, 1.0, torch.zeros(64, device=DEV))
+    with pytest.raises(RuntimeError, match="elements"):
+        D().weight_grad(dy.to(bf), A, 1.0, torch.zeros(32, device=DEV))
+    x = torch.randn(2, 64, 4, 4, device=DEV).to(bf).contiguous(memory_format=torch.channels_last)
+    w, b = torch.ones(64, device=DEV), torch.zeros(64, device=DEV)
+    with pytest.raises(RuntimeError, match="float32"):
+        D().bn_eval(x, w, b, torch.zeros(64, device=DEV).half(), torch.ones(64, device=DEV), 1e-5, False)
+    with pytest.raises(RuntimeError, match="elements"):
+        D().bn_fwd(x, w[:32], b, None, None, 0.1, 1e-5, False)
+    with pytest.raises(RuntimeError, match="elements"):
+        D().layernorm_fwd(torch.randn(8, 64, device=DEV), w[:32], b, torch.float32, 1e-5)
+    # and the good calls still run
+    D().gemm(A, B, 0, good, None, bf, 1.0)
+    D().bn_eval(x, w, b, torch.zeros(64, device=DEV), torch.ones(64, device=DEV), 1e-5, True)

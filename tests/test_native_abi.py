@@ -61,3 +61,16 @@ def test_argument_errors_are_reported(call, needle):
 def test_missing_library_fails_loudly(tmp_path):
     with pytest.raises(N.NativeError):
         N.load(str(tmp_path / "nope.so"))
+
+
+def test_dclip_lib_mismatch_raises(tmp_path):
+    """DCLIP_LIB pointing at another libdclip.so than the one libdclip_torch.so binds
+    (its own directory) raises instead of configuring a library no op calls."""
+    import subprocess
+    import sys
+    other = tmp_path / "libdclip.so"
+    other.write_bytes(b"")
+    code = "from denseclip_vit_multimodal_amd import _torch_ops; _torch_ops.load()"
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True,
+                       env=dict(os.environ, DCLIP_LIB=str(other)), timeout=300)
+    assert r.returncode != 0 and "DCLIP_LIB" in r.stderr, r.stderr[-2000:]

@@ -3,11 +3,12 @@
 The reference has no tests or golden vectors of its own; these fixtures
 were generated from /root/reference by tests/golden/gen_golden.py.
 """
+import pytest
 import torch
 import torch.nn.functional as F
 
-from helpers import (TINY_CFG, TINY_CTX_CFG, CITYSCAPES_CFG, VITL14_CFG, spec_state_dict, golden, class_tokens,
-                     images, rel_err, stats)
+from helpers import (TINY_CFG, TINY_CTX_CFG, CITYSCAPES_CFG, VITL14_CFG, MID_CFG, spec_state_dict, golden,
+                     class_tokens, images, rel_err, stats)
 from oracle import denseclip_oracle as O
 
 
@@ -94,13 +95,27 @@ def test_silog_restatement():
     assert abs(float(O.silog_loss(pred, tgt, m)) - float(ref)) < 1e-6
 
 
-def test_tiny_train_step_matches_reference():
+def test_mid_eval_matches_reference():
+    """MID_CFG (the widths the HIP neck / heads take; score_concat_index 1) in eval."""
+    g = golden("mid_eval")
+    out, _ = _fwd("mid", MID_CFG, g["input"])
+    for i in range(2):
+        assert rel_err(out["maps"][i], g[f"map{i}"]) < 1e-5
+    for k in ("text", "score", "seg_low", "depth_low", "seg", "depth"):
+        assert rel_err(out[k], g[k]) < 1e-5, k
+
+
+@pytest.mark.parametrize("name,cfg", [("tiny", TINY_CFG), ("mid", MID_CFG)])
+def test_train_step_matches_reference(name, cfg):
     """Loss and sampled gradients of one seeded train step (BN batch stats, no dropout)."""
-    g = golden("tiny_train")
-    p = spec_state_dict("tiny")
+    g = golden(name + "_train")
+    p = spec_state_dict(name)
     p = {k: (v.clone().requires_grad_(True) if v.is_floating_point() else v) for k, v in p.items()}
-    out = O.denseclip_forward(g["input"], p, class_tokens(), TINY_CFG,
+    out = O.denseclip_forward(g["input"], p, class_tokens(), cfg,
                               gt_hw=tuple(g["seg_t"].shape[-2:]), training=True)
+    if "seg_low" in g:
+        assert rel_err(out["seg_low"], g["seg_low"]) < 1e-5
+        assert rel_err(out["depth_low"], g["depth_low"]) < 1e-5
     ce = F.cross_entropy(out["seg"], g["seg_t"], ignore_index=255)
     sl = O.silog_loss(out["depth"], g["depth_t"], g["depth_m"].bool())
     loss = ce + 0.1 * sl
@@ -117,7 +132,7 @@ def test_tiny_train_step_matches_reference():
         ref = float(g[k])
         assert abs(n - ref) <= 1e-4 * ref + 1e-7, (name, n, ref)
         checked += 1
-    assert checked > 50
+    assert checked > 50 if name == "tiny" else checked > 40
 
 
 def test_train_step_gradient_conditioning():
