@@ -166,6 +166,7 @@ __device__ __forceinline__ void gemm_epilogue(f32x16 (&acc)[2][2], char* smem, i
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] += rsd[e];
             store8<float>((float*)C + (int64_t)m * ldc + nb, v, full, N - nb);
+            if (C2 != nullptr) store8<T>((T*)C2 + (int64_t)m * ldc2 + nb, v, full, N - nb);  // 16-bit copy
         } else if constexpr (EPI == DCLIP_EPI_GELU_BWD) {
             float z[8];
             load8<T>((const T*)aux + (int64_t)m * ld_aux + nb, z, full, N - nb);
@@ -284,6 +285,7 @@ __device__ __forceinline__ void epi_row8(float (&v)[8], int m, int nb, int N, co
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += rsd[e];
         store8<float>((float*)C + (int64_t)m * ldc + nb, v, full, rem);
+        if (C2 != nullptr) store8<T>((T*)C2 + (int64_t)m * ldc2 + nb, v, full, rem);  // 16-bit copy
     } else if constexpr (EPI == DCLIP_EPI_GELU_BWD) {
         float z[8];
         load8<T>((const T*)aux + (int64_t)m * ld_aux + nb, z, full, rem);
@@ -702,6 +704,11 @@ __device__ __forceinline__ void pers_epilogue(const f32x4 (&acc)[Cfg::NB][Cfg::M
                     if constexpr (EPI == DCLIP_EPI_RESIDUAL)
                         v[h] += *(const f32x4*)((const float*)aux + row * ld_aux + col + 16 * h);
                     store4_out<OutT>((OutT*)C + row * ldc + col + 16 * h, v[h]);
+                }
+                if constexpr (EPI == DCLIP_EPI_RESIDUAL) {
+                    // the 16-bit copy of the new residual (a read-out map's token buffer): C2 is
+                    // null or set for the whole launch, so every lane takes the pair exchange
+                    if (C2 != nullptr) store_pair16<T>((T*)C2 + row * ldc2, col, v[0], v[1], lq);
                 }
             } else if constexpr (EPI == DCLIP_EPI_STORE) {
                 store_pair16<OutT>((OutT*)C + row * ldc, col, v[0], v[1], lq);

@@ -162,6 +162,27 @@ Tensor gemm(const Tensor& A, const Tensor& B, int64_t epi, const c10::optional<T
     return out;
 }
 
+// out = aux + A B^T + bias (f32 residual epilogue) and lp = (A's dtype) out in the same epilogue:
+// the new residual stream and its 16-bit copy (a per-layer read-out map's token buffer,
+// models.py:577-582) without a separate cast pass
+std::tuple<Tensor, Tensor> gemm_residual_lp(const Tensor& A, const Tensor& B, const c10::optional<Tensor>& bias,
+                                            const Tensor& aux) {
+    gemm_checks(A, B);
+    c10::DeviceGuard g(A.device());
+    const int64_t M = A.size(0), N = B.size(0), K = A.size(1);
+    check_vec(bias, N, "gemm_residual_lp bias");
+    check_gpu(aux, "aux", false);
+    TORCH_CHECK(aux.dim() == 2 && aux.size(0) == M && aux.size(1) == N && aux.stride(1) == 1 &&
+                    aux.scalar_type() == at::kFloat,
+                "gemm_residual_lp: aux must be the f32 (M, N) residual");
+    Tensor out = at::empty({M, N}, like(A, at::kFloat)), lp = at::empty({M, N}, A.options());
+    DCLIP_CALL(dclip_gemm(DCLIP_EPI_RESIDUAL, dt_code(A.scalar_type()), A.data_ptr(), A.stride(0), B.data_ptr(),
+                          B.stride(0), M, N, K, 1, 1.0f, nullptr, optr<float>(bias), aux.data_ptr(), DCLIP_F32,
+                          aux.stride(0), out.data_ptr(), DCLIP_F32, out.stride(0), lp.data_ptr(), lp.stride(0),
+                          stream_of(A)));
+    return {out, lp};
+}
+
 // z = A B^T + bias, h = quick_gelu(z)  (c_fc + QuickGELU, models.py:277-281, 252-254)
 std::tuple<Tensor, Tensor> gemm_gelu(const Tensor& A, const Tensor& B, const c10::optional<Tensor>& bias) {
     gemm_checks(A, B);
@@ -673,6 +694,7 @@ TORCH_LIBRARY(dclip, m) {
     m.def("gemm(Tensor A, Tensor B, int epi, Tensor? bias, Tensor? aux, ScalarType out_dtype, float alpha, "
           "Tensor? scale=None) -> Tensor");
     m.def("gemm_gelu(Tensor A, Tensor B, Tensor? bias) -> (Tensor, Tensor)");
+    m.def("gemm_residual_lp(Tensor A, Tensor B, Tensor? bias, Tensor aux) -> (Tensor, Tensor)");
     m.def("weight_grad(Tensor dy, Tensor x, float alpha, Tensor(a!)? db, Tensor? scale=None) -> Tensor");
     m.def("gemm_tn(Tensor A, Tensor B) -> Tensor");
     m.def("cast(Tensor x, ScalarType dtype, float scale, Tensor? scale_t=None) -> Tensor");
@@ -721,6 +743,7 @@ TORCH_LIBRARY_IMPL(dclip, CUDA, m) {
     m.impl("layernorm_bwd_lp", &layernorm_bwd_lp);
     m.impl("gemm", &gemm);
     m.impl("gemm_gelu", &gemm_gelu);
+    m.impl("gemm_residual_lp", &gemm_residual_lp);
     m.impl("weight_grad", &weight_grad);
     m.impl("gemm_tn", &gemm_tn);
     m.impl("cast", &cast);

@@ -117,14 +117,18 @@ def layernorm_bwd(dy, x, w, mean, rstd, dw, db, res=None, lp_dtype=None):
     return D().layernorm_bwd_lp(dy, x, w, mean, rstd, res, dw, db, lp_dtype)
 
 
-def gemm(A, B, epi=N.EPI_STORE, bias=None, aux=None, out_dtype=None, alpha=1.0, scale=None):
+def gemm(A, B, epi=N.EPI_STORE, bias=None, aux=None, out_dtype=None, alpha=1.0, scale=None, lp_copy=False):
     """out[m][n] = alpha * sum_k A[m][k] B[n][k] (+ epilogue).  A: (M, K), B: (N, K).
     EPI_GELU returns (z, quick_gelu(z)).  scale: a grad_scale() buffer whose 1/s also
-    multiplies the result (read on the device)."""
+    multiplies the result (read on the device).  lp_copy (EPI_RESIDUAL only): returns (out, a
+    copy of out in A's dtype) written by the same epilogue."""
     _check(A, B, bias, aux, scale)
     assert A.shape[1] == B.shape[1], (A.shape, B.shape)
     e0 = _tic()
-    if epi == N.EPI_GELU:
+    if lp_copy:
+        assert epi == N.EPI_RESIDUAL and alpha == 1.0 and scale is None and out_dtype in (None, torch.float32)
+        out = D().gemm_residual_lp(A, B, bias, aux)
+    elif epi == N.EPI_GELU:
         out = D().gemm_gelu(A, B, bias)
     else:
         odt = out_dtype or (torch.float32 if epi == N.EPI_RESIDUAL else A.dtype)
@@ -333,9 +337,14 @@ class _Cast:
     address, the last optimizer step that held it and the global generation are all unchanged."""
 
     @staticmethod
+    def stamp(p):
+        w = p.detach()
+        return (_GENERATION[0], p.__dict__.get("_dclip_step", 0), w._version, w.data_ptr())
+
+    @staticmethod
     def _lookup(p, key):
         w = p.detach()
-        stamp = (_GENERATION[0], p.__dict__.get("_dclip_step", 0), w._version, w.data_ptr())
+        stamp = _Cast.stamp(p)
         cache = p.__dict__.get("_dclip_cache")
         if cache is None:
             cache = p.__dict__["_dclip_cache"] = {}
@@ -452,7 +461,11 @@ class BlockFn(torch.autograd.Function):
                                dp[0])
         xh2, mu2, rs2 = layernorm_fwd(xm, ln2w.detach(), ln2b.detach(), cdt)
         z, h = gemm(xh2, WEIGHTS.get(w1, cdt), N.EPI_GELU, bias=b1.detach())
-        if dp is None:
+        lp = None
+        if dp is None and ro is not None and ro[2] == cdt:
+            # the read-out map's token buffer comes out of the residual epilogue itself
+            xo, lp = gemm(h, WEIGHTS.get(w2, cdt), N.EPI_RESIDUAL, bias=b2.detach(), aux=xm, lp_copy=True)
+        elif dp is None:
             xo = gemm(h, WEIGHTS.get(w2, cdt), N.EPI_RESIDUAL, bias=b2.detach(), aux=xm)
         else:
             xo = row_scale_add(xm, gemm(h, WEIGHTS.get(w2, cdt), bias=b2.detach(), out_dtype=torch.float32), dp[1])
@@ -463,7 +476,7 @@ class BlockFn(torch.autograd.Function):
             return xo
         gh, gw, mdt = ro[:3]
         ctx.set_materialize_grads(False)  # an unused map (or block output) brings None, not zeros
-        buf = xo.clone() if mdt == torch.float32 else cast(xo, mdt)
+        buf = lp if lp is not None else (xo.clone() if mdt == torch.float32 else cast(xo, mdt))
         return xo, buf.as_strided((B, C, gh, gw), (Ntok * C, 1, gw * C, C), C)
 
     @staticmethod
@@ -1142,6 +1155,26 @@ def conv1x1_supported(xmap, weight):
 
 
 # ============================================================================ FCN heads
+def _merged_tail(w1, b1, wc, bc, cdt, Kp):
+    """The merged head tail (Kp x Cin weight Wc W1 in cdt, zero rows past K; f32 bias Wc b1 + bc),
+    cached on the classifier weight until any of the four parameters changes (the weight cache's
+    stamps: optimizer step, version, storage) — not recomputed by torch matmuls every forward."""
+    stamp = (cdt, Kp) + tuple(_Cast.stamp(p) for p in (w1, b1, wc, bc))
+    ent = wc.__dict__.get("_dclip_merged")
+    if ent is not None and ent[0] == stamp:
+        return ent[1], ent[2]
+    C1, Cin, K = w1.shape[0], w1.shape[1], wc.shape[0]
+    with torch.autocast("cuda", enabled=False), torch.no_grad():
+        W1m = w1.detach().reshape(C1, Cin).float()
+        Wcm = wc.detach().reshape(K, C1).float()
+        Wp = torch.zeros(Kp, Cin, dtype=cdt, device=w1.device)
+        Wp[:K] = Wcm @ W1m
+        bp = torch.zeros(Kp, dtype=torch.float32, device=w1.device)
+        bp[:K] = Wcm @ b1.detach().float() + bc.detach().float()
+    wc.__dict__["_dclip_merged"] = (stamp, Wp, bp)
+    return Wp, bp
+
+
 class MergedPointwiseFn(torch.autograd.Function):
     """The FCN head's tail — 1x1 conv (Cin -> C1, bias) then the classifier 1x1 conv (C1 -> K,
     bias) (torchvision FCNHead + DenseCLIP's classifier, reference denseclip.py:305-309,
@@ -1156,15 +1189,7 @@ class MergedPointwiseFn(torch.autograd.Function):
         B, Cin, H, W = y.shape
         C1, K = w1.shape[0], wc.shape[0]
         Kp = _pad64(K)
-        with torch.autocast("cuda", enabled=False):
-            W1m = w1.detach().reshape(C1, Cin).float()
-            Wcm = wc.detach().reshape(K, C1).float()
-            Wm = Wcm @ W1m
-            bm = Wcm @ b1.detach().float() + bc.detach().float()
-        Wp = torch.zeros(Kp, Cin, dtype=cdt, device=y.device)
-        Wp[:K] = Wm
-        bp = torch.zeros(Kp, dtype=torch.float32, device=y.device)
-        bp[:K] = bm
+        Wp, bp = _merged_tail(w1, b1, wc, bc, cdt, Kp)
         y2 = y.to(cdt).permute(0, 2, 3, 1).reshape(B * H * W, Cin)
         if not y2.is_contiguous():
             y2 = y2.contiguous()

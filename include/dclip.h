@@ -56,7 +56,7 @@ extern "C" {
 /* GEMM epilogues (dclip_gemm) */
 #define DCLIP_EPI_STORE 0      /* C = acc (+ bias[n])                                  */
 #define DCLIP_EPI_GELU 1       /* C = z = acc + bias ; C2 = z * sigmoid(1.702 z)       */
-#define DCLIP_EPI_RESIDUAL 2   /* C(f32) = aux(f32) + acc + bias   (aux may alias C)   */
+#define DCLIP_EPI_RESIDUAL 2   /* C(f32) = aux(f32) + acc + bias (aux may alias C); C2, when set, gets the same values in ab_dt */
 #define DCLIP_EPI_GELU_BWD 3   /* C = acc * quick_gelu'(aux)       (aux = z)           */
 #define DCLIP_EPI_SPLITK 4     /* C(f32) = sum over K splits (+ bias): partial f32 slabs
                                   in the caller's workspace aux (splits*M*N f32), then
@@ -78,7 +78,7 @@ int dclip_abi_version(void);
 #define DCLIP_OPT_ATTN_DKDV_QS 5     /* dK/dV pass query rows per barrier: 64 (default) or 128 */
 #define DCLIP_OPT_ATTN_BWD_KERNEL 7  /* 0 (default): CLS-split passes for N >= 257 (a ragged N-1 with the default pass variants only); 1: generic */
 #define DCLIP_OPT_ATTN_FWD_KERNEL 6  /* 0 (default): CLS-split kernel for N - 1 >= the query block (ragged N-1 included); 1: generic */
-#define DCLIP_OPT_ATTN_BWD_BLOCK 8   /* 0 (default): software-pipelined CLS-split dK/dV pass; 1: the unpipelined one */
+#define DCLIP_OPT_ATTN_BWD_BLOCK 8   /* 0 (default): software-pipelined CLS-split dK/dV pass; 1: the unpipelined one; 6: 64 keys per wave, AGPR dK / dV */
 #define DCLIP_OPT_GEMM_TN_COLSUM 9   /* 0 (default): the 256x256 weight-gradient kernel sums dY's columns (bias gradient) itself; 1: a separate pass */
 #define DCLIP_OPT_COUNT 10
 int dclip_set_option(int id, int value);

@@ -490,6 +490,41 @@ def test_attention_bwd_cls_split_spikes(where, spike, bwd_kernel_pair):
         assert a < 1.5 * b + 4 * TOL[torch.float16], (split, gen)
 
 
+@pytest.fixture
+def bwd_block():
+    from denseclip_vit_multimodal_amd import _native as N
+    yield lambda v: N.call("dclip_set_option", N.OPT_ATTN_BWD_BLOCK, v)
+    N.call("dclip_set_option", N.OPT_ATTN_BWD_BLOCK, 0)
+
+
+@pytest.mark.parametrize("B,H,N", [(3, 2, 257), (2, 2, 290), (2, 3, 803), (3, 2, 1345), (2, 2, 2049), (1, 2, 8193),
+                                   (1, 1, 10659)])
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+def test_attention_dkdv6_matches_dkdv5(B, H, N, dt, bwd_block):
+    """The 64-keys-per-wave dK/dV pass with AGPR accumulators (DCLIP_OPT_ATTN_BWD_BLOCK 6,
+    attention_dkdv6.hip) against fp32 autograd, and against the default dkdv5 pass on the same
+    inputs (same products, same per-key summation order: equal up to fp32 rounding), full and
+    ragged N - 1, partial last key blocks included."""
+    O = ops()
+    C = 64 * H
+    torch.manual_seed(3)
+    qkv, _ = prescale((torch.randn(B * N, 3 * C, device=DEV) * 1.5).to(dt), H)
+    dout = torch.randn(B * N, C, device=DEV).to(dt)
+    o, lse = O.attn_fwd(qkv, B, N, H, 64 ** -0.5)
+    res = []
+    for v in (0, 6):
+        bwd_block(v)
+        res.append(O.attn_bwd(qkv, o, dout, lse, B, N, H, 64 ** -0.5).float())
+    a, b = res
+    assert torch.isfinite(b).all()
+    assert rel_err(b[:, C:], a[:, C:]) < 1e-3, rel_err(b[:, C:], a[:, C:])  # dK, dV columns
+    assert torch.equal(b[:, :C], a[:, :C])  # dQ: the same dQ pass
+    if N <= 2049:
+        bwd_block(6)
+        errs = _attn_bwd_check(B, H, N, dt)
+        assert max(errs) < 4 * TOL[dt], errs
+
+
 def test_attention_bwd_full_length():
     """N = 8193 (the benchmark's sequence) through the CLS-split passes, against fp32 autograd."""
     errs = _attn_bwd_check(1, 1, 8193, torch.bfloat16)

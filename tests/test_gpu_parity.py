@@ -378,3 +378,22 @@ def test_ddp_two_ranks_one_gpu_graphed_text_path():
                        cwd=root, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "parameters identical across ranks: True" in r.stdout
+
+
+@pytest.mark.parametrize("img", ["fp32", "bf16"])
+def test_ddp_two_ranks_mode_f_gradients_match_single_process(img):
+    """mode F DDP (ViT BlockFn backward, HIP neck / heads; gloo, 2 ranks on the
+    GPU) — every post-all-reduce gradient equals the single-process average of the two shards'
+    gradients (per-rank BatchNorm, as in the reference), and the ranks agree."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29563" if img == "fp32" else "29564",
+                        os.path.join(root, "tools", "ddp_gpu_check.py"), "--grads", "--img", img],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    print(r.stdout[-1500:])
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    assert "grads check ok: True" in r.stdout

@@ -168,3 +168,21 @@ def test_custom_ops_reject_bad_dtypes_and_sizes():
     # and the good calls still run
     D().gemm(A, B, 0, good, None, bf, 1.0)
     D().bn_eval(x, w, b, torch.zeros(64, device=DEV), torch.ones(64, device=DEV), 1e-5, True)
+
+
+@pytest.mark.parametrize("M", [520, 65544])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_gemm_residual_lp_copy(M, dt):
+    """The residual epilogue's 16-bit copy (the read-out map's token buffer, BlockFn): the f32
+    output equals the plain residual GEMM and the copy equals its cast, bit for bit — both the
+    persistent kernel's epilogue and the row-tail path (M = 8 x 8193 = 65544 rows)."""
+    A = torch.randn(M, 768, device=DEV).to(dt)
+    B = torch.randn(256, 768, device=DEV).to(dt)
+    bias = torch.randn(256, device=DEV)
+    aux = torch.randn(M, 256, device=DEV)
+    out, lp = D().gemm_residual_lp(A, B, bias, aux)
+    ref = D().gemm(A, B, 2, bias, aux, torch.float32, 1.0)
+    assert torch.equal(out, ref)
+    assert lp.dtype == dt and torch.equal(lp, ref.to(dt))
+    if M == 520:
+        _opcheck(D().gemm_residual_lp, (A, B, bias, aux))
