@@ -1,5 +1,5 @@
-// Clock probe: does the MFMA shape change the clock the chip holds under an attention-like
-// load?  Two kernels with the same FLOPs, operand bytes and VALU work per iteration, one on
+// Clock probe: the dense bf16 MFMA rate the chip sustains on random operands (MFMA-only loops),
+// and does the MFMA shape change the clock the chip holds under an attention-like load?  Two kernels with the same FLOPs, operand bytes and VALU work per iteration, one on
 // v_mfma_f32_32x32x16_bf16 (as the attention kernels), one on v_mfma_f32_16x16x32_bf16:
 //   S = K Q^T chain over 4 (or 2) K-steps from zero, P = exp2(S * c - 1), row sums += P,
 //   P packed to bf16 and fed as the B operand of O += V P.  Operands are re-read from LDS
@@ -25,7 +25,34 @@ __global__ __launch_bounds__(256, 2) void probe(const __bf16* __restrict__ src, 
     __syncthreads();
     float rs = 0.f;
     const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
-    if constexpr (SHAPE == 32) {
+    if constexpr (SHAPE == 0 || SHAPE == 1) {
+        // the MFMA-only ceiling on random operands: 16 v_mfma_f32_32x32x16_bf16 per iteration into
+        // four independent accumulators, no VALU; SHAPE 0 keeps the operands in registers, SHAPE 1
+        // re-reads them from LDS every iteration (one ds_read_b128 per MFMA)
+        f32x16 o[4] = {};
+        bf16x8 a[4], b[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            a[k] = lds8(sm + lane * 16 + 1024 * k);
+            b[k] = lds8(sm + 8192 + lane * 16 + 1024 * k);
+        }
+        for (int it = 0; it < iters; ++it) {
+            if constexpr (SHAPE == 1) {
+                const char* base = sm + ((it * 4096) & 16383) + lane * 16;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    a[k] = lds8(base + 1024 * k);
+                    b[k] = lds8(base + 8192 + 1024 * k);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) o[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[(k + j) & 3], b[k], o[j], 0, 0, 0);
+        }
+        for (int j = 0; j < 4; ++j)
+            for (int r = 0; r < 16; ++r) rs += o[j][r];
+    } else if constexpr (SHAPE == 32) {
         f32x16 o[2] = {};
         for (int it = 0; it < iters; ++it) {
             const char* base = sm + ((it * 4096) & 16383) + lane * 16;
@@ -125,8 +152,9 @@ void run(const __bf16* src, float* out, unsigned long long* st, int iters, int b
         free(h);
         // FLOP per iteration per wave: 16 (32x32x16) MFMAs = 32 (16x16x32) = 524288
         const double flop = 524288.0 * 4 * blocks * (double)iters;
-        printf("mfma %dx%d: %.3f ms  %.1f TFLOP/s  in-kernel clock %.0f MHz\n", SHAPE, SHAPE, ms, flop / ms / 1e9,
-               clk / blocks);
+        const char* name = SHAPE == 0 ? "mfma-only 32x32 (register operands)" : SHAPE == 1 ? "mfma-only 32x32 (LDS operands)"
+                         : SHAPE == 32 ? "attention-like 32x32" : "attention-like 16x16";
+        printf("%s: %.3f ms  %.1f TFLOP/s  in-kernel clock %.0f MHz\n", name, ms, flop / ms / 1e9, clk / blocks);
     }
     hipEventDestroy(e0);
     hipEventDestroy(e1);
@@ -146,6 +174,8 @@ int main(int argc, char** argv) {
     for (int i = 0; i < 16384; ++i) h[i] = (__bf16)((rand() / (float)RAND_MAX - 0.5f) * 4.f);
     hipMemcpy(src, h, 32768, hipMemcpyHostToDevice);
     for (int round = 0; round < 2; ++round) {
+        run<0>(src, out, st, iters, blocks);
+        run<1>(src, out, st, iters, blocks);
         run<32>(src, out, st, iters, blocks);
         run<16>(src, out, st, iters, blocks);
     }
