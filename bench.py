@@ -301,7 +301,7 @@ def main():
         # per launch, 2.5x the forward's): it is the headline roofline whenever it ran
         rf_bwd = None
         if n_ab:
-            rf_bwd = {"kernel": "attn_bwd_dq2_kernel + attn_bwd_dkdv5_kernel (+ row-0 passes)" if cls_split
+            rf_bwd = {"kernel": "attn_bwd_dq2_kernel + attn_bwd_dkdv6_kernel (+ row-0 passes)" if cls_split
                       else "attn_bwd_dq_kernel + attn_bwd_dkdv_kernel",
                       "bound": "mfma", "achieved": round(ach_b, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                       "frac": round(ach_b / PEAK_BF16_TFLOPS, 4), "traffic": traffic_b,

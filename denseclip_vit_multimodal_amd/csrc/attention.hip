@@ -2212,7 +2212,7 @@ bool bwd2_launch(const void* qkv, const void* o, const void* dout, const float* 
     // a ragged N - 1 (partial last query / key blocks, masked tails) in the default passes only
     const bool ragged = (N - 1) % 256 != 0;
     const int bwd_block = dclip_option(DCLIP_OPT_ATTN_BWD_BLOCK);
-    if (ragged && (dclip_option(DCLIP_OPT_ATTN_DQ_WAVES) == 4 || (bwd_block != 0 && bwd_block != 6)))
+    if (ragged && (dclip_option(DCLIP_OPT_ATTN_DQ_WAVES) == 4 || (bwd_block != 0 && bwd_block != 5 && bwd_block != 6)))
         return false;
     const int nsplit = (N + R0_CHUNK - 1) / R0_CHUNK;
     float* ws0 = delta + (int64_t)B * H * N;
@@ -2230,10 +2230,10 @@ bool bwd2_launch(const void* qkv, const void* o, const void* dout, const float* 
     attn_bwd_row0_dkdv_part<T><<<B * H * nsplit, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, ws0, N, H,
                                                               nsplit);
     attn_bwd_row0_dkdv_merge<T><<<B * H, 64, 0, st>>>(ws0, (T*)dqkv, N, H, nsplit, 1.0f / LOG2E);
-    if (bwd_block == 6)  // 64 keys per wave, one wave per SIMD, AGPR dK / dV (attention_dkdv6.hip)
+    if (bwd_block == 0 || bwd_block == 6)  // default: 64 keys per wave, one wave per SIMD, AGPR dK / dV
         attn_bwd_dkdv6_launch(std::is_same<T, bf16>::value ? DCLIP_BF16 : DCLIP_F16, qkv, dout, lse, delta, nstat,
                               nstat + (int64_t)B * H * N, dqkv, B, N, H, 1.0f / LOG2E, st);
-    else if (bwd_block == 0)  // default: pipelined, 32 keys per wave, 2 waves per SIMD
+    else if (bwd_block == 5)  // pipelined, 32 keys per wave, 2 waves per SIMD (round 2's default)
         attn_bwd_dkdv5_kernel<T><<<B * H * ((N - 1 + 127) / 128), 256, 0, st>>>(
             (const T*)qkv, (const T*)dout, lse, delta, nstat, nstat + (int64_t)B * H * N, (T*)dqkv, N, H, 1.0f / LOG2E);
     else if (dclip_option(DCLIP_OPT_ATTN_DKDV_WAVES) == 8)  // 256 keys per workgroup (one Q / dO slice per 256 keys)

@@ -17,6 +17,8 @@
 // since LDS-DMA writes lane-linearly — which makes the ds_read_b128 fragment reads
 // bank-conflict free.  Block ids are remapped XCD-aware so the tiles of one A row
 // panel run on one XCD and share its L2.
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -658,6 +660,37 @@ __device__ __forceinline__ void store4_out(OutT* p, const f32x4& v) {
     }
 }
 
+// acc[j] += b . a[j] for j < 8 (v_mfma_f32_16x16x32, accumulators in AGPRs).  Opens with s_nop 1:
+// a fragment (or a zeroed accumulator) may have been written by VALU just before (the compiler pads
+// no hazard into an asm statement).
+template <typename T>
+__device__ __forceinline__ void tn_mfma_row(f32x4 (&acc)[8], const typename Mfma<T>::frag& b,
+                                            const typename Mfma<T>::frag (&a)[8]) {
+#define TN_MFMA8(OP)                                                                                         \
+    asm volatile("s_nop 1\n\t" OP " %0, %8, %9, %0\n\t" OP " %1, %8, %10, %1\n\t" OP " %2, %8, %11, %2\n\t" OP \
+                 " %3, %8, %12, %3\n\t" OP " %4, %8, %13, %4\n\t" OP " %5, %8, %14, %5\n\t" OP                   \
+                 " %6, %8, %15, %6\n\t" OP " %7, %8, %16, %7"                                                   \
+                 : "+a"(acc[0]), "+a"(acc[1]), "+a"(acc[2]), "+a"(acc[3]), "+a"(acc[4]), "+a"(acc[5]),         \
+                   "+a"(acc[6]), "+a"(acc[7])                                                                  \
+                 : "v"(b), "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]),         \
+                   "v"(a[7]))
+    if constexpr (std::is_same<T, bf16>::value) TN_MFMA8("v_mfma_f32_16x16x32_bf16");
+    else TN_MFMA8("v_mfma_f32_16x16x32_f16");
+#undef TN_MFMA8
+}
+
+// the accumulators' last asm MFMA results: wait states before anything reads them (one group)
+__device__ __forceinline__ void tn_acc_fence(f32x4 (&acc)[8], bool nops) {
+    if (nops)
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7"
+                     : "+a"(acc[0]), "+a"(acc[1]), "+a"(acc[2]), "+a"(acc[3]), "+a"(acc[4]), "+a"(acc[5]),
+                       "+a"(acc[6]), "+a"(acc[7]));
+    else
+        asm volatile(""
+                     : "+a"(acc[0]), "+a"(acc[1]), "+a"(acc[2]), "+a"(acc[3]), "+a"(acc[4]), "+a"(acc[5]),
+                       "+a"(acc[6]), "+a"(acc[7]));
+}
+
 // epilogue of the persistent kernels, from the accumulators straight to global memory:
 // acc[i][j] = C[mw + 16 j + l16][nw + 16 i + 4 lq + e]
 // the per-column constants (bias, QKV scale) of a wave's columns, loaded when its tile starts so
@@ -811,13 +844,22 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_nt_pers_kernel(
                 for (int i = 0; i < Cfg::NB; ++i) fb[i] = big_frag<T, 64>(Bt, wn * Cfg::WTN + i * 16 + l16, ch);
 #pragma unroll
                 for (int j = 0; j < Cfg::MB; ++j) fa[j] = big_frag<T, 64>(At, wm * Cfg::WTM + j * 16 + l16, ch);
+                if constexpr (NW == 4) {  // 128 x 128 per wave: the accumulators as AGPR asm operands
 #pragma unroll
-                for (int j = 0; j < Cfg::MB; ++j)
+                    for (int i = 0; i < Cfg::NB; ++i) tn_mfma_row<T>(acc[i], fb[i], fa);
+                } else {
 #pragma unroll
-                    for (int i = 0; i < Cfg::NB; ++i) acc[i][j] = Mfma16<T>::mma(fb[i], fa[j], acc[i][j]);
+                    for (int j = 0; j < Cfg::MB; ++j)
+#pragma unroll
+                        for (int i = 0; i < Cfg::NB; ++i) acc[i][j] = Mfma16<T>::mma(fb[i], fa[j], acc[i][j]);
+                }
             }
             __builtin_amdgcn_sched_barrier(0);
             slot ^= 1;
+        }
+        if constexpr (NW == 4) {
+#pragma unroll
+            for (int i = 0; i < Cfg::NB; ++i) tn_acc_fence(acc[i], i == 0);
         }
         pers_epilogue<T, EPI, OutT, Cfg>(acc, pc, m0 + wm * 128, n0 + wn * Cfg::WTN, l16, lq, alpha, aux, ld_aux, C, ldc,
                                          C2, ldc2);
@@ -1152,21 +1194,28 @@ __device__ __forceinline__ void tn_stage_buf(const void* A, uint32_t abytes, con
 // the bias gradient when A is dY): the tiles in column 0 of the tile grid own them, and of their
 // waves the ones with wn == 0 (the other three hold the same A fragments) add their fragments
 // with v_dot2c beside the MFMAs -- no separate pass re-reading A from HBM.
-template <typename T, int EPI, int BKT = 64, int STAGES = 2, bool CS = false>
-__global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(const T* __restrict__ A, int64_t lda,
+//
+// NW = 8: 2 x 4 waves of 128 x 64 (two waves per SIMD); NW = 4: 2 x 2 waves of 128 x 128 (one wave
+// per SIMD): each transposed fragment read then feeds 8 MFMAs instead of 4 or 8 — 0.5 instead of
+// 0.75 LDS reads per MFMA (this pass is LDS-bound).  Its 256 accumulator registers
+// live in AGPRs as "+a" operands of inline-asm MFMAs (tn_mfma_row): left to itself, hipcc shuttled
+// them between the two files (~300 v_accvgpr copies per 128 MFMAs).
+template <typename T, int EPI, int BKT = 64, int STAGES = 2, bool CS = false, int NW = 8>
+__global__ __launch_bounds__(64 * NW, 1) void gemm_tn_big_kernel(const T* __restrict__ A, int64_t lda,
                                                              const T* __restrict__ B, int64_t ldb, int M, int N,
                                                              int Kreal, int k_chunk, int tiles_m, int tiles_n,
                                                              void* __restrict__ C, int64_t ldc, int64_t slab,
                                                              Alpha alpha_arg, float* __restrict__ colsum) {
     const float alpha = alpha_arg.get();
-    typedef BigCfg<256, 256, 2, 4, 2> Cfg;
+    typedef BigCfg<256, 256, 2, NW / 2, 2> Cfg;
     typedef typename Mfma<T>::frag frag;
     constexpr int STAGE = 2 * BKT * 512;  // A | B
-    constexpr int G = 2 * (BKT / 16);     // LDS-DMA instructions per thread per K-step
+    constexpr int PW = BKT / (2 * NW);    // 1-KiB pieces (2 rows) of each operand per wave per K-step
+    constexpr int G = 2 * PW;             // LDS-DMA instructions per thread per K-step
     __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE > Cfg::EP_BYTES ? STAGES * STAGE : Cfg::EP_BYTES];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wm = wave / 4, wn = wave % 4;
+    const int wm = wave / (NW / 2), wn = wave % (NW / 2);
     const int lq = lane >> 4;
 
     // one-dimensional grid over (K split, tile), split-major, in XCD-contiguous ranges: the
@@ -1199,7 +1248,6 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(const T* __restrict
     // arithmetic of a pointer per piece cost ~11 VALU instructions, 3 of them 64-bit multiplies,
     // per load, all of them between the barrier and the first MFMA).  Rows past Kreal fall
     // outside the buffer and read 0.
-    constexpr int PW = BKT / 16;
     const uint32_t abytes = (uint32_t)((int64_t)Kreal * lda * sizeof(T));
     const uint32_t bbytes = (uint32_t)((int64_t)Kreal * ldb * sizeof(T));
     uint32_t va[PW], vb[PW];
@@ -1247,8 +1295,12 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(const T* __restrict
             if (CS && do_cs) {                                                                                      \
                 _Pragma("unroll") for (int j = 0; j < Cfg::MB; ++j) cs[j] = frag_sum8(fa[j], cs[j]);               \
             }                                                                                                       \
-            _Pragma("unroll") for (int j = 0; j < Cfg::MB; ++j)                                                     \
-                _Pragma("unroll") for (int i = 0; i < Cfg::NB; ++i) acc[i][j] = Mfma16<T>::mma(fb[i], fa[j], acc[i][j]); \
+            if constexpr (NW == 4) {                                                                                \
+                _Pragma("unroll") for (int i = 0; i < Cfg::NB; ++i) tn_mfma_row<T>(acc[i], fb[i], fa);               \
+            } else {                                                                                                \
+                _Pragma("unroll") for (int j = 0; j < Cfg::MB; ++j)                                                 \
+                    _Pragma("unroll") for (int i = 0; i < Cfg::NB; ++i) acc[i][j] = Mfma16<T>::mma(fb[i], fa[j], acc[i][j]); \
+            }                                                                                                       \
         }                                                                                                           \
         __builtin_amdgcn_sched_barrier(0);                                                                          \
     } while (0)
@@ -1267,6 +1319,10 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(const T* __restrict
             const int col = m0 + wm * Cfg::WTM + j * 16 + (lane & 15);
             if (lq == 0 && col < M) atomicAdd(colsum + col, v * alpha);  // columns past M: clamped copies
         }
+    }
+    if constexpr (NW == 4) {
+#pragma unroll
+        for (int i = 0; i < Cfg::NB; ++i) tn_acc_fence(acc[i], i == 0);
     }
     // the split's slab (blockIdx.y is 0 on this grid, so the epilogue's own slab offset vanishes)
     float* Cs = (float*)C + (EPI == DCLIP_EPI_SPLITK ? (int64_t)split * slab : 0);
@@ -1975,16 +2031,18 @@ extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda
     gemm_tn_kernel<T, EPI, float><<<grid, 256, 0, st>>>((const T*)A, lda, (const T*)B, ldb, (int)M, (int)N,   \
                                                         (int)K, k_chunk, tiles_m, tiles_n, nullptr, OUT,        \
                                                         EPI == DCLIP_EPI_SPLITK ? N : ldc, (int64_t)M * N, alpha)
-#define TN_BIG_V(T, EPI, OUT, BKT, STG, CS)                                                                    \
-    gemm_tn_big_kernel<T, EPI, BKT, STG, CS><<<dim3(tm2 * tn2 * splits), 512, 0, st>>>(                        \
+#define TN_BIG_V(T, EPI, OUT, BKT, STG, CS, NW)                                                                \
+    gemm_tn_big_kernel<T, EPI, BKT, STG, CS, NW><<<dim3(tm2 * tn2 * splits), 64 * NW, 0, st>>>(                \
         (const T*)A, lda, (const T*)B, ldb, (int)M, (int)N, (int)K, k_chunk, tm2, tn2, OUT,                     \
         EPI == DCLIP_EPI_SPLITK ? N : ldc, (int64_t)M * N, alpha, colsum_a)
 #define TN_BIG(T, EPI, OUT)                                                                                    \
     do {                                                                                                       \
-        if (tn_opt == 2) TN_BIG_V(T, EPI, OUT, 32, 4, false);                                                  \
-        else if (tn_opt == 3) TN_BIG_V(T, EPI, OUT, 32, 5, false);                                             \
-        else if (fused_cs) TN_BIG_V(T, EPI, OUT, 64, 2, true);                                                 \
-        else TN_BIG_V(T, EPI, OUT, 64, 2, false);                                                              \
+        if (tn_opt == 2) TN_BIG_V(T, EPI, OUT, 32, 4, false, 8);                                               \
+        else if (tn_opt == 3) TN_BIG_V(T, EPI, OUT, 32, 5, false, 8);                                          \
+        else if (tn_opt == 4 && fused_cs) TN_BIG_V(T, EPI, OUT, 64, 2, true, 4);                               \
+        else if (tn_opt == 4) TN_BIG_V(T, EPI, OUT, 64, 2, false, 4);                                          \
+        else if (fused_cs) TN_BIG_V(T, EPI, OUT, 64, 2, true, 8);                                              \
+        else TN_BIG_V(T, EPI, OUT, 64, 2, false, 8);                                                           \
     } while (0)
     const int tm2 = (int)((M + 255) / 256), tn2 = (int)((N + 255) / 256);
     if (epilogue == DCLIP_EPI_STORE) {

@@ -196,7 +196,7 @@ def tn_tile(request):
     N.call("dclip_set_option", N.OPT_GEMM_TN_TILE, 0)
 
 
-@pytest.mark.parametrize("tn_tile", [0, 1], indirect=True)
+@pytest.mark.parametrize("tn_tile", [0, 1, 4], indirect=True)
 @pytest.mark.parametrize("M,N,K", [(777, 256, 128), (65544 // 8, 768, 3072), (5000, 2304, 768), (300, 264, 520)])
 def test_weight_grad_splitk(M, N, K, tn_tile):
     O = ops()
@@ -208,9 +208,10 @@ def test_weight_grad_splitk(M, N, K, tn_tile):
     assert rel_err(db, dy.float().sum(0)) < 1e-5
 
 
+@pytest.mark.parametrize("tn_tile", [0, 4], indirect=True)
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("M,N,K", [(65544, 768, 768), (5000, 2304, 768), (300, 264, 520), (4100, 3072, 768)])
-def test_weight_grad_fused_bias_sum(M, N, K, dt):
+def test_weight_grad_fused_bias_sum(M, N, K, dt, tn_tile):
     """The 256x256 TN kernel's folded column sums (bias gradient) == the separate colsum pass
     (DCLIP_OPT_GEMM_TN_COLSUM 1) and torch, with a host alpha; dW is unaffected by the fold."""
     from denseclip_vit_multimodal_amd import _native as NT
@@ -229,7 +230,7 @@ def test_weight_grad_fused_bias_sum(M, N, K, dt):
     assert rel_err(db, 0.5 * dy.double().sum(0)) < 1e-6
 
 
-@pytest.mark.parametrize("tn_tile", [0, 1], indirect=True)
+@pytest.mark.parametrize("tn_tile", [0, 1, 4], indirect=True)
 @pytest.mark.parametrize("K,M,N", [(64, 128, 128), (100, 136, 72), (1000, 256, 384), (8193, 768, 768), (70, 264, 520)])
 def test_gemm_tn(K, M, N, tn_tile):
     O = ops()
@@ -501,8 +502,8 @@ def bwd_block():
                                    (1, 1, 10659)])
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
 def test_attention_dkdv6_matches_dkdv5(B, H, N, dt, bwd_block):
-    """The 64-keys-per-wave dK/dV pass with AGPR accumulators (DCLIP_OPT_ATTN_BWD_BLOCK 6,
-    attention_dkdv6.hip) against fp32 autograd, and against the default dkdv5 pass on the same
+    """The 64-keys-per-wave dK/dV pass with AGPR accumulators (the default since round 3,
+    attention_dkdv6.hip) against fp32 autograd, and against round 2's dkdv5 pass (option 5) on the same
     inputs (same products, same per-key summation order: equal up to fp32 rounding), full and
     ragged N - 1, partial last key blocks included."""
     O = ops()
@@ -512,7 +513,7 @@ def test_attention_dkdv6_matches_dkdv5(B, H, N, dt, bwd_block):
     dout = torch.randn(B * N, C, device=DEV).to(dt)
     o, lse = O.attn_fwd(qkv, B, N, H, 64 ** -0.5)
     res = []
-    for v in (0, 6):
+    for v in (5, 0):  # dkdv5 (round 2's pass), then the default dkdv6
         bwd_block(v)
         res.append(O.attn_bwd(qkv, o, dout, lse, B, N, H, 64 ** -0.5).float())
     a, b = res
@@ -520,7 +521,7 @@ def test_attention_dkdv6_matches_dkdv5(B, H, N, dt, bwd_block):
     assert rel_err(b[:, C:], a[:, C:]) < 1e-3, rel_err(b[:, C:], a[:, C:])  # dK, dV columns
     assert torch.equal(b[:, :C], a[:, :C])  # dQ: the same dQ pass
     if N <= 2049:
-        bwd_block(6)
+        bwd_block(0)
         errs = _attn_bwd_check(B, H, N, dt)
         assert max(errs) < 4 * TOL[dt], errs
 
