@@ -231,7 +231,7 @@ def main():
         with open(pmc_b) as f:
             traffic_b = json.load(f).get("hbm_bytes_per_launch")
     kernels = {k: {"launches": v[0], "ms_total": round(v[1], 3), "ms_mean": round(v[2], 4)} for k, v in summ.items()}
-    # the attention backward (row-0 passes + dQ pass + dK/dV pass per launch): useful work = the
+    # the attention backward (dQ pass + dK/dV pass + the CLS row's merge per launch): useful work = the
     # 5 N^2-matmuls of flash backward (2.5x the forward's), same HIP-event timing
     n_ab, _, mean_ab = summ.get("attn_bwd", (0, 0.0, float("nan")))
     fl_b = 2.5 * fl
@@ -301,7 +301,7 @@ def main():
         # per launch, 2.5x the forward's): it is the headline roofline whenever it ran
         rf_bwd = None
         if n_ab:
-            rf_bwd = {"kernel": "attn_bwd_dq2_kernel + attn_bwd_dkdv6_kernel (+ row-0 passes)" if cls_split
+            rf_bwd = {"kernel": "attn_bwd_dq2_kernel + attn_bwd_dkdv6_kernel (+ CLS-row fold merge)" if cls_split
                       else "attn_bwd_dq_kernel + attn_bwd_dkdv_kernel",
                       "bound": "mfma", "achieved": round(ach_b, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                       "frac": round(ach_b / PEAK_BF16_TFLOPS, 4), "traffic": traffic_b,

@@ -1227,7 +1227,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const T* _
 // ---------------------------------------------------------------------------- dQ pass, CLS split
 // The dQ pass on N = 1 + 256k: the same 32-key unit pipeline as attn_bwd_dq_kernel, with the
 // forward's CLS split (key 0 folded into each query's dQ on the VALU in the prologue, queries
-// 1..N-1 in full 256-row blocks, query 0 by the split-key row pass attn_bwd_row0_dq_*), K / V
+// 1..N-1 in full 256-row blocks; query 0 and key 0 by the CLS-row fold — the epilogues of this
+// pass and of the dK/dV pass plus attn_bwd_row0_fold_merge — by default, by the split-key row
+// passes attn_bwd_row0_* under DCLIP_OPT_ATTN_BWD_BLOCK 1..5), K / V
 // tiles by LDS-DMA into a 4-slot ring three tiles ahead (no staging registers, no ds_write,
 // a bare barrier behind a counted vmcnt) and widened dQ stores.
 template <typename T, int NW>
@@ -1336,10 +1338,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq2_kernel(const T* 
                                                                        float* __restrict__ delta,
                                                                        float* __restrict__ nstat,
                                                                        T* __restrict__ dqkv, int N, int H,
-                                                                       float scale) {
+                                                                       float scale, float* __restrict__ r0ws) {
     constexpr int QB = 32 * NW, PIECES = Dq2Ctx<T, NW>::PIECES;
     typedef typename Mfma<T>::frag frag;
-    __shared__ __attribute__((aligned(16))) char smem[4 * 16384];
+    // the ring, then the CLS-row fold's per-query weights [dS_0 | P_0] (used when r0ws != null)
+    __shared__ __attribute__((aligned(16))) char smem[4 * 16384 + 2 * QB * 4];
     Dq2Ctx<T, NW> c;
     c.smem = smem;
     c.lane = threadIdx.x & 63;
@@ -1420,6 +1423,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq2_kernel(const T* 
             for (int e = 0; e < 4; ++e) c.dq[db][4 * g + e] = ds0 * (float)k0d[db][g][e];
 #pragma unroll
     for (int s = 0; s < 4; ++s) frag_ds_scale<T>(c.gf[s]);  // dP chains now give DsScale dP
+    float* r0w = (float*)(smem + 4 * 16384);
+    if (r0ws != nullptr && c.h == 0) {  // key 0's weights for the epilogue's dK_0 / dV_0 sums
+        r0w[c.wave * 32 + c.l32] = qok ? ds0 : 0.f;
+        r0w[QB + c.wave * 32 + c.l32] = qok ? p0 : 0.f;
+    }
 
     wait_vmcnt<2 * PIECES>();  // tiles 0 and 1 landed (tile 2 in flight)
     __builtin_amdgcn_s_barrier();
@@ -1439,6 +1447,32 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq2_kernel(const T* 
     if (t < c.nt) dq2_step<T, NW, 2>(c, t++, sA, pA, sB, pB);
     wait_vmcnt<0>();
     if (qok) store_row_t21<T>(dqkv + ((int64_t)b * N + q) * ld + hd * HD, c.dq, scale / DsScale<T>::v, c.h);
+    if (r0ws != nullptr) {
+        // CLS-row fold: this block's share of key 0's sums, dK_0 += dS_0 q', dV_0 += P_0 dO (both
+        // DsScale-scaled: dS_0 carries it, dO was scaled above), one partial per workgroup
+        __syncthreads();  // every wave is done with the ring
+        char* img = smem + c.wave * 32 * 128;
+        r0_put<T>(img, c.qf, c.l32, c.h);
+        const float ak = r0_colsum<T, 32>(img, r0w + c.wave * 32, c.lane);
+        asm volatile("" ::: "memory");
+        r0_put<T>(img, c.gf, c.l32, c.h);
+        const float av = r0_colsum<T, 32>(img, r0w + QB + c.wave * 32, c.lane);
+        float* part = (float*)(smem + NW * 32 * 128);
+        part[c.wave * 128 + c.lane] = ak;
+        part[c.wave * 128 + 64 + c.lane] = av;
+        if (qblk == 0 && c.wave == 0) {  // delta of query 0, for the dK/dV pass and the merge
+            const int64_t r0 = (int64_t)b * N * C + hd * HD + c.lane;
+            const float d0 = wave_sum((float)dout[r0] * (float)o[r0]);
+            if (c.lane == 0) delta[(int64_t)bh * N] = d0;
+        }
+        __syncthreads();
+        if (threadIdx.x < 128) {
+            float sum = 0.f;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) sum += part[w * 128 + threadIdx.x];
+            r0ws[((int64_t)bh * nq + qblk) * 128 + threadIdx.x] = sum;
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------- row 0 of the backward
@@ -1585,6 +1619,40 @@ __global__ __launch_bounds__(64) void attn_bwd_row0_dkdv_merge(const float* __re
     T* row = dqkv + (int64_t)b * N * 3 * C + hd * HD;
     row[C + lane] = (T)(ak * dk_scale);
     row[2 * C + lane] = (T)av;
+}
+
+// the CLS-row fold's merge (the default dK/dV pass): row 0 of dQ, dK, dV from the dQ pass's
+// partials (r0kv: [dK_0 | dV_0] over each query block, queries 1..), the dK/dV pass's (r0q: dQ_0
+// over each key block, keys 1..), and the (query 0, key 0) term itself; the partials carry
+// DsScale (attn_frag.h)
+template <typename T>
+__global__ __launch_bounds__(64) void attn_bwd_row0_fold_merge(const T* __restrict__ qkv, const T* __restrict__ dout,
+                                                               const float* __restrict__ lse,
+                                                               const float* __restrict__ delta,
+                                                               const float* __restrict__ r0kv, int nq,
+                                                               const float* __restrict__ r0q, int nkb,
+                                                               T* __restrict__ dqkv, int N, int H, float scale,
+                                                               float dk_scale) {
+    const int lane = threadIdx.x;
+    const int bh = blockIdx.x, b = bh / H, hd = bh % H;
+    const int C = H * HD;
+    const int64_t row = (int64_t)b * N * 3 * C + hd * HD + lane;
+    const float q0 = (float)qkv[row], k0 = (float)qkv[row + C], v0 = (float)qkv[row + 2 * C];
+    const float g0 = (float)dout[(int64_t)b * N * C + hd * HD + lane];
+    const float p00 = __builtin_amdgcn_exp2f(wave_sum(q0 * k0) - lse[(int64_t)bh * N]);
+    const float ds00 = p00 * (wave_sum(g0 * v0) - delta[(int64_t)bh * N]);
+    float aq = 0.f, ak = 0.f, av = 0.f;
+#pragma unroll 4
+    for (int j = 0; j < nkb; ++j) aq += r0q[((int64_t)bh * nkb + j) * 64 + lane];
+#pragma unroll 4
+    for (int j = 0; j < nq; ++j) {
+        ak += r0kv[((int64_t)bh * nq + j) * 128 + lane];
+        av += r0kv[((int64_t)bh * nq + j) * 128 + 64 + lane];
+    }
+    constexpr float inv = 1.0f / DsScale<T>::v;
+    dqkv[row] = (T)((aq * inv + ds00 * k0) * scale);
+    dqkv[row + C] = (T)((ak * inv + ds00 * q0) * dk_scale);
+    dqkv[row + 2 * C] = (T)(av * inv + p00 * g0);
 }
 
 // ---------------------------------------------------------------------------- dK/dV pass
@@ -2217,23 +2285,39 @@ bool bwd2_launch(const void* qkv, const void* o, const void* dout, const float* 
     const int nsplit = (N + R0_CHUNK - 1) / R0_CHUNK;
     float* ws0 = delta + (int64_t)B * H * N;
     float* nstat = ws0 + (int64_t)B * H * ((N + 63) / 64) * 192;  // [-lse | -delta], B*H*N each
+    const bool dq4 = dclip_option(DCLIP_OPT_ATTN_DQ_WAVES) == 4;
+    if (bwd_block == 0 || bwd_block == 6) {
+        // default: the CLS row's sums folded into the two passes' epilogues (partials in ws0) and
+        // one merge; 64 keys per wave, one wave per SIMD, AGPR dK / dV
+        const int nq = (N - 1 + (dq4 ? 127 : 255)) / (dq4 ? 128 : 256), nkb = (N - 1 + 255) / 256;
+        float* r0kv = ws0;
+        float* r0q = ws0 + (int64_t)B * H * nq * 128;
+        if (dq4)
+            attn_bwd_dq2_kernel<T, 4><<<B * H * nq, 256, 0, st>>>((const T*)qkv, (const T*)o, (const T*)dout, lse,
+                                                                   delta, nstat, (T*)dqkv, N, H, scale, r0kv);
+        else
+            attn_bwd_dq2_kernel<T, 8><<<B * H * nq, 512, 0, st>>>((const T*)qkv, (const T*)o, (const T*)dout, lse,
+                                                                   delta, nstat, (T*)dqkv, N, H, scale, r0kv);
+        attn_bwd_dkdv6_launch(std::is_same<T, bf16>::value ? DCLIP_BF16 : DCLIP_F16, qkv, dout, lse, delta, nstat,
+                              nstat + (int64_t)B * H * N, dqkv, B, N, H, 1.0f / LOG2E, r0q, st);
+        attn_bwd_row0_fold_merge<T><<<B * H, 64, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, r0kv, nq, r0q, nkb,
+                                                          (T*)dqkv, N, H, scale, 1.0f / LOG2E);
+        return true;
+    }
     attn_bwd_row0_dq_part<T><<<B * H * nsplit, 256, 0, st>>>((const T*)qkv, (const T*)o, (const T*)dout, lse, ws0, N, H,
                                                             nsplit);
     attn_bwd_row0_dq_merge<T><<<B * H, 64, 0, st>>>((const T*)o, (const T*)dout, ws0, delta, (T*)dqkv, N, H, nsplit,
                                                     scale);
-    if (dclip_option(DCLIP_OPT_ATTN_DQ_WAVES) == 4)  // 128 queries per workgroup, two workgroups per CU
+    if (dq4)  // 128 queries per workgroup, two workgroups per CU
         attn_bwd_dq2_kernel<T, 4><<<B * H * ((N - 1) / 128), 256, 0, st>>>(
-            (const T*)qkv, (const T*)o, (const T*)dout, lse, delta, nstat, (T*)dqkv, N, H, scale);
+            (const T*)qkv, (const T*)o, (const T*)dout, lse, delta, nstat, (T*)dqkv, N, H, scale, nullptr);
     else
         attn_bwd_dq2_kernel<T, 8><<<B * H * ((N - 1 + 255) / 256), 512, 0, st>>>(
-            (const T*)qkv, (const T*)o, (const T*)dout, lse, delta, nstat, (T*)dqkv, N, H, scale);
+            (const T*)qkv, (const T*)o, (const T*)dout, lse, delta, nstat, (T*)dqkv, N, H, scale, nullptr);
     attn_bwd_row0_dkdv_part<T><<<B * H * nsplit, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, ws0, N, H,
                                                               nsplit);
     attn_bwd_row0_dkdv_merge<T><<<B * H, 64, 0, st>>>(ws0, (T*)dqkv, N, H, nsplit, 1.0f / LOG2E);
-    if (bwd_block == 0 || bwd_block == 6)  // default: 64 keys per wave, one wave per SIMD, AGPR dK / dV
-        attn_bwd_dkdv6_launch(std::is_same<T, bf16>::value ? DCLIP_BF16 : DCLIP_F16, qkv, dout, lse, delta, nstat,
-                              nstat + (int64_t)B * H * N, dqkv, B, N, H, 1.0f / LOG2E, st);
-    else if (bwd_block == 5)  // pipelined, 32 keys per wave, 2 waves per SIMD (round 2's default)
+    if (bwd_block == 5)  // pipelined, 32 keys per wave, 2 waves per SIMD (round 2's default)
         attn_bwd_dkdv5_kernel<T><<<B * H * ((N - 1 + 127) / 128), 256, 0, st>>>(
             (const T*)qkv, (const T*)dout, lse, delta, nstat, nstat + (int64_t)B * H * N, (T*)dqkv, N, H, 1.0f / LOG2E);
     else if (dclip_option(DCLIP_OPT_ATTN_DKDV_WAVES) == 8)  // 256 keys per workgroup (one Q / dO slice per 256 keys)

@@ -218,11 +218,13 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv6_kernel(const T* __restr
                                                                 const float* __restrict__ delta,
                                                                 const float* __restrict__ nlse,
                                                                 const float* __restrict__ ndelta,
-                                                                T* __restrict__ dqkv, int N, int H, float dk_scale) {
+                                                                T* __restrict__ dqkv, int N, int H, float dk_scale,
+                                                                float* __restrict__ r0q) {
     constexpr int NW = 4, KB = 64 * NW;
     typedef Dkv2Ctx<T, NW> X;
     typedef typename Mfma<T>::frag frag;
-    __shared__ __attribute__((aligned(16))) char smem[4 * X::SLOT];
+    // the ring, then the CLS-row fold's per-key weights dS_0 (used when r0q != null)
+    __shared__ __attribute__((aligned(16))) char smem[4 * X::SLOT + KB * 4];
     X c;  // the LDS-DMA ring of Q / dO / statistics slices (its key-fragment members stay unused)
     K6<T> k;
     c.smem = smem;
@@ -303,6 +305,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv6_kernel(const T* __restr
             }
         const float p0 = __builtin_amdgcn_exp2f(xhalf_sum(spart) - L0);
         const float ds0 = p0 * (xhalf_sum(ppart) - d0) * DsScale<T>::v;
+        // the fold's weight (both half-waves store the same value; a guarded store here made the
+        // compiler spill in the main loop)
+        ((float*)(smem + 4 * X::SLOT))[c.wave * 64 + kb * 32 + c.l32] = kok[kb] ? ds0 : 0.f;
 #pragma unroll
         for (int db = 0; db < 2; ++db)
 #pragma unroll
@@ -333,6 +338,27 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv6_kernel(const T* __restr
     if (t < c.nt) step6<T, 1>(c, k, t++, qa, ga, S0, P0);
     if (t < c.nt) step6<T, 2>(c, k, t++, qa, ga, S0, P0);
     wait_vmcnt<0>();
+    if (r0q != nullptr) {
+        // CLS-row fold: this block's share of query 0's dQ_0 += dS_0 k (DsScale-scaled), one
+        // partial per workgroup (attn_frag.h); before the dK / dV stores, so that the K fragments
+        // are dead by then
+        // (the lane index is recomputed here: one more VGPR live across the loop spilled)
+        __syncthreads();  // every wave is done with the ring
+        const int lane = __lane_id();
+        char* img = smem + c.wave * 64 * 128;
+        r0_put<T>(img, k.kf[0], lane & 31, lane >> 5);
+        r0_put<T>(img, k.kf[1], 32 + (lane & 31), lane >> 5);
+        const float aq = r0_colsum<T, 64>(img, (const float*)(smem + 4 * X::SLOT) + c.wave * 64, lane);
+        float* part = (float*)(smem + NW * 64 * 128);
+        part[c.wave * 64 + lane] = aq;
+        __syncthreads();
+        if (c.wave == 0) {
+            float sum = 0.f;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) sum += part[w * 64 + lane];
+            r0q[((int64_t)bh * nkb + kblk) * 64 + lane] = sum;
+        }
+    }
     // the last asm MFMAs' AGPR results: >= 18 wait states before anything reads them
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3"
                  : "+a"(k.dk[0][0]), "+a"(k.dk[0][1]), "+a"(k.dk[1][0]), "+a"(k.dk[1][1]), "+a"(k.dv[0][0]),
@@ -350,15 +376,15 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv6_kernel(const T* __restr
 }  // namespace
 
 // launched by attention.hip's bwd2_launch (DCLIP_OPT_ATTN_BWD_BLOCK selects it); key 0 is the
-// row-0 kernels' (as for dkdv5)
+// fold merge's (attn_bwd_row0_fold_merge), which also takes the dQ_0 partials written to r0q
 void attn_bwd_dkdv6_launch(int dt, const void* qkv, const void* dout, const float* lse, const float* delta,
                            const float* nlse, const float* ndelta, void* dqkv, int B, int N, int H, float dk_scale,
-                           hipStream_t st) {
+                           float* r0q, hipStream_t st) {
     const int grid = B * H * ((N - 1 + 255) / 256);
     if (dt == DCLIP_BF16)
         attn_bwd_dkdv6_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)qkv, (const bf16*)dout, lse, delta, nlse, ndelta,
-                                                          (bf16*)dqkv, N, H, dk_scale);
+                                                          (bf16*)dqkv, N, H, dk_scale, r0q);
     else
         attn_bwd_dkdv6_kernel<f16><<<grid, 256, 0, st>>>((const f16*)qkv, (const f16*)dout, lse, delta, nlse, ndelta,
-                                                         (f16*)dqkv, N, H, dk_scale);
+                                                         (f16*)dqkv, N, H, dk_scale, r0q);
 }

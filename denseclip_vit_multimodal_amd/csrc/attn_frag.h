@@ -133,6 +133,31 @@ __device__ __forceinline__ void store_row_t21(T* row, const f32x16 (&acc)[2], fl
     }
 }
 
+// ---------------------------------------------------------------------------- CLS-row fold
+// The CLS row's backward sums that run over the OTHER axis of a pass — dK_0 / dV_0 (sums over
+// queries) in the query-major dQ pass, dQ_0 (a sum over keys) in the key-major dK/dV pass — are
+// taken in the pass's epilogue from the register-resident rows: each wave copies its rows into
+// a plain [rows][64] LDS image (the ring is free by then) and lane d sums column d against the
+// per-row weights the prologue parked in LDS.  One partial per workgroup goes to the workspace;
+// attn_bwd_row0_fold_merge adds them up in a fixed order (deterministic, no atomics).
+template <typename T>
+__device__ __forceinline__ void r0_put(char* img, const typename Mfma<T>::frag (&x)[4], int row, int h) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) *(typename Mfma<T>::frag*)(img + row * 128 + (2 * s + h) * 16) = x[s];
+}
+
+// sum over the image's ROWS rows of w[r] * img[r][lane] (lane < 64: one column per lane).  The
+// image was written by this wave's own lanes: LDS executes a wave's operations in order, the
+// wait only keeps the compiler from hoisting the reads over the writes
+template <typename T, int ROWS>
+__device__ __forceinline__ float r0_colsum(const char* img, const float* w, int lane) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    float acc = 0.f;
+#pragma unroll 8
+    for (int r = 0; r < ROWS; ++r) acc += w[r] * (float)((const T*)(img + r * 128))[lane];
+    return acc;
+}
+
 // ---------------------------------------------------------------------------- dK/dV pass, CLS split
 // Key-major dK/dV pass on N = 1 + 32*NW*k: keys 1..N-1 in full blocks (key 0 by the row-0
 // kernels above), query 0 folded into every key's dK / dV on the VALU in the prologue, and

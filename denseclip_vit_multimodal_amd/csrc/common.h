@@ -162,7 +162,8 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
 
 // query 0 (CLS row) of the 16-bit forward: split-key row pass + merge (attention.hip)
 void attn_row0_fwd(int dt, const void* qkv, void* o, float* lse, int B, int N, int H, hipStream_t st);
-// CLS-split dK/dV pass with 64 keys per wave and AGPR accumulators (attention_dkdv6.hip)
+// CLS-split dK/dV pass with 64 keys per wave and AGPR accumulators (attention_dkdv6.hip); r0q
+// receives one dQ_0 partial (64 floats) per key block
 void attn_bwd_dkdv6_launch(int dt, const void* qkv, const void* dout, const float* lse, const float* delta,
                            const float* nlse, const float* ndelta, void* dqkv, int B, int N, int H, float dk_scale,
-                           hipStream_t st);
+                           float* r0q, hipStream_t st);

@@ -519,7 +519,12 @@ def test_attention_dkdv6_matches_dkdv5(B, H, N, dt, bwd_block):
     a, b = res
     assert torch.isfinite(b).all()
     assert rel_err(b[:, C:], a[:, C:]) < 1e-3, rel_err(b[:, C:], a[:, C:])  # dK, dV columns
-    assert torch.equal(b[:, :C], a[:, :C])  # dQ: the same dQ pass
+    # dQ: the same dQ pass for queries 1..N-1; the CLS row (query 0, and key 0's dK / dV) comes
+    # from the row-0 kernels under option 5 and from the passes' epilogue fold under the default
+    rest = torch.ones(B * N, dtype=torch.bool, device=DEV)
+    rest[::N] = False
+    assert torch.equal(b[rest, :C], a[rest, :C])
+    assert rel_err(b[~rest], a[~rest]) < 1e-3, rel_err(b[~rest], a[~rest])
     if N <= 2049:
         bwd_block(0)
         errs = _attn_bwd_check(B, H, N, dt)
