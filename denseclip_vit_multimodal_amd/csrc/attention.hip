@@ -954,10 +954,17 @@ __device__ __forceinline__ void store_grp0(float* dst, const float (&v)[8], int 
 
 // Forward: partial (max, sum, o[64]) of query 0 over the wave's 256 keys, online softmax per
 // lane group over 4 batches of 8 keys.  Partials of (b, h, part) are parked in o + b*N*C + C
-// (rows 1.. of batch b, rewritten later by the main pass), (h * nparts + part) * 66 floats.
+// (rows 1.. of batch b, rewritten later by the main pass), (h * nparts + part) * 66 floats, or
+// at pws + ((b * H + h) * nparts + part) * 66 when the caller passes a workspace (pws != null:
+// the fp8 forward, whose N may be too small for the parking rows).
+__device__ __forceinline__ float* row0_ws(void* out, float* pws, int b, int N, int C, int H, int hd, int nparts) {
+    return pws != nullptr ? pws + (int64_t)(b * H + hd) * nparts * 66
+                          : (float*)((char*)out + ((int64_t)b * N * C + C) * 2) + (int64_t)hd * nparts * 66;
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void attn_row0_part_kernel(const T* __restrict__ qkv, T* __restrict__ out, int N,
-                                                            int H, int nsplit) {
+                                                            int H, int nsplit, float* __restrict__ pws) {
     typedef T t8 __attribute__((ext_vector_type(8)));
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int sub = lane & 7, grp = lane >> 3;
@@ -1009,7 +1016,7 @@ __global__ __launch_bounds__(256) void attn_row0_part_kernel(const T* __restrict
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = grps_sum(o[e] * a);
     const int nparts = nsplit * R0_PARTS;
-    float* ws = (float*)(out + (int64_t)b * N * C + C) + (int64_t)(hd * nparts + sp * R0_PARTS + wave) * 66;
+    float* ws = row0_ws(out, pws, b, N, C, H, hd, nparts) + (int64_t)(sp * R0_PARTS + wave) * 66;
     store_grp0(ws + 2, o, lane);
     if (lane == 0) {
         ws[0] = mw;
@@ -1019,12 +1026,12 @@ __global__ __launch_bounds__(256) void attn_row0_part_kernel(const T* __restrict
 
 template <typename T>
 __global__ __launch_bounds__(64) void attn_row0_merge_kernel(T* __restrict__ out, float* __restrict__ lse, int N,
-                                                             int H, int nsplit) {
+                                                             int H, int nsplit, float* __restrict__ pws) {
     const int lane = threadIdx.x;
     const int bh = blockIdx.x, b = bh / H, hd = bh % H;
     const int C = H * HD;
     const int nparts = nsplit * R0_PARTS;
-    const float* ws = (const float*)(out + (int64_t)b * N * C + C) + (int64_t)hd * nparts * 66;
+    const float* ws = row0_ws(out, pws, b, N, C, H, hd, nparts);
     float M = -INFINITY;
 #pragma unroll 4
     for (int s = 0; s < nparts; ++s) M = fmaxf(M, ws[s * 66]);
@@ -2239,8 +2246,8 @@ bool fwd2_launch_nw(const void* qkv, void* o, float* lse, int B, int N, int H, h
     constexpr int QB = 32 * NW;
     if (N < 1 + QB) return false;  // any N - 1 >= QB (a ragged tail: masked last key tile, partial last block)
     const int nsplit = (N + R0_CHUNK - 1) / R0_CHUNK;
-    attn_row0_part_kernel<T><<<B * H * nsplit, 256, 0, st>>>((const T*)qkv, (T*)o, N, H, nsplit);
-    attn_row0_merge_kernel<T><<<B * H, 64, 0, st>>>((T*)o, lse, N, H, nsplit);
+    attn_row0_part_kernel<T><<<B * H * nsplit, 256, 0, st>>>((const T*)qkv, (T*)o, N, H, nsplit, nullptr);
+    attn_row0_merge_kernel<T><<<B * H, 64, 0, st>>>((T*)o, lse, N, H, nsplit, nullptr);
     const dim3 grid(B * H * ((N - 1 + QB - 1) / QB));
     attn_fwd2_kernel<T, NW><<<grid, 64 * NW, 0, st>>>((const T*)qkv, (T*)o, lse, N, H);
     return true;
@@ -2251,8 +2258,8 @@ template <typename T, int NW, int NB>
 bool fwd3_launch(const void* qkv, void* o, float* lse, int B, int N, int H, hipStream_t st) {
     if (N < 257 || (N - 1) % 256 != 0) return false;
     const int nsplit = (N + R0_CHUNK - 1) / R0_CHUNK;
-    attn_row0_part_kernel<T><<<B * H * nsplit, 256, 0, st>>>((const T*)qkv, (T*)o, N, H, nsplit);
-    attn_row0_merge_kernel<T><<<B * H, 64, 0, st>>>((T*)o, lse, N, H, nsplit);
+    attn_row0_part_kernel<T><<<B * H * nsplit, 256, 0, st>>>((const T*)qkv, (T*)o, N, H, nsplit, nullptr);
+    attn_row0_merge_kernel<T><<<B * H, 64, 0, st>>>((T*)o, lse, N, H, nsplit, nullptr);
     attn_fwd3_kernel<T, NW, NB><<<B * H * ((N - 1) / 256), 64 * NW, 0, st>>>((const T*)qkv, (T*)o, lse, N, H);
     return true;
 }
@@ -2367,14 +2374,14 @@ void bwd_launch(const void* qkv, const void* o, const void* dout, const float* l
 
 // query 0 (the CLS row) of the forward by the split-key row pass + merge (o row 0 and lse[0]
 // of every (image, head)); used by the fp8 forward's CLS split (attention_fp8.hip)
-void attn_row0_fwd(int dt, const void* qkv, void* o, float* lse, int B, int N, int H, hipStream_t st) {
+void attn_row0_fwd(int dt, const void* qkv, void* o, float* lse, int B, int N, int H, hipStream_t st, float* pws) {
     const int nsplit = (N + R0_CHUNK - 1) / R0_CHUNK;
     if (dt == DCLIP_BF16) {
-        attn_row0_part_kernel<bf16><<<B * H * nsplit, 256, 0, st>>>((const bf16*)qkv, (bf16*)o, N, H, nsplit);
-        attn_row0_merge_kernel<bf16><<<B * H, 64, 0, st>>>((bf16*)o, lse, N, H, nsplit);
+        attn_row0_part_kernel<bf16><<<B * H * nsplit, 256, 0, st>>>((const bf16*)qkv, (bf16*)o, N, H, nsplit, pws);
+        attn_row0_merge_kernel<bf16><<<B * H, 64, 0, st>>>((bf16*)o, lse, N, H, nsplit, pws);
     } else {
-        attn_row0_part_kernel<f16><<<B * H * nsplit, 256, 0, st>>>((const f16*)qkv, (f16*)o, N, H, nsplit);
-        attn_row0_merge_kernel<f16><<<B * H, 64, 0, st>>>((f16*)o, lse, N, H, nsplit);
+        attn_row0_part_kernel<f16><<<B * H * nsplit, 256, 0, st>>>((const f16*)qkv, (f16*)o, N, H, nsplit, pws);
+        attn_row0_merge_kernel<f16><<<B * H, 64, 0, st>>>((f16*)o, lse, N, H, nsplit, pws);
     }
 }
 

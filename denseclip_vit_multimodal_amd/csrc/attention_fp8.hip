@@ -1,38 +1,54 @@
-// fp8 (OCP e4m3) attention forward for inference — BASELINE config 5 ("fp8 MFMA attention").
+// fp8 (OCP e4m3) attention forward — BASELINE config 5 ("fp8 MFMA attention").
 //
 // Same contract as dclip_attn_fwd (reference: the nn.MultiheadAttention core of
 // ResidualAttentionBlock.attention, models.py:287-289; q columns of the packed qkv pre-multiplied
-// by d^-0.5 * log2(e)), computed on the block-scaled gfx950 MFMA
-// v_mfma_scale_f32_32x32x64_f8f6f4 with unit (E8M0 = 127) block scales, which runs at twice the
-// bf16 rate: one instruction covers K = 64, i.e. a whole head dimension or 64 keys.
+// by d^-0.5 * log2(e)), computed on the block-scaled gfx950 MFMA v_mfma_scale_f32_32x32x64_f8f6f4,
+// which runs at twice the bf16 rate (one instruction covers K = 64: a whole head dimension, or
+// 64 keys) and applies an E8M0 (power-of-two) scale per lane to each operand's 32-element K block.
 //
-// Three launches:
-//   1. fp8_amax_kernel   per-(image, q/k/v, head) amax of the 16-bit qkv (integer atomicMax on
-//                        the float bits: all values are >= 0)
-//   2. fp8_pack_kernel   quantise with scale 448 / amax (saturating) into a per-head layout:
-//                          q8, k8 [b][h][Npad][64] bytes      (token rows, 64 B each)
-//                          vt8   [b][h][64][Npad] bytes       (V transposed, keys permuted per
-//                                                              64-key unit, see kappa() below)
-//                        rows / keys past N are zero
-//   3. attn_fp8_kernel   flash forward: 8 waves x 32 queries per workgroup; per 64-key unit the
-//                        K tile (4 KB) and V^T tile (4 KB) are staged in LDS (double-buffered,
-//                        prefetched into registers one unit ahead); per wave
-//                          S^T = K Q^T          2 MFMAs (keys 0-31, 32-63), lane = query
-//                          online softmax       log2 domain, one cross-half max per unit
-//                          O^T += V^T P^T       2 MFMAs (d 0-31, 32-63); P^T straight from the
-//                                               S^T accumulators, converted to fp8 in registers
+// MX block scales.  Every 32-element K block of every operand row carries its own power-of-two
+// scale, the largest 2^s with amax * 2^s <= 448 (the e4m3 maximum): q and k rows per 32-dim half,
+// V^T rows (one head dim d) per 32-key half of each 64-key unit.  So no global amax pass is
+// needed (each block's scale is local to the pack), small rows keep their precision, and the
+// MFMA hands back S exactly dequantised and already in the log2 domain: the softmax takes
+// exp2 of the accumulator as it stands — no per-score dequantisation multiply.
+//
+// Two launches after query 0 (the CLS row: the 16-bit forward's split-key row pass):
+//   1. fp8mx_pack_kernel  tokens 1..N-1 of one 64-token unit per workgroup:
+//                           q8, k8 [b][h][n1p][64] bytes (token rows), qs [b][h][n1p][2] E8M0
+//                           vt8    [b][h][64][n1p] bytes (V transposed, keys permuted per unit,
+//                                                       see vt_key() below)
+//                           sc     [b][h][unit][64] dwords: lane (half, r)'s four E8M0 scales
+//                                  {K(key r, d-half), K(key 32+r, d-half), V^T(d r, key-half),
+//                                  V^T(d 32+r, key-half)}, half = the d-half / key-half
+//                         rows past N are zero
+//   2. attn_fp8mx_kernel  CLS-split flash forward (the 16-bit attn_fwd2_kernel's structure): key 0
+//                         folded into every query's softmax state on the VALU from the 16-bit
+//                         qkv; keys 1..N-1 in 64-key units staged by LDS-DMA (K tile, V^T tile,
+//                         the unit's 256 scale bytes) into a 4-slot ring three units ahead; per
+//                         wave and unit
+//                           S^T = K Q^T     2 MFMAs, accumulators seeded with -m (the running
+//                                           max), scales: K (opsel 0/1 of the lane's dword), q
+//                           softmax         max over the unit; on a move (any lane) rescale
+//                                           o, l and S; P = exp2(S) in place, P in [0, 1]
+//                           O^T += V^T P^T  2 MFMAs, P^T converted to e4m3 in registers, scales:
+//                                           V^T (opsel 2/3), 1 for P
 //
 // Operand maps.  For the 32x32x64 f8f6f4 MFMA a lane (r = lane & 31, half = lane >> 5) holds
-// 32 bytes of row r of A (column r of B); byte j of half `half` is one K index kappa(half, j),
-// the SAME for A and B.  Only that sameness is relied on: every contraction below assigns its
-// logical K index to (half, j) identically on both sides.  For S^T = K Q^T the K index is the
-// head dim d = 32 half + j (both operands are plain 64-byte token rows).  For O^T = V^T P^T it
-// is the key: the S^T accumulator of key sub-tile t has key (reg & 3) + 8 (reg >> 2) + 4 half
-// in register reg (the dtype-independent C/D map), so the lane's 32 P values are used as
-// bytes j = 16 t + reg, which makes slot (half, j) = key kappa(half, j) below; fp8_pack_kernel
-// writes V^T with that permutation inside every 64-key unit so the V^T operand is 32
-// contiguous bytes too.
-#include "common.h"
+// 32 bytes of row r of A (column r of B); byte j of half `half` is the K index
+// kappa_hw(half, j) = 16 half + 32 (j >> 4) + (j & 15), and the two 32-element scale blocks are
+// K 0-31 (bytes 0-15 of both halves), scaled by lane r's E8M0 byte, and K 32-63 (bytes 16-31),
+// scaled by lane r + 32's (measured: tools/mfma_scale_probe.hip, profiles/r03/r03k_mfma_scale_probe.log).
+// For S^T = K Q^T the K index is the head dim: a lane loads 16-byte chunks `half` and 2 + half of
+// its 64-byte token row, so kappa_hw is d itself and the blocks are d 0-31 / 32-63, the lane's
+// scale that of d-block `half`.  For O^T = V^T P^T it is the key: the S^T accumulator of key
+// sub-tile t has key (reg & 3) + 8 (reg >> 2) + 4 half in register reg, so the lane's 32 P values
+// are used as bytes j = 16 t + reg, which makes byte (half, j) = key kappa(half, j) below and the
+// scale blocks keys 0-31 / 32-63 of the unit (block t, scale from the lane of half t); the pack
+// stores each unit's V^T row with key vt_key(q) at byte q, so that the same two-chunk row load
+// (tile_row) pairs every V^T byte with its P byte, and takes the block amax over the natural key
+// halves (bytes 0-31 / 32-63 of the row).
+#include "attn_frag.h"
 
 #include <type_traits>
 
@@ -41,308 +57,396 @@ namespace {
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
-constexpr float FP8_MAX = 448.0f;
 constexpr int FP8_FMT_E4M3 = 0;  // f8f6f4 format code of OCP e4m3
-constexpr int E8M0_ONE = 127;    // block scale 2^0
+constexpr int E8M0_ONE = 127;    // scale 2^0
+constexpr int U8SLOT = 8192 + 256;  // ring slot: K tile [64][64 B] | V^T tile [64][64 B] | 64 scale dwords
 
-__device__ __forceinline__ int kappa(int half, int j) {  // key within a 64-key unit
+__device__ __forceinline__ int kappa(int half, int j) {  // key of P byte j of a lane of `half`
     const int t = j >> 4, reg = j & 15;
     return 32 * t + (reg & 3) + 8 * (reg >> 2) + 4 * half;
 }
+// key stored at byte p of a unit's V^T row: the byte a lane of half (p >> 4) & 1 loads as its
+// byte 16 (p >> 5) + (p & 15) (tile_row), paired with that P byte
+__device__ __forceinline__ int vt_key(int p) { return kappa((p >> 4) & 1, 16 * (p >> 5) + (p & 15)); }
 
-__device__ __forceinline__ f32x16 mfma_fp8(i32x8 a, i32x8 b, f32x16 c) {
-    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, FP8_FMT_E4M3, FP8_FMT_E4M3, 0, E8M0_ONE, 0,
-                                                           E8M0_ONE);
+// the block scale exponent: the largest s with amax * 2^s <= 448 (0 for an all-zero block)
+__device__ __forceinline__ int mx_exp(float amax) {
+    if (!(amax > 0.f)) return 0;
+    int e;
+    frexpf(448.0f / amax, &e);  // 448 / amax = f 2^e, f in [0.5, 1): floor(log2) = e - 1
+    return max(-120, min(120, e - 1));
 }
 
-// 4 floats -> 4 e4m3 bytes of one dword (saturated to +-448 first: the convert does not clamp)
+// 4 floats -> 4 e4m3 bytes of one dword (clamped to +-448: the convert does not saturate)
 __device__ __forceinline__ int pack4_fp8(float a, float b, float c, float d) {
-    a = fminf(fmaxf(a, -FP8_MAX), FP8_MAX);
-    b = fminf(fmaxf(b, -FP8_MAX), FP8_MAX);
-    c = fminf(fmaxf(c, -FP8_MAX), FP8_MAX);
-    d = fminf(fmaxf(d, -FP8_MAX), FP8_MAX);
+    a = fminf(fmaxf(a, -448.f), 448.f);
+    b = fminf(fmaxf(b, -448.f), 448.f);
+    c = fminf(fmaxf(c, -448.f), 448.f);
+    d = fminf(fmaxf(d, -448.f), 448.f);
     int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
     return __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
 }
-// the same for values known to lie in [0, 1] (softmax probabilities): no clamp needed
+// the same for softmax probabilities (in [0, 1]: no clamp)
 __device__ __forceinline__ int pack4_fp8_unit(float a, float b, float c, float d) {
     int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
     return __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
 }
 
-// ---------------------------------------------------------------------------- 1. amax
-// grid (ceil(N / 64), B), 256 threads; amax[b][which][h] (float bits as int, pre-zeroed)
-template <typename T>
-__global__ void __launch_bounds__(256) fp8_amax_kernel(const T* __restrict__ qkv, int* __restrict__ amax, int N,
-                                                       int H) {
-    __shared__ int red[3 * 64];
-    const int C = H * 64, ncol8 = 3 * C / 8;
-    const int b = blockIdx.y, t0 = blockIdx.x * 64;
-    for (int i = threadIdx.x; i < 3 * H; i += 256) red[i] = 0;
-    __syncthreads();
-    const int ntok = min(64, N - t0);
-    // a thread keeps one 8-column chunk (fixed head) while it walks tokens when 256 % ncol8 == 0;
-    // in general it re-derives the chunk per item
-    for (int c8 = threadIdx.x; c8 < ncol8; c8 += 256) {
-        float m = 0.f;
-        const T* p = qkv + ((int64_t)b * N + t0) * 3 * C + c8 * 8;
-        for (int t = 0; t < ntok; ++t) {
-            const uint4 raw = *(const uint4*)(p + (int64_t)t * 3 * C);
-            const T* e = (const T*)&raw;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) m = fmaxf(m, fabsf((float)e[k]));
-        }
-        const int col = c8 * 8, which = col / C, h = (col % C) / 64;
-        atomicMax(&red[which * H + h], __float_as_int(m));
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < 3 * H; i += 256) atomicMax(&amax[b * 3 * H + i], red[i]);
+template <int OPSEL_A>
+__device__ __forceinline__ f32x16 mfma_mx(i32x8 a, int sa, i32x8 b, int sb, f32x16 c) {
+    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, FP8_FMT_E4M3, FP8_FMT_E4M3, OPSEL_A, sa, 0, sb);
 }
 
-// the same with one thread per (8-column chunk, token parity): blockDim = 2 * ncol8 (<= 1024),
-// every thread walks 32 of the 64 tokens with 8 loads in flight (the loop above keeps one
-// load in flight per thread and leaves 256 - ncol8 % 256 threads idle on its last pass)
-template <typename T>
-__global__ void __launch_bounds__(1024) fp8_amax2_kernel(const T* __restrict__ qkv, int* __restrict__ amax, int N,
-                                                         int H) {
-    __shared__ int red[3 * 64];
-    const int C = H * 64, ncol8 = 3 * C / 8;
-    const int b = blockIdx.y, t0 = blockIdx.x * 64;
-    const int c8 = threadIdx.x % ncol8, par = threadIdx.x / ncol8;
-    for (int i = threadIdx.x; i < 3 * H; i += blockDim.x) red[i] = 0;
-    __syncthreads();
-    const int ntok = min(64, N - t0);
-    const T* p = qkv + ((int64_t)b * N + t0) * 3 * C + c8 * 8;
-    float m = 0.f;
-#pragma unroll 8
-    for (int t = par; t < ntok; t += 2) {
-        const uint4 raw = *(const uint4*)(p + (int64_t)t * 3 * C);
-        const T* e = (const T*)&raw;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) m = fmaxf(m, fabsf((float)e[k]));
-    }
-    const int col = c8 * 8, which = col / C, h = (col % C) / 64;
-    atomicMax(&red[which * H + h], __float_as_int(m));
-    __syncthreads();
-    for (int i = threadIdx.x; i < 3 * H; i += blockDim.x) atomicMax(&amax[b * 3 * H + i], red[i]);
-}
+// 16-B chunk XOR of a 64-B row in a ring tile (conflict-free 16-lane groups of ds_read_b128)
+__device__ __forceinline__ int sw8(int row) { return (row >> 2) & 3; }
 
-// ---------------------------------------------------------------------------- 2. pack
-// grid (Npad / 64, H, B), 256 threads: one 64-token unit of one head
+// ---------------------------------------------------------------------------- 1. pack
+// grid (n1p / 64, H, B), 256 threads: tokens 1 + 64u .. 64 + 64u of one head
 template <typename T>
-__global__ void __launch_bounds__(256) fp8_pack_kernel(const T* __restrict__ qkv, const int* __restrict__ amax,
-                                                       uint8_t* __restrict__ q8, uint8_t* __restrict__ k8,
-                                                       uint8_t* __restrict__ vt8, int N, int H, int Npad) {
+__global__ void __launch_bounds__(256) fp8mx_pack_kernel(const T* __restrict__ qkv, uint8_t* __restrict__ q8,
+                                                         uint8_t* __restrict__ qs, uint8_t* __restrict__ k8,
+                                                         uint8_t* __restrict__ vt8, uint32_t* __restrict__ sc, int N,
+                                                         int H, int n1p) {
     __shared__ float vs[64][65];
+    __shared__ uint32_t scw[64];
     const int C = H * 64;
-    const int unit = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-    const int t0 = unit * 64;
+    const int u = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
     const int tid = threadIdx.x;
-    const float* am = (const float*)amax + b * 3 * H;
-    const float aq = am[h], ak = am[H + h], av = am[2 * H + h];
-    const float sq = aq > 0.f ? FP8_MAX / aq : 1.f;
-    const float sk = ak > 0.f ? FP8_MAX / ak : 1.f;
-    const float sv = av > 0.f ? FP8_MAX / av : 1.f;
     const int64_t hb = (int64_t)b * H + h;
-    // q and k rows: thread -> (token, 16-wide d chunk)
     {
-        const int t = tid >> 2, d0 = (tid & 3) * 16;
-        const int tok = t0 + t;
-        i32x4 oq = {0, 0, 0, 0}, ok = {0, 0, 0, 0};
-        float v[16];
+        // q and k rows: thread -> (token t, 16-dim chunk d0); a 32-dim block is two threads
+        const int t = tid >> 2, d0 = (tid & 3) * 16, dh = d0 >> 5;
+        const int tok = 1 + u * 64 + t;
+        float q[16], k[16];
         if (tok < N) {
             const T* row = qkv + ((int64_t)b * N + tok) * 3 * C + h * 64 + d0;
-            const uint4 r0 = *(const uint4*)row, r1 = *(const uint4*)(row + 8);
-            const T* e0 = (const T*)&r0;
-            const T* e1 = (const T*)&r1;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = (float)e0[k] * sq, v[8 + k] = (float)e1[k] * sq;
+            for (int p = 0; p < 3; ++p) {
+                const uint4 r0 = *(const uint4*)(row + p * C), r1 = *(const uint4*)(row + p * C + 8);
+                const T* e0 = (const T*)&r0;
+                const T* e1 = (const T*)&r1;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) oq[k] = pack4_fp8(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
-            const uint4 s0 = *(const uint4*)(row + C), s1 = *(const uint4*)(row + C + 8);
-            const T* f0 = (const T*)&s0;
-            const T* f1 = (const T*)&s1;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = (float)f0[k] * sk, v[8 + k] = (float)f1[k] * sk;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) ok[k] = pack4_fp8(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
-            const uint4 u0 = *(const uint4*)(row + 2 * C), u1 = *(const uint4*)(row + 2 * C + 8);
-            const T* g0 = (const T*)&u0;
-            const T* g1 = (const T*)&u1;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) vs[t][d0 + k] = (float)g0[k] * sv, vs[t][d0 + 8 + k] = (float)g1[k] * sv;
+                for (int i = 0; i < 8; ++i) {
+                    const float x0 = (float)e0[i], x1 = (float)e1[i];
+                    if (p == 0) q[i] = x0, q[8 + i] = x1;
+                    else if (p == 1) k[i] = x0, k[8 + i] = x1;
+                    else vs[t][d0 + i] = x0, vs[t][d0 + 8 + i] = x1;
+                }
+            }
         } else {
 #pragma unroll
-            for (int k = 0; k < 16; ++k) vs[t][d0 + k] = 0.f;
+            for (int i = 0; i < 16; ++i) q[i] = k[i] = vs[t][d0 + i] = 0.f;
         }
-        *(i32x4*)(q8 + (hb * Npad + tok) * 64 + d0) = oq;
-        *(i32x4*)(k8 + (hb * Npad + tok) * 64 + d0) = ok;
+        float aq = 0.f, ak = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) aq = fmaxf(aq, fabsf(q[i])), ak = fmaxf(ak, fabsf(k[i]));
+        aq = fmaxf(aq, __shfl_xor(aq, 1, 64));
+        ak = fmaxf(ak, __shfl_xor(ak, 1, 64));
+        const int sq = mx_exp(aq), sk = mx_exp(ak);
+        i32x4 oq, ok;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            oq[i] = pack4_fp8(ldexpf(q[4 * i], sq), ldexpf(q[4 * i + 1], sq), ldexpf(q[4 * i + 2], sq),
+                              ldexpf(q[4 * i + 3], sq));
+            ok[i] = pack4_fp8(ldexpf(k[4 * i], sk), ldexpf(k[4 * i + 1], sk), ldexpf(k[4 * i + 2], sk),
+                              ldexpf(k[4 * i + 3], sk));
+        }
+        const int64_t r = hb * n1p + u * 64 + t;
+        *(i32x4*)(q8 + r * 64 + d0) = oq;
+        *(i32x4*)(k8 + r * 64 + d0) = ok;
+        if ((tid & 1) == 0) {
+            qs[r * 2 + dh] = (uint8_t)(E8M0_ONE - sq);
+            ((uint8_t*)scw)[(dh * 32 + (t & 31)) * 4 + (t >> 5)] = (uint8_t)(E8M0_ONE - sk);
+        }
     }
     __syncthreads();
-    // V^T: thread -> (d, 16 consecutive permuted key slots)
     {
-        const int d = tid >> 2, s0 = (tid & 3) * 16;
+        // V^T: thread -> (d, bytes 16p .. 16p + 15 of the unit's row, p = tid & 3), byte q holding
+        // key vt_key(q): keys of half p >> 1 only, so the thread pair (p, p ^ 1) spans one scale
+        // block (the unit's natural key halves)
+        const int d = tid >> 2, p = tid & 3, s0 = p * 16;
+        float e[16];
+        float am = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            e[i] = vs[vt_key(s0 + i)][d];
+            am = fmaxf(am, fabsf(e[i]));
+        }
+        am = fmaxf(am, __shfl_xor(am, 1, 64));
+        const int kh = p >> 1;
+        const int sv = mx_exp(am);
         i32x4 o;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            float e[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int s = s0 + 4 * k + q;  // slot = 32 half + j
-                e[q] = vs[kappa(s >> 5, s & 31)][d];
-            }
-            o[k] = pack4_fp8(e[0], e[1], e[2], e[3]);
-        }
-        *(i32x4*)(vt8 + (hb * 64 + d) * Npad + t0 + s0) = o;
+        for (int i = 0; i < 4; ++i)
+            o[i] = pack4_fp8(ldexpf(e[4 * i], sv), ldexpf(e[4 * i + 1], sv), ldexpf(e[4 * i + 2], sv),
+                             ldexpf(e[4 * i + 3], sv));
+        *(i32x4*)(vt8 + (hb * 64 + d) * n1p + u * 64 + s0) = o;
+        if ((p & 1) == 0) ((uint8_t*)scw)[(kh * 32 + (d & 31)) * 4 + 2 + (d >> 5)] = (uint8_t)(E8M0_ONE - sv);
     }
+    __syncthreads();
+    if (tid < 64) sc[(hb * (n1p / 64) + u) * 64 + tid] = scw[tid];
 }
 
-// ---------------------------------------------------------------------------- 3. attention
-// grid (ceil(N / (32 NW)), H, B), 64 NW threads (NW waves x 32 queries)
-template <typename T, int NW>
-__global__ void __launch_bounds__(64 * NW) attn_fp8_kernel(const uint8_t* __restrict__ q8, const uint8_t* __restrict__ k8,
-                                                       const uint8_t* __restrict__ vt8, const int* __restrict__ amax,
-                                                       T* __restrict__ o, float* __restrict__ lse, int N, int H,
-                                                       int Npad, int q0) {
-    __shared__ __attribute__((aligned(16))) uint8_t sm[2][2][64 * 64];  // [buf][K | V^T][64 rows x 64 B]
-    const int h = blockIdx.y, b = blockIdx.z;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int r = lane & 31, half = lane >> 5;
-    const int q = q0 + blockIdx.x * (32 * NW) + wave * 32 + r;  // this lane's query (column of S^T)
-    const int64_t hb = (int64_t)b * H + h;
-    const float* am = (const float*)amax + b * 3 * H;
-    const float dq = am[h] > 0.f ? am[h] / FP8_MAX : 1.f;
-    const float dk = am[H + h] > 0.f ? am[H + h] / FP8_MAX : 1.f;
-    const float dv = am[2 * H + h] > 0.f ? am[2 * H + h] / FP8_MAX : 1.f;
-    const float sscale = dq * dk;  // S (log2 domain) = sscale * (q8 . k8)
+// ---------------------------------------------------------------------------- 2. attention
+struct F8Ctx {
+    char* smem;     // 4 ring slots of U8SLOT bytes
+    rsrc_t rmine;   // this wave's piece source: the K plane (waves 0-3) or the V^T plane (4-7)
+    rsrc_t rsc;     // the scale plane of this (image, head)
+    uint32_t voff;  // this lane's source offset inside a tile (its 16 B of the wave's 1-KiB piece)
+    uint32_t soff_unit;  // the piece's source stride per unit (4096 for K, 64 for V^T)
+    int nt, lane, l32, h, wave;
+    int rem;        // keys in the last unit (64 unless N - 1 is ragged)
+    i32x8 qf;       // this lane's q8 half row
+    int qsc;        // its E8M0 scale
+    f32x16 o[2];
+    f32x16 negm;
+    float m;
+    float l4[4];
+};
 
-    // Q^T operand: 32 bytes of this lane's query row (zero rows past N were packed as zeros)
-    const uint8_t* qrow = q8 + (hb * Npad + min(q, Npad - 1)) * 64 + 32 * half;
-    const i32x8 qf = *(const i32x8*)qrow;
+// unit t into ring slot `slot`: one 1-KiB piece per wave (waves 0-3: K rows 16w.., 4-7: V^T
+// rows), then 32 B of the scale dwords per wave (lanes 0-7); two vmcnt entries per wave
+__device__ __forceinline__ void f8_issue(F8Ctx& c, int t, int slot) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    char* base = c.smem + slot * U8SLOT;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rmine, LDS_PTR(base + c.wave * 1024), 16, c.voff,
+                                             (uint32_t)t * c.soff_unit, 0, 0);
+    if (c.lane < 8)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rsc, LDS_PTR(base + 8192 + c.wave * 32), 4,
+                                                 (uint32_t)(c.wave * 8 + c.lane) * 4, (uint32_t)t * 256, 0, 0);
+#endif
+}
 
-    // cooperative tile loads of a unit's K tile (4 KB contiguous) and V^T tile (64 rows x 64 B):
-    // NW = 8: threads 0-255 K, 256-511 V^T, 16 B each; NW = 4: every thread 16 B of both
-    static_assert(NW == 4 || NW == 8, "4 or 8 waves");
-    const int t256 = tid & 255;
-    const uint8_t* ksrc = k8 + hb * Npad * 64 + t256 * 16;
-    const int vd = t256 >> 2, vpart = (tid & 3) * 16;
-    const uint8_t* vsrc = vt8 + (hb * 64 + vd) * Npad + vpart;
-    const int nunit = Npad / 64;
-    struct Pre { i32x4 k, v; };
-    auto load_unit = [&](int u) -> Pre {
-        Pre p;
-        if (NW == 4 || tid < 256) p.k = *(const i32x4*)(ksrc + (int64_t)u * 4096);
-        if (NW == 4 || tid >= 256) p.v = *(const i32x4*)(vsrc + u * 64);
-        return p;
-    };
-    auto store_unit = [&](int buf, const Pre& p) {
-        if (NW == 4 || tid < 256) *(i32x4*)(&sm[buf][0][t256 * 16]) = p.k;
-        if (NW == 4 || tid >= 256) *(i32x4*)(&sm[buf][1][vd * 64 + vpart]) = p.v;
-    };
+// 32 bytes of row `row` of a 64-B-row tile image: 16-B chunks h and 2 + h (swizzled), so that
+// byte j is element kappa_hw(h, j) of the row (header)
+__device__ __forceinline__ i32x8 tile_row(const char* img, int row, int h) {
+    const int x = sw8(row);
+    const i32x4 a = *(const i32x4*)(img + row * 64 + ((h ^ x) << 4));
+    const i32x4 b = *(const i32x4*)(img + row * 64 + (((2 + h) ^ x) << 4));
+    return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
 
-    f32x16 o0, o1;
+// S^T of the unit in slot image `img` (scales `scw`: the lane's dword of that unit), seeded with init
+__device__ __forceinline__ void f8_s(f32x16 (&s)[2], const char* img, int scw, const F8Ctx& c, const f32x16& init) {
+    const i32x8 ka = tile_row(img, c.l32, c.h);
+    const i32x8 kb = tile_row(img, 32 + c.l32, c.h);
+    s[0] = mfma_mx<0>(ka, scw, c.qf, c.qsc, init);
+    s[1] = mfma_mx<1>(kb, scw, c.qf, c.qsc, init);
+}
+
+__device__ __forceinline__ float f8_rowmax(const f32x16 (&s)[2]) {
+    float mx[4] = {s[0][0], s[0][1], s[0][2], s[0][3]};
 #pragma unroll
-    for (int i = 0; i < 16; ++i) o0[i] = 0.f, o1[i] = 0.f;
-    float m = -INFINITY, l = 0.f;
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = (kb == 0 ? 4 : 0); r < 16; r += 4)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) mx[j] = fmaxf(mx[j], s[kb][r + j]);
+    return xhalf_max(fmaxf(fmaxf(mx[0], mx[1]), fmaxf(mx[2], mx[3])));
+}
 
-    Pre pre = load_unit(0);
-    store_unit(0, pre);
-    if (nunit > 1) pre = load_unit(1);
-    __syncthreads();
-    // one 64-key unit; TAIL: the last unit when N is not a multiple of 64 (keys >= N masked).
-    // VALU per unit and lane is the limit at the fp8 MFMA rate (4 MFMAs = 256 cycles against
-    // 32 exponentials = 256 issue cycles), so: raw v_exp_f32 (no denormal range-reduction
-    // sequence), the dequantisation scale folded into the exponent's FMA, the maximum taken
-    // on the raw scores (sscale > 0: max(raw) * sscale == max(raw * sscale) exactly), the mask
-    // only in the peeled tail unit, and the O / l rescale skipped when no lane's maximum moved
-    // (alpha == 1 exactly then: the skipped multiplications were identities).
-    auto unit = [&](int u, auto tail_tag) {
-        constexpr bool TAIL = decltype(tail_tag)::value;
-        const int buf = u & 1;
-        if (u + 1 < nunit) {
-            store_unit(buf ^ 1, pre);  // buffer buf^1 was last read in unit u-1 (barrier below)
-            if (u + 2 < nunit) pre = load_unit(u + 2);
+// keys past the ragged end to -inf: key kb * 32 + acc_row(r, h) of the unit
+__device__ __forceinline__ void f8_mask(f32x16 (&s)[2], int rem, int h) {
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            if (kb * 32 + acc_row(r, h) >= rem) s[kb][r] = -INFINITY;
+}
+
+// P(t) from sc (S - m of unit t: the running max checked and moved first), O^T += V^T P^T
+__device__ __forceinline__ void f8_pv(F8Ctx& c, f32x16 (&sc)[2], f32x16 (&sn)[2], const char* cur) {
+    const float mx = f8_rowmax(sc);
+    if (__any(mx > 0.f)) {  // some row's maximum moved: rescale o, l and the seeded scores
+        const float shift = fmaxf(mx, 0.f);
+        const float alpha = __builtin_amdgcn_exp2f(-shift);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c.l4[j] *= alpha;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) c.o[db][r] *= alpha;
+        c.m += shift;
+        const float nm = -c.m;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {  // into negm's own registers (tied), as attn_fwd2_kernel
+            float x = c.negm[r];
+            asm volatile("v_mov_b32 %0, %1" : "+v"(x) : "v"(nm));
+            c.negm[r] = x;
         }
-        const uint8_t* ks = sm[buf][0];
-        const uint8_t* vs = sm[buf][1];
-        // S^T tiles: A = K rows (keys 0-31 / 32-63 of the unit), B = Q^T
-        const i32x8 ka = *(const i32x8*)(ks + r * 64 + 32 * half);
-        const i32x8 kb = *(const i32x8*)(ks + (32 + r) * 64 + 32 * half);
-        f32x16 zero;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) zero[i] = 0.f;
-        f32x16 s0 = mfma_fp8(ka, qf, zero);
-        f32x16 s1 = mfma_fp8(kb, qf, zero);
-        if constexpr (TAIL) {
-            const int kbase = u * 64 + 4 * half;
+        for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int kr = (i & 3) + 8 * (i >> 2);
-                if (kbase + kr >= N) s0[i] = -INFINITY;
-                if (kbase + 32 + kr >= N) s1[i] = -INFINITY;
+            for (int r = 0; r < 16; ++r) {
+                sc[kb][r] -= shift;
+                sn[kb][r] -= shift;
             }
-        }
-        float mx = -INFINITY;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) mx = fmaxf(mx, fmaxf(s0[i], s1[i]));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));  // the other half holds the query's other keys
-        const float mnew = fmaxf(m, mx * sscale);
-        if (__builtin_amdgcn_read_exec() & __ballot(mnew > m)) {  // some lane's maximum moved
-            const float alpha = __builtin_amdgcn_exp2f(m - mnew);
-            l *= alpha;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) o0[i] *= alpha, o1[i] *= alpha;
-            m = mnew;
-        }
-        const float nm = -mnew;
-        float rs = 0.f;
-        i32x8 pf;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const float p0 = __builtin_amdgcn_exp2f(fmaf(s0[4 * g], sscale, nm));
-            const float p1 = __builtin_amdgcn_exp2f(fmaf(s0[4 * g + 1], sscale, nm));
-            const float p2 = __builtin_amdgcn_exp2f(fmaf(s0[4 * g + 2], sscale, nm));
-            const float p3 = __builtin_amdgcn_exp2f(fmaf(s0[4 * g + 3], sscale, nm));
-            const float p4 = __builtin_amdgcn_exp2f(fmaf(s1[4 * g], sscale, nm));
-            const float p5 = __builtin_amdgcn_exp2f(fmaf(s1[4 * g + 1], sscale, nm));
-            const float p6 = __builtin_amdgcn_exp2f(fmaf(s1[4 * g + 2], sscale, nm));
-            const float p7 = __builtin_amdgcn_exp2f(fmaf(s1[4 * g + 3], sscale, nm));
-            rs += (p0 + p1) + (p2 + p3) + (p4 + p5) + (p6 + p7);
-            pf[g] = pack4_fp8_unit(p0, p1, p2, p3);      // bytes j = 4g .. 4g+3   (t = 0)
-            pf[4 + g] = pack4_fp8_unit(p4, p5, p6, p7);  // bytes j = 16 + 4g ..   (t = 1)
-        }
-        l += rs;
-        // O^T += V^T P^T: A = V^T rows d (0-31 / 32-63), permuted key slots
-        const i32x8 va = *(const i32x8*)(vs + r * 64 + 32 * half);
-        const i32x8 vb = *(const i32x8*)(vs + (32 + r) * 64 + 32 * half);
-        o0 = mfma_fp8(va, pf, o0);
-        o1 = mfma_fp8(vb, pf, o1);
-        __syncthreads();  // everyone is done with sm[buf] and the next unit's tile is stored
-    };
-    const int nfull = N / 64;  // units with 64 valid keys; a ragged last unit is peeled
-    for (int u = 0; u < nfull; ++u) unit(u, std::false_type{});
-    if (nfull < nunit) unit(nfull, std::true_type{});
-    l += __shfl_xor(l, 32, 64);
-    if (q >= N) return;
-    const float inv = dv / l;
-    T* orow = o + ((int64_t)b * N + q) * (H * 64) + h * 64;
+    }
+    float rsp[4];
+    i32x8 pf;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-        const int d = 8 * g + 4 * half;
-        T v0[4], v1[4];
+        float p[8];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v0[e] = (T)(o0[4 * g + e] * inv), v1[e] = (T)(o1[4 * g + e] * inv);
-        *(uint2*)(orow + d) = *(const uint2*)v0;
-        *(uint2*)(orow + 32 + d) = *(const uint2*)v1;
+        for (int e = 0; e < 4; ++e) {
+            p[e] = __builtin_amdgcn_exp2f(sc[0][4 * g + e]);
+            p[4 + e] = __builtin_amdgcn_exp2f(sc[1][4 * g + e]);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float pe = p[e] + p[4 + e];
+            if (g == 0) rsp[e] = pe;
+            else rsp[e] += pe;
+        }
+        pf[g] = pack4_fp8_unit(p[0], p[1], p[2], p[3]);      // bytes j = 4g .. 4g+3   (t = 0)
+        pf[4 + g] = pack4_fp8_unit(p[4], p[5], p[6], p[7]);  // bytes j = 16 + 4g ..   (t = 1)
     }
-    if (half == 0) lse[hb * N + q] = m + log2f(l);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c.l4[j] += rsp[j];
+    const int scw = *(const int*)(cur + 8192 + c.lane * 4);
+    const i32x8 va = tile_row(cur + 4096, c.l32, c.h);
+    const i32x8 vb = tile_row(cur + 4096, 32 + c.l32, c.h);
+    c.o[0] = mfma_mx<2>(va, scw, pf, E8M0_ONE, c.o[0]);
+    c.o[1] = mfma_mx<3>(vb, scw, pf, E8M0_ONE, c.o[1]);
+}
+
+// step t (slot Q = t % 4): S(t+1) into sn beside P(t) / PV(t) from sc
+template <int Q>
+__device__ __forceinline__ void f8_step(F8Ctx& c, int t, f32x16 (&sc)[2], f32x16 (&sn)[2]) {
+    wait_vmcnt<2>();               // units t and t+1 landed (own entries; unit t+2 in flight)
+    __builtin_amdgcn_s_barrier();  // everyone's; everyone done with step t-1 (slot (t+3) % 4 free)
+    f8_issue(c, t + 3 < c.nt ? t + 3 : c.nt - 1, (Q + 3) & 3);
+    const char* cur = c.smem + Q * U8SLOT;
+    const char* nxt = c.smem + ((Q + 1) & 3) * U8SLOT;
+    // S(t+1): past the last unit the slot holds a copy of the last unit (the issue clamp), and
+    // the result is dropped — the step stays branch-free
+    f8_s(sn, nxt, *(const int*)(nxt + 8192 + c.lane * 4), c, c.negm);
+    if (t == c.nt - 1 && c.rem < 64) f8_mask(sc, c.rem, c.h);  // wave-uniform: the ragged last unit
+    f8_pv(c, sc, sn, cur);
+}
+
+// grid B * H * ceil((N - 1) / 256), 512 threads (8 waves x 32 queries 1 + ..)
+template <typename T>
+__global__ __launch_bounds__(512, 1) void attn_fp8mx_kernel(const T* __restrict__ qkv, const uint8_t* __restrict__ q8,
+                                                            const uint8_t* __restrict__ qs,
+                                                            const uint8_t* __restrict__ k8,
+                                                            const uint8_t* __restrict__ vt8,
+                                                            const uint32_t* __restrict__ sc, T* __restrict__ out,
+                                                            float* __restrict__ lse, int N, int H, int n1p) {
+    constexpr int NW = 8, QB = 32 * NW;
+    typedef typename Mfma<T>::frag frag;
+    __shared__ __attribute__((aligned(16))) char smem[4 * U8SLOT];
+    F8Ctx c;
+    c.smem = smem;
+    c.lane = threadIdx.x & 63;
+    c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    c.h = c.lane >> 5;
+    c.l32 = c.lane & 31;
+    const int n1 = N - 1;
+    const int nq = (n1 + QB - 1) / QB;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int qblk = tile % nq, bh = tile / nq, b = bh / H, hd = bh % H;
+    const int C = H * HD;
+    const int64_t ld = 3 * (int64_t)C;
+    const int64_t hb = bh;
+    c.nt = (n1 + 63) / 64;
+    c.rem = n1 - 64 * (c.nt - 1);
+    // this lane's query (row qi of the planes = token 1 + qi); rows past N compute on zero rows
+    const int qi = qblk * QB + c.wave * 32 + c.l32;
+    const bool qok = qi < n1;
+    const int qr = qok ? qi : n1 - 1;
+    {
+        const uint8_t* qrow = q8 + (hb * n1p + qr) * 64;
+        const i32x4 a = *(const i32x4*)(qrow + 16 * c.h), b = *(const i32x4*)(qrow + 32 + 16 * c.h);
+        c.qf = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+    c.qsc = qs[(hb * n1p + qr) * 2 + c.h];
+    // key 0 (CLS) from the 16-bit qkv, as attn_fwd2_kernel: s0 = q . k0 on the VALU
+    const T* Bb = qkv + (int64_t)b * N * ld;
+    const T* Qrow = Bb + (int64_t)(1 + qr) * ld + hd * HD;
+    frag q16[4], k0[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        q16[s] = *(const frag*)(Qrow + (2 * s + c.h) * 8);
+        k0[s] = *(const frag*)(Bb + C + hd * HD + (2 * s + c.h) * 8);
+    }
+    typedef T t4 __attribute__((ext_vector_type(4)));
+    t4 v0[2][4];
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) v0[db][g] = *(const t4*)(Bb + 2 * C + hd * HD + db * 32 + 8 * g + 4 * c.h);
+
+    // LDS-DMA sources: waves 0-3 the K plane (rows 16w.. of a unit), 4-7 the V^T plane
+    const bool kw = c.wave < 4;
+    const int prow = (c.wave & 3) * 16 + (c.lane >> 2);
+    const uint32_t gchunk = (uint32_t)(((c.lane & 3) ^ sw8(prow)) * 16);
+    c.rmine = kw ? make_rsrc(k8 + hb * n1p * 64, (uint32_t)n1p * 64) : make_rsrc(vt8 + hb * 64 * n1p, (uint32_t)n1p * 64);
+    c.voff = kw ? (uint32_t)prow * 64 + gchunk : (uint32_t)prow * (uint32_t)n1p + gchunk;
+    c.soff_unit = kw ? 4096u : 64u;
+    c.rsc = make_rsrc(sc + hb * (n1p / 64) * 64, (uint32_t)n1p * 4);
+    f8_issue(c, 0, 0);
+    f8_issue(c, c.nt > 1 ? 1 : 0, 1);
+    f8_issue(c, c.nt > 2 ? 2 : c.nt - 1, 2);
+
+    float part = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) part += (float)q16[s][j] * (float)k0[s][j];
+    const float s0 = xhalf_sum(part);
+
+    wait_vmcnt<4>();  // unit 0 landed (units 1, 2 in flight)
+    __builtin_amdgcn_s_barrier();
+    f32x16 sA[2], sB[2];
+    f8_s(sA, smem, *(const int*)(smem + 8192 + c.lane * 4), c, zero16());
+    if (c.nt == 1 && c.rem < 64) f8_mask(sA, c.rem, c.h);
+    c.m = fmaxf(f8_rowmax(sA), s0);
+    c.negm = splat16(-c.m);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sA[kb][r] -= c.m;
+    const float p0 = __builtin_amdgcn_exp2f(s0 - c.m);
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) c.o[db][4 * g + e] = p0 * (float)v0[db][g][e];
+    c.l4[0] = c.h == 0 ? p0 : 0.f;
+    c.l4[1] = c.l4[2] = c.l4[3] = 0.f;
+    if (c.wave >= NW / 2) __builtin_amdgcn_s_setprio(1);  // static priority for the younger half
+
+    int t = 0;
+    while (true) {  // unrolled by four: ring slots are immediates
+        if (t >= c.nt) break;
+        f8_step<0>(c, t++, sA, sB);
+        if (t >= c.nt) break;
+        f8_step<1>(c, t++, sB, sA);
+        if (t >= c.nt) break;
+        f8_step<2>(c, t++, sA, sB);
+        if (t >= c.nt) break;
+        f8_step<3>(c, t++, sB, sA);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    wait_vmcnt<0>();  // no LDS-DMA may still be landing when the workgroup retires
+
+    const float lt = xhalf_sum((c.l4[0] + c.l4[1]) + (c.l4[2] + c.l4[3]));
+    if (qok) {
+        const int q = 1 + qi;
+        store_row_t21<T>(out + ((int64_t)b * N + q) * C + hd * HD, c.o, 1.0f / lt, c.h);
+        if (c.h == 0) lse[(int64_t)bh * N + q] = c.m + __log2f(lt);
+    }
 }
 
 }  // namespace
 
 extern "C" int64_t dclip_attn_fwd_fp8_workspace(int B, int N, int H) {
-    const int64_t npad = (N + 63) / 64 * 64;
-    return 3 * (int64_t)B * H * npad * 64 + (int64_t)B * 3 * H * 4;  // q8, k8, vt8, amax
+    const int64_t n1p = (int64_t)(N - 1 + 63) / 64 * 64;
+    // q8, k8, vt8 planes, the q scales, the unit scale dwords, the row-0 pass's partials
+    return 3 * (int64_t)B * H * n1p * 64 + (int64_t)B * H * n1p * 2 + (int64_t)B * H * (n1p / 64) * 256 +
+           4 * attn_row0_ws_floats(B, N, H) + 256;
 }
 
 extern "C" int dclip_attn_fwd_fp8(int dt, const void* qkv, void* o, float* lse, void* ws, int B, int N, int H, int D,
@@ -350,43 +454,32 @@ extern "C" int dclip_attn_fwd_fp8(int dt, const void* qkv, void* o, float* lse, 
     DCLIP_HOST_CHECK(D == 64, "dclip_attn_fwd_fp8: head_dim must be 64 (got %d)", D);
     DCLIP_HOST_CHECK(dt == DCLIP_BF16 || dt == DCLIP_F16, "dclip_attn_fwd_fp8: dtype must be f16/bf16");
     DCLIP_HOST_CHECK(B > 0 && N > 0 && H > 0 && H <= 64, "dclip_attn_fwd_fp8: bad problem (B, N > 0, 0 < H <= 64)");
-    DCLIP_HOST_CHECK(((uintptr_t)qkv % 16) == 0 && ((uintptr_t)o % 8) == 0 && ((uintptr_t)ws % 256) == 0,
+    DCLIP_HOST_CHECK(((uintptr_t)qkv % 16) == 0 && ((uintptr_t)o % 16) == 0 && ((uintptr_t)ws % 256) == 0,
                      "dclip_attn_fwd_fp8: unaligned buffers");
-    const int npad = (N + 63) / 64 * 64;
-    const int64_t plane = (int64_t)B * H * npad * 64;
+    DCLIP_HOST_CHECK((int64_t)(N + 63) / 64 * 64 * 64 < (1ll << 31), "dclip_attn_fwd_fp8: N too large");
+    hipStream_t st = (hipStream_t)stream;
+    const int n1p = (N - 1 + 63) / 64 * 64;
+    const int64_t plane = (int64_t)B * H * n1p * 64;
     uint8_t* q8 = (uint8_t*)ws;
     uint8_t* k8 = q8 + plane;
     uint8_t* vt8 = k8 + plane;
-    int* amax = (int*)(vt8 + plane);  // plane is a multiple of 4096 bytes
-    hipStream_t st = (hipStream_t)stream;
-    if (hipMemsetAsync(amax, 0, (size_t)B * 3 * H * 4, st) != hipSuccess) {
-        dclip_set_error("dclip_attn_fwd_fp8: memset failed");
-        return DCLIP_ERR_HIP;
-    }
-    // CLS split (N = 1 + 256k, the benchmark's 8193): query 0 by the bf16 row pass of the
-    // 16-bit forward, queries 1..N-1 as full 256-query blocks — no near-empty last block
-    // (at N = 8193 that block held 1 query and cost a full key sweep: 33 blocks -> 32, and
-    // B*H*32 workgroups fill whole rounds of 2 workgroups per CU)
-    const bool cls = N >= 257 && (N - 1) % 256 == 0;
-    const int q0 = cls ? 1 : 0;
-    // 4-wave workgroups (128 queries; DCLIP_OPT_ATTN_FWD_WAVES 4) or 8-wave (256 queries)
-    const int fnw = dclip_option(DCLIP_OPT_ATTN_FWD_WAVES) == 4 ? 4 : 8;
-    const dim3 ga((N + 63) / 64, B), gp(npad / 64, H, B), gf((N - q0 + 32 * fnw - 1) / (32 * fnw), H, B);
-    if (cls) attn_row0_fwd(dt, qkv, o, lse, B, N, H, st);
-    const int ncol8 = 3 * H * 64 / 8;
-    const bool amax2 = 2 * ncol8 <= 1024 && (2 * ncol8) % 64 == 0;
-    if (dt == DCLIP_BF16) {
-        if (amax2) fp8_amax2_kernel<bf16><<<ga, 2 * ncol8, 0, st>>>((const bf16*)qkv, amax, N, H);
-        else fp8_amax_kernel<bf16><<<ga, 256, 0, st>>>((const bf16*)qkv, amax, N, H);
-        fp8_pack_kernel<bf16><<<gp, 256, 0, st>>>((const bf16*)qkv, amax, q8, k8, vt8, N, H, npad);
-        if (fnw == 4) attn_fp8_kernel<bf16, 4><<<gf, 256, 0, st>>>(q8, k8, vt8, amax, (bf16*)o, lse, N, H, npad, q0);
-        else attn_fp8_kernel<bf16, 8><<<gf, 512, 0, st>>>(q8, k8, vt8, amax, (bf16*)o, lse, N, H, npad, q0);
-    } else {
-        if (amax2) fp8_amax2_kernel<f16><<<ga, 2 * ncol8, 0, st>>>((const f16*)qkv, amax, N, H);
-        else fp8_amax_kernel<f16><<<ga, 256, 0, st>>>((const f16*)qkv, amax, N, H);
-        fp8_pack_kernel<f16><<<gp, 256, 0, st>>>((const f16*)qkv, amax, q8, k8, vt8, N, H, npad);
-        if (fnw == 4) attn_fp8_kernel<f16, 4><<<gf, 256, 0, st>>>(q8, k8, vt8, amax, (f16*)o, lse, N, H, npad, q0);
-        else attn_fp8_kernel<f16, 8><<<gf, 512, 0, st>>>(q8, k8, vt8, amax, (f16*)o, lse, N, H, npad, q0);
+    uint8_t* qs = vt8 + plane;
+    uint32_t* sc = (uint32_t*)(qs + (int64_t)B * H * n1p * 2);  // 4-B aligned: plane, n1p multiples of 64
+    float* r0ws = (float*)(sc + (int64_t)B * H * (n1p / 64) * 64);
+    // query 0 (the CLS row) by the 16-bit split-key row pass (its partials in the workspace)
+    attn_row0_fwd(dt, qkv, o, lse, B, N, H, st, r0ws);
+    if (N > 1) {
+        const dim3 gp(n1p / 64, H, B);
+        const int grid = B * H * ((N - 1 + 255) / 256);
+        if (dt == DCLIP_BF16) {
+            fp8mx_pack_kernel<bf16><<<gp, 256, 0, st>>>((const bf16*)qkv, q8, qs, k8, vt8, sc, N, H, n1p);
+            attn_fp8mx_kernel<bf16><<<grid, 512, 0, st>>>((const bf16*)qkv, q8, qs, k8, vt8, sc, (bf16*)o, lse, N, H,
+                                                           n1p);
+        } else {
+            fp8mx_pack_kernel<f16><<<gp, 256, 0, st>>>((const f16*)qkv, q8, qs, k8, vt8, sc, N, H, n1p);
+            attn_fp8mx_kernel<f16><<<grid, 512, 0, st>>>((const f16*)qkv, q8, qs, k8, vt8, sc, (f16*)o, lse, N, H,
+                                                          n1p);
+        }
     }
     DCLIP_LAUNCH_CHECK();
     return 0;

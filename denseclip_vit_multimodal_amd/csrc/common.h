@@ -160,8 +160,11 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
 
-// query 0 (CLS row) of the 16-bit forward: split-key row pass + merge (attention.hip)
-void attn_row0_fwd(int dt, const void* qkv, void* o, float* lse, int B, int N, int H, hipStream_t st);
+// query 0 (CLS row) of the 16-bit forward: split-key row pass + merge (attention.hip); the
+// partials go to pws (attn_row0_ws_floats floats) or, when null, into rows 1.. of o (N >= 257)
+void attn_row0_fwd(int dt, const void* qkv, void* o, float* lse, int B, int N, int H, hipStream_t st,
+                   float* pws = nullptr);
+inline int64_t attn_row0_ws_floats(int B, int N, int H) { return (int64_t)B * H * ((N + 1023) / 1024) * 4 * 66; }
 // CLS-split dK/dV pass with 64 keys per wave and AGPR accumulators (attention_dkdv6.hip); r0q
 // receives one dQ_0 partial (64 floats) per key block
 void attn_bwd_dkdv6_launch(int dt, const void* qkv, const void* dout, const float* lse, const float* delta,

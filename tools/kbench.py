@@ -78,6 +78,8 @@ def attn():
     fl = 4.0 * B * H * NT * NT * 64
     ms = timeit(lambda: O.attn_fwd(qkv, B, NT, H, 0.125))
     report("attn_fwd", ms, fl)
+    ms = timeit(lambda: O.attn_fwd_fp8(qkv, B, NT, H))
+    report("attn_fwd_fp8 (row 0 + pack + e4m3 MX kernel)", ms, fl)
     o, lse = O.attn_fwd(qkv, B, NT, H, 0.125)
     ms = timeit(lambda: O.attn_bwd(qkv, o, dout, lse, B, NT, H, 0.125))
     report("attn_bwd (delta+dq+dkdv), 2.5x fwd flops", ms, 2.5 * fl)
