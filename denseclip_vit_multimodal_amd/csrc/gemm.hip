@@ -717,6 +717,9 @@ __device__ __forceinline__ void pers_epilogue(const f32x4 (&acc)[Cfg::NB][Cfg::M
                                               int mw, int nw, int l16, int lq, float alpha,
                                               const void* __restrict__ aux, int64_t ld_aux, void* __restrict__ C,
                                               int64_t ldc, void* __restrict__ C2, int64_t ldc2) {
+#ifdef DCLIP_GEMM_DIAG_NOSTORE
+    if (alpha != 12345.0f) return;  // tools/gemm_epi_probe.hip only: the K-loop without its epilogue
+#endif
     // rows outer, column pairs inner (a row's segments stored back to back)
 #pragma unroll
     for (int j = 0; j < Cfg::MB; ++j) {
@@ -772,9 +775,104 @@ __device__ __forceinline__ void pers_epilogue(const f32x4 (&acc)[Cfg::NB][Cfg::M
     }
 }
 
+// The same epilogue with every global access a run of whole 128-B lines: a store instruction of
+// the accumulator layout above covers 16 rows x 64 B, and one CU issues those at ~32 GB/s
+// (4.3 us for a 256 x 256 bf16 tile), while 8 rows x 128 B per instruction go at ~120 GB/s
+// (tools/gemm_epi_probe.hip, profiles/r03/r03q_*).  Each wave turns its 128 x 64 tile around
+// in 16-row chunks through its own 4 KiB of LDS (past the staging ring): the accumulator-layout
+// values go in (16-bit for the bf16 / fp16 outputs, f32 where the row-major side still adds or
+// multiplies: RESIDUAL, GELU_BWD, f32 outputs) and come back out row-major, 16 B per lane.
+// XOR swizzles keep both sides free of bank conflicts:
+//   16-bit image (128-B rows, 16-B chunks c): physical chunk c ^ ((row >> 1) & 7)
+//   f32 image    (256-B rows, 16-B chunks c): physical chunk c ^ (row & 15)
+template <typename T, int EPI, typename OutT, typename Cfg>
+__device__ __forceinline__ void pers_epilogue_lds(const f32x4 (&acc)[Cfg::NB][Cfg::MB],
+                                                  const PersCols<EPI, Cfg::NB>& pc, int mw, int nw, int l16, int lq,
+                                                  int lane, float alpha, const void* __restrict__ aux, int64_t ld_aux,
+                                                  void* __restrict__ C, int64_t ldc, void* __restrict__ C2,
+                                                  int64_t ldc2, char* __restrict__ img) {
+    static_assert(Cfg::NB == 4 && Cfg::MB == 8, "128 x 64 wave tiles");
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    constexpr bool F32IMG = sizeof(OutT) == 4 || EPI == DCLIP_EPI_RESIDUAL || EPI == DCLIP_EPI_GELU_BWD;
+    // unrolled: a runtime chunk index into acc[][] would move the accumulators to scratch
+#pragma unroll
+    for (int j = 0; j < Cfg::MB; ++j) {
+        // ---- in: this lane's row l16 of the chunk, 4 columns per 16-column block i
+        if constexpr (F32IMG) {
+#pragma unroll
+            for (int i = 0; i < Cfg::NB; ++i) {
+                const f32x4 v = acc[i][j] * alpha + pc.bv[i];  // bv = 0 for GELU_BWD (as pers_epilogue)
+                const int c = (4 * i + lq) ^ (l16 & 15);
+                *(f32x4*)(img + l16 * 256 + c * 16) = v;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < Cfg::NB; ++i) {
+                f32x4 v = acc[i][j] * alpha + pc.bv[i];
+                if constexpr (EPI == DCLIP_EPI_STORE_SCALED) v *= pc.sv[i];
+                typedef OutT t4 __attribute__((ext_vector_type(4)));
+                const int c = (2 * i + (lq >> 1)) ^ ((l16 >> 1) & 7);
+                const int off = l16 * 128 + c * 16 + 8 * (lq & 1);
+                t4 z = {(OutT)v[0], (OutT)v[1], (OutT)v[2], (OutT)v[3]};
+                *(u32x2*)(img + off) = __builtin_bit_cast(u32x2, z);
+                if constexpr (EPI == DCLIP_EPI_GELU) {  // the activation sees the rounded pre-activation
+                    t4 g;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) g[e] = (OutT)quick_gelu((float)z[e]);
+                    *(u32x2*)(img + 2048 + off) = __builtin_bit_cast(u32x2, g);
+                }
+            }
+        }
+        // one wave's LDS accesses execute in order; this keeps the compiler from hoisting the
+        // reads above the writes
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // ---- out: whole rows, 16 B per lane
+        const int64_t row0 = mw + 16 * j;
+        if constexpr (F32IMG) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int rr = (lane >> 4) + 4 * q, cc = lane & 15;
+                f32x4 x = *(const f32x4*)(img + rr * 256 + ((cc ^ (rr & 15)) * 16));
+                const int64_t row = row0 + rr;
+                const int col = nw + 4 * cc;
+                if constexpr (EPI == DCLIP_EPI_RESIDUAL) {
+                    x += *(const f32x4*)((const float*)aux + row * ld_aux + col);
+                    *(f32x4*)((float*)C + row * ldc + col) = x;
+                    if (C2 != nullptr) {
+                        typedef T t4 __attribute__((ext_vector_type(4)));
+                        const t4 y = {(T)x[0], (T)x[1], (T)x[2], (T)x[3]};
+                        *(t4*)((T*)C2 + row * ldc2 + col) = y;
+                    }
+                } else if constexpr (EPI == DCLIP_EPI_GELU_BWD) {
+                    typedef T t4 __attribute__((ext_vector_type(4)));
+                    const t4 z = *(const t4*)((const T*)aux + row * ld_aux + col);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) x[e] *= quick_gelu_grad((float)z[e]);
+                    store4_out<OutT>((OutT*)C + row * ldc + col, x);
+                } else {
+                    store4_out<OutT>((OutT*)C + row * ldc + col, x);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int rr = (lane >> 3) + 8 * q, cc = lane & 7;
+                const int off = rr * 128 + ((cc ^ ((rr >> 1) & 7)) * 16);
+                const int64_t row = row0 + rr;
+                const int col = nw + 8 * cc;
+                *(u32x4*)((OutT*)C + row * ldc + col) = *(const u32x4*)(img + off);
+                if constexpr (EPI == DCLIP_EPI_GELU)
+                    *(u32x4*)((OutT*)C2 + row * ldc2 + col) = *(const u32x4*)(img + 2048 + off);
+            }
+        }
+        asm volatile("" ::: "memory");  // the next chunk's writes stay behind these reads
+    }
+}
+
 // NW = 8: 2 x 4 waves of 128 x 64 (two waves per SIMD); NW = 4: 2 x 2 waves of 128 x 128 (one
 // wave per SIMD, the accumulators in AGPRs: 2/3 of the fragment reads per MFMA)
-template <typename T, int EPI, typename OutT, int NW = 8>
+template <typename T, int EPI, typename OutT, int NW = 8, bool ELDS = false>
 __global__ __launch_bounds__(64 * NW, 1) void gemm_nt_pers_kernel(
     const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb, int K, int tiles_m, int tiles_n,
     const float* __restrict__ bias, const void* __restrict__ aux, int64_t ld_aux, void* __restrict__ C, int64_t ldc,
@@ -782,10 +880,13 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_nt_pers_kernel(
     const float alpha = alpha_arg.get();
     typedef BigCfg<256, 256, 2, NW / 2, 2, 64> Cfg;
     typedef typename Mfma<T>::frag frag;
-    __shared__ __attribute__((aligned(16))) char smem[Cfg::SMEM];
+    // the staging ring, then (NW = 8) each wave's 4 KiB epilogue image (pers_epilogue_lds)
+    constexpr int EPI_IMG = (NW == 8 && ELDS) ? 4096 : 0;
+    __shared__ __attribute__((aligned(16))) char smem[Cfg::SMEM + NW * EPI_IMG];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wm = wave / (NW / 2), wn = wave % (NW / 2);
+    constexpr bool epi_lds = NW == 8 && ELDS;
     const int l16 = lane & 15, lq = lane >> 4;
     const int ntiles = tiles_m * tiles_n;
     const int G = gridDim.x;
@@ -861,8 +962,17 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_nt_pers_kernel(
 #pragma unroll
             for (int i = 0; i < Cfg::NB; ++i) tn_acc_fence(acc[i], i == 0);
         }
-        pers_epilogue<T, EPI, OutT, Cfg>(acc, pc, m0 + wm * 128, n0 + wn * Cfg::WTN, l16, lq, alpha, aux, ld_aux, C, ldc,
-                                         C2, ldc2);
+        if constexpr (NW == 8) {
+            if constexpr (epi_lds)
+                pers_epilogue_lds<T, EPI, OutT, Cfg>(acc, pc, m0 + wm * 128, n0 + wn * Cfg::WTN, l16, lq, lane, alpha,
+                                                     aux, ld_aux, C, ldc, C2, ldc2, smem + Cfg::SMEM + wave * EPI_IMG);
+            else
+                pers_epilogue<T, EPI, OutT, Cfg>(acc, pc, m0 + wm * 128, n0 + wn * Cfg::WTN, l16, lq, alpha, aux, ld_aux,
+                                                 C, ldc, C2, ldc2);
+        } else {
+            pers_epilogue<T, EPI, OutT, Cfg>(acc, pc, m0 + wm * 128, n0 + wn * Cfg::WTN, l16, lq, alpha, aux, ld_aux, C,
+                                             ldc, C2, ldc2);
+        }
         if (un >= ntiles) break;
         u = un;
         m0 = nm0;
@@ -1812,9 +1922,17 @@ bool launch_pers(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t
                                                                          (int)(Mfull / 256), (int)(N / 256), bias, aux,
                                                                          ld_aux, C, ldc, C2, ldc2, alpha);
         else
-            gemm_nt_pers_kernel<T, EPI, OutT, NW><<<G, 64 * NW, 0, st>>>((const T*)A, lda, (const T*)B, ldb, (int)K,
-                                                                         (int)(Mfull / 256), (int)(N / 256), bias, aux,
-                                                                         ld_aux, C, ldc, C2, ldc2, alpha);
+        {
+            // the row-major LDS epilogue (default) or, DCLIP_OPT_GEMM_EPI 1, the accumulator-layout stores
+            if (NW == 8 && dclip_option(DCLIP_OPT_GEMM_EPI) != 1)
+                gemm_nt_pers_kernel<T, EPI, OutT, NW, true><<<G, 64 * NW, 0, st>>>(
+                    (const T*)A, lda, (const T*)B, ldb, (int)K, (int)(Mfull / 256), (int)(N / 256), bias, aux, ld_aux, C,
+                    ldc, C2, ldc2, alpha);
+            else
+                gemm_nt_pers_kernel<T, EPI, OutT, NW, false><<<G, 64 * NW, 0, st>>>(
+                    (const T*)A, lda, (const T*)B, ldb, (int)K, (int)(Mfull / 256), (int)(N / 256), bias, aux, ld_aux, C,
+                    ldc, C2, ldc2, alpha);
+        }
         return true;
     }
 }

@@ -188,6 +188,48 @@ def test_gemm_gelu_and_residual(M, N, K, gemm_tile):
     assert rel_err(dz.float(), ref) < TOL[dt]
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_gemm_persistent_epilogue_bitwise(dt):
+    """The persistent NT GEMM's row-major LDS epilogue (default) against the accumulator-layout
+    stores (DCLIP_OPT_GEMM_EPI 1): only the order of memory traffic differs, so every epilogue's
+    outputs must be bitwise equal (M = 8 x 8193 rows: full 256 x 256 tiles + the M tail)."""
+    from denseclip_vit_multimodal_amd import _native as Nat
+    O = ops()
+    M, K = 65544, 768
+    torch.manual_seed(3)
+    A = torch.randn(M, K, device=DEV).to(dt)
+    W = {n: (torch.randn(n, K, device=DEV) * K ** -0.5).to(dt) for n in (768, 3072)}
+    bias = {n: torch.randn(n, device=DEV) for n in (768, 3072)}
+    sc = torch.rand(768, device=DEV) + 0.5
+    res = torch.randn(M, 768, device=DEV)
+    z0 = torch.randn(M, 768, device=DEV).to(dt)
+
+    def run_all():
+        out = {}
+        out["store16"] = O.gemm(A, W[3072], bias=bias[3072])
+        out["store32"] = O.gemm(A, W[768], bias=bias[768], out_dtype=torch.float32)
+        out["scaled"] = O.gemm(A, W[768], Nat.EPI_STORE_SCALED, bias=bias[768], aux=sc)
+        out["gelu_z"], out["gelu_h"] = O.gemm(A, W[3072], Nat.EPI_GELU, bias=bias[3072])
+        out["resid"] = O.gemm(A, W[768], Nat.EPI_RESIDUAL, bias=bias[768], aux=res)
+        out["resid_lp"] = O.gemm(A, W[768], Nat.EPI_RESIDUAL, bias=bias[768], aux=res, lp_copy=True)
+        out["gelu_bwd"] = O.gemm(A, W[768], Nat.EPI_GELU_BWD, aux=z0)
+        return out
+
+    got = run_all()
+    try:
+        Nat.call("dclip_set_option", Nat.OPT_GEMM_EPI, 1)
+        ref = run_all()
+    finally:
+        Nat.call("dclip_set_option", Nat.OPT_GEMM_EPI, 0)
+    for k in ref:
+        a, b = ref[k], got[k]
+        if isinstance(a, tuple):
+            for x, y in zip(a, b):
+                assert torch.equal(x, y), k
+        else:
+            assert torch.equal(a, b), k
+
+
 @pytest.fixture
 def tn_tile(request):
     from denseclip_vit_multimodal_amd import _native as N
