@@ -63,6 +63,8 @@ _SIGS = {
     "dclip_bn_eval": [_i32, _c_void_p, _i64, _i32, _i64, _c_void_p, _c_void_p, _f32, _c_void_p, _c_void_p,
                       _c_void_p, _c_void_p, _i32, _c_void_p],
     "dclip_row_scale_add": [_c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _i64, _i32, _c_void_p],
+    "dclip_add_readout_amax": [_c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _i64, _i32, _i32, _f32, _c_void_p,
+                               _c_void_p],
     "dclip_add_readout_cast": [_c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _i32, _i64, _i32, _i32, _f32,
                                _c_void_p],
     "dclip_bn_workspace": [_i64, _i32],

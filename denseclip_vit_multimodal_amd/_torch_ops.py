@@ -106,6 +106,10 @@ def _register_fakes():
     def _(a, b, ntok, lp_dtype, scale):
         return _e(*a.shape, like=a), _e(*a.shape, like=a, dtype=lp_dtype)
 
+    @reg("dclip::add_readout_amax")
+    def _(a, b, ntok, b_scale, target):
+        return _e(*a.shape, like=a), _e(4, like=a)
+
     @reg("dclip::attn_fwd")
     def _(qkv, B, N, H, scale):
         return _e(B * N, 64 * H, like=qkv), _e(B * H * N, like=qkv, dtype=f32)

@@ -468,17 +468,9 @@ __global__ __launch_bounds__(256) void score_map_kernel(const TV* __restrict__ v
 //   0 or not finite); ws[2] = running amax bits, ws[3] = finished-workgroup count (both zero on
 //   entry, zero again on exit: the last workgroup to finish computes s and resets them).
 // |g| as uint32 bits orders like the float (non-negative), NaN / inf sort above every finite value.
-__global__ __launch_bounds__(256) void grad_scale_kernel(const float* __restrict__ g, int64_t n, float target,
-                                                         float* __restrict__ ws) {
-    uint32_t m = 0;
-    const int64_t n4 = n / 4;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-        const f32x4 v = *(const f32x4*)(g + 4 * i);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) m = max(m, __float_as_uint(v[e]) & 0x7fffffffu);
-    }
-    if (blockIdx.x == 0)
-        for (int64_t i = 4 * n4 + threadIdx.x; i < n; i += blockDim.x) m = max(m, __float_as_uint(g[i]) & 0x7fffffffu);
+// the workgroup's |x| maximum (as uint32 bits) joined into ws[2]; the last workgroup to finish
+// turns it into ws[0] = s, ws[1] = 1/s and clears ws[2], ws[3] for the next use
+__device__ __forceinline__ void amax_finish(uint32_t m, float target, float* __restrict__ ws) {
     for (int o = 32; o >= 1; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
     __shared__ uint32_t red[4];
     __shared__ bool last;
@@ -508,12 +500,40 @@ __global__ __launch_bounds__(256) void grad_scale_kernel(const float* __restrict
     }
 }
 
+// four 16-B loads in flight per thread and iteration (one at a time reached 2.2 TB/s on 201 MB)
+__global__ __launch_bounds__(256) void grad_scale_kernel(const float* __restrict__ g, int64_t n, float target,
+                                                         float* __restrict__ ws) {
+    uint32_t m = 0;
+    const int64_t n4 = n / 4;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n4; i += 4 * stride) {
+        f32x4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *(const f32x4*)(g + 4 * (i + u * stride));
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) m = max(m, __float_as_uint(v[u][e]) & 0x7fffffffu);
+    }
+    for (; i < n4; i += stride) {
+        const f32x4 v = *(const f32x4*)(g + 4 * i);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) m = max(m, __float_as_uint(v[e]) & 0x7fffffffu);
+    }
+    if (blockIdx.x == 0)
+        for (int64_t j = 4 * n4 + threadIdx.x; j < n; j += blockDim.x) m = max(m, __float_as_uint(g[j]) & 0x7fffffffu);
+    amax_finish(m, target, ws);
+}
+
 extern "C" int dclip_grad_scale(const float* g, int64_t n, float target, float* ws, void* stream) {
     DCLIP_HOST_CHECK(n >= 0 && ws != nullptr && target > 0.f, "dclip_grad_scale: bad arguments");
     DCLIP_HOST_CHECK(((uintptr_t)g % 16) == 0, "dclip_grad_scale: g must be 16-byte aligned");
     hipStream_t st = (hipStream_t)stream;
+    // every workgroup ends in one atomic on the same two words: a few hundred workgroups, not
+    // thousands (the fan-in costs ~13 ns per arrival under load)
     int64_t blocks = (n / 4 + 255) / 256;
-    blocks = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks);
+    blocks = blocks < 1 ? 1 : (blocks > 512 ? 512 : blocks);
     grad_scale_kernel<<<(unsigned)blocks, 256, 0, st>>>(g, n, target, ws);
     DCLIP_LAUNCH_CHECK();
     return 0;
@@ -786,6 +806,57 @@ extern "C" int dclip_add_readout_cast(const float* a, const void* b, int b_dt, f
     DISPATCH_DT(b_dt, TB, DISPATCH_DT(lp_dt, TO,
         if constexpr (sizeof(TO) == 2)
             add_readout_cast_kernel<TB, TO><<<g, 256, 0, st>>>(a, (const TB*)b, sum, (TO*)lp, rows, cols, ntok, scale)));
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
+
+// The fp16 backward's block-input gradient: sum = a + b * (*bsc) with b's CLS rows read as 0
+// (the read-out map's gradient joining the block output's, as dclip_add_readout_cast) and, in
+// the same pass, the power-of-two scale of sum for its fp16 cast (dclip_grad_scale's ws
+// protocol).  Replaces a 16->32-bit copy, the CLS zeroing, the HeadScale unscale, the add and
+// the separate amax pass over sum.
+template <typename TB>
+__global__ __launch_bounds__(256) void add_readout_amax_kernel(const float* a, const TB* __restrict__ b,
+                                                               const float* __restrict__ bsc, float* sum,
+                                                               int64_t rows, int cols, int ntok, float target,
+                                                               float* __restrict__ ws) {
+    const int c8 = cols / 8;
+    const int64_t n8 = rows * c8;
+    const float sb = bsc != nullptr ? *bsc : 1.0f;
+    uint32_t m = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t row = i / c8;
+        const int64_t off = i * 8;
+        f32x4 x0 = *(const f32x4*)(a + off), x1 = *(const f32x4*)(a + off + 4);
+        if (row % ntok != 0) {
+            if constexpr (sizeof(TB) == 4) {
+                x0 += *(const f32x4*)(b + off) * sb;
+                x1 += *(const f32x4*)(b + off + 4) * sb;
+            } else {
+                typedef TB tb8 __attribute__((ext_vector_type(8)));
+                const tb8 y = *(const tb8*)(b + off);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) x0[e] += (float)y[e] * sb, x1[e] += (float)y[4 + e] * sb;
+            }
+        }
+        *(f32x4*)(sum + off) = x0;
+        *(f32x4*)(sum + off + 4) = x1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            m = max(m, max(__float_as_uint(x0[e]) & 0x7fffffffu, __float_as_uint(x1[e]) & 0x7fffffffu));
+    }
+    amax_finish(m, target, ws);
+}
+
+extern "C" int dclip_add_readout_amax(const float* a, const void* b, int b_dt, const float* b_scale_ptr, float* sum,
+                                      int64_t rows, int cols, int ntok, float target, float* ws, void* stream) {
+    DCLIP_HOST_CHECK(cols % 8 == 0 && ntok > 0 && rows >= 0 && ws != nullptr && target > 0.f,
+                     "dclip_add_readout_amax: cols %% 8 == 0, ntok > 0, a workspace and target > 0");
+    DCLIP_HOST_CHECK(((uintptr_t)a | (uintptr_t)b | (uintptr_t)sum) % 16 == 0, "dclip_add_readout_amax: unaligned buffers");
+    hipStream_t st = (hipStream_t)stream;
+    const unsigned g = rows == 0 ? 1u : grid_for(rows * (cols / 8), 512);  // the fan-in (dclip_grad_scale)
+    DISPATCH_DT(b_dt, TB,
+        add_readout_amax_kernel<TB><<<g, 256, 0, st>>>(a, (const TB*)b, b_scale_ptr, sum, rows, cols, ntok, target, ws));
     DCLIP_LAUNCH_CHECK();
     return 0;
 }

@@ -290,6 +290,22 @@ std::tuple<Tensor, Tensor> add_readout_cast(const Tensor& a, const Tensor& b, in
     return {sum, lp};
 }
 
+// fp16 form: (a + b * 1/s_heads with b's CLS rows masked, the grad_scale() pair of that sum)
+std::tuple<Tensor, Tensor> add_readout_amax(const Tensor& a, const Tensor& b, int64_t ntok,
+                                            const c10::optional<Tensor>& b_scale, double target) {
+    check_gpu(a, "a"); check_gpu(b, "b", false);
+    TORCH_CHECK(a.scalar_type() == at::kFloat, "add_readout_amax: a must be f32");
+    TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && b.stride(1) == 1 && b.stride(0) == a.size(1) && a.sizes() == b.sizes(),
+                "add_readout_amax: a, b (rows, cols) row-major");
+    c10::DeviceGuard g(a.device());
+    Tensor sum = at::empty(a.sizes(), a.options());
+    Tensor ws = at::zeros({4}, a.options());
+    DCLIP_CALL(dclip_add_readout_amax(ptr<float>(a), b.data_ptr(), dt_code(b.scalar_type()), scale_entry(b_scale, 1),
+                                      ptr<float>(sum), a.size(0), (int)a.size(1), (int)ntok, (float)target,
+                                      ptr<float>(ws), stream_of(a)));
+    return {sum, ws};
+}
+
 // (x ? x : 0) + s[row % ntok] * y, f32 (rows, cols): a drop_path-scaled residual branch
 Tensor row_scale_add(const c10::optional<Tensor>& x, const Tensor& y, const Tensor& s) {
     check_gpu(y, "y"); check_gpu(s, "s"); check_opt(x, "x");
@@ -704,6 +720,7 @@ TORCH_LIBRARY(dclip, m) {
     m.def("transpose2d(Tensor x, ScalarType dtype) -> Tensor");
     m.def("transpose_batched(Tensor x, int B, int rows, int cols, int ld_in, int rows_pad, ScalarType dtype) -> Tensor");
     m.def("add_readout_cast(Tensor a, Tensor b, int ntok, ScalarType lp_dtype, float scale) -> (Tensor, Tensor)");
+    m.def("add_readout_amax(Tensor a, Tensor b, int ntok, Tensor? b_scale, float target) -> (Tensor, Tensor)");
     m.def("attn_fwd(Tensor qkv, int B, int N, int H, float scale) -> (Tensor, Tensor)");
     m.def("attn_fwd_fp8(Tensor qkv, int B, int N, int H) -> (Tensor, Tensor)");
     m.def("attn_bwd(Tensor qkv, Tensor o, Tensor dout, Tensor lse, int B, int N, int H, float scale) -> Tensor");
@@ -753,6 +770,7 @@ TORCH_LIBRARY_IMPL(dclip, CUDA, m) {
     m.impl("transpose2d", &transpose2d);
     m.impl("transpose_batched", &transpose_batched);
     m.impl("add_readout_cast", &add_readout_cast);
+    m.impl("add_readout_amax", &add_readout_amax);
     m.impl("attn_fwd", &attn_fwd);
     m.impl("attn_fwd_fp8", &attn_fwd_fp8);
     m.impl("attn_bwd", &attn_bwd);

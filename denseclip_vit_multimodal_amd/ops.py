@@ -499,6 +499,7 @@ class BlockFn(torch.autograd.Function):
         dln1w, dln1b, dln2w, dln2b = (arena[i * C:(i + 1) * C] for i in range(4))
         zb2, zb1, zbo, zbi = arena[4 * C:5 * C], arena[5 * C:9 * C], arena[9 * C:10 * C], arena[10 * C:13 * C]
         dy = None
+        s1 = None  # set here when the fold below also produced the fp16 scale of the MLP gradient
         if dxo is None:
             dxo = torch.zeros(B * Ntok, C, dtype=torch.float32, device=x.device)
         dxo = dxo.contiguous()
@@ -509,6 +510,10 @@ class BlockFn(torch.autograd.Function):
             if base is not None and cdt == torch.bfloat16 and dp is None and hsb is None:
                 # one pass: dxo + map gradient (CLS rows masked) in fp32, and its bf16 copy
                 dxo, dy = D().add_readout_cast(dxo, base, Ntok, cdt, 1.0)
+            elif base is not None and cdt == torch.float16 and dp is None:
+                # one pass: dxo + the unscaled map gradient (CLS rows masked) in fp32 and the
+                # power-of-two fp16 scale of that sum (grad_scale's pair), read by the cast below
+                dxo, s1 = D().add_readout_amax(dxo, base, Ntok, hsb, FP16_GRAD_AMAX)
             elif base is not None:
                 dr = base.float() if base.dtype != torch.float32 else base.clone()
                 dr.view(B, Ntok, C)[:, 0].zero_()
@@ -519,7 +524,8 @@ class BlockFn(torch.autograd.Function):
         # ---- MLP: xo = xm + h W2^T + b2,  h = qgelu(z),  z = xh2 W1^T + b1
         # (s1, s2: device-side power-of-two gradient scales, None unless fp16 — see grad_scale)
         dbr = dxo if dp is None else row_scale_add(None, dxo, dp[1])  # the MLP branch's gradient
-        s1 = grad_scale(dbr, cdt)
+        if s1 is None:
+            s1 = grad_scale(dbr, cdt)
         if dy is None:
             dy = cast(dbr, cdt, scale_t=s1)
         del dbr

@@ -348,6 +348,13 @@ int dclip_grad_scale(const float* g, int64_t n, float target, float* ws, void* s
 int dclip_add_readout_cast(const float* a, const void* b, int b_dt, float* sum, void* lp, int lp_dt,
                            int64_t rows, int cols, int ntok, float scale, void* stream);
 
+/* The fp16 backward's form of the same fold: sum = a + b * (*b_scale_ptr, or 1 when null) with
+ * b's CLS rows read as 0, and in the same pass ws = the dclip_grad_scale pair (s, 1/s, 0, 0) of
+ * sum for its fp16 cast (ws zeroed before first use, left reusable).  b_scale_ptr: the 1/s entry
+ * of the fp16 heads' gradient scale (the map gradient arrives scaled).  cols % 8 == 0.      */
+int dclip_add_readout_amax(const float* a, const void* b, int b_dt, const float* b_scale_ptr, float* sum,
+                           int64_t rows, int cols, int ntok, float target, float* ws, void* stream);
+
 /* Train-mode BatchNorm2d (+ optionally the ReLU after it) on a channels-last 16-bit map viewed as
  * rows (B*H*W) of C channels at a row pitch of ld elements (ld = C for a whole map; larger for a
  * channel slice of a wider buffer, e.g. one level of the neck's concatenation).  Replaces

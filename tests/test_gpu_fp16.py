@@ -45,6 +45,29 @@ def test_grad_scale_degenerate_is_one(bad):
     assert ops.grad_scale(g, torch.float16).cpu().tolist() == [1.0, 1.0, 0.0, 0.0]
 
 
+@pytest.mark.parametrize("bdt", [torch.float16, torch.float32])
+@pytest.mark.parametrize("rows,ntok,with_scale", [(2 * 513, 513, True), (8 * 8193, 8193, True), (3 * 65, 65, False)])
+def test_add_readout_amax(bdt, rows, ntok, with_scale):
+    """dclip_add_readout_amax (the fp16 backward's read-out fold): sum = a + b * (1/s of a HeadScale
+    pair) with b's CLS rows masked, bitwise as torch computes it, and the grad_scale pair of the
+    sum (the host formula); the workspace protocol leaves the pair reusable."""
+    from denseclip_vit_multimodal_amd import ops
+    cols = 768
+    a = torch.randn(rows, cols, device=DEV) * 1e-6
+    b = (torch.randn(rows, cols, device=DEV) * 8).to(bdt)
+    b[ntok + 3, 5] = 4000.0  # the maximum, in a non-CLS row
+    b[0, 7] = 1e30 if bdt == torch.float32 else 6e4  # CLS rows are ignored, maximum or not
+    hs = torch.tensor([2.0 ** 20, 2.0 ** -20, 0.0, 0.0], device=DEV) if with_scale else None
+    sm, ws = ops.D().add_readout_amax(a, b, ntok, hs, ops.FP16_GRAD_AMAX)
+    keep = (torch.arange(rows, device=DEV) % ntok != 0)[:, None]
+    bs = b.float() * (hs[1] if with_scale else 1.0)
+    ref = torch.where(keep, a + bs, a)
+    assert torch.equal(sm, ref)
+    s = host_scale(ref)
+    assert ws.cpu().tolist() == [s, 1.0 / s, 0.0, 0.0]
+    assert torch.equal(ops.grad_scale(sm, torch.float16), ws)  # same pair as the separate pass
+
+
 @pytest.mark.parametrize("M,N,K", [(200, 256, 128), (4100, 768, 768), (16392, 3072, 768)])
 def test_scaled_ops_equal_host_alpha(M, N, K):
     """gemm / weight_grad / cast / tokens_bwd with the device scale == the host-float path (the
