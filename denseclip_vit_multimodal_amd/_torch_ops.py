@@ -66,6 +66,10 @@ def _register_fakes():
     def _(A, B, bias):
         return _e(A.shape[0], B.shape[0], like=A), _e(A.shape[0], B.shape[0], like=A)
 
+    @reg("dclip::gemm_gelu_h")
+    def _(A, B, bias):
+        return _e(A.shape[0], B.shape[0], like=A)
+
     @reg("dclip::gemm_residual_lp")
     def _(A, B, bias, aux):
         return _e(A.shape[0], B.shape[0], like=A, dtype=f32), _e(A.shape[0], B.shape[0], like=A)

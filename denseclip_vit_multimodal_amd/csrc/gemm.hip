@@ -160,7 +160,7 @@ __device__ __forceinline__ void gemm_epilogue(f32x16 (&acc)[2][2], char* smem, i
                 v[e] = (float)(OutT)v[e];
                 g[e] = quick_gelu(v[e]);
             }
-            store8<OutT>((OutT*)C + (int64_t)m * ldc + nb, v, full, N - nb);
+            if (C != nullptr) store8<OutT>((OutT*)C + (int64_t)m * ldc + nb, v, full, N - nb);  // z: optional
             store8<OutT>((OutT*)C2 + (int64_t)m * ldc2 + nb, g, full, N - nb);
         } else if constexpr (EPI == DCLIP_EPI_RESIDUAL) {
             float rsd[8];
@@ -279,7 +279,7 @@ __device__ __forceinline__ void epi_row8(float (&v)[8], int m, int nb, int N, co
             v[e] = (float)(OutT)v[e];  // the activation sees the rounded pre-activation
             g[e] = quick_gelu(v[e]);
         }
-        store8<OutT>((OutT*)C + (int64_t)m * ldc + nb, v, full, rem);
+        if (C != nullptr) store8<OutT>((OutT*)C + (int64_t)m * ldc + nb, v, full, rem);  // z: optional
         store8<OutT>((OutT*)C2 + (int64_t)m * ldc2 + nb, g, full, rem);
     } else if constexpr (EPI == DCLIP_EPI_RESIDUAL) {
         float rsd[8];
@@ -759,7 +759,7 @@ __device__ __forceinline__ void pers_epilogue(const f32x4 (&acc)[Cfg::NB][Cfg::M
                         v[h][e] = (float)(OutT)v[h][e];  // the activation sees the rounded pre-activation
                         g[h][e] = quick_gelu(v[h][e]);
                     }
-                store_pair16<OutT>((OutT*)C + row * ldc, col, v[0], v[1], lq);
+                if (C != nullptr) store_pair16<OutT>((OutT*)C + row * ldc, col, v[0], v[1], lq);  // z: optional
                 store_pair16<OutT>((OutT*)C2 + row * ldc2, col, g[0], g[1], lq);
             } else if constexpr (EPI == DCLIP_EPI_GELU_BWD) {
                 typedef T t4 __attribute__((ext_vector_type(4)));
@@ -861,7 +861,8 @@ __device__ __forceinline__ void pers_epilogue_lds(const f32x4 (&acc)[Cfg::NB][Cf
                 const int off = rr * 128 + ((cc ^ ((rr >> 1) & 7)) * 16);
                 const int64_t row = row0 + rr;
                 const int col = nw + 8 * cc;
-                *(u32x4*)((OutT*)C + row * ldc + col) = *(const u32x4*)(img + off);
+                if (EPI != DCLIP_EPI_GELU || C != nullptr)  // GELU: z optional
+                    *(u32x4*)((OutT*)C + row * ldc + col) = *(const u32x4*)(img + off);
                 if constexpr (EPI == DCLIP_EPI_GELU)
                     *(u32x4*)((OutT*)C2 + row * ldc2 + col) = *(const u32x4*)(img + 2048 + off);
             }
@@ -2060,7 +2061,8 @@ extern "C" int dclip_gemm(int epilogue, int ab_dt, const void* A, int64_t lda, c
                              "dclip_gemm: STORE_SCALED needs an f32 per-column scale vector in aux and C of the operand dtype");
             break;
         case DCLIP_EPI_GELU:
-            DCLIP_HOST_CHECK(c_dt == ab_dt && C2 != nullptr, "dclip_gemm: GELU needs C and C2 of the operand dtype");
+            DCLIP_HOST_CHECK(c_dt == ab_dt && C2 != nullptr,
+                             "dclip_gemm: GELU needs C2 (and C, when z is wanted) of the operand dtype");
             break;
         case DCLIP_EPI_RESIDUAL:
             DCLIP_HOST_CHECK(c_dt == DCLIP_F32 && aux_dt == DCLIP_F32 && aux != nullptr && ldc % 4 == 0 && ld_aux % 4 == 0,

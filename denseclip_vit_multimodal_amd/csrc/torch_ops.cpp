@@ -196,6 +196,19 @@ std::tuple<Tensor, Tensor> gemm_gelu(const Tensor& A, const Tensor& B, const c10
     return {z, h};
 }
 
+// inference form: h = quick_gelu(x W^T + b) only (no z for a backward)
+Tensor gemm_gelu_h(const Tensor& A, const Tensor& B, const c10::optional<Tensor>& bias) {
+    gemm_checks(A, B);
+    c10::DeviceGuard g(A.device());
+    const int64_t M = A.size(0), N = B.size(0), K = A.size(1);
+    check_vec(bias, N, "gemm_gelu_h bias");
+    Tensor h = at::empty({M, N}, A.options());
+    DCLIP_CALL(dclip_gemm(DCLIP_EPI_GELU, dt_code(A.scalar_type()), A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0),
+                          M, N, K, 1, 1.0f, nullptr, optr<float>(bias), nullptr, 0, 0, nullptr, dt_code(A.scalar_type()),
+                          N, h.data_ptr(), h.stride(0), stream_of(A)));
+    return h;
+}
+
 // dW = alpha dy^T x (f32) and, when db is given, db += alpha colsum(dy)
 Tensor weight_grad(const Tensor& dy, const Tensor& x, double alpha, c10::optional<Tensor> db,
                    const c10::optional<Tensor>& scale) {
@@ -710,6 +723,7 @@ TORCH_LIBRARY(dclip, m) {
     m.def("gemm(Tensor A, Tensor B, int epi, Tensor? bias, Tensor? aux, ScalarType out_dtype, float alpha, "
           "Tensor? scale=None) -> Tensor");
     m.def("gemm_gelu(Tensor A, Tensor B, Tensor? bias) -> (Tensor, Tensor)");
+    m.def("gemm_gelu_h(Tensor A, Tensor B, Tensor? bias) -> Tensor");
     m.def("gemm_residual_lp(Tensor A, Tensor B, Tensor? bias, Tensor aux) -> (Tensor, Tensor)");
     m.def("weight_grad(Tensor dy, Tensor x, float alpha, Tensor(a!)? db, Tensor? scale=None) -> Tensor");
     m.def("gemm_tn(Tensor A, Tensor B) -> Tensor");
@@ -760,6 +774,7 @@ TORCH_LIBRARY_IMPL(dclip, CUDA, m) {
     m.impl("layernorm_bwd_lp", &layernorm_bwd_lp);
     m.impl("gemm", &gemm);
     m.impl("gemm_gelu", &gemm_gelu);
+    m.impl("gemm_gelu_h", &gemm_gelu_h);
     m.impl("gemm_residual_lp", &gemm_residual_lp);
     m.impl("weight_grad", &weight_grad);
     m.impl("gemm_tn", &gemm_tn);

@@ -137,6 +137,16 @@ def gemm(A, B, epi=N.EPI_STORE, bias=None, aux=None, out_dtype=None, alpha=1.0, 
     return out
 
 
+def gemm_gelu_h(A, B, bias=None):
+    """quick_gelu(A B^T + bias) alone: EPI_GELU without its pre-activation output (the forward of a
+    block no backward will run through)."""
+    _check(A, B, bias)
+    e0 = _tic()
+    out = D().gemm_gelu_h(A, B, bias)
+    _toc("gemm", e0)
+    return out
+
+
 def transpose2d(x, out_dtype):
     """(rows, cols) -> (cols, rows) in out_dtype."""
     _check(x)
@@ -460,7 +470,10 @@ class BlockFn(torch.autograd.Function):
             xm = row_scale_add(x, gemm(o, WEIGHTS.get(w_out, cdt), bias=b_out.detach(), out_dtype=torch.float32),
                                dp[0])
         xh2, mu2, rs2 = layernorm_fwd(xm, ln2w.detach(), ln2b.detach(), cdt)
-        z, h = gemm(xh2, WEIGHTS.get(w1, cdt), N.EPI_GELU, bias=b1.detach())
+        if any(ctx.needs_input_grad):
+            z, h = gemm(xh2, WEIGHTS.get(w1, cdt), N.EPI_GELU, bias=b1.detach())
+        else:  # no backward will run (frozen backbone, inference): h alone, z is never stored
+            z, h = None, gemm_gelu_h(xh2, WEIGHTS.get(w1, cdt), b1.detach())
         lp = None
         if dp is None and ro is not None and ro[2] == cdt:
             # the read-out map's token buffer comes out of the residual epilogue itself

@@ -55,7 +55,7 @@ extern "C" {
 
 /* GEMM epilogues (dclip_gemm) */
 #define DCLIP_EPI_STORE 0      /* C = acc (+ bias[n])                                  */
-#define DCLIP_EPI_GELU 1       /* C = z = acc + bias ; C2 = z * sigmoid(1.702 z)       */
+#define DCLIP_EPI_GELU 1       /* C = z = acc + bias ; C2 = z * sigmoid(1.702 z) ; C null: C2 only */
 #define DCLIP_EPI_RESIDUAL 2   /* C(f32) = aux(f32) + acc + bias (aux may alias C); C2, when set, gets the same values in ab_dt */
 #define DCLIP_EPI_GELU_BWD 3   /* C = acc * quick_gelu'(aux)       (aux = z)           */
 #define DCLIP_EPI_SPLITK 4     /* C(f32) = sum over K splits (+ bias): partial f32 slabs

@@ -169,6 +169,7 @@ def test_gemm_gelu_and_residual(M, N, K, gemm_tile):
     assert rel_err(z.float(), zr) < TOL[dt]
     hr = z.float() * torch.sigmoid(1.702 * z.float())
     assert rel_err(h.float(), hr) < TOL[dt]
+    assert torch.equal(O.gemm_gelu_h(A, B, bias), h)  # the z-less inference form: the same h
     res = torch.randn(M, N, device=DEV)
     out = O.gemm(A, B, Nat.EPI_RESIDUAL, bias=bias, aux=res)
     assert rel_err(out, res + zr) < 1e-5
