@@ -795,9 +795,29 @@ __device__ __forceinline__ void pers_epilogue_lds(const f32x4 (&acc)[Cfg::NB][Cf
     typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
     typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
     constexpr bool F32IMG = sizeof(OutT) == 4 || EPI == DCLIP_EPI_RESIDUAL || EPI == DCLIP_EPI_GELU_BWD;
+    // the row-major side input (residual rows / GELU' pre-activations), one chunk ahead: the loads
+    // of chunk j + 1 are issued before chunk j's LDS round trip, so their latency is not exposed
+    // once per chunk (the memory clobbers below keep the compiler from hoisting them itself)
+    constexpr bool AUX = EPI == DCLIP_EPI_RESIDUAL || EPI == DCLIP_EPI_GELU_BWD;
+    typedef T t4 __attribute__((ext_vector_type(4)));
+    typedef typename std::conditional<EPI == DCLIP_EPI_RESIDUAL, f32x4, t4>::type auxv;
+    auxv cur[4], nxt[4];
+    auto aux_load = [&](auxv (&dst)[4], int jj) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t row = mw + 16 * jj + (lane >> 4) + 4 * q;
+            const int col = nw + 4 * (lane & 15);
+            if constexpr (EPI == DCLIP_EPI_RESIDUAL) dst[q] = *(const f32x4*)((const float*)aux + row * ld_aux + col);
+            else dst[q] = *(const t4*)((const T*)aux + row * ld_aux + col);
+        }
+    };
+    if constexpr (AUX) aux_load(cur, 0);
     // unrolled: a runtime chunk index into acc[][] would move the accumulators to scratch
 #pragma unroll
     for (int j = 0; j < Cfg::MB; ++j) {
+        if constexpr (AUX) {
+            if (j + 1 < Cfg::MB) aux_load(nxt, j + 1);
+        }
         // ---- in: this lane's row l16 of the chunk, 4 columns per 16-column block i
         if constexpr (F32IMG) {
 #pragma unroll
@@ -837,18 +857,15 @@ __device__ __forceinline__ void pers_epilogue_lds(const f32x4 (&acc)[Cfg::NB][Cf
                 const int64_t row = row0 + rr;
                 const int col = nw + 4 * cc;
                 if constexpr (EPI == DCLIP_EPI_RESIDUAL) {
-                    x += *(const f32x4*)((const float*)aux + row * ld_aux + col);
+                    x += cur[q];
                     *(f32x4*)((float*)C + row * ldc + col) = x;
                     if (C2 != nullptr) {
-                        typedef T t4 __attribute__((ext_vector_type(4)));
                         const t4 y = {(T)x[0], (T)x[1], (T)x[2], (T)x[3]};
                         *(t4*)((T*)C2 + row * ldc2 + col) = y;
                     }
                 } else if constexpr (EPI == DCLIP_EPI_GELU_BWD) {
-                    typedef T t4 __attribute__((ext_vector_type(4)));
-                    const t4 z = *(const t4*)((const T*)aux + row * ld_aux + col);
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) x[e] *= quick_gelu_grad((float)z[e]);
+                    for (int e = 0; e < 4; ++e) x[e] *= quick_gelu_grad((float)cur[q][e]);
                     store4_out<OutT>((OutT*)C + row * ldc + col, x);
                 } else {
                     store4_out<OutT>((OutT*)C + row * ldc + col, x);
@@ -868,6 +885,12 @@ __device__ __forceinline__ void pers_epilogue_lds(const f32x4 (&acc)[Cfg::NB][Cf
             }
         }
         asm volatile("" ::: "memory");  // the next chunk's writes stay behind these reads
+        if constexpr (AUX) {
+            if (j + 1 < Cfg::MB) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
+            }
+        }
     }
 }
 

@@ -189,31 +189,33 @@ def test_gemm_gelu_and_residual(M, N, K, gemm_tile):
     assert rel_err(dz.float(), ref) < TOL[dt]
 
 
+@pytest.mark.parametrize("M,C", [(65544, 768), (85272, 1024)])  # ViT-B/16 (8 x 8193), ViT-L/14 (8 x 10659)
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
-def test_gemm_persistent_epilogue_bitwise(dt):
+def test_gemm_persistent_epilogue_bitwise(M, C, dt):
     """The persistent NT GEMM's row-major LDS epilogue (default) against the accumulator-layout
     stores (DCLIP_OPT_GEMM_EPI 1): only the order of memory traffic differs, so every epilogue's
-    outputs must be bitwise equal (M = 8 x 8193 rows: full 256 x 256 tiles + the M tail)."""
+    outputs must be bitwise equal (full 256 x 256 tiles + the M tail, at both backbones' widths)."""
     from denseclip_vit_multimodal_amd import _native as Nat
     O = ops()
-    M, K = 65544, 768
+    K = C
     torch.manual_seed(3)
     A = torch.randn(M, K, device=DEV).to(dt)
-    W = {n: (torch.randn(n, K, device=DEV) * K ** -0.5).to(dt) for n in (768, 3072)}
-    bias = {n: torch.randn(n, device=DEV) for n in (768, 3072)}
-    sc = torch.rand(768, device=DEV) + 0.5
-    res = torch.randn(M, 768, device=DEV)
-    z0 = torch.randn(M, 768, device=DEV).to(dt)
+    W = {n: (torch.randn(n, K, device=DEV) * K ** -0.5).to(dt) for n in (C, 4 * C)}
+    bias = {n: torch.randn(n, device=DEV) for n in (C, 4 * C)}
+    sc = torch.rand(C, device=DEV) + 0.5
+    res = torch.randn(M, C, device=DEV)
+    z0 = torch.randn(M, C, device=DEV).to(dt)
 
     def run_all():
         out = {}
-        out["store16"] = O.gemm(A, W[3072], bias=bias[3072])
-        out["store32"] = O.gemm(A, W[768], bias=bias[768], out_dtype=torch.float32)
-        out["scaled"] = O.gemm(A, W[768], Nat.EPI_STORE_SCALED, bias=bias[768], aux=sc)
-        out["gelu_z"], out["gelu_h"] = O.gemm(A, W[3072], Nat.EPI_GELU, bias=bias[3072])
-        out["resid"] = O.gemm(A, W[768], Nat.EPI_RESIDUAL, bias=bias[768], aux=res)
-        out["resid_lp"] = O.gemm(A, W[768], Nat.EPI_RESIDUAL, bias=bias[768], aux=res, lp_copy=True)
-        out["gelu_bwd"] = O.gemm(A, W[768], Nat.EPI_GELU_BWD, aux=z0)
+        out["store16"] = O.gemm(A, W[4 * C], bias=bias[4 * C])
+        out["store32"] = O.gemm(A, W[C], bias=bias[C], out_dtype=torch.float32)
+        out["scaled"] = O.gemm(A, W[C], Nat.EPI_STORE_SCALED, bias=bias[C], aux=sc)
+        out["gelu_z"], out["gelu_h"] = O.gemm(A, W[4 * C], Nat.EPI_GELU, bias=bias[4 * C])
+        out["gelu_h_only"] = O.gemm_gelu_h(A, W[4 * C], bias[4 * C])
+        out["resid"] = O.gemm(A, W[C], Nat.EPI_RESIDUAL, bias=bias[C], aux=res)
+        out["resid_lp"] = O.gemm(A, W[C], Nat.EPI_RESIDUAL, bias=bias[C], aux=res, lp_copy=True)
+        out["gelu_bwd"] = O.gemm(A, W[C], Nat.EPI_GELU_BWD, aux=z0)
         return out
 
     got = run_all()
