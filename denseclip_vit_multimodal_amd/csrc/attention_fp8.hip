@@ -29,8 +29,9 @@
 //                         wave and unit
 //                           S^T = K Q^T     2 MFMAs, accumulators seeded with -m (the running
 //                                           max), scales: K (opsel 0/1 of the lane's dword), q
-//                           softmax         max over the unit; on a move (any lane) rescale
-//                                           o, l and S; P = exp2(S) in place, P in [0, 1]
+//                           softmax         P = exp2(S) against the running reference; when a
+//                                           lane's row sum passes 448 (the e4m3 maximum) the
+//                                           reference moves to the unit's max and P is redone
 //                           O^T += V^T P^T  2 MFMAs, P^T converted to e4m3 in registers, scales:
 //                                           V^T (opsel 2/3), 1 for P
 //
@@ -254,11 +255,41 @@ __device__ __forceinline__ void f8_mask(f32x16 (&s)[2], int rem, int h) {
             if (kb * 32 + acc_row(r, h) >= rem) s[kb][r] = -INFINITY;
 }
 
-// P(t) from sc (S - m of unit t: the running max checked and moved first), O^T += V^T P^T
+// P = exp2(s) of unit scores s (S - m), the lane's partial row sums and the e4m3 P^T operand
+__device__ __forceinline__ void f8_exp_pack(const f32x16 (&sc)[2], float (&rsp)[4], i32x8& pf) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        float p[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            p[e] = __builtin_amdgcn_exp2f(sc[0][4 * g + e]);
+            p[4 + e] = __builtin_amdgcn_exp2f(sc[1][4 * g + e]);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float pe = p[e] + p[4 + e];
+            if (g == 0) rsp[e] = pe;
+            else rsp[e] += pe;
+        }
+        pf[g] = pack4_fp8_unit(p[0], p[1], p[2], p[3]);      // bytes j = 4g .. 4g+3   (t = 0)
+        pf[4 + g] = pack4_fp8_unit(p[4], p[5], p[6], p[7]);  // bytes j = 16 + 4g ..   (t = 1)
+    }
+}
+
+// P(t) from sc (S - m of unit t), O^T += V^T P^T.  As attn_fwd2_kernel, no per-unit row max:
+// P = exp2(S - m) is taken against the current reference m and the lane's partial row sum is
+// checked instead; only when it exceeds 448 (some P past the e4m3 maximum) is the unit re-done
+// with the reference moved to the unit's row max (o, l and the seeded S(t+1) rescaled) before
+// P(t) enters O or l.  A reference below the true running max only scales P up: e4m3's relative
+// rounding does not depend on the scale, and fewer small P fall into the subnormal range.
 __device__ __forceinline__ void f8_pv(F8Ctx& c, f32x16 (&sc)[2], f32x16 (&sn)[2], const char* cur) {
-    const float mx = f8_rowmax(sc);
-    if (__any(mx > 0.f)) {  // some row's maximum moved: rescale o, l and the seeded scores
-        const float shift = fmaxf(mx, 0.f);
+    constexpr float LIM = 448.0f;
+    float rsp[4];
+    i32x8 pf;
+    f8_exp_pack(sc, rsp, pf);
+    const float tot = (rsp[0] + rsp[1]) + (rsp[2] + rsp[3]);
+    if (__any(!(tot <= LIM))) {  // rare: move the reference to the unit's row max and redo P(t)
+        const float shift = fmaxf(f8_rowmax(sc), 0.f);
         const float alpha = __builtin_amdgcn_exp2f(-shift);
 #pragma unroll
         for (int j = 0; j < 4; ++j) c.l4[j] *= alpha;
@@ -281,25 +312,7 @@ __device__ __forceinline__ void f8_pv(F8Ctx& c, f32x16 (&sc)[2], f32x16 (&sn)[2]
                 sc[kb][r] -= shift;
                 sn[kb][r] -= shift;
             }
-    }
-    float rsp[4];
-    i32x8 pf;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-        float p[8];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            p[e] = __builtin_amdgcn_exp2f(sc[0][4 * g + e]);
-            p[4 + e] = __builtin_amdgcn_exp2f(sc[1][4 * g + e]);
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const float pe = p[e] + p[4 + e];
-            if (g == 0) rsp[e] = pe;
-            else rsp[e] += pe;
-        }
-        pf[g] = pack4_fp8_unit(p[0], p[1], p[2], p[3]);      // bytes j = 4g .. 4g+3   (t = 0)
-        pf[4 + g] = pack4_fp8_unit(p[4], p[5], p[6], p[7]);  // bytes j = 16 + 4g ..   (t = 1)
+        f8_exp_pack(sc, rsp, pf);
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) c.l4[j] += rsp[j];

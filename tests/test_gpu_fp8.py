@@ -77,8 +77,14 @@ def make_qkv(B, N, H, dt, spread=1.5):
 
 
 def emulate(qkv, B, N, H, rows):
-    """float64 on the host; `rows`: the query rows to evaluate (>= 1: row 0 is the CLS row pass).
-    Returns o (B, len(rows), C) and lse (B, H, len(rows))."""
+    """float64 on the host (the firing test in float32, as the kernel); `rows`: the query rows to
+    evaluate (>= 1: row 0 is the CLS row pass).  Returns o (B, len(rows), C) and lse (B, H, len(rows)).
+
+    The kernel's softmax schedule (attention_fp8.hip f8_pv): the reference m starts at the row max
+    of key 0 and the first unit; each unit's P = exp2(S - m) is taken against the current m, and
+    only when some lane's partial row sum (the keys of one half, (key >> 2) & 1, of the 64) in a
+    wave (32 consecutive query rows) passes 448 does every row of that wave move its m to the
+    unit's row max (by max(., 0)), rescale l and o, and redo P."""
     rows = torch.as_tensor(rows)
     assert int(rows.min()) >= 1
     C = 64 * H
@@ -89,35 +95,48 @@ def emulate(qkv, B, N, H, rows):
     xt = torch.zeros(B, n1p, 3, H, 64)
     xt[:, :n1] = x[:, 1:]
     q, k, v = xt.permute(2, 0, 3, 1, 4)  # (B, H, n1p, 64): tokens 1..
-    q8 = mx_deq(q.reshape(B, H, n1p, 2, 32)).reshape(B, H, n1p, 64)[:, :, rows - 1]
+    # every wave (32 consecutive query rows) holding a requested row, clamped past N as the kernel
+    groups = torch.unique((rows - 1) // 32)
+    G = len(groups)
+    grow = (1 + 32 * groups[:, None] + torch.arange(32)[None]).clamp(max=N - 1)  # (G, 32)
+    q8 = mx_deq(q.reshape(B, H, n1p, 2, 32)).reshape(B, H, n1p, 64)[:, :, grow - 1]  # (B, H, G, 32, 64)
     k8 = mx_deq(k.reshape(B, H, n1p, 2, 32)).reshape(B, H, n1p, 64)
     # V^T blocks: per head dim, the unit's key halves 0-31 / 32-63
     vu = v.reshape(B, H, U, 2, 32, 64).permute(0, 1, 2, 5, 3, 4)  # (B, H, U, d, key half, 32)
     v8 = mx_deq(vu).permute(0, 1, 2, 4, 5, 3).reshape(B, H, n1p, 64)
     xd = x.double()
-    q16 = xd[:, rows, 0].permute(0, 2, 1, 3)  # (B, H, R, 64)
+    q16 = xd[:, grow.reshape(-1), 0].permute(0, 2, 1, 3).reshape(B, H, G, 32, 64)
     k0, v0 = xd[:, 0, 1], xd[:, 0, 2]  # (B, H, 64)
-    s0 = (q16 @ k0.unsqueeze(-1))  # (B, H, R, 1)
-    R = len(rows)
-    m = None
-    l = acc = None
+    s0 = q16 @ k0[:, :, None, :, None]  # (B, H, G, 32, 1)
+    half = (torch.arange(64) >> 2) & 1
+    m = l = acc = None
     for u in range(U):
-        s = q8 @ k8[:, :, 64 * u:64 * u + 64].transpose(-1, -2)
+        s = q8 @ k8[:, :, None, 64 * u:64 * u + 64].transpose(-1, -2)  # (B, H, G, 32, 64)
         if 64 * u + 64 > n1:
             s[..., n1 - 64 * u:] = -math.inf
         if m is None:  # key 0 first, the reference from key 0 and the first unit
             m = torch.maximum(s0, s.amax(-1, keepdim=True))
             p0 = torch.exp2(s0 - m)
             l = p0.clone()
-            acc = p0 * v0.unsqueeze(2)
-        mn = torch.maximum(m, s.amax(-1, keepdim=True))
-        alpha = torch.exp2(m - mn)
-        p = torch.exp2(s - mn)
-        l = l * alpha + p.sum(-1, keepdim=True)
-        acc = acc * alpha + p.float().to(torch.float8_e4m3fn).double() @ v8[:, :, 64 * u:64 * u + 64]
-        m = mn
-    o = acc / l
-    return o.permute(0, 2, 1, 3).reshape(B, R, C), (m + torch.log2(l))[..., 0]
+            acc = p0 * v0[:, :, None, None, :]
+        p = torch.exp2(s - m)
+        p32 = torch.exp2((s - m).float())
+        psum = torch.stack([p32[..., half == 0].sum(-1), p32[..., half == 1].sum(-1)], -1)  # (B, H, G, 32, 2)
+        fire = ~(psum <= 448.0).all(-1).all(-1)  # (B, H, G): any lane of the wave past 448 (or NaN)
+        if bool(fire.any()):
+            shift = torch.clamp((s - m).amax(-1, keepdim=True), min=0.0) * fire[..., None, None]
+            m = m + shift
+            l = l * torch.exp2(-shift)
+            acc = acc * torch.exp2(-shift)
+            p = torch.exp2(s - m)
+        l = l + p.sum(-1, keepdim=True)
+        acc = acc + p.float().to(torch.float8_e4m3fn).double() @ v8[:, :, None, 64 * u:64 * u + 64]
+    o = (acc / l).reshape(B, H, G * 32, 64)
+    lse = (m + torch.log2(l)).reshape(B, H, G * 32)
+    gi = {int(g): i for i, g in enumerate(groups)}
+    idx = torch.tensor([gi[int((r - 1) // 32)] * 32 + int((r - 1) % 32) for r in rows])
+    o = o[:, :, idx]
+    return o.permute(0, 2, 1, 3).reshape(B, len(rows), C), lse[:, :, idx]
 
 
 def exact(qkv, B, N, H, rows=None):
