@@ -136,19 +136,41 @@ __device__ __forceinline__ void lerp_range(int i, int in, int out, int* lo, int*
     *hi = b > out - 1 ? out - 1 : b;
 }
 
+// one workgroup per (output row, 1024-column segment): the row's vertical lerp once per workgroup
+// (scalar), 4 consecutive outputs per thread, 16-byte stores when the row pitch allows.  The
+// element-per-thread form (64-bit div / mod per output, 4-byte stores) ran at ~1.1 TB/s on the
+// eval-mode 8 x 19 x 1024 x 2048 fp32 logits (`profiles/r03/r04i_*`); the arithmetic per output is
+// unchanged (same lerp, same evaluation order: bitwise the same values).
 template <typename TI, typename TO>
-__global__ void bilinear_fwd_kernel(const TI* __restrict__ in, TO* __restrict__ out, int64_t NC, int Hi, int Wi,
-                                    int Ho, int Wo) {
-    const int64_t total = NC * Ho * Wo;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-        const int x = (int)(i % Wo);
-        const int y = (int)((i / Wo) % Ho);
-        const int64_t nc = i / ((int64_t)Wo * Ho);
-        const Lerp ly = lerp_index(y, Hi, Ho), lx = lerp_index(x, Wi, Wo);
-        const TI* p = in + nc * Hi * Wi;
-        const float v00 = (float)p[ly.i0 * Wi + lx.i0], v01 = (float)p[ly.i0 * Wi + lx.i1];
-        const float v10 = (float)p[ly.i1 * Wi + lx.i0], v11 = (float)p[ly.i1 * Wi + lx.i1];
-        out[i] = (TO)(ly.l0 * (lx.l0 * v00 + lx.l1 * v01) + ly.l1 * (lx.l0 * v10 + lx.l1 * v11));
+__global__ __launch_bounds__(256) void bilinear_fwd_kernel(const TI* __restrict__ in, TO* __restrict__ out, int64_t NC,
+                                                           int Hi, int Wi, int Ho, int Wo) {
+    const int xblocks = (Wo + 1023) / 1024;
+    const int64_t row = blockIdx.x / xblocks;  // nc * Ho + y
+    const int xb = blockIdx.x - (int)(row * xblocks);
+    const int64_t nc = row / Ho;
+    const int y = (int)(row - nc * Ho);
+    const Lerp ly = lerp_index(y, Hi, Ho);
+    const TI* p0 = in + (nc * Hi + ly.i0) * Wi;
+    const TI* p1 = in + (nc * Hi + ly.i1) * Wi;
+    TO* o = out + row * Wo;
+    const int x0 = xb * 1024 + 4 * (int)threadIdx.x;
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int x = x0 + e < Wo ? x0 + e : Wo - 1;
+        const Lerp lx = lerp_index(x, Wi, Wo);
+        const float v00 = (float)p0[lx.i0], v01 = (float)p0[lx.i1];
+        const float v10 = (float)p1[lx.i0], v11 = (float)p1[lx.i1];
+        v[e] = ly.l0 * (lx.l0 * v00 + lx.l1 * v01) + ly.l1 * (lx.l0 * v10 + lx.l1 * v11);
+    }
+    if (x0 + 4 <= Wo && (Wo & 3) == 0) {
+        typedef TO to4 __attribute__((ext_vector_type(4)));
+        const to4 w = {(TO)v[0], (TO)v[1], (TO)v[2], (TO)v[3]};
+        *(to4*)(o + x0) = w;
+    } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (x0 + e < Wo) o[x0 + e] = (TO)v[e];
     }
 }
 
@@ -740,10 +762,11 @@ extern "C" int dclip_score_map(const void* v, int v_dt, int64_t bstride, int64_t
 extern "C" int dclip_bilinear_fwd(const void* in, int in_dt, void* out, int out_dt, int64_t NC, int Hi, int Wi, int Ho,
                                   int Wo, void* stream) {
     DCLIP_HOST_CHECK(Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0, "dclip_bilinear_fwd: bad sizes");
-    const int64_t total = NC * Ho * Wo;
+    const int64_t blocks = NC * Ho * ((Wo + 1023) / 1024);
+    DCLIP_HOST_CHECK(blocks < (1ll << 31), "dclip_bilinear_fwd: output too large");
     hipStream_t st = (hipStream_t)stream;
     DISPATCH_DT(in_dt, TI, DISPATCH_DT(out_dt, TO,
-        bilinear_fwd_kernel<TI, TO><<<grid_for(total), 256, 0, st>>>((const TI*)in, (TO*)out, NC, Hi, Wi, Ho, Wo)));
+        bilinear_fwd_kernel<TI, TO><<<(unsigned)blocks, 256, 0, st>>>((const TI*)in, (TO*)out, NC, Hi, Wi, Ho, Wo)));
     DCLIP_LAUNCH_CHECK();
     return 0;
 }
