@@ -1816,6 +1816,65 @@ float* tail_scratch(size_t floats) {
 
 // sum of the tail's split-K slabs + the GEMM's epilogue for rows m0 + r (r < rows), 8 columns
 // per thread
+// The M tail of a persistent NT GEMM (M = 256k + mt, mt <= 16: the 8 rows of 8 x 8193 tokens) in
+// ONE launch: a workgroup per 64 output columns, its 8 waves each summing a K / 8 slice of the
+// 16 x 64 block with 16x16x32 MFMAs on fragments loaded straight from global memory (the mt rows
+// of A are read by every workgroup from L2; rows >= mt are zero fragments), the slices added in
+// LDS in a fixed order and the epilogue applied per 8-column row segment (epi_row8).  Replaces the
+// 256-row split-K tile kernel + combine launch pair (8 + 6 us per GEMM, 97 GEMMs per step).
+template <typename T, int EPI, typename OutT>
+__global__ __launch_bounds__(512) void gemm_tail16_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B,
+                                                          int64_t ldb, int mt, int N, int K, int m0,
+                                                          const float* __restrict__ bias, const void* __restrict__ aux,
+                                                          int64_t ld_aux, void* __restrict__ C, int64_t ldc,
+                                                          void* __restrict__ C2, int64_t ldc2, Alpha alpha_arg) {
+    typedef typename Mfma<T>::frag frag;
+    __shared__ float red[8][16][68];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int l16 = lane & 15, lq = lane >> 4;
+    const int n0 = blockIdx.x * 64;
+    const int ks = K / 8, kbeg = wave * ks;
+    const bool rowok = l16 < mt;
+    const T* arow = A + (int64_t)(rowok ? l16 : 0) * lda + kbeg + 8 * lq;
+    const T* brow = B + (int64_t)(n0 + l16) * ldb + kbeg + 8 * lq;
+    f32x4 acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    frag zf;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) zf[j] = (T)0.f;
+#pragma unroll 4
+    for (int k = 0; k < ks; k += 32) {
+        const frag a = rowok ? *(const frag*)(arow + k) : zf;
+        frag b[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) b[i] = *(const frag*)(brow + (int64_t)16 * i * ldb + k);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i] = Mfma16<T>::mma(a, b[i], acc[i]);  // D[4 lq + e][16 i + l16]
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) red[wave][4 * lq + e][16 * i + l16] = acc[i][e];
+    __syncthreads();
+    const int t = threadIdx.x;
+    if (t < 128) {
+        const int r = t >> 3, cb = (t & 7) * 8;
+        if (r < mt) {
+            const float alpha = alpha_arg.get();
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                float sum = 0.f;
+#pragma unroll
+                for (int w = 0; w < 8; ++w) sum += red[w][r][cb + e];
+                v[e] = sum * alpha;
+            }
+            epi_row8<T, EPI, OutT>(v, m0 + r, n0 + cb, N, bias, aux, ld_aux, C, ldc, C2, ldc2, 0);
+        }
+    }
+}
+
 template <typename T, int EPI, typename OutT>
 __global__ void tail_combine_kernel(const float* __restrict__ ws, int splits, int rows, int N, int64_t m0,
                                     const float* __restrict__ bias, const void* __restrict__ aux, int64_t ld_aux,
@@ -1922,7 +1981,11 @@ bool launch_pers(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t
         if (ldc % 4 != 0 || (C2 != nullptr && ldc2 % 4 != 0) || (EPI == DCLIP_EPI_RESIDUAL && ld_aux % 4 != 0) ||
             (EPI == DCLIP_EPI_GELU_BWD && ld_aux % 4 != 0))
             return false;
-        if (tail > 0) {
+        if (tail > 0 && tail <= 16 && K % 256 == 0 && dclip_option(DCLIP_OPT_GEMM_TAIL) != 1) {
+            gemm_tail16_kernel<T, EPI, OutT><<<(unsigned)(N / 64), 512, 0, st>>>(
+                (const T*)A + Mfull * lda, lda, (const T*)B, ldb, (int)tail, (int)N, (int)K, (int)Mfull, bias, aux,
+                ld_aux, C, ldc, C2, ldc2, alpha);
+        } else if (tail > 0) {
             const int tiles_n = (int)(N / 256);
             const int ksteps = (int)(K / 64);
             int ts = 1;

@@ -233,6 +233,49 @@ def test_gemm_persistent_epilogue_bitwise(M, C, dt):
             assert torch.equal(a, b), k
 
 
+@pytest.mark.parametrize("K", [768, 3072])
+def test_gemm_m_tail_single_launch(K):
+    """The persistent GEMM's 8-row M tail (8 x 8193 tokens) in one MFMA launch (default) against
+    the split-K tile + combine pair (DCLIP_OPT_GEMM_TAIL 1) and an fp32 reference, every epilogue:
+    the rows before the tail are untouched by the choice (bitwise), the tail rows agree to fp32
+    summation order."""
+    from denseclip_vit_multimodal_amd import _native as Nat
+    O = ops()
+    M, C = 65544, 768
+    dt = torch.bfloat16
+    torch.manual_seed(11)
+    A = torch.randn(M, K, device=DEV).to(dt)
+    Wn = (torch.randn(C, K, device=DEV) * K ** -0.5).to(dt)
+    bias = torch.randn(C, device=DEV)
+    res = torch.randn(M, C, device=DEV)
+    z0 = torch.randn(M, C, device=DEV).to(dt)
+    sc = torch.rand(C, device=DEV) + 0.5
+
+    def run_all():
+        return {"store32": O.gemm(A, Wn, bias=bias, out_dtype=torch.float32),
+                "store16": O.gemm(A, Wn, bias=bias),
+                "scaled": O.gemm(A, Wn, Nat.EPI_STORE_SCALED, bias=bias, aux=sc),
+                "gelu_z": O.gemm(A, Wn, Nat.EPI_GELU, bias=bias)[0],
+                "gelu_h": O.gemm_gelu_h(A, Wn, bias),
+                "resid": O.gemm(A, Wn, Nat.EPI_RESIDUAL, bias=bias, aux=res),
+                "resid_lp": O.gemm(A, Wn, Nat.EPI_RESIDUAL, bias=bias, aux=res, lp_copy=True)[1],
+                "gelu_bwd": O.gemm(A, Wn, Nat.EPI_GELU_BWD, aux=z0)}
+
+    new = run_all()
+    try:
+        Nat.call("dclip_set_option", Nat.OPT_GEMM_TAIL, 1)
+        old = run_all()
+    finally:
+        Nat.call("dclip_set_option", Nat.OPT_GEMM_TAIL, 0)
+    ref = A[-8:].float() @ Wn.float().t() + bias
+    for k in new:
+        assert torch.equal(new[k][:-8], old[k][:-8]), k
+        tol = 1e-5 if new[k].dtype == torch.float32 else TOL[dt]
+        assert rel_err(new[k][-8:].float(), old[k][-8:].float()) < tol, k
+    assert rel_err(new["store32"][-8:], ref) < 1e-5
+    assert rel_err(new["resid"][-8:], res[-8:] + ref) < 1e-5
+
+
 @pytest.fixture
 def tn_tile(request):
     from denseclip_vit_multimodal_amd import _native as N
