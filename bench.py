@@ -4,6 +4,13 @@ metric, configs[1] per GPU: batch 8 per GPU, bf16), data-parallel over RCCL for 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--mode F|R]
   torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
+`--gpus N > 1` without a launcher: this process makes NO HIP call; it starts
+`python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...` as a child
+(one rank per GPU, the reference's mp.spawn world, train_denseclip.py:1649-1657), whose
+rank 0 prints the JSON line on the inherited stdout, and exits with the child's status.
+Under a launcher `--gpus` must equal WORLD_SIZE; `n_gpus` is the process group's size and
+`rccl_ranks` an all-reduce of ones over it.
+
 One step = forward of the whole DenseCLIP (ViT on the HIP kernels, text encoder, neck,
 heads, bilinear resize to the label size), CE(ignore 255) + 0.1 SILog, backward,
 gradient all-reduce (DDP over RCCL when N > 1) and AdamW.  Mode F (default, full
@@ -21,8 +28,9 @@ including the same SDPA op the reference calls) on a bounded sample on the host 
 """
 import argparse
 import json
-import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -46,9 +54,11 @@ ARCHS = {
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs of this node (default: WORLD_SIZE under a launcher, else 1); N > 1 without a "
+                         "launcher spawns torch.distributed.run with N ranks")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=8, help="images per GPU")
@@ -74,7 +84,57 @@ def parse():
                     help="process group (RCCL) + DDP even at world size 1 (torchrun --nproc-per-node 1)")
     ap.add_argument("--grad-dtype", choices=["fp32", "bf16"], default="fp32",
                     help="dtype of the DDP gradient all-reduce buckets (bf16: DDP's compression hook)")
-    return ap.parse_args()
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the BASELINE configs[3] (ViT-L/14) / configs[4] (fp8 attention) sub-measurements "
+                         "and the configs[0] CPU forward")
+    ap.add_argument("--no-op-timing", action="store_true",
+                    help="no per-op HIP-event breakdown (`ops` objects) of the headline and fp16 steps")
+    return ap.parse_args(argv)
+
+
+def free_port():
+    """An unused localhost TCP port for the rendezvous (no GPU involved)."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_cmd(argv, n, port, script=None):
+    """argv of the child that runs N ranks of this benchmark (one process per GPU, RCCL over
+    xGMI): torch.distributed.run on one node at 127.0.0.1, the same bench arguments."""
+    script = script or os.path.abspath(__file__)
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", script] + list(argv)
+
+
+def launch_env(base=None):
+    env = dict(os.environ if base is None else base)
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"  # dmabuf IPC only on this host driver (RCCL)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return env
+
+
+def spawn_ranks(argv, n, script=None):
+    """Run N ranks as a CHILD process (never exec: this process stays the parent) and return
+    its exit status; rank 0's JSON line reaches our stdout directly."""
+    proc = subprocess.run(launch_cmd(argv, n, free_port(), script), env=launch_env())
+    return proc.returncode
+
+
+def resolve_world(args, env=None):
+    """(world, spawn): world size this process runs at, and whether it must spawn the ranks
+    itself.  Under a launcher (WORLD_SIZE set) --gpus must match it."""
+    env = os.environ if env is None else env
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if args.gpus is not None and args.gpus != world:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+        return world, False
+    n = 1 if args.gpus is None else args.gpus
+    if n < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1 (got {n})")
+    return n, n > 1
 
 
 def attn_flops_fwd(B, N, H, D=64):
@@ -120,7 +180,9 @@ def run_steps(model, opt, batch, steps, silog):
     return loss
 
 
-def timed(model, opt, batch, steps, warmup, silog, world, dist_on=None):
+def timed(model, opt, batch, steps, warmup, silog, world, dist_on=None, op_timing=False):
+    """(seconds for `steps` steps, max over ranks; per-op HIP-event summary; last loss).
+    op_timing also brackets every torch.ops.dclip launch with events (ops.TIMING_OPS)."""
     from denseclip_vit_multimodal_amd import ops
     dist_on = world > 1 if dist_on is None else dist_on
     run_steps(model, opt, batch, warmup, silog)
@@ -128,6 +190,7 @@ def timed(model, opt, batch, steps, warmup, silog, world, dist_on=None):
         dist.barrier()
     torch.cuda.synchronize()
     ops.TIMING = {}
+    ops.TIMING_OPS = bool(op_timing)
     t0 = time.perf_counter()
     loss = run_steps(model, opt, batch, steps, silog)
     torch.cuda.synchronize()
@@ -136,11 +199,36 @@ def timed(model, opt, batch, steps, warmup, silog, world, dist_on=None):
     dt = time.perf_counter() - t0
     summary = ops.timing_summary()
     ops.TIMING = None
+    ops.TIMING_OPS = False
     if dist_on:
         t = torch.tensor([dt], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t)
     return dt, summary, float(loss)
+
+
+def op_breakdown(summary, steps, ms_per_step):
+    """Per-op device time per step from the `op:` events (every dclip custom-op launch on the
+    step's stream) and what is left of the step: torch-native kernels (AdamW, copies, fills),
+    the text graph's side-stream share and launch gaps."""
+    ops_ms = {k[3:]: round(v[1] / steps, 3) for k, v in summary.items() if k.startswith("op:")}
+    if not ops_ms:
+        return None
+    ops_ms = dict(sorted(ops_ms.items(), key=lambda kv: -kv[1]))
+    tot = sum(ops_ms.values())
+    return {"ms_per_step": ops_ms, "dclip_ops_ms": round(tot, 2),
+            "not_dclip_ms": round(ms_per_step - tot, 2),
+            "what": "HIP events around each torch.ops.dclip launch, per step; not_dclip = step - their sum "
+                    "(torch-native kernels: fused AdamW, copies, fills; launch gaps)"}
+
+
+def roofline(summary, key, flops, peak):
+    n, _, mean = summary.get(key, (0, 0.0, float("nan")))
+    if not n:
+        return None
+    a = flops / (mean * 1e-3) / 1e12
+    return {"achieved": round(a, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(a / peak, 4),
+            "ms_per_launch": round(mean, 4), "launches": n}
 
 
 def cpu_baseline(H, W, threads):
@@ -170,18 +258,52 @@ def cpu_baseline(H, W, threads):
                       f"oracle with SDPA attention, {dt:.1f} s"}
 
 
+def cpu_baseline_cfg0(threads):
+    """BASELINE configs[0] / SURVEY 8(d): the reference algorithm's DenseCLIP ViT-B/16 eval
+    FORWARD on 2x3x512x1024 fp32 (the oracle restatement, SDPA attention as the reference
+    calls it), all `threads` host cores."""
+    for p in (os.path.join(ROOT, "tests"), os.path.join(ROOT, "tests", "golden")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from helpers import CITYSCAPES_CFG, spec_state_dict, class_tokens, images
+    from oracle import denseclip_oracle as O
+    torch.set_num_threads(threads)
+    O.USE_SDPA = True
+    sd = spec_state_dict("cityscapes")
+    x = images(2, 512, 1024)
+    tok = class_tokens()
+    with torch.no_grad():
+        O.denseclip_forward(x[:1, :, :64, :128], sd, tok, CITYSCAPES_CFG)  # warm the allocator / MKL
+        t0 = time.perf_counter()
+        O.denseclip_forward(x, sd, tok, CITYSCAPES_CFG)
+        dt = time.perf_counter() - t0
+    O.USE_SDPA = False
+    return {"value": round(2.0 / dt, 4), "unit": "images/sec", "cores": threads, "kind": "port",
+            "sample": f"BASELINE configs[0]: DenseCLIP ViT-B/16 eval forward, 2x3x512x1024 fp32, torch CPU oracle "
+                      f"with SDPA attention, one timed pass {dt:.2f} s"}
+
+
 def main():
     global FUSED_HEAD_LOSS
     args = parse()
+    world, spawn = resolve_world(args)
+    if spawn:  # N ranks as a child process; this parent makes no HIP call at all
+        sys.exit(spawn_ranks(sys.argv[1:], world))
     FUSED_HEAD_LOSS = not args.unfused_head_loss
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist_on = world > 1 or args.ddp
+    rccl_ranks = None
     if dist_on:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")  # RCCL on ROCm (reference utils.py:106)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))  # RCCL (reference utils.py:106)
+        world = dist.get_world_size()
+        ones = torch.ones(1, device="cuda")
+        dist.all_reduce(ones)  # every rank reachable over RCCL: must equal the world size
+        rccl_ranks = int(ones.item())
+        if rccl_ranks != world:
+            raise RuntimeError(f"RCCL all-reduce over {world} ranks gave {rccl_ranks}")
     dev = torch.device("cuda", local)
     torch.manual_seed(0)
     from denseclip_vit_multimodal_amd.losses import SILogLoss
@@ -192,9 +314,9 @@ def main():
     img_dtype = torch.float16 if args.dtype == "fp16" else torch.bfloat16
     batch = synth_batch(B, H, W, dev, rank, image_dtype=img_dtype)
 
-    def setup(mode, compute_dtype=None):
-        model = make_model(dev, mode, args.arch)
-        model.backbone.attn_fp8 = args.attn_fp8
+    def setup(mode, compute_dtype=None, arch=None, attn_fp8=None):
+        model = make_model(dev, mode, arch or args.arch)
+        model.backbone.attn_fp8 = args.attn_fp8 if attn_fp8 is None else attn_fp8
         if compute_dtype is not None:
             model.backbone.compute_dtype = compute_dtype
         if args.infer:  # replicas: no gradients, no collective
@@ -206,12 +328,15 @@ def main():
         opt = make_optimizer([p for p in model.parameters() if p.requires_grad])
         return model, opt
 
+    def geometry(arch):
+        bb = ARCHS[arch] or dict(patch_size=16, heads=12)
+        return (H // bb["patch_size"]) * (W // bb["patch_size"]) + 1, bb["heads"]
+
+    op_timing = not args.no_op_timing
     model, opt = setup(args.mode)
-    dt, summ, loss = timed(model, opt, batch, args.steps, args.warmup, silog, world, dist_on)
+    dt, summ, loss = timed(model, opt, batch, args.steps, args.warmup, silog, world, dist_on, op_timing)
     value = world * B * args.steps / dt
-    bb = ARCHS[args.arch] or dict(patch_size=16, heads=12)
-    N = (H // bb["patch_size"]) * (W // bb["patch_size"]) + 1
-    heads = bb["heads"]
+    N, heads = geometry(args.arch)
 
     # attention forward roofline (one dclip_attn_fwd launch per layer)
     akey = "attn_fwd_fp8" if args.attn_fp8 else "attn_fwd"
@@ -230,7 +355,9 @@ def main():
     if os.path.exists(pmc_b) and probe_shape and not args.infer:
         with open(pmc_b) as f:
             traffic_b = json.load(f).get("hbm_bytes_per_launch")
-    kernels = {k: {"launches": v[0], "ms_total": round(v[1], 3), "ms_mean": round(v[2], 4)} for k, v in summ.items()}
+    kernels = {k: {"launches": v[0], "ms_total": round(v[1], 3), "ms_mean": round(v[2], 4)}
+               for k, v in summ.items() if not k.startswith("op:")}
+    ops_head = op_breakdown(summ, args.steps, dt / args.steps * 1e3)
     # the attention backward (dQ pass + dK/dV pass + the CLS row's merge per launch): useful work = the
     # 5 N^2-matmuls of flash backward (2.5x the forward's), same HIP-event timing
     n_ab, _, mean_ab = summ.get("attn_bwd", (0, 0.0, float("nan")))
@@ -244,52 +371,92 @@ def main():
     else:
         model_fl = 3 * model_fwd_flops(H, W, args.arch) if args.mode == "F" else None
 
+    def release():
+        nonlocal model, opt
+        model = opt = None
+        torch.cuda.empty_cache()
+
+    k_sub = max(3, args.steps // 2)
     mode_r = None
     if args.mode == "F" and not args.no_mode_r and not args.infer:
-        del model, opt
-        torch.cuda.empty_cache()
+        release()
         model, opt = setup("R")
-        dtr, _, _ = timed(model, opt, batch, max(3, args.steps // 2), 2, silog, world, dist_on)
-        mode_r = {"value": round(world * B * max(3, args.steps // 2) / dtr, 4), "unit": "images/sec",
-                  "ms_per_step": round(dtr / max(3, args.steps // 2) * 1e3, 2),
+        dtr, _, _ = timed(model, opt, batch, k_sub, 2, silog, world, dist_on)
+        mode_r = {"value": round(world * B * k_sub / dtr, 4), "unit": "images/sec",
+                  "ms_per_step": round(dtr / k_sub * 1e3, 2),
                   "what": "reference regime: backbone + text encoder frozen (train_denseclip.py:1040-1044)"}
 
     fp16 = None
     if args.mode == "F" and not args.no_fp16 and not args.infer and args.dtype == "bf16" and not args.attn_fp8:
         # the 1e-3 dtype: fp32 images (what the reference trainer feeds), fp16 compute
-        del model, opt
-        torch.cuda.empty_cache()
+        release()
         model, opt = setup("F", torch.float16)
         batch16 = synth_batch(B, H, W, dev, rank, image_dtype=torch.float32)
-        k16 = max(3, args.steps // 2)
-        dt16, s16, loss16 = timed(model, opt, batch16, k16, 2, silog, world, dist_on)
+        dt16, s16, loss16 = timed(model, opt, batch16, k_sub, 2, silog, world, dist_on, op_timing)
         del batch16
-
-        def rf(key, flops):
-            n, _, mean = s16.get(key, (0, 0.0, float("nan")))
-            if not n:
-                return None
-            a = flops / (mean * 1e-3) / 1e12
-            return {"achieved": round(a, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(a / PEAK_BF16_TFLOPS, 4), "ms_per_launch": round(mean, 4), "launches": n}
-        fp16 = {"value": round(world * B * k16 / dt16, 4), "unit": "images/sec", "ms_per_step": round(dt16 / k16 * 1e3, 2),
+        fp16 = {"value": round(world * B * k_sub / dt16, 4), "unit": "images/sec",
+                "ms_per_step": round(dt16 / k_sub * 1e3, 2),
                 "what": "mode F with fp32 images and fp16 compute (neck / heads on the HIP kernels in fp16)",
-                "loss": round(loss16, 4), "roofline_attn_bwd": rf("attn_bwd", fl_b), "roofline_attn_fwd": rf("attn_fwd", fl)}
+                "loss": round(loss16, 4), "roofline_attn_bwd": roofline(s16, "attn_bwd", fl_b, PEAK_BF16_TFLOPS),
+                "roofline_attn_fwd": roofline(s16, "attn_fwd", fl, PEAK_BF16_TFLOPS),
+                "kernels": {k: {"launches": v[0], "ms_total": round(v[1], 3), "ms_mean": round(v[2], 4)}
+                            for k, v in s16.items() if not k.startswith("op:")},
+                "ops": op_breakdown(s16, k_sub, dt16 / k_sub * 1e3)}
 
-    cpu = None
+    extras = not args.no_extras and args.mode == "F" and not args.infer and args.arch == "vitb16" \
+        and not args.attn_fp8 and args.dtype == "bf16" and (H, W) == (1024, 2048)
+    fp8 = None
+    vitl14 = None
+    if extras:
+        # BASELINE configs[4]: seg + depth heads, e4m3 MX-scaled MFMA attention forward (training: the
+        # 16-bit flash backward on its (o, lse)), same batch / resolution / dtype otherwise
+        release()
+        model, opt = setup("F", attn_fp8=True)
+        dt8, s8, loss8 = timed(model, opt, batch, k_sub, 2, silog, world, dist_on)
+        fp8 = {"value": round(world * B * k_sub / dt8, 4), "unit": "images/sec",
+               "ms_per_step": round(dt8 / k_sub * 1e3, 2), "loss": round(loss8, 4),
+               "what": "BASELINE configs[4]: mode F, seg + depth heads, attention forward on the e4m3 MFMA "
+                       "(MX E8M0 block scales), 16-bit flash backward",
+               "roofline_attn_fwd": roofline(s8, "attn_fwd_fp8", fl, PEAK_FP8_TFLOPS),
+               "roofline_attn_bwd": roofline(s8, "attn_bwd", fl_b, PEAK_BF16_TFLOPS)}
+        # BASELINE configs[3]: ViT-L/14 backbone (C 1024, 24 layers, 16 heads, N = 10659)
+        release()
+        model, opt = setup("F", arch="vitl14")
+        kl = max(2, k_sub // 2)
+        dtl, sl, lossl = timed(model, opt, batch, kl, 1, silog, world, dist_on)
+        NL, hl = geometry("vitl14")
+        fll = attn_flops_fwd(B, NL, hl)
+        vl_val = world * B * kl / dtl
+        vl_fl = 3 * model_fwd_flops(H, W, "vitl14")
+        vitl14 = {"value": round(vl_val, 4), "unit": "images/sec", "ms_per_step": round(dtl / kl * 1e3, 2),
+                  "steps": kl, "loss": round(lossl, 4), "tokens_per_image": NL,
+                  "what": "BASELINE configs[3]: ViT-L/14 DenseCLIP train step (mode F, bf16), out_indices "
+                          "[5, 11, 17, 23]",
+                  "roofline_attn_fwd": roofline(sl, "attn_fwd", fll, PEAK_BF16_TFLOPS),
+                  "roofline_attn_bwd": roofline(sl, "attn_bwd", 2.5 * fll, PEAK_BF16_TFLOPS),
+                  "model_mfma": {"flops_per_image": vl_fl,
+                                 "frac": round(vl_val / world * vl_fl / 1e12 / PEAK_BF16_TFLOPS, 4)}}
+    release()
+
+    cpu = cpu0 = None
     if rank == 0 and world == 1 and args.cpu_baseline == "auto" and args.arch == "vitb16" and not args.infer:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         try:
             cpu = cpu_baseline(H, W, threads)
         except Exception as e:  # report, do not hide
             cpu = {"value": None, "error": repr(e)[:300]}
+        if not args.no_extras:
+            try:
+                cpu0 = cpu_baseline_cfg0(threads)
+            except Exception as e:
+                cpu0 = {"value": None, "error": repr(e)[:300]}
 
     if rank == 0:
         # N >= 257 runs the CLS-split attention kernels (attention.hip bwd2_launch / fwd2, a ragged
         # N - 1 included); the fp8 forward splits CLS for N = 1 + 256k only
         cls_split = N >= 257
         fp8_split = N >= 257 and (N - 1) % 256 == 0
-        rf_fwd = {"kernel": ("attn_fp8_kernel (+ amax / pack%s)" % (" / row-0 pass" if fp8_split else "")
+        rf_fwd = {"kernel": ("attn_fp8mx_kernel (+ pack%s)" % (" / row-0 pass" if fp8_split else "")
                              if args.attn_fp8 else
                              "attn_fwd2_kernel (+ row-0 pass)" if cls_split else "attn_fwd_kernel"),
                   "bound": "mfma",
@@ -313,6 +480,7 @@ def main():
             "value": round(value, 4),
             "unit": "images/sec",
             "n_gpus": world,
+            "rccl_ranks": rccl_ranks,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 2),
@@ -334,9 +502,13 @@ def main():
             "model_mfma": {"flops_per_image": model_fl, "peak_tflops": PEAK_BF16_TFLOPS, "achieved_tflops": round(value / world * model_fl / 1e12, 1),
                            "frac": round(value / world * model_fl / 1e12 / PEAK_BF16_TFLOPS, 4)} if model_fl else None,
             "kernels": kernels,
+            "ops": ops_head,
             "mode_R": mode_r,
             "fp16": fp16,
+            "fp8": fp8,
+            "vitl14": vitl14,
             "cpu_baseline": cpu,
+            "cpu_baseline_cfg0": cpu0,
             "loss": round(loss, 4),
         }
         print(json.dumps(line), flush=True)

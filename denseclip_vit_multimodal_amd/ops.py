@@ -40,6 +40,7 @@ def _stream():
 # events recorded on the launching stream around each op (bench.py uses it to derive the
 # per-launch kernel duration inside its timed region).
 TIMING = None
+TIMING_OPS = False  # with TIMING: also every torch.ops.dclip launch, as "op:<name>" (bench's breakdown)
 STATS = {}  # path counters (tests check which path ran)
 
 
@@ -93,12 +94,31 @@ def _check(*ts, strided=()):
 _D = None
 
 
+class _TimedOps:
+    """torch.ops.dclip with HIP events around each launch (TIMING_OPS)."""
+
+    def __init__(self, d):
+        self._d = d
+
+    def __getattr__(self, name):
+        fn = getattr(self._d, name)
+
+        def call(*a, **k):
+            e0 = _tic()
+            r = fn(*a, **k)
+            _toc("op:" + name, e0)
+            return r
+        return call
+
+
 def D():
     """torch.ops.dclip (loads libdclip_torch.so on first use; raises if it is missing)."""
     global _D
     if _D is None:
         from . import _torch_ops
         _D = _torch_ops.load()
+    if TIMING_OPS and TIMING is not None:
+        return _TimedOps(_D)
     return _D
 
 
@@ -766,8 +786,11 @@ class HeadScale:
 
     def __init__(self, device, cdt):
         self.cdt = cdt
-        self.buf = torch.tensor([1.0, 1.0, 0.0, 0.0], dtype=torch.float32, device=device) \
-            if cdt == torch.float16 and torch.is_grad_enabled() else None
+        self.buf = None
+        if cdt == torch.float16 and torch.is_grad_enabled():
+            # built on the device (a host tensor would be a pageable copy + stream sync per forward)
+            self.buf = torch.ones(4, dtype=torch.float32, device=device)
+            self.buf[2:].zero_()
         self.torch_fallback = False
 
 
@@ -818,6 +841,7 @@ class HeadsOutFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, hs, *outs):
         ctx.hs = hs
+        ctx.set_materialize_grads(False)  # an unused output's gradient stays None, not zeros
         return tuple(o.float() for o in outs)
 
     @staticmethod
@@ -825,17 +849,34 @@ class HeadsOutFn(torch.autograd.Function):
         hs = ctx.hs
         cdt = hs.cdt
         if hs.buf is None or hs.torch_fallback:
+            if hs.buf is not None:
+                _warn_unscaled_fp16()
             return (None,) + tuple(None if g is None else g.to(cdt) for g in gs)
-        gs = [None if g is None else g.contiguous() for g in gs]
-        bufs = [grad_scale(g, cdt) for g in gs if g is not None]
-        if not bufs:
+        live = [g.contiguous() for g in gs if g is not None]
+        if not live:
             return (None,) + tuple(None for _ in gs)
-        sb = bufs[0]
-        for b in bufs[1:]:  # the smaller scale of the two (the larger max |g|)
-            sb = torch.where(b[0] < sb[0], b, sb)
-        hs.buf.copy_(sb)
+        # ONE scale from the joint max |g| of both heads' gradients (they sum in the neck): an
+        # all-zero gradient (an empty depth mask, silog weight 0) adds nothing to the maximum,
+        # where taking the smaller of two per-head scales let its s = 1 flush the other head's
+        # 1e-5..1e-8 gradients in the fp16 cast
+        joint = live[0] if len(live) == 1 else torch.cat([g.reshape(-1) for g in live])
+        hs.buf.copy_(grad_scale(joint, cdt))
         _stat("head_grad_scale")
-        return (None,) + tuple(None if g is None else cast(g, cdt, scale_t=hs.buf) for g in gs)
+        return (None,) + tuple(None if g is None else cast(g.contiguous(), cdt, scale_t=hs.buf) for g in gs)
+
+
+_WARNED_UNSCALED = [False]
+
+
+def _warn_unscaled_fp16():
+    """A torch fallback op in an fp16 neck / head backward: its gradients run unscaled (s = 1), so
+    the 1e-5..1e-8 segmentation gradients may flush to zero in fp16.  Said once, loudly."""
+    if not _WARNED_UNSCALED[0]:
+        import warnings
+        warnings.warn("denseclip: a neck / head op fell back to torch in an fp16 backward; its gradients are "
+                      "cast to fp16 without the power-of-two scale and may underflow (use bf16 compute, or a "
+                      "config whose neck / heads all run on the HIP kernels)", RuntimeWarning, stacklevel=2)
+        _WARNED_UNSCALED[0] = True
 
 
 def _divides(a, b):
@@ -844,12 +885,18 @@ def _divides(a, b):
 
 def neck_heads_hip_capable(model):
     """Whether every neck / head op of `model` (a DenseCLIP) has a HIP kernel for 16-bit maps at
-    its widths (decided from the module shapes before the backbone runs): the per-level 3x3
+    its widths and in its current mode (decided before the backbone runs): the per-level 3x3
     convs (Cin % 128, Cout % 64, concatenated width <= 2048), the 1x1 fusion conv (Cin, Cout %
-    64), the BN widths (% 8, <= 2048) and the FCN heads (3x3 Cin % 128, 1x1 Cin % 64)."""
+    64), the BNs (width % 8, <= 2048, a momentum, and training mode whenever a gradient will
+    pass them) and the FCN heads (3x3 Cin % 128, 1x1 Cin % 64)."""
+    # an eval-mode BN that a gradient must pass (the frozen-BN fine-tune pattern) has no HIP
+    # backward (bn_hip_ok: training mode; bn_eval_ok: no gradient), and would fall back to torch
+    grads = torch.is_grad_enabled() and any(p.requires_grad for p in model.parameters())
+
     def bn_ok(bn):
         return (isinstance(bn, torch.nn.BatchNorm2d) and _divides(bn.num_features, 8) and bn.num_features <= 2048
-                and bn.affine and bn.track_running_stats)
+                and bn.affine and bn.track_running_stats and bn.momentum is not None
+                and (bn.training or not grads))
 
     def conv3_ok(conv, cin):
         return (conv.kernel_size == (3, 3) and conv.padding == (1, 1) and conv.stride == (1, 1) and conv.bias is None

@@ -132,22 +132,40 @@ def make_optimizer(params, fused=None):
     return torch.optim.AdamW(params, lr=2e-5, weight_decay=0.01, fused=fused)
 
 
-def step_unless_nonfinite(opt, loss):
-    """opt.step(), skipped when the loss is NaN / Inf — the reference trainer skips such a step
-    (train_denseclip.py:1323; e.g. a batch whose labels are all ignored gives a NaN CE).
-
-    Fused torch optimizers take the decision ON THE DEVICE through their `found_inf` input (the
-    AdamW kernel leaves parameters, moments and the step count untouched when it is non-zero): no
-    host sync.  Under torch.distributed the flag is MAX-reduced first, so every rank skips
-    together and the replicas stay identical.  Non-fused optimizers check on the host."""
-    if not all(g.get("fused") for g in opt.param_groups):
-        if bool(torch.isfinite(loss.detach()).all()):
-            opt.step()
-        return
-    flag = (~torch.isfinite(loss.detach().reshape(-1)[0])).to(torch.float32)  # 0-dim, like GradScaler's
+def nonfinite_flag(opt, loss, check_grads=True):
+    """0-dim f32 on the loss's device: 1 when the loss — or, with check_grads, any gradient the
+    optimizer would apply — is NaN / Inf; MAX-reduced over the process group so every rank takes
+    the same decision.  The gradient check is one multi-tensor inf-norm pass (no host sync); it
+    catches an fp16 overflow in a backward whose loss stayed finite (the neck / heads run on one
+    power-of-two gradient scale, ops.HeadScale)."""
+    flag = (~torch.isfinite(loss.detach().reshape(-1)[0])).to(torch.float32)
+    if check_grads:
+        grads = [p.grad for g in opt.param_groups for p in g["params"] if p.grad is not None]
+        if grads:
+            norms = torch._foreach_norm(grads, float("inf"))
+            bad = (~torch.isfinite(torch.stack([n.to(flag.device) for n in norms]))).any()
+            flag = torch.maximum(flag, bad.to(torch.float32))
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+    return flag
+
+
+def step_unless_nonfinite(opt, loss, check_grads=True):
+    """opt.step(), skipped when the loss (or a gradient, check_grads) is NaN / Inf — the reference
+    trainer skips such a step (train_denseclip.py:1323; e.g. a batch whose labels are all ignored
+    gives a NaN CE).
+
+    Fused torch optimizers take the decision ON THE DEVICE through their `found_inf` input (the
+    AdamW kernel leaves parameters, moments and the step count untouched when it is non-zero): no
+    host sync.  Non-fused optimizers read the flag on the host.  Either way the flag is
+    MAX-reduced over the process group first, so every rank skips together and the replicas stay
+    identical (a per-rank host check would let one rank skip while the others step)."""
+    flag = nonfinite_flag(opt, loss, check_grads)
+    if not all(g.get("fused") for g in opt.param_groups):
+        if not bool(flag):
+            opt.step()
+        return
     opt.found_inf = flag
     try:
         opt.step()

@@ -256,3 +256,24 @@ def test_frozen_weights_keep_their_cache():
     assert ops.WEIGHTS.get_with(p, torch.bfloat16, "t", lambda w: w * 1) is not vp
     ops.invalidate_weight_cache()
     assert ops.WEIGHTS.get_with(frozen, torch.bfloat16, "t", lambda w: w * 1) is not vf
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_nonfinite_gradient_skips_the_step(fused):
+    """a finite loss with a non-finite gradient (an fp16 overflow in the neck / heads
+    backward) skips the step too; the check makes no host sync on the fused path."""
+    from denseclip_vit_multimodal_amd.train import step_unless_nonfinite
+    p = torch.nn.Parameter(torch.ones(4))
+    q = torch.nn.Parameter(torch.ones(3))
+    opt = torch.optim.AdamW([p, q], lr=0.1, fused=fused)
+    p.grad = torch.ones(4)
+    q.grad = torch.tensor([1.0, float("inf"), 0.0])
+    step_unless_nonfinite(opt, torch.tensor(0.5))
+    assert torch.equal(p.detach(), torch.ones(4)) and torch.equal(q.detach(), torch.ones(3))
+    q.grad = torch.ones(3)
+    step_unless_nonfinite(opt, torch.tensor(0.5))
+    assert not torch.equal(p.detach(), torch.ones(4))
+    p0 = p.detach().clone()
+    q.grad = torch.tensor([float("nan"), 0.0, 0.0])
+    step_unless_nonfinite(opt, torch.tensor(0.5), check_grads=False)  # the reference's loss-only rule
+    assert not torch.equal(p.detach(), p0)

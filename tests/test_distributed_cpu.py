@@ -160,3 +160,33 @@ def test_wrap_ddp_leaves_gradless_parameters_out(tmp_path, cfg):
             assert (id(p) in managed) == (n not in dead), n
     finally:
         dist.destroy_process_group()
+
+
+def _skip_worker(rank, world, port, out_dir, fused):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    from denseclip_vit_multimodal_amd.utils import init_distributed, cleanup
+    from denseclip_vit_multimodal_amd.train import step_unless_nonfinite
+    init_distributed(rank, world, backend="gloo")
+    try:
+        w = torch.nn.Parameter(torch.ones(5))
+        opt = torch.optim.AdamW([w], lr=0.1, fused=fused)
+        w.grad = torch.full((5,), 0.5)  # all-reduced gradients are identical on every rank
+        loss = torch.tensor(float("nan") if rank == 1 else 1.0)  # only rank 1's local loss is NaN
+        step_unless_nonfinite(opt, loss)
+        torch.save({"w": w.detach().clone()}, os.path.join(out_dir, f"skip{rank}.pt"))
+    finally:
+        cleanup()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("fused", [False, True], ids=["foreach", "fused"])
+def test_nonfinite_skip_is_rank_consistent(tmp_path, fused):
+    """one rank's non-finite loss skips the step on EVERY rank (the flag is MAX-reduced
+    for non-fused optimizers too), so the replicas stay identical."""
+    world = 2
+    mp.spawn(_skip_worker, args=(world, _free_port(), str(tmp_path), fused), nprocs=world, join=True)
+    for i in range(world):
+        w = torch.load(tmp_path / f"skip{i}.pt", weights_only=True)["w"]
+        assert torch.equal(w, torch.ones(5)), (i, w)
