@@ -216,10 +216,12 @@ def op_breakdown(summary, steps, ms_per_step):
         return None
     ops_ms = dict(sorted(ops_ms.items(), key=lambda kv: -kv[1]))
     tot = sum(ops_ms.values())
-    return {"ms_per_step": ops_ms, "dclip_ops_ms": round(tot, 2),
+    return {"ms_per_step": ops_ms, "dclip_ops_ms": round(tot, 2), "step_ms_with_events": round(ms_per_step, 2),
             "not_dclip_ms": round(ms_per_step - tot, 2),
-            "what": "HIP events around each torch.ops.dclip launch, per step; not_dclip = step - their sum "
-                    "(torch-native kernels: fused AdamW, copies, fills; launch gaps)"}
+            "what": "a separate 2-step pass after the timed region with HIP events around each torch.ops.dclip "
+                    "launch (the events slow the step by ~4 %, so they are kept out of the reported time); "
+                    "not_dclip = that pass's step time - the ops' sum (torch-native kernels: fused AdamW, "
+                    "copies, fills; launch gaps)"}
 
 
 def roofline(summary, key, flops, peak):
@@ -297,7 +299,7 @@ def main():
     if dist_on:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))  # RCCL (reference utils.py:106)
+        dist.init_process_group("nccl")  # RCCL on ROCm (reference utils.py:106)
         world = dist.get_world_size()
         ones = torch.ones(1, device="cuda")
         dist.all_reduce(ones)  # every rank reachable over RCCL: must equal the world size
@@ -333,8 +335,18 @@ def main():
         return (H // bb["patch_size"]) * (W // bb["patch_size"]) + 1, bb["heads"]
 
     op_timing = not args.no_op_timing
+
+    def op_pass(model, opt, batch_, steps=2):
+        """The per-op breakdown from its OWN short pass after the timed region: HIP events around
+        every launch cost ~4 % of a step, so they never bracket the reported time."""
+        if not op_timing:
+            return None
+        dto, so, _ = timed(model, opt, batch_, steps, 0, silog, world, dist_on, True)
+        return op_breakdown(so, steps, dto / steps * 1e3)
+
     model, opt = setup(args.mode)
-    dt, summ, loss = timed(model, opt, batch, args.steps, args.warmup, silog, world, dist_on, op_timing)
+    dt, summ, loss = timed(model, opt, batch, args.steps, args.warmup, silog, world, dist_on)
+    ops_head = op_pass(model, opt, batch)
     value = world * B * args.steps / dt
     N, heads = geometry(args.arch)
 
@@ -357,7 +369,6 @@ def main():
             traffic_b = json.load(f).get("hbm_bytes_per_launch")
     kernels = {k: {"launches": v[0], "ms_total": round(v[1], 3), "ms_mean": round(v[2], 4)}
                for k, v in summ.items() if not k.startswith("op:")}
-    ops_head = op_breakdown(summ, args.steps, dt / args.steps * 1e3)
     # the attention backward (dQ pass + dK/dV pass + the CLS row's merge per launch): useful work = the
     # 5 N^2-matmuls of flash backward (2.5x the forward's), same HIP-event timing
     n_ab, _, mean_ab = summ.get("attn_bwd", (0, 0.0, float("nan")))
@@ -392,7 +403,8 @@ def main():
         release()
         model, opt = setup("F", torch.float16)
         batch16 = synth_batch(B, H, W, dev, rank, image_dtype=torch.float32)
-        dt16, s16, loss16 = timed(model, opt, batch16, k_sub, 2, silog, world, dist_on, op_timing)
+        dt16, s16, loss16 = timed(model, opt, batch16, k_sub, 2, silog, world, dist_on)
+        ops16 = op_pass(model, opt, batch16)
         del batch16
         fp16 = {"value": round(world * B * k_sub / dt16, 4), "unit": "images/sec",
                 "ms_per_step": round(dt16 / k_sub * 1e3, 2),
@@ -401,7 +413,7 @@ def main():
                 "roofline_attn_fwd": roofline(s16, "attn_fwd", fl, PEAK_BF16_TFLOPS),
                 "kernels": {k: {"launches": v[0], "ms_total": round(v[1], 3), "ms_mean": round(v[2], 4)}
                             for k, v in s16.items() if not k.startswith("op:")},
-                "ops": op_breakdown(s16, k_sub, dt16 / k_sub * 1e3)}
+                "ops": ops16}
 
     extras = not args.no_extras and args.mode == "F" and not args.infer and args.arch == "vitb16" \
         and not args.attn_fp8 and args.dtype == "bf16" and (H, W) == (1024, 2048)

@@ -114,6 +114,14 @@ def _register_fakes():
     def _(a, b, ntok, b_scale, target):
         return _e(*a.shape, like=a), _e(4, like=a)
 
+    @reg("dclip::add_readout_cast_scaled")
+    def _(a, b, ntok, b_scale, st, target):
+        return (_e(*a.shape, like=a) if b is not None else _e(0, like=a)), _e(*a.shape, like=a, dtype=torch.float16), _e(4, like=a)
+
+    @reg("dclip::layernorm_bwd_scaled")
+    def _(dy, x, w, mean, rstd, res, dw, db, st, target):
+        return _e(*x.shape, like=x, dtype=f32), _e(*x.shape, like=x, dtype=torch.float16), _e(4, like=x)
+
     @reg("dclip::attn_fwd")
     def _(qkv, B, N, H, scale):
         return _e(B * N, 64 * H, like=qkv), _e(B * H * N, like=qkv, dtype=f32)

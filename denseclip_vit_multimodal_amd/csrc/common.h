@@ -152,6 +152,49 @@ struct Alpha {
     __device__ __forceinline__ float get() const { return p ? v * *p : v; }
 };
 
+// Power-of-two fp16 gradient scale from a grid-wide |x| maximum, on the device.  st = {s, 1/s,
+// amax bits, arrivals}; st[2], st[3] are zero on entry.  Every workgroup (NW waves) joins its
+// maximum m (|x| as uint32 bits: they order like the floats, NaN / inf above every finite value);
+// the last workgroup to arrive writes st[0] = s = 2^clamp(floor(log2(target / amax)), -60, 60),
+// st[1] = 1/s (s = 1 for an all-zero or non-finite maximum) and clears st[2], st[3] for the next
+// use.  (dclip_grad_scale; the delayed-scale casts write the scale of the NEXT use into st, and
+// KEEP the current one when the maximum is not finite: an inf that arrived from an overflow
+// upstream says nothing about this site's own range.)
+template <int NW, bool KEEP_ON_NONFINITE = false>
+__device__ __forceinline__ void scale_finish(uint32_t m, float target, float* __restrict__ st) {
+    for (int o = 32; o >= 1; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+    __shared__ uint32_t red[NW];
+    __shared__ bool last;
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        m = red[0];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) m = max(m, red[w]);
+        uint32_t* stu = (uint32_t*)st;
+        atomicMax(stu + 2, m);
+        __threadfence();
+        last = atomicAdd(stu + 3, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last && threadIdx.x == 0) {
+        __threadfence();
+        uint32_t* stu = (uint32_t*)st;
+        const uint32_t bits = atomicMax(stu + 2, 0u);
+        int e = 0;
+        if (bits != 0 && bits < 0x7f800000u) {
+            const double l = floor(log2((double)target / (double)__uint_as_float(bits)));
+            e = (int)fmin(60.0, fmax(-60.0, l));
+        }
+        if (!KEEP_ON_NONFINITE || bits < 0x7f800000u) {
+            st[0] = ldexpf(1.f, e);
+            st[1] = ldexpf(1.f, -e);
+        }
+        atomicExch(stu + 2, 0u);
+        atomicExch(stu + 3, 0u);
+    }
+}
+
 // bijective XCD-aware remap of a linear block id (8 XCDs, round-robin dispatch):
 // consecutive logical tiles land on the same XCD so they share its L2.
 __device__ __forceinline__ int xcd_remap(int bid, int nblk) {

@@ -493,33 +493,7 @@ __global__ __launch_bounds__(256) void score_map_kernel(const TV* __restrict__ v
 // the workgroup's |x| maximum (as uint32 bits) joined into ws[2]; the last workgroup to finish
 // turns it into ws[0] = s, ws[1] = 1/s and clears ws[2], ws[3] for the next use
 __device__ __forceinline__ void amax_finish(uint32_t m, float target, float* __restrict__ ws) {
-    for (int o = 32; o >= 1; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
-    __shared__ uint32_t red[4];
-    __shared__ bool last;
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        m = max(max(red[0], red[1]), max(red[2], red[3]));
-        uint32_t* wsu = (uint32_t*)ws;
-        atomicMax(wsu + 2, m);
-        __threadfence();
-        last = atomicAdd(wsu + 3, 1u) == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (last && threadIdx.x == 0) {
-        __threadfence();
-        uint32_t* wsu = (uint32_t*)ws;
-        const uint32_t bits = atomicMax(wsu + 2, 0u);
-        int e = 0;
-        if (bits != 0 && bits < 0x7f800000u) {
-            const double l = floor(log2((double)target / (double)__uint_as_float(bits)));
-            e = (int)fmin(60.0, fmax(-60.0, l));
-        }
-        ws[0] = ldexpf(1.f, e);
-        ws[1] = ldexpf(1.f, -e);
-        atomicExch(wsu + 2, 0u);
-        atomicExch(wsu + 3, 0u);
-    }
+    scale_finish<4>(m, target, ws);
 }
 
 // four 16-B loads in flight per thread and iteration (one at a time reached 2.2 TB/s on 201 MB)
@@ -880,6 +854,75 @@ extern "C" int dclip_add_readout_amax(const float* a, const void* b, int b_dt, c
     const unsigned g = rows == 0 ? 1u : grid_for(rows * (cols / 8), 512);  // the fan-in (dclip_grad_scale)
     DISPATCH_DT(b_dt, TB,
         add_readout_amax_kernel<TB><<<g, 256, 0, st>>>(a, (const TB*)b, b_scale_ptr, sum, rows, cols, ntok, target, ws));
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
+
+// The fp16 backward's block-input gradient on a DELAYED scale: sum = a (+ b * (*bsc), b's CLS
+// rows read as 0; b may be null) and lp = (f16)(sum * s) in one pass, s = st[0] the power-of-two
+// scale the previous use of this gradient derived from its maximum; (s, 1/s) go to spair for
+// lp's consumers and this use's |sum| maximum becomes st's scale for the next (scale_finish).
+// One pass where the exact scale needs two (the maximum, then the cast).
+template <typename TB>
+__global__ __launch_bounds__(256) void add_readout_cast_ds_kernel(const float* a, const TB* __restrict__ b,
+                                                                  const float* __restrict__ bsc, float* sum,
+                                                                  f16* __restrict__ lp, int64_t rows, int cols,
+                                                                  int ntok, float target, float* __restrict__ st,
+                                                                  float* __restrict__ spair) {
+    const int c8 = cols / 8;
+    const int64_t n8 = rows * c8;
+    const float sb = bsc != nullptr ? *bsc : 1.0f;
+    const float ls = st[0];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        spair[0] = ls;
+        spair[1] = st[1];
+    }
+    uint32_t m = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t row = i / c8;
+        const int64_t off = i * 8;
+        f32x4 x0 = *(const f32x4*)(a + off), x1 = *(const f32x4*)(a + off + 4);
+        if (b != nullptr) {
+            if (row % ntok != 0) {
+                if constexpr (sizeof(TB) == 4) {
+                    x0 += *(const f32x4*)(b + off) * sb;
+                    x1 += *(const f32x4*)(b + off + 4) * sb;
+                } else {
+                    typedef TB tb8 __attribute__((ext_vector_type(8)));
+                    const tb8 y = *(const tb8*)(b + off);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) x0[e] += (float)y[e] * sb, x1[e] += (float)y[4 + e] * sb;
+                }
+            }
+            *(f32x4*)(sum + off) = x0;
+            *(f32x4*)(sum + off + 4) = x1;
+        }
+        f16x8 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            m = max(m, max(__float_as_uint(x0[e]) & 0x7fffffffu, __float_as_uint(x1[e]) & 0x7fffffffu));
+            o[e] = (f16)(x0[e] * ls);
+            o[4 + e] = (f16)(x1[e] * ls);
+        }
+        *(f16x8*)(lp + off) = o;
+    }
+    scale_finish<4, true>(m, target, st);
+}
+
+extern "C" int dclip_add_readout_cast_scaled(const float* a, const void* b, int b_dt, const float* b_scale_ptr,
+                                             float* sum, void* lp, int64_t rows, int cols, int ntok, float target,
+                                             float* st, float* spair, void* stream) {
+    DCLIP_HOST_CHECK(cols % 8 == 0 && ntok > 0 && rows > 0 && target > 0.f && st != nullptr && spair != nullptr,
+                     "dclip_add_readout_cast_scaled: cols %% 8 == 0, ntok > 0, rows > 0, target > 0, st and spair");
+    DCLIP_HOST_CHECK(b == nullptr || sum != nullptr, "dclip_add_readout_cast_scaled: sum is required with b");
+    DCLIP_HOST_CHECK(((uintptr_t)a | (uintptr_t)b | (uintptr_t)sum | (uintptr_t)lp) % 16 == 0,
+                     "dclip_add_readout_cast_scaled: unaligned buffers");
+    hipStream_t s = (hipStream_t)stream;
+    const unsigned g = grid_for(rows * (cols / 8), 512);  // the fan-in (dclip_grad_scale)
+    if (b == nullptr) b_dt = DCLIP_F32;
+    DISPATCH_DT(b_dt, TB,
+        add_readout_cast_ds_kernel<TB><<<g, 256, 0, s>>>(a, (const TB*)b, b_scale_ptr, sum, (f16*)lp, rows, cols, ntok,
+                                                         target, st, spair));
     DCLIP_LAUNCH_CHECK();
     return 0;
 }

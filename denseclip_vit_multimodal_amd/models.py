@@ -294,21 +294,33 @@ class CLIPVisionTransformer(nn.Module):
         hsb = ops._head_scale_buf()  # the 16-bit heads' gradient scale (DenseCLIP, fp16, fp32 images)
         rmeta = (B, Ntok, gh, gw, mdt, hsb)
         last = max(self.out_indices) if self.out_indices else -1
+        fp16_bwd = cdt == torch.float16 and torch.is_grad_enabled()
         for i, blk in enumerate(self.transformer.resblocks):
             if i > last:
                 break  # later blocks feed nothing the reference returns
             dp = _drop_path_masks(blk, Ntok, x.device) if self.training else None
+            # the fp16 backward's delayed gradient scales live on the block across steps (meta[7])
+            ds = _delayed_scale(blk) if fp16_bwd else None
             if i in self.out_indices and i != self.layers - 1:
                 # read-out without ln_post: produced by the block itself, so its gradient is
                 # folded into the block's backward (ops.BlockFn, meta[5])
-                bmeta = meta + ((gh, gw, mdt, hsb),) + ((dp,) if dp is not None else ())
+                bmeta = meta + ((gh, gw, mdt, hsb), dp, ds)
                 tok, fmap = ops.BlockFn.apply(tok, bmeta, *blk.hip_params())
                 outs.append(fmap)
                 continue
-            tok = ops.BlockFn.apply(tok, meta + ((None, dp) if dp is not None else ()), *blk.hip_params())
+            tok = ops.BlockFn.apply(tok, meta + (None, dp, ds), *blk.hip_params())
             if i in self.out_indices:  # the last layer: ln_post (models.py:576)
                 outs.append(ops.ReadoutFn.apply(tok, self.ln_post.weight, self.ln_post.bias, rmeta))
         return outs
+
+
+def _delayed_scale(blk):
+    """The block's ops.DelayedScale (created on first use; not a parameter or buffer: it is no part
+    of the state dict)."""
+    ds = blk.__dict__.get("_dclip_dscale")
+    if ds is None:
+        ds = blk.__dict__["_dclip_dscale"] = ops.DelayedScale()
+    return ds
 
 
 def _drop_path_masks(blk, ntok, device):

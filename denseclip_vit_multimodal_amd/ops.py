@@ -200,6 +200,50 @@ def grad_scale(g, cdt):
     return D().grad_scale(g if g.is_contiguous() else g.contiguous(), FP16_GRAD_AMAX)
 
 
+# fp16 backward: the block gradients' casts on DELAYED scales (the previous step's maximum at the
+# same site; dclip_add_readout_cast_scaled / dclip_layernorm_bwd_scaled) — one pass where the
+# exact scale needs a maximum pass and a cast pass.  False: exact scales every step.
+FP16_DELAYED_SCALE = True
+
+
+class DelayedScale:
+    """Per-block state of the fp16 backward's delayed gradient scales, kept on the block module
+    across training steps: site 0 = the MLP branch's incoming gradient, site 1 = the attention
+    branch's.  A site's first backward takes the exact two-pass scale and seeds the state
+    (`primed`); later ones cast with the scale the previous backward derived from its own maximum
+    and leave this one's for the next (include/dclip.h, dclip_add_readout_cast_scaled)."""
+
+    def __init__(self):
+        self.buf = None
+        self.primed = [False, False]
+
+    def site(self, i, device):
+        if self.buf is None or self.buf.device != device:
+            self.buf = torch.zeros(8, dtype=torch.float32, device=device)
+            self.primed = [False, False]
+        return self.buf[4 * i:4 * i + 4]
+
+    def prime(self, i, pair):
+        """Seed site i with the exact (s, 1/s, ..) pair of this backward."""
+        st = self.site(i, pair.device)
+        st[:2].copy_(pair[:2])
+        self.primed[i] = True
+
+
+def add_readout_cast_scaled(a, b, ntok, b_scale, st):
+    """(a + b * 1/s_heads with b's CLS rows masked, or a when b is None; its fp16 copy on st's
+    delayed scale; the (s, 1/s) pair of that copy)."""
+    _check(a, b_scale, st, strided=(b,) if b is not None else ())
+    sm, lp, pair = D().add_readout_cast_scaled(a, b, ntok, b_scale, st, FP16_GRAD_AMAX)
+    return (sm if b is not None else a), lp, pair
+
+
+def layernorm_bwd_scaled(dy, x, w, mean, rstd, dw, db, res, st):
+    """layernorm_bwd with res and an fp16 copy of dx on st's delayed scale: (dx, lp, pair)."""
+    _check(dy, x, w, mean, rstd, dw, db, res, st)
+    return D().layernorm_bwd_scaled(dy, x, w, mean, rstd, res, dw, db, st, FP16_GRAD_AMAX)
+
+
 def weight_grad(dy, x, want_bias=True, alpha=1.0, db=None, scale=None):
     """dW = alpha dy^T x (N x K, fp32) and db += alpha colsum(dy) for dy (M, N), x (M, K)
     (compute dtype); scale: a grad_scale() buffer whose 1/s also multiplies both.
@@ -521,6 +565,8 @@ class BlockFn(torch.autograd.Function):
         # its o — the straight-through gradient of the quantised forward
         B, Ntok, H, cdt, fp8 = ctx.meta[:5]
         dp = ctx.meta[6] if len(ctx.meta) > 6 else None
+        # fp16 delayed scales (meta[7], a DelayedScale): only on the plain residual form
+        ds = ctx.meta[7] if len(ctx.meta) > 7 and cdt == torch.float16 and dp is None and FP16_DELAYED_SCALE else None
         C = x.shape[1]
         scale = (C // H) ** -0.5
         need = ctx.needs_input_grad
@@ -536,6 +582,17 @@ class BlockFn(torch.autograd.Function):
         if dxo is None:
             dxo = torch.zeros(B * Ntok, C, dtype=torch.float32, device=x.device)
         dxo = dxo.contiguous()
+        dev = x.device
+        if ds is not None and ds.primed[0]:
+            base = hsb = None
+            if dmap is not None:
+                gh, gw = ctx.meta[5][:2]
+                hsb = ctx.meta[5][3] if len(ctx.meta[5]) > 3 else None
+                base = _readout_grad_buffer(dmap, B, Ntok, gh, gw, C)
+            if dmap is None or base is not None:
+                # one pass: (+ the map gradient) and the fp16 operand on the delayed scale
+                dxo, dy, s1 = add_readout_cast_scaled(dxo, base, Ntok, hsb, ds.site(0, dev))
+                dmap = None
         if dmap is not None:  # the read-out map's gradient joins the block output's
             gh, gw = ctx.meta[5][:2]
             hsb = ctx.meta[5][3] if len(ctx.meta[5]) > 3 else None  # HeadScale buffer (fp16 heads)
@@ -561,6 +618,8 @@ class BlockFn(torch.autograd.Function):
             s1 = grad_scale(dbr, cdt)
         if dy is None:
             dy = cast(dbr, cdt, scale_t=s1)
+        if ds is not None and not ds.primed[0]:
+            ds.prime(0, s1)
         del dbr
         dz = gemm(dy, WEIGHTS.get(w2, cdt, transposed=True), N.EPI_GELU_BWD, aux=z)
         dW2 = db2 = dW1 = db1 = None
@@ -570,18 +629,23 @@ class BlockFn(torch.autograd.Function):
         if wg:
             dW1, db1 = weight_grad(dz, xh2, db=zb1, scale=s1)
         del dz
+        dyo = None
         if cdt == torch.bfloat16 and dp is None:  # no gradient scaling: the attention branch's operand comes out of the LN pass
             dxm, dyo = layernorm_bwd(dxh2, xm, ln2w.detach(), mu2, rs2, dln2w, dln2b, res=dxo, lp_dtype=cdt)
             s2 = None
+        elif ds is not None and ds.primed[1]:  # fp16: the operand on the delayed scale, same pass
+            dxm, dyo, s2 = layernorm_bwd_scaled(dxh2, xm, ln2w.detach(), mu2, rs2, dln2w, dln2b, dxo, ds.site(1, dev))
         else:
             dxm = layernorm_bwd(dxh2, xm, ln2w.detach(), mu2, rs2, dln2w, dln2b, res=dxo)
         del dxh2
         # ---- attention: xm = x + o Wout^T + bout
-        if cdt != torch.bfloat16 or dp is not None:
+        if dyo is None:
             dab = dxm if dp is None else row_scale_add(None, dxm, dp[0])  # the attention branch's gradient
             s2 = grad_scale(dab, cdt)
             dyo = cast(dab, cdt, scale_t=s2)
             del dab
+            if ds is not None:
+                ds.prime(1, s2)
         do = gemm(dyo, WEIGHTS.get(w_out, cdt, transposed=True))
         dWo = dbo = dWi = dbi = None
         if wg:

@@ -182,8 +182,16 @@ def train_step(model, opt, batch, silog=None, seg_weight=1.0, silog_weight=0.1):
     loss = loss_fn(out, seg, depth, mask, silog, seg_weight, silog_weight)
     opt.zero_grad(set_to_none=True)
     loss.backward()
-    step_unless_nonfinite(opt, loss)
+    # the gradients are checked too when the backward ran in fp16 (power-of-two scaled casts can
+    # overflow there); bf16 / fp32 keep the reference's loss-only rule
+    step_unless_nonfinite(opt, loss, check_grads=fp16_backward(model))
     return loss.detach()
+
+
+def fp16_backward(model):
+    """Whether the model's backward runs in fp16 (the backbone's compute dtype)."""
+    bb = getattr(_unwrap(model), "backbone", None)
+    return getattr(bb, "compute_dtype", None) == torch.float16
 
 
 # ---------------------------------------------------------------------------- checkpoints

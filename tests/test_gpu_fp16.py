@@ -68,6 +68,101 @@ def test_add_readout_amax(bdt, rows, ntok, with_scale):
     assert torch.equal(ops.grad_scale(sm, torch.float16), ws)  # same pair as the separate pass
 
 
+@pytest.mark.parametrize("with_b", [True, False])
+@pytest.mark.parametrize("rows,ntok", [(2 * 513, 513), (8 * 8193, 8193)])
+def test_add_readout_cast_scaled(rows, ntok, with_b):
+    """The delayed-scale fold: sum as dclip_add_readout_amax computes it (bitwise), lp = (f16)(sum *
+    s) with s the state's scale (bitwise: a power of two), the pair it used, and the state left at
+    THIS sum's exact scale (the host formula) for the next call; a second call then casts with it."""
+    from denseclip_vit_multimodal_amd import ops
+    cols = 768
+    a = torch.randn(rows, cols, device=DEV) * 1e-6
+    b = (torch.randn(rows, cols, device=DEV) * 8).half() if with_b else None
+    hs = torch.tensor([2.0 ** 20, 2.0 ** -20, 0.0, 0.0], device=DEV)
+    st = torch.tensor([2.0 ** 17, 2.0 ** -17, 0.0, 0.0], device=DEV)  # the previous use's scale
+    sm, lp, pair = ops.add_readout_cast_scaled(a, b, ntok, hs if with_b else None, st)
+    if with_b:
+        keep = (torch.arange(rows, device=DEV) % ntok != 0)[:, None]
+        ref = torch.where(keep, a + b.float() * hs[1], a)
+        assert torch.equal(sm, ref)
+    else:
+        ref = a
+        assert sm is a
+    assert torch.equal(lp, (ref * 2.0 ** 17).half())
+    assert pair[:2].cpu().tolist() == [2.0 ** 17, 2.0 ** -17]
+    s = host_scale(ref)
+    assert st.cpu().tolist() == [s, 1.0 / s, 0.0, 0.0]
+    _, lp2, pair2 = ops.add_readout_cast_scaled(a, b, ntok, hs if with_b else None, st)
+    assert torch.equal(lp2, (ref * s).half()) and pair2[:2].cpu().tolist() == [s, 1.0 / s]
+
+
+def test_delayed_scale_keeps_state_on_nonfinite():
+    """An inf arriving from an overflow upstream leaves the site's scale as it was."""
+    from denseclip_vit_multimodal_amd import ops
+    a = torch.randn(4 * 65, 768, device=DEV) * 1e-3
+    a[7, 9] = float("inf")
+    st = torch.tensor([2.0 ** 12, 2.0 ** -12, 0.0, 0.0], device=DEV)
+    ops.add_readout_cast_scaled(a, None, 65, None, st)
+    assert st.cpu().tolist() == [2.0 ** 12, 2.0 ** -12, 0.0, 0.0]
+
+
+@pytest.mark.parametrize("cols", [768, 1024])
+def test_layernorm_bwd_scaled(cols):
+    """dclip_layernorm_bwd_scaled == layernorm_bwd (dx, dw, db) plus lp = (f16)(dx * s) on the
+    state's scale, the pair, and the state advanced to dx's exact scale."""
+    from denseclip_vit_multimodal_amd import ops
+    rows = 8 * 1025
+    x = torch.randn(rows, cols, device=DEV)
+    w = torch.rand(cols, device=DEV) + 0.5
+    b = torch.randn(cols, device=DEV)
+    _, mean, rstd = ops.layernorm_fwd(x, w, b, torch.float16)
+    dy = torch.randn(rows, cols, device=DEV) * 1e-7
+    res = torch.randn(rows, cols, device=DEV) * 1e-7
+    dw0, db0 = torch.zeros(cols, device=DEV), torch.zeros(cols, device=DEV)
+    dx0 = ops.layernorm_bwd(dy, x, w, mean, rstd, dw0, db0, res=res)
+    dw1, db1 = torch.zeros(cols, device=DEV), torch.zeros(cols, device=DEV)
+    st = torch.tensor([2.0 ** 21, 2.0 ** -21, 0.0, 0.0], device=DEV)
+    dx1, lp, pair = ops.layernorm_bwd_scaled(dy, x, w, mean, rstd, dw1, db1, res, st)
+    assert torch.equal(dx1, dx0)
+    assert rel_err(dw1, dw0) < 1e-6 and rel_err(db1, db0) < 1e-6  # atomics: order-dependent sums
+    assert torch.equal(lp, (dx0 * 2.0 ** 21).half())
+    assert pair[:2].cpu().tolist() == [2.0 ** 21, 2.0 ** -21]
+    s = host_scale(dx0)
+    assert st.cpu().tolist() == [s, 1.0 / s, 0.0, 0.0]
+
+
+def test_fp16_delayed_scale_steps_match_exact():
+    """ViT-B/16 fp16 backward, three passes with the same data: the first takes the exact scales
+    and primes every block's DelayedScale; the later ones cast on the delayed scales (no
+    grad_scale pass left in the blocks) and give the same gradients as the exact-scale path
+    (identical data, so the delayed scale IS the exact one: equal up to the order of the LN /
+    bias-gradient atomics)."""
+    from denseclip_vit_multimodal_amd import ops
+    m = _model(torch.float16)
+    bb = m.backbone.train()
+    x = images(1, 128, 256).to(DEV).half()
+    gen = torch.Generator().manual_seed(7)
+    ws = None
+    grads = []
+    for it in range(3):
+        if it == 2:
+            ops.FP16_DELAYED_SCALE = False  # exact scales again, as a reference
+        try:
+            bb.zero_grad(set_to_none=True)
+            maps = bb(x)
+            if ws is None:
+                ws = [(torch.randn(mp.shape, generator=gen) * 1e-6).to(DEV) for mp in maps]
+            sum((mp.float() * w).sum() for mp, w in zip(maps, ws)).backward()
+            grads.append({n: p.grad.clone() for n, p in bb.named_parameters() if p.grad is not None})
+        finally:
+            ops.FP16_DELAYED_SCALE = True
+    blk = bb.transformer.resblocks[3]
+    assert blk.__dict__["_dclip_dscale"].primed == [True, True]
+    for n in grads[0]:
+        assert rel_err(grads[1][n], grads[2][n]) < 1e-5, n  # delayed == exact on identical data
+        assert rel_err(grads[0][n], grads[2][n]) < 1e-5, n
+
+
 @pytest.mark.parametrize("M,N,K", [(200, 256, 128), (4100, 768, 768), (16392, 3072, 768)])
 def test_scaled_ops_equal_host_alpha(M, N, K):
     """gemm / weight_grad / cast / tokens_bwd with the device scale == the host-float path (the
