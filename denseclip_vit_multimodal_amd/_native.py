@@ -75,7 +75,7 @@ _SIGS = {
     "dclip_bn_fwd": [_i32, _c_void_p, _i64, _i32, _i64, _c_void_p, _c_void_p, _f32, _f32, _c_void_p, _c_void_p,
                      _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p],
     "dclip_bn_bwd": [_i32, _c_void_p, _c_void_p, _i64, _i32, _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
-                     _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p],
+                     _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p],
     "dclip_conv3x3": [_i32, _i32, _c_void_p, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _c_void_p, _i32, _c_void_p,
                       _i32, _i64, _i32, _i32, _i32, _c_void_p],
     "dclip_upsample_ce": [_i32, _c_void_p, _i32, _i32, _i32, _i32, _c_void_p, _i32, _i32, _i32, _i32, _c_void_p,
@@ -83,7 +83,7 @@ _SIGS = {
     "dclip_upsample_silog": [_i32, _i32, _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p, _i32, _i32, _f32, _f32,
                              _c_void_p, _c_void_p, _c_void_p],
     "dclip_conv3x3_wgrad": [_i32, _c_void_p, _i64, _i32, _c_void_p, _i64, _i64, _i64, _i32, _i32, _i32, _i32,
-                            _c_void_p, _c_void_p, _i32, _c_void_p],
+                            _c_void_p, _c_void_p, _i32, _i32, _c_void_p, _c_void_p],
     "dclip_set_option": [_i32, _i32],
     "dclip_cityscapes_prepare": [_c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p, _i32, _i32,
                                  _c_void_p, _c_void_p, _f32, _f32, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p,

@@ -179,7 +179,7 @@ def _register_fakes():
                 _e(C, like=x, dtype=f32))
 
     @reg("dclip::bn_bwd")
-    def _(dy, x, w, b, mean, rstd, relu, want_w, want_b):
+    def _(dy, x, w, b, mean, rstd, relu, want_w, want_b, scale=None):
         C = x.shape[1]
         return (torch.empty_like(x, memory_format=torch.channels_last), _e(C if want_w else 0, like=x, dtype=f32),
                 _e(C if want_b else 0, like=x, dtype=f32))
@@ -189,7 +189,7 @@ def _register_fakes():
         return _e(x.shape[1], like=x, dtype=f32), _e(x.shape[1], like=x, dtype=f32)
 
     @reg("dclip::bn_bwd_rows")
-    def _(dy, x, w, b, mean, rstd, relu, want_w, want_b, dx):
+    def _(dy, x, w, b, mean, rstd, relu, want_w, want_b, dx, scale=None):
         C = x.shape[1]
         return _e(C if want_w else 0, like=x, dtype=f32), _e(C if want_b else 0, like=x, dtype=f32)
 
@@ -198,8 +198,8 @@ def _register_fakes():
         return None
 
     @reg("dclip::conv3x3_wgrad")
-    def _(dY, ldy, Nout, X, x_bstride, x_off, x_ld, B, H, W, Cin, splits):
-        return _e(Nout, 9 * Cin, like=X, dtype=f32)
+    def _(dY, ldy, Nout, X, x_bstride, x_off, x_ld, B, H, W, Cin, splits, oihw=False, scale=None):
+        return _e(Nout, Cin, 3, 3, like=X, dtype=f32) if oihw else _e(Nout, 9 * Cin, like=X, dtype=f32)
 
     @reg("dclip::upsample_ce")
     def _(logits, labels, ignore_index):

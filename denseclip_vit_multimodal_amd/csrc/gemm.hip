@@ -1532,6 +1532,27 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, i
     }
 }
 
+// the conv weight gradient's split-K slabs ([co][tap][ci], K = 9 Cin) summed in a fixed order
+// and written in torch's (Cout, Cin, 3, 3) layout, times alpha (the 1/s of an fp16 gradient
+// scale): one thread per (co, ci), 9 taps each — no permute copy and no separate unscale
+__global__ void conv_wgrad_reduce_oihw_kernel(const float* __restrict__ ws, int splits, int64_t slab, int M, int Cin,
+                                              Alpha alpha, float* __restrict__ out) {
+    const int64_t total = (int64_t)M * Cin;
+    const float a = alpha.get();
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int co = (int)(i / Cin), ci = (int)(i % Cin);
+        const float* src = ws + (int64_t)co * 9 * Cin + ci;
+        float v[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) v[t] = src[(int64_t)t * Cin];
+        for (int z = 1; z < splits; ++z)
+#pragma unroll
+            for (int t = 0; t < 9; ++t) v[t] += src[z * slab + (int64_t)t * Cin];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) out[i * 9 + t] = v[t] * a;
+    }
+}
+
 // ---------------------------------------------------------------------------- 3x3 convolution
 // Implicit-GEMM 3x3 / stride 1 / pad 1 convolution on channels-last pixel rows — the
 // ViTFeatureFusionNeck's per-level ConvBNReLU convs (reference models.py:741-745, 13-20) run
@@ -2328,7 +2349,7 @@ extern "C" int dclip_conv3x3(int mode, int ab_dt, const void* X, int64_t x_bstri
 
 extern "C" int dclip_conv3x3_wgrad(int ab_dt, const void* dY, int64_t ldy, int Nout, const void* X, int64_t x_bstride,
                                    int64_t x_off, int64_t x_ld, int B, int H, int W, int Cin, float* dW, void* ws,
-                                   int splits, void* stream) {
+                                   int splits, int oihw, const float* alpha_ptr, void* stream) {
     DCLIP_HOST_CHECK(ab_dt == DCLIP_BF16 || ab_dt == DCLIP_F16, "dclip_conv3x3_wgrad: operands must be f16/bf16");
     DCLIP_HOST_CHECK(Cin % 128 == 0 && Nout % 8 == 0 && Nout > 0 && ldy % 8 == 0 && ldy >= Nout,
                      "dclip_conv3x3_wgrad: Cin %% 128 == 0 and Nout %% 8 == 0 required");
@@ -2352,6 +2373,17 @@ extern "C" int dclip_conv3x3_wgrad(int ab_dt, const void* dY, int64_t ldy, int N
         conv_wgrad_kernel<f16><<<grid, 256, 0, st>>>((const f16*)dY, ldy, (const f16*)X, (const f16*)zero, g, Cin,
                                                      Nout, N, Kpix, kp, tiles_m, tiles_n, (float*)ws,
                                                      (int64_t)Nout * N);
+    if (oihw || alpha_ptr != nullptr) {
+        const int64_t total = (int64_t)Nout * Cin;
+        const int blocks = (int)((total + 255) / 256 > 4096 ? 4096 : (total + 255) / 256);
+        if (oihw) {
+            conv_wgrad_reduce_oihw_kernel<<<blocks, 256, 0, st>>>((const float*)ws, splits, (int64_t)Nout * N, Nout, Cin,
+                                                                  Alpha(1.f, alpha_ptr), dW);
+            DCLIP_LAUNCH_CHECK();
+            return 0;
+        }
+        DCLIP_HOST_CHECK(false, "dclip_conv3x3_wgrad: alpha_ptr needs the OIHW output");
+    }
     const int64_t total4 = (int64_t)Nout * (N / 4);
     int blocks = (int)((total4 + 255) / 256);
     blocks = blocks > 4096 ? 4096 : blocks;

@@ -1092,14 +1092,16 @@ __global__ void bn_fwd_finalize_kernel(const float* __restrict__ part, int nblk,
 __global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int64_t rows, int C,
                                        const float* __restrict__ w, const float* __restrict__ mean,
                                        const float* __restrict__ rstd, float* __restrict__ dw, float* __restrict__ db,
-                                       float* __restrict__ k) {
+                                       float* __restrict__ k, const float* __restrict__ gscale) {
     int c;
     float S, Q;
     bn_reduce_parts(part, nblk, C, c, S, Q);
     if (threadIdx.x >= 8 || c >= C) return;
     const float n = (float)rows, rs = rstd[c], wc = w ? w[c] : 1.f;
-    if (dw) dw[c] = Q * rs;
-    if (db) db[c] = S;
+    // the parameter gradients unscaled by 1/s of the fp16 heads' gradient scale (dx keeps s)
+    const float ga = gscale ? *gscale : 1.f;
+    if (dw) dw[c] = Q * rs * ga;
+    if (db) db[c] = S * ga;
     const float k1 = wc * rs;
     const float k2 = -wc * rs * rs * rs * (Q / n);
     k[c] = k1;
@@ -1231,7 +1233,7 @@ extern "C" int dclip_bn_eval(int dt, const void* x, int64_t rows, int C, int64_t
 
 extern "C" int dclip_bn_bwd(int dt, const void* dy, const void* x, int64_t rows, int C, int64_t ld, const float* w,
                             const float* b, const float* mean, const float* rstd, float* ws, void* dx, float* dw,
-                            float* db, int relu, void* stream) {
+                            float* db, int relu, const float* gscale, void* stream) {
     DCLIP_HOST_CHECK(dt == DCLIP_BF16 || dt == DCLIP_F16, "dclip_bn_bwd: dtype must be bf16/f16");
     DCLIP_HOST_CHECK(bn_shape_ok(rows, C, ld), "dclip_bn_bwd: need rows > 0, C %% 8 == 0, C <= 2048, ld >= C, "
                      "ld %% 8 == 0 (C = %d)", C);
@@ -1245,12 +1247,12 @@ extern "C" int dclip_bn_bwd(int dt, const void* dy, const void* x, int64_t rows,
 #define BN_BWD(T)                                                                                                      \
     if (relu) {                                                                                                        \
         bn_stats_kernel<T, 1, true><<<nblk, 256, 0, st>>>((const T*)dy, (const T*)x, w, b, mean, rstd, rows, C, ld, ws); \
-        bn_bwd_finalize_kernel<<<(C + 7) / 8, 256, 0, st>>>(ws, nblk, rows, C, w, mean, rstd, dw, db, k);               \
+        bn_bwd_finalize_kernel<<<(C + 7) / 8, 256, 0, st>>>(ws, nblk, rows, C, w, mean, rstd, dw, db, k, gscale);               \
         bn_apply_kernel<T, true, true><<<ga, 256, 0, st>>>((const T*)dy, (const T*)x, k, rows, C, ld, (T*)dx);          \
     } else {                                                                                                           \
         bn_stats_kernel<T, 1, false><<<nblk, 256, 0, st>>>((const T*)dy, (const T*)x, w, b, mean, rstd, rows, C, ld,   \
                                                            ws);                                                        \
-        bn_bwd_finalize_kernel<<<(C + 7) / 8, 256, 0, st>>>(ws, nblk, rows, C, w, mean, rstd, dw, db, k);               \
+        bn_bwd_finalize_kernel<<<(C + 7) / 8, 256, 0, st>>>(ws, nblk, rows, C, w, mean, rstd, dw, db, k, gscale);               \
         bn_apply_kernel<T, true, false><<<ga, 256, 0, st>>>((const T*)dy, (const T*)x, k, rows, C, ld, (T*)dx);         \
     }
     if (dt == DCLIP_BF16) {

@@ -606,7 +606,8 @@ std::tuple<Tensor, Tensor> bn_fwd_rows(const Tensor& x, const c10::optional<Tens
 
 std::tuple<Tensor, Tensor> bn_bwd_into(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& w,
                                        const c10::optional<Tensor>& b, const Tensor& mean, const Tensor& rstd, bool relu,
-                                       bool want_w, bool want_b, const Tensor& dx) {
+                                       bool want_w, bool want_b, const Tensor& dx,
+                                       const c10::optional<Tensor>& scale = c10::nullopt) {
     const Rows r = rows_of(x), rd = rows_of(dy), rdx = rows_of(dx);
     TORCH_CHECK(rd.rows == r.rows && rd.C == r.C && rd.ld == r.ld && rdx.ld == r.ld && rdx.rows == r.rows,
                 "dclip: BatchNorm backward tensors must share rows, channels and pitch");
@@ -620,23 +621,23 @@ std::tuple<Tensor, Tensor> bn_bwd_into(const Tensor& dy, const Tensor& x, const 
     DCLIP_CALL(dclip_bn_bwd(dt_code(x.scalar_type()), dy.data_ptr(), x.data_ptr(), r.rows, (int)r.C, r.ld, optr<float>(w),
                             optr<float>(b), ptr<float>(mean), ptr<float>(rstd), ptr<float>(ws), dx.data_ptr(),
                             want_w ? ptr<float>(dw) : nullptr, want_b ? ptr<float>(db) : nullptr, relu ? 1 : 0,
-                            stream_of(x)));
+                            scale_entry(scale, 1), stream_of(x)));
     return {dw, db};
 }
 
 std::tuple<Tensor, Tensor, Tensor> bn_bwd(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& w,
                                           const c10::optional<Tensor>& b, const Tensor& mean, const Tensor& rstd,
-                                          bool relu, bool want_w, bool want_b) {
+                                          bool relu, bool want_w, bool want_b, const c10::optional<Tensor>& scale) {
     TORCH_CHECK(x.dim() == 4, "bn_bwd: a channels-last 4-D map");
     Tensor dx = at::empty_like(x, at::MemoryFormat::ChannelsLast);
-    auto g = bn_bwd_into(dy, x, w, b, mean, rstd, relu, want_w, want_b, dx);
+    auto g = bn_bwd_into(dy, x, w, b, mean, rstd, relu, want_w, want_b, dx, scale);
     return {dx, std::get<0>(g), std::get<1>(g)};
 }
 
 std::tuple<Tensor, Tensor> bn_bwd_rows(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& w,
                                        const c10::optional<Tensor>& b, const Tensor& mean, const Tensor& rstd, bool relu,
-                                       bool want_w, bool want_b, Tensor& dx) {
-    return bn_bwd_into(dy, x, w, b, mean, rstd, relu, want_w, want_b, dx);
+                                       bool want_w, bool want_b, Tensor& dx, const c10::optional<Tensor>& scale) {
+    return bn_bwd_into(dy, x, w, b, mean, rstd, relu, want_w, want_b, dx, scale);
 }
 
 // ----------------------------------------------------------------------------- neck 3x3 conv
@@ -654,14 +655,16 @@ void conv3x3(int64_t mode, const Tensor& X, int64_t x_bstride, int64_t x_off, in
 }
 
 Tensor conv3x3_wgrad(const Tensor& dY, int64_t ldy, int64_t Nout, const Tensor& X, int64_t x_bstride, int64_t x_off,
-                     int64_t x_ld, int64_t B, int64_t H, int64_t W, int64_t Cin, int64_t splits) {
+                     int64_t x_ld, int64_t B, int64_t H, int64_t W, int64_t Cin, int64_t splits, bool oihw,
+                     const c10::optional<Tensor>& scale) {
     check_gpu(dY, "dY", false); check_gpu(X, "X", false);
+    TORCH_CHECK(oihw || !(scale.has_value() && scale->defined()), "conv3x3_wgrad: a scale needs the OIHW output");
     c10::DeviceGuard g(X.device());
-    Tensor dW = at::empty({Nout, 9 * Cin}, like(X, at::kFloat));
+    Tensor dW = oihw ? at::empty({Nout, Cin, 3, 3}, like(X, at::kFloat)) : at::empty({Nout, 9 * Cin}, like(X, at::kFloat));
     Tensor ws = at::empty({splits * Nout * 9 * Cin}, like(X, at::kFloat));
     DCLIP_CALL(dclip_conv3x3_wgrad(dt_code(dY.scalar_type()), dY.data_ptr(), ldy, (int)Nout, X.data_ptr(), x_bstride,
                                    x_off, x_ld, (int)B, (int)H, (int)W, (int)Cin, ptr<float>(dW), ws.data_ptr(),
-                                   (int)splits, stream_of(X)));
+                                   (int)splits, oihw ? 1 : 0, scale_entry(scale, 1), stream_of(X)));
     return dW;
 }
 
@@ -809,15 +812,15 @@ TORCH_LIBRARY(dclip, m) {
     m.def("bn_fwd(Tensor x, Tensor? w, Tensor? b, Tensor(a!)? running_mean, Tensor(b!)? running_var, float momentum, "
           "float eps, bool relu) -> (Tensor, Tensor, Tensor)");
     m.def("bn_bwd(Tensor dy, Tensor x, Tensor? w, Tensor? b, Tensor mean, Tensor rstd, bool relu, bool want_w, "
-          "bool want_b) -> (Tensor, Tensor, Tensor)");
+          "bool want_b, Tensor? scale=None) -> (Tensor, Tensor, Tensor)");
     m.def("bn_fwd_rows(Tensor x, Tensor? w, Tensor? b, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
           "float momentum, float eps, bool relu, Tensor(c!) y) -> (Tensor, Tensor)");
     m.def("bn_bwd_rows(Tensor dy, Tensor x, Tensor? w, Tensor? b, Tensor mean, Tensor rstd, bool relu, bool want_w, "
-          "bool want_b, Tensor(a!) dx) -> (Tensor, Tensor)");
+          "bool want_b, Tensor(a!) dx, Tensor? scale=None) -> (Tensor, Tensor)");
     m.def("conv3x3(int mode, Tensor X, int x_bstride, int x_off, int x_ld, int B, int H, int W, int Cin, Tensor Wt, "
           "int Nout, Tensor(a!) out, int out_ld, int out_gap, int out_off, int accumulate) -> ()");
     m.def("conv3x3_wgrad(Tensor dY, int ldy, int Nout, Tensor X, int x_bstride, int x_off, int x_ld, int B, int H, "
-          "int W, int Cin, int splits) -> Tensor");
+          "int W, int Cin, int splits, bool oihw=False, Tensor? scale=None) -> Tensor");
     m.def("upsample_ce(Tensor logits, Tensor labels, int ignore_index) -> (Tensor, Tensor, Tensor)");
     m.def("upsample_silog_sums(Tensor pred, Tensor target, Tensor? mask, float eps) -> Tensor");
     m.def("upsample_silog_grad(Tensor pred, Tensor target, Tensor? mask, Tensor sums, float eps, float lambd) -> Tensor");

@@ -771,10 +771,9 @@ class BatchNormFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, w, b, mean, rstd = ctx.saved_tensors
         dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last)
-        dx, dw, db = D().bn_bwd(dy, x, w, b, mean, rstd, ctx.relu, ctx.has_w[0], ctx.has_w[1])
-        dw = _unscale_(dw, ctx.hsb) if ctx.has_w[0] else None
-        db = _unscale_(db, ctx.hsb) if ctx.has_w[1] else None
-        return dx, dw, db, None, None, None, None, None
+        # dw / db unscaled by the heads' 1/s inside the kernel (dx keeps the scale)
+        dx, dw, db = D().bn_bwd(dy, x, w, b, mean, rstd, ctx.relu, ctx.has_w[0], ctx.has_w[1], ctx.hsb)
+        return dx, (dw if ctx.has_w[0] else None), (db if ctx.has_w[1] else None), None, None, None, None, None
 
 
 def bn_train(bn, x, relu=False):
@@ -1043,11 +1042,7 @@ class Conv3x3Fn(torch.autograd.Function):
         Cout = weight.shape[0]
         cp = _pad64(Cout)
 
-        def rows(w):  # (Cout, Cin, 3, 3) -> (cp, 9*Cin), (ky, kx, ci) order, zero rows past Cout
-            r = w.permute(0, 2, 3, 1).reshape(Cout, 9 * Cin)
-            return torch.cat([r, r.new_zeros(cp - Cout, 9 * Cin)]) if cp > Cout else r
-
-        w_rows = WEIGHTS.get_with(weight, cdt, "conv3x3_rows", rows)
+        w_rows = _conv3x3_rows(weight, cdt)
         out, (xr, bs, ld) = conv3x3_fwd(xmap, w_rows, cp, cdt)
         ctx.save_for_backward(xr, weight)
         ctx.geo = (B, Cin, H, W, Cout, cp, bs, ld, xmap.dtype, tuple(xmap.stride()), xmap.storage_offset() -
@@ -1068,13 +1063,7 @@ class Conv3x3Fn(torch.autograd.Function):
         dyr[:, :Cout] = dy.permute(0, 2, 3, 1).reshape(M, Cout)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            def trows(w):  # (Cout, Cin, 3, 3) -> (Cin, 9*cp): [ci][tap][co], zero columns past Cout
-                t = w.permute(1, 2, 3, 0)  # ci, ky, kx, co
-                if cp > Cout:
-                    t = torch.cat([t, t.new_zeros(Cin, 3, 3, cp - Cout)], dim=3)
-                return t.reshape(Cin, 9 * cp)
-
-            w_t = WEIGHTS.get_with(weight, cdt, "conv3x3_dgrad", trows)
+            w_t = _conv3x3_dgrad_rows(weight, cdt)
             if in_place and in_strides[0] == bs:
                 # same layout as the input view: batches of bs elements, pixel rows after a gap
                 gap_rows = (bs - H * W * ld) // ld
@@ -1093,28 +1082,39 @@ class Conv3x3Fn(torch.autograd.Function):
             tiles = (cp + 127) // 128 * (9 * Cin // 128)
             splits = max(1, min(32, 512 // max(1, tiles), M // 4096 or 1))
             e0 = _tic()
-            dwr = D().conv3x3_wgrad(dyr, cp, cp, xr, bs, 0, ld, B, H, W, Cin, splits)
+            # torch's (Cout, Cin, 3, 3) layout and the heads' 1/s straight out of the split-K sum
+            dw = D().conv3x3_wgrad(dyr, cp, cp, xr, bs, 0, ld, B, H, W, Cin, splits, True, ctx.hsb)
             _toc("conv_wgrad", e0)
-            dw = _unscale_(dwr[:Cout].view(Cout, 3, 3, Cin).permute(0, 3, 1, 2).contiguous().to(weight.dtype),
-                           ctx.hsb)
+            dw = dw[:Cout]
+            if dw.dtype != weight.dtype:
+                dw = dw.to(weight.dtype)
         return dx, dw, None
 
 
 def _conv3x3_rows(weight, cdt):
-    """(Cout, Cin, 3, 3) -> cached (cp, 9*Cin) rows in (ky, kx, ci) order, zero rows past Cout."""
+    """(Cout, Cin, 3, 3) -> cached (cp, 9*Cin) rows in (ky, kx, ci) order, zero rows past Cout.
+    Cout % 64 == 0 (every conv of the Cityscapes configs): one batched transpose launch
+    (per output channel, (Cin, 9) -> (9, Cin), cast on the fly) instead of a permute copy and a
+    cast copy."""
     Cout, Cin = weight.shape[:2]
     cp = _pad64(Cout)
 
     def rows(w):
+        if cp == Cout and w.is_cuda:
+            return D().transpose_batched(w.contiguous(), Cout, Cin, 9, 9, Cin, cdt).view(Cout, 9 * Cin)
         r = w.permute(0, 2, 3, 1).reshape(Cout, 9 * Cin)
         return torch.cat([r, r.new_zeros(cp - Cout, 9 * Cin)]) if cp > Cout else r
     return WEIGHTS.get_with(weight, cdt, "conv3x3_rows", rows)
 
 
 def _conv3x3_dgrad_rows(weight, cdt):
-    """(Cout, Cin, 3, 3) -> cached (Cin, 9*cp): [ci][tap][co], zero columns past Cout."""
+    """(Cout, Cin, 3, 3) -> cached (Cin, 9*cp): [ci][tap][co], zero columns past Cout.  For
+    Cout % 64 == 0 this is the plain transposed weight copy ((Cout, 9 Cin) -> (9 Cin, Cout), the
+    16-byte transpose kernel) viewed as (Cin, 9 Cout)."""
     Cout, Cin = weight.shape[:2]
     cp = _pad64(Cout)
+    if cp == Cout and weight.is_cuda:
+        return WEIGHTS.get(weight, cdt, transposed=True).view(Cin, 9 * cp)
 
     def trows(w):
         t = w.permute(1, 2, 3, 0)
@@ -1189,9 +1189,7 @@ class NeckLevelsFn(torch.autograd.Function):
         for l in range(L):
             sl = slice(l * Ci, (l + 1) * Ci)
             dbnw[l], dbnb[l] = D().bn_bwd_rows(d[:, sl], pre[:, sl], bnw[l].detach(), bnb[l].detach(), stats[2 * l],
-                                               stats[2 * l + 1], True, True, True, dpre[:, sl])
-            _unscale_(dbnw[l], ctx.hsb)
-            _unscale_(dbnb[l], ctx.hsb)
+                                               stats[2 * l + 1], True, True, True, dpre[:, sl], ctx.hsb)
             bs, ld = bsld[l]
             if need[1 + l]:  # input gradient: the dgrad conv, in the input's own layout when it is a token view
                 w_t = _conv3x3_dgrad_rows(convw[l], cdt)
@@ -1208,10 +1206,9 @@ class NeckLevelsFn(torch.autograd.Function):
                 dmaps[l] = dm if in_dts[l] == cdt else dm.to(in_dts[l])
             if need[1 + L + l]:
                 e0 = _tic()
-                dwr = D().conv3x3_wgrad(dpre[:, l * Ci:], LC, Ci, xrs[l], bs, 0, ld, B, H, W, Cin, splits)
+                dwc = D().conv3x3_wgrad(dpre[:, l * Ci:], LC, Ci, xrs[l], bs, 0, ld, B, H, W, Cin, splits, True, ctx.hsb)
                 _toc("conv_wgrad", e0)
-                dconv[l] = _unscale_(dwr[:Ci].view(Ci, 3, 3, Cin).permute(0, 3, 1, 2).contiguous().to(convw[l].dtype),
-                                     ctx.hsb)
+                dconv[l] = dwc if dwc.dtype == convw[l].dtype else dwc.to(convw[l].dtype)
         return (None, *dmaps, *dconv, *dbnw, *dbnb)
 
 

@@ -250,10 +250,12 @@ int dclip_conv3x3(int mode, int ab_dt, const void* X, int64_t x_bstride, int64_t
 
 /* Weight gradient of the 3x3 conv: dW[co][tap*Cin + c] = sum_p dY[p][co] * X[p + d(tap)][c]
  * (f32, Nout x 9*Cin), pixels split into `splits` chunks summed through ws
- * (splits * Nout * 9*Cin f32) in a fixed order.  Cin % 128 == 0.                       */
+ * (splits * Nout * 9*Cin f32) in a fixed order.  Cin % 128 == 0.  oihw = 1 writes torch's
+ * weight layout instead, dW[co][c][tap] (Nout, Cin, 3, 3), times *alpha_ptr when given (the 1/s
+ * entry of an fp16 gradient-scale pair; alpha_ptr needs oihw = 1).                       */
 int dclip_conv3x3_wgrad(int ab_dt, const void* dY, int64_t ldy, int Nout, const void* X, int64_t x_bstride,
                         int64_t x_off, int64_t x_ld, int B, int H, int W, int Cin, float* dW, void* ws,
-                        int splits, void* stream);
+                        int splits, int oihw, const float* alpha_ptr, void* stream);
 
 /* Fused bilinear upsample (align_corners=False) + loss + gradient of the heads
  * (denseclip.py:843-868 resize, train_denseclip.py:1265-1314 losses), without materialising
@@ -392,9 +394,11 @@ int64_t dclip_bn_workspace(int64_t rows, int C);
 int dclip_bn_fwd(int dt, const void* x, int64_t rows, int C, int64_t ld, const float* w, const float* b,
                  float eps, float momentum, float* running_mean, float* running_var, float* ws, float* mean,
                  float* rstd, void* y, int relu, void* stream);
+/* gscale (nullable): dw and db are multiplied by *gscale (the 1/s entry of the fp16 heads'
+ * gradient-scale pair; dx keeps the scale of dy).                                         */
 int dclip_bn_bwd(int dt, const void* dy, const void* x, int64_t rows, int C, int64_t ld, const float* w,
                  const float* b, const float* mean, const float* rstd, float* ws, void* dx, float* dw,
-                 float* db, int relu, void* stream);
+                 float* db, int relu, const float* gscale, void* stream);
 
 #ifdef __cplusplus
 }
