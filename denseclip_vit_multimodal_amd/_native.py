@@ -68,9 +68,10 @@ _SIGS = {
     "dclip_add_readout_cast": [_c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _i32, _i64, _i32, _i32, _f32,
                                _c_void_p],
     "dclip_add_readout_cast_scaled": [_c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _i64, _i32, _i32,
-                                      _f32, _c_void_p, _c_void_p, _c_void_p],
+                                      _f32, _c_void_p, _i32, _c_void_p, _c_void_p],
     "dclip_layernorm_bwd_scaled": [_c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
-                                   _c_void_p, _c_void_p, _c_void_p, _i64, _i64, _f32, _c_void_p, _c_void_p, _c_void_p],
+                                   _c_void_p, _c_void_p, _c_void_p, _i64, _i64, _f32, _c_void_p, _i32, _c_void_p,
+                                   _c_void_p],
     "dclip_bn_workspace": [_i64, _i32],
     "dclip_bn_fwd": [_i32, _c_void_p, _i64, _i32, _i64, _c_void_p, _c_void_p, _f32, _f32, _c_void_p, _c_void_p,
                      _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p],

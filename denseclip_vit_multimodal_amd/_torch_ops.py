@@ -115,11 +115,11 @@ def _register_fakes():
         return _e(*a.shape, like=a), _e(4, like=a)
 
     @reg("dclip::add_readout_cast_scaled")
-    def _(a, b, ntok, b_scale, st, target):
+    def _(a, b, ntok, b_scale, st, use, target):
         return (_e(*a.shape, like=a) if b is not None else _e(0, like=a)), _e(*a.shape, like=a, dtype=torch.float16), _e(4, like=a)
 
     @reg("dclip::layernorm_bwd_scaled")
-    def _(dy, x, w, mean, rstd, res, dw, db, st, target):
+    def _(dy, x, w, mean, rstd, res, dw, db, st, use, target):
         return _e(*x.shape, like=x, dtype=f32), _e(*x.shape, like=x, dtype=torch.float16), _e(4, like=x)
 
     @reg("dclip::attn_fwd")

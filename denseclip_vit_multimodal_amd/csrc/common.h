@@ -157,10 +157,8 @@ struct Alpha {
 // maximum m (|x| as uint32 bits: they order like the floats, NaN / inf above every finite value);
 // the last workgroup to arrive writes st[0] = s = 2^clamp(floor(log2(target / amax)), -60, 60),
 // st[1] = 1/s (s = 1 for an all-zero or non-finite maximum) and clears st[2], st[3] for the next
-// use.  (dclip_grad_scale; the delayed-scale casts write the scale of the NEXT use into st, and
-// KEEP the current one when the maximum is not finite: an inf that arrived from an overflow
-// upstream says nothing about this site's own range.)
-template <int NW, bool KEEP_ON_NONFINITE = false>
+// use.  (dclip_grad_scale, dclip_add_readout_amax.)
+template <int NW>
 __device__ __forceinline__ void scale_finish(uint32_t m, float target, float* __restrict__ st) {
     for (int o = 32; o >= 1; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
     __shared__ uint32_t red[NW];
@@ -186,12 +184,57 @@ __device__ __forceinline__ void scale_finish(uint32_t m, float target, float* __
             const double l = floor(log2((double)target / (double)__uint_as_float(bits)));
             e = (int)fmin(60.0, fmax(-60.0, l));
         }
-        if (!KEEP_ON_NONFINITE || bits < 0x7f800000u) {
-            st[0] = ldexpf(1.f, e);
-            st[1] = ldexpf(1.f, -e);
-        }
+        st[0] = ldexpf(1.f, e);
+        st[1] = ldexpf(1.f, -e);
         atomicExch(stu + 2, 0u);
         atomicExch(stu + 3, 0u);
+    }
+}
+
+// Delayed power-of-two fp16 gradient scale of one gradient site (dclip.h, the *_scaled casts),
+// without fences or an arrival counter: st = [3][DS_SHARDS] |x|-maximum shards (uint32 bits of
+// positive floats) + [3] used scales.  Use k casts with the scale of use k-1's maximum (shards
+// (k+2) % 3), joins its own maximum into shards k % 3 (one no-return atomic per workgroup, spread
+// over the shards) and clears shards (k+1) % 3 for use k+1 (nobody reads them during use k).
+// A previous maximum that is 0 or not finite (an inf from an overflow upstream) keeps the scale
+// that use k-1 itself used.
+constexpr int DS_SHARDS = 64;
+constexpr int DS_STATE_FLOATS = 3 * DS_SHARDS + 4;
+static_assert(DS_STATE_FLOATS == DCLIP_DS_STATE_FLOATS, "dclip.h state size");
+
+// the scale of use k, computed by every calling wave (one load per lane, L2-resident)
+__device__ __forceinline__ float ds_scale_of_use(const float* __restrict__ st, int use, float target) {
+    const uint32_t* sh = (const uint32_t*)st + ((use + 2) % 3) * DS_SHARDS;
+    uint32_t m = sh[threadIdx.x & 63];
+    for (int o = 32; o >= 1; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+    if (m == 0 || m >= 0x7f800000u) return st[3 * DS_SHARDS + (use + 2) % 3];
+    const double l = floor(log2((double)target / (double)__uint_as_float(m)));
+    return ldexpf(1.f, (int)fmin(60.0, fmax(-60.0, l)));
+}
+
+// workgroup 0: publish (s, 1/s) for the consumers, record s as use k's scale, clear shards k+1
+__device__ __forceinline__ void ds_begin(float* __restrict__ st, int use, float s, float* __restrict__ spair) {
+    if (blockIdx.x != 0 || threadIdx.x >= 64) return;
+    ((uint32_t*)st)[((use + 1) % 3) * DS_SHARDS + threadIdx.x] = 0u;
+    if (threadIdx.x == 0) {
+        spair[0] = s;
+        spair[1] = 1.f / s;
+        st[3 * DS_SHARDS + use % 3] = s;
+    }
+}
+
+// the workgroup's (NW waves) |x| maximum m joined into use k's shards
+template <int NW>
+__device__ __forceinline__ void ds_end(uint32_t m, float* __restrict__ st, int use) {
+    for (int o = 32; o >= 1; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+    __shared__ uint32_t red[NW];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        m = red[0];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) m = max(m, red[w]);
+        if (m != 0) atomicMax((uint32_t*)st + (use % 3) * DS_SHARDS + blockIdx.x % DS_SHARDS, m);
     }
 }
 

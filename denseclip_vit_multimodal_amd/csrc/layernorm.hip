@@ -234,16 +234,16 @@ __global__ __launch_bounds__(256) void ln_fwd_fast(const TX* __restrict__ x, con
 // in LDS and added with ONE atomic per column per block — every block adds into the same
 // 2 * cols floats, so the atomic count (not the bytes) sets that tail's cost
 //
-// DS (delayed scale, fp16 lp): lp = (f16)(dx * s) with s = st[0] — the power-of-two scale this
-// gradient's previous use derived from ITS maximum — (s, 1/s) copied to spair for the consumers
-// of lp, and the |dx| maximum of this use turned into st's scale for the next (scale_finish).
+// DS (delayed scale, fp16 lp): lp = (f16)(dx * s), s the power-of-two scale of this gradient
+// site's previous use (common.h ds_*: use `use` of the state st), (s, 1/s) to spair for the
+// consumers of lp, and this use's |dx| maximum joined into st for the next.
 template <typename TDY, typename TX, int NV, bool DS = false>
 __global__ __launch_bounds__(512) void ln_bwd_fast(const TDY* __restrict__ dy, const TX* __restrict__ x,
                                                    const float* __restrict__ w, const float* __restrict__ mean,
                                                    const float* __restrict__ rstd, const float* res, float* dx,
                                                    void* __restrict__ lp, int lp_dt, float* __restrict__ dw,
                                                    float* __restrict__ db, int64_t rows, float* st = nullptr,
-                                                   float* spair = nullptr, float target = 0.f) {
+                                                   int use = 0, float* spair = nullptr, float target = 0.f) {
     constexpr int cols = 256 * NV;
     __shared__ float red[8][2][4 * NV][64];
     const int lane = threadIdx.x & 63;
@@ -251,11 +251,8 @@ __global__ __launch_bounds__(512) void ln_bwd_fast(const TDY* __restrict__ dy, c
     float ls = 1.f;
     uint32_t amax = 0;
     if constexpr (DS) {
-        ls = st[0];
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
-            spair[0] = ls;
-            spair[1] = st[1];
-        }
+        ls = ds_scale_of_use(st, use, target);
+        ds_begin(st, use, ls, spair);
     }
     const int64_t stride = (int64_t)gridDim.x * 8;
     float aw[4 * NV], ab[4 * NV], wl[4 * NV];
@@ -351,7 +348,7 @@ __global__ __launch_bounds__(512) void ln_bwd_fast(const TDY* __restrict__ dy, c
         float* out = which ? db : dw;
         if (out) atomicAdd(out + c, sum);
     }
-    if constexpr (DS) scale_finish<8, true>(amax, target, st);
+    if constexpr (DS) ds_end<8>(amax, st, use);
 }
 
 // blocks of 4 waves: enough persistent waves to fill the chip (8 per SIMD), fewer for small inputs
@@ -424,30 +421,30 @@ void bwd_dispatch_x(int x_dt, const void* dy, const void* x, const float* w, con
 
 template <typename TX, int NV>
 void bwd_fast_ds(const float* dy, const void* x, const float* w, const float* mean, const float* rstd,
-                 const float* res, float* dx, void* lp, float* dw, float* db, int64_t rows, float* st, float* spair,
-                 float target, hipStream_t s) {
+                 const float* res, float* dx, void* lp, float* dw, float* db, int64_t rows, float* st, int use,
+                 float* spair, float target, hipStream_t s) {
     int64_t blocks = (rows + 7) / 8;
     blocks = blocks > 512 ? 512 : blocks;
     ln_bwd_fast<float, TX, NV, true><<<(unsigned)blocks, 512, 0, s>>>(dy, (const TX*)x, w, mean, rstd, res, dx, lp,
-                                                                    DCLIP_F16, dw, db, rows, st, spair, target);
+                                                                    DCLIP_F16, dw, db, rows, st, use, spair, target);
 }
 
 }  // namespace
 
 extern "C" int dclip_layernorm_bwd_scaled(const float* dy, const void* x, int x_dt, const float* w, const float* mean,
                                           const float* rstd, const float* res, float* dx, void* lp, float* dw,
-                                          float* db, int64_t rows, int64_t cols, float target, float* st, float* spair,
-                                          void* stream) {
+                                          float* db, int64_t rows, int64_t cols, float target, float* st, int use,
+                                          float* spair, void* stream) {
     DCLIP_HOST_CHECK(cols == 512 || cols == 768 || cols == 1024,
                      "dclip_layernorm_bwd_scaled: cols must be 512, 768 or 1024 (got %lld)", (long long)cols);
     DCLIP_HOST_CHECK(x_dt == DCLIP_F32, "dclip_layernorm_bwd_scaled: x must be f32 (the residual stream)");
-    DCLIP_HOST_CHECK(lp != nullptr && st != nullptr && spair != nullptr && target > 0.f,
-                     "dclip_layernorm_bwd_scaled: lp, the scale state, the scale pair and target > 0 are required");
+    DCLIP_HOST_CHECK(lp != nullptr && st != nullptr && spair != nullptr && target > 0.f && use >= 1,
+                     "dclip_layernorm_bwd_scaled: lp, the scale state, use >= 1, the scale pair and target > 0");
     DCLIP_HOST_CHECK(rows > 0, "dclip_layernorm_bwd_scaled: rows must be > 0");
     hipStream_t s = (hipStream_t)stream;
-    if (cols == 512) bwd_fast_ds<float, 2>(dy, x, w, mean, rstd, res, dx, lp, dw, db, rows, st, spair, target, s);
-    else if (cols == 768) bwd_fast_ds<float, 3>(dy, x, w, mean, rstd, res, dx, lp, dw, db, rows, st, spair, target, s);
-    else bwd_fast_ds<float, 4>(dy, x, w, mean, rstd, res, dx, lp, dw, db, rows, st, spair, target, s);
+    if (cols == 512) bwd_fast_ds<float, 2>(dy, x, w, mean, rstd, res, dx, lp, dw, db, rows, st, use, spair, target, s);
+    else if (cols == 768) bwd_fast_ds<float, 3>(dy, x, w, mean, rstd, res, dx, lp, dw, db, rows, st, use, spair, target, s);
+    else bwd_fast_ds<float, 4>(dy, x, w, mean, rstd, res, dx, lp, dw, db, rows, st, use, spair, target, s);
     DCLIP_LAUNCH_CHECK();
     return 0;
 }

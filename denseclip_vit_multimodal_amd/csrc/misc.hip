@@ -859,70 +859,84 @@ extern "C" int dclip_add_readout_amax(const float* a, const void* b, int b_dt, c
 }
 
 // The fp16 backward's block-input gradient on a DELAYED scale: sum = a (+ b * (*bsc), b's CLS
-// rows read as 0; b may be null) and lp = (f16)(sum * s) in one pass, s = st[0] the power-of-two
-// scale the previous use of this gradient derived from its maximum; (s, 1/s) go to spair for
-// lp's consumers and this use's |sum| maximum becomes st's scale for the next (scale_finish).
-// One pass where the exact scale needs two (the maximum, then the cast).
+// rows read as 0; b may be null) and lp = (f16)(sum * s) in one pass, s the scale of this
+// gradient site's previous use (common.h ds_*: use `use` of the state st), (s, 1/s) to spair
+// for lp's consumers and this use's |sum| maximum joined into st for the next use.  One pass
+// where the exact scale needs two (the maximum, then the cast); two 8-column chunks per thread
+// and iteration, their loads issued together.
+template <typename TB>
+__device__ __forceinline__ void readout_sum8(const float* a, const TB* b, float sb, int64_t off, bool keep,
+                                             f32x4& x0, f32x4& x1) {
+    x0 = *(const f32x4*)(a + off);
+    x1 = *(const f32x4*)(a + off + 4);
+    if (b != nullptr && keep) {
+        if constexpr (sizeof(TB) == 4) {
+            x0 += *(const f32x4*)(b + off) * sb;
+            x1 += *(const f32x4*)(b + off + 4) * sb;
+        } else {
+            typedef TB tb8 __attribute__((ext_vector_type(8)));
+            const tb8 y = *(const tb8*)(b + off);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x0[e] += (float)y[e] * sb, x1[e] += (float)y[4 + e] * sb;
+        }
+    }
+}
+
 template <typename TB>
 __global__ __launch_bounds__(256) void add_readout_cast_ds_kernel(const float* a, const TB* __restrict__ b,
                                                                   const float* __restrict__ bsc, float* sum,
                                                                   f16* __restrict__ lp, int64_t rows, int cols,
                                                                   int ntok, float target, float* __restrict__ st,
-                                                                  float* __restrict__ spair) {
+                                                                  int use, float* __restrict__ spair) {
     const int c8 = cols / 8;
     const int64_t n8 = rows * c8;
     const float sb = bsc != nullptr ? *bsc : 1.0f;
-    const float ls = st[0];
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        spair[0] = ls;
-        spair[1] = st[1];
-    }
+    const float ls = ds_scale_of_use(st, use, target);
+    ds_begin(st, use, ls, spair);
     uint32_t m = 0;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t row = i / c8;
-        const int64_t off = i * 8;
-        f32x4 x0 = *(const f32x4*)(a + off), x1 = *(const f32x4*)(a + off + 4);
-        if (b != nullptr) {
-            if (row % ntok != 0) {
-                if constexpr (sizeof(TB) == 4) {
-                    x0 += *(const f32x4*)(b + off) * sb;
-                    x1 += *(const f32x4*)(b + off + 4) * sb;
-                } else {
-                    typedef TB tb8 __attribute__((ext_vector_type(8)));
-                    const tb8 y = *(const tb8*)(b + off);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += 2 * stride) {
+        const int64_t i2 = i + stride;
+        const bool two = i2 < n8;
+        f32x4 x[4];
+        readout_sum8<TB>(a, b, sb, i * 8, (i / c8) % ntok != 0, x[0], x[1]);
+        if (two) readout_sum8<TB>(a, b, sb, i2 * 8, (i2 / c8) % ntok != 0, x[2], x[3]);
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) x0[e] += (float)y[e] * sb, x1[e] += (float)y[4 + e] * sb;
-                }
+        for (int h = 0; h < 2; ++h) {
+            if (h == 1 && !two) break;
+            const int64_t off = (h ? i2 : i) * 8;
+            if (b != nullptr) {
+                *(f32x4*)(sum + off) = x[2 * h];
+                *(f32x4*)(sum + off + 4) = x[2 * h + 1];
             }
-            *(f32x4*)(sum + off) = x0;
-            *(f32x4*)(sum + off + 4) = x1;
-        }
-        f16x8 o;
+            f16x8 o;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            m = max(m, max(__float_as_uint(x0[e]) & 0x7fffffffu, __float_as_uint(x1[e]) & 0x7fffffffu));
-            o[e] = (f16)(x0[e] * ls);
-            o[4 + e] = (f16)(x1[e] * ls);
+            for (int e = 0; e < 4; ++e) {
+                m = max(m, max(__float_as_uint(x[2 * h][e]) & 0x7fffffffu, __float_as_uint(x[2 * h + 1][e]) & 0x7fffffffu));
+                o[e] = (f16)(x[2 * h][e] * ls);
+                o[4 + e] = (f16)(x[2 * h + 1][e] * ls);
+            }
+            *(f16x8*)(lp + off) = o;
         }
-        *(f16x8*)(lp + off) = o;
     }
-    scale_finish<4, true>(m, target, st);
+    ds_end<4>(m, st, use);
 }
 
 extern "C" int dclip_add_readout_cast_scaled(const float* a, const void* b, int b_dt, const float* b_scale_ptr,
                                              float* sum, void* lp, int64_t rows, int cols, int ntok, float target,
-                                             float* st, float* spair, void* stream) {
-    DCLIP_HOST_CHECK(cols % 8 == 0 && ntok > 0 && rows > 0 && target > 0.f && st != nullptr && spair != nullptr,
-                     "dclip_add_readout_cast_scaled: cols %% 8 == 0, ntok > 0, rows > 0, target > 0, st and spair");
+                                             float* st, int use, float* spair, void* stream) {
+    DCLIP_HOST_CHECK(cols % 8 == 0 && ntok > 0 && rows > 0 && target > 0.f && st != nullptr && spair != nullptr &&
+                         use >= 1,
+                     "dclip_add_readout_cast_scaled: cols %% 8 == 0, ntok > 0, rows > 0, target > 0, st, use >= 1, spair");
     DCLIP_HOST_CHECK(b == nullptr || sum != nullptr, "dclip_add_readout_cast_scaled: sum is required with b");
     DCLIP_HOST_CHECK(((uintptr_t)a | (uintptr_t)b | (uintptr_t)sum | (uintptr_t)lp) % 16 == 0,
                      "dclip_add_readout_cast_scaled: unaligned buffers");
     hipStream_t s = (hipStream_t)stream;
-    const unsigned g = grid_for(rows * (cols / 8), 512);  // the fan-in (dclip_grad_scale)
+    const unsigned g = grid_for((rows * (cols / 8) + 1) / 2, 4096);
     if (b == nullptr) b_dt = DCLIP_F32;
     DISPATCH_DT(b_dt, TB,
         add_readout_cast_ds_kernel<TB><<<g, 256, 0, s>>>(a, (const TB*)b, b_scale_ptr, sum, (f16*)lp, rows, cols, ntok,
-                                                         target, st, spair));
+                                                         target, st, use, spair));
     DCLIP_LAUNCH_CHECK();
     return 0;
 }

@@ -319,18 +319,18 @@ std::tuple<Tensor, Tensor> add_readout_amax(const Tensor& a, const Tensor& b, in
     return {sum, ws};
 }
 
-// delayed-scale state of one fp16 gradient site: 4 contiguous f32 on the op's device
+// delayed-scale state of one fp16 gradient site: DCLIP_DS_STATE_FLOATS contiguous f32 on the op's device
 float* scale_state(const Tensor& st, const Tensor& like_t) {
-    TORCH_CHECK(st.is_cuda() && st.scalar_type() == at::kFloat && st.numel() == 4 && st.is_contiguous() &&
-                    st.device() == like_t.device(), "scale state must be 4 contiguous f32 on the op's GPU");
+    TORCH_CHECK(st.is_cuda() && st.scalar_type() == at::kFloat && st.numel() == DCLIP_DS_STATE_FLOATS &&
+                    st.is_contiguous() && st.device() == like_t.device(),
+                "scale state must be DCLIP_DS_STATE_FLOATS contiguous f32 on the op's GPU");
     return (float*)st.data_ptr();
 }
 
 // fp16 delayed-scale form: (sum = a + b * 1/s_heads (b's CLS rows masked; no b: an empty tensor, the sum is a),
 // lp = (f16)(sum * s_state), the (s, 1/s) pair lp was cast with); st advanced to this use's scale
 std::tuple<Tensor, Tensor, Tensor> add_readout_cast_scaled(const Tensor& a, const c10::optional<Tensor>& b, int64_t ntok,
-                                                           const c10::optional<Tensor>& b_scale, Tensor& st,
-                                                           double target) {
+                                                           const c10::optional<Tensor>& b_scale, Tensor& st, int64_t use, double target) {
     check_gpu(a, "a");
     const bool has_b = b.has_value() && b->defined();
     TORCH_CHECK(a.scalar_type() == at::kFloat && a.dim() == 2 && a.numel() > 0, "add_readout_cast_scaled: a (rows, cols) f32");
@@ -346,7 +346,7 @@ std::tuple<Tensor, Tensor, Tensor> add_readout_cast_scaled(const Tensor& a, cons
     DCLIP_CALL(dclip_add_readout_cast_scaled(ptr<float>(a), has_b ? b->data_ptr() : nullptr,
                                              has_b ? dt_code(b->scalar_type()) : DCLIP_F32, scale_entry(b_scale, 1),
                                              has_b ? ptr<float>(sum) : nullptr, lp.data_ptr(), a.size(0), (int)a.size(1),
-                                             (int)ntok, (float)target, scale_state(st, a), ptr<float>(pair),
+                                             (int)ntok, (float)target, scale_state(st, a), (int)use, ptr<float>(pair),
                                              stream_of(a)));
     return {sum, lp, pair};
 }
@@ -355,7 +355,7 @@ std::tuple<Tensor, Tensor, Tensor> add_readout_cast_scaled(const Tensor& a, cons
 std::tuple<Tensor, Tensor, Tensor> layernorm_bwd_scaled(const Tensor& dy, const Tensor& x, const Tensor& w,
                                                         const Tensor& mean, const Tensor& rstd,
                                                         const c10::optional<Tensor>& res, Tensor& dw, Tensor& db,
-                                                        Tensor& st, double target) {
+                                                        Tensor& st, int64_t use, double target) {
     check_gpu(dy, "dy"); check_gpu(x, "x"); check_gpu(w, "w"); check_gpu(mean, "mean"); check_gpu(rstd, "rstd");
     check_opt(res, "res");
     TORCH_CHECK(x.dim() == 2 && dy.sizes() == x.sizes() && x.size(0) > 0, "layernorm_bwd_scaled: dy and x (rows, cols)");
@@ -369,7 +369,7 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_bwd_scaled(const Tensor& dy, const 
     DCLIP_CALL(dclip_layernorm_bwd_scaled(ptr<float>(dy), x.data_ptr(), dt_code(x.scalar_type()), ptr<float>(w),
                                           ptr<float>(mean), ptr<float>(rstd), optr<float>(res), ptr<float>(dx),
                                           lp.data_ptr(), ptr<float>(dw), ptr<float>(db), x.size(0), x.size(1),
-                                          (float)target, scale_state(st, x), ptr<float>(pair), stream_of(x)));
+                                          (float)target, scale_state(st, x), (int)use, ptr<float>(pair), stream_of(x)));
     return {dx, lp, pair};
 }
 
@@ -792,10 +792,10 @@ TORCH_LIBRARY(dclip, m) {
     m.def("transpose_batched(Tensor x, int B, int rows, int cols, int ld_in, int rows_pad, ScalarType dtype) -> Tensor");
     m.def("add_readout_cast(Tensor a, Tensor b, int ntok, ScalarType lp_dtype, float scale) -> (Tensor, Tensor)");
     m.def("add_readout_amax(Tensor a, Tensor b, int ntok, Tensor? b_scale, float target) -> (Tensor, Tensor)");
-    m.def("add_readout_cast_scaled(Tensor a, Tensor? b, int ntok, Tensor? b_scale, Tensor(a!) st, float target) "
+    m.def("add_readout_cast_scaled(Tensor a, Tensor? b, int ntok, Tensor? b_scale, Tensor(a!) st, int use, float target) "
           "-> (Tensor, Tensor, Tensor)");
     m.def("layernorm_bwd_scaled(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, Tensor? res, Tensor(a!) dw, "
-          "Tensor(b!) db, Tensor(c!) st, float target) -> (Tensor, Tensor, Tensor)");
+          "Tensor(b!) db, Tensor(c!) st, int use, float target) -> (Tensor, Tensor, Tensor)");
     m.def("attn_fwd(Tensor qkv, int B, int N, int H, float scale) -> (Tensor, Tensor)");
     m.def("attn_fwd_fp8(Tensor qkv, int B, int N, int H) -> (Tensor, Tensor)");
     m.def("attn_bwd(Tensor qkv, Tensor o, Tensor dout, Tensor lse, int B, int N, int H, float scale) -> Tensor");

@@ -206,42 +206,60 @@ def grad_scale(g, cdt):
 FP16_DELAYED_SCALE = True
 
 
+DS_STATE_FLOATS = 196  # DCLIP_DS_STATE_FLOATS (include/dclip.h)
+
+
 class DelayedScale:
     """Per-block state of the fp16 backward's delayed gradient scales, kept on the block module
     across training steps: site 0 = the MLP branch's incoming gradient, site 1 = the attention
     branch's.  A site's first backward takes the exact two-pass scale and seeds the state
-    (`primed`); later ones cast with the scale the previous backward derived from its own maximum
-    and leave this one's for the next (include/dclip.h, dclip_add_readout_cast_scaled)."""
+    (`prime`); later ones cast with the scale of the previous backward's maximum at that site and
+    record their own (include/dclip.h, dclip_add_readout_cast_scaled).  `uses[i]` counts the
+    site's delayed calls (1, 2, ...: the kernels' `use`)."""
 
     def __init__(self):
         self.buf = None
-        self.primed = [False, False]
+        self.uses = [0, 0]
+
+    @property
+    def primed(self):
+        return [u > 0 for u in self.uses]
 
     def site(self, i, device):
         if self.buf is None or self.buf.device != device:
-            self.buf = torch.zeros(8, dtype=torch.float32, device=device)
-            self.primed = [False, False]
-        return self.buf[4 * i:4 * i + 4]
+            self.buf = torch.zeros(2, DS_STATE_FLOATS, dtype=torch.float32, device=device)
+            self.uses = [0, 0]
+        return self.buf[i]
+
+    def next_use(self, i):
+        u = self.uses[i]
+        self.uses[i] = u + 1
+        return u
 
     def prime(self, i, pair):
-        """Seed site i with the exact (s, 1/s, ..) pair of this backward."""
+        """Seed site i from the exact (s, 1/s, ..) pair of this backward: call 1 then reads a
+        maximum of target / s, i.e. the scale s again (dclip.h's seeding rule)."""
         st = self.site(i, pair.device)
-        st[:2].copy_(pair[:2])
-        self.primed[i] = True
+        st.zero_()
+        st[0:1].copy_(FP16_GRAD_AMAX / pair[0:1])
+        st[192:193].copy_(pair[0:1])
+        self.uses[i] = 1
 
 
-def add_readout_cast_scaled(a, b, ntok, b_scale, st):
-    """(a + b * 1/s_heads with b's CLS rows masked, or a when b is None; its fp16 copy on st's
+def add_readout_cast_scaled(a, b, ntok, b_scale, ds, i):
+    """(a + b * 1/s_heads with b's CLS rows masked, or a when b is None; its fp16 copy on site i's
     delayed scale; the (s, 1/s) pair of that copy)."""
+    st = ds.site(i, a.device)
     _check(a, b_scale, st, strided=(b,) if b is not None else ())
-    sm, lp, pair = D().add_readout_cast_scaled(a, b, ntok, b_scale, st, FP16_GRAD_AMAX)
+    sm, lp, pair = D().add_readout_cast_scaled(a, b, ntok, b_scale, st, ds.next_use(i), FP16_GRAD_AMAX)
     return (sm if b is not None else a), lp, pair
 
 
-def layernorm_bwd_scaled(dy, x, w, mean, rstd, dw, db, res, st):
-    """layernorm_bwd with res and an fp16 copy of dx on st's delayed scale: (dx, lp, pair)."""
+def layernorm_bwd_scaled(dy, x, w, mean, rstd, dw, db, res, ds, i):
+    """layernorm_bwd with res and an fp16 copy of dx on site i's delayed scale: (dx, lp, pair)."""
+    st = ds.site(i, x.device)
     _check(dy, x, w, mean, rstd, dw, db, res, st)
-    return D().layernorm_bwd_scaled(dy, x, w, mean, rstd, res, dw, db, st, FP16_GRAD_AMAX)
+    return D().layernorm_bwd_scaled(dy, x, w, mean, rstd, res, dw, db, st, ds.next_use(i), FP16_GRAD_AMAX)
 
 
 def weight_grad(dy, x, want_bias=True, alpha=1.0, db=None, scale=None):
@@ -566,8 +584,9 @@ class BlockFn(torch.autograd.Function):
         B, Ntok, H, cdt, fp8 = ctx.meta[:5]
         dp = ctx.meta[6] if len(ctx.meta) > 6 else None
         # fp16 delayed scales (meta[7], a DelayedScale): only on the plain residual form
-        ds = ctx.meta[7] if len(ctx.meta) > 7 and cdt == torch.float16 and dp is None and FP16_DELAYED_SCALE else None
         C = x.shape[1]
+        ds = ctx.meta[7] if (len(ctx.meta) > 7 and cdt == torch.float16 and dp is None and FP16_DELAYED_SCALE
+                             and C in (512, 768, 1024)) else None  # the widths dclip_layernorm_bwd_scaled takes
         scale = (C // H) ** -0.5
         need = ctx.needs_input_grad
         wg = any(need[2:])
@@ -582,7 +601,6 @@ class BlockFn(torch.autograd.Function):
         if dxo is None:
             dxo = torch.zeros(B * Ntok, C, dtype=torch.float32, device=x.device)
         dxo = dxo.contiguous()
-        dev = x.device
         if ds is not None and ds.primed[0]:
             base = hsb = None
             if dmap is not None:
@@ -591,7 +609,7 @@ class BlockFn(torch.autograd.Function):
                 base = _readout_grad_buffer(dmap, B, Ntok, gh, gw, C)
             if dmap is None or base is not None:
                 # one pass: (+ the map gradient) and the fp16 operand on the delayed scale
-                dxo, dy, s1 = add_readout_cast_scaled(dxo, base, Ntok, hsb, ds.site(0, dev))
+                dxo, dy, s1 = add_readout_cast_scaled(dxo, base, Ntok, hsb, ds, 0)
                 dmap = None
         if dmap is not None:  # the read-out map's gradient joins the block output's
             gh, gw = ctx.meta[5][:2]
@@ -634,7 +652,7 @@ class BlockFn(torch.autograd.Function):
             dxm, dyo = layernorm_bwd(dxh2, xm, ln2w.detach(), mu2, rs2, dln2w, dln2b, res=dxo, lp_dtype=cdt)
             s2 = None
         elif ds is not None and ds.primed[1]:  # fp16: the operand on the delayed scale, same pass
-            dxm, dyo, s2 = layernorm_bwd_scaled(dxh2, xm, ln2w.detach(), mu2, rs2, dln2w, dln2b, dxo, ds.site(1, dev))
+            dxm, dyo, s2 = layernorm_bwd_scaled(dxh2, xm, ln2w.detach(), mu2, rs2, dln2w, dln2b, dxo, ds, 1)
         else:
             dxm = layernorm_bwd(dxh2, xm, ln2w.detach(), mu2, rs2, dln2w, dln2b, res=dxo)
         del dxh2

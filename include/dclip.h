@@ -360,25 +360,29 @@ int dclip_add_readout_amax(const float* a, const void* b, int b_dt, const float*
 
 /* DELAYED-scale fp16 casts of the backward's block gradients (the fp16 line; replaces a
  * dclip_grad_scale + dclip_cast pair, or dclip_add_readout_amax + dclip_cast, per block branch).
- * st: a per-site state {s, 1/s, 0, 0} that persists across training steps — s is the scale the
- * site's PREVIOUS use derived from its own maximum.  Each call casts with s, writes (s, 1/s) to
- * spair (2 floats: what the consumers of lp unscale by) and leaves in st the scale of THIS use's
- * maximum (s_next = 2^clamp(floor(log2(target / max)), -60, 60)) for the next call.  A gradient
- * that grew by more than 65504 / target between two uses overflows to inf in lp (the fp16
- * train step then checks its gradients and skips, train.step_unless_nonfinite).  The first use
- * of a site takes the exact two-pass scale and seeds st.  (No reference counterpart: the
- * reference trains in fp32.)
+ * st: the state of one gradient site, DCLIP_DS_STATE_FLOATS floats that persist across training
+ * steps (3 x 64 shards of |x|-maximum bits, then 3 used scales); `use` counts the site's calls
+ * from 1.  Call k casts with s = 2^clamp(floor(log2(target / max_{k-1})), -60, 60), the scale of
+ * call k-1's own maximum (call k-1's scale again when that maximum was 0 or not finite), writes
+ * (s, 1/s) to spair (2 floats: what the consumers of lp unscale by) and records its maximum in st
+ * for call k+1 — no fences, no arrival counter.  Seeding for call 1 (after an exact two-pass cast
+ * with scale s0): st all zero except st[0] = target / s0 and st[192] = s0.  A gradient that grew
+ * by more than 65504 / target between two calls overflows to inf in lp (the fp16 train step
+ * then checks its gradients and skips, train.step_unless_nonfinite).  (No reference
+ * counterpart: the reference trains in fp32.)
  *   dclip_add_readout_cast_scaled: sum = a (+ b * (*b_scale_ptr), b's CLS rows read as 0; b may be
  *     null, then sum is not written), lp = (f16)(sum * s).  models.py:565 -> 577-597 as
  *     dclip_add_readout_cast.  cols % 8 == 0.
  *   dclip_layernorm_bwd_scaled: dclip_layernorm_bwd_res with an f32 dy / x and lp = (f16)(dx * s)
  *     (models.py:243-249 backward).  cols in {512, 768, 1024}.                              */
+#define DCLIP_DS_STATE_FLOATS 196
 int dclip_add_readout_cast_scaled(const float* a, const void* b, int b_dt, const float* b_scale_ptr, float* sum,
-                                  void* lp, int64_t rows, int cols, int ntok, float target, float* st, float* spair,
-                                  void* stream);
+                                  void* lp, int64_t rows, int cols, int ntok, float target, float* st, int use,
+                                  float* spair, void* stream);
 int dclip_layernorm_bwd_scaled(const float* dy, const void* x, int x_dt, const float* w, const float* mean,
                                const float* rstd, const float* res, float* dx, void* lp, float* dw, float* db,
-                               int64_t rows, int64_t cols, float target, float* st, float* spair, void* stream);
+                               int64_t rows, int64_t cols, float target, float* st, int use, float* spair,
+                               void* stream);
 
 /* Train-mode BatchNorm2d (+ optionally the ReLU after it) on a channels-last 16-bit map viewed as
  * rows (B*H*W) of C channels at a row pitch of ld elements (ld = C for a whole map; larger for a

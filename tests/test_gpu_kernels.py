@@ -1036,6 +1036,45 @@ def test_bn_rows_fused_relu(C, ld, relu):
     dw, db = O.D().bn_bwd_rows(g[:, :C], x, w, b, mean, rstd, relu, True, True, dx[:, :C])
     assert rel_err(dx[:, :C].float(), xr.grad) < 2e-2
     assert rel_err(dw, wr.grad) < 1e-2 and rel_err(db, br.grad) < 1e-2
+    # the fp16 heads' gradient scale: dw / db times its 1/s in the kernel (bitwise: a power of
+    # two), dx unchanged
+    hs = torch.tensor([2.0 ** 13, 2.0 ** -13, 0.0, 0.0], device=DEV)
+    dx2 = torch.empty(rows, ld, device=DEV, dtype=torch.bfloat16)
+    dw2, db2 = O.D().bn_bwd_rows(g[:, :C], x, w, b, mean, rstd, relu, True, True, dx2[:, :C], hs)
+    assert torch.equal(dw2, dw * 2.0 ** -13) and torch.equal(db2, db * 2.0 ** -13)
+    assert torch.equal(dx2[:, :C], dx[:, :C])
+
+
+@pytest.mark.parametrize("Cin,Nout,splits", [(768, 128, 4), (256, 64, 1), (128, 192, 3)])
+def test_conv3x3_wgrad_oihw_and_scale(Cin, Nout, splits):
+    """dclip_conv3x3_wgrad's OIHW output (the split-K sum written in torch's (Cout, Cin, 3, 3)
+    layout) equals the (Nout, 9 Cin) [co][tap][ci] output permuted, bitwise (same summation
+    order), and the scaled form is that times 1/s (a power of two), bitwise."""
+    O = ops()
+    B, H, W = 2, 16, 24
+    X = torch.randn(B * H * W, Cin, device=DEV).half()
+    dY = torch.randn(B * H * W, Nout, device=DEV).half()
+    args = (dY, Nout, Nout, X, H * W * Cin, 0, Cin, B, H, W, Cin, splits)
+    rows = O.D().conv3x3_wgrad(*args)
+    oihw = O.D().conv3x3_wgrad(*args, True)
+    assert oihw.shape == (Nout, Cin, 3, 3)
+    assert torch.equal(oihw, rows.view(Nout, 3, 3, Cin).permute(0, 3, 1, 2))
+    hs = torch.tensor([2.0 ** 9, 2.0 ** -9, 0.0, 0.0], device=DEV)
+    assert torch.equal(O.D().conv3x3_wgrad(*args, True, hs), oihw * 2.0 ** -9)
+    ref = torch.nn.grad.conv2d_weight(X.float().view(B, H, W, Cin).permute(0, 3, 1, 2), (Nout, Cin, 3, 3),
+                                      dY.float().view(B, H, W, Nout).permute(0, 3, 1, 2), padding=1)
+    assert rel_err(oihw, ref) < 1e-5
+
+
+@pytest.mark.parametrize("Cin,Cout", [(768, 128), (256, 64)])
+def test_conv3x3_weight_layouts(Cin, Cout):
+    """The cached implicit-GEMM weight layouts built by the transpose kernels equal the permute
+    definitions: forward rows (Cout, 9 Cin) [co][tap][ci] and dgrad rows (Cin, 9 Cout) [ci][tap][co]."""
+    O = ops()
+    w = torch.randn(Cout, Cin, 3, 3, device=DEV)
+    for cdt in (torch.bfloat16, torch.float16):
+        assert torch.equal(O._conv3x3_rows(w, cdt), w.permute(0, 2, 3, 1).reshape(Cout, 9 * Cin).to(cdt))
+        assert torch.equal(O._conv3x3_dgrad_rows(w, cdt), w.permute(1, 2, 3, 0).reshape(Cin, 9 * Cout).to(cdt))
 
 
 @pytest.mark.parametrize("K,C1", [(19, 256), (1, 128)])
