@@ -103,7 +103,8 @@ __device__ __forceinline__ int sw8(int row) { return (row >> 2) & 3; }
 
 // ---------------------------------------------------------------------------- 1. pack
 // grid (n1p / 64, H, B), 256 threads: tokens 1 + 64u .. 64 + 64u of one head
-template <typename T>
+// QK = false (the default S16 kernel, which takes q and k from the 16-bit qkv): V^T only
+template <typename T, bool QK>
 __global__ void __launch_bounds__(256) fp8mx_pack_kernel(const T* __restrict__ qkv, uint8_t* __restrict__ q8,
                                                          uint8_t* __restrict__ qs, uint8_t* __restrict__ k8,
                                                          uint8_t* __restrict__ vt8, uint32_t* __restrict__ sc, int N,
@@ -114,7 +115,22 @@ __global__ void __launch_bounds__(256) fp8mx_pack_kernel(const T* __restrict__ q
     const int u = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
     const int tid = threadIdx.x;
     const int64_t hb = (int64_t)b * H + h;
-    {
+    if constexpr (!QK) {
+        // the unit's V rows into LDS (thread -> token t, 16-dim chunk d0)
+        const int t = tid >> 2, d0 = (tid & 3) * 16;
+        const int tok = 1 + u * 64 + t;
+        if (tok < N) {
+            const T* row = qkv + ((int64_t)b * N + tok) * 3 * C + 2 * C + h * 64 + d0;
+            const uint4 r0 = *(const uint4*)row, r1 = *(const uint4*)(row + 8);
+            const T* e0 = (const T*)&r0;
+            const T* e1 = (const T*)&r1;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) vs[t][d0 + i] = (float)e0[i], vs[t][d0 + 8 + i] = (float)e1[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) vs[t][d0 + i] = 0.f;
+        }
+    } else {
         // q and k rows: thread -> (token t, 16-dim chunk d0); a 32-dim block is two threads
         const int t = tid >> 2, d0 = (tid & 3) * 16, dh = d0 >> 5;
         const int tok = 1 + u * 64 + t;
@@ -189,6 +205,15 @@ __global__ void __launch_bounds__(256) fp8mx_pack_kernel(const T* __restrict__ q
 }
 
 // ---------------------------------------------------------------------------- 2. attention
+// S16 (the default): S^T = K Q^T on the 16-bit MFMA from the 16-bit qkv (K tiles staged by
+// LDS-DMA in the 128-B-row swizzled image of the 16-bit kernels) and only O^T += V^T P^T on the
+// block-scaled fp8 MFMA.  The scores are exponentiated, so an e4m3 error in S (3 mantissa bits:
+// ~6 % of the score's spread) becomes a multiplicative error in P that grows with the score
+// scale (27.8 % from exact on a head with 16x scores, round 3), whereas P V's e4m3 errors
+// average over the keys.  Ring slot for S16: [K 16-bit 64 x 128 B | V^T 64 x 64 B | scales].
+constexpr int U16SLOT = 8192 + 4096 + 256;
+
+template <bool S16>
 struct F8Ctx {
     char* smem;     // 4 ring slots of U8SLOT bytes
     rsrc_t rmine;   // this wave's piece source: the K plane (waves 0-3) or the V^T plane (4-7)
@@ -199,6 +224,9 @@ struct F8Ctx {
     int rem;        // keys in the last unit (64 unless N - 1 is ragged)
     i32x8 qf;       // this lane's q8 half row
     int qsc;        // its E8M0 scale
+    rsrc_t rk;       // S16: the 16-bit qkv rows of this image (K tiles)
+    uint32_t voffk;  // S16: this lane's K-piece offset (row 8 wave + lane / 8, swizzled chunk)
+    uint32_t ldb;    // S16: qkv row pitch in bytes
     f32x16 o[2];
     f32x16 negm;
     float m;
@@ -206,9 +234,34 @@ struct F8Ctx {
 };
 
 // unit t into ring slot `slot`: one 1-KiB piece per wave (waves 0-3: K rows 16w.., 4-7: V^T
-// rows), then 32 B of the scale dwords per wave (lanes 0-7); two vmcnt entries per wave
-__device__ __forceinline__ void f8_issue(F8Ctx& c, int t, int slot) {
+// rows), then 32 B of the scale dwords per wave (lanes 0-7); two vmcnt entries per wave.
+// S16: every wave one 1-KiB piece of the 16-bit K tile (rows 8w .. 8w + 7 of the unit, straight
+// from qkv: keys 1 + 64t + row, rows past N at 0xFFFFFFF0 = zeros), then waves 0-3 a V^T piece
+// and waves 4-7 64 B of the scale dwords (lanes 0-15): two entries per wave as well.
+template <bool S16>
+__device__ __forceinline__ void f8_issue(F8Ctx<S16>& c, int t, int slot) {
 #if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (S16) {
+        char* base = c.smem + slot * U16SLOT;
+        const uint32_t soff = (uint32_t)(1 + 64 * t) * c.ldb;
+        const bool ragged = t == c.nt - 1 && c.rem < 64;  // wave-uniform
+        if (__builtin_expect(ragged, 0)) {
+            const bool ok = c.wave * 8 + (c.lane >> 3) < c.rem;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rk, LDS_PTR(base + c.wave * 1024), 16,
+                                                     ok ? c.voffk + soff : 0xFFFFFFF0u, 0, 0, 0);
+        } else {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rk, LDS_PTR(base + c.wave * 1024), 16, c.voffk, soff, 0, 0);
+        }
+        if (c.wave < 4) {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rmine, LDS_PTR(base + 8192 + c.wave * 1024), 16, c.voff,
+                                                     (uint32_t)t * c.soff_unit, 0, 0);
+        } else if (c.lane < 16) {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rsc, LDS_PTR(base + 12288 + (c.wave - 4) * 64), 4,
+                                                     (uint32_t)((c.wave - 4) * 16 + c.lane) * 4, (uint32_t)t * 256, 0,
+                                                     0);
+        }
+        return;
+    }
     char* base = c.smem + slot * U8SLOT;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rmine, LDS_PTR(base + c.wave * 1024), 16, c.voff,
                                              (uint32_t)t * c.soff_unit, 0, 0);
@@ -228,11 +281,28 @@ __device__ __forceinline__ i32x8 tile_row(const char* img, int row, int h) {
 }
 
 // S^T of the unit in slot image `img` (scales `scw`: the lane's dword of that unit), seeded with init
-__device__ __forceinline__ void f8_s(f32x16 (&s)[2], const char* img, int scw, const F8Ctx& c, const f32x16& init) {
+template <bool S16>
+__device__ __forceinline__ void f8_s(f32x16 (&s)[2], const char* img, int scw, const F8Ctx<S16>& c, const f32x16& init) {
     const i32x8 ka = tile_row(img, c.l32, c.h);
     const i32x8 kb = tile_row(img, 32 + c.l32, c.h);
     s[0] = mfma_mx<0>(ka, scw, c.qf, c.qsc, init);
     s[1] = mfma_mx<1>(kb, scw, c.qf, c.qsc, init);
+}
+
+// S16: S^T of the unit from its 16-bit K image (32-key blocks kb), q16 the lane's 16-bit q row
+template <typename T>
+__device__ __forceinline__ void f16_s(f32x16 (&s)[2], const char* img, const typename Mfma<T>::frag (&q16)[4], int l32,
+                                      int h, const f32x16& init) {
+    typedef typename Mfma<T>::frag frag;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+        frag kf[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) kf[j] = row_frag<T>(img, kb * 32 + l32, 2 * j + h);
+        s[kb] = init;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s[kb] = Mfma<T>::mma(kf[j], q16[j], s[kb]);
+    }
 }
 
 __device__ __forceinline__ float f8_rowmax(const f32x16 (&s)[2]) {
@@ -282,7 +352,9 @@ __device__ __forceinline__ void f8_exp_pack(const f32x16 (&sc)[2], float (&rsp)[
 // with the reference moved to the unit's row max (o, l and the seeded S(t+1) rescaled) before
 // P(t) enters O or l.  A reference below the true running max only scales P up: e4m3's relative
 // rounding does not depend on the scale, and fewer small P fall into the subnormal range.
-__device__ __forceinline__ void f8_pv(F8Ctx& c, f32x16 (&sc)[2], f32x16 (&sn)[2], const char* cur) {
+template <bool S16>
+__device__ __forceinline__ void f8_pv(F8Ctx<S16>& c, f32x16 (&sc)[2], f32x16 (&sn)[2], const char* cur) {
+    constexpr int VOFF = S16 ? 8192 : 4096, SOFF = S16 ? 12288 : 8192;  // V^T tile, scales in the slot
     constexpr float LIM = 448.0f;
     float rsp[4];
     i32x8 pf;
@@ -316,30 +388,35 @@ __device__ __forceinline__ void f8_pv(F8Ctx& c, f32x16 (&sc)[2], f32x16 (&sn)[2]
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) c.l4[j] += rsp[j];
-    const int scw = *(const int*)(cur + 8192 + c.lane * 4);
-    const i32x8 va = tile_row(cur + 4096, c.l32, c.h);
-    const i32x8 vb = tile_row(cur + 4096, 32 + c.l32, c.h);
+    const int scw = *(const int*)(cur + SOFF + c.lane * 4);
+    const i32x8 va = tile_row(cur + VOFF, c.l32, c.h);
+    const i32x8 vb = tile_row(cur + VOFF, 32 + c.l32, c.h);
     c.o[0] = mfma_mx<2>(va, scw, pf, E8M0_ONE, c.o[0]);
     c.o[1] = mfma_mx<3>(vb, scw, pf, E8M0_ONE, c.o[1]);
 }
 
 // step t (slot Q = t % 4): S(t+1) into sn beside P(t) / PV(t) from sc
-template <int Q>
-__device__ __forceinline__ void f8_step(F8Ctx& c, int t, f32x16 (&sc)[2], f32x16 (&sn)[2]) {
+template <typename T, bool S16, int Q>
+__device__ __forceinline__ void f8_step(F8Ctx<S16>& c, int t, f32x16 (&sc)[2], f32x16 (&sn)[2],
+                                        const typename Mfma<T>::frag (&q16)[4]) {
+    constexpr int SLOT = S16 ? U16SLOT : U8SLOT;
     wait_vmcnt<2>();               // units t and t+1 landed (own entries; unit t+2 in flight)
     __builtin_amdgcn_s_barrier();  // everyone's; everyone done with step t-1 (slot (t+3) % 4 free)
     f8_issue(c, t + 3 < c.nt ? t + 3 : c.nt - 1, (Q + 3) & 3);
-    const char* cur = c.smem + Q * U8SLOT;
-    const char* nxt = c.smem + ((Q + 1) & 3) * U8SLOT;
+    const char* cur = c.smem + Q * SLOT;
+    const char* nxt = c.smem + ((Q + 1) & 3) * SLOT;
     // S(t+1): past the last unit the slot holds a copy of the last unit (the issue clamp), and
     // the result is dropped — the step stays branch-free
-    f8_s(sn, nxt, *(const int*)(nxt + 8192 + c.lane * 4), c, c.negm);
+    if constexpr (S16)
+        f16_s<T>(sn, nxt, q16, c.l32, c.h, c.negm);
+    else
+        f8_s(sn, nxt, *(const int*)(nxt + 8192 + c.lane * 4), c, c.negm);
     if (t == c.nt - 1 && c.rem < 64) f8_mask(sc, c.rem, c.h);  // wave-uniform: the ragged last unit
     f8_pv(c, sc, sn, cur);
 }
 
 // grid B * H * ceil((N - 1) / 256), 512 threads (8 waves x 32 queries 1 + ..)
-template <typename T>
+template <typename T, bool S16>
 __global__ __launch_bounds__(512, 1) void attn_fp8mx_kernel(const T* __restrict__ qkv, const uint8_t* __restrict__ q8,
                                                             const uint8_t* __restrict__ qs,
                                                             const uint8_t* __restrict__ k8,
@@ -348,8 +425,8 @@ __global__ __launch_bounds__(512, 1) void attn_fp8mx_kernel(const T* __restrict_
                                                             float* __restrict__ lse, int N, int H, int n1p) {
     constexpr int NW = 8, QB = 32 * NW;
     typedef typename Mfma<T>::frag frag;
-    __shared__ __attribute__((aligned(16))) char smem[4 * U8SLOT];
-    F8Ctx c;
+    __shared__ __attribute__((aligned(16))) char smem[4 * (S16 ? U16SLOT : U8SLOT)];
+    F8Ctx<S16> c;
     c.smem = smem;
     c.lane = threadIdx.x & 63;
     c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -368,12 +445,12 @@ __global__ __launch_bounds__(512, 1) void attn_fp8mx_kernel(const T* __restrict_
     const int qi = qblk * QB + c.wave * 32 + c.l32;
     const bool qok = qi < n1;
     const int qr = qok ? qi : n1 - 1;
-    {
+    if constexpr (!S16) {
         const uint8_t* qrow = q8 + (hb * n1p + qr) * 64;
         const i32x4 a = *(const i32x4*)(qrow + 16 * c.h), b = *(const i32x4*)(qrow + 32 + 16 * c.h);
         c.qf = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+        c.qsc = qs[(hb * n1p + qr) * 2 + c.h];
     }
-    c.qsc = qs[(hb * n1p + qr) * 2 + c.h];
     // key 0 (CLS) from the 16-bit qkv, as attn_fwd2_kernel: s0 = q . k0 on the VALU
     const T* Bb = qkv + (int64_t)b * N * ld;
     const T* Qrow = Bb + (int64_t)(1 + qr) * ld + hd * HD;
@@ -390,13 +467,28 @@ __global__ __launch_bounds__(512, 1) void attn_fp8mx_kernel(const T* __restrict_
 #pragma unroll
         for (int g = 0; g < 4; ++g) v0[db][g] = *(const t4*)(Bb + 2 * C + hd * HD + db * 32 + 8 * g + 4 * c.h);
 
-    // LDS-DMA sources: waves 0-3 the K plane (rows 16w.. of a unit), 4-7 the V^T plane
-    const bool kw = c.wave < 4;
-    const int prow = (c.wave & 3) * 16 + (c.lane >> 2);
-    const uint32_t gchunk = (uint32_t)(((c.lane & 3) ^ sw8(prow)) * 16);
-    c.rmine = kw ? make_rsrc(k8 + hb * n1p * 64, (uint32_t)n1p * 64) : make_rsrc(vt8 + hb * 64 * n1p, (uint32_t)n1p * 64);
-    c.voff = kw ? (uint32_t)prow * 64 + gchunk : (uint32_t)prow * (uint32_t)n1p + gchunk;
-    c.soff_unit = kw ? 4096u : 64u;
+    if constexpr (S16) {
+        // LDS-DMA sources: every wave a K piece (16-bit rows 8w + lane / 8 of a unit), waves 0-3 a
+        // V^T piece (rows 16w + lane / 4), waves 4-7 the scale dwords
+        const int prow = (c.wave & 3) * 16 + (c.lane >> 2);
+        const uint32_t gchunk = (uint32_t)(((c.lane & 3) ^ sw8(prow)) * 16);
+        c.rmine = make_rsrc(vt8 + hb * 64 * n1p, (uint32_t)n1p * 64);
+        c.voff = (uint32_t)prow * (uint32_t)n1p + gchunk;
+        c.soff_unit = 64u;
+        c.ldb = (uint32_t)(ld * sizeof(T));
+        c.rk = make_rsrc(Bb, (uint32_t)N * c.ldb);
+        const int kr = c.wave * 8 + (c.lane >> 3);
+        c.voffk = (uint32_t)kr * c.ldb + (uint32_t)(((c.lane & 7) ^ xsw(kr)) * 16) + (uint32_t)((C + hd * HD) * sizeof(T));
+    } else {
+        // LDS-DMA sources: waves 0-3 the K plane (rows 16w.. of a unit), 4-7 the V^T plane
+        const bool kw = c.wave < 4;
+        const int prow = (c.wave & 3) * 16 + (c.lane >> 2);
+        const uint32_t gchunk = (uint32_t)(((c.lane & 3) ^ sw8(prow)) * 16);
+        c.rmine = kw ? make_rsrc(k8 + hb * n1p * 64, (uint32_t)n1p * 64)
+                     : make_rsrc(vt8 + hb * 64 * n1p, (uint32_t)n1p * 64);
+        c.voff = kw ? (uint32_t)prow * 64 + gchunk : (uint32_t)prow * (uint32_t)n1p + gchunk;
+        c.soff_unit = kw ? 4096u : 64u;
+    }
     c.rsc = make_rsrc(sc + hb * (n1p / 64) * 64, (uint32_t)n1p * 4);
     f8_issue(c, 0, 0);
     f8_issue(c, c.nt > 1 ? 1 : 0, 1);
@@ -412,7 +504,10 @@ __global__ __launch_bounds__(512, 1) void attn_fp8mx_kernel(const T* __restrict_
     wait_vmcnt<4>();  // unit 0 landed (units 1, 2 in flight)
     __builtin_amdgcn_s_barrier();
     f32x16 sA[2], sB[2];
-    f8_s(sA, smem, *(const int*)(smem + 8192 + c.lane * 4), c, zero16());
+    if constexpr (S16)
+        f16_s<T>(sA, smem, q16, c.l32, c.h, zero16());
+    else
+        f8_s(sA, smem, *(const int*)(smem + 8192 + c.lane * 4), c, zero16());
     if (c.nt == 1 && c.rem < 64) f8_mask(sA, c.rem, c.h);
     c.m = fmaxf(f8_rowmax(sA), s0);
     c.negm = splat16(-c.m);
@@ -434,13 +529,13 @@ __global__ __launch_bounds__(512, 1) void attn_fp8mx_kernel(const T* __restrict_
     int t = 0;
     while (true) {  // unrolled by four: ring slots are immediates
         if (t >= c.nt) break;
-        f8_step<0>(c, t++, sA, sB);
+        f8_step<T, S16, 0>(c, t++, sA, sB, q16);
         if (t >= c.nt) break;
-        f8_step<1>(c, t++, sB, sA);
+        f8_step<T, S16, 1>(c, t++, sB, sA, q16);
         if (t >= c.nt) break;
-        f8_step<2>(c, t++, sA, sB);
+        f8_step<T, S16, 2>(c, t++, sA, sB, q16);
         if (t >= c.nt) break;
-        f8_step<3>(c, t++, sB, sA);
+        f8_step<T, S16, 3>(c, t++, sB, sA, q16);
     }
     __builtin_amdgcn_s_setprio(0);
     wait_vmcnt<0>();  // no LDS-DMA may still be landing when the workgroup retires
@@ -484,15 +579,17 @@ extern "C" int dclip_attn_fwd_fp8(int dt, const void* qkv, void* o, float* lse, 
     if (N > 1) {
         const dim3 gp(n1p / 64, H, B);
         const int grid = B * H * ((N - 1 + 255) / 256);
+        // DCLIP_OPT_ATTN_FP8_QK 1: S on the fp8 MFMA too (round 3's all-e4m3 kernel)
+        const bool s16 = dclip_option(DCLIP_OPT_ATTN_FP8_QK) != 1;
+#define FP8_LAUNCH(T, S)                                                                                        \
+    fp8mx_pack_kernel<T, !S><<<gp, 256, 0, st>>>((const T*)qkv, q8, qs, k8, vt8, sc, N, H, n1p);                  \
+    attn_fp8mx_kernel<T, S><<<grid, 512, 0, st>>>((const T*)qkv, q8, qs, k8, vt8, sc, (T*)o, lse, N, H, n1p);
         if (dt == DCLIP_BF16) {
-            fp8mx_pack_kernel<bf16><<<gp, 256, 0, st>>>((const bf16*)qkv, q8, qs, k8, vt8, sc, N, H, n1p);
-            attn_fp8mx_kernel<bf16><<<grid, 512, 0, st>>>((const bf16*)qkv, q8, qs, k8, vt8, sc, (bf16*)o, lse, N, H,
-                                                           n1p);
+            if (s16) { FP8_LAUNCH(bf16, true) } else { FP8_LAUNCH(bf16, false) }
         } else {
-            fp8mx_pack_kernel<f16><<<gp, 256, 0, st>>>((const f16*)qkv, q8, qs, k8, vt8, sc, N, H, n1p);
-            attn_fp8mx_kernel<f16><<<grid, 512, 0, st>>>((const f16*)qkv, q8, qs, k8, vt8, sc, (f16*)o, lse, N, H,
-                                                          n1p);
+            if (s16) { FP8_LAUNCH(f16, true) } else { FP8_LAUNCH(f16, false) }
         }
+#undef FP8_LAUNCH
     }
     DCLIP_LAUNCH_CHECK();
     return 0;

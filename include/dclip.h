@@ -82,7 +82,8 @@ int dclip_abi_version(void);
 #define DCLIP_OPT_GEMM_TN_COLSUM 9   /* 0 (default): the 256x256 weight-gradient kernel sums dY's columns (bias gradient) itself; 1: a separate pass */
 #define DCLIP_OPT_GEMM_EPI 10      /* persistent NT GEMM epilogue: 0 (default) row-major through LDS, whole 128-B lines per store; 1 the accumulator-layout stores (16 rows x 64 B) */
 #define DCLIP_OPT_GEMM_TAIL 11     /* persistent NT GEMM M tail (<= 16 rows, K % 256 == 0): 0 (default) one MFMA launch over K slices; 1 the 256-row split-K tile + combine pair */
-#define DCLIP_OPT_COUNT 12
+#define DCLIP_OPT_ATTN_FP8_QK 12   /* dclip_attn_fwd_fp8: 0 (default) S = QK^T on the 16-bit MFMA, P V on the fp8 one; 1 both on fp8 (the round-3 kernel) */
+#define DCLIP_OPT_COUNT 13
 int dclip_set_option(int id, int value);
 
 /* LayerNorm over the last dim (cols), eps, affine w/b (fp32).  y = (x-mu)*rstd*w+b.

@@ -76,7 +76,20 @@ def make_qkv(B, N, H, dt, spread=1.5):
     return qkv
 
 
-def emulate(qkv, B, N, H, rows):
+@pytest.fixture(params=["s16", "qk8"])
+def fp8_mode(request, hip):
+    """The default kernel (S = QK^T on the 16-bit MFMA, P V on e4m3) and round 3's all-e4m3 one
+    (DCLIP_OPT_ATTN_FP8_QK 1)."""
+    from denseclip_vit_multimodal_amd import _native as NATIVE
+    if request.param == "qk8":
+        assert hip.dclip_set_option(NATIVE.OPT_ATTN_FP8_QK, 1) == 0
+    try:
+        yield request.param
+    finally:
+        hip.dclip_set_option(NATIVE.OPT_ATTN_FP8_QK, 0)
+
+
+def emulate(qkv, B, N, H, rows, qk16=True):
     """float64 on the host (the firing test in float32, as the kernel); `rows`: the query rows to
     evaluate (>= 1: row 0 is the CLS row pass).  Returns o (B, len(rows), C) and lse (B, H, len(rows)).
 
@@ -84,7 +97,8 @@ def emulate(qkv, B, N, H, rows):
     of key 0 and the first unit; each unit's P = exp2(S - m) is taken against the current m, and
     only when some lane's partial row sum (the keys of one half, (key >> 2) & 1, of the 64) in a
     wave (32 consecutive query rows) passes 448 does every row of that wave move its m to the
-    unit's row max (by max(., 0)), rescale l and o, and redo P."""
+    unit's row max (by max(., 0)), rescale l and o, and redo P.  qk16: the scores from the 16-bit
+    q, k (the default kernel); otherwise from their MX e4m3 quantisation (DCLIP_OPT_ATTN_FP8_QK 1)."""
     rows = torch.as_tensor(rows)
     assert int(rows.min()) >= 1
     C = 64 * H
@@ -99,8 +113,12 @@ def emulate(qkv, B, N, H, rows):
     groups = torch.unique((rows - 1) // 32)
     G = len(groups)
     grow = (1 + 32 * groups[:, None] + torch.arange(32)[None]).clamp(max=N - 1)  # (G, 32)
-    q8 = mx_deq(q.reshape(B, H, n1p, 2, 32)).reshape(B, H, n1p, 64)[:, :, grow - 1]  # (B, H, G, 32, 64)
-    k8 = mx_deq(k.reshape(B, H, n1p, 2, 32)).reshape(B, H, n1p, 64)
+    if qk16:
+        q8 = q.double()[:, :, grow - 1]
+        k8 = k.double()
+    else:
+        q8 = mx_deq(q.reshape(B, H, n1p, 2, 32)).reshape(B, H, n1p, 64)[:, :, grow - 1]  # (B, H, G, 32, 64)
+        k8 = mx_deq(k.reshape(B, H, n1p, 2, 32)).reshape(B, H, n1p, 64)
     # V^T blocks: per head dim, the unit's key halves 0-31 / 32-63
     vu = v.reshape(B, H, U, 2, 32, 64).permute(0, 1, 2, 5, 3, 4)  # (B, H, U, d, key half, 32)
     v8 = mx_deq(vu).permute(0, 1, 2, 4, 5, 3).reshape(B, H, n1p, 64)
@@ -174,7 +192,7 @@ def pick(o, lse, B, N, H, rows):
 
 @pytest.mark.parametrize("N", [1, 2, 63, 64, 65, 129, 257, 1000, 2049])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
-def test_attn_fp8_matches_emulation_and_exact(N, dt):
+def test_attn_fp8_matches_emulation_and_exact(N, dt, fp8_mode):
     from denseclip_vit_multimodal_amd import ops
     B, H = 2, 3
     qkv = make_qkv(B, N, H, dt)
@@ -186,16 +204,17 @@ def test_attn_fp8_matches_emulation_and_exact(N, dt):
         return
     rows = torch.arange(1, N)
     o, lse = pick(o, lse, B, N, H, rows)
-    ref, lref = emulate(qkv, B, N, H, rows)
+    ref, lref = emulate(qkv, B, N, H, rows, qk16=fp8_mode == "s16")
     check_emulation(o, lse, ref, lref)
     e = rel_err(o, exact(qkv, B, N, H, rows))
-    assert e < 1e-1, e
+    assert e < (5e-2 if fp8_mode == "s16" else 1e-1), e
 
 
-def test_attn_fp8_full_length_heads_and_batch():
+def test_attn_fp8_full_length_heads_and_batch(fp8_mode):
     """The benchmark's sequence (N = 8193, 12 heads), MX block scales: a head scaled
     by 4x (scores x16) and an image scaled by 1/100 (uniform attention) come out as accurate as
-    the rest."""
+    the rest — with the default kernel (16-bit scores).  Round 3's all-e4m3 kernel (qk8) has the
+    accuracy cliff on the peaked head: its score errors are exponentiated."""
     from denseclip_vit_multimodal_amd import ops
     B, N, H = 2, 8193, 12
     qkv = make_qkv(B, N, H, torch.bfloat16).float().view(B, N, 3, H, 64)
@@ -208,20 +227,26 @@ def test_attn_fp8_full_length_heads_and_batch():
     check_row0_exact(o0[:, 0], l0[:, :, 0], qkv, B, N, H)
     rows = torch.cat([torch.arange(1, 70), torch.randperm(N - 140)[:300] + 70, torch.arange(N - 70, N)])
     o, lse = pick(o, lse, B, N, H, rows)
-    ref, lref = emulate(qkv, B, N, H, rows)
+    ref, lref = emulate(qkv, B, N, H, rows, qk16=fp8_mode == "s16")
     ex = exact(qkv, B, N, H, rows)
     assert ((lse - lref).abs() <= 1e-3 + 5e-3 * lref.abs()).all()
+    errs = {}
     for b in range(B):
         for h in (0, 5, 11):
             sl = (b, slice(None), slice(64 * h, 64 * h + 64))
             check_emulation(o[sl], lse[b, h], ref[sl], lref[b, h])
-            # head 5's scores are 16x larger, and so is their absolute e4m3 error (measured 27.8 %
-            # from exact on image 0; the emulation check above still holds): fp8 attention is for
-            # moderately peaked scores, as in the model test below
-            assert rel_err(o[sl], ex[sl]) < (1e-1 if h != 5 else 3.5e-1), (b, h, rel_err(o[sl], ex[sl]))
+            errs[(b, h)] = rel_err(o[sl], ex[sl])
+    print(fp8_mode, "error vs exact per (image, head)", errs)
+    for (b, h), e in errs.items():
+        if fp8_mode == "s16":
+            assert e < 1e-1, (b, h, e)
+        else:
+            # head 5's scores are 16x larger, and so is their absolute e4m3 error (27.8 % from
+            # exact on image 0 in round 3): the cliff the default kernel's 16-bit scores remove
+            assert e < (1e-1 if h != 5 else 3.5e-1), (b, h, e)
 
 
-def test_attn_fp8_spiky_scores():
+def test_attn_fp8_spiky_scores(fp8_mode):
     """A few dominant keys (the CLS-like spike): the running max moves mid-sweep."""
     from denseclip_vit_multimodal_amd import ops
     B, N, H = 1, 700, 2
@@ -232,7 +257,7 @@ def test_attn_fp8_spiky_scores():
     o, lse = ops.attn_fwd_fp8(qkv, B, N, H)
     rows = torch.arange(1, N)
     o, lse = pick(o, lse, B, N, H, rows)
-    ref, lref = emulate(qkv, B, N, H, rows)
+    ref, lref = emulate(qkv, B, N, H, rows, qk16=fp8_mode == "s16")
     check_emulation(o, lse, ref, lref)
     assert rel_err(o, exact(qkv, B, N, H, rows)) < 1e-1
 

@@ -1,6 +1,7 @@
 """Byte-compare every packed plane of dclip_attn_fwd_fp8 (q8 / k8 rows, their E8M0 scales, the
 de-permuted vt8 and the per-unit scale dwords) with a torch restatement of fp8mx_pack_kernel
 (attention_fp8.hip), for the test shape B=2, N=2049, H=3 (tokens 1..N-1 in 64-token units).
+Runs the all-e4m3 kernel (DCLIP_OPT_ATTN_FP8_QK 1): the default one packs V^T only.
 
   python tools/fp8_planes.py
 """
@@ -15,6 +16,7 @@ from denseclip_vit_multimodal_amd import ops  # noqa: E402
 
 
 def main():
+    assert N.lib().dclip_set_option(N.OPT_ATTN_FP8_QK, 1) == 0
     ok_all = True
     for dt, code in ((torch.bfloat16, N.BF16), (torch.float16, N.F16)):
         torch.manual_seed(0)
