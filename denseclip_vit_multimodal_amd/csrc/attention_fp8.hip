@@ -294,15 +294,17 @@ template <typename T>
 __device__ __forceinline__ void f16_s(f32x16 (&s)[2], const char* img, const typename Mfma<T>::frag (&q16)[4], int l32,
                                       int h, const f32x16& init) {
     typedef typename Mfma<T>::frag frag;
+    frag kf[2][4];  // all eight fragment reads first: one LDS round trip, then the MFMA chains
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-        frag kf[4];
+    for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) kf[j] = row_frag<T>(img, kb * 32 + l32, 2 * j + h);
-        s[kb] = init;
+        for (int j = 0; j < 4; ++j) kf[kb][j] = row_frag<T>(img, kb * 32 + l32, 2 * j + h);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) s[kb] = Mfma<T>::mma(kf[j], q16[j], s[kb]);
-    }
+    for (int kb = 0; kb < 2; ++kb) s[kb] = init;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) s[kb] = Mfma<T>::mma(kf[kb][j], q16[j], s[kb]);
 }
 
 __device__ __forceinline__ float f8_rowmax(const f32x16 (&s)[2]) {
@@ -395,8 +397,11 @@ __device__ __forceinline__ void f8_pv(F8Ctx<S16>& c, f32x16 (&sc)[2], f32x16 (&s
     c.o[1] = mfma_mx<3>(vb, scw, pf, E8M0_ONE, c.o[1]);
 }
 
-// step t (slot Q = t % 4): S(t+1) into sn beside P(t) / PV(t) from sc
-template <typename T, bool S16, int Q>
+// step t (slot Q = t % 4): S(t+1) into sn beside P(t) / PV(t) from sc.  MASK: the last step of
+// a ragged N - 1 (its unit's keys past N to -inf); peeled off the loop so that the steady-state
+// step has no branch between the S(t+1) MFMAs and unit t's softmax VALU (a branch there splits
+// the scheduling region and serialises the two)
+template <typename T, bool S16, int Q, bool MASK = false>
 __device__ __forceinline__ void f8_step(F8Ctx<S16>& c, int t, f32x16 (&sc)[2], f32x16 (&sn)[2],
                                         const typename Mfma<T>::frag (&q16)[4]) {
     constexpr int SLOT = S16 ? U16SLOT : U8SLOT;
@@ -411,8 +416,20 @@ __device__ __forceinline__ void f8_step(F8Ctx<S16>& c, int t, f32x16 (&sc)[2], f
         f16_s<T>(sn, nxt, q16, c.l32, c.h, c.negm);
     else
         f8_s(sn, nxt, *(const int*)(nxt + 8192 + c.lane * 4), c, c.negm);
-    if (t == c.nt - 1 && c.rem < 64) f8_mask(sc, c.rem, c.h);  // wave-uniform: the ragged last unit
+    if constexpr (MASK) f8_mask(sc, c.rem, c.h);  // the ragged last unit
     f8_pv(c, sc, sn, cur);
+}
+
+// the last step of a ragged sequence, slot (nt - 1) % 4 at run time
+template <typename T, bool S16>
+__device__ __forceinline__ void f8_step_masked(F8Ctx<S16>& c, int t, f32x16 (&sc)[2], f32x16 (&sn)[2],
+                                               const typename Mfma<T>::frag (&q16)[4]) {
+    switch (t & 3) {
+        case 0: f8_step<T, S16, 0, true>(c, t, sc, sn, q16); break;
+        case 1: f8_step<T, S16, 1, true>(c, t, sc, sn, q16); break;
+        case 2: f8_step<T, S16, 2, true>(c, t, sc, sn, q16); break;
+        default: f8_step<T, S16, 3, true>(c, t, sc, sn, q16); break;
+    }
 }
 
 // grid B * H * ceil((N - 1) / 256), 512 threads (8 waves x 32 queries 1 + ..)
@@ -526,16 +543,22 @@ __global__ __launch_bounds__(512, 1) void attn_fp8mx_kernel(const T* __restrict_
     c.l4[1] = c.l4[2] = c.l4[3] = 0.f;
     if (c.wave >= NW / 2) __builtin_amdgcn_s_setprio(1);  // static priority for the younger half
 
+    // the last step of a ragged N - 1 is peeled (its mask); the loop runs the branch-free steps
+    const int nfull = c.rem < 64 ? c.nt - 1 : c.nt;
     int t = 0;
     while (true) {  // unrolled by four: ring slots are immediates
-        if (t >= c.nt) break;
+        if (t >= nfull) break;
         f8_step<T, S16, 0>(c, t++, sA, sB, q16);
-        if (t >= c.nt) break;
+        if (t >= nfull) break;
         f8_step<T, S16, 1>(c, t++, sB, sA, q16);
-        if (t >= c.nt) break;
+        if (t >= nfull) break;
         f8_step<T, S16, 2>(c, t++, sA, sB, q16);
-        if (t >= c.nt) break;
+        if (t >= nfull) break;
         f8_step<T, S16, 3>(c, t++, sB, sA, q16);
+    }
+    if (t < c.nt) {  // ragged: the masked last step, sc in sA when t is even
+        if ((t & 1) == 0) f8_step_masked<T, S16>(c, t, sA, sB, q16);
+        else f8_step_masked<T, S16>(c, t, sB, sA, q16);
     }
     __builtin_amdgcn_s_setprio(0);
     wait_vmcnt<0>();  // no LDS-DMA may still be landing when the workgroup retires

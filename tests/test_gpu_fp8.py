@@ -1,9 +1,13 @@
 """fp8 attention forward (BASELINE config 5: "fp8 MFMA attention"); training runs the 16-bit
 flash backward on the fp8 forward's (o, lse).
 
-The kernel (attention_fp8.hip) quantises with MX block scales: every 32-element block of a q / k
-row (per 32-dim half) and of a V^T row (per head dim, per 32-key half of a 64-key unit) gets the
-largest power-of-two scale that keeps it within the e4m3 range.  Query 0 (the CLS row) is computed by the 16-bit split-key row pass and key 0 is folded
+The default kernel (attention_fp8.hip, S16) computes the scores S = Q K^T on the 16-bit MFMA and
+P V on the block-scaled e4m3 MFMA: an e4m3 error in S is exponentiated (round 3's all-e4m3
+kernel, kept behind DCLIP_OPT_ATTN_FP8_QK 1 and tested as "qk8", lands 23-28 % from exact on a
+head with 16x scores), while P V's errors average over the keys.  Quantisation uses MX block
+scales: every 32-element block of a V^T row (per head dim, per 32-key half of a 64-key unit) —
+and in qk8 of a q / k row (per 32-dim half) — gets the largest power-of-two scale that keeps it
+within the e4m3 range.  Query 0 (the CLS row) is computed by the 16-bit split-key row pass and key 0 is folded
 into every query from the 16-bit q, k, v, so neither is quantised.
 
 Two references per case:
@@ -265,8 +269,9 @@ def test_attn_fp8_spiky_scores(fp8_mode):
 def test_fp8_model_forward_vs_reference():
     """ViT-B/16 DenseCLIP (seg + depth heads) at 128x256 with every block's attention on the fp8
     kernel, against the reference's fp32 outputs (golden fixture): the fp8 error through 12
-    blocks stays within 5e-2 on the maps, score map and head outputs (measured values are
-    printed); the bf16-attention model is held to 1e-2 by test_gpu_parity."""
+    blocks stays within 3e-2 on the maps, score map and head outputs (measured 0.3-1.1 %,
+    printed; round 3's all-e4m3 kernel needed 5e-2); the bf16-attention model is held to 1e-2
+    by test_gpu_parity."""
     from helpers import CITYSCAPES_CFG, CITYSCAPES_CLASSES, spec_state_dict, golden, images
     from denseclip_vit_multimodal_amd import DenseCLIP
     g = golden("vitb16_1x128x256")
@@ -284,15 +289,14 @@ def test_fp8_model_forward_vs_reference():
             "seg_low": rel_err(cap["seg"], g["seg_low"]), "depth_low": rel_err(cap["depth"], g["depth_low"])}
     print("fp8 model errors", errs)
     for k, e in errs.items():
-        assert e < 5e-2, (k, e)
+        assert e < 3e-2, (k, e)
 
 
 def test_fp8_forward_bf16_backward_kernel():
     """Config 5 training: the fp8 forward's (o, lse) drive the 16-bit flash backward (P recomputed
     from the 16-bit q, k against the fp8 lse).  Against exact fp32 autograd the gradient carries
-    the fp8 forward's error (o ~7 % off exact here); held to 1.5e-1 per q / k / v slice, and to
-    the 16-bit backward's own tolerance against the same backward fed the exact forward's o / lse
-    for dV (linear in P)."""
+    the fp8 forward's error: 0.2-0.6 % per q / k / v slice with the 16-bit scores (round 3's
+    all-e4m3 forward: o ~7 % off exact, gradients held to 1.5e-1); held to 3e-2."""
     from denseclip_vit_multimodal_amd import ops
     B, N, H = 2, 2049, 2
     C = 64 * H
@@ -309,13 +313,13 @@ def test_fp8_forward_bf16_backward_kernel():
     o.permute(0, 2, 1, 3).reshape(B * N, C).backward(dout.float())
     errs = [rel_err(dq8[:, s].float(), r.grad[:, s]) for s in (slice(0, C), slice(C, 2 * C), slice(2 * C, 3 * C))]
     print("fp8-forward gradient errors vs exact (q, k, v)", errs)
-    assert max(errs) < 1.5e-1, errs
+    assert max(errs) < 3e-2, errs
 
 
 def test_fp8_model_backbone_gradients():
     """ViT-B/16 widths, fp8 attention forward + 16-bit backward through all 12 blocks: backbone
     gradients of a linear functional of the maps against autograd through the fp32 oracle
-    (bf16 attention is held to 2e-2 by test_gpu_parity)."""
+    within 6e-2 (bf16 attention is held to 2e-2 by test_gpu_parity)."""
     from helpers import CITYSCAPES_CFG, CITYSCAPES_CLASSES, spec_state_dict, images
     from oracle import denseclip_oracle as O
     from denseclip_vit_multimodal_amd import DenseCLIP
@@ -339,4 +343,4 @@ def test_fp8_model_backbone_gradients():
         errs[name] = rel_err(p.grad, sd["backbone." + name].grad)
     worst = max(errs, key=errs.get)
     print("fp8 model gradient error: worst", worst, errs[worst], "median", sorted(errs.values())[len(errs) // 2])
-    assert errs[worst] < 1.5e-1, (worst, errs[worst])
+    assert errs[worst] < 6e-2, (worst, errs[worst])  # measured 3.0e-2 (round 3, all-e4m3: bound 1.5e-1)
