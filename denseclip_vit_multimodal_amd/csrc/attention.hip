@@ -1256,10 +1256,25 @@ struct Dq2Ctx {
 
 // a ragged last tile as in fwd2_issue (keys past N land as zero rows: their dS multiplies a zero
 // K row, so they add nothing to dQ)
-template <typename T, int NW>
+// BF: branch-free — every issue takes the whole offset in the per-lane voffset, rows past N
+// selected to 0xFFFFFFF0 (two VALU per piece), so no branch splits the step's scheduling region
+template <typename T, int NW, bool BF = false>
 __device__ __forceinline__ void dq2_issue(Dq2Ctx<T, NW>& c, int t, int slot) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const uint32_t soff = (uint32_t)(1 + 64 * t) * c.ldb;
+    if constexpr (BF) {
+        const int lim = t == c.nt - 1 ? c.rem : 64;
+#pragma unroll
+        for (int i = 0; i < Dq2Ctx<T, NW>::PIECES; ++i) {
+            const int piece = c.wave + NW * i;
+            const bool ok = piece * 8 + (c.lane >> 3) < lim;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rs, LDS_PTR(c.smem + slot * 16384 + piece * 1024), 16,
+                                                     ok ? c.voffK[i] + soff : 0xFFFFFFF0u, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rs, LDS_PTR(c.smem + slot * 16384 + 8192 + piece * 1024), 16,
+                                                     ok ? c.voffV[i] + soff : 0xFFFFFFF0u, 0, 0, 0);
+        }
+        return;
+    }
     const bool ragged = t == c.nt - 1 && c.rem < 64;  // wave-uniform
     if (__builtin_expect(ragged, 0)) {
 #pragma unroll
@@ -1323,21 +1338,21 @@ __device__ __forceinline__ void dq2_ds(Dq2Ctx<T, NW>& c, const char* Kt, int kb,
 }
 
 // tile t in slot Q = t % 4; on entry (sA, pA) = unit (t, 0), on exit (sA, pA) = unit (t+1, 0)
-template <typename T, int NW, int Q>
+template <typename T, int NW, int Q, bool BF = false>
 __device__ __forceinline__ void dq2_step(Dq2Ctx<T, NW>& c, int t, f32x16& sA, f32x16& pA, f32x16& sB, f32x16& pB) {
     constexpr int PIECES = Dq2Ctx<T, NW>::PIECES;
     const char* Kt = c.smem + Q * 16384;
     const char* Kn = c.smem + ((Q + 1) & 3) * 16384;
     wait_vmcnt<2 * PIECES>();      // own pieces of tile t+1 landed (tile t+2 in flight)
     __builtin_amdgcn_s_barrier();  // everyone's; everyone done with step t-1 (slot (t+3) % 4 free)
-    dq2_issue<T, NW>(c, t + 3 < c.nt ? t + 3 : c.nt - 1, (Q + 3) & 3);
+    dq2_issue<T, NW, BF>(c, t + 3 < c.nt ? t + 3 : c.nt - 1, (Q + 3) & 3);
     dq2_sdp<T, NW>(c, Kt, 1, sB, pB);  // unit (t, 1) on the matrix pipe ...
     dq2_ds<T, NW>(c, Kt, 0, sA, pA);   // ... beside dS / dQ of unit (t, 0)
     dq2_sdp<T, NW>(c, Kn, 0, sA, pA);  // unit (t+1, 0) ...
     dq2_ds<T, NW>(c, Kt, 1, sB, pB);   // ... beside unit (t, 1)
 }
 
-template <typename T, int NW>
+template <typename T, int NW, bool BF = false>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq2_kernel(const T* __restrict__ qkv,
                                                                        const T* __restrict__ o,
                                                                        const T* __restrict__ dout,
@@ -1396,9 +1411,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq2_kernel(const T* 
         c.voffK[i] = base + (uint32_t)((C + hd * HD) * sizeof(T));
         c.voffV[i] = base + (uint32_t)((2 * C + hd * HD) * sizeof(T));
     }
-    dq2_issue<T, NW>(c, 0, 0);
-    dq2_issue<T, NW>(c, c.nt > 1 ? 1 : 0, 1);
-    dq2_issue<T, NW>(c, c.nt > 2 ? 2 : c.nt - 1, 2);
+    dq2_issue<T, NW, BF>(c, 0, 0);
+    dq2_issue<T, NW, BF>(c, c.nt > 1 ? 1 : 0, 1);
+    dq2_issue<T, NW, BF>(c, c.nt > 2 ? 2 : c.nt - 1, 2);
 
     // delta = rowsum(dO * O); key 0 (CLS) folded into dQ on the VALU:
     //   dS_0 = P_0 (dP_0 - delta), P_0 = exp2(q . k0 - L), dP_0 = dO . v0;  dQ^T[d] += dS_0 k0[d]
@@ -1444,14 +1459,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq2_kernel(const T* 
     // tile count (a loop with an exit after every step spilled ~90 VGPRs to scratch)
     int t = 0;
     for (; t + 4 <= c.nt; t += 4) {
-        dq2_step<T, NW, 0>(c, t, sA, pA, sB, pB);
-        dq2_step<T, NW, 1>(c, t + 1, sA, pA, sB, pB);
-        dq2_step<T, NW, 2>(c, t + 2, sA, pA, sB, pB);
-        dq2_step<T, NW, 3>(c, t + 3, sA, pA, sB, pB);
+        dq2_step<T, NW, 0, BF>(c, t, sA, pA, sB, pB);
+        dq2_step<T, NW, 1, BF>(c, t + 1, sA, pA, sB, pB);
+        dq2_step<T, NW, 2, BF>(c, t + 2, sA, pA, sB, pB);
+        dq2_step<T, NW, 3, BF>(c, t + 3, sA, pA, sB, pB);
     }
-    if (t < c.nt) dq2_step<T, NW, 0>(c, t++, sA, pA, sB, pB);
-    if (t < c.nt) dq2_step<T, NW, 1>(c, t++, sA, pA, sB, pB);
-    if (t < c.nt) dq2_step<T, NW, 2>(c, t++, sA, pA, sB, pB);
+    if (t < c.nt) dq2_step<T, NW, 0, BF>(c, t++, sA, pA, sB, pB);
+    if (t < c.nt) dq2_step<T, NW, 1, BF>(c, t++, sA, pA, sB, pB);
+    if (t < c.nt) dq2_step<T, NW, 2, BF>(c, t++, sA, pA, sB, pB);
     wait_vmcnt<0>();
     if (qok) store_row_t21<T>(dqkv + ((int64_t)b * N + q) * ld + hd * HD, c.dq, scale / DsScale<T>::v, c.h);
     if (r0ws != nullptr) {
@@ -2302,6 +2317,9 @@ bool bwd2_launch(const void* qkv, const void* o, const void* dout, const float* 
         if (dq4)
             attn_bwd_dq2_kernel<T, 4><<<B * H * nq, 256, 0, st>>>((const T*)qkv, (const T*)o, (const T*)dout, lse,
                                                                    delta, nstat, (T*)dqkv, N, H, scale, r0kv);
+        else if (dclip_option(DCLIP_OPT_ATTN_DQ_ISSUE) == 1)
+            attn_bwd_dq2_kernel<T, 8, true><<<B * H * nq, 512, 0, st>>>((const T*)qkv, (const T*)o, (const T*)dout,
+                                                                         lse, delta, nstat, (T*)dqkv, N, H, scale, r0kv);
         else
             attn_bwd_dq2_kernel<T, 8><<<B * H * nq, 512, 0, st>>>((const T*)qkv, (const T*)o, (const T*)dout, lse,
                                                                    delta, nstat, (T*)dqkv, N, H, scale, r0kv);

@@ -12,5 +12,5 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/s
 tail -1 $OUT/smoke.log
 timeout -k 10 400 python -u bench.py > $OUT/bench.log 2>&1 || { tail -20 $OUT/bench.log; exit 1; }
 grep '"metric"' $OUT/bench.log | cut -c1-400
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$OUT/prof -o bench -- python3 $R/bench.py --steps 5 --warmup 2 --no-mode-r --no-fp16 --cpu-baseline off > $R/$OUT/prof.log 2>&1 || { tail -20 $R/$OUT/prof.log; exit 1; }
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$OUT/prof -o bench -- python3 $R/bench.py --steps 5 --warmup 2 --no-mode-r --no-fp16 --no-extras --no-op-timing --cpu-baseline off > $R/$OUT/prof.log 2>&1 || { tail -20 $R/$OUT/prof.log; exit 1; }
 cd $R; f=$(find $OUT/prof -name "*kernel_stats.csv" | head -1); cut -d, -f1-8 $f | head -25
