@@ -1,7 +1,10 @@
 """DenseCLIP modules with the reference's class names, constructor kwargs and state-dict keys
 (reference seg/denseclip/models.py).  The CLIPVisionTransformer forward — the hot path —
-runs entirely on the HIP kernels of libdclip.so (see ops.py); the text encoder, context
-decoder and fusion neck keep plain torch modules (out of kernel scope).
+runs entirely on the HIP kernels of libdclip.so (see ops.py).  ViTFeatureFusionNeck keeps the
+reference's torch module structure (its state-dict keys), but on 16-bit GPU maps its levels,
+BatchNorms and fusion conv run on the HIP implicit-GEMM conv / BN kernels (ops.NeckLevelsFn,
+ops.bn_train, ops.Conv1x1Fn); the text encoder and the ContextDecoder stay plain torch modules
+(batch-independent; SURVEY §2 row 4-5, out of kernel scope).
 """
 import logging
 import math
