@@ -184,12 +184,15 @@ def train_step(model, opt, batch, silog=None, seg_weight=1.0, silog_weight=0.1):
     loss.backward()
     # the gradients are checked too when the backward ran in fp16 (power-of-two scaled casts can
     # overflow there); bf16 / fp32 keep the reference's loss-only rule
-    step_unless_nonfinite(opt, loss, check_grads=fp16_backward(model))
+    step_unless_nonfinite(opt, loss, check_grads=fp16_backward(model, img))
     return loss.detach()
 
 
-def fp16_backward(model):
-    """Whether the model's backward runs in fp16 (the backbone's compute dtype)."""
+def fp16_backward(model, img=None):
+    """Whether the model's backward runs in fp16: 16-bit images set the compute dtype themselves
+    (CLIPVisionTransformer._cdt), fp32 images use the backbone's compute_dtype."""
+    if img is not None and img.dtype in (torch.bfloat16, torch.float16):
+        return img.dtype == torch.float16
     bb = getattr(_unwrap(model), "backbone", None)
     return getattr(bb, "compute_dtype", None) == torch.float16
 
