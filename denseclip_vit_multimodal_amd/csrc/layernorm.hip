@@ -9,6 +9,7 @@
 namespace {
 
 constexpr int MAXV = 32;  // elements per lane => cols <= 2048
+constexpr int LN_SHARDS = 16;  // copies of [dw | db] the fast backward's blocks add into
 
 template <typename T>
 __device__ __forceinline__ void load4(const T* p, float* v) {
@@ -231,8 +232,11 @@ __global__ __launch_bounds__(256) void ln_fwd_fast(const TX* __restrict__ x, con
 }
 
 // 8 waves per block and at most 512 blocks: the dw / db partial sums of a block are reduced
-// in LDS and added with ONE atomic per column per block — every block adds into the same
-// 2 * cols floats, so the atomic count (not the bytes) sets that tail's cost
+// in LDS and added atomically into one of LN_SHARDS copies of [dw | db] (block b -> copy
+// b % LN_SHARDS, ln_shards: zero on entry), which ln_dwdb_reduce_kernel sums into dw / db and
+// clears again — every block adding into the same 2 * cols floats took 16-23 us of a 112-190 us
+// pass (512 adds per address on 48 cache lines, tools/ln_probe.py); a partials table reduced in
+// a fixed order cost more (the reduction's dependent loads)
 //
 // DS (delayed scale, fp16 lp): lp = (f16)(dx * s), s the power-of-two scale of this gradient
 // site's previous use (common.h ds_*: use `use` of the state st), (s, 1/s) to spair for the
@@ -242,8 +246,9 @@ __global__ __launch_bounds__(512) void ln_bwd_fast(const TDY* __restrict__ dy, c
                                                    const float* __restrict__ w, const float* __restrict__ mean,
                                                    const float* __restrict__ rstd, const float* res, float* dx,
                                                    void* __restrict__ lp, int lp_dt, float* __restrict__ dw,
-                                                   float* __restrict__ db, int64_t rows, float* st = nullptr,
-                                                   int use = 0, float* spair = nullptr, float target = 0.f) {
+                                                   float* __restrict__ db, int64_t rows, float* part,
+                                                   float* st = nullptr, int use = 0, float* spair = nullptr,
+                                                   float target = 0.f) {
     constexpr int cols = 256 * NV;
     __shared__ float red[8][2][4 * NV][64];
     const int lane = threadIdx.x & 63;
@@ -339,16 +344,56 @@ __global__ __launch_bounds__(512) void ln_bwd_fast(const TDY* __restrict__ dy, c
     }
     __syncthreads();
     // thread t sums the 8 waves' partials of entries t, t + 512, ... of the [2][4NV][64] table
+    // into this block's row [dw | db] of the partials table (or, without one, atomically into dw / db)
     for (int e = threadIdx.x; e < 2 * 4 * NV * 64; e += 512) {
         const int which = e / (4 * NV * 64), k = (e / 64) % (4 * NV), l = e % 64;
         float sum = 0.f;
 #pragma unroll
         for (int wv = 0; wv < 8; ++wv) sum += red[wv][which][k][l];
         const int c = 4 * l + 256 * (k / 4) + (k % 4);
-        float* out = which ? db : dw;
-        if (out) atomicAdd(out + c, sum);
+        if (part != nullptr) {
+            atomicAdd(part + ((int64_t)(blockIdx.x % LN_SHARDS) * 2 + which) * cols + c, sum);
+        } else {
+            float* out = which ? db : dw;
+            if (out) atomicAdd(out + c, sum);
+        }
     }
     if constexpr (DS) ds_end<8>(amax, st, use);
+}
+
+// dw[c] += sum over the shards of part[k][0][c], db[c] += part[k][1][c]; the shards cleared
+__global__ void ln_dwdb_reduce_kernel(float* __restrict__ part, int cols, float* __restrict__ dw,
+                                      float* __restrict__ db) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;  // which * cols + c
+    if (e >= 2 * cols) return;
+    const int which = e / cols, c = e % cols;
+    float v[LN_SHARDS];
+#pragma unroll
+    for (int k = 0; k < LN_SHARDS; ++k) v[k] = part[((int64_t)k * 2 + which) * cols + c];
+#pragma unroll
+    for (int k = 0; k < LN_SHARDS; ++k) part[((int64_t)k * 2 + which) * cols + c] = 0.f;
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < LN_SHARDS; ++k) sum += v[k];
+    float* out = which ? db : dw;
+    if (out != nullptr) out[c] += sum;
+}
+
+// the LN_SHARDS copies of [dw | db] (<= 1024 cols), one set per device, zeroed at allocation and
+// left zero by every reduction (the library's ops are stream-ordered: one stream at a time per
+// device)
+float* ln_partials(int cols) {
+    static float* buf[64] = {nullptr};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || cols > 1024) return nullptr;
+    if (buf[dev] == nullptr) {
+        const size_t bytes = (size_t)LN_SHARDS * 2 * 1024 * sizeof(float);
+        if (hipMalloc(&buf[dev], bytes) != hipSuccess || hipMemset(buf[dev], 0, bytes) != hipSuccess) {
+            buf[dev] = nullptr;
+            return nullptr;
+        }
+    }
+    return buf[dev];
 }
 
 // blocks of 4 waves: enough persistent waves to fill the chip (8 per SIMD), fewer for small inputs
@@ -369,8 +414,10 @@ void bwd_fast(const void* dy, const void* x, const float* w, const float* mean, 
               float* dx, void* lp, int lp_dt, float* dw, float* db, int64_t rows, hipStream_t st) {
     int64_t blocks = (rows + 7) / 8;
     blocks = blocks > 512 ? 512 : blocks;
+    float* part = (dw || db) ? ln_partials(256 * NV) : nullptr;
     ln_bwd_fast<TDY, TX, NV><<<(unsigned)blocks, 512, 0, st>>>((const TDY*)dy, (const TX*)x, w, mean, rstd, res, dx,
-                                                              lp, lp_dt, dw, db, rows);
+                                                              lp, lp_dt, dw, db, rows, part);
+    if (part) ln_dwdb_reduce_kernel<<<(2 * 256 * NV + 255) / 256, 256, 0, st>>>(part, 256 * NV, dw, db);
 }
 
 template <typename TX, typename TY>
@@ -425,8 +472,11 @@ void bwd_fast_ds(const float* dy, const void* x, const float* w, const float* me
                  float* spair, float target, hipStream_t s) {
     int64_t blocks = (rows + 7) / 8;
     blocks = blocks > 512 ? 512 : blocks;
+    float* part = (dw || db) ? ln_partials(256 * NV) : nullptr;
     ln_bwd_fast<float, TX, NV, true><<<(unsigned)blocks, 512, 0, s>>>(dy, (const TX*)x, w, mean, rstd, res, dx, lp,
-                                                                    DCLIP_F16, dw, db, rows, st, use, spair, target);
+                                                                    DCLIP_F16, dw, db, rows, part, st, use, spair,
+                                                                    target);
+    if (part) ln_dwdb_reduce_kernel<<<(2 * 256 * NV + 255) / 256, 256, 0, s>>>(part, 256 * NV, dw, db);
 }
 
 }  // namespace
