@@ -884,7 +884,7 @@ def test_neck_hip_vs_torch(train):
 
 # ----------------------------------------------------------------------------- fused head losses
 @pytest.mark.parametrize("hw,HW", [((8, 16), (128, 256)), ((7, 9), (20, 13)), ((64, 128), (1024, 2048)),
-                                   ((5, 33), (41, 100))])
+                                   ((5, 33), (41, 100)), ((16, 40), (12, 25))])  # the last: downsampling
 @pytest.mark.parametrize("ldt", [torch.float32, torch.bfloat16])
 def test_upsample_ce_vs_torch(hw, HW, ldt):
     """Fused upsample + CE(ignore 255): loss and the gradient wrt the low-res logits vs
@@ -904,7 +904,8 @@ def test_upsample_ce_vs_torch(hw, HW, ldt):
     assert rel_err(lg.grad.float(), lr.grad) < (1e-5 if ldt == torch.float32 else 1e-2)
 
 
-@pytest.mark.parametrize("hw,HW", [((8, 16), (128, 256)), ((64, 128), (1024, 2048)), ((5, 33), (41, 100))])
+@pytest.mark.parametrize("hw,HW", [((8, 16), (128, 256)), ((64, 128), (1024, 2048)), ((5, 33), (41, 100)),
+                                   ((16, 40), (12, 25))])
 @pytest.mark.parametrize("with_mask", [True, False])
 def test_upsample_silog_vs_reference(hw, HW, with_mask):
     from denseclip_vit_multimodal_amd.losses import SILogLoss

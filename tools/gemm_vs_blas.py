@@ -37,6 +37,12 @@ for name, n, k in [("qkv", 3 * C, C), ("out_proj", C, C), ("c_fc", 4 * C, C), ("
     b = torch.randn(n, device="cuda")  # every token GEMM of the model carries a bias
     cases.append((f"NT {name:11s} N={n:5d} K={k:5d}", lambda a=a, w=w, b=b: O.gemm(a, w, bias=b),
                   lambda a=a, w=w, b=b: torch.addmm(b.to(bf), a, w.t()), 2.0 * M * n * k))
+for name, n, k in [("dX in_proj", C, 3 * C), ("dX out_proj", C, C), ("dX c_fc", C, 4 * C)]:
+    # the model's dX GEMMs that feed a LayerNorm backward write fp32 and carry no bias
+    a = torch.randn(M, k, device="cuda").to(bf)
+    w = (torch.randn(n, k, device="cuda") * k ** -0.5).to(bf)
+    cases.append((f"NT {name:11s} N={n:5d} K={k:5d} f32", lambda a=a, w=w: O.gemm(a, w, out_dtype=torch.float32),
+                  lambda a=a, w=w: torch.mm(a, w.t(), out_dtype=torch.float32), 2.0 * M * n * k))
 for name, n, k in [("in_proj", 3 * C, C), ("out_proj", C, C), ("c_fc", 4 * C, C), ("c_proj", C, 4 * C)]:
     dy = torch.randn(M, n, device="cuda").to(bf)
     x = torch.randn(M, k, device="cuda").to(bf)
