@@ -47,6 +47,7 @@ _SIGS = {
     "dclip_pos_interp_bwd": [_c_void_p, _c_void_p, _i32, _i32, _i32, _i32, _c_void_p],
     "dclip_transpose": [_c_void_p, _i32, _i64, _i64, _i64, _c_void_p, _i32, _i64, _i64, _i32, _i64, _i64, _i64,
                         _i32, _c_void_p, _c_void_p],
+    "dclip_weight_refresh": [_c_void_p, _i32, _i64, _i32, _c_void_p],
     "dclip_row_mean_workspace": [_i32, _i64, _i32],
     "dclip_row_mean": [_c_void_p, _i32, _i64, _i64, _i64, _i32, _i64, _i32, _c_void_p, _c_void_p, _c_void_p],
     "dclip_score_map": [_c_void_p, _i32, _i64, _i64, _i64, _c_void_p, _c_void_p, _i32, _i32, _i32, _i32, _f32,

@@ -102,6 +102,10 @@ def _register_fakes():
     def _(x, dtype):
         return _e(x.shape[1], x.shape[0], like=x, dtype=dtype)
 
+    @reg("dclip::weight_refresh")
+    def _(desc, tiles, dtype):
+        return None
+
     @reg("dclip::transpose_batched")
     def _(x, B, rows, cols, ld_in, rows_pad, dtype):
         return _e(B, cols, rows_pad, like=x, dtype=dtype)

@@ -326,6 +326,83 @@ __global__ __launch_bounds__(256) void transpose_f32_fast_kernel(const float* __
     }
 }
 
+// ---------------------------------------------------------------------------- weight refresh
+// After an optimizer step every cached compute-dtype copy of a stepped fp32 weight (ops.WEIGHTS:
+// the plain (rows, cols) copy the forward GEMMs read and the (cols, rows) transposed copy of the
+// dX GEMMs) is rewritten in place by ONE launch over all weights: a workgroup per 64 x 64 tile of
+// one weight reads the fp32 tile once and writes both copies (the transposed one through LDS).
+// Entry e of the device descriptor (8 int64): src, plain dst (0: none), transposed dst (0: none),
+// rows, cols, first tile, column tiles, unused.  Replaces ~120 per-weight cast / transpose
+// launches per step.
+template <typename TO>
+__global__ __launch_bounds__(256) void weight_refresh_kernel(const int64_t* __restrict__ desc, int n) {
+    __shared__ float tile[64][65];
+    const int64_t blk = blockIdx.x;
+    int lo = 0, hi = n - 1;  // the entry whose tile range holds this block
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (desc[(int64_t)mid * 8 + 5] <= blk) lo = mid;
+        else hi = mid - 1;
+    }
+    const int64_t* d = desc + (int64_t)lo * 8;
+    const float* __restrict__ src = (const float*)d[0];
+    TO* __restrict__ dp = (TO*)d[1];
+    TO* __restrict__ dt = (TO*)d[2];
+    const int64_t rows = d[3], cols = d[4], local = blk - d[5], tcn = d[6];
+    const int64_t rb = (local / tcn) * 64, cb = (local % tcn) * 64;
+    const int t = threadIdx.x, c4 = t & 15, r = t >> 4;
+    const bool vec = (cols & 3) == 0;  // 16-byte source rows / 8-byte plain stores
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int64_t row = rb + r + 16 * i, col = cb + 4 * c4;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (row < rows) {
+            if (vec && col + 4 <= cols) {
+                v = *(const f32x4*)(src + row * cols + col);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (col + e < cols) v[e] = src[row * cols + col + e];
+            }
+            if (dp != nullptr) {
+                if (vec && col + 4 <= cols) {
+                    typedef TO to4 __attribute__((ext_vector_type(4)));
+                    const to4 o = {(TO)v[0], (TO)v[1], (TO)v[2], (TO)v[3]};
+                    *(to4*)(dp + row * cols + col) = o;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (col + e < cols) dp[row * cols + col + e] = (TO)v[e];
+                }
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) tile[r + 16 * i][4 * c4 + e] = v[e];
+    }
+    if (dt == nullptr) return;  // block-uniform
+    __syncthreads();
+    // transposed copy (cols, rows): row c of it = column c of the tile, 8 source rows per lane
+    const int j = t & 7, oc = t >> 3;
+    const bool tvec = (rows & 7) == 0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int c = oc + 32 * i;
+        const int64_t gc = cb + c, gr = rb + 8 * j;
+        if (gc >= cols || gr >= rows) continue;
+        if (tvec && gr + 8 <= rows) {
+            typedef TO to8 __attribute__((ext_vector_type(8)));
+            to8 o;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = (TO)tile[8 * j + e][c];
+            *(to8*)(dt + gc * rows + gr) = o;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                if (gr + e < rows) dt[gc * rows + gr + e] = (TO)tile[8 * j + e][c];
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------- row mean
 // F.adaptive_avg_pool2d(x, 1) of a pixel-row map (denseclip.py:596) read in place from a strided
 // row layout (the ViT token buffer: batch stride N*C, row offset 1 skips CLS).  Stage 1: one
@@ -659,6 +736,17 @@ extern "C" int dclip_pos_interp_bwd(const float* dout, float* dpos, int g, int C
     DCLIP_HOST_CHECK(g > 0 && H > 0 && W > 0, "dclip_pos_interp_bwd: bad sizes");
     const int64_t total = (int64_t)(g * g + 1) * C;
     pos_interp_bwd_kernel<<<grid_for(total), 256, 0, (hipStream_t)stream>>>(dout, dpos, g, C, H, W);
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int dclip_weight_refresh(const int64_t* desc, int n, int64_t tiles, int out_dt, void* stream) {
+    DCLIP_HOST_CHECK(desc != nullptr && n > 0 && tiles > 0, "dclip_weight_refresh: empty descriptor");
+    DCLIP_HOST_CHECK(out_dt == DCLIP_BF16 || out_dt == DCLIP_F16, "dclip_weight_refresh: 16-bit copies only");
+    DCLIP_HOST_CHECK(tiles < (1ll << 31), "dclip_weight_refresh: too many tiles");
+    hipStream_t st = (hipStream_t)stream;
+    if (out_dt == DCLIP_BF16) weight_refresh_kernel<bf16><<<(unsigned)tiles, 256, 0, st>>>(desc, n);
+    else weight_refresh_kernel<f16><<<(unsigned)tiles, 256, 0, st>>>(desc, n);
     DCLIP_LAUNCH_CHECK();
     return 0;
 }

@@ -276,6 +276,18 @@ Tensor transpose2d(const Tensor& x, at::ScalarType dtype) {
     return out;
 }
 
+// every cached compute-dtype copy of the stepped weights rewritten in one launch (C ABI
+// dclip_weight_refresh): desc = the (n, 8) int64 descriptor on the weights' device (built and
+// cached by ops.refresh_weight_copies); writes only through the pointers it holds
+void weight_refresh(const Tensor& desc, int64_t tiles, at::ScalarType dtype) {
+    check_gpu(desc, "desc");
+    TORCH_CHECK(desc.scalar_type() == at::kLong && desc.dim() == 2 && desc.size(1) == 8,
+                "weight_refresh: desc must be an (n, 8) int64 tensor");
+    c10::DeviceGuard g(desc.device());
+    DCLIP_CALL(dclip_weight_refresh((const int64_t*)desc.data_ptr(), (int)desc.size(0), tiles, dt_code(dtype),
+                                    stream_of(desc)));
+}
+
 // out[b][c][r] = x[b][r][c] for r < rows, c < cols (x rows of ld_in elements, batch stride
 // rows*ld_in); r in [rows, rows_pad) written as zeros: (B, cols, rows_pad) in dtype
 Tensor transpose_batched(const Tensor& x, int64_t B, int64_t rows, int64_t cols, int64_t ld_in, int64_t rows_pad,
@@ -789,6 +801,7 @@ TORCH_LIBRARY(dclip, m) {
     m.def("row_scale_add(Tensor? x, Tensor y, Tensor s) -> Tensor");
     m.def("bn_eval(Tensor x, Tensor? w, Tensor? b, Tensor running_mean, Tensor running_var, float eps, bool relu) -> Tensor");
     m.def("transpose2d(Tensor x, ScalarType dtype) -> Tensor");
+    m.def("weight_refresh(Tensor desc, int tiles, ScalarType dtype) -> ()");
     m.def("transpose_batched(Tensor x, int B, int rows, int cols, int ld_in, int rows_pad, ScalarType dtype) -> Tensor");
     m.def("add_readout_cast(Tensor a, Tensor b, int ntok, ScalarType lp_dtype, float scale) -> (Tensor, Tensor)");
     m.def("add_readout_amax(Tensor a, Tensor b, int ntok, Tensor? b_scale, float target) -> (Tensor, Tensor)");
@@ -844,6 +857,7 @@ TORCH_LIBRARY_IMPL(dclip, CUDA, m) {
     m.impl("row_scale_add", &row_scale_add);
     m.impl("bn_eval", &bn_eval);
     m.impl("transpose2d", &transpose2d);
+    m.impl("weight_refresh", &weight_refresh);
     m.impl("transpose_batched", &transpose_batched);
     m.impl("add_readout_cast", &add_readout_cast);
     m.impl("add_readout_amax", &add_readout_amax);

@@ -407,6 +407,68 @@ def _stamp_stepped_params(opt, *_):
     for group in opt.param_groups:
         for p in group["params"]:
             p.__dict__["_dclip_step"] = _STEP[0]
+    if EAGER_WEIGHT_REFRESH:
+        refresh_weight_copies([p for group in opt.param_groups for p in group["params"]])
+
+
+# rewrite the cached 16-bit copies of the stepped weights right after the step, all in one launch
+# per (device, dtype) (misc.hip weight_refresh_kernel), instead of one cast / transpose launch per
+# weight at its first use in the next forward / backward
+EAGER_WEIGHT_REFRESH = True
+_REFRESH_DESC = {}  # (device, dtype) -> (key, device descriptor, tiles, pinned host copy)
+
+
+def refresh_weight_copies(params):
+    """Refresh, in place, the plain and transposed compute-dtype copies WEIGHTS holds for these
+    fp32 parameters (the entries earlier forwards / backwards created), and re-stamp them valid.
+    The copies keep their storage, so the device descriptor of the launch is built once and
+    reused while the set of copies is unchanged.  A no-op during stream capture and for
+    parameters without cached copies; derived layouts (get_with) stay lazy."""
+    if not torch.cuda.is_available() or torch.cuda.is_current_stream_capturing():
+        return
+    groups = {}
+    for p in params:
+        cache = p.__dict__.get("_dclip_cache")
+        if not cache:
+            continue
+        w = p.detach()
+        if not w.is_cuda or w.dtype != torch.float32 or not w.is_contiguous() or w.data_ptr() % 16:
+            continue
+        stamp = _Cast.stamp(p)
+        rows = w.shape[0] if w.dim() else 1
+        cols = w.numel() // max(rows, 1)
+        for dt in (torch.bfloat16, torch.float16):
+            ep, et = cache.get((dt, False)), cache.get((dt, True))
+            vp = ep[1] if ep is not None else None
+            vt = et[1] if et is not None else None
+            if vp is not None and (vp.shape != (rows, cols) or vp.dtype != dt or not vp.is_contiguous()
+                                   or vp.data_ptr() % 16 or vp.data_ptr() == w.data_ptr()):
+                vp = None
+            if vt is not None and (vt.shape != (cols, rows) or vt.dtype != dt or not vt.is_contiguous()
+                                   or vt.data_ptr() % 16):
+                vt = None
+            if vp is None and vt is None:
+                continue
+            groups.setdefault((w.device, dt), []).append((cache, dt, w, vp, vt, stamp, rows, cols))
+    for (dev, dt), items in groups.items():
+        key = tuple((w.data_ptr(), 0 if vp is None else vp.data_ptr(), 0 if vt is None else vt.data_ptr(), r, c)
+                    for _, _, w, vp, vt, _, r, c in items)
+        ent = _REFRESH_DESC.get((dev, dt))
+        if ent is None or ent[0] != key:
+            table, tiles = [], 0
+            for src, dp, dtp, r, c in key:
+                tc = (c + 63) // 64
+                table.append([src, dp, dtp, r, c, tiles, tc, 0])
+                tiles += ((r + 63) // 64) * tc
+            host = torch.tensor(table, dtype=torch.int64).pin_memory()
+            desc = host.to(dev, non_blocking=True)
+            ent = _REFRESH_DESC[(dev, dt)] = (key, desc, tiles, host)
+        D().weight_refresh(ent[1], ent[2], dt)
+        for cache, dt_, w, vp, vt, stamp, _, _ in items:
+            if vp is not None:
+                cache[(dt_, False)] = (stamp, vp)
+            if vt is not None:
+                cache[(dt_, True)] = (stamp, vt)
 
 
 from torch.optim.optimizer import register_optimizer_step_post_hook  # noqa: E402

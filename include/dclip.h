@@ -210,6 +210,14 @@ int dclip_transpose(const void* in, int in_dt, int64_t in_bstride, int64_t in_ld
                     int batch, int64_t rows, int64_t rows_pad, int64_t cols,
                     int accumulate, float* colsum, void* stream);
 
+/* Compute-dtype weight copies after an optimizer step (no reference counterpart: the reference
+ * runs fp32 weights; replaces one cast and one transpose launch per weight per step).  desc:
+ * n entries of 8 int64 ON THE DEVICE: [src (f32, rows x cols, contiguous, 16-B aligned),
+ * plain dst (out_dt, rows x cols) or 0, transposed dst (out_dt, cols x rows) or 0, rows, cols,
+ * first tile, column tiles = ceil(cols / 64), 0]; entry e covers tiles [first, first +
+ * ceil(rows / 64) * column tiles), the entries in order, tiles = the total.  One launch.      */
+int dclip_weight_refresh(const int64_t* desc, int n, int64_t tiles, int out_dt, void* stream);
+
 /* Strided pixel rows: row r (< rows) of image b is X + b*bstride + (row_off + r)*ld (elements; a ViT
  * token buffer (B*N, C) has bstride N*C, row_off 1 (skips CLS), ld C).  16-bit X, 16-byte aligned rows.
  *

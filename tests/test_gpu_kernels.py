@@ -1148,3 +1148,49 @@ def test_neck_levels_fn_matches_per_level_path():
         assert rel_err(p.grad, pr.grad) < 2e-2, (n, rel_err(p.grad, pr.grad))
     for (n, bu), (_, br) in zip(neck.named_buffers(), ref.named_buffers()):
         assert rel_err(bu.float(), br.float()) < 1e-4, n
+
+
+# ----------------------------------------------------------------------------- weight copies
+@pytest.mark.parametrize("fused", [True, False])
+def test_weight_refresh_after_step_matches_fresh_casts(fused):
+    """After an optimizer step the cached 16-bit weight copies (plain and transposed) are rewritten
+    in place by one weight_refresh launch per dtype (ops.refresh_weight_copies, the step hook):
+    the same tensors come back from the cache, bitwise equal to fresh casts of the stepped fp32
+    weights — ragged tiles, odd column counts and 4-D conv weights included."""
+    O = ops()
+    torch.manual_seed(11)
+    shapes = [(2304, 768), (768, 768), (19, 64), (100, 37), (256, 1536), (64, 3, 5, 5)]
+    params = [torch.nn.Parameter(torch.randn(s, device=DEV)) for s in shapes]
+    held = {}
+    for p in params:
+        for dt in (torch.bfloat16, torch.float16):
+            held[(id(p), dt)] = (O.WEIGHTS.get(p, dt), O.WEIGHTS.get(p, dt, transposed=True))
+    opt = torch.optim.AdamW(params, lr=0.1, fused=fused)
+    for it in range(2):
+        for p in params:
+            p.grad = torch.randn_like(p)
+        opt.step()
+        for p in params:
+            w2 = p.detach().reshape(p.shape[0], -1)
+            for dt in (torch.bfloat16, torch.float16):
+                a = O.WEIGHTS.get(p, dt)
+                b = O.WEIGHTS.get(p, dt, transposed=True)
+                assert a is held[(id(p), dt)][0] and b is held[(id(p), dt)][1], "re-cast instead of refreshed"
+                assert torch.equal(a, w2.to(dt)), (p.shape, dt, it)
+                assert torch.equal(b, w2.t().contiguous().to(dt)), (p.shape, dt, it)
+
+
+def test_weight_refresh_off_falls_back_to_lazy_casts():
+    O = ops()
+    torch.manual_seed(12)
+    p = torch.nn.Parameter(torch.randn(768, 768, device=DEV))
+    a0 = O.WEIGHTS.get(p, torch.bfloat16)
+    opt = torch.optim.AdamW([p], lr=0.1, fused=True)
+    p.grad = torch.randn_like(p)
+    O.EAGER_WEIGHT_REFRESH = False
+    try:
+        opt.step()
+    finally:
+        O.EAGER_WEIGHT_REFRESH = True
+    a1 = O.WEIGHTS.get(p, torch.bfloat16)
+    assert a1 is not a0 and torch.equal(a1, p.detach().to(torch.bfloat16))
