@@ -1239,7 +1239,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const T* _
 // passes attn_bwd_row0_* under DCLIP_OPT_ATTN_BWD_BLOCK 1..5), K / V
 // tiles by LDS-DMA into a 4-slot ring three tiles ahead (no staging registers, no ds_write,
 // a bare barrier behind a counted vmcnt) and widened dQ stores.
-template <typename T, int NW>
+// QR = 32-query row blocks per wave: 1 (default: 8 waves, two per SIMD) or 2 (4 waves, one per
+// SIMD, 512 registers: each K / V / K^T fragment read from LDS feeds both row blocks — half the
+// LDS reads per MFMA — the dK/dV pass's register blocking applied to this pass; DCLIP_OPT_ATTN_DQ_ROWS 64)
+template <typename T, int NW, int QR = 1>
 struct Dq2Ctx {
     typedef typename Mfma<T>::frag frag;
     static constexpr int PIECES = 8 / NW;  // 1-KiB pieces of a 64-row K (and of a V) tile per wave
@@ -1249,23 +1252,24 @@ struct Dq2Ctx {
     uint32_t ldb;
     int nt, lane, l32, h, wave;
     int rem;  // keys in the last tile (64 unless N - 1 is ragged)
-    frag qf[4], gf[4];
-    float negL, negD;
-    f32x16 dq[2];
+    frag qf[QR][4], gf[QR][4];
+    float negL[QR], negD[QR];
+    f32x16 dq[QR][2];
 };
 
 // a ragged last tile as in fwd2_issue (keys past N land as zero rows: their dS multiplies a zero
 // K row, so they add nothing to dQ)
 // BF: branch-free — every issue takes the whole offset in the per-lane voffset, rows past N
 // selected to 0xFFFFFFF0 (two VALU per piece), so no branch splits the step's scheduling region
-template <typename T, int NW, bool BF = false>
-__device__ __forceinline__ void dq2_issue(Dq2Ctx<T, NW>& c, int t, int slot) {
+template <typename T, int NW, bool BF = false, int QR = 1>
+__device__ __forceinline__ void dq2_issue(Dq2Ctx<T, NW, QR>& c, int t, int slot) {
 #if defined(__HIP_DEVICE_COMPILE__)
+    typedef Dq2Ctx<T, NW, QR> X;
     const uint32_t soff = (uint32_t)(1 + 64 * t) * c.ldb;
     if constexpr (BF) {
         const int lim = t == c.nt - 1 ? c.rem : 64;
 #pragma unroll
-        for (int i = 0; i < Dq2Ctx<T, NW>::PIECES; ++i) {
+        for (int i = 0; i < X::PIECES; ++i) {
             const int piece = c.wave + NW * i;
             const bool ok = piece * 8 + (c.lane >> 3) < lim;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rs, LDS_PTR(c.smem + slot * 16384 + piece * 1024), 16,
@@ -1278,7 +1282,7 @@ __device__ __forceinline__ void dq2_issue(Dq2Ctx<T, NW>& c, int t, int slot) {
     const bool ragged = t == c.nt - 1 && c.rem < 64;  // wave-uniform
     if (__builtin_expect(ragged, 0)) {
 #pragma unroll
-        for (int i = 0; i < Dq2Ctx<T, NW>::PIECES; ++i) {
+        for (int i = 0; i < X::PIECES; ++i) {
             const int piece = c.wave + NW * i;
             const bool ok = piece * 8 + (c.lane >> 3) < c.rem;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rs, LDS_PTR(c.smem + slot * 16384 + piece * 1024), 16,
@@ -1289,7 +1293,7 @@ __device__ __forceinline__ void dq2_issue(Dq2Ctx<T, NW>& c, int t, int slot) {
         return;
     }
 #pragma unroll
-    for (int i = 0; i < Dq2Ctx<T, NW>::PIECES; ++i) {
+    for (int i = 0; i < X::PIECES; ++i) {
         const int piece = c.wave + NW * i;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rs, LDS_PTR(c.smem + slot * 16384 + piece * 1024), 16, c.voffK[i],
                                                  soff, 0, 0);
@@ -1299,9 +1303,11 @@ __device__ __forceinline__ void dq2_issue(Dq2Ctx<T, NW>& c, int t, int slot) {
 #endif
 }
 
-// S^T - L and dP^T - delta of the 32-key block `kb` of the tile image at Kt (V at Kt + 8 KiB)
-template <typename T, int NW>
-__device__ __forceinline__ void dq2_sdp(const Dq2Ctx<T, NW>& c, const char* Kt, int kb, f32x16& sacc, f32x16& pacc) {
+// S^T - L and dP^T - delta of the 32-key block `kb` of the tile image at Kt (V at Kt + 8 KiB), for
+// each of the wave's QR row blocks (the K / V fragments read once)
+template <typename T, int NW, int QR>
+__device__ __forceinline__ void dq2_sdp(const Dq2Ctx<T, NW, QR>& c, const char* Kt, int kb, f32x16 (&sacc)[QR],
+                                        f32x16 (&pacc)[QR]) {
     typedef typename Mfma<T>::frag frag;
     frag kf[4], vf[4];
 #pragma unroll
@@ -1309,18 +1315,42 @@ __device__ __forceinline__ void dq2_sdp(const Dq2Ctx<T, NW>& c, const char* Kt, 
         kf[s] = row_frag<T>(Kt, kb * 32 + c.l32, 2 * s + c.h);
         vf[s] = row_frag<T>(Kt + 8192, kb * 32 + c.l32, 2 * s + c.h);
     }
-    sacc = splat16(c.negL);
-    pacc = splat16(c.negD);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        sacc = Mfma<T>::mma(kf[s], c.qf[s], sacc);
-        pacc = Mfma<T>::mma(vf[s], c.gf[s], pacc);
+    for (int r = 0; r < QR; ++r) {
+        sacc[r] = splat16(c.negL[r]);
+        pacc[r] = splat16(c.negD[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < QR; ++r)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            sacc[r] = Mfma<T>::mma(kf[s], c.qf[r][s], sacc[r]);
+            pacc[r] = Mfma<T>::mma(vf[s], c.gf[r][s], pacc[r]);
+        }
+}
+
+// acc += x . b (32x32x16) with the accumulator in AGPRs (the QR = 2 pass: its dQ^T sums stay out of
+// the arch VGPRs the softmax works in); NOP: open with s_nop 1 for a B operand a VALU instruction
+// may have written right before (the compiler pads no hazard into an asm statement)
+template <typename T, bool NOP>
+__device__ __forceinline__ void dq_mfma_acc(f32x16& acc, const typename Mfma<T>::frag& x, const typename Mfma<T>::frag& b) {
+    if constexpr (std::is_same<T, bf16>::value) {
+        if constexpr (NOP)
+            asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(x), "v"(b));
+        else
+            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(x), "v"(b));
+    } else {
+        if constexpr (NOP)
+            asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(x), "v"(b));
+        else
+            asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(x), "v"(b));
     }
 }
 
-// dS^T of one unit (consumes sacc / pacc), then dQ^T[d][q] += K^T[d][key] dS^T[key][q]
-template <typename T, int NW>
-__device__ __forceinline__ void dq2_ds(Dq2Ctx<T, NW>& c, const char* Kt, int kb, f32x16& sacc, const f32x16& pacc) {
+// dS^T of one unit per row block (consumes sacc / pacc), then dQ^T[d][q] += K^T[d][key] dS^T[key][q]
+template <typename T, int NW, int QR>
+__device__ __forceinline__ void dq2_ds(Dq2Ctx<T, NW, QR>& c, const char* Kt, int kb, f32x16 (&sacc)[QR],
+                                       const f32x16 (&pacc)[QR]) {
     typedef typename Mfma<T>::frag frag;
     frag kt[2][2];
 #pragma unroll
@@ -1328,44 +1358,54 @@ __device__ __forceinline__ void dq2_ds(Dq2Ctx<T, NW>& c, const char* Kt, int kb,
 #pragma unroll
         for (int db = 0; db < 2; ++db) kt[s][db] = tr_frag<T>(Kt, kb, s, db, c.lane);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) sacc[r] = __builtin_amdgcn_exp2f(sacc[r]) * pacc[r];  // pacc: DsScale (dP - delta)
+    for (int r = 0; r < QR; ++r) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-        const frag sf = pack_frag<T>(sacc, s);
+        for (int e = 0; e < 16; ++e) sacc[r][e] = __builtin_amdgcn_exp2f(sacc[r][e]) * pacc[r][e];  // pacc: DsScale (dP - delta)
 #pragma unroll
-        for (int db = 0; db < 2; ++db) c.dq[db] = Mfma<T>::mma(kt[s][db], sf, c.dq[db]);
+        for (int s = 0; s < 2; ++s) {
+            const frag sf = pack_frag<T>(sacc[r], s);
+            if constexpr (QR == 1) {
+#pragma unroll
+                for (int db = 0; db < 2; ++db) c.dq[r][db] = Mfma<T>::mma(kt[s][db], sf, c.dq[r][db]);
+            } else {
+                dq_mfma_acc<T, true>(c.dq[r][0], kt[s][0], sf);
+                dq_mfma_acc<T, false>(c.dq[r][1], kt[s][1], sf);
+            }
+        }
     }
 }
 
 // tile t in slot Q = t % 4; on entry (sA, pA) = unit (t, 0), on exit (sA, pA) = unit (t+1, 0)
-template <typename T, int NW, int Q, bool BF = false>
-__device__ __forceinline__ void dq2_step(Dq2Ctx<T, NW>& c, int t, f32x16& sA, f32x16& pA, f32x16& sB, f32x16& pB) {
-    constexpr int PIECES = Dq2Ctx<T, NW>::PIECES;
+template <typename T, int NW, int Q, bool BF = false, int QR = 1>
+__device__ __forceinline__ void dq2_step(Dq2Ctx<T, NW, QR>& c, int t, f32x16 (&sA)[QR], f32x16 (&pA)[QR],
+                                         f32x16 (&sB)[QR], f32x16 (&pB)[QR]) {
+    constexpr int PIECES = Dq2Ctx<T, NW, QR>::PIECES;
     const char* Kt = c.smem + Q * 16384;
     const char* Kn = c.smem + ((Q + 1) & 3) * 16384;
     wait_vmcnt<2 * PIECES>();      // own pieces of tile t+1 landed (tile t+2 in flight)
     __builtin_amdgcn_s_barrier();  // everyone's; everyone done with step t-1 (slot (t+3) % 4 free)
-    dq2_issue<T, NW, BF>(c, t + 3 < c.nt ? t + 3 : c.nt - 1, (Q + 3) & 3);
-    dq2_sdp<T, NW>(c, Kt, 1, sB, pB);  // unit (t, 1) on the matrix pipe ...
-    dq2_ds<T, NW>(c, Kt, 0, sA, pA);   // ... beside dS / dQ of unit (t, 0)
-    dq2_sdp<T, NW>(c, Kn, 0, sA, pA);  // unit (t+1, 0) ...
-    dq2_ds<T, NW>(c, Kt, 1, sB, pB);   // ... beside unit (t, 1)
+    dq2_issue<T, NW, BF, QR>(c, t + 3 < c.nt ? t + 3 : c.nt - 1, (Q + 3) & 3);
+    dq2_sdp<T, NW, QR>(c, Kt, 1, sB, pB);  // unit (t, 1) on the matrix pipe ...
+    dq2_ds<T, NW, QR>(c, Kt, 0, sA, pA);   // ... beside dS / dQ of unit (t, 0)
+    dq2_sdp<T, NW, QR>(c, Kn, 0, sA, pA);  // unit (t+1, 0) ...
+    dq2_ds<T, NW, QR>(c, Kt, 1, sB, pB);   // ... beside unit (t, 1)
 }
 
-template <typename T, int NW, bool BF = false>
-__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq2_kernel(const T* __restrict__ qkv,
-                                                                       const T* __restrict__ o,
-                                                                       const T* __restrict__ dout,
-                                                                       const float* __restrict__ lse,
-                                                                       float* __restrict__ delta,
-                                                                       float* __restrict__ nstat,
-                                                                       T* __restrict__ dqkv, int N, int H,
-                                                                       float scale, float* __restrict__ r0ws) {
-    constexpr int QB = 32 * NW, PIECES = Dq2Ctx<T, NW>::PIECES;
+template <typename T, int NW, bool BF = false, int QR = 1>
+__global__ __launch_bounds__(64 * NW, QR == 1 ? 8 / NW : 1) void attn_bwd_dq2_kernel(const T* __restrict__ qkv,
+                                                                                   const T* __restrict__ o,
+                                                                                   const T* __restrict__ dout,
+                                                                                   const float* __restrict__ lse,
+                                                                                   float* __restrict__ delta,
+                                                                                   float* __restrict__ nstat,
+                                                                                   T* __restrict__ dqkv, int N, int H,
+                                                                                   float scale, float* __restrict__ r0ws) {
+    constexpr int WR = 32 * QR;  // query rows per wave
+    constexpr int QB = WR * NW, PIECES = Dq2Ctx<T, NW, QR>::PIECES;
     typedef typename Mfma<T>::frag frag;
     // the ring, then the CLS-row fold's per-query weights [dS_0 | P_0] (used when r0ws != null)
     __shared__ __attribute__((aligned(16))) char smem[4 * 16384 + 2 * QB * 4];
-    Dq2Ctx<T, NW> c;
+    Dq2Ctx<T, NW, QR> c;
     c.smem = smem;
     c.lane = threadIdx.x & 63;
     c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (scalar) for the DMA
@@ -1380,28 +1420,39 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq2_kernel(const T* 
     c.ldb = (uint32_t)(ld * sizeof(T));
     c.nt = (N - 1 + 63) / 64;
     c.rem = N - 1 - 64 * (c.nt - 1);
-    const int q = 1 + qblk * QB + c.wave * 32 + c.l32;
-    const bool qok = q < N;  // rows past N compute on row N - 1 and store nothing
-    const int qc = qok ? q : N - 1;
-    // register loads first (their waits must not queue behind the DMA)
+    int q[QR];
+    bool qok[QR];
+    float ds0[QR], p0[QR];
     const T* dOb = dout + (int64_t)b * N * C + hd * HD;
-    const T* Orow = o + ((int64_t)b * N + qc) * C + hd * HD;
-    frag of[4], k0[4], v0[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        c.qf[s] = *(const frag*)(Bb + (int64_t)qc * ld + hd * HD + (2 * s + c.h) * 8);
-        c.gf[s] = *(const frag*)(dOb + (int64_t)qc * C + (2 * s + c.h) * 8);
-        of[s] = *(const frag*)(Orow + (2 * s + c.h) * 8);
-        k0[s] = *(const frag*)(Bb + C + hd * HD + (2 * s + c.h) * 8);
-        v0[s] = *(const frag*)(Bb + 2 * C + hd * HD + (2 * s + c.h) * 8);
-    }
     typedef T t4 __attribute__((ext_vector_type(4)));
     t4 k0d[2][4];  // key 0 at this lane's dQ^T rows d = 32 db + 8 g + 4 h + e
 #pragma unroll
     for (int db = 0; db < 2; ++db)
 #pragma unroll
         for (int g = 0; g < 4; ++g) k0d[db][g] = *(const t4*)(Bb + C + hd * HD + db * 32 + 8 * g + 4 * c.h);
-    const float L = lse[(int64_t)bh * N + qc];
+    frag k0[4], v0[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        k0[s] = *(const frag*)(Bb + C + hd * HD + (2 * s + c.h) * 8);
+        v0[s] = *(const frag*)(Bb + 2 * C + hd * HD + (2 * s + c.h) * 8);
+    }
+    // register loads first (their waits must not queue behind the DMA)
+    frag of[QR][4];
+    float L[QR];
+#pragma unroll
+    for (int r = 0; r < QR; ++r) {
+        q[r] = 1 + qblk * QB + c.wave * WR + r * 32 + c.l32;
+        qok[r] = q[r] < N;  // rows past N compute on row N - 1 and store nothing
+        const int qc = qok[r] ? q[r] : N - 1;
+        const T* Orow = o + ((int64_t)b * N + qc) * C + hd * HD;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            c.qf[r][s] = *(const frag*)(Bb + (int64_t)qc * ld + hd * HD + (2 * s + c.h) * 8);
+            c.gf[r][s] = *(const frag*)(dOb + (int64_t)qc * C + (2 * s + c.h) * 8);
+            of[r][s] = *(const frag*)(Orow + (2 * s + c.h) * 8);
+        }
+        L[r] = lse[(int64_t)bh * N + qc];
+    }
 
     c.rs = make_rsrc(Bb, (uint32_t)N * c.ldb);
 #pragma unroll
@@ -1411,75 +1462,88 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq2_kernel(const T* 
         c.voffK[i] = base + (uint32_t)((C + hd * HD) * sizeof(T));
         c.voffV[i] = base + (uint32_t)((2 * C + hd * HD) * sizeof(T));
     }
-    dq2_issue<T, NW, BF>(c, 0, 0);
-    dq2_issue<T, NW, BF>(c, c.nt > 1 ? 1 : 0, 1);
-    dq2_issue<T, NW, BF>(c, c.nt > 2 ? 2 : c.nt - 1, 2);
+    dq2_issue<T, NW, BF, QR>(c, 0, 0);
+    dq2_issue<T, NW, BF, QR>(c, c.nt > 1 ? 1 : 0, 1);
+    dq2_issue<T, NW, BF, QR>(c, c.nt > 2 ? 2 : c.nt - 1, 2);
 
     // delta = rowsum(dO * O); key 0 (CLS) folded into dQ on the VALU:
     //   dS_0 = P_0 (dP_0 - delta), P_0 = exp2(q . k0 - L), dP_0 = dO . v0;  dQ^T[d] += dS_0 k0[d]
-    float dpart = 0.f, spart = 0.f, ppart = 0.f;
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
+    for (int r = 0; r < QR; ++r) {
+        float dpart = 0.f, spart = 0.f, ppart = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            dpart += (float)of[s][j] * (float)c.gf[s][j];
-            spart += (float)c.qf[s][j] * (float)k0[s][j];
-            ppart += (float)c.gf[s][j] * (float)v0[s][j];
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                dpart += (float)of[r][s][j] * (float)c.gf[r][s][j];
+                spart += (float)c.qf[r][s][j] * (float)k0[s][j];
+                ppart += (float)c.gf[r][s][j] * (float)v0[s][j];
+            }
+        const float dl = xhalf_sum(dpart);
+        if (c.h == 0 && qok[r]) {
+            delta[(int64_t)bh * N + q[r]] = dl;
+            // negated copies for the dK/dV pass, whose S / dP chains start from -L / -delta
+            nstat[(int64_t)bh * N + q[r]] = -L[r];
+            nstat[(int64_t)gridDim.x / nq * N + (int64_t)bh * N + q[r]] = -dl * DsScale<T>::v;
         }
-    const float dl = xhalf_sum(dpart);
-    if (c.h == 0 && qok) {
-        delta[(int64_t)bh * N + q] = dl;
-        // negated copies for the dK/dV pass, whose S / dP chains start from -L / -delta
-        nstat[(int64_t)bh * N + q] = -L;
-        nstat[(int64_t)gridDim.x / nq * N + (int64_t)bh * N + q] = -dl * DsScale<T>::v;
+        c.negL[r] = -L[r];
+        c.negD[r] = -dl * DsScale<T>::v;
+        p0[r] = __builtin_amdgcn_exp2f(xhalf_sum(spart) - L[r]);
+        ds0[r] = p0[r] * (xhalf_sum(ppart) - dl) * DsScale<T>::v;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) c.dq[r][db][4 * g + e] = ds0[r] * (float)k0d[db][g][e];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) frag_ds_scale<T>(c.gf[r][s]);  // dP chains now give DsScale dP
     }
-    c.negL = -L;
-    c.negD = -dl * DsScale<T>::v;
-    const float p0 = __builtin_amdgcn_exp2f(xhalf_sum(spart) - L);
-    const float ds0 = p0 * (xhalf_sum(ppart) - dl) * DsScale<T>::v;
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) c.dq[db][4 * g + e] = ds0 * (float)k0d[db][g][e];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) frag_ds_scale<T>(c.gf[s]);  // dP chains now give DsScale dP
     float* r0w = (float*)(smem + 4 * 16384);
     if (r0ws != nullptr && c.h == 0) {  // key 0's weights for the epilogue's dK_0 / dV_0 sums
-        r0w[c.wave * 32 + c.l32] = qok ? ds0 : 0.f;
-        r0w[QB + c.wave * 32 + c.l32] = qok ? p0 : 0.f;
+#pragma unroll
+        for (int r = 0; r < QR; ++r) {
+            r0w[c.wave * WR + r * 32 + c.l32] = qok[r] ? ds0[r] : 0.f;
+            r0w[QB + c.wave * WR + r * 32 + c.l32] = qok[r] ? p0[r] : 0.f;
+        }
     }
 
     wait_vmcnt<2 * PIECES>();  // tiles 0 and 1 landed (tile 2 in flight)
     __builtin_amdgcn_s_barrier();
-    f32x16 sA, pA, sB, pB;
-    dq2_sdp<T, NW>(c, smem, 0, sA, pA);
+    f32x16 sA[QR], pA[QR], sB[QR], pB[QR];
+    dq2_sdp<T, NW, QR>(c, smem, 0, sA, pA);
     // unrolled by four (ring slots are immediates), then up to three single steps for a ragged
     // tile count (a loop with an exit after every step spilled ~90 VGPRs to scratch)
     int t = 0;
     for (; t + 4 <= c.nt; t += 4) {
-        dq2_step<T, NW, 0, BF>(c, t, sA, pA, sB, pB);
-        dq2_step<T, NW, 1, BF>(c, t + 1, sA, pA, sB, pB);
-        dq2_step<T, NW, 2, BF>(c, t + 2, sA, pA, sB, pB);
-        dq2_step<T, NW, 3, BF>(c, t + 3, sA, pA, sB, pB);
+        dq2_step<T, NW, 0, BF, QR>(c, t, sA, pA, sB, pB);
+        dq2_step<T, NW, 1, BF, QR>(c, t + 1, sA, pA, sB, pB);
+        dq2_step<T, NW, 2, BF, QR>(c, t + 2, sA, pA, sB, pB);
+        dq2_step<T, NW, 3, BF, QR>(c, t + 3, sA, pA, sB, pB);
     }
-    if (t < c.nt) dq2_step<T, NW, 0, BF>(c, t++, sA, pA, sB, pB);
-    if (t < c.nt) dq2_step<T, NW, 1, BF>(c, t++, sA, pA, sB, pB);
-    if (t < c.nt) dq2_step<T, NW, 2, BF>(c, t++, sA, pA, sB, pB);
+    if (t < c.nt) dq2_step<T, NW, 0, BF, QR>(c, t++, sA, pA, sB, pB);
+    if (t < c.nt) dq2_step<T, NW, 1, BF, QR>(c, t++, sA, pA, sB, pB);
+    if (t < c.nt) dq2_step<T, NW, 2, BF, QR>(c, t++, sA, pA, sB, pB);
     wait_vmcnt<0>();
-    if (qok) store_row_t21<T>(dqkv + ((int64_t)b * N + q) * ld + hd * HD, c.dq, scale / DsScale<T>::v, c.h);
+    if constexpr (QR == 2)  // the last asm MFMAs' AGPR results: >= 18 wait states before anything reads them
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3"
+                     : "+a"(c.dq[0][0]), "+a"(c.dq[0][1]), "+a"(c.dq[1][0]), "+a"(c.dq[1][1]));
+#pragma unroll
+    for (int r = 0; r < QR; ++r)
+        if (qok[r]) store_row_t21<T>(dqkv + ((int64_t)b * N + q[r]) * ld + hd * HD, c.dq[r], scale / DsScale<T>::v, c.h);
     if (r0ws != nullptr) {
         // CLS-row fold: this block's share of key 0's sums, dK_0 += dS_0 q', dV_0 += P_0 dO (both
         // DsScale-scaled: dS_0 carries it, dO was scaled above), one partial per workgroup
         __syncthreads();  // every wave is done with the ring
-        char* img = smem + c.wave * 32 * 128;
-        r0_put<T>(img, c.qf, c.l32, c.h);
-        const float ak = r0_colsum<T, 32>(img, r0w + c.wave * 32, c.lane);
+        char* img = smem + c.wave * WR * 128;
+#pragma unroll
+        for (int r = 0; r < QR; ++r) r0_put<T>(img, c.qf[r], r * 32 + c.l32, c.h);
+        const float ak = r0_colsum<T, WR>(img, r0w + c.wave * WR, c.lane);
         asm volatile("" ::: "memory");
-        r0_put<T>(img, c.gf, c.l32, c.h);
-        const float av = r0_colsum<T, 32>(img, r0w + QB + c.wave * 32, c.lane);
-        float* part = (float*)(smem + NW * 32 * 128);
+#pragma unroll
+        for (int r = 0; r < QR; ++r) r0_put<T>(img, c.gf[r], r * 32 + c.l32, c.h);
+        const float av = r0_colsum<T, WR>(img, r0w + QB + c.wave * WR, c.lane);
+        float* part = (float*)(smem + NW * WR * 128);
         part[c.wave * 128 + c.lane] = ak;
         part[c.wave * 128 + 64 + c.lane] = av;
         if (qblk == 0 && c.wave == 0) {  // delta of query 0, for the dK/dV pass and the merge
@@ -2317,6 +2381,10 @@ bool bwd2_launch(const void* qkv, const void* o, const void* dout, const float* 
         if (dq4)
             attn_bwd_dq2_kernel<T, 4><<<B * H * nq, 256, 0, st>>>((const T*)qkv, (const T*)o, (const T*)dout, lse,
                                                                    delta, nstat, (T*)dqkv, N, H, scale, r0kv);
+        else if (dclip_option(DCLIP_OPT_ATTN_DQ_ROWS) == 64)  // 4 waves x 64 rows, one wave per SIMD
+            attn_bwd_dq2_kernel<T, 4, false, 2><<<B * H * nq, 256, 0, st>>>((const T*)qkv, (const T*)o,
+                                                                             (const T*)dout, lse, delta, nstat,
+                                                                             (T*)dqkv, N, H, scale, r0kv);
         else if (dclip_option(DCLIP_OPT_ATTN_DQ_ISSUE) == 1)
             attn_bwd_dq2_kernel<T, 8, true><<<B * H * nq, 512, 0, st>>>((const T*)qkv, (const T*)o, (const T*)dout,
                                                                          lse, delta, nstat, (T*)dqkv, N, H, scale, r0kv);

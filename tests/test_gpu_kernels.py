@@ -619,6 +619,35 @@ def test_attention_dkdv6_matches_dkdv5(B, H, N, dt, bwd_block):
         assert max(errs) < 4 * TOL[dt], errs
 
 
+@pytest.mark.parametrize("B,H,N", [(3, 2, 257), (2, 2, 290), (2, 3, 803), (1, 2, 8193)])
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+def test_attention_dq_rows64_matches_default(B, H, N, dt):
+    """The dQ pass with 64 query rows per wave (4 waves, one per SIMD, dQ^T in AGPRs;
+    DCLIP_OPT_ATTN_DQ_ROWS 64) against the default 32-row pass: every query's dQ is the same
+    products summed in the same order (bitwise equal); the CLS row's fold partials are summed over
+    other row groups (fp32 rounding only).  Ragged N - 1 and partial last blocks included."""
+    from denseclip_vit_multimodal_amd import _native as N_
+    O = ops()
+    C = 64 * H
+    torch.manual_seed(5)
+    qkv, _ = prescale((torch.randn(B * N, 3 * C, device=DEV) * 1.5).to(dt), H)
+    dout = torch.randn(B * N, C, device=DEV).to(dt)
+    o, lse = O.attn_fwd(qkv, B, N, H, 64 ** -0.5)
+    res = []
+    try:
+        for v in (0, 64):
+            N_.call("dclip_set_option", N_.OPT_ATTN_DQ_ROWS, v)
+            res.append(O.attn_bwd(qkv, o, dout, lse, B, N, H, 64 ** -0.5).float())
+    finally:
+        N_.call("dclip_set_option", N_.OPT_ATTN_DQ_ROWS, 0)
+    a, b = res
+    assert torch.isfinite(b).all()
+    rest = torch.ones(B * N, dtype=torch.bool, device=DEV)
+    rest[::N] = False
+    assert torch.equal(b[rest], a[rest])
+    assert rel_err(b[~rest], a[~rest]) < 1e-5, rel_err(b[~rest], a[~rest])
+
+
 def test_attention_bwd_full_length():
     """N = 8193 (the benchmark's sequence) through the CLS-split passes, against fp32 autograd."""
     errs = _attn_bwd_check(1, 1, 8193, torch.bfloat16)
