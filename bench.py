@@ -467,13 +467,14 @@ def main():
                 cpu0 = {"value": None, "error": repr(e)[:300]}
 
     if rank == 0:
-        # N >= 257 runs the CLS-split attention kernels (attention.hip bwd2_launch / fwd2, a ragged
-        # N - 1 included); the fp8 forward splits CLS for N = 1 + 256k only
+        # N >= 257 runs the CLS-split attention kernels (attention.hip bwd2_launch / fwd3 when N - 1 is a
+        # multiple of 256, else fwd2 with a ragged N - 1); the fp8 forward splits CLS for N = 1 + 256k only
         cls_split = N >= 257
         fp8_split = N >= 257 and (N - 1) % 256 == 0
         rf_fwd = {"kernel": ("attn_fp8mx_kernel (+ pack%s)" % (" / row-0 pass" if fp8_split else "")
                              if args.attn_fp8 else
-                             "attn_fwd2_kernel (+ row-0 pass)" if cls_split else "attn_fwd_kernel"),
+                             ("attn_fwd3_kernel (+ row-0 pass)" if (N - 1) % 256 == 0 else
+                              "attn_fwd2_kernel (+ row-0 pass)") if cls_split else "attn_fwd_kernel"),
                   "bound": "mfma",
                   "achieved": round(achieved, 2) if achieved else None, "peak": peak_attn,
                   "unit": "TFLOP/s", "frac": round(achieved / peak_attn, 4) if achieved else None,

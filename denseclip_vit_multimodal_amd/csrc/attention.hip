@@ -2348,8 +2348,10 @@ void fwd_launch(const void* qkv, void* o, float* lse, int B, int N, int H, hipSt
     const int nw = dclip_option(DCLIP_OPT_ATTN_FWD_WAVES) == 4 ? 4 : 8;
     const int kopt = dclip_option(DCLIP_OPT_ATTN_FWD_KERNEL);
     if (kopt == 2 && fwd3_launch<T, 4, 2>(qkv, o, lse, B, N, H, st)) return;
-    if (kopt == 3 && fwd3_launch<T, 8, 1>(qkv, o, lse, B, N, H, st)) return;
-    if (kopt != 1) {  // 0: CLS-split when the shape allows it
+    // default since round 4 (N - 1 a multiple of 256, 8 waves): the pipelined CLS-split kernel,
+    // bitwise equal to attn_fwd2_kernel and 1.8-2.2 % faster per launch (profiles/r04/r05w_*)
+    if ((kopt == 0 || kopt == 3) && nw == 8 && fwd3_launch<T, 8, 1>(qkv, o, lse, B, N, H, st)) return;
+    if (kopt != 1) {  // 0 / 4: CLS-split when the shape allows it (4: attn_fwd2_kernel always)
         if (nw == 4 ? fwd2_launch_nw<T, 4>(qkv, o, lse, B, N, H, st) : fwd2_launch_nw<T, 8>(qkv, o, lse, B, N, H, st))
             return;
     }

@@ -77,7 +77,7 @@ int dclip_abi_version(void);
 #define DCLIP_OPT_GEMM_TN_TILE 4     /* dclip_gemm_tn tiles: 0 auto (default: 256x256 when M, N >= 256), 1 128x128, 2 256x256 with 32-row K-steps in a 4-deep ring, 3 the same 5-deep, 4 256x256 on 4 waves of 128x128 */
 #define DCLIP_OPT_ATTN_DKDV_QS 5     /* dK/dV pass query rows per barrier: 64 (default) or 128 */
 #define DCLIP_OPT_ATTN_BWD_KERNEL 7  /* 0 (default): CLS-split passes for N >= 257 (a ragged N-1 with the default pass variants only); 1: generic */
-#define DCLIP_OPT_ATTN_FWD_KERNEL 6  /* 0 (default): CLS-split kernel for N - 1 >= the query block (ragged N-1 included); 1: generic */
+#define DCLIP_OPT_ATTN_FWD_KERNEL 6  /* 0 (default): CLS-split kernels (the pipelined attn_fwd3 when N - 1 is a multiple of 256, else attn_fwd2, ragged N-1 included); 1: generic; 2: attn_fwd3 4 waves x 64 rows; 3: attn_fwd3 8 waves; 4: attn_fwd2 always */
 #define DCLIP_OPT_ATTN_BWD_BLOCK 8   /* CLS-split dK/dV pass: 0 (default) / 6: 64 keys per wave, AGPR dK / dV (attention_dkdv6.hip); 5: software-pipelined 32 keys per wave; 1: the unpipelined one */
 #define DCLIP_OPT_GEMM_TN_COLSUM 9   /* 0 (default): the 256x256 weight-gradient kernel sums dY's columns (bias gradient) itself; 1: a separate pass */
 #define DCLIP_OPT_GEMM_EPI 10      /* persistent NT GEMM epilogue: 0 (default) row-major through LDS, whole 128-B lines per store; 1 the accumulator-layout stores (16 rows x 64 B) */

@@ -20,6 +20,7 @@ ap.add_argument("--n", type=int, default=8193)
 ap.add_argument("--b", type=int, default=8)
 ap.add_argument("--h", type=int, default=12)
 ap.add_argument("--rounds", type=int, default=7)
+ap.add_argument("--fwd", action="store_true", help="time the forward instead of the backward")
 a = ap.parse_args()
 B, NT, H = a.b, a.n, a.h
 C = 64 * H
@@ -43,6 +44,10 @@ def bwd():
                             dqkv.data_ptr(), B, NT, H, 64, 0.125, st) == 0
 
 
+def fwd():
+    assert L.dclip_attn_fwd(code, qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), B, NT, H, 64, 0.125, st) == 0
+
+
 def ev(fn, reps=3):
     fn()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -57,6 +62,12 @@ def ev(fn, reps=3):
 outs = []
 for v in a.values:
     L.dclip_set_option(a.opt, v)
+    if a.fwd:
+        o.zero_()
+        fwd()
+        torch.cuda.synchronize()
+        outs.append(o.clone())
+        continue
     dqkv.zero_()
     bwd()
     torch.cuda.synchronize()
@@ -70,10 +81,10 @@ t = {v: [] for v in a.values}
 for r in range(a.rounds):
     for v in a.values:
         L.dclip_set_option(a.opt, v)
-        t[v].append(ev(bwd))
+        t[v].append(ev(fwd if a.fwd else bwd))
 L.dclip_set_option(a.opt, 0)
-fl = 10.0 * B * H * NT * NT * 64
+fl = (4.0 if a.fwd else 10.0) * B * H * NT * NT * 64
 for v in a.values:
     s = sorted(t[v])
-    print(f"opt {a.opt}={v}: bwd med {s[len(s) // 2]:.3f} min {s[0]:.3f} ms  ({fl / (s[len(s) // 2] * 1e-3) / 1e12:.0f} "
+    print(f"opt {a.opt}={v}: {'fwd' if a.fwd else 'bwd'} med {s[len(s) // 2]:.3f} min {s[0]:.3f} ms  ({fl / (s[len(s) // 2] * 1e-3) / 1e12:.0f} "
           f"TFLOP/s useful)", flush=True)

@@ -2,6 +2,7 @@
 bf16 images unless --fp16) in ONE process: the arms alternate over rounds on the same model.
 
   python tools/ab_flag.py ops.EAGER_WEIGHT_REFRESH True False [--rounds 3] [--steps 10] [--fp16]
+  python tools/ab_flag.py opt:6 0 3      (a libdclip kernel-variant option, dclip_set_option)
 """
 import argparse
 import importlib
@@ -25,9 +26,19 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--fp16", action="store_true")
     a = ap.parse_args()
-    modname, attr = a.flag.rsplit(".", 1)
-    mod = importlib.import_module("denseclip_vit_multimodal_amd." + modname)
     vals = [eval(v) for v in a.values]  # noqa: S307 (literals from the command line)
+    if a.flag.startswith("opt:"):
+        from denseclip_vit_multimodal_amd import _native
+        oid = int(a.flag[4:])
+
+        def setv(v):
+            _native.call("dclip_set_option", oid, int(v))
+    else:
+        modname, attr = a.flag.rsplit(".", 1)
+        mod = importlib.import_module("denseclip_vit_multimodal_amd." + modname)
+
+        def setv(v):
+            setattr(mod, attr, v)
     from denseclip_vit_multimodal_amd.losses import SILogLoss
     from denseclip_vit_multimodal_amd.train import synth_batch, make_optimizer
     dev = torch.device("cuda", 0)
@@ -41,7 +52,7 @@ def main():
     res = {repr(v): [] for v in vals}
     for r in range(a.rounds):
         for v in vals:
-            setattr(mod, attr, v)
+            setv(v)
             bench.run_steps(model, opt, batch, 3, silog)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
