@@ -1375,6 +1375,68 @@ __device__ __forceinline__ void dq2_ds(Dq2Ctx<T, NW, QR>& c, const char* Kt, int
     }
 }
 
+// the deferred form (DCLIP_OPT_ATTN_DQ_DEFER 1): a unit's softmax VALU packs dS^T and reads its K^T
+// fragments, and its dQ MFMAs run half a step later beside the next unit's S / dP chains, so no
+// MFMA of a half-step waits on that half-step's VALU (the forward's attn_fwd3 pipelining)
+template <typename T, int QR>
+__device__ __forceinline__ void dq2_soft(f32x16 (&sacc)[QR], const f32x16 (&pacc)[QR],
+                                         typename Mfma<T>::frag (&sf)[QR][2]) {
+#pragma unroll
+    for (int r = 0; r < QR; ++r) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) sacc[r][e] = __builtin_amdgcn_exp2f(sacc[r][e]) * pacc[r][e];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) sf[r][s] = pack_frag<T>(sacc[r], s);
+    }
+}
+
+template <typename T, int NW, int QR>
+__device__ __forceinline__ void dq2_kt(const Dq2Ctx<T, NW, QR>& c, const char* Kt, int kb,
+                                       typename Mfma<T>::frag (&kt)[2][2]) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int db = 0; db < 2; ++db) kt[s][db] = tr_frag<T>(Kt, kb, s, db, c.lane);
+}
+
+template <typename T, int NW, int QR>
+__device__ __forceinline__ void dq2_dqmma(Dq2Ctx<T, NW, QR>& c, const typename Mfma<T>::frag (&kt)[2][2],
+                                          const typename Mfma<T>::frag (&sf)[QR][2]) {
+#pragma unroll
+    for (int r = 0; r < QR; ++r)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int db = 0; db < 2; ++db) c.dq[r][db] = Mfma<T>::mma(kt[s][db], sf[r][s], c.dq[r][db]);
+}
+
+// deferred step, tile t in slot Q: on entry (sA, pA) = unit (t, 0) and (sfP, ktP) = the packed
+// dS^T / K^T of unit (t-1, 1) (its dQ MFMAs not yet issued); on exit the same one unit later.
+// Slot (t+3) % 4, which this step's issue overwrites, held tile t-1, whose K^T fragments ktP
+// already sit in registers.
+template <typename T, int NW, int Q, bool BF, int QR>
+__device__ __forceinline__ void dq2_step_deferred(Dq2Ctx<T, NW, QR>& c, int t, f32x16 (&sA)[QR], f32x16 (&pA)[QR],
+                                                  f32x16 (&sB)[QR], f32x16 (&pB)[QR],
+                                                  typename Mfma<T>::frag (&sfP)[QR][2],
+                                                  typename Mfma<T>::frag (&ktP)[2][2]) {
+    typedef typename Mfma<T>::frag frag;
+    constexpr int PIECES = Dq2Ctx<T, NW, QR>::PIECES;
+    const char* Kt = c.smem + Q * 16384;
+    const char* Kn = c.smem + ((Q + 1) & 3) * 16384;
+    wait_vmcnt<2 * PIECES>();
+    __builtin_amdgcn_s_barrier();
+    dq2_issue<T, NW, BF, QR>(c, t + 3 < c.nt ? t + 3 : c.nt - 1, (Q + 3) & 3);
+    frag sfA[QR][2], ktA[2][2];
+    dq2_sdp<T, NW, QR>(c, Kt, 1, sB, pB);  // C(t, 1)
+    dq2_dqmma<T, NW, QR>(c, ktP, sfP);     // D(t-1, 1)
+    dq2_soft<T, QR>(sA, pA, sfA);          // V(t, 0)
+    dq2_kt<T, NW, QR>(c, Kt, 0, ktA);
+    dq2_sdp<T, NW, QR>(c, Kn, 0, sA, pA);  // C(t+1, 0)
+    dq2_dqmma<T, NW, QR>(c, ktA, sfA);     // D(t, 0)
+    dq2_soft<T, QR>(sB, pB, sfP);          // V(t, 1): its D runs next step
+    dq2_kt<T, NW, QR>(c, Kt, 1, ktP);
+}
+
 // tile t in slot Q = t % 4; on entry (sA, pA) = unit (t, 0), on exit (sA, pA) = unit (t+1, 0)
 template <typename T, int NW, int Q, bool BF = false, int QR = 1>
 __device__ __forceinline__ void dq2_step(Dq2Ctx<T, NW, QR>& c, int t, f32x16 (&sA)[QR], f32x16 (&pA)[QR],
@@ -1391,7 +1453,7 @@ __device__ __forceinline__ void dq2_step(Dq2Ctx<T, NW, QR>& c, int t, f32x16 (&s
     dq2_ds<T, NW, QR>(c, Kt, 1, sB, pB);   // ... beside unit (t, 1)
 }
 
-template <typename T, int NW, bool BF = false, int QR = 1>
+template <typename T, int NW, bool BF = false, int QR = 1, bool DEFER = false>
 __global__ __launch_bounds__(64 * NW, QR == 1 ? 8 / NW : 1) void attn_bwd_dq2_kernel(const T* __restrict__ qkv,
                                                                                    const T* __restrict__ o,
                                                                                    const T* __restrict__ dout,
@@ -1515,15 +1577,41 @@ __global__ __launch_bounds__(64 * NW, QR == 1 ? 8 / NW : 1) void attn_bwd_dq2_ke
     // unrolled by four (ring slots are immediates), then up to three single steps for a ragged
     // tile count (a loop with an exit after every step spilled ~90 VGPRs to scratch)
     int t = 0;
-    for (; t + 4 <= c.nt; t += 4) {
-        dq2_step<T, NW, 0, BF, QR>(c, t, sA, pA, sB, pB);
-        dq2_step<T, NW, 1, BF, QR>(c, t + 1, sA, pA, sB, pB);
-        dq2_step<T, NW, 2, BF, QR>(c, t + 2, sA, pA, sB, pB);
-        dq2_step<T, NW, 3, BF, QR>(c, t + 3, sA, pA, sB, pB);
+    if constexpr (DEFER) {
+        frag sfP[QR][2], ktP[2][2];  // no unit before (0, 0): zero operands add nothing
+#pragma unroll
+        for (int r = 0; r < QR; ++r)
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) sfP[r][s][j] = (T)0.f;
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int db = 0; db < 2; ++db)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) ktP[s][db][j] = (T)0.f;
+        for (; t + 4 <= c.nt; t += 4) {
+            dq2_step_deferred<T, NW, 0, BF, QR>(c, t, sA, pA, sB, pB, sfP, ktP);
+            dq2_step_deferred<T, NW, 1, BF, QR>(c, t + 1, sA, pA, sB, pB, sfP, ktP);
+            dq2_step_deferred<T, NW, 2, BF, QR>(c, t + 2, sA, pA, sB, pB, sfP, ktP);
+            dq2_step_deferred<T, NW, 3, BF, QR>(c, t + 3, sA, pA, sB, pB, sfP, ktP);
+        }
+        if (t < c.nt) dq2_step_deferred<T, NW, 0, BF, QR>(c, t++, sA, pA, sB, pB, sfP, ktP);
+        if (t < c.nt) dq2_step_deferred<T, NW, 1, BF, QR>(c, t++, sA, pA, sB, pB, sfP, ktP);
+        if (t < c.nt) dq2_step_deferred<T, NW, 2, BF, QR>(c, t++, sA, pA, sB, pB, sfP, ktP);
+        dq2_dqmma<T, NW, QR>(c, ktP, sfP);  // the last unit's D
+    } else {
+        for (; t + 4 <= c.nt; t += 4) {
+            dq2_step<T, NW, 0, BF, QR>(c, t, sA, pA, sB, pB);
+            dq2_step<T, NW, 1, BF, QR>(c, t + 1, sA, pA, sB, pB);
+            dq2_step<T, NW, 2, BF, QR>(c, t + 2, sA, pA, sB, pB);
+            dq2_step<T, NW, 3, BF, QR>(c, t + 3, sA, pA, sB, pB);
+        }
+        if (t < c.nt) dq2_step<T, NW, 0, BF, QR>(c, t++, sA, pA, sB, pB);
+        if (t < c.nt) dq2_step<T, NW, 1, BF, QR>(c, t++, sA, pA, sB, pB);
+        if (t < c.nt) dq2_step<T, NW, 2, BF, QR>(c, t++, sA, pA, sB, pB);
     }
-    if (t < c.nt) dq2_step<T, NW, 0, BF, QR>(c, t++, sA, pA, sB, pB);
-    if (t < c.nt) dq2_step<T, NW, 1, BF, QR>(c, t++, sA, pA, sB, pB);
-    if (t < c.nt) dq2_step<T, NW, 2, BF, QR>(c, t++, sA, pA, sB, pB);
     wait_vmcnt<0>();
     if constexpr (QR == 2)  // the last asm MFMAs' AGPR results: >= 18 wait states before anything reads them
         asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3"
@@ -2383,6 +2471,10 @@ bool bwd2_launch(const void* qkv, const void* o, const void* dout, const float* 
         if (dq4)
             attn_bwd_dq2_kernel<T, 4><<<B * H * nq, 256, 0, st>>>((const T*)qkv, (const T*)o, (const T*)dout, lse,
                                                                    delta, nstat, (T*)dqkv, N, H, scale, r0kv);
+        else if (dclip_option(DCLIP_OPT_ATTN_DQ_DEFER) == 1)  // dQ MFMAs half a step behind their softmax
+            attn_bwd_dq2_kernel<T, 8, false, 1, true><<<B * H * nq, 512, 0, st>>>((const T*)qkv, (const T*)o,
+                                                                                   (const T*)dout, lse, delta, nstat,
+                                                                                   (T*)dqkv, N, H, scale, r0kv);
         else if (dclip_option(DCLIP_OPT_ATTN_DQ_ROWS) == 64)  // 4 waves x 64 rows, one wave per SIMD
             attn_bwd_dq2_kernel<T, 4, false, 2><<<B * H * nq, 256, 0, st>>>((const T*)qkv, (const T*)o,
                                                                              (const T*)dout, lse, delta, nstat,

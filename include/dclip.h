@@ -85,7 +85,8 @@ int dclip_abi_version(void);
 #define DCLIP_OPT_ATTN_FP8_QK 12   /* dclip_attn_fwd_fp8: 0 (default) S = QK^T on the 16-bit MFMA, P V on the fp8 one; 1 both on fp8 (the round-3 kernel) */
 #define DCLIP_OPT_ATTN_DQ_ISSUE 13  /* CLS-split dQ pass LDS-DMA issue: 0 (default) a ragged-tile branch; 1 branch-free per-lane select */
 #define DCLIP_OPT_ATTN_DQ_ROWS 14   /* CLS-split dQ pass query rows per wave: 32 (default; 8 waves, two per SIMD) or 64 (4 waves, one per SIMD) */
-#define DCLIP_OPT_COUNT 15
+#define DCLIP_OPT_ATTN_DQ_DEFER 15  /* CLS-split dQ pass: 0 (default) a unit's dQ MFMAs right after its softmax; 1 half a step later, beside the next unit's S / dP chains */
+#define DCLIP_OPT_COUNT 16
 int dclip_set_option(int id, int value);
 
 /* LayerNorm over the last dim (cols), eps, affine w/b (fp32).  y = (x-mu)*rstd*w+b.

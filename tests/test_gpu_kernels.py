@@ -619,14 +619,17 @@ def test_attention_dkdv6_matches_dkdv5(B, H, N, dt, bwd_block):
         assert max(errs) < 4 * TOL[dt], errs
 
 
+@pytest.mark.parametrize("variant", ["rows64", "defer"])
 @pytest.mark.parametrize("B,H,N", [(3, 2, 257), (2, 2, 290), (2, 3, 803), (1, 2, 8193)])
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
-def test_attention_dq_rows64_matches_default(B, H, N, dt):
-    """The dQ pass with 64 query rows per wave (4 waves, one per SIMD, dQ^T in AGPRs;
-    DCLIP_OPT_ATTN_DQ_ROWS 64) against the default 32-row pass: every query's dQ is the same
-    products summed in the same order (bitwise equal); the CLS row's fold partials are summed over
-    other row groups (fp32 rounding only).  Ragged N - 1 and partial last blocks included."""
+def test_attention_dq_variants_match_default(B, H, N, dt, variant):
+    """dQ pass variants against the default: 64 query rows per wave (4 waves, one per SIMD, dQ^T in
+    AGPRs; DCLIP_OPT_ATTN_DQ_ROWS 64) and the dQ MFMAs deferred half a step (DCLIP_OPT_ATTN_DQ_DEFER
+    1).  Every query's dQ is the same products summed in the same order (bitwise equal); the CLS
+    row's fold partials may be summed over other row groups (fp32 rounding only).  Ragged N - 1 and
+    partial last blocks included."""
     from denseclip_vit_multimodal_amd import _native as N_
+    opt, val = {"rows64": (N_.OPT_ATTN_DQ_ROWS, 64), "defer": (N_.OPT_ATTN_DQ_DEFER, 1)}[variant]
     O = ops()
     C = 64 * H
     torch.manual_seed(5)
@@ -635,11 +638,11 @@ def test_attention_dq_rows64_matches_default(B, H, N, dt):
     o, lse = O.attn_fwd(qkv, B, N, H, 64 ** -0.5)
     res = []
     try:
-        for v in (0, 64):
-            N_.call("dclip_set_option", N_.OPT_ATTN_DQ_ROWS, v)
+        for v in (0, val):
+            N_.call("dclip_set_option", opt, v)
             res.append(O.attn_bwd(qkv, o, dout, lse, B, N, H, 64 ** -0.5).float())
     finally:
-        N_.call("dclip_set_option", N_.OPT_ATTN_DQ_ROWS, 0)
+        N_.call("dclip_set_option", opt, 0)
     a, b = res
     assert torch.isfinite(b).all()
     rest = torch.ones(B * N, dtype=torch.bool, device=DEV)
