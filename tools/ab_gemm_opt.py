@@ -1,4 +1,4 @@
-"""A/B the NT GEMM tile variants (DCLIP_OPT_GEMM_TILE values) in ONE process on the ViT-B/16
+"""A/B the NT GEMM tile variants (DCLIP_OPT_GEMM_TILE values, or --opt=ID) in ONE process on the ViT-B/16
 block's seven NT shapes at the headline batch (65544 token rows), interleaved rounds, with the
 epilogues the block uses; every variant is checked against the first (max |difference|).
 
@@ -13,7 +13,12 @@ import torch  # noqa: E402
 from denseclip_vit_multimodal_amd import _native as N  # noqa: E402
 from denseclip_vit_multimodal_amd import ops  # noqa: E402
 
-vals = [int(v) for v in sys.argv[1:]] or [0, 7]
+args = sys.argv[1:]
+OPT = N.OPT_GEMM_TILE
+if args and args[0].startswith("--opt="):  # another option id, e.g. --opt=16 (DCLIP_OPT_GEMM_NT)
+    OPT = int(args[0][6:])
+    args = args[1:]
+vals = [int(v) for v in args] or [0, 7]
 M = 8 * 8193
 bf = torch.bfloat16
 torch.manual_seed(0)
@@ -57,13 +62,13 @@ for name, (n, k, epi) in shapes.items():
            torch.randn(M, n, device="cuda").to(bf) if epi == N.EPI_GELU_BWD else None)
     outs = []
     for v in vals:
-        N.call("dclip_set_option", N.OPT_GEMM_TILE, v)
+        N.call("dclip_set_option", OPT, v)
         outs.append(call(n, k, epi, A, B, bias, aux).float())
     msg = ", ".join(f"tile {v} max|d| {float((o - outs[0]).abs().max()):.2e}" for v, o in zip(vals[1:], outs[1:]))
     t = {v: [] for v in vals}
     for r in range(5):
         for v in vals:
-            N.call("dclip_set_option", N.OPT_GEMM_TILE, v)
+            N.call("dclip_set_option", OPT, v)
             t[v].append(ev(lambda: call(n, k, epi, A, B, bias, aux)))
     fl = 2.0 * M * n * k
     med = {v: sorted(t[v])[2] for v in vals}
@@ -71,5 +76,5 @@ for name, (n, k, epi) in shapes.items():
         tot[v] += med[v]
     print(f"{name:11s} " + "  ".join(f"tile {v}: {med[v]:.3f} ms {fl / med[v] / 1e9:5.0f} TF/s" for v in vals) + "  | " + msg,
           flush=True)
-N.call("dclip_set_option", N.OPT_GEMM_TILE, 0)
+N.call("dclip_set_option", OPT, 0)
 print("total " + "  ".join(f"tile {v}: {tot[v]:.3f} ms" for v in vals))
