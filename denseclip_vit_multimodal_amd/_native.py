@@ -53,6 +53,8 @@ _SIGS = {
     "dclip_row_mean": [_c_void_p, _i32, _i64, _i64, _i64, _i32, _i64, _i32, _c_void_p, _c_void_p, _c_void_p],
     "dclip_score_map": [_c_void_p, _i32, _i64, _i64, _i64, _c_void_p, _c_void_p, _i32, _i32, _i32, _i32, _f32,
                         _c_void_p],
+    "dclip_score_concat": [_c_void_p, _i32, _i64, _i64, _i64, _i32, _c_void_p, _i32, _i32, _i32, _c_void_p, _i32, _i32,
+                           _i32, _c_void_p],
     "dclip_bilinear_fwd": [_c_void_p, _i32, _c_void_p, _i32, _i64, _i32, _i32, _i32, _i32, _c_void_p],
     "dclip_bilinear_bwd": [_c_void_p, _i32, _c_void_p, _c_void_p, _i64, _i32, _i32, _i32, _i32, _c_void_p],
     "dclip_cast": [_c_void_p, _i32, _c_void_p, _i32, _i64, _f32, _c_void_p, _c_void_p],

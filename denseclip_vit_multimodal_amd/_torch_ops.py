@@ -168,6 +168,10 @@ def _register_fakes():
     def _(v, bstride, row_off, ld, text, B, HW, eps):
         return _e(B, text.shape[1], HW, like=v, dtype=f32)
 
+    @reg("dclip::score_concat")
+    def _(rows, bstride, row_off, ld, C, score, B, h, w):
+        return _e(B * h * w, C + score.shape[1], like=rows)
+
     @reg("dclip::bilinear")
     def _(x, Ho, Wo, dtype):
         return _e(x.shape[0], x.shape[1], Ho, Wo, like=x, dtype=dtype)

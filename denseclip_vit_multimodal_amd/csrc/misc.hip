@@ -821,6 +821,57 @@ extern "C" int dclip_score_map(const void* v, int v_dt, int64_t bstride, int64_t
     return 0;
 }
 
+// ---------------------------------------------------------------------------- score concat
+// torch.cat([x_i, F.interpolate(score, x_i's size, bilinear).to(x_i.dtype)], dim=1) of the
+// score_concat_index branch (denseclip.py:684-694) in ONE pass: every output pixel row (channels
+// last, C + K wide) gets the read-out map's C channels copied from its strided token row and the K
+// score channels interpolated with bilinear_fwd_kernel's arithmetic (bitwise the same values) —
+// no resized score map and no separate concatenation copy in HBM.  One wave per pixel row.
+template <typename T>
+__global__ __launch_bounds__(256) void score_concat_kernel(const T* __restrict__ rows, int64_t bstride, int64_t row_off,
+                                                           int64_t ld, int C, const float* __restrict__ score, int K,
+                                                           int hs, int ws, T* __restrict__ out, int B, int h, int w) {
+    const int64_t npix = (int64_t)B * h * w;
+    const int CK = C + K;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int64_t p = (int64_t)blockIdx.x * 4 + wave; p < npix; p += (int64_t)gridDim.x * 4) {
+        const int64_t b = p / ((int64_t)h * w);
+        const int rem = (int)(p - b * h * w);
+        const int y = rem / w, x = rem - y * w;
+        const T* src = rows + b * bstride + (row_off + rem) * ld;
+        T* dst = out + p * CK;
+        for (int c = lane; c < C; c += 64) dst[c] = src[c];
+        if (lane < K) {
+            const Lerp ly = lerp_index(y, hs, h), lx = lerp_index(x, ws, w);
+            const float* pl = score + ((int64_t)b * K + lane) * hs * ws;
+            const float* p0 = pl + (int64_t)ly.i0 * ws;
+            const float* p1 = pl + (int64_t)ly.i1 * ws;
+            const float v = ly.l0 * (lx.l0 * p0[lx.i0] + lx.l1 * p0[lx.i1]) + ly.l1 * (lx.l0 * p1[lx.i0] + lx.l1 * p1[lx.i1]);
+            dst[C + lane] = (T)v;
+        }
+    }
+}
+
+extern "C" int dclip_score_concat(const void* rows, int dt, int64_t bstride, int64_t row_off, int64_t ld, int C,
+                                  const float* score, int K, int hs, int ws, void* out, int B, int h, int w,
+                                  void* stream) {
+    DCLIP_HOST_CHECK(rows && score && out && B > 0 && h > 0 && w > 0 && C > 0 && hs > 0 && ws > 0,
+                     "dclip_score_concat: bad arguments");
+    DCLIP_HOST_CHECK(K > 0 && K <= 64, "dclip_score_concat: 1 <= K <= 64 score channels (one lane each)");
+    DCLIP_HOST_CHECK(dt == DCLIP_BF16 || dt == DCLIP_F16, "dclip_score_concat: 16-bit maps");
+    const int64_t npix = (int64_t)B * h * w;
+    const int blocks = (int)((npix + 3) / 4 > 8192 ? 8192 : (npix + 3) / 4);
+    hipStream_t st = (hipStream_t)stream;
+    if (dt == DCLIP_BF16)
+        score_concat_kernel<bf16><<<blocks, 256, 0, st>>>((const bf16*)rows, bstride, row_off, ld, C, score, K, hs, ws,
+                                                          (bf16*)out, B, h, w);
+    else
+        score_concat_kernel<f16><<<blocks, 256, 0, st>>>((const f16*)rows, bstride, row_off, ld, C, score, K, hs, ws,
+                                                         (f16*)out, B, h, w);
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
+
 extern "C" int dclip_bilinear_fwd(const void* in, int in_dt, void* out, int out_dt, int64_t NC, int Hi, int Wi, int Ho,
                                   int Wo, void* stream) {
     DCLIP_HOST_CHECK(Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0, "dclip_bilinear_fwd: bad sizes");

@@ -527,6 +527,23 @@ Tensor score_map(const Tensor& v, int64_t bstride, int64_t row_off, int64_t ld, 
     return out;
 }
 
+// (B*h*w, C+K) channels-last rows: the C strided pixel-row channels of a read-out map, then the K
+// channels of the f32 score (B, K, hs, ws) bilinearly resized to (h, w)
+Tensor score_concat(const Tensor& rows, int64_t bstride, int64_t row_off, int64_t ld, int64_t C, const Tensor& score,
+                    int64_t B, int64_t h, int64_t w) {
+    check_gpu(score, "score");
+    TORCH_CHECK(score.scalar_type() == at::kFloat && score.dim() == 4 && score.size(0) == B,
+                "score_concat: score (B, K, hs, ws) fp32");
+    check_rows(rows, bstride, row_off, ld, B, h * w, C);
+    c10::DeviceGuard g(rows.device());
+    const int64_t K = score.size(1);
+    Tensor out = at::empty({B * h * w, C + K}, rows.options());
+    DCLIP_CALL(dclip_score_concat(rows.data_ptr(), dt_code(rows.scalar_type()), bstride, row_off, ld, (int)C,
+                                  ptr<float>(score), (int)K, (int)score.size(2), (int)score.size(3), out.data_ptr(),
+                                  (int)B, (int)h, (int)w, stream_of(rows)));
+    return out;
+}
+
 Tensor bilinear(const Tensor& x, int64_t Ho, int64_t Wo, at::ScalarType dtype) {
     check_gpu(x, "x");
     TORCH_CHECK(x.dim() == 4, "bilinear: x (n, c, h, w)");
@@ -820,6 +837,7 @@ TORCH_LIBRARY(dclip, m) {
     m.def("pos_interp_bwd(Tensor dout, int g, int H, int W) -> Tensor");
     m.def("row_mean(Tensor x, int bstride, int row_off, int ld, int B, int rows, int C) -> Tensor");
     m.def("score_map(Tensor v, int bstride, int row_off, int ld, Tensor text, int B, int HW, float eps) -> Tensor");
+    m.def("score_concat(Tensor rows, int bstride, int row_off, int ld, int C, Tensor score, int B, int h, int w) -> Tensor");
     m.def("bilinear(Tensor x, int Ho, int Wo, ScalarType dtype) -> Tensor");
     m.def("bilinear_bwd(Tensor dout, int Hi, int Wi) -> Tensor");
     m.def("bn_fwd(Tensor x, Tensor? w, Tensor? b, Tensor(a!)? running_mean, Tensor(b!)? running_var, float momentum, "
@@ -873,6 +891,7 @@ TORCH_LIBRARY_IMPL(dclip, CUDA, m) {
     m.impl("pos_interp_bwd", &pos_interp_bwd);
     m.impl("row_mean", &row_mean);
     m.impl("score_map", &score_map);
+    m.impl("score_concat", &score_concat);
     m.impl("bilinear", &bilinear);
     m.impl("bilinear_bwd", &bilinear_bwd);
     m.impl("bn_fwd", &bn_fwd);

@@ -373,10 +373,8 @@ class DenseCLIP(nn.Module):
             score = ops.score_map(v, text, B, HW, row_off=off, bstride=Nr * Ct).view(B, -1, h, w)
         feats = list(x)
         if 0 <= self.score_concat_index < len(feats):
-            with torch.no_grad():
-                tgt = feats[self.score_concat_index]
-                sc = ops.upsample(score, tgt.shape[2:]).to(tgt.dtype)
-                feats[self.score_concat_index] = torch.cat([tgt, sc], dim=1)
+            with torch.no_grad():  # one pass: copy + resize into the concatenated map
+                feats[self.score_concat_index] = ops.score_concat(feats[self.score_concat_index], score)
         return text, feats, score, list(x)
 
     def _heads(self, x_maps):

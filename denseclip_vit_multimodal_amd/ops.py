@@ -382,6 +382,22 @@ def score_map(v, text, B, HW, row_off=0, bstride=None, eps=1e-12):
     return D().score_map(v, bstride, row_off, C, text, B, HW, float(eps))
 
 
+def score_concat(tgt, score):
+    """torch.cat([tgt, upsample(score, tgt's size).to(tgt.dtype)], dim=1) — the score_concat_index
+    branch (denseclip.py:684-694) — as one HIP pass when tgt is a 16-bit read-out map over its token
+    buffer (the backbone's maps): a channels-last (B, C + K, h, w) result, no resized score map or
+    concatenation copy in HBM.  Other inputs take the resize + torch.cat it replaces."""
+    score = score.contiguous()
+    _check(score)  # tgt is a strided view by design (token_rows below)
+    B, C, h, w = tgt.shape
+    tok = token_rows(tgt)
+    if tok is None or tgt.dtype not in (torch.bfloat16, torch.float16) or score.dtype != torch.float32 \
+            or score.dim() != 4 or score.shape[1] > 64:
+        return torch.cat([tgt, upsample(score, (h, w)).to(tgt.dtype)], dim=1)
+    out = D().score_concat(tok, (h * w + 1) * C, 1, C, C, score, B, h, w)
+    return out.view(B, h, w, C + score.shape[1]).permute(0, 3, 1, 2)
+
+
 def bilinear(x, Ho, Wo, out_dtype=torch.float32):
     _check(x)
     return D().bilinear(x, Ho, Wo, out_dtype)

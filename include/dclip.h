@@ -30,6 +30,8 @@
  *   dclip_row_mean             F.adaptive_avg_pool2d(...,(1,1)) denseclip.py:596
  *   dclip_score_map            F.normalize x2 + einsum('bchw,bkc->bkhw')
  *                              denseclip.py:672-675
+ *   dclip_score_concat         upsample + torch.cat of the score map onto a read-out map
+ *                              denseclip.py:684-694
  *   dclip_bilinear_fwd/bwd     F.interpolate(bilinear, align_corners=False)
  *                              denseclip.py:847,860,899,909 (logits/depth upsample)
  *   dclip_cast                 dtype conversion of operands (.type()/.to() casts)
@@ -236,6 +238,13 @@ int dclip_row_mean(const void* x, int x_dt, int64_t bstride, int64_t row_off, in
  * C % 16 == 0, C <= 2048.                                                                      */
 int dclip_score_map(const void* v, int v_dt, int64_t bstride, int64_t row_off, int64_t ld, const float* t,
                     float* score, int B, int HW, int C, int K, float eps, void* stream);
+
+/* The score_concat_index branch's torch.cat([x_i, F.interpolate(score, (h, w)).to(x_i.dtype)], 1)
+ * (denseclip.py:684-694) in one pass: out (B*h*w, C + K) channels-last rows, 16-bit (dt) = the
+ * strided pixel rows of x_i (as dclip_row_mean: image b's pixel p at b*bstride + (row_off + p)*ld)
+ * followed by the bilinearly resized (align_corners=False) f32 score (B, K, hs, ws), K <= 64.      */
+int dclip_score_concat(const void* rows, int dt, int64_t bstride, int64_t row_off, int64_t ld, int C,
+                       const float* score, int K, int hs, int ws, void* out, int B, int h, int w, void* stream);
 
 /* Bilinear resize, align_corners=False, of NC planes (NC, Hi, Wi) -> (NC, Ho, Wo).   */
 int dclip_bilinear_fwd(const void* in, int in_dt, void* out, int out_dt,

@@ -1226,3 +1226,26 @@ def test_weight_refresh_off_falls_back_to_lazy_casts():
         O.EAGER_WEIGHT_REFRESH = True
     a1 = O.WEIGHTS.get(p, torch.bfloat16)
     assert a1 is not a0 and torch.equal(a1, p.detach().to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("hw,shw", [((8, 16), (8, 16)), ((12, 20), (6, 10)), ((7, 9), (13, 5))])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_score_concat_matches_upsample_and_cat(hw, shw, dt):
+    """ops.score_concat (one HIP pass: the read-out map's strided token rows + the bilinearly resized
+    score, channels last) is bitwise the resize + cast + torch.cat of the score_concat_index branch
+    (denseclip.py:684-694), for identity, 2x and non-integer resizes; a map that is not a token view
+    takes that torch path itself."""
+    O = ops()
+    torch.manual_seed(9)
+    B, C, K = 2, 96, 19
+    h, w = hw
+    ntok = h * w + 1
+    buf = torch.randn(B * ntok, C, device=DEV).to(dt)
+    tgt = buf.as_strided((B, C, h, w), (ntok * C, 1, w * C, C), C)  # a read-out map over its token buffer
+    score = torch.randn(B, K, *shw, device=DEV)
+    ref = torch.cat([tgt, O.upsample(score, (h, w)).to(dt)], dim=1)
+    out = O.score_concat(tgt, score)
+    assert out.shape == ref.shape and out.dtype == dt
+    assert torch.equal(out, ref)
+    plain = tgt.contiguous()
+    assert torch.equal(O.score_concat(plain, score), ref)
