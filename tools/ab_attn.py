@@ -1,7 +1,7 @@
 """A/B two builds of libdclip.so on the attention kernels in ONE process (interleaved rounds,
 same device, same random data) — the way to compare code changes (guide §5.4 rule 24).
 
-  python tools/ab_attn.py [-r ROUNDS] libA.so libB.so [libC.so ...]
+  python tools/ab_attn.py [-r ROUNDS] [--fp16] libA.so libB.so [libC.so ...]
 """
 import ctypes
 import os
@@ -18,12 +18,16 @@ rounds = 7
 if args[0] == "-r":
     rounds = int(args[1])
     args = args[2:]
+DT, TDT = 2, torch.bfloat16
+if args[0] == "--fp16":
+    DT, TDT = 1, torch.float16
+    args = args[1:]
 names = args
 libs = [_native.load(p) for p in names]
 torch.manual_seed(0)
-qkv = torch.randn(B * NT, 3 * C, device="cuda").to(torch.bfloat16)
-dout = torch.randn(B * NT, C, device="cuda").to(torch.bfloat16)
-o = torch.empty(B * NT, C, device="cuda", dtype=torch.bfloat16)
+qkv = torch.randn(B * NT, 3 * C, device="cuda").to(TDT)
+dout = torch.randn(B * NT, C, device="cuda").to(TDT)
+o = torch.empty(B * NT, C, device="cuda", dtype=TDT)
 lse = torch.empty(B * H * NT, device="cuda")
 delta = torch.empty(libs[0].dclip_attn_bwd_workspace(B, NT, H), device="cuda")
 dqkv = torch.empty_like(qkv)
@@ -31,11 +35,11 @@ st = torch.cuda.current_stream().cuda_stream
 
 
 def fwd(L):
-    assert L.dclip_attn_fwd(2, qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), B, NT, H, 64, 0.125, st) == 0
+    assert L.dclip_attn_fwd(DT, qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), B, NT, H, 64, 0.125, st) == 0
 
 
 def bwd(L):
-    assert L.dclip_attn_bwd(2, qkv.data_ptr(), o.data_ptr(), dout.data_ptr(), lse.data_ptr(), delta.data_ptr(),
+    assert L.dclip_attn_bwd(DT, qkv.data_ptr(), o.data_ptr(), dout.data_ptr(), lse.data_ptr(), delta.data_ptr(),
                             dqkv.data_ptr(), B, NT, H, 64, 0.125, st) == 0
 
 
