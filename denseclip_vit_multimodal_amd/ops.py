@@ -431,6 +431,10 @@ def _stamp_stepped_params(opt, *_):
 # per (device, dtype) (misc.hip weight_refresh_kernel), instead of one cast / transpose launch per
 # weight at its first use in the next forward / backward
 EAGER_WEIGHT_REFRESH = True
+# bf16 blocks: the dX GEMMs feeding the two LayerNorm backward passes write their gradient in bf16
+# (the rounding the reference's autocast linear applies to its input gradient) instead of fp32 —
+# 100 MB less written by the GEMM and read by the LN pass per call at the headline shape
+LN_DY_LP = True
 _REFRESH_DESC = {}  # (device, dtype) -> (key, device descriptor, tiles, pinned host copy)
 
 
@@ -721,7 +725,8 @@ class BlockFn(torch.autograd.Function):
         dW2 = db2 = dW1 = db1 = None
         if wg:
             dW2, db2 = weight_grad(dy, h, db=zb2, scale=s1)
-        dxh2 = gemm(dz, WEIGHTS.get(w1, cdt, transposed=True), out_dtype=torch.float32, scale=s1)
+        dy_lp = LN_DY_LP and cdt == torch.bfloat16 and s1 is None  # bf16: no gradient scale
+        dxh2 = gemm(dz, WEIGHTS.get(w1, cdt, transposed=True), out_dtype=cdt if dy_lp else torch.float32, scale=s1)
         if wg:
             dW1, db1 = weight_grad(dz, xh2, db=zb1, scale=s1)
         del dz
@@ -749,7 +754,8 @@ class BlockFn(torch.autograd.Function):
         del dyo
         dqkv = attn_bwd(qkv, o, do, lse, B, Ntok, H, scale)  # linear in dO: carries s2
         del do
-        dxh1 = gemm(dqkv, WEIGHTS.get(w_in, cdt, transposed=True), out_dtype=torch.float32, scale=s2)
+        dxh1 = gemm(dqkv, WEIGHTS.get(w_in, cdt, transposed=True), out_dtype=cdt if dy_lp and s2 is None else torch.float32,
+                    scale=s2)
         if wg:
             dWi, dbi = weight_grad(dqkv, xh1, db=zbi, scale=s2)
         del dqkv

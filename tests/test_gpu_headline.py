@@ -74,7 +74,13 @@ def _backbone():
 
 def test_vitb16_full_resolution_backward_is_additive_over_images():
     """ViT-B/16 at B = 8 x 1024x2048 (bf16, mode F backbone): d/dparams of sum_i <map_i, W_i>
-    for the batch equals the sum over images of the same derivative taken image by image."""
+    for the batch equals the sum over images of the same derivative taken image by image.
+
+    Bound: bf16 rounding noise between two summation orders.  Measured in one process
+    (tools/additivity_probe.py, profiles/r04/r06j_additivity.log): worst parameter class_embedding
+    at 2.00e-3 with fp32 LayerNorm-backward inputs (the round-3 bound of 2e-3 sat on it) and
+    2.34e-3 with the bf16 ones (ops.LN_DY_LP, one more bf16 rounding per element per block); the
+    next parameters at 1.8e-3 either way."""
     bb = _backbone()
     B = 8
     x = images(B, 1024, 2048).to(DEV).to(torch.bfloat16)
@@ -94,7 +100,7 @@ def test_vitb16_full_resolution_backward_is_additive_over_images():
         gi = grads(slice(i, i + 1))
         g_sum = gi if g_sum is None else {k: g_sum[k] + gi[k] for k in g_sum}
     worst = max(((rel_err(g_batch[k], g_sum[k]), k) for k in g_batch))
-    assert worst[0] < 2e-3, worst
+    assert worst[0] < 3e-3, worst
 
 
 def test_headline_train_step_two_steps():
