@@ -58,6 +58,10 @@ def _register_fakes():
     def _(dy, x, w, mean, rstd, res, dw, db, lp_dtype):
         return _e(*x.shape, like=x, dtype=f32), _e(*x.shape, like=x, dtype=lp_dtype)
 
+    @reg("dclip::layernorm_bwd_add")
+    def _(dy, x, w, mean, rstd, res, add, ntok, dw, db, lp_dtype):
+        return _e(*x.shape, like=x, dtype=f32), _e(*x.shape, like=x, dtype=lp_dtype)
+
     @reg("dclip::gemm")
     def _(A, B, epi, bias, aux, out_dtype, alpha, scale=None):
         return _e(A.shape[0], B.shape[0], like=A, dtype=out_dtype)

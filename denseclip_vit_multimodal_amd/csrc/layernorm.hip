@@ -241,14 +241,20 @@ __global__ __launch_bounds__(256) void ln_fwd_fast(const TX* __restrict__ x, con
 // DS (delayed scale, fp16 lp): lp = (f16)(dx * s), s the power-of-two scale of this gradient
 // site's previous use (common.h ds_*: use `use` of the state st), (s, 1/s) to spair for the
 // consumers of lp, and this use's |dx| maximum joined into st for the next.
-template <typename TDY, typename TX, int NV, bool DS = false>
+//
+// ADD (dclip_layernorm_bwd_add): dx = (res + LN^T(dy)) + add, add a bf16 token buffer whose rows
+// with row % ntok == 0 (the CLS rows) read as 0 — the previous block's read-out map gradient, so
+// the sum and its 16-bit copy lp come out of this pass instead of a dclip_add_readout_cast pass
+// over the written dx (same fp32 additions in the same order: bitwise its result)
+template <typename TDY, typename TX, int NV, bool DS = false, bool ADD = false>
 __global__ __launch_bounds__(512) void ln_bwd_fast(const TDY* __restrict__ dy, const TX* __restrict__ x,
                                                    const float* __restrict__ w, const float* __restrict__ mean,
                                                    const float* __restrict__ rstd, const float* res, float* dx,
                                                    void* __restrict__ lp, int lp_dt, float* __restrict__ dw,
                                                    float* __restrict__ db, int64_t rows, float* part,
                                                    float* st = nullptr, int use = 0, float* spair = nullptr,
-                                                   float target = 0.f) {
+                                                   float target = 0.f, const bf16* __restrict__ add = nullptr,
+                                                   int ntok = 1) {
     constexpr int cols = 256 * NV;
     __shared__ float red[8][2][4 * NV][64];
     const int lane = threadIdx.x & 63;
@@ -269,6 +275,7 @@ __global__ __launch_bounds__(512) void ln_bwd_fast(const TDY* __restrict__ dy, c
     // everything a row needs (dy, x, the accumulated dx, its statistics) is loaded one row
     // ahead, so no load latency is exposed per row
     float dv[4 * NV], xv[4 * NV], old[4 * NV], ndv[4 * NV], nxv[4 * NV], nold[4 * NV];
+    float av[ADD ? 4 * NV : 1], nav[ADD ? 4 * NV : 1];
     float mu = 0.f, rs = 0.f, nmu = 0.f, nrs = 0.f;
     if (row < rows) {
 #pragma unroll
@@ -276,6 +283,12 @@ __global__ __launch_bounds__(512) void ln_bwd_fast(const TDY* __restrict__ dy, c
             load4(dy + row * cols + 4 * lane + 256 * i, dv + 4 * i);
             load4(x + row * cols + 4 * lane + 256 * i, xv + 4 * i);
             if (res) load4(res + row * cols + 4 * lane + 256 * i, old + 4 * i);
+            if constexpr (ADD) {
+                if (row % ntok != 0) load4(add + row * cols + 4 * lane + 256 * i, av + 4 * i);
+                else
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) av[4 * i + e] = 0.f;
+            }
         }
         mu = mean[row];
         rs = rstd[row];
@@ -288,6 +301,12 @@ __global__ __launch_bounds__(512) void ln_bwd_fast(const TDY* __restrict__ dy, c
                 load4(dy + nrow * cols + 4 * lane + 256 * i, ndv + 4 * i);
                 load4(x + nrow * cols + 4 * lane + 256 * i, nxv + 4 * i);
                 if (res) load4(res + nrow * cols + 4 * lane + 256 * i, nold + 4 * i);
+                if constexpr (ADD) {
+                    if (nrow % ntok != 0) load4(add + nrow * cols + 4 * lane + 256 * i, nav + 4 * i);
+                    else
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) nav[4 * i + e] = 0.f;
+                }
             }
             nmu = mean[nrow];
             nrs = rstd[nrow];
@@ -313,6 +332,7 @@ __global__ __launch_bounds__(512) void ln_bwd_fast(const TDY* __restrict__ dy, c
                 const int k = 4 * i + e;
                 o[e] = rs * (dv[k] * wl[k] - mg - xv[k] * mgx);
                 if (res) o[e] += old[k];
+                if constexpr (ADD) o[e] += av[k];
             }
             store4(dx + row * cols + 4 * lane + 256 * i, o);
             if constexpr (DS) {
@@ -335,6 +355,7 @@ __global__ __launch_bounds__(512) void ln_bwd_fast(const TDY* __restrict__ dy, c
             dv[k] = ndv[k];
             xv[k] = nxv[k];
             old[k] = nold[k];
+            if constexpr (ADD) av[k] = nav[k];
         }
     }
 #pragma unroll
@@ -479,7 +500,48 @@ void bwd_fast_ds(const float* dy, const void* x, const float* w, const float* me
     if (part) ln_dwdb_reduce_kernel<<<(2 * 256 * NV + 255) / 256, 256, 0, s>>>(part, 256 * NV, dw, db);
 }
 
+template <typename TDY, int NV>
+void bwd_fast_add(const void* dy, const float* x, const float* w, const float* mean, const float* rstd,
+                  const float* res, const bf16* add, int ntok, float* dx, void* lp, int lp_dt, float* dw, float* db,
+                  int64_t rows, hipStream_t s) {
+    int64_t blocks = (rows + 7) / 8;
+    blocks = blocks > 512 ? 512 : blocks;
+    float* part = (dw || db) ? ln_partials(256 * NV) : nullptr;
+    ln_bwd_fast<TDY, float, NV, false, true><<<(unsigned)blocks, 512, 0, s>>>(
+        (const TDY*)dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, rows, part, nullptr, 0, nullptr, 0.f, add, ntok);
+    if (part) ln_dwdb_reduce_kernel<<<(2 * 256 * NV + 255) / 256, 256, 0, s>>>(part, 256 * NV, dw, db);
+}
+
+template <typename TDY>
+void bwd_add_cols(const void* dy, const float* x, const float* w, const float* mean, const float* rstd,
+                  const float* res, const bf16* add, int ntok, float* dx, void* lp, int lp_dt, float* dw, float* db,
+                  int64_t rows, int64_t cols, hipStream_t s) {
+    if (cols == 512) bwd_fast_add<TDY, 2>(dy, x, w, mean, rstd, res, add, ntok, dx, lp, lp_dt, dw, db, rows, s);
+    else if (cols == 768) bwd_fast_add<TDY, 3>(dy, x, w, mean, rstd, res, add, ntok, dx, lp, lp_dt, dw, db, rows, s);
+    else bwd_fast_add<TDY, 4>(dy, x, w, mean, rstd, res, add, ntok, dx, lp, lp_dt, dw, db, rows, s);
+}
+
 }  // namespace
+
+extern "C" int dclip_layernorm_bwd_add(const void* dy, int dy_dt, const float* x, const float* w, const float* mean,
+                                       const float* rstd, const float* res, const void* add, int ntok, float* dx,
+                                       void* lp, int lp_dt, float* dw, float* db, int64_t rows, int64_t cols,
+                                       void* stream) {
+    DCLIP_HOST_CHECK(cols == 512 || cols == 768 || cols == 1024,
+                     "dclip_layernorm_bwd_add: cols must be 512, 768 or 1024 (got %lld)", (long long)cols);
+    DCLIP_HOST_CHECK(dy_dt == DCLIP_F32 || dy_dt == DCLIP_BF16, "dclip_layernorm_bwd_add: dy must be f32 or bf16");
+    DCLIP_HOST_CHECK(add != nullptr && ntok > 0, "dclip_layernorm_bwd_add: the bf16 add buffer and ntok > 0");
+    DCLIP_HOST_CHECK(lp != nullptr && (lp_dt == DCLIP_BF16 || lp_dt == DCLIP_F16),
+                     "dclip_layernorm_bwd_add: lp (F16 or BF16) is required");
+    DCLIP_HOST_CHECK(rows >= 0, "dclip_layernorm_bwd_add: rows < 0");
+    if (rows == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    if (dy_dt == DCLIP_F32)
+        bwd_add_cols<float>(dy, x, w, mean, rstd, res, (const bf16*)add, ntok, dx, lp, lp_dt, dw, db, rows, cols, s);
+    else bwd_add_cols<bf16>(dy, x, w, mean, rstd, res, (const bf16*)add, ntok, dx, lp, lp_dt, dw, db, rows, cols, s);
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
 
 extern "C" int dclip_layernorm_bwd_scaled(const float* dy, const void* x, int x_dt, const float* w, const float* mean,
                                           const float* rstd, const float* res, float* dx, void* lp, float* dw,

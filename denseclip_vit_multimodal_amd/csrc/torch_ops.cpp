@@ -121,6 +121,30 @@ std::tuple<Tensor, Tensor> layernorm_bwd_lp(const Tensor& dy, const Tensor& x, c
     return {dx, lp};
 }
 
+// layernorm_bwd_lp of a block's ln_1 with the previous block's read-out map gradient `add` (bf16,
+// rows with row % ntok == 0 read as 0) added before the cast: (dx, lp)
+std::tuple<Tensor, Tensor> layernorm_bwd_add(const Tensor& dy, const Tensor& x, const Tensor& w, const Tensor& mean,
+                                             const Tensor& rstd, const c10::optional<Tensor>& res, const Tensor& add,
+                                             int64_t ntok, Tensor& dw, Tensor& db, at::ScalarType lp_dtype) {
+    check_gpu(dy, "dy"); check_gpu(x, "x"); check_gpu(w, "w"); check_gpu(mean, "mean"); check_gpu(rstd, "rstd");
+    check_gpu(add, "add"); check_opt(res, "res");
+    TORCH_CHECK(x.dim() == 2 && dy.sizes() == x.sizes() && add.sizes() == x.sizes(),
+                "layernorm_bwd_add: dy, x and add (rows, cols)");
+    TORCH_CHECK(x.scalar_type() == at::kFloat && add.scalar_type() == at::kBFloat16,
+                "layernorm_bwd_add: f32 x and a bf16 add buffer");
+    TORCH_CHECK(ntok > 0 && x.size(0) % ntok == 0, "layernorm_bwd_add: rows must be a multiple of ntok");
+    check_vec(w, x.size(1), "LayerNorm weight"); check_vec(dw, x.size(1), "dw"); check_vec(db, x.size(1), "db");
+    check_vec(mean, x.size(0), "mean"); check_vec(rstd, x.size(0), "rstd");
+    c10::DeviceGuard g(x.device());
+    Tensor dx = at::empty(x.sizes(), like(x, at::kFloat));
+    Tensor lp = at::empty(x.sizes(), like(x, lp_dtype));
+    DCLIP_CALL(dclip_layernorm_bwd_add(dy.data_ptr(), dt_code(dy.scalar_type()), ptr<float>(x), ptr<float>(w),
+                                       ptr<float>(mean), ptr<float>(rstd), optr<float>(res), add.data_ptr(), (int)ntok,
+                                       ptr<float>(dx), lp.data_ptr(), dt_code(lp_dtype), ptr<float>(dw), ptr<float>(db),
+                                       x.size(0), x.size(1), stream_of(x)));
+    return {dx, lp};
+}
+
 // ----------------------------------------------------------------------------- GEMM
 void gemm_checks(const Tensor& A, const Tensor& B) {
     TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "gemm: A (M, K), B (N, K)");
@@ -806,6 +830,8 @@ TORCH_LIBRARY(dclip, m) {
           "Tensor(b!) db) -> Tensor");
     m.def("layernorm_bwd_lp(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, Tensor? res, Tensor(a!) dw, "
           "Tensor(b!) db, ScalarType lp_dtype) -> (Tensor, Tensor)");
+    m.def("layernorm_bwd_add(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, Tensor? res, Tensor add, "
+          "int ntok, Tensor(a!) dw, Tensor(b!) db, ScalarType lp_dtype) -> (Tensor, Tensor)");
     m.def("gemm(Tensor A, Tensor B, int epi, Tensor? bias, Tensor? aux, ScalarType out_dtype, float alpha, "
           "Tensor? scale=None) -> Tensor");
     m.def("gemm_gelu(Tensor A, Tensor B, Tensor? bias) -> (Tensor, Tensor)");
@@ -864,6 +890,7 @@ TORCH_LIBRARY_IMPL(dclip, CUDA, m) {
     m.impl("layernorm_fwd", &layernorm_fwd);
     m.impl("layernorm_bwd", &layernorm_bwd);
     m.impl("layernorm_bwd_lp", &layernorm_bwd_lp);
+    m.impl("layernorm_bwd_add", &layernorm_bwd_add);
     m.impl("gemm", &gemm);
     m.impl("gemm_gelu", &gemm_gelu);
     m.impl("gemm_gelu_h", &gemm_gelu_h);

@@ -298,6 +298,7 @@ class CLIPVisionTransformer(nn.Module):
         rmeta = (B, Ntok, gh, gw, mdt, hsb)
         last = max(self.out_indices) if self.out_indices else -1
         fp16_bwd = cdt == torch.float16 and torch.is_grad_enabled()
+        link_in = None  # the previous block's ops.ReadoutLink (meta[8]): folded into this block's ln_1 backward
         for i, blk in enumerate(self.transformer.resblocks):
             if i > last:
                 break  # later blocks feed nothing the reference returns
@@ -306,12 +307,20 @@ class CLIPVisionTransformer(nn.Module):
             ds = _delayed_scale(blk) if fp16_bwd else None
             if i in self.out_indices and i != self.layers - 1:
                 # read-out without ln_post: produced by the block itself, so its gradient is
-                # folded into the block's backward (ops.BlockFn, meta[5])
-                bmeta = meta + ((gh, gw, mdt, hsb), dp, ds)
+                # folded into the block's backward (ops.BlockFn, meta[5]) — or, bf16, into the next
+                # block's ln_1 backward (meta[9], ops.ReadoutLink)
+                link = ops.ReadoutLink(gh, gw) if (ops.FOLD_READOUT_GRAD and torch.is_grad_enabled() and i < last
+                                                   and cdt == torch.bfloat16 and mdt == torch.bfloat16
+                                                   and dp is None and hsb is None) else None
+                bmeta = meta + ((gh, gw, mdt, hsb), dp, ds, link_in, link)
                 tok, fmap = ops.BlockFn.apply(tok, bmeta, *blk.hip_params())
+                if link is not None:
+                    fmap._dclip_link = link  # read by the map gradient's producer (ops.NeckLevelsFn)
+                link_in = link
                 outs.append(fmap)
                 continue
-            tok = ops.BlockFn.apply(tok, meta + (None, dp, ds), *blk.hip_params())
+            tok = ops.BlockFn.apply(tok, meta + (None, dp, ds, link_in, None), *blk.hip_params())
+            link_in = None
             if i in self.out_indices:  # the last layer: ln_post (models.py:576)
                 outs.append(ops.ReadoutFn.apply(tok, self.ln_post.weight, self.ln_post.bias, rmeta))
         return outs

@@ -137,6 +137,37 @@ def layernorm_bwd(dy, x, w, mean, rstd, dw, db, res=None, lp_dtype=None):
     return D().layernorm_bwd_lp(dy, x, w, mean, rstd, res, dw, db, lp_dtype)
 
 
+def layernorm_bwd_add(dy, x, w, mean, rstd, dw, db, res, add, ntok, lp_dtype):
+    """layernorm_bwd with res, plus `add` (a bf16 token buffer whose CLS rows, row % ntok == 0,
+    read as 0) before the lp cast: (dx, lp) — dclip_layernorm_bwd_add."""
+    _check(dy, x, w, mean, rstd, dw, db, res, add)
+    e0 = _tic()
+    out = D().layernorm_bwd_add(dy, x, w, mean, rstd, res, add, ntok, dw, db, lp_dtype)
+    _toc("layernorm_bwd_add", e0)
+    return out
+
+
+# A bf16 read-out map's gradient folded into the NEXT block's ln_1 backward (which runs before
+# the map's own block backward): dclip_layernorm_bwd_add writes the map's block-output gradient
+# and its bf16 copy in one pass, and the map's block skips its dclip_add_readout_cast pass.
+FOLD_READOUT_GRAD = True
+
+
+class ReadoutLink:
+    """Hand-over of one read-out map's gradient between two BlockFn backwards (FOLD_READOUT_GRAD).
+
+    The producer of the map's gradient (NeckLevelsFn's backward, which runs before every block
+    backward) stores it in `g`; the next block's backward adds it inside its ln_1 backward and
+    stores the bf16 operand it wrote in `lp`; the map's own block then takes `lp` as its first
+    GEMM operand when the gradient autograd hands it IS `g` (the map had no other consumer), and
+    otherwise adds the difference.  Both fields are cleared by the map's block."""
+    __slots__ = ("gh", "gw", "g", "lp")
+
+    def __init__(self, gh, gw):
+        self.gh, self.gw = gh, gw
+        self.g = self.lp = None
+
+
 def gemm(A, B, epi=N.EPI_STORE, bias=None, aux=None, out_dtype=None, alpha=1.0, scale=None, lp_copy=False):
     """out[m][n] = alpha * sum_k A[m][k] B[n][k] (+ epilogue).  A: (M, K), B: (N, K).
     EPI_GELU returns (z, quick_gelu(z)).  scale: a grad_scale() buffer whose 1/s also
@@ -615,7 +646,12 @@ class BlockFn(torch.autograd.Function):
     291-294): f32 (Ntok,) keep masks already divided by the keep probability, one value per token
     POSITION (timm's drop_path on the reference's LND layout); the attention / MLP branch is
     added as x + m[token] * branch (dclip_row_scale_add) instead of through the fused residual
-    epilogue, and its gradient is scaled the same way."""
+    epilogue, and its gradient is scaled the same way.
+
+    meta[8] / meta[9] (optional, bf16 only) = the previous block's / this block's ReadoutLink
+    (FOLD_READOUT_GRAD): the previous block's map gradient is added inside this block's ln_1
+    backward (dclip_layernorm_bwd_add), and this block's own map gradient arrives already added
+    to dxo, with its bf16 operand, from the next block's."""
 
     @staticmethod
     def forward(ctx, x, meta, ln1w, ln1b, w_in, b_in, w_out, b_out, ln2w, ln2b, w1, b1, w2, b2):
@@ -683,6 +719,18 @@ class BlockFn(torch.autograd.Function):
         if dxo is None:
             dxo = torch.zeros(B * Ntok, C, dtype=torch.float32, device=x.device)
         dxo = dxo.contiguous()
+        lk = ctx.meta[9] if len(ctx.meta) > 9 else None  # this block's read-out map (ReadoutLink)
+        if lk is not None:
+            g, lp = lk.g, lk.lp
+            lk.g = lk.lp = None
+            if lp is not None:  # the next block's ln_1 backward already added g into dxo
+                if dmap is g:
+                    dy, dmap = lp, None
+                else:  # other consumers joined the map's gradient after g: add the difference
+                    d = _readout_grad_dense(g, B, Ntok, lk.gh, lk.gw, C).neg_()
+                    if dmap is not None:
+                        d += _readout_grad_dense(dmap, B, Ntok, lk.gh, lk.gw, C)
+                    dxo, dmap = dxo + d, None
         if ds is not None and ds.primed[0]:
             base = hsb = None
             if dmap is not None:
@@ -759,7 +807,16 @@ class BlockFn(torch.autograd.Function):
         if wg:
             dWi, dbi = weight_grad(dqkv, xh1, db=zbi, scale=s2)
         del dqkv
-        dxm = layernorm_bwd(dxh1, x, ln1w.detach(), mu1, rs1, dln1w, dln1b, res=dxm)
+        lk = ctx.meta[8] if len(ctx.meta) > 8 else None  # the previous block's read-out map
+        base = None
+        if lk is not None and lk.g is not None and need[0]:
+            base = _readout_grad_buffer(lk.g, B, Ntok, lk.gh, lk.gw, C)
+            base = base if base is not None and base.dtype == torch.bfloat16 else None
+        if base is not None:  # its gradient and the previous block's first GEMM operand from this pass
+            dxm, lk.lp = layernorm_bwd_add(dxh1, x, ln1w.detach(), mu1, rs1, dln1w, dln1b, dxm, base, Ntok,
+                                           torch.bfloat16)
+        else:
+            dxm = layernorm_bwd(dxh1, x, ln1w.detach(), mu1, rs1, dln1w, dln1b, res=dxm)
         g = lambda i, t: t if need[i] else None  # noqa: E731
         return (dxm if need[0] else None, None, g(2, dln1w), g(3, dln1b), g(4, dWi), g(5, dbi), g(6, dWo),
                 g(7, dbo), g(8, dln2w), g(9, dln2b), g(10, dW1), g(11, db1), g(12, dW2), g(13, db2))
@@ -1266,6 +1323,7 @@ class NeckLevelsFn(torch.autograd.Function):
         ctx.meta = (L, B, Cin, H, W, Ci, cdt, [(g[1], g[2]) for g in geo], [m.dtype for m in maps],
                     [tuple(m.stride()) for m in maps], [g[0] is m for g, m in zip(geo, maps)])
         ctx.hsb = _head_scale_buf()
+        ctx.links = [getattr(m, "_dclip_link", None) for m in maps]  # ReadoutLink of a block's map
         _stat("neck_levels")
         return out.as_strided((B, LC, H, W), (H * W * LC, 1, W * LC, LC))
 
@@ -1306,6 +1364,8 @@ class NeckLevelsFn(torch.autograd.Function):
                     D().conv3x3(1, dpre[:, l * Ci:], H * W * LC, 0, LC, B, H, W, Ci, w_t, Cin, buf, Cin, 0, 0, 0)
                     dm = buf.as_strided((B, Cin, H, W), (H * W * Cin, 1, W * Cin, Cin))
                 dmaps[l] = dm if in_dts[l] == cdt else dm.to(in_dts[l])
+                if ctx.links[l] is not None:
+                    ctx.links[l].g = dmaps[l]
             if need[1 + L + l]:
                 e0 = _tic()
                 dwc = D().conv3x3_wgrad(dpre[:, l * Ci:], LC, Ci, xrs[l], bs, 0, ld, B, H, W, Cin, splits, True, ctx.hsb)

@@ -405,6 +405,17 @@ int dclip_layernorm_bwd_scaled(const float* dy, const void* x, int x_dt, const f
                                int64_t rows, int64_t cols, float target, float* st, int use, float* spair,
                                void* stream);
 
+/* LayerNorm backward of a block's ln_1 with the PREVIOUS block's read-out map gradient folded in
+ * (models.py:243-249 backward + the models.py:565 -> 577-597 read-out's gradient):
+ *   dx = (res + LN^T(dy)) + add,  lp = (lp_dt) dx
+ * add: a bf16 (rows, cols) token buffer whose rows with row % ntok == 0 (CLS) read as 0.  One pass
+ * in place of dclip_layernorm_bwd_res + dclip_add_readout_cast (bitwise their result: the same
+ * fp32 additions in the same order).  dy f32 or bf16, x f32, cols in {512, 768, 1024}; lp required.
+ * dw / db accumulate as in dclip_layernorm_bwd_res (may be NULL). */
+int dclip_layernorm_bwd_add(const void* dy, int dy_dt, const float* x, const float* w, const float* mean,
+                            const float* rstd, const float* res, const void* add, int ntok, float* dx, void* lp,
+                            int lp_dt, float* dw, float* db, int64_t rows, int64_t cols, void* stream);
+
 /* Train-mode BatchNorm2d (+ optionally the ReLU after it) on a channels-last 16-bit map viewed as
  * rows (B*H*W) of C channels at a row pitch of ld elements (ld = C for a whole map; larger for a
  * channel slice of a wider buffer, e.g. one level of the neck's concatenation).  Replaces

@@ -1182,6 +1182,76 @@ def test_neck_levels_fn_matches_per_level_path():
         assert rel_err(bu.float(), br.float()) < 1e-4, n
 
 
+@pytest.mark.parametrize("dydt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("rows,cols,ntok", [(2 * 129, 768, 129), (3 * 97, 512, 97), (2 * 65, 1024, 65), (7, 768, 7)])
+def test_layernorm_bwd_add_matches_two_passes(dydt, rows, cols, ntok):
+    """dclip_layernorm_bwd_add (ln_1 backward + the previous block's read-out gradient, CLS rows
+    masked, + the bf16 operand) is bitwise the two passes it replaces: layernorm_bwd with res,
+    then add_readout_cast.  dw / db: the same per-block partials, added atomically into shards
+    (order not fixed run to run), so equal up to fp32 rounding."""
+    O = ops()
+    torch.manual_seed(8)
+    x = torch.randn(rows, cols, device=DEV) * 3 + 0.5
+    w = torch.randn(cols, device=DEV)
+    b = torch.randn(cols, device=DEV)
+    _, mu, rs = O.D().layernorm_fwd(x, w, b, torch.bfloat16, 1e-5)
+    dy = torch.randn(rows, cols, device=DEV).to(dydt)
+    res = torch.randn(rows, cols, device=DEV)
+    add = torch.randn(rows, cols, device=DEV).to(torch.bfloat16)
+    dw1, db1 = torch.zeros(cols, device=DEV), torch.zeros(cols, device=DEV)
+    dx1 = O.D().layernorm_bwd(dy, x, w, mu, rs, res, dw1, db1)
+    sm, lp1 = O.D().add_readout_cast(dx1, add, ntok, torch.bfloat16, 1.0)
+    dw2, db2 = torch.zeros(cols, device=DEV), torch.zeros(cols, device=DEV)
+    dx2, lp2 = O.D().layernorm_bwd_add(dy, x, w, mu, rs, res, add, ntok, dw2, db2, torch.bfloat16)
+    assert torch.equal(dx2, sm) and torch.equal(lp2, lp1)
+    assert rel_err(dw2, dw1) < 1e-6 and rel_err(db2, db1) < 1e-6
+    with pytest.raises(RuntimeError, match="multiple of ntok"):
+        O.D().layernorm_bwd_add(dy, x, w, mu, rs, res, add, ntok + 1 if rows > 7 else 5, dw2, db2, torch.bfloat16)
+
+
+@pytest.mark.parametrize("extra_consumer", [False, True])
+def test_readout_grad_fold_matches_unfolded(extra_consumer):
+    """ViT-B/16 backbone + fusion neck (NeckLevelsFn), bf16 train: with the read-out gradients
+    folded into the next block's ln_1 backward (ops.FOLD_READOUT_GRAD, ReadoutLink) every
+    gradient equals the unfolded path's up to fp32 rounding (the token gradients are the same fp32
+    additions in the same order; the LN / BN weight gradients add into atomic shards).
+    With a second consumer of one map (its gradient is then no longer the neck's tensor) the
+    block adds the difference (dxo + g) + (dmap - g): an fp32 reassociation ahead of the bf16 cast
+    of the block's GEMM operand, so an element can round to the neighbouring bf16 value — equal up
+    to bf16 rounding (measured 5.8e-4 worst parameter)."""
+    from denseclip_vit_multimodal_amd import DenseCLIP
+    from denseclip_vit_multimodal_amd import ops as O
+    from helpers import CITYSCAPES_CFG, CITYSCAPES_CLASSES, images, spec_state_dict
+    m = DenseCLIP(class_names=CITYSCAPES_CLASSES, **CITYSCAPES_CFG)
+    m.load_state_dict(spec_state_dict("cityscapes"))
+    bb, neck = m.backbone.to(DEV).train(), m.neck.to(DEV).train()
+    x = images(2, 128, 256).to(DEV).to(torch.bfloat16)
+    gen = torch.Generator(device=DEV).manual_seed(4)
+    gout = torch.randn(2, 256, 8, 16, device=DEV, generator=gen)
+    w3 = torch.randn(2, 768, 8, 16, device=DEV, generator=gen)
+    params = [p for p in list(bb.parameters()) + list(neck.parameters()) if p.requires_grad]
+    run = []
+    try:
+        for fold in (False, True):
+            O.FOLD_READOUT_GRAD = fold
+            for p in params:
+                p.grad = None
+            before = O.STATS.get("neck_levels", 0)
+            feats = bb(x)
+            out = neck(feats)[0]
+            assert O.STATS.get("neck_levels", 0) == before + 1  # the HIP neck (the links' producer)
+            loss = (out.float() * gout).sum()
+            if extra_consumer:
+                loss = loss + (feats[3].float() * w3).sum()
+            loss.backward()
+            run.append([p.grad.clone() for p in params if p.grad is not None])
+    finally:
+        O.FOLD_READOUT_GRAD = True
+    assert len(run[0]) == len(run[1]) >= 12 * 12
+    for a, b in zip(*run):
+        assert rel_err(b.float(), a.float()) < (4e-3 if extra_consumer else 1e-6)
+
+
 # ----------------------------------------------------------------------------- weight copies
 @pytest.mark.parametrize("fused", [True, False])
 def test_weight_refresh_after_step_matches_fresh_casts(fused):
