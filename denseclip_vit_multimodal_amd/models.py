@@ -311,7 +311,8 @@ class CLIPVisionTransformer(nn.Module):
                 # block's ln_1 backward (meta[9], ops.ReadoutLink)
                 link = ops.ReadoutLink(gh, gw) if (ops.FOLD_READOUT_GRAD and torch.is_grad_enabled() and i < last
                                                    and cdt == torch.bfloat16 and mdt == torch.bfloat16
-                                                   and dp is None and hsb is None) else None
+                                                   and dp is None and hsb is None
+                                                   and self.width in (512, 768, 1024)) else None
                 bmeta = meta + ((gh, gw, mdt, hsb), dp, ds, link_in, link)
                 tok, fmap = ops.BlockFn.apply(tok, bmeta, *blk.hip_params())
                 if link is not None:

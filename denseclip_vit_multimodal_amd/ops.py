@@ -809,7 +809,7 @@ class BlockFn(torch.autograd.Function):
         del dqkv
         lk = ctx.meta[8] if len(ctx.meta) > 8 else None  # the previous block's read-out map
         base = None
-        if lk is not None and lk.g is not None and need[0]:
+        if lk is not None and lk.g is not None and need[0] and C in (512, 768, 1024):  # dclip_layernorm_bwd_add's widths
             base = _readout_grad_buffer(lk.g, B, Ntok, lk.gh, lk.gw, C)
             base = base if base is not None and base.dtype == torch.bfloat16 else None
         if base is not None:  # its gradient and the previous block's first GEMM operand from this pass
