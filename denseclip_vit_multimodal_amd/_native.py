@@ -33,6 +33,9 @@ _SIGS = {
                                 _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _i64, _i64, _c_void_p],
     "dclip_layernorm_bwd_add": [_c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                                 _i32, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _i64, _i64, _c_void_p],
+    "dclip_layernorm_bwd_scaled_add": [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                       _i32, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _i64,
+                                       _f32, _c_void_p, _i32, _c_void_p, _c_void_p],
     "dclip_gemm": [_i32, _i32, _c_void_p, _i64, _c_void_p, _i64, _i64, _i64, _i64, _i32, _f32, _c_void_p, _c_void_p,
                    _c_void_p,
                    _i32, _i64, _c_void_p, _i32, _i64, _c_void_p, _i64, _c_void_p],

@@ -130,6 +130,10 @@ def _register_fakes():
     def _(dy, x, w, mean, rstd, res, dw, db, st, use, target):
         return _e(*x.shape, like=x, dtype=f32), _e(*x.shape, like=x, dtype=torch.float16), _e(4, like=x)
 
+    @reg("dclip::layernorm_bwd_scaled_add")
+    def _(dy, x, w, mean, rstd, res, add, add_scale, ntok, dw, db, st, use, target):
+        return _e(*x.shape, like=x, dtype=f32), _e(*x.shape, like=x, dtype=torch.float16), _e(4, like=x)
+
     @reg("dclip::attn_fwd")
     def _(qkv, B, N, H, scale):
         return _e(B * N, 64 * H, like=qkv), _e(B * H * N, like=qkv, dtype=f32)

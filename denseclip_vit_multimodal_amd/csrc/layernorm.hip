@@ -4,6 +4,8 @@
 // HBM-bound: forward reads the row once (f32) and writes it once (bf16/f16/f32);
 // backward reads dy and x once and writes dx once, with dw/db summed in registers over a
 // grid-strided set of rows and flushed once per block.
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -242,20 +244,26 @@ __global__ __launch_bounds__(256) void ln_fwd_fast(const TX* __restrict__ x, con
 // site's previous use (common.h ds_*: use `use` of the state st), (s, 1/s) to spair for the
 // consumers of lp, and this use's |dx| maximum joined into st for the next.
 //
-// ADD (dclip_layernorm_bwd_add): dx = (res + LN^T(dy)) + add, add a bf16 token buffer whose rows
-// with row % ntok == 0 (the CLS rows) read as 0 — the previous block's read-out map gradient, so
-// the sum and its 16-bit copy lp come out of this pass instead of a dclip_add_readout_cast pass
-// over the written dx (same fp32 additions in the same order: bitwise its result)
-template <typename TDY, typename TX, int NV, bool DS = false, bool ADD = false>
+// TA (dclip_layernorm_bwd_add / _scaled_add): dx = (res + LN^T(dy)) + add * (*add_scale), add a
+// 16-bit (TA) token buffer whose rows with row % ntok == 0 (the CLS rows) read as 0 — the previous
+// block's read-out map gradient, so the sum and its 16-bit copy lp come out of this pass instead
+// of a dclip_add_readout_cast(_scaled) pass over the written dx (the same fp32 arithmetic in the
+// same order: bitwise its result)
+template <typename TDY, typename TX, int NV, bool DS = false, typename TA = void>
 __global__ __launch_bounds__(512) void ln_bwd_fast(const TDY* __restrict__ dy, const TX* __restrict__ x,
                                                    const float* __restrict__ w, const float* __restrict__ mean,
                                                    const float* __restrict__ rstd, const float* res, float* dx,
                                                    void* __restrict__ lp, int lp_dt, float* __restrict__ dw,
                                                    float* __restrict__ db, int64_t rows, float* part,
                                                    float* st = nullptr, int use = 0, float* spair = nullptr,
-                                                   float target = 0.f, const bf16* __restrict__ add = nullptr,
-                                                   int ntok = 1) {
+                                                   float target = 0.f, const void* __restrict__ add = nullptr,
+                                                   int ntok = 1, const float* __restrict__ add_scale = nullptr) {
     constexpr int cols = 256 * NV;
+    constexpr bool ADD = !std::is_void<TA>::value;
+    typedef typename std::conditional<ADD, TA, bf16>::type TAV;  // (a loadable type when ADD is off)
+    const TAV* addp = (const TAV*)add;
+    float sb = 1.f;
+    if constexpr (ADD) sb = add_scale != nullptr ? *add_scale : 1.f;
     __shared__ float red[8][2][4 * NV][64];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -284,7 +292,7 @@ __global__ __launch_bounds__(512) void ln_bwd_fast(const TDY* __restrict__ dy, c
             load4(x + row * cols + 4 * lane + 256 * i, xv + 4 * i);
             if (res) load4(res + row * cols + 4 * lane + 256 * i, old + 4 * i);
             if constexpr (ADD) {
-                if (row % ntok != 0) load4(add + row * cols + 4 * lane + 256 * i, av + 4 * i);
+                if (row % ntok != 0) load4(addp + row * cols + 4 * lane + 256 * i, av + 4 * i);
                 else
 #pragma unroll
                     for (int e = 0; e < 4; ++e) av[4 * i + e] = 0.f;
@@ -302,7 +310,7 @@ __global__ __launch_bounds__(512) void ln_bwd_fast(const TDY* __restrict__ dy, c
                 load4(x + nrow * cols + 4 * lane + 256 * i, nxv + 4 * i);
                 if (res) load4(res + nrow * cols + 4 * lane + 256 * i, nold + 4 * i);
                 if constexpr (ADD) {
-                    if (nrow % ntok != 0) load4(add + nrow * cols + 4 * lane + 256 * i, nav + 4 * i);
+                    if (nrow % ntok != 0) load4(addp + nrow * cols + 4 * lane + 256 * i, nav + 4 * i);
                     else
 #pragma unroll
                         for (int e = 0; e < 4; ++e) nav[4 * i + e] = 0.f;
@@ -332,7 +340,7 @@ __global__ __launch_bounds__(512) void ln_bwd_fast(const TDY* __restrict__ dy, c
                 const int k = 4 * i + e;
                 o[e] = rs * (dv[k] * wl[k] - mg - xv[k] * mgx);
                 if (res) o[e] += old[k];
-                if constexpr (ADD) o[e] += av[k];
+                if constexpr (ADD) o[e] += av[k] * sb;
             }
             store4(dx + row * cols + 4 * lane + 256 * i, o);
             if constexpr (DS) {
@@ -507,7 +515,7 @@ void bwd_fast_add(const void* dy, const float* x, const float* w, const float* m
     int64_t blocks = (rows + 7) / 8;
     blocks = blocks > 512 ? 512 : blocks;
     float* part = (dw || db) ? ln_partials(256 * NV) : nullptr;
-    ln_bwd_fast<TDY, float, NV, false, true><<<(unsigned)blocks, 512, 0, s>>>(
+    ln_bwd_fast<TDY, float, NV, false, bf16><<<(unsigned)blocks, 512, 0, s>>>(
         (const TDY*)dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, rows, part, nullptr, 0, nullptr, 0.f, add, ntok);
     if (part) ln_dwdb_reduce_kernel<<<(2 * 256 * NV + 255) / 256, 256, 0, s>>>(part, 256 * NV, dw, db);
 }
@@ -519,6 +527,34 @@ void bwd_add_cols(const void* dy, const float* x, const float* w, const float* m
     if (cols == 512) bwd_fast_add<TDY, 2>(dy, x, w, mean, rstd, res, add, ntok, dx, lp, lp_dt, dw, db, rows, s);
     else if (cols == 768) bwd_fast_add<TDY, 3>(dy, x, w, mean, rstd, res, add, ntok, dx, lp, lp_dt, dw, db, rows, s);
     else bwd_fast_add<TDY, 4>(dy, x, w, mean, rstd, res, add, ntok, dx, lp, lp_dt, dw, db, rows, s);
+}
+
+template <typename TA, int NV>
+void bwd_fast_ds_add(const float* dy, const float* x, const float* w, const float* mean, const float* rstd,
+                     const float* res, const void* add, const float* add_scale, int ntok, float* dx, void* lp, float* dw,
+                     float* db, int64_t rows, float* st, int use, float* spair, float target, hipStream_t s) {
+    int64_t blocks = (rows + 7) / 8;
+    blocks = blocks > 512 ? 512 : blocks;
+    float* part = (dw || db) ? ln_partials(256 * NV) : nullptr;
+    ln_bwd_fast<float, float, NV, true, TA><<<(unsigned)blocks, 512, 0, s>>>(
+        dy, x, w, mean, rstd, res, dx, lp, DCLIP_F16, dw, db, rows, part, st, use, spair, target, add, ntok, add_scale);
+    if (part) ln_dwdb_reduce_kernel<<<(2 * 256 * NV + 255) / 256, 256, 0, s>>>(part, 256 * NV, dw, db);
+}
+
+template <typename TA>
+void bwd_ds_add_cols(const float* dy, const float* x, const float* w, const float* mean, const float* rstd,
+                     const float* res, const void* add, const float* add_scale, int ntok, float* dx, void* lp,
+                     float* dw, float* db, int64_t rows, int64_t cols, float* st, int use, float* spair, float target,
+                     hipStream_t s) {
+    if (cols == 512)
+        bwd_fast_ds_add<TA, 2>(dy, x, w, mean, rstd, res, add, add_scale, ntok, dx, lp, dw, db, rows, st, use, spair,
+                               target, s);
+    else if (cols == 768)
+        bwd_fast_ds_add<TA, 3>(dy, x, w, mean, rstd, res, add, add_scale, ntok, dx, lp, dw, db, rows, st, use, spair,
+                               target, s);
+    else
+        bwd_fast_ds_add<TA, 4>(dy, x, w, mean, rstd, res, add, add_scale, ntok, dx, lp, dw, db, rows, st, use, spair,
+                               target, s);
 }
 
 }  // namespace
@@ -539,6 +575,29 @@ extern "C" int dclip_layernorm_bwd_add(const void* dy, int dy_dt, const float* x
     if (dy_dt == DCLIP_F32)
         bwd_add_cols<float>(dy, x, w, mean, rstd, res, (const bf16*)add, ntok, dx, lp, lp_dt, dw, db, rows, cols, s);
     else bwd_add_cols<bf16>(dy, x, w, mean, rstd, res, (const bf16*)add, ntok, dx, lp, lp_dt, dw, db, rows, cols, s);
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int dclip_layernorm_bwd_scaled_add(const float* dy, const float* x, const float* w, const float* mean,
+                                              const float* rstd, const float* res, const void* add, int add_dt,
+                                              const float* add_scale, int ntok, float* dx, void* lp, float* dw,
+                                              float* db, int64_t rows, int64_t cols, float target, float* st, int use,
+                                              float* spair, void* stream) {
+    DCLIP_HOST_CHECK(cols == 512 || cols == 768 || cols == 1024,
+                     "dclip_layernorm_bwd_scaled_add: cols must be 512, 768 or 1024 (got %lld)", (long long)cols);
+    DCLIP_HOST_CHECK(add != nullptr && ntok > 0 && (add_dt == DCLIP_F16 || add_dt == DCLIP_BF16),
+                     "dclip_layernorm_bwd_scaled_add: a 16-bit add buffer and ntok > 0");
+    DCLIP_HOST_CHECK(lp != nullptr && st != nullptr && spair != nullptr && target > 0.f && use >= 1,
+                     "dclip_layernorm_bwd_scaled_add: lp, the scale state, use >= 1, the scale pair and target > 0");
+    DCLIP_HOST_CHECK(rows > 0, "dclip_layernorm_bwd_scaled_add: rows must be > 0");
+    hipStream_t s = (hipStream_t)stream;
+    if (add_dt == DCLIP_F16)
+        bwd_ds_add_cols<f16>(dy, x, w, mean, rstd, res, add, add_scale, ntok, dx, lp, dw, db, rows, cols, st, use, spair,
+                             target, s);
+    else
+        bwd_ds_add_cols<bf16>(dy, x, w, mean, rstd, res, add, add_scale, ntok, dx, lp, dw, db, rows, cols, st, use,
+                              spair, target, s);
     DCLIP_LAUNCH_CHECK();
     return 0;
 }

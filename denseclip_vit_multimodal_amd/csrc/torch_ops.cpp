@@ -409,6 +409,38 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_bwd_scaled(const Tensor& dy, const 
     return {dx, lp, pair};
 }
 
+// layernorm_bwd_scaled with the previous block's read-out map gradient `add` (16-bit, CLS rows read
+// as 0) times add_scale[1] (a HeadScale (s, 1/s, ..) buffer: the heads' 1/s; optional) added before
+// the delayed-scale fp16 cast
+std::tuple<Tensor, Tensor, Tensor> layernorm_bwd_scaled_add(const Tensor& dy, const Tensor& x, const Tensor& w,
+                                                            const Tensor& mean, const Tensor& rstd,
+                                                            const c10::optional<Tensor>& res, const Tensor& add,
+                                                            const c10::optional<Tensor>& add_scale, int64_t ntok,
+                                                            Tensor& dw, Tensor& db, Tensor& st, int64_t use,
+                                                            double target) {
+    check_gpu(dy, "dy"); check_gpu(x, "x"); check_gpu(w, "w"); check_gpu(mean, "mean"); check_gpu(rstd, "rstd");
+    check_gpu(add, "add"); check_opt(res, "res"); check_opt(add_scale, "add_scale");
+    TORCH_CHECK(x.dim() == 2 && dy.sizes() == x.sizes() && add.sizes() == x.sizes() && x.size(0) > 0,
+                "layernorm_bwd_scaled_add: dy, x and add (rows, cols)");
+    TORCH_CHECK(dy.scalar_type() == at::kFloat && x.scalar_type() == at::kFloat &&
+                    (add.scalar_type() == at::kHalf || add.scalar_type() == at::kBFloat16),
+                "layernorm_bwd_scaled_add: f32 dy and x, a 16-bit add buffer");
+    TORCH_CHECK(ntok > 0 && x.size(0) % ntok == 0, "layernorm_bwd_scaled_add: rows must be a multiple of ntok");
+    check_vec(w, x.size(1), "LayerNorm weight"); check_vec(dw, x.size(1), "dw"); check_vec(db, x.size(1), "db");
+    check_vec(mean, x.size(0), "mean"); check_vec(rstd, x.size(0), "rstd");
+    c10::DeviceGuard g(x.device());
+    Tensor dx = at::empty(x.sizes(), like(x, at::kFloat));
+    Tensor lp = at::empty(x.sizes(), like(x, at::kHalf));
+    Tensor pair = at::empty({4}, x.options());
+    DCLIP_CALL(dclip_layernorm_bwd_scaled_add(ptr<float>(dy), ptr<float>(x), ptr<float>(w), ptr<float>(mean),
+                                              ptr<float>(rstd), optr<float>(res), add.data_ptr(),
+                                              dt_code(add.scalar_type()), scale_entry(add_scale, 1), (int)ntok,
+                                              ptr<float>(dx), lp.data_ptr(), ptr<float>(dw), ptr<float>(db), x.size(0),
+                                              x.size(1), (float)target, scale_state(st, x), (int)use, ptr<float>(pair),
+                                              stream_of(x)));
+    return {dx, lp, pair};
+}
+
 // (x ? x : 0) + s[row % ntok] * y, f32 (rows, cols): a drop_path-scaled residual branch
 Tensor row_scale_add(const c10::optional<Tensor>& x, const Tensor& y, const Tensor& s) {
     check_gpu(y, "y"); check_gpu(s, "s"); check_opt(x, "x");
@@ -852,6 +884,9 @@ TORCH_LIBRARY(dclip, m) {
           "-> (Tensor, Tensor, Tensor)");
     m.def("layernorm_bwd_scaled(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, Tensor? res, Tensor(a!) dw, "
           "Tensor(b!) db, Tensor(c!) st, int use, float target) -> (Tensor, Tensor, Tensor)");
+    m.def("layernorm_bwd_scaled_add(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, Tensor? res, "
+          "Tensor add, Tensor? add_scale, int ntok, Tensor(a!) dw, Tensor(b!) db, Tensor(c!) st, int use, "
+          "float target) -> (Tensor, Tensor, Tensor)");
     m.def("attn_fwd(Tensor qkv, int B, int N, int H, float scale) -> (Tensor, Tensor)");
     m.def("attn_fwd_fp8(Tensor qkv, int B, int N, int H) -> (Tensor, Tensor)");
     m.def("attn_bwd(Tensor qkv, Tensor o, Tensor dout, Tensor lse, int B, int N, int H, float scale) -> Tensor");
@@ -908,6 +943,7 @@ TORCH_LIBRARY_IMPL(dclip, CUDA, m) {
     m.impl("add_readout_amax", &add_readout_amax);
     m.impl("add_readout_cast_scaled", &add_readout_cast_scaled);
     m.impl("layernorm_bwd_scaled", &layernorm_bwd_scaled);
+    m.impl("layernorm_bwd_scaled_add", &layernorm_bwd_scaled_add);
     m.impl("attn_fwd", &attn_fwd);
     m.impl("attn_fwd_fp8", &attn_fwd_fp8);
     m.impl("attn_bwd", &attn_bwd);

@@ -309,10 +309,14 @@ class CLIPVisionTransformer(nn.Module):
                 # read-out without ln_post: produced by the block itself, so its gradient is
                 # folded into the block's backward (ops.BlockFn, meta[5]) — or, bf16, into the next
                 # block's ln_1 backward (meta[9], ops.ReadoutLink)
-                link = ops.ReadoutLink(gh, gw) if (ops.FOLD_READOUT_GRAD and torch.is_grad_enabled() and i < last
-                                                   and cdt == torch.bfloat16 and mdt == torch.bfloat16
-                                                   and dp is None and hsb is None
-                                                   and self.width in (512, 768, 1024)) else None
+                link = None
+                if ops.FOLD_READOUT_GRAD and torch.is_grad_enabled() and i < last and dp is None \
+                        and self.width in (512, 768, 1024):
+                    if cdt == torch.bfloat16 and mdt == torch.bfloat16 and hsb is None:
+                        link = ops.ReadoutLink(gh, gw)
+                    elif cdt == torch.float16 and ds is not None and ops.FP16_DELAYED_SCALE and \
+                            mdt in (torch.float16, torch.bfloat16):
+                        link = ops.ReadoutLink(gh, gw, ds, hsb)
                 bmeta = meta + ((gh, gw, mdt, hsb), dp, ds, link_in, link)
                 tok, fmap = ops.BlockFn.apply(tok, bmeta, *blk.hip_params())
                 if link is not None:

@@ -160,12 +160,17 @@ class ReadoutLink:
     backward) stores it in `g`; the next block's backward adds it inside its ln_1 backward and
     stores the bf16 operand it wrote in `lp`; the map's own block then takes `lp` as its first
     GEMM operand when the gradient autograd hands it IS `g` (the map had no other consumer), and
-    otherwise adds the difference.  Both fields are cleared by the map's block."""
-    __slots__ = ("gh", "gw", "g", "lp")
+    otherwise adds the difference.  Both fields are cleared by the map's block.
 
-    def __init__(self, gh, gw):
-        self.gh, self.gw = gh, gw
-        self.g = self.lp = None
+    fp16 (delayed scales): `ds` / `hsb` are the map block's DelayedScale and HeadScale buffer; the
+    next block's ln_1 backward then adds the map gradient times the heads' 1/s and casts on the
+    map block's MLP-site delayed scale (dclip_layernorm_bwd_scaled_add), handing over the scale
+    pair in `pair` — only once that site is primed."""
+    __slots__ = ("gh", "gw", "g", "lp", "ds", "hsb", "pair")
+
+    def __init__(self, gh, gw, ds=None, hsb=None):
+        self.gh, self.gw, self.ds, self.hsb = gh, gw, ds, hsb
+        self.g = self.lp = self.pair = None
 
 
 def gemm(A, B, epi=N.EPI_STORE, bias=None, aux=None, out_dtype=None, alpha=1.0, scale=None, lp_copy=False):
@@ -291,6 +296,18 @@ def layernorm_bwd_scaled(dy, x, w, mean, rstd, dw, db, res, ds, i):
     st = ds.site(i, x.device)
     _check(dy, x, w, mean, rstd, dw, db, res, st)
     return D().layernorm_bwd_scaled(dy, x, w, mean, rstd, res, dw, db, st, ds.next_use(i), FP16_GRAD_AMAX)
+
+
+def layernorm_bwd_scaled_add(dy, x, w, mean, rstd, dw, db, res, add, ntok, add_scale, ds, i):
+    """layernorm_bwd with res, plus `add` (16-bit, CLS rows read as 0) times *add_scale (optional),
+    and an fp16 copy on site i's delayed scale of the state `ds`: (dx, lp, pair)."""
+    st = ds.site(i, x.device)
+    _check(dy, x, w, mean, rstd, dw, db, res, add, add_scale, st)
+    e0 = _tic()
+    out = D().layernorm_bwd_scaled_add(dy, x, w, mean, rstd, res, add, add_scale, ntok, dw, db, st, ds.next_use(i),
+                                       FP16_GRAD_AMAX)
+    _toc("layernorm_bwd_add", e0)
+    return out
 
 
 def weight_grad(dy, x, want_bias=True, alpha=1.0, db=None, scale=None):
@@ -721,17 +738,17 @@ class BlockFn(torch.autograd.Function):
         dxo = dxo.contiguous()
         lk = ctx.meta[9] if len(ctx.meta) > 9 else None  # this block's read-out map (ReadoutLink)
         if lk is not None:
-            g, lp = lk.g, lk.lp
-            lk.g = lk.lp = None
+            g, lp, pair = lk.g, lk.lp, lk.pair
+            lk.g = lk.lp = lk.pair = None
             if lp is not None:  # the next block's ln_1 backward already added g into dxo
                 if dmap is g:
-                    dy, dmap = lp, None
+                    dy, s1, dmap = lp, pair, None
                 else:  # other consumers joined the map's gradient after g: add the difference
                     d = _readout_grad_dense(g, B, Ntok, lk.gh, lk.gw, C).neg_()
                     if dmap is not None:
                         d += _readout_grad_dense(dmap, B, Ntok, lk.gh, lk.gw, C)
-                    dxo, dmap = dxo + d, None
-        if ds is not None and ds.primed[0]:
+                    dxo, dmap = dxo + _unscale_(d, lk.hsb), None
+        if ds is not None and ds.primed[0] and dy is None:
             base = hsb = None
             if dmap is not None:
                 gh, gw = ctx.meta[5][:2]
@@ -811,10 +828,16 @@ class BlockFn(torch.autograd.Function):
         base = None
         if lk is not None and lk.g is not None and need[0] and C in (512, 768, 1024):  # dclip_layernorm_bwd_add's widths
             base = _readout_grad_buffer(lk.g, B, Ntok, lk.gh, lk.gw, C)
-            base = base if base is not None and base.dtype == torch.bfloat16 else None
-        if base is not None:  # its gradient and the previous block's first GEMM operand from this pass
+            if lk.ds is None:
+                base = base if base is not None and base.dtype == torch.bfloat16 else None
+            elif not (lk.ds.primed[0] and dxh1.dtype == torch.float32 and x.dtype == torch.float32):
+                base = None
+        if base is not None and lk.ds is None:  # its gradient and the previous block's first GEMM operand from this pass
             dxm, lk.lp = layernorm_bwd_add(dxh1, x, ln1w.detach(), mu1, rs1, dln1w, dln1b, dxm, base, Ntok,
                                            torch.bfloat16)
+        elif base is not None:  # fp16: on the previous block's MLP-site delayed scale
+            dxm, lk.lp, lk.pair = layernorm_bwd_scaled_add(dxh1, x, ln1w.detach(), mu1, rs1, dln1w, dln1b, dxm, base,
+                                                           Ntok, lk.hsb, lk.ds, 0)
         else:
             dxm = layernorm_bwd(dxh1, x, ln1w.detach(), mu1, rs1, dln1w, dln1b, res=dxm)
         g = lambda i, t: t if need[i] else None  # noqa: E731

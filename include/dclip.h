@@ -415,6 +415,16 @@ int dclip_layernorm_bwd_scaled(const float* dy, const void* x, int x_dt, const f
 int dclip_layernorm_bwd_add(const void* dy, int dy_dt, const float* x, const float* w, const float* mean,
                             const float* rstd, const float* res, const void* add, int ntok, float* dx, void* lp,
                             int lp_dt, float* dw, float* db, int64_t rows, int64_t cols, void* stream);
+/* The fp16 backward's form: dclip_layernorm_bwd_scaled (f32 dy / x, lp = (f16)(dx * s) on the
+ * delayed scale of st's use `use`, (s, 1/s) to spair) with dx = (res + LN^T(dy)) + add * (*add_scale)
+ * (add: f16 or bf16 (add_dt), CLS rows read as 0; add_scale may be NULL = 1) — in place of
+ * dclip_layernorm_bwd_res + dclip_add_readout_cast_scaled on the same site state.  cols in
+ * {512, 768, 1024}. */
+int dclip_layernorm_bwd_scaled_add(const float* dy, const float* x, const float* w, const float* mean,
+                                   const float* rstd, const float* res, const void* add, int add_dt,
+                                   const float* add_scale, int ntok, float* dx, void* lp, float* dw, float* db,
+                                   int64_t rows, int64_t cols, float target, float* st, int use, float* spair,
+                                   void* stream);
 
 /* Train-mode BatchNorm2d (+ optionally the ReLU after it) on a channels-last 16-bit map viewed as
  * rows (B*H*W) of C channels at a row pitch of ld elements (ld = C for a whole map; larger for a

@@ -143,6 +143,78 @@ def test_layernorm_bwd_scaled(cols):
         s_expect = host_scale(dx1)
 
 
+@pytest.mark.parametrize("adt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("with_scale", [True, False])
+def test_layernorm_bwd_scaled_add(adt, with_scale):
+    """dclip_layernorm_bwd_scaled_add (the fp16 read-out fold: ln_1 backward of the next block +
+    the map gradient times the heads' 1/s, CLS rows masked, + the fp16 operand on the map block's
+    delayed scale) == layernorm_bwd then the add (dx within ulps: another instantiation may contract
+    the multiply-adds differently), lp = (f16)(dx * s) with the previous use's scale (bitwise), the
+    pair; the next call casts with this dx's exact scale."""
+    from denseclip_vit_multimodal_amd import ops
+    rows, cols, ntok = 4 * 257, 768, 257
+    x = torch.randn(rows, cols, device=DEV)
+    w = torch.rand(cols, device=DEV) + 0.5
+    b = torch.randn(cols, device=DEV)
+    _, mean, rstd = ops.layernorm_fwd(x, w, b, torch.float16)
+    dy = torch.randn(rows, cols, device=DEV) * 1e-7
+    res = torch.randn(rows, cols, device=DEV) * 1e-7
+    add = (torch.randn(rows, cols, device=DEV) * 8).to(adt)
+    hs = torch.tensor([2.0 ** 20, 2.0 ** -20, 0.0, 0.0], device=DEV) if with_scale else None
+    dw0, db0 = torch.zeros(cols, device=DEV), torch.zeros(cols, device=DEV)
+    dx0 = ops.layernorm_bwd(dy, x, w, mean, rstd, dw0, db0, res=res)
+    keep = (torch.arange(rows, device=DEV) % ntok != 0)[:, None]
+    ref = torch.where(keep, dx0 + add.float() * (hs[1] if with_scale else 1.0), dx0)
+    ds = _ds_state(2.0 ** 17)
+    s_expect = 2.0 ** 17
+    for it in range(2):
+        dw1, db1 = torch.zeros(cols, device=DEV), torch.zeros(cols, device=DEV)
+        dx1, lp, pair = ops.layernorm_bwd_scaled_add(dy, x, w, mean, rstd, dw1, db1, res, add, ntok, hs, ds, 0)
+        assert rel_err(dx1, ref) < 1e-6
+        assert rel_err(dw1, dw0) < 1e-6 and rel_err(db1, db0) < 1e-6  # atomics: order-dependent sums
+        assert torch.equal(lp, (dx1 * s_expect).half()), it
+        assert pair[:2].cpu().tolist() == [s_expect, 1.0 / s_expect], it
+        s_expect = host_scale(dx1)
+
+
+def test_fp16_readout_grad_fold_matches_unfolded():
+    """ViT-B/16 backbone + fusion neck in fp16 with delayed scales: a first backward primes every
+    block's scales (no fold: a site's first cast is exact), the second folds each read-out map's
+    gradient into the next block's ln_1 backward on the map block's delayed scale
+    (dclip_layernorm_bwd_scaled_add).  Its gradients equal the unfolded path's within the 16-bit
+    noise floor: the two LN instantiations may round dx an ulp apart, and such ulps re-rounded
+    through every fp16 cast of the backward move gradients by ~1e-3 — measured in one process
+    (tools/fold_fp16_probe.py, profiles/r04/r06o_fold_probe.log): fold on vs off 9.9e-4 worst
+    parameter, the output gradient scaled by (1 + 2^-20) 3.4e-3, a repeat 4e-8."""
+    from denseclip_vit_multimodal_amd import DenseCLIP
+    from denseclip_vit_multimodal_amd import ops as O
+    from helpers import CITYSCAPES_CFG, CITYSCAPES_CLASSES, images, spec_state_dict
+    m = DenseCLIP(class_names=CITYSCAPES_CLASSES, **CITYSCAPES_CFG)
+    m.load_state_dict(spec_state_dict("cityscapes"))
+    bb, neck = m.backbone.to(DEV).train(), m.neck.to(DEV).train()
+    x = images(2, 128, 256).to(DEV).half()
+    gen = torch.Generator(device=DEV).manual_seed(4)
+    gout = torch.randn(2, 256, 8, 16, device=DEV, generator=gen) * 1e-4
+    params = [p for p in list(bb.parameters()) + list(neck.parameters()) if p.requires_grad]
+    run = []
+    try:
+        for fold in (False, True):
+            O.FOLD_READOUT_GRAD = fold
+            for blk in bb.transformer.resblocks:
+                blk.__dict__.pop("_dclip_dscale", None)  # fresh delayed-scale states per arm
+            for _ in range(2):
+                for p in params:
+                    p.grad = None
+                out = neck(bb(x))[0]
+                (out.float() * gout).sum().backward()
+            run.append([p.grad.clone() for p in params if p.grad is not None])
+    finally:
+        O.FOLD_READOUT_GRAD = True
+    assert len(run[0]) == len(run[1]) >= 12 * 12
+    worst = max(rel_err(b.float(), a.float()) for a, b in zip(*run))
+    assert worst < 5e-3, worst
+
+
 def test_fp16_delayed_scale_steps_match_exact():
     """ViT-B/16 fp16 backward, three passes with the same data: the first takes the exact scales
     and primes every block's DelayedScale; the later ones cast on the delayed scales (no
