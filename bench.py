@@ -427,7 +427,9 @@ def main():
         # 16-bit flash backward on its (o, lse)), same batch / resolution / dtype otherwise
         release()
         model, opt = setup("F", attn_fp8=True)
-        dt8, s8, loss8 = timed(model, opt, batch, k_sub, 2, silog, world, dist_on)
+        # 3 untimed steps: a fresh model's first steps still build its weight caches, optimizer
+        # state and allocator pools (2 left the fp8 line 5-10 % low on some boxes)
+        dt8, s8, loss8 = timed(model, opt, batch, k_sub, 3, silog, world, dist_on)
         fp8 = {"value": round(world * B * k_sub / dt8, 4), "unit": "images/sec",
                "ms_per_step": round(dt8 / k_sub * 1e3, 2), "loss": round(loss8, 4),
                "what": "BASELINE configs[4]: mode F, seg + depth heads, attention forward with P V on the e4m3 "
@@ -437,8 +439,8 @@ def main():
         # BASELINE configs[3]: ViT-L/14 backbone (C 1024, 24 layers, 16 heads, N = 10659)
         release()
         model, opt = setup("F", arch="vitl14")
-        kl = max(2, k_sub // 2)
-        dtl, sl, lossl = timed(model, opt, batch, kl, 1, silog, world, dist_on)
+        kl = max(3, k_sub // 2)
+        dtl, sl, lossl = timed(model, opt, batch, kl, 2, silog, world, dist_on)
         NL, hl = geometry("vitl14")
         fll = attn_flops_fwd(B, NL, hl)
         vl_val = world * B * kl / dtl

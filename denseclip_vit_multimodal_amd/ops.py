@@ -744,6 +744,7 @@ class BlockFn(torch.autograd.Function):
                 if dmap is g:
                     dy, s1, dmap = lp, pair, None
                 else:  # other consumers joined the map's gradient after g: add the difference
+                    _stat("readout_fold_fixup")
                     d = _readout_grad_dense(g, B, Ntok, lk.gh, lk.gw, C).neg_()
                     if dmap is not None:
                         d += _readout_grad_dense(dmap, B, Ntok, lk.gh, lk.gw, C)
@@ -832,6 +833,8 @@ class BlockFn(torch.autograd.Function):
                 base = base if base is not None and base.dtype == torch.bfloat16 else None
             elif not (lk.ds.primed[0] and dxh1.dtype == torch.float32 and x.dtype == torch.float32):
                 base = None
+        if base is not None:
+            _stat("readout_fold")
         if base is not None and lk.ds is None:  # its gradient and the previous block's first GEMM operand from this pass
             dxm, lk.lp = layernorm_bwd_add(dxh1, x, ln1w.detach(), mu1, rs1, dln1w, dln1b, dxm, base, Ntok,
                                            torch.bfloat16)

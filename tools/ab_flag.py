@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--fp16", action="store_true")
+    ap.add_argument("--fp8", action="store_true", help="the fp8 attention forward (BASELINE configs[4])")
     a = ap.parse_args()
     vals = [eval(v) for v in a.values]  # noqa: S307 (literals from the command line)
     if a.flag.startswith("opt:"):
@@ -45,6 +46,8 @@ def main():
     model = bench.make_model(dev, "F")
     if a.fp16:
         model.backbone.compute_dtype = torch.float16
+    if a.fp8:
+        model.backbone.attn_fp8 = True
     model.train()
     opt = make_optimizer([p for p in model.parameters() if p.requires_grad])
     batch = synth_batch(8, 1024, 2048, dev, 0, image_dtype=torch.float32 if a.fp16 else torch.bfloat16)
@@ -61,6 +64,8 @@ def main():
             ms = (time.perf_counter() - t0) / a.steps * 1e3
             res[repr(v)].append(ms)
             print(f"round {r} {a.flag}={v!r:8}  {ms:8.2f} ms/step  {8e3 / ms:6.2f} img/s", flush=True)
+    from denseclip_vit_multimodal_amd import ops
+    print("path counters:", {k: v for k, v in ops.STATS.items() if "fold" in k or "readout" in k})
     for k, v in res.items():
         s = sorted(v)
         print(f"{a.flag}={k:8} median {s[len(s) // 2]:8.2f} ms/step  ({', '.join(f'{x:.2f}' for x in v)})")
