@@ -453,6 +453,54 @@ def main():
                   "roofline_attn_bwd": roofline(sl, "attn_bwd", 2.5 * fll, PEAK_BF16_TFLOPS),
                   "model_mfma": {"flops_per_image": vl_fl,
                                  "frac": round(vl_val / world * vl_fl / 1e12 / PEAK_BF16_TFLOPS, 4)}}
+    infer = None
+    if extras:
+        # inference forward (eval, seg + depth resized to the image, no grad), bf16 attention vs the
+        # configs[4] fp8 attention forward: where the e4m3 P.V pays (no 16-bit backward behind it)
+        infer = {}
+        k_inf = max(6, args.steps)
+        for name, f8 in (("bf16", False), ("fp8", True)):
+            release()
+            model = make_model(dev, "F", "vitb16").eval()
+            model.backbone.attn_fp8 = f8
+            opt = None
+            dti, si, _ = timed(model, None, batch, k_inf, 3, silog, world, dist_on)
+            infer[name] = {"value": round(world * B * k_inf / dti, 4), "unit": "images/sec",
+                           "ms_per_step": round(dti / k_inf * 1e3, 2), "steps": k_inf,
+                           "roofline_attn_fwd": roofline(si, "attn_fwd_fp8" if f8 else "attn_fwd", fl,
+                                                         PEAK_FP8_MIXED_TFLOPS if f8 else PEAK_BF16_TFLOPS)}
+        infer["fp8_over_bf16"] = round(infer["fp8"]["value"] / infer["bf16"]["value"], 4)
+        infer["what"] = ("inference forward (eval, seg + depth at full resolution, no grad), same batch / resolution, "
+                         "bf16 attention vs the configs[4] fp8 attention forward")
+    ddp1 = None
+    if extras and world == 1 and not dist_on:
+        # DDP's own per-step cost at world size 1: the same mode-F step with the model wrapped in DDP
+        # over an RCCL process group of one rank (fp32 100 MB buckets all-reduced during the backward)
+        release()
+        env_keys = ("MASTER_ADDR", "MASTER_PORT", "RANK", "WORLD_SIZE", "LOCAL_RANK")
+        saved = {k: os.environ.get(k) for k in env_keys}
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1",
+                          LOCAL_RANK=str(local))
+        try:
+            dist.init_process_group("nccl")
+            model, opt = setup("F")
+            model = wrap_ddp(model, dev)
+            opt = make_optimizer([p for p in model.parameters() if p.requires_grad])
+            dtd, _, lossd = timed(model, opt, batch, k_sub, 3, silog, 1, True)
+            ms_d = dtd / k_sub * 1e3
+            ddp1 = {"value": round(B * k_sub / dtd, 4), "unit": "images/sec", "ms_per_step": round(ms_d, 2),
+                    "overhead_vs_headline": round(ms_d / (dt / args.steps * 1e3) - 1.0, 4), "loss": round(lossd, 4),
+                    "what": "mode F under DistributedDataParallel on an RCCL process group of world size 1 (fp32 "
+                            "gradient buckets of 100 MB all-reduced during the backward): DDP's per-step cost"}
+        finally:
+            release()
+            if dist.is_initialized():
+                dist.destroy_process_group()
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
     release()
 
     cpu = cpu0 = None
@@ -525,6 +573,8 @@ def main():
             "fp16": fp16,
             "fp8": fp8,
             "vitl14": vitl14,
+            "infer": infer,
+            "ddp1": ddp1,
             "cpu_baseline": cpu,
             "cpu_baseline_cfg0": cpu0,
             "loss": round(loss, 4),

@@ -30,12 +30,14 @@ _SIGS = {
     "dclip_layernorm_bwd": [_c_void_p, _i32, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32,
                             _c_void_p, _c_void_p, _i64, _i64, _c_void_p],
     "dclip_layernorm_bwd_res": [_c_void_p, _i32, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
-                                _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _i64, _i64, _c_void_p],
+                                _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _i64, _i64, _c_void_p],
+    "dclip_layernorm_bwd_ws_floats": [_i64, _i64],
     "dclip_layernorm_bwd_add": [_c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
-                                _i32, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _i64, _i64, _c_void_p],
+                                _i32, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _i64, _i64,
+                                _c_void_p],
     "dclip_layernorm_bwd_scaled_add": [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
-                                       _i32, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _i64,
-                                       _f32, _c_void_p, _i32, _c_void_p, _c_void_p],
+                                       _i32, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                       _i64, _i64, _f32, _c_void_p, _i32, _c_void_p, _c_void_p],
     "dclip_gemm": [_i32, _i32, _c_void_p, _i64, _c_void_p, _i64, _i64, _i64, _i64, _i32, _f32, _c_void_p, _c_void_p,
                    _c_void_p,
                    _i32, _i64, _c_void_p, _i32, _i64, _c_void_p, _i64, _c_void_p],
@@ -79,8 +81,8 @@ _SIGS = {
     "dclip_add_readout_cast_scaled": [_c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _i64, _i32, _i32,
                                       _f32, _c_void_p, _i32, _c_void_p, _c_void_p],
     "dclip_layernorm_bwd_scaled": [_c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
-                                   _c_void_p, _c_void_p, _c_void_p, _i64, _i64, _f32, _c_void_p, _i32, _c_void_p,
-                                   _c_void_p],
+                                   _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _i64, _f32, _c_void_p, _i32,
+                                   _c_void_p, _c_void_p],
     "dclip_bn_workspace": [_i64, _i32],
     "dclip_bn_fwd": [_i32, _c_void_p, _i64, _i32, _i64, _c_void_p, _c_void_p, _f32, _f32, _c_void_p, _c_void_p,
                      _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p],
@@ -137,6 +139,7 @@ def load(path=None):
         lib.dclip_bn_workspace.restype = ctypes.c_int64
         lib.dclip_attn_fwd_fp8_workspace.restype = ctypes.c_int64
         lib.dclip_row_mean_workspace.restype = ctypes.c_int64
+        lib.dclip_layernorm_bwd_ws_floats.restype = ctypes.c_int64
         # kernel-variant knobs for A/B runs: DCLIP_OPTIONS="id=value,..." (DCLIP_OPT_* ids of dclip.h)
         for kv in filter(None, os.environ.get("DCLIP_OPTIONS", "").split(",")):
             k, v = kv.split("=")

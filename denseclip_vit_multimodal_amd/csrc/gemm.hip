@@ -1451,7 +1451,12 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_tn_big_kernel(const T* __rest
             v += __shfl_xor(v, 16, 64);
             v += __shfl_xor(v, 32, 64);
             const int col = m0 + wm * Cfg::WTM + j * 16 + (lane & 15);
-            if (lq == 0 && col < M) atomicAdd(colsum + col, v * alpha);  // columns past M: clamped copies
+            // columns past M: clamped copies.  SPLITK: this split's partial, summed in split order by
+            // splitk_reduce_kernel (deterministic); STORE has one split, so one add per column
+            if (lq == 0 && col < M) {
+                if constexpr (EPI == DCLIP_EPI_SPLITK) colsum[(int64_t)split * M + col] = v * alpha;
+                else colsum[col] += v * alpha;
+            }
         }
     }
     if constexpr (NW == 4) {
@@ -1511,15 +1516,22 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ x, in
     }
 }
 
-// out[m][n] = sum_z ws[z][m][n] (+ bias[n]) — the split-K combine (deterministic order)
+// out[m][n] = sum_z ws[z][m][n] (+ bias[n]) — the split-K combine (deterministic order); with
+// cs_part (the fused column sums' per-split partials [splits][M]) also colsum[m] += sum_z cs_part[z][m]
 __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, int64_t slab,
                                      int M, int N, const float* __restrict__ bias,
-                                     float* __restrict__ out, int64_t ldo) {
+                                     float* __restrict__ out, int64_t ldo, const float* __restrict__ cs_part = nullptr,
+                                     float* __restrict__ colsum = nullptr) {
     const int64_t total4 = (int64_t)M * (N / 4);
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4;
          i += (int64_t)gridDim.x * blockDim.x) {
         const int m = (int)(i / (N / 4));
         const int n = (int)(i % (N / 4)) * 4;
+        if (cs_part != nullptr && n == 0) {
+            float c = cs_part[m];
+            for (int z = 1; z < splits; ++z) c += cs_part[(int64_t)z * M + m];
+            colsum[m] += c;
+        }
         f32x4 s = *(const f32x4*)(ws + (int64_t)m * N + n);
         for (int z = 1; z < splits; ++z) {
             f32x4 v = *(const f32x4*)(ws + z * slab + (int64_t)m * N + n);
@@ -2236,7 +2248,7 @@ extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda
     DCLIP_HOST_CHECK(epilogue == DCLIP_EPI_STORE || epilogue == DCLIP_EPI_SPLITK,
                      "dclip_gemm_tn: epilogue must be STORE or SPLITK (f32 output)");
     DCLIP_HOST_CHECK(epilogue == DCLIP_EPI_STORE ? splits == 1 : ws != nullptr,
-                     "dclip_gemm_tn: STORE needs splits == 1; SPLITK needs a workspace of splits*M*N f32");
+                     "dclip_gemm_tn: STORE needs splits == 1; SPLITK needs a workspace of splits*(M*N + M) f32");
     DCLIP_HOST_CHECK(ldc % 4 == 0, "dclip_gemm_tn: ldc %% 4 != 0");
     DCLIP_HOST_CHECK(K * lda * 2 < (1ll << 32) && K * ldb * 2 < (1ll << 32),
                      "dclip_gemm_tn: operands must stay below 4 GiB (buffer-load staging)");
@@ -2261,7 +2273,7 @@ extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda
 #define TN_BIG_V(T, EPI, OUT, BKT, STG, CS, NW)                                                                \
     gemm_tn_big_kernel<T, EPI, BKT, STG, CS, NW><<<dim3(tm2 * tn2 * splits), 64 * NW, 0, st>>>(                \
         (const T*)A, lda, (const T*)B, ldb, (int)M, (int)N, (int)K, k_chunk, tm2, tn2, OUT,                     \
-        EPI == DCLIP_EPI_SPLITK ? N : ldc, (int64_t)M * N, alpha, colsum_a)
+        EPI == DCLIP_EPI_SPLITK ? N : ldc, (int64_t)M * N, alpha, EPI == DCLIP_EPI_SPLITK ? cs_part : colsum_a)
 #define TN_BIG(T, EPI, OUT)                                                                                    \
     do {                                                                                                       \
         if (tn_opt == 2) TN_BIG_V(T, EPI, OUT, 32, 4, false, 8);                                               \
@@ -2272,6 +2284,8 @@ extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda
         else TN_BIG_V(T, EPI, OUT, 64, 2, false, 8);                                                           \
     } while (0)
     const int tm2 = (int)((M + 255) / 256), tn2 = (int)((N + 255) / 256);
+    // the fused column sums' per-split partials, past the slabs (SPLITK): summed in split order
+    float* cs_part = (fused_cs && epilogue == DCLIP_EPI_SPLITK) ? (float*)ws + (int64_t)splits * M * N : nullptr;
     if (epilogue == DCLIP_EPI_STORE) {
         DCLIP_HOST_CHECK(bias == nullptr, "dclip_gemm_tn: bias only with SPLITK");
         if (big) {
@@ -2293,7 +2307,7 @@ extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda
         int blocks = (int)((total4 + 255) / 256);
         blocks = blocks > 4096 ? 4096 : blocks;
         splitk_reduce_kernel<<<blocks, 256, 0, st>>>((const float*)ws, splits, M * N, (int)M, (int)N, bias,
-                                                     (float*)C, ldc);
+                                                     (float*)C, ldc, cs_part, colsum_a);
     }
 #undef TN_LAUNCH
 #undef TN_BIG

@@ -11,7 +11,6 @@
 namespace {
 
 constexpr int MAXV = 32;  // elements per lane => cols <= 2048
-constexpr int LN_SHARDS = 16;  // copies of [dw | db] the fast backward's blocks add into
 
 template <typename T>
 __device__ __forceinline__ void load4(const T* p, float* v) {
@@ -234,11 +233,11 @@ __global__ __launch_bounds__(256) void ln_fwd_fast(const TX* __restrict__ x, con
 }
 
 // 8 waves per block and at most 512 blocks: the dw / db partial sums of a block are reduced
-// in LDS and added atomically into one of LN_SHARDS copies of [dw | db] (block b -> copy
-// b % LN_SHARDS, ln_shards: zero on entry), which ln_dwdb_reduce_kernel sums into dw / db and
-// clears again — every block adding into the same 2 * cols floats took 16-23 us of a 112-190 us
-// pass (512 adds per address on 48 cache lines, tools/ln_probe.py); a partials table reduced in
-// a fixed order cost more (the reduction's dependent loads)
+// in LDS and stored as the block's row of the caller's partials table `part` ([block][2][cols],
+// dclip_layernorm_bwd_ws_floats), which ln_dwdb_reduce_kernel sums in block order into dw / db —
+// deterministic, and private to the call (no state shared between streams or graph replays).
+// Without a table the blocks add atomically into dw / db (512 adds per address: 16-23 us of a
+// 112-190 us pass, tools/ln_probe.py)
 //
 // DS (delayed scale, fp16 lp): lp = (f16)(dx * s), s the power-of-two scale of this gradient
 // site's previous use (common.h ds_*: use `use` of the state st), (s, 1/s) to spair for the
@@ -381,7 +380,7 @@ __global__ __launch_bounds__(512) void ln_bwd_fast(const TDY* __restrict__ dy, c
         for (int wv = 0; wv < 8; ++wv) sum += red[wv][which][k][l];
         const int c = 4 * l + 256 * (k / 4) + (k % 4);
         if (part != nullptr) {
-            atomicAdd(part + ((int64_t)(blockIdx.x % LN_SHARDS) * 2 + which) * cols + c, sum);
+            part[((int64_t)blockIdx.x * 2 + which) * cols + c] = sum;
         } else {
             float* out = which ? db : dw;
             if (out) atomicAdd(out + c, sum);
@@ -390,39 +389,38 @@ __global__ __launch_bounds__(512) void ln_bwd_fast(const TDY* __restrict__ dy, c
     if constexpr (DS) ds_end<8>(amax, st, use);
 }
 
-// dw[c] += sum over the shards of part[k][0][c], db[c] += part[k][1][c]; the shards cleared
-__global__ void ln_dwdb_reduce_kernel(float* __restrict__ part, int cols, float* __restrict__ dw,
-                                      float* __restrict__ db) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;  // which * cols + c
-    if (e >= 2 * cols) return;
-    const int which = e / cols, c = e % cols;
-    float v[LN_SHARDS];
-#pragma unroll
-    for (int k = 0; k < LN_SHARDS; ++k) v[k] = part[((int64_t)k * 2 + which) * cols + c];
-#pragma unroll
-    for (int k = 0; k < LN_SHARDS; ++k) part[((int64_t)k * 2 + which) * cols + c] = 0.f;
+// dw[c] += sum_b part[b][0][c], db[c] += sum_b part[b][1][c] over the nblk blocks' rows, in
+// block order (deterministic): a workgroup per 32 consecutive entries of the [2][cols] row, 8 row
+// slices of 32 lanes (128-B row segments), the slices added in LDS in slice order
+__global__ __launch_bounds__(256) void ln_dwdb_reduce_kernel(const float* __restrict__ part, int cols, int nblk,
+                                                             float* __restrict__ dw, float* __restrict__ db) {
+    __shared__ float red[8][32];
+    const int l = threadIdx.x & 31, sl = threadIdx.x >> 5;
+    const int e = blockIdx.x * 32 + l;  // which * cols + c
     float sum = 0.f;
+    if (e < 2 * cols) {
+#pragma unroll 8
+        for (int b = sl; b < nblk; b += 8) sum += part[(int64_t)b * 2 * cols + e];
+    }
+    red[sl][l] = sum;
+    __syncthreads();
+    if (sl == 0 && e < 2 * cols) {
+        float t = 0.f;
 #pragma unroll
-    for (int k = 0; k < LN_SHARDS; ++k) sum += v[k];
-    float* out = which ? db : dw;
-    if (out != nullptr) out[c] += sum;
+        for (int k = 0; k < 8; ++k) t += red[k][l];
+        float* out = e < cols ? dw : db;
+        if (out != nullptr) out[e % cols] += t;
+    }
 }
 
-// the LN_SHARDS copies of [dw | db] (<= 1024 cols), one set per device, zeroed at allocation and
-// left zero by every reduction (the library's ops are stream-ordered: one stream at a time per
-// device)
-float* ln_partials(int cols) {
-    static float* buf[64] = {nullptr};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || cols > 1024) return nullptr;
-    if (buf[dev] == nullptr) {
-        const size_t bytes = (size_t)LN_SHARDS * 2 * 1024 * sizeof(float);
-        if (hipMalloc(&buf[dev], bytes) != hipSuccess || hipMemset(buf[dev], 0, bytes) != hipSuccess) {
-            buf[dev] = nullptr;
-            return nullptr;
-        }
-    }
-    return buf[dev];
+inline int64_t ln_bwd_blocks(int64_t rows) {
+    const int64_t blocks = (rows + 7) / 8;
+    return blocks > 512 ? 512 : blocks;
+}
+
+// the partials table (ws) sum, when the caller gave one and the pass has dw / db
+inline void ln_dwdb_reduce(float* part, int cols, int64_t blocks, float* dw, float* db, hipStream_t st) {
+    if (part) ln_dwdb_reduce_kernel<<<(2 * cols + 31) / 32, 256, 0, st>>>(part, cols, (int)blocks, dw, db);
 }
 
 // blocks of 4 waves: enough persistent waves to fill the chip (8 per SIMD), fewer for small inputs
@@ -440,13 +438,12 @@ void fwd_fast(const void* x, const float* w, const float* b, void* y, float* mea
 
 template <typename TDY, typename TX, int NV>
 void bwd_fast(const void* dy, const void* x, const float* w, const float* mean, const float* rstd, const float* res,
-              float* dx, void* lp, int lp_dt, float* dw, float* db, int64_t rows, hipStream_t st) {
-    int64_t blocks = (rows + 7) / 8;
-    blocks = blocks > 512 ? 512 : blocks;
-    float* part = (dw || db) ? ln_partials(256 * NV) : nullptr;
+              float* dx, void* lp, int lp_dt, float* dw, float* db, float* ws, int64_t rows, hipStream_t st) {
+    const int64_t blocks = ln_bwd_blocks(rows);
+    float* part = (dw || db) ? ws : nullptr;
     ln_bwd_fast<TDY, TX, NV><<<(unsigned)blocks, 512, 0, st>>>((const TDY*)dy, (const TX*)x, w, mean, rstd, res, dx,
                                                               lp, lp_dt, dw, db, rows, part);
-    if (part) ln_dwdb_reduce_kernel<<<(2 * 256 * NV + 255) / 256, 256, 0, st>>>(part, 256 * NV, dw, db);
+    ln_dwdb_reduce(part, 256 * NV, blocks, dw, db, st);
 }
 
 template <typename TX, typename TY>
@@ -472,12 +469,12 @@ void fwd_dispatch_y(int y_dt, const void* x, const float* w, const float* b, voi
 
 template <typename TDY, typename TX>
 void bwd_launch(const void* dy, const void* x, const float* w, const float* mean, const float* rstd,
-                const float* res, float* dx, void* lp, int lp_dt, float* dw, float* db, int64_t rows, int cols,
+                const float* res, float* dx, void* lp, int lp_dt, float* dw, float* db, float* ws, int64_t rows, int cols,
                 hipStream_t st) {
     switch (cols) {
-        case 512: return bwd_fast<TDY, TX, 2>(dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, rows, st);
-        case 768: return bwd_fast<TDY, TX, 3>(dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, rows, st);
-        case 1024: return bwd_fast<TDY, TX, 4>(dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, rows, st);
+        case 512: return bwd_fast<TDY, TX, 2>(dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows, st);
+        case 768: return bwd_fast<TDY, TX, 3>(dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows, st);
+        case 1024: return bwd_fast<TDY, TX, 4>(dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows, st);
         default: break;
     }
     int64_t blocks = (rows + 3) / 4;
@@ -489,71 +486,68 @@ void bwd_launch(const void* dy, const void* x, const float* w, const float* mean
 template <typename TDY>
 void bwd_dispatch_x(int x_dt, const void* dy, const void* x, const float* w, const float* mean,
                     const float* rstd, const float* res, float* dx, void* lp, int lp_dt, float* dw, float* db,
-                    int64_t rows, int cols, hipStream_t st) {
-    if (x_dt == DCLIP_F32) bwd_launch<TDY, float>(dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, rows, cols, st);
-    else if (x_dt == DCLIP_F16) bwd_launch<TDY, f16>(dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, rows, cols, st);
-    else bwd_launch<TDY, bf16>(dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, rows, cols, st);
+                    float* ws, int64_t rows, int cols, hipStream_t st) {
+    if (x_dt == DCLIP_F32) bwd_launch<TDY, float>(dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows, cols, st);
+    else if (x_dt == DCLIP_F16) bwd_launch<TDY, f16>(dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows, cols, st);
+    else bwd_launch<TDY, bf16>(dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows, cols, st);
 }
 
 template <typename TX, int NV>
 void bwd_fast_ds(const float* dy, const void* x, const float* w, const float* mean, const float* rstd,
-                 const float* res, float* dx, void* lp, float* dw, float* db, int64_t rows, float* st, int use,
+                 const float* res, float* dx, void* lp, float* dw, float* db, float* ws, int64_t rows, float* st, int use,
                  float* spair, float target, hipStream_t s) {
-    int64_t blocks = (rows + 7) / 8;
-    blocks = blocks > 512 ? 512 : blocks;
-    float* part = (dw || db) ? ln_partials(256 * NV) : nullptr;
+    const int64_t blocks = ln_bwd_blocks(rows);
+    float* part = (dw || db) ? ws : nullptr;
     ln_bwd_fast<float, TX, NV, true><<<(unsigned)blocks, 512, 0, s>>>(dy, (const TX*)x, w, mean, rstd, res, dx, lp,
                                                                     DCLIP_F16, dw, db, rows, part, st, use, spair,
                                                                     target);
-    if (part) ln_dwdb_reduce_kernel<<<(2 * 256 * NV + 255) / 256, 256, 0, s>>>(part, 256 * NV, dw, db);
+    ln_dwdb_reduce(part, 256 * NV, blocks, dw, db, s);
 }
 
 template <typename TDY, int NV>
 void bwd_fast_add(const void* dy, const float* x, const float* w, const float* mean, const float* rstd,
                   const float* res, const bf16* add, int ntok, float* dx, void* lp, int lp_dt, float* dw, float* db,
-                  int64_t rows, hipStream_t s) {
-    int64_t blocks = (rows + 7) / 8;
-    blocks = blocks > 512 ? 512 : blocks;
-    float* part = (dw || db) ? ln_partials(256 * NV) : nullptr;
+                  float* ws, int64_t rows, hipStream_t s) {
+    const int64_t blocks = ln_bwd_blocks(rows);
+    float* part = (dw || db) ? ws : nullptr;
     ln_bwd_fast<TDY, float, NV, false, bf16><<<(unsigned)blocks, 512, 0, s>>>(
         (const TDY*)dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, rows, part, nullptr, 0, nullptr, 0.f, add, ntok);
-    if (part) ln_dwdb_reduce_kernel<<<(2 * 256 * NV + 255) / 256, 256, 0, s>>>(part, 256 * NV, dw, db);
+    ln_dwdb_reduce(part, 256 * NV, blocks, dw, db, s);
 }
 
 template <typename TDY>
 void bwd_add_cols(const void* dy, const float* x, const float* w, const float* mean, const float* rstd,
                   const float* res, const bf16* add, int ntok, float* dx, void* lp, int lp_dt, float* dw, float* db,
-                  int64_t rows, int64_t cols, hipStream_t s) {
-    if (cols == 512) bwd_fast_add<TDY, 2>(dy, x, w, mean, rstd, res, add, ntok, dx, lp, lp_dt, dw, db, rows, s);
-    else if (cols == 768) bwd_fast_add<TDY, 3>(dy, x, w, mean, rstd, res, add, ntok, dx, lp, lp_dt, dw, db, rows, s);
-    else bwd_fast_add<TDY, 4>(dy, x, w, mean, rstd, res, add, ntok, dx, lp, lp_dt, dw, db, rows, s);
+                  float* ws, int64_t rows, int64_t cols, hipStream_t s) {
+    if (cols == 512) bwd_fast_add<TDY, 2>(dy, x, w, mean, rstd, res, add, ntok, dx, lp, lp_dt, dw, db, ws, rows, s);
+    else if (cols == 768) bwd_fast_add<TDY, 3>(dy, x, w, mean, rstd, res, add, ntok, dx, lp, lp_dt, dw, db, ws, rows, s);
+    else bwd_fast_add<TDY, 4>(dy, x, w, mean, rstd, res, add, ntok, dx, lp, lp_dt, dw, db, ws, rows, s);
 }
 
 template <typename TA, int NV>
 void bwd_fast_ds_add(const float* dy, const float* x, const float* w, const float* mean, const float* rstd,
                      const float* res, const void* add, const float* add_scale, int ntok, float* dx, void* lp, float* dw,
-                     float* db, int64_t rows, float* st, int use, float* spair, float target, hipStream_t s) {
-    int64_t blocks = (rows + 7) / 8;
-    blocks = blocks > 512 ? 512 : blocks;
-    float* part = (dw || db) ? ln_partials(256 * NV) : nullptr;
+                     float* db, float* ws, int64_t rows, float* st, int use, float* spair, float target, hipStream_t s) {
+    const int64_t blocks = ln_bwd_blocks(rows);
+    float* part = (dw || db) ? ws : nullptr;
     ln_bwd_fast<float, float, NV, true, TA><<<(unsigned)blocks, 512, 0, s>>>(
         dy, x, w, mean, rstd, res, dx, lp, DCLIP_F16, dw, db, rows, part, st, use, spair, target, add, ntok, add_scale);
-    if (part) ln_dwdb_reduce_kernel<<<(2 * 256 * NV + 255) / 256, 256, 0, s>>>(part, 256 * NV, dw, db);
+    ln_dwdb_reduce(part, 256 * NV, blocks, dw, db, s);
 }
 
 template <typename TA>
 void bwd_ds_add_cols(const float* dy, const float* x, const float* w, const float* mean, const float* rstd,
                      const float* res, const void* add, const float* add_scale, int ntok, float* dx, void* lp,
-                     float* dw, float* db, int64_t rows, int64_t cols, float* st, int use, float* spair, float target,
+                     float* dw, float* db, float* ws, int64_t rows, int64_t cols, float* st, int use, float* spair, float target,
                      hipStream_t s) {
     if (cols == 512)
-        bwd_fast_ds_add<TA, 2>(dy, x, w, mean, rstd, res, add, add_scale, ntok, dx, lp, dw, db, rows, st, use, spair,
+        bwd_fast_ds_add<TA, 2>(dy, x, w, mean, rstd, res, add, add_scale, ntok, dx, lp, dw, db, ws, rows, st, use, spair,
                                target, s);
     else if (cols == 768)
-        bwd_fast_ds_add<TA, 3>(dy, x, w, mean, rstd, res, add, add_scale, ntok, dx, lp, dw, db, rows, st, use, spair,
+        bwd_fast_ds_add<TA, 3>(dy, x, w, mean, rstd, res, add, add_scale, ntok, dx, lp, dw, db, ws, rows, st, use, spair,
                                target, s);
     else
-        bwd_fast_ds_add<TA, 4>(dy, x, w, mean, rstd, res, add, add_scale, ntok, dx, lp, dw, db, rows, st, use, spair,
+        bwd_fast_ds_add<TA, 4>(dy, x, w, mean, rstd, res, add, add_scale, ntok, dx, lp, dw, db, ws, rows, st, use, spair,
                                target, s);
 }
 
@@ -561,7 +555,7 @@ void bwd_ds_add_cols(const float* dy, const float* x, const float* w, const floa
 
 extern "C" int dclip_layernorm_bwd_add(const void* dy, int dy_dt, const float* x, const float* w, const float* mean,
                                        const float* rstd, const float* res, const void* add, int ntok, float* dx,
-                                       void* lp, int lp_dt, float* dw, float* db, int64_t rows, int64_t cols,
+                                       void* lp, int lp_dt, float* dw, float* db, float* ws, int64_t rows, int64_t cols,
                                        void* stream) {
     DCLIP_HOST_CHECK(cols == 512 || cols == 768 || cols == 1024,
                      "dclip_layernorm_bwd_add: cols must be 512, 768 or 1024 (got %lld)", (long long)cols);
@@ -573,8 +567,8 @@ extern "C" int dclip_layernorm_bwd_add(const void* dy, int dy_dt, const float* x
     if (rows == 0) return 0;
     hipStream_t s = (hipStream_t)stream;
     if (dy_dt == DCLIP_F32)
-        bwd_add_cols<float>(dy, x, w, mean, rstd, res, (const bf16*)add, ntok, dx, lp, lp_dt, dw, db, rows, cols, s);
-    else bwd_add_cols<bf16>(dy, x, w, mean, rstd, res, (const bf16*)add, ntok, dx, lp, lp_dt, dw, db, rows, cols, s);
+        bwd_add_cols<float>(dy, x, w, mean, rstd, res, (const bf16*)add, ntok, dx, lp, lp_dt, dw, db, ws, rows, cols, s);
+    else bwd_add_cols<bf16>(dy, x, w, mean, rstd, res, (const bf16*)add, ntok, dx, lp, lp_dt, dw, db, ws, rows, cols, s);
     DCLIP_LAUNCH_CHECK();
     return 0;
 }
@@ -582,7 +576,7 @@ extern "C" int dclip_layernorm_bwd_add(const void* dy, int dy_dt, const float* x
 extern "C" int dclip_layernorm_bwd_scaled_add(const float* dy, const float* x, const float* w, const float* mean,
                                               const float* rstd, const float* res, const void* add, int add_dt,
                                               const float* add_scale, int ntok, float* dx, void* lp, float* dw,
-                                              float* db, int64_t rows, int64_t cols, float target, float* st, int use,
+                                              float* db, float* ws, int64_t rows, int64_t cols, float target, float* st, int use,
                                               float* spair, void* stream) {
     DCLIP_HOST_CHECK(cols == 512 || cols == 768 || cols == 1024,
                      "dclip_layernorm_bwd_scaled_add: cols must be 512, 768 or 1024 (got %lld)", (long long)cols);
@@ -593,10 +587,10 @@ extern "C" int dclip_layernorm_bwd_scaled_add(const float* dy, const float* x, c
     DCLIP_HOST_CHECK(rows > 0, "dclip_layernorm_bwd_scaled_add: rows must be > 0");
     hipStream_t s = (hipStream_t)stream;
     if (add_dt == DCLIP_F16)
-        bwd_ds_add_cols<f16>(dy, x, w, mean, rstd, res, add, add_scale, ntok, dx, lp, dw, db, rows, cols, st, use, spair,
+        bwd_ds_add_cols<f16>(dy, x, w, mean, rstd, res, add, add_scale, ntok, dx, lp, dw, db, ws, rows, cols, st, use, spair,
                              target, s);
     else
-        bwd_ds_add_cols<bf16>(dy, x, w, mean, rstd, res, add, add_scale, ntok, dx, lp, dw, db, rows, cols, st, use,
+        bwd_ds_add_cols<bf16>(dy, x, w, mean, rstd, res, add, add_scale, ntok, dx, lp, dw, db, ws, rows, cols, st, use,
                               spair, target, s);
     DCLIP_LAUNCH_CHECK();
     return 0;
@@ -604,7 +598,7 @@ extern "C" int dclip_layernorm_bwd_scaled_add(const float* dy, const float* x, c
 
 extern "C" int dclip_layernorm_bwd_scaled(const float* dy, const void* x, int x_dt, const float* w, const float* mean,
                                           const float* rstd, const float* res, float* dx, void* lp, float* dw,
-                                          float* db, int64_t rows, int64_t cols, float target, float* st, int use,
+                                          float* db, float* ws, int64_t rows, int64_t cols, float target, float* st, int use,
                                           float* spair, void* stream) {
     DCLIP_HOST_CHECK(cols == 512 || cols == 768 || cols == 1024,
                      "dclip_layernorm_bwd_scaled: cols must be 512, 768 or 1024 (got %lld)", (long long)cols);
@@ -613,9 +607,9 @@ extern "C" int dclip_layernorm_bwd_scaled(const float* dy, const void* x, int x_
                      "dclip_layernorm_bwd_scaled: lp, the scale state, use >= 1, the scale pair and target > 0");
     DCLIP_HOST_CHECK(rows > 0, "dclip_layernorm_bwd_scaled: rows must be > 0");
     hipStream_t s = (hipStream_t)stream;
-    if (cols == 512) bwd_fast_ds<float, 2>(dy, x, w, mean, rstd, res, dx, lp, dw, db, rows, st, use, spair, target, s);
-    else if (cols == 768) bwd_fast_ds<float, 3>(dy, x, w, mean, rstd, res, dx, lp, dw, db, rows, st, use, spair, target, s);
-    else bwd_fast_ds<float, 4>(dy, x, w, mean, rstd, res, dx, lp, dw, db, rows, st, use, spair, target, s);
+    if (cols == 512) bwd_fast_ds<float, 2>(dy, x, w, mean, rstd, res, dx, lp, dw, db, ws, rows, st, use, spair, target, s);
+    else if (cols == 768) bwd_fast_ds<float, 3>(dy, x, w, mean, rstd, res, dx, lp, dw, db, ws, rows, st, use, spair, target, s);
+    else bwd_fast_ds<float, 4>(dy, x, w, mean, rstd, res, dx, lp, dw, db, ws, rows, st, use, spair, target, s);
     DCLIP_LAUNCH_CHECK();
     return 0;
 }
@@ -635,9 +629,15 @@ extern "C" int dclip_layernorm_fwd(const void* x, int x_dt, const float* w, cons
     return 0;
 }
 
+extern "C" int64_t dclip_layernorm_bwd_ws_floats(int64_t rows, int64_t cols) {
+    if (rows <= 0 || !(cols == 512 || cols == 768 || cols == 1024)) return 0;
+    return ln_bwd_blocks(rows) * 2 * cols;
+}
+
 extern "C" int dclip_layernorm_bwd_res(const void* dy, int dy_dt, const void* x, int x_dt, const float* w,
                                        const float* mean, const float* rstd, const float* res, float* dx, void* lp,
-                                       int lp_dt, float* dw, float* db, int64_t rows, int64_t cols, void* stream) {
+                                       int lp_dt, float* dw, float* db, float* ws, int64_t rows, int64_t cols,
+                                       void* stream) {
     DCLIP_HOST_CHECK(cols > 0 && cols % 4 == 0 && cols <= 64 * MAXV,
                      "dclip_layernorm_bwd: cols=%lld must be a multiple of 4 and <= %d", (long long)cols, 64 * MAXV);
     DCLIP_HOST_CHECK(lp == nullptr || lp_dt == DCLIP_BF16 || lp_dt == DCLIP_F16,
@@ -645,10 +645,10 @@ extern "C" int dclip_layernorm_bwd_res(const void* dy, int dy_dt, const void* x,
     if (rows == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
     if (dy_dt == DCLIP_F32)
-        bwd_dispatch_x<float>(x_dt, dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, rows, (int)cols, st);
+        bwd_dispatch_x<float>(x_dt, dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows, (int)cols, st);
     else if (dy_dt == DCLIP_F16)
-        bwd_dispatch_x<f16>(x_dt, dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, rows, (int)cols, st);
-    else bwd_dispatch_x<bf16>(x_dt, dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, rows, (int)cols, st);
+        bwd_dispatch_x<f16>(x_dt, dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows, (int)cols, st);
+    else bwd_dispatch_x<bf16>(x_dt, dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows, (int)cols, st);
     DCLIP_LAUNCH_CHECK();
     return 0;
 }
@@ -657,5 +657,5 @@ extern "C" int dclip_layernorm_bwd(const void* dy, int dy_dt, const void* x, int
                                    const float* mean, const float* rstd, float* dx, int accumulate,
                                    float* dw, float* db, int64_t rows, int64_t cols, void* stream) {
     return dclip_layernorm_bwd_res(dy, dy_dt, x, x_dt, w, mean, rstd, accumulate ? dx : nullptr, dx, nullptr, 0, dw,
-                                   db, rows, cols, stream);
+                                   db, nullptr, rows, cols, stream);
 }

@@ -71,6 +71,13 @@ const float* scale_entry(const c10::optional<Tensor>& t, int i) {
 at::TensorOptions like(const Tensor& t, at::ScalarType dt) { return t.options().dtype(dt); }
 
 // ----------------------------------------------------------------------------- LayerNorm
+// the LN backward's per-workgroup dw / db partials: private scratch of the call from the caching
+// allocator (stream-ordered), or none when the pass has no dw / db or the width has no table
+Tensor ln_ws(const Tensor& x, const Tensor& dw, const Tensor& db) {
+    const int64_t n = (dw.defined() || db.defined()) ? dclip_layernorm_bwd_ws_floats(x.size(0), x.size(1)) : 0;
+    return n > 0 ? at::empty({n}, like(x, at::kFloat)) : Tensor();
+}
+
 std::tuple<Tensor, Tensor, Tensor> layernorm_fwd(const Tensor& x, const Tensor& w, const Tensor& b,
                                                  at::ScalarType out_dtype, double eps) {
     check_gpu(x, "x"); check_gpu(w, "w"); check_gpu(b, "b");
@@ -96,9 +103,11 @@ Tensor layernorm_bwd(const Tensor& dy, const Tensor& x, const Tensor& w, const T
     check_vec(mean, x.size(0), "mean"); check_vec(rstd, x.size(0), "rstd");
     c10::DeviceGuard g(x.device());
     Tensor dx = at::empty(x.sizes(), like(x, at::kFloat));
+    Tensor ws = ln_ws(x, dw, db);
     DCLIP_CALL(dclip_layernorm_bwd_res(dy.data_ptr(), dt_code(dy.scalar_type()), x.data_ptr(), dt_code(x.scalar_type()),
                                        ptr<float>(w), ptr<float>(mean), ptr<float>(rstd), optr<float>(res), ptr<float>(dx),
-                                       nullptr, 0, ptr<float>(dw), ptr<float>(db), x.size(0), x.size(1), stream_of(x)));
+                                       nullptr, 0, ptr<float>(dw), ptr<float>(db), ptr<float>(ws), x.size(0), x.size(1),
+                                       stream_of(x)));
     return dx;
 }
 
@@ -114,10 +123,11 @@ std::tuple<Tensor, Tensor> layernorm_bwd_lp(const Tensor& dy, const Tensor& x, c
     c10::DeviceGuard g(x.device());
     Tensor dx = at::empty(x.sizes(), like(x, at::kFloat));
     Tensor lp = at::empty(x.sizes(), like(x, lp_dtype));
+    Tensor ws = ln_ws(x, dw, db);
     DCLIP_CALL(dclip_layernorm_bwd_res(dy.data_ptr(), dt_code(dy.scalar_type()), x.data_ptr(), dt_code(x.scalar_type()),
                                        ptr<float>(w), ptr<float>(mean), ptr<float>(rstd), optr<float>(res), ptr<float>(dx),
-                                       lp.data_ptr(), dt_code(lp_dtype), ptr<float>(dw), ptr<float>(db), x.size(0),
-                                       x.size(1), stream_of(x)));
+                                       lp.data_ptr(), dt_code(lp_dtype), ptr<float>(dw), ptr<float>(db), ptr<float>(ws),
+                                       x.size(0), x.size(1), stream_of(x)));
     return {dx, lp};
 }
 
@@ -138,10 +148,11 @@ std::tuple<Tensor, Tensor> layernorm_bwd_add(const Tensor& dy, const Tensor& x, 
     c10::DeviceGuard g(x.device());
     Tensor dx = at::empty(x.sizes(), like(x, at::kFloat));
     Tensor lp = at::empty(x.sizes(), like(x, lp_dtype));
+    Tensor ws = ln_ws(x, dw, db);
     DCLIP_CALL(dclip_layernorm_bwd_add(dy.data_ptr(), dt_code(dy.scalar_type()), ptr<float>(x), ptr<float>(w),
                                        ptr<float>(mean), ptr<float>(rstd), optr<float>(res), add.data_ptr(), (int)ntok,
                                        ptr<float>(dx), lp.data_ptr(), dt_code(lp_dtype), ptr<float>(dw), ptr<float>(db),
-                                       x.size(0), x.size(1), stream_of(x)));
+                                       ptr<float>(ws), x.size(0), x.size(1), stream_of(x)));
     return {dx, lp};
 }
 
@@ -247,7 +258,7 @@ Tensor weight_grad(const Tensor& dy, const Tensor& x, double alpha, c10::optiona
     int64_t k_pad = 0;
     DCLIP_CALL(dclip_gemm_tn_plan(N, K, M, &splits, &k_pad));
     Tensor dW = at::empty({N, K}, like(dy, at::kFloat));
-    Tensor ws = at::empty({(int64_t)splits * N * K}, like(dy, at::kFloat));
+    Tensor ws = at::empty({(int64_t)splits * (N * K + N)}, like(dy, at::kFloat));
     DCLIP_CALL(dclip_gemm_tn(DCLIP_EPI_SPLITK, dt_code(dy.scalar_type()), dy.data_ptr(), dy.stride(0), x.data_ptr(),
                              x.stride(0), N, K, M, k_pad, splits, (float)alpha, scale_entry(scale, 1), nullptr, ws.data_ptr(),
                              dW.data_ptr(), K,
@@ -402,9 +413,10 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_bwd_scaled(const Tensor& dy, const 
     Tensor dx = at::empty(x.sizes(), like(x, at::kFloat));
     Tensor lp = at::empty(x.sizes(), like(x, at::kHalf));
     Tensor pair = at::empty({4}, x.options());
+    Tensor ws = ln_ws(x, dw, db);
     DCLIP_CALL(dclip_layernorm_bwd_scaled(ptr<float>(dy), x.data_ptr(), dt_code(x.scalar_type()), ptr<float>(w),
                                           ptr<float>(mean), ptr<float>(rstd), optr<float>(res), ptr<float>(dx),
-                                          lp.data_ptr(), ptr<float>(dw), ptr<float>(db), x.size(0), x.size(1),
+                                          lp.data_ptr(), ptr<float>(dw), ptr<float>(db), ptr<float>(ws), x.size(0), x.size(1),
                                           (float)target, scale_state(st, x), (int)use, ptr<float>(pair), stream_of(x)));
     return {dx, lp, pair};
 }
@@ -432,10 +444,12 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_bwd_scaled_add(const Tensor& dy, co
     Tensor dx = at::empty(x.sizes(), like(x, at::kFloat));
     Tensor lp = at::empty(x.sizes(), like(x, at::kHalf));
     Tensor pair = at::empty({4}, x.options());
+    Tensor ws = ln_ws(x, dw, db);
     DCLIP_CALL(dclip_layernorm_bwd_scaled_add(ptr<float>(dy), ptr<float>(x), ptr<float>(w), ptr<float>(mean),
                                               ptr<float>(rstd), optr<float>(res), add.data_ptr(),
                                               dt_code(add.scalar_type()), scale_entry(add_scale, 1), (int)ntok,
-                                              ptr<float>(dx), lp.data_ptr(), ptr<float>(dw), ptr<float>(db), x.size(0),
+                                              ptr<float>(dx), lp.data_ptr(), ptr<float>(dw), ptr<float>(db),
+                                              ptr<float>(ws), x.size(0),
                                               x.size(1), (float)target, scale_state(st, x), (int)use, ptr<float>(pair),
                                               stream_of(x)));
     return {dx, lp, pair};

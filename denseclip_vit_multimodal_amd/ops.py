@@ -11,6 +11,7 @@ Numerics (the contract checked by tests/test_gpu_parity.py):
     accumulation; softmax statistics are fp32.
 """
 import math
+import weakref
 
 import torch
 
@@ -239,10 +240,47 @@ def grad_scale(g, cdt):
 # fp16 backward: the block gradients' casts on DELAYED scales (the previous step's maximum at the
 # same site; dclip_add_readout_cast_scaled / dclip_layernorm_bwd_scaled) — one pass where the
 # exact scale needs a maximum pass and a cast pass.  False: exact scales every step.
+#
+# Overflow contract (torch.cuda.amp.GradScaler's): a gradient that grows more than
+# 65504 / FP16_GRAD_AMAX = 4096x between two backwards of a site overflows to inf in its
+# fp16 copy, so that backward's parameter gradients are non-finite — never silently wrong finite
+# values.  Such a step must be skipped: train.train_step / train.step_unless_nonfinite do it (a
+# plain `loss.backward(); opt.step()` loop would apply the inf / NaN update, as it would with
+# GradScaler's scaled gradients), and the non-finite flag they compute re-primes every site
+# (watch_fp16_overflow), so the next backward takes exact scales and the one after is delayed
+# again.  A backward captured into a graph (torch.cuda.graph) takes exact scales: the delayed
+# scales' use counter is host state a replay could not advance.
 FP16_DELAYED_SCALE = True
 
 
 DS_STATE_FLOATS = 196  # DCLIP_DS_STATE_FLOATS (include/dclip.h)
+
+
+_DELAYED = weakref.WeakSet()  # every DelayedScale (re-primed together after an overflowed step)
+_OVERFLOW_WATCH = []  # (event, pinned host copy of a non-finite flag) not yet read
+
+
+def watch_fp16_overflow(flag):
+    """Queue a device-side non-finite-gradient flag (train.nonfinite_flag) for the delayed fp16
+    scales: once the copy has landed (an event query, never a wait) a non-zero flag re-primes every
+    site, so the next backward takes exact scales instead of scales from an overflowed step's
+    maxima (whose non-finite values keep the previous, too large, scale at every later site)."""
+    if not _DELAYED or not flag.is_cuda or torch.cuda.is_current_stream_capturing():
+        return
+    host = torch.empty((), dtype=torch.float32, pin_memory=True)
+    host.copy_(flag.detach().reshape(()).float(), non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    _OVERFLOW_WATCH.append((ev, host))
+
+
+def _poll_fp16_overflow():
+    while _OVERFLOW_WATCH and _OVERFLOW_WATCH[0][0].query():
+        _, host = _OVERFLOW_WATCH.pop(0)
+        if float(host) != 0.0:
+            _stat("fp16_scale_reprime")
+            for ds in list(_DELAYED):
+                ds.uses = [0, 0]
 
 
 class DelayedScale:
@@ -256,6 +294,7 @@ class DelayedScale:
     def __init__(self):
         self.buf = None
         self.uses = [0, 0]
+        _DELAYED.add(self)
 
     @property
     def primed(self):
@@ -480,8 +519,11 @@ def _stamp_stepped_params(opt, *_):
 # weight at its first use in the next forward / backward
 EAGER_WEIGHT_REFRESH = True
 # bf16 blocks: the dX GEMMs feeding the two LayerNorm backward passes write their gradient in bf16
-# (the rounding the reference's autocast linear applies to its input gradient) instead of fp32 —
-# 100 MB less written by the GEMM and read by the LN pass per call at the headline shape
+# instead of fp32 — 100 MB less written by the GEMM and read by the LN pass per call at the
+# headline shape.  An intentional precision trade-off of the bf16 THROUGHPUT line, not reference
+# parity (the reference trains in fp32 and has no autocast): one more bf16 rounding of each LN
+# input gradient, which tests/emulation16.py models and tests/test_gpu_grad_parity.py bounds
+# against the fp32 reference restatement.  The parity dtype (fp16, the default for fp32 images) never takes it.
 LN_DY_LP = True
 _REFRESH_DESC = {}  # (device, dtype) -> (key, device descriptor, tiles, pinned host copy)
 
@@ -720,8 +762,11 @@ class BlockFn(torch.autograd.Function):
         dp = ctx.meta[6] if len(ctx.meta) > 6 else None
         # fp16 delayed scales (meta[7], a DelayedScale): only on the plain residual form
         C = x.shape[1]
+        capturing = torch.cuda.is_current_stream_capturing()
         ds = ctx.meta[7] if (len(ctx.meta) > 7 and cdt == torch.float16 and dp is None and FP16_DELAYED_SCALE
-                             and C in (512, 768, 1024)) else None  # the widths dclip_layernorm_bwd_scaled takes
+                             and C in (512, 768, 1024) and not capturing) else None  # the widths dclip_layernorm_bwd_scaled takes
+        if ds is not None:
+            _poll_fp16_overflow()
         scale = (C // H) ** -0.5
         need = ctx.needs_input_grad
         wg = any(need[2:])
@@ -831,7 +876,7 @@ class BlockFn(torch.autograd.Function):
             base = _readout_grad_buffer(lk.g, B, Ntok, lk.gh, lk.gw, C)
             if lk.ds is None:
                 base = base if base is not None and base.dtype == torch.bfloat16 else None
-            elif not (lk.ds.primed[0] and dxh1.dtype == torch.float32 and x.dtype == torch.float32):
+            elif capturing or not (lk.ds.primed[0] and dxh1.dtype == torch.float32 and x.dtype == torch.float32):
                 base = None
         if base is not None:
             _stat("readout_fold")

@@ -148,6 +148,9 @@ def nonfinite_flag(opt, loss, check_grads=True):
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+    if check_grads:  # an overflowed fp16 step re-primes the delayed gradient scales (ops.FP16_DELAYED_SCALE)
+        from . import ops
+        ops.watch_fp16_overflow(flag)
     return flag
 
 

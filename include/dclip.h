@@ -111,7 +111,15 @@ int dclip_layernorm_bwd(const void* dy, int dy_dt, const void* x, int x_dt,
 int dclip_layernorm_bwd_res(const void* dy, int dy_dt, const void* x, int x_dt,
                             const float* w, const float* mean, const float* rstd,
                             const float* res, float* dx, void* lp, int lp_dt, float* dw, float* db,
-                            int64_t rows, int64_t cols, void* stream);
+                            float* ws, int64_t rows, int64_t cols, void* stream);
+/* ws (ABI 5; dclip_layernorm_bwd_res, _scaled, _add, _scaled_add): the caller's scratch of
+ * dclip_layernorm_bwd_ws_floats(rows, cols) floats (contents on entry irrelevant, clobbered) for
+ * the per-workgroup dw / db partials, summed into dw / db in a fixed order (deterministic) by a
+ * second launch on the same stream; private to the call, so concurrent calls on different
+ * streams or graph replays never share it.  NULL: the workgroups add atomically into dw / db
+ * (correct, summation order not fixed).  Widths without the fast kernels (cols not 512 / 768 /
+ * 1024; the query returns 0 for them) always add atomically.                               */
+int64_t dclip_layernorm_bwd_ws_floats(int64_t rows, int64_t cols);
 
 /* C[m][n] = alpha * sum_k A[m][k] * B[n][k]  ("NT": both operands k-contiguous, ab_dt in
  * {F16, BF16}), m < M, n < N, k < K (K % 64 == 0, lda/ldb % 8 == 0), then the
@@ -130,10 +138,12 @@ int dclip_gemm(int epilogue, int ab_dt,
  * the weight-gradient shape dW = dY^T X without transposed copies).  A: (K, lda >= M),
  * B: (K, ldb >= N), M % 8 == N % 8 == 0.  The K range is split into `splits` chunks of
  * K_pad / splits (K_pad >= K, multiple of 64*splits; rows >= K contribute zero).
- * epilogue STORE (f32 C, splits == 1) or SPLITK (f32 slabs in ws, splits*M*N, then a
- * combine that adds bias[n] when non-null).  colsum_a (f32, M), when non-null, receives
- * += alpha * the column sums of A over the K rows (the bias gradient of dY).  alpha_ptr
- * as in dclip_gemm.                                                                   */
+ * epilogue STORE (f32 C, splits == 1) or SPLITK (f32 slabs in ws, then a combine that adds
+ * bias[n] when non-null; ws holds splits*(M*N + M) floats: the slabs, then (ABI 5) the column
+ * sums' per-split partials).  colsum_a (f32, M), when non-null, receives += alpha * the column
+ * sums of A over the K rows (the bias gradient of dY) — in a fixed order (deterministic) on the
+ * 256x256 path (M, N >= 256), by per-row-chunk atomics on the small-tile path.  alpha_ptr as in
+ * dclip_gemm.                                                                          */
 /* The K-split plan dclip_gemm_tn runs best with for an M x N output over K rows
  * (splits, and K_pad = K rounded up to 64*splits); host-side only, no GPU work.      */
 int dclip_gemm_tn_plan(int64_t M, int64_t N, int64_t K, int* splits, int64_t* K_pad);
@@ -402,8 +412,8 @@ int dclip_add_readout_cast_scaled(const float* a, const void* b, int b_dt, const
                                   float* spair, void* stream);
 int dclip_layernorm_bwd_scaled(const float* dy, const void* x, int x_dt, const float* w, const float* mean,
                                const float* rstd, const float* res, float* dx, void* lp, float* dw, float* db,
-                               int64_t rows, int64_t cols, float target, float* st, int use, float* spair,
-                               void* stream);
+                               float* ws, int64_t rows, int64_t cols, float target, float* st, int use,
+                               float* spair, void* stream);
 
 /* LayerNorm backward of a block's ln_1 with the PREVIOUS block's read-out map gradient folded in
  * (models.py:243-249 backward + the models.py:565 -> 577-597 read-out's gradient):
@@ -414,7 +424,7 @@ int dclip_layernorm_bwd_scaled(const float* dy, const void* x, int x_dt, const f
  * dw / db accumulate as in dclip_layernorm_bwd_res (may be NULL). */
 int dclip_layernorm_bwd_add(const void* dy, int dy_dt, const float* x, const float* w, const float* mean,
                             const float* rstd, const float* res, const void* add, int ntok, float* dx, void* lp,
-                            int lp_dt, float* dw, float* db, int64_t rows, int64_t cols, void* stream);
+                            int lp_dt, float* dw, float* db, float* ws, int64_t rows, int64_t cols, void* stream);
 /* The fp16 backward's form: dclip_layernorm_bwd_scaled (f32 dy / x, lp = (f16)(dx * s) on the
  * delayed scale of st's use `use`, (s, 1/s) to spair) with dx = (res + LN^T(dy)) + add * (*add_scale)
  * (add: f16 or bf16 (add_dt), CLS rows read as 0; add_scale may be NULL = 1) — in place of
@@ -423,8 +433,8 @@ int dclip_layernorm_bwd_add(const void* dy, int dy_dt, const float* x, const flo
 int dclip_layernorm_bwd_scaled_add(const float* dy, const float* x, const float* w, const float* mean,
                                    const float* rstd, const float* res, const void* add, int add_dt,
                                    const float* add_scale, int ntok, float* dx, void* lp, float* dw, float* db,
-                                   int64_t rows, int64_t cols, float target, float* st, int use, float* spair,
-                                   void* stream);
+                                   float* ws, int64_t rows, int64_t cols, float target, float* st, int use,
+                                   float* spair, void* stream);
 
 /* Train-mode BatchNorm2d (+ optionally the ReLU after it) on a channels-last 16-bit map viewed as
  * rows (B*H*W) of C channels at a row pitch of ld elements (ld = C for a whole map; larger for a

@@ -7,6 +7,7 @@ GPU box):
     python tests/golden/gen_golden.py ctx        # only the ContextDecoder fixture (+ manifest)
     python tests/golden/gen_golden.py vitl14     # only the ViT-L/14 fixture (+ manifest)
     python tests/golden/gen_golden.py mid        # only the MID_CFG fixtures (+ manifest)
+    python tests/golden/gen_golden.py full8193   # only the 1x1024x2048 (N = 8193) ViT-B/16 fixture
 
 The reference package imports `timm`, `ftfy` and `torchvision`, none of which are
 installed here.  The shims below are written into a temporary directory at run
@@ -263,7 +264,7 @@ def gen_tiny_ctx():
     print("tiny_ctx: text norm", t["text"].norm().item())
 
 
-def gen_full(name, b, h, w, keep_full_maps=(0, 11), cfg=CITYSCAPES_CFG):
+def gen_full(name, b, h, w, keep_full_maps=(0, 11), cfg=CITYSCAPES_CFG, map_samples=256):
     model = build_reference(cfg).eval()
     cap = capture(model)
     x = images(b, h, w, seed=1234)
@@ -279,7 +280,7 @@ def gen_full(name, b, h, w, keep_full_maps=(0, 11), cfg=CITYSCAPES_CFG):
     for i, mp in enumerate(cap["maps"]):
         t[f"map_stats{i}"] = stats(mp)
         fl = mp.flatten()
-        ii = sample_idx(fl.numel(), 256, seed=100 + i)
+        ii = sample_idx(fl.numel(), map_samples, seed=100 + i)
         t[f"map_idx{i}"] = ii
         t[f"map_val{i}"] = fl[ii]
         if i in keep_full_maps:
@@ -327,6 +328,12 @@ if __name__ == "__main__":
         sys.exit(0)
     if sys.argv[1:] == ["cfg1"]:
         gen_full("vitb16_2x512x1024", 2, 512, 1024, keep_full_maps=(0, 11))
+        sys.exit(0)
+    if sys.argv[1:] == ["full8193"]:
+        # BASELINE config 1's resolution (1024x2048 -> N = 8193 tokens, the CLS-split attention
+        # kernels the benchmark runs) on one image: pre-upsample seg / depth, the score map, and
+        # 2048 sampled elements + stats of each of the 12 read-out maps (full maps would be 25 MB each)
+        gen_full("vitb16_1x1024x2048", 1, 1024, 2048, keep_full_maps=(), map_samples=2048)
         sys.exit(0)
     if sys.argv[1:] == ["vitl14"]:
         gen_manifest()

@@ -253,6 +253,109 @@ def test_fp16_delayed_scale_steps_match_exact():
     print("delayed vs exact scales, worst gradient rel. err.", worst)
 
 
+def test_fp16_delayed_scale_overflow_is_flagged_and_reprimed():
+    """ADVICE r4 (the delayed scales' overflow contract, ops.FP16_DELAYED_SCALE): a gradient that
+    grows 1e5x between two backwards (past the 4096x margin) overflows in the delayed-scale fp16
+    casts — the parameter gradients of that backward are NON-FINITE (a plain loop would apply
+    them, as with GradScaler's scaled gradients; never silently wrong finite values), and
+    train.nonfinite_flag (what train_step / step_unless_nonfinite compute) flags it and re-primes
+    every site: the next backward takes exact scales and matches the exact-scale path, and the one
+    after is on delayed scales again, within fp16 rounding of it."""
+    from denseclip_vit_multimodal_amd import ops, train
+    m = _model(torch.float16)
+    bb = m.backbone.train()
+    x = images(1, 128, 256).to(DEV).half()
+    gen = torch.Generator().manual_seed(8)
+    params = [p for p in bb.parameters() if p.requires_grad]
+    opt = torch.optim.SGD(params, lr=0.0)  # only the parameter list nonfinite_flag checks
+    ws = None
+
+    def backward(c):
+        nonlocal ws
+        bb.zero_grad(set_to_none=True)
+        maps = bb(x)
+        if ws is None:
+            ws = [(torch.randn(mp.shape, generator=gen) * 1e-6).to(DEV) for mp in maps]
+        sum((mp.float() * (w * c)).sum() for mp, w in zip(maps, ws)).backward()
+        return {n: p.grad.clone() for n, p in bb.named_parameters() if p.grad is not None}
+
+    backward(1.0)  # exact scales; primes every site
+    g2 = backward(1e5)
+    assert not all(torch.isfinite(t).all() for t in g2.values())
+    n0 = ops.STATS.get("fp16_scale_reprime", 0)
+    flag = train.nonfinite_flag(opt, torch.zeros((), device=DEV))
+    assert float(flag) == 1.0
+    g3 = backward(1e5)  # re-primed: exact scales
+    assert ops.STATS.get("fp16_scale_reprime", 0) == n0 + 1
+    assert float(train.nonfinite_flag(opt, torch.zeros((), device=DEV))) == 0.0
+    g4 = backward(1e5)  # delayed scales again (from g3's maxima)
+    ops.FP16_DELAYED_SCALE = False
+    try:
+        ref = backward(1e5)
+    finally:
+        ops.FP16_DELAYED_SCALE = True
+    for n in ref:
+        assert torch.isfinite(g3[n]).all() and torch.isfinite(g4[n]).all(), n
+        assert rel_err(g3[n], ref[n]) < 1e-5, n
+        assert rel_err(g4[n], ref[n]) < 3e-3, n
+
+
+def test_fp16_block_backward_under_graph_capture_takes_exact_scales():
+    """an fp16 block backward captured with torch.cuda.graph does not use the delayed
+    scales (their use counter is host state a replay cannot advance): with the block's
+    DelayedScale primed, the captured backward equals the exact-scale eager backward bit for bit on
+    every replay, also after the gradient grew 1e5x (which would overflow a frozen delayed scale)."""
+    from denseclip_vit_multimodal_amd import ops
+    from test_gpu_torch_ops import _block
+    blk = _block()
+    B, N, H, C = 2, 257, 12, 768
+    ds = ops.DelayedScale()
+    meta = (B, N, H, torch.float16, False, None, None, ds)
+    x = torch.randn(B * N, C, device=DEV).requires_grad_(True)
+    gy = torch.randn(B * N, C, device=DEV) * 1e-6
+    scale = torch.ones((), device=DEV)
+
+    def step():
+        y = ops.BlockFn.apply(x, meta, *blk.hip_params())
+        y.backward(gy * scale)
+        return y
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):  # primes both sites, warms the allocator and the weight casts
+            x.grad = None
+            blk.zero_grad(set_to_none=True)
+            step()
+    torch.cuda.current_stream().wait_stream(s)
+    assert ds.primed == [True, True]
+    refs = []
+    ops.FP16_DELAYED_SCALE = False
+    try:
+        for c in (1.0, 1e5):
+            scale.fill_(c)
+            x.grad = None
+            blk.zero_grad(set_to_none=True)
+            step()
+            refs.append((x.grad.clone(), {n: p.grad.clone() for n, p in blk.named_parameters() if p.grad is not None}))
+    finally:
+        ops.FP16_DELAYED_SCALE = True
+    x.grad = None
+    blk.zero_grad(set_to_none=True)
+    scale.fill_(1.0)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step()
+    for c, (gx_ref, gw_ref) in zip((1.0, 1e5), refs):
+        scale.fill_(c)
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(x.grad, gx_ref), c
+        for n, p in blk.named_parameters():
+            if n in gw_ref:
+                assert torch.equal(p.grad, gw_ref[n]), (c, n)
+
+
 @pytest.mark.parametrize("M,N,K", [(200, 256, 128), (4100, 768, 768), (16392, 3072, 768)])
 def test_scaled_ops_equal_host_alpha(M, N, K):
     """gemm / weight_grad / cast / tokens_bwd with the device scale == the host-float path (the

@@ -91,7 +91,7 @@ def test_layernorm_bwd_res(cols, lpdt):
     from denseclip_vit_multimodal_amd import _native as Nat
     dx2 = res.clone()
     Nat.call("dclip_layernorm_bwd_res", dy.data_ptr(), Nat.BF16, x.data_ptr(), Nat.F32, w.data_ptr(), mu.data_ptr(),
-             rs.data_ptr(), dx2.data_ptr(), dx2.data_ptr(), None, 0, dw.data_ptr(), None, rows, cols,
+             rs.data_ptr(), dx2.data_ptr(), dx2.data_ptr(), None, 0, dw.data_ptr(), None, None, rows, cols,
              torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     assert rel_err(dx2, res + x.grad) < 1e-5
@@ -1237,6 +1237,7 @@ def test_readout_grad_fold_matches_unfolded(extra_consumer):
             for p in params:
                 p.grad = None
             before = O.STATS.get("neck_levels", 0)
+            fix0 = O.STATS.get("readout_fold_fixup", 0)
             feats = bb(x)
             out = neck(feats)[0]
             assert O.STATS.get("neck_levels", 0) == before + 1  # the HIP neck (the links' producer)
@@ -1244,6 +1245,8 @@ def test_readout_grad_fold_matches_unfolded(extra_consumer):
             if extra_consumer:
                 loss = loss + (feats[3].float() * w3).sum()
             loss.backward()
+            # the second consumer of map 3 sends its block down the fixup path, once
+            assert O.STATS.get("readout_fold_fixup", 0) - fix0 == (1 if fold and extra_consumer else 0)
             run.append([p.grad.clone() for p in params if p.grad is not None])
     finally:
         O.FOLD_READOUT_GRAD = True
