@@ -95,6 +95,12 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
+def progress(msg):
+    """A progress line on stderr (the JSON result stays the only stdout line)."""
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def free_port():
     """An unused localhost TCP port for the rendezvous (no GPU involved)."""
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -351,6 +357,7 @@ def main():
     dt, summ, loss = timed(model, opt, batch, args.steps, args.warmup, silog, world, dist_on)
     ops_head = op_pass(model, opt, batch)
     value = world * B * args.steps / dt
+    progress(f"headline {dt / args.steps * 1e3:.2f} ms per step")
     N, heads = geometry(args.arch)
 
     # attention forward roofline (one dclip_attn_fwd launch per layer)
@@ -396,6 +403,7 @@ def main():
         release()
         model, opt = setup("R")
         dtr, _, _ = timed(model, opt, batch, k_sub, 2, silog, world, dist_on)
+        progress(f"mode R {dtr / k_sub * 1e3:.2f} ms per step")
         mode_r = {"value": round(world * B * k_sub / dtr, 4), "unit": "images/sec",
                   "ms_per_step": round(dtr / k_sub * 1e3, 2),
                   "what": "reference regime: backbone + text encoder frozen (train_denseclip.py:1040-1044)"}
@@ -408,6 +416,7 @@ def main():
         batch16 = synth_batch(B, H, W, dev, rank, image_dtype=torch.float32)
         dt16, s16, loss16 = timed(model, opt, batch16, k_sub, 2, silog, world, dist_on)
         ops16 = op_pass(model, opt, batch16)
+        progress(f"fp16 {dt16 / k_sub * 1e3:.2f} ms per step")
         del batch16
         fp16 = {"value": round(world * B * k_sub / dt16, 4), "unit": "images/sec",
                 "ms_per_step": round(dt16 / k_sub * 1e3, 2),
@@ -430,6 +439,7 @@ def main():
         # 3 untimed steps: a fresh model's first steps still build its weight caches, optimizer
         # state and allocator pools (2 left the fp8 line 5-10 % low on some boxes)
         dt8, s8, loss8 = timed(model, opt, batch, k_sub, 3, silog, world, dist_on)
+        progress(f"fp8 {dt8 / k_sub * 1e3:.2f} ms per step")
         fp8 = {"value": round(world * B * k_sub / dt8, 4), "unit": "images/sec",
                "ms_per_step": round(dt8 / k_sub * 1e3, 2), "loss": round(loss8, 4),
                "what": "BASELINE configs[4]: mode F, seg + depth heads, attention forward with P V on the e4m3 "
@@ -444,6 +454,7 @@ def main():
         NL, hl = geometry("vitl14")
         fll = attn_flops_fwd(B, NL, hl)
         vl_val = world * B * kl / dtl
+        progress(f"ViT-L/14 {dtl / kl * 1e3:.2f} ms per step")
         vl_fl = 3 * model_fwd_flops(H, W, "vitl14")
         vitl14 = {"value": round(vl_val, 4), "unit": "images/sec", "ms_per_step": round(dtl / kl * 1e3, 2),
                   "steps": kl, "loss": round(lossl, 4), "tokens_per_image": NL,
@@ -465,6 +476,7 @@ def main():
             model.backbone.attn_fp8 = f8
             opt = None
             dti, si, _ = timed(model, None, batch, k_inf, 3, silog, world, dist_on)
+            progress(f"inference {name} {dti / k_inf * 1e3:.2f} ms per step")
             infer[name] = {"value": round(world * B * k_inf / dti, 4), "unit": "images/sec",
                            "ms_per_step": round(dti / k_inf * 1e3, 2), "steps": k_inf,
                            "roofline_attn_fwd": roofline(si, "attn_fwd_fp8" if f8 else "attn_fwd", fl,
@@ -488,6 +500,7 @@ def main():
             opt = make_optimizer([p for p in model.parameters() if p.requires_grad])
             dtd, _, lossd = timed(model, opt, batch, k_sub, 3, silog, 1, True)
             ms_d = dtd / k_sub * 1e3
+            progress(f"ddp1 {ms_d:.2f} ms per step")
             ddp1 = {"value": round(B * k_sub / dtd, 4), "unit": "images/sec", "ms_per_step": round(ms_d, 2),
                     "overhead_vs_headline": round(ms_d / (dt / args.steps * 1e3) - 1.0, 4), "loss": round(lossd, 4),
                     "what": "mode F under DistributedDataParallel on an RCCL process group of world size 1 (fp32 "
@@ -507,6 +520,7 @@ def main():
     if rank == 0 and world == 1 and args.cpu_baseline == "auto" and args.arch == "vitb16" and not args.infer:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         try:
+            progress("cpu baseline")
             cpu = cpu_baseline(H, W, threads)
         except Exception as e:  # report, do not hide
             cpu = {"value": None, "error": repr(e)[:300]}

@@ -17,6 +17,7 @@
 // since LDS-DMA writes lane-linearly — which makes the ds_read_b128 fragment reads
 // bank-conflict free.  Block ids are remapped XCD-aware so the tiles of one A row
 // panel run on one XCD and share its L2.
+#include <mutex>
 #include <type_traits>
 
 #include "common.h"
@@ -896,11 +897,74 @@ __device__ __forceinline__ void pers_epilogue_lds(const f32x4 (&acc)[Cfg::NB][Cf
 
 // NW = 8: 2 x 4 waves of 128 x 64 (two waves per SIMD); NW = 4: 2 x 2 waves of 128 x 128 (one
 // wave per SIMD, the accumulators in AGPRs: 2/3 of the fragment reads per MFMA)
-template <typename T, int EPI, typename OutT, int NW = 8, bool ELDS = false>
+// Work-conserving tile walk (DYN, sched != null): every tile is claimed, none is tied to a
+// workgroup.  Round 0: workgroup b takes tile r = xcd_remap(b) by setting its bit in a bitmap
+// (atomicOr, issued beside the first K-step's loads, read behind their wait); a workgroup that
+// starts late — its CU held by RCCL's channel kernels or a side-stream graph — finds its bit already
+// set by a thief and goes straight to the next claim.  Later tiles: the tiles past round 0 are cut
+// into 8 XCD-contiguous ranges; a workgroup takes the next tile of its own XCD's range (L2 locality
+// as in the static walk), then steals from the other ranges, then steals round-0 tiles whose
+// workgroups have not started.  So a displaced workgroup costs its share of the work, not the
+// launch's length.
+// Off the critical path: the claim for the tile after the current one is an atomicAdd on the own
+// range counter issued by thread 0 at the start of the current tile's epilogue (or at launch), not
+// inspected until the next tile's K-step nk - 3 (the next tile's first K-step waits only for loads
+// older than the epilogue's stores, so it has the whole epilogue to return); thread 0 then resolves
+// it (stealing only when its range is empty) and publishes it in the first word of wave 0's epilogue
+// image (the 160 KiB of LDS are all taken; that word is free until wave 0's epilogue); the waves
+// read it behind K-step nk - 2's barrier, so K-step nk - 1's barrier orders every read before wave
+// 0's epilogue overwrites it.  Needs nk >= 2 and ntiles >= G (launch_pers).
+// sched (zero on entry): the 8 range counters at words 0, 32, .., 224 (one 128-B line each: the
+// claims of one XCD never queue behind another's), finished workgroups at 256, the round-0 bitmap at
+// [288, 296).  Each workgroup's claims end with exactly one that fails; the last workgroup to
+// fail zeroes the set again (every claim has returned by then), so the next launch on the stream
+// finds it zero (gemm_sched_counters gives each stream its own set).
+__device__ __forceinline__ void pers_range(int x, int G, int ntiles, int& lo, int& hi) {
+    const int rest = ntiles - G;
+    lo = G + (int)((int64_t)rest * x / 8);
+    hi = G + (int)((int64_t)rest * (x + 1) / 8);
+}
+
+// thread 0: the tile of claim v on the own range counter, else a stolen one, else ntiles
+__device__ __forceinline__ int pers_resolve(unsigned* __restrict__ sched, int v, int xcd, int G, int ntiles) {
+    int lo, hi;
+    pers_range(xcd, G, ntiles, lo, hi);
+    if (lo + v < hi) return lo + v;
+#pragma unroll 1
+    for (int k = 1; k < 8; ++k) {
+        const int x = (xcd + k) & 7;
+        pers_range(x, G, ntiles, lo, hi);
+        if (lo >= hi) continue;
+        const int w = (int)atomicAdd(sched + 32 * x, 1u);
+        if (lo + w < hi) return lo + w;
+    }
+    unsigned* const bm = sched + 288;  // round-0 tiles whose workgroups have not started
+#pragma unroll 1
+    for (int w = 0; w < (G + 31) / 32; ++w) {
+        const unsigned valid = (w * 32 + 32 <= G) ? 0xffffffffu : ((1u << (G - w * 32)) - 1u);
+        unsigned bits = atomicOr(bm + w, 0u);
+        while ((~bits & valid) != 0u) {
+            const int bit = __builtin_ctz(~bits & valid);
+            const unsigned old = atomicOr(bm + w, 1u << bit);
+            if (!(old & (1u << bit))) return w * 32 + bit;
+            bits |= old;
+        }
+    }
+    if ((int)atomicAdd(sched + 256, 1u) == G - 1) {  // the last workgroup out: re-arm for the next launch
+#pragma unroll 1
+        for (int i = 0; i < 8; ++i) atomicExch(sched + 32 * i, 0u);
+        atomicExch(sched + 256, 0u);
+#pragma unroll 1
+        for (int i = 288; i < 296; ++i) atomicExch(sched + i, 0u);
+    }
+    return ntiles;
+}
+
+template <typename T, int EPI, typename OutT, int NW = 8, bool ELDS = false, bool DYN = false>
 __global__ __launch_bounds__(64 * NW, 1) void gemm_nt_pers_kernel(
     const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb, int K, int tiles_m, int tiles_n,
     const float* __restrict__ bias, const void* __restrict__ aux, int64_t ld_aux, void* __restrict__ C, int64_t ldc,
-    void* __restrict__ C2, int64_t ldc2, Alpha alpha_arg) {
+    void* __restrict__ C2, int64_t ldc2, Alpha alpha_arg, unsigned* __restrict__ sched = nullptr) {
     const float alpha = alpha_arg.get();
     typedef BigCfg<256, 256, 2, NW / 2, 2, 64> Cfg;
     typedef typename Mfma<T>::frag frag;
@@ -936,6 +1000,17 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_nt_pers_kernel(
     int u = r;
     if (u >= ntiles) return;
     int m0 = (u / tiles_n) * 256, n0 = (u % tiles_n) * 256;
+    int* const pub = (int*)(smem + Cfg::SMEM);  // DYN: [0] next tile, [1] round-0 ownership (wave 0's image)
+    const int xcd = blockIdx.x & 7;
+    unsigned own_old = 0;  // thread 0 (DYN): the round-0 bitmap word before this workgroup's bit
+    int pend = 0;          // thread 0 (DYN): the claim in flight on the own range counter
+    if constexpr (DYN) {
+        static_assert(!DYN || (NW == 8 && ELDS), "the claim words live in wave 0's epilogue image");
+        if (threadIdx.x == 0) {
+            own_old = atomicOr(sched + 288 + (r >> 5), 1u << (r & 31));
+            pend = (int)atomicAdd(sched + 32 * xcd, 1u);
+        }
+    }
     PERS_STAGE(m0, n0, 0, 0);
     int slot = 0;
     bool first = true;
@@ -947,13 +1022,37 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_nt_pers_kernel(
             for (int j = 0; j < Cfg::MB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         PersCols<EPI, Cfg::NB> pc;
         pers_cols<EPI, Cfg::NB>(pc, bias, aux, n0 + wn * Cfg::WTN, lq);
-        const int un = u + G;
-        const int nm0 = (un / tiles_n) * 256, nn0 = (un % tiles_n) * 256;
+        int un = u + G;
+        if constexpr (DYN) {
+            if (nk == 2 && threadIdx.x == 0) {  // no K-step nk - 3: the next tile published before the loop
+                pub[0] = pers_resolve(sched, pend, xcd, G, ntiles);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            }
+        }
+        int nm0 = (un / tiles_n) * 256, nn0 = (un % tiles_n) * 256;
+        bool skip = false;
         for (int kt = 0; kt < nk; ++kt) {
             if (kt == 0 && !first) wait_vmcnt<PERS_EPI_MIN>();  // this K-step's loads, not the epilogue's stores
             else wait_vmcnt<0>();
+            if constexpr (DYN) {
+                if (kt == 0 && first && u == r && threadIdx.x == 0) {  // round-0 ownership (the atomicOr has returned)
+                    pub[1] = (own_old >> (r & 31)) & 1u;
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                }
+            }
             __builtin_amdgcn_s_barrier();  // K-step kt visible to every wave; the other slot free
             __builtin_amdgcn_sched_barrier(0);
+            if constexpr (DYN) {
+                if (kt == 0 && first && u == r && __builtin_amdgcn_readfirstlane(pub[1]) != 0) {
+                    skip = true;  // a thief took tile r before this workgroup started
+                    break;
+                }
+                if (kt == nk - 2) {  // the claim, published behind K-step nk - 3 (or before the loop)
+                    un = __builtin_amdgcn_readfirstlane(pub[0]);
+                    nm0 = (un / tiles_n) * 256;
+                    nn0 = (un % tiles_n) * 256;
+                }
+            }
             if (kt + 1 < nk) {
                 PERS_STAGE(m0, n0, kt + 1, slot ^ 1);
             } else if (un < ntiles) {  // the next tile's first K-step
@@ -980,11 +1079,38 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_nt_pers_kernel(
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
+            if constexpr (DYN) {
+                if (kt == nk - 3 && threadIdx.x == 0) {
+                    pub[0] = pers_resolve(sched, pend, xcd, G, ntiles);
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // visible at the next barrier
+                }
+            }
             slot ^= 1;
+        }
+        if constexpr (DYN) {
+            if (skip) {  // nothing computed: resolve the pending claim now and start over on that tile
+                if (threadIdx.x == 0) {
+                    pub[0] = pers_resolve(sched, pend, xcd, G, ntiles);
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                }
+                __builtin_amdgcn_s_barrier();
+                un = __builtin_amdgcn_readfirstlane(pub[0]);
+                __builtin_amdgcn_s_barrier();  // every wave has read it before it can be rewritten
+                if (un >= ntiles) break;
+                if (threadIdx.x == 0) pend = (int)atomicAdd(sched + 32 * xcd, 1u);
+                u = un;
+                m0 = (u / tiles_n) * 256;
+                n0 = (u % tiles_n) * 256;
+                PERS_STAGE(m0, n0, 0, slot);  // the slot K-step 0 of tile r landed in (waited for)
+                continue;                     // `first` stays: the next K-step 0 waits for everything
+            }
         }
         if constexpr (NW == 4) {
 #pragma unroll
             for (int i = 0; i < Cfg::NB; ++i) tn_acc_fence(acc[i], i == 0);
+        }
+        if constexpr (DYN) {  // the claim for the tile after the next one, while the epilogue runs
+            if (un < ntiles && threadIdx.x == 0) pend = (int)atomicAdd(sched + 32 * xcd, 1u);
         }
         if constexpr (NW == 8) {
             if constexpr (epi_lds)
@@ -1993,6 +2119,38 @@ int cu_count() {
     return n[dev];
 }
 
+// the persistent GEMM's tile-claim counters (gemm_nt_pers_kernel DYN): one zeroed set of 512 words per
+// stream per device, so launches that may run concurrently (different streams) never share one; a
+// launch on a capturing stream (a graph replay may run beside eager work on that stream) or past
+// the 64 sets of a device takes the static walk (null)
+unsigned* gemm_sched_counters(hipStream_t st) {
+    static std::mutex mu;
+    static unsigned* base[64] = {nullptr};
+    static hipStream_t owner[64][64];
+    static int used[64] = {0};
+    if (dclip_option(DCLIP_OPT_GEMM_SCHED) != 1) return nullptr;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> lock(mu);
+    if (base[dev] == nullptr) {
+        unsigned* p = nullptr;
+        const size_t bytes = 64 * 512 * sizeof(unsigned);
+        if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+        if (hipMemset(p, 0, bytes) != hipSuccess) {
+            (void)hipFree(p);
+            return nullptr;
+        }
+        base[dev] = p;
+    }
+    for (int i = 0; i < used[dev]; ++i)
+        if (owner[dev][i] == st) return base[dev] + 512 * i;
+    if (used[dev] == 64) return nullptr;
+    owner[dev][used[dev]] = st;
+    return base[dev] + 512 * used[dev]++;
+}
+
 template <typename T, int EPI, typename OutT, int NW = 8, bool PIPE = false>
 bool launch_pers(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
                  Alpha alpha, const float* bias, const void* aux, int64_t ld_aux, void* C, int64_t ldc, void* C2,
@@ -2044,7 +2202,15 @@ bool launch_pers(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t
         else
         {
             // the row-major LDS epilogue (default) or, DCLIP_OPT_GEMM_EPI 1, the accumulator-layout stores
-            if (NW == 8 && dclip_option(DCLIP_OPT_GEMM_EPI) != 1)
+            // (launch_pers runs only with >= 2 G full tiles; the round-0 bitmap holds up to 256 workgroups)
+            unsigned* sched = (NW == 8 && dclip_option(DCLIP_OPT_GEMM_EPI) != 1 && K >= 128 && G <= 256)
+                                  ? gemm_sched_counters(st)
+                                  : nullptr;
+            if (sched != nullptr)  // work-conserving: tiles past round 0 claimed (default)
+                gemm_nt_pers_kernel<T, EPI, OutT, NW, true, NW == 8><<<G, 64 * NW, 0, st>>>(
+                    (const T*)A, lda, (const T*)B, ldb, (int)K, (int)(Mfull / 256), (int)(N / 256), bias, aux, ld_aux, C,
+                    ldc, C2, ldc2, alpha, sched);
+            else if (NW == 8 && dclip_option(DCLIP_OPT_GEMM_EPI) != 1)
                 gemm_nt_pers_kernel<T, EPI, OutT, NW, true><<<G, 64 * NW, 0, st>>>(
                     (const T*)A, lda, (const T*)B, ldb, (int)K, (int)(Mfull / 256), (int)(N / 256), bias, aux, ld_aux, C,
                     ldc, C2, ldc2, alpha);

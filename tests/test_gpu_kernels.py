@@ -188,6 +188,64 @@ def test_gemm_gelu_and_residual(M, N, K, gemm_tile):
     ref = (g.float() @ Bt.float().t()) * (s + 1.702 * zf * s * (1 - s))
     assert rel_err(dz.float(), ref) < TOL[dt]
 
+@pytest.mark.parametrize("held", [0, 24])
+def test_gemm_work_conserving_walk_matches_static(held):
+    """The persistent NT GEMM's work-conserving tile walk (DCLIP_OPT_GEMM_SCHED 1: every tile claimed —
+    round-0 ownership bitmap, XCD-local ranges, stealing) against the static walk: which workgroup
+    computes a tile changes nothing, so every output is bitwise equal — also while `held` CUs are
+    occupied by side-stream kernels (the displaced workgroups' tiles are stolen), over back-to-back
+    launches (the claim counters re-arm themselves) and with two streams launching at once (each
+    stream has its own counters)."""
+    from denseclip_vit_multimodal_amd import _native as Nat
+    O = ops()
+    M, C, dt = 8 * 8193, 768, torch.bfloat16
+    torch.manual_seed(4)
+    A = torch.randn(M, C, device=DEV).to(dt)
+    A4 = torch.randn(M, 4 * C, device=DEV).to(dt)
+    W = {n: (torch.randn(n, C, device=DEV) * C ** -0.5).to(dt) for n in (C, 3 * C, 4 * C)}
+    W4 = (torch.randn(C, 4 * C, device=DEV) * (4 * C) ** -0.5).to(dt)
+    bias = {n: torch.randn(n, device=DEV) for n in (C, 3 * C, 4 * C)}
+    res = torch.randn(M, C, device=DEV)
+
+    def run_all():
+        out = {"qkv": O.gemm(A, W[3 * C], bias=bias[3 * C])}
+        out["gelu_z"], out["gelu_h"] = O.gemm(A, W[4 * C], Nat.EPI_GELU, bias=bias[4 * C])
+        out["c_proj"] = O.gemm(A4, W4, Nat.EPI_RESIDUAL, bias=bias[C], aux=res)
+        out["dx"] = O.gemm(A4, W4, out_dtype=torch.float32)
+        return out
+
+    ref = run_all()  # the static walk (default)
+    side = torch.cuda.Stream()
+    sink = torch.zeros(64, dtype=torch.int32, device=DEV)
+    # tools/libcu_hog.so: `held` one-wave workgroups with 96 KiB of LDS each, so no GEMM workgroup
+    # fits on their CUs for ~1 ms (each wave leaves on a 100 MHz clock)
+    import ctypes
+    import os
+    hog = ctypes.CDLL(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "libcu_hog.so"))
+    hog.cu_hog.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p]
+    Nat.call("dclip_set_option", Nat.OPT_GEMM_SCHED, 1)
+    try:
+        for it in range(3):
+            torch.cuda.synchronize()
+            assert hog.cu_hog(held, 1000.0, sink.data_ptr(), side.cuda_stream) == 0
+            got = run_all()
+            torch.cuda.synchronize()
+            for k in ref:
+                assert torch.equal(ref[k], got[k]), (k, it)
+        # two streams at once, each with its own claim counters
+        s2 = torch.cuda.Stream()
+        s2.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s2):
+            got2 = run_all()
+        got1 = run_all()
+        torch.cuda.current_stream().wait_stream(s2)
+        torch.cuda.synchronize()
+    finally:
+        Nat.call("dclip_set_option", Nat.OPT_GEMM_SCHED, 0)
+    for k in ref:
+        assert torch.equal(ref[k], got1[k]) and torch.equal(ref[k], got2[k]), k
+
+
 
 @pytest.mark.parametrize("M,C", [(65544, 768), (85272, 1024)])  # ViT-B/16 (8 x 8193), ViT-L/14 (8 x 10659)
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])

@@ -7,8 +7,8 @@ error ||y - y_ref|| / ||y_ref|| of the maps, score map and pre-upsample logits m
 <= 1e-3 for the small fixtures; bf16 (the throughput dtype, 8 mantissa bits) is held to
 1e-2.
 
-Gradients.  The well-conditioned check is test_backbone_grads_vs_oracle_vitb16 (a linear
-functional of the ViT-B/16 maps, every backbone parameter within 2e-2).  The full tiny
+Gradients.  The well-conditioned checks are in test_gpu_grad_parity.py (a linear functional of
+the ViT-B/16 maps / heads at N = 129, 513 and 466, bounded by a 16-bit emulation's error).  The full tiny
 train step (CE + SILog through train-mode BatchNorm, ReLU neck/heads at random init) is
 ill-conditioned: perturbing the fp32 oracle's feature maps by 1e-3 relative noise moves
 its own parameter gradients by 8-33 % element-wise (0.3 % in norm), so that step is held
@@ -209,29 +209,6 @@ def test_vitl14_full_resolution_train_step():
         seg1 = cap["seg_low"]
     assert torch.isfinite(seg2).all()
     assert rel_err(seg2[1:], seg1) < 1e-2
-
-
-def test_backbone_grads_vs_oracle_vitb16():
-    """ViT-B/16 widths (12 heads x 64), N = 129: d(sum(maps * w))/d(params) of the HIP
-    backward vs autograd through the fp32 oracle."""
-    from oracle import denseclip_oracle as O
-    m = build("cityscapes", CITYSCAPES_CFG, torch.float16)
-    bb = m.backbone
-    bb.train()
-    x = images(1, 128, 256)
-    maps = bb(x.to(DEV))
-    gen = torch.Generator().manual_seed(5)
-    ws = [torch.randn(mp.shape, generator=gen) for mp in maps]
-    sum(float(1) * (mp * w.to(DEV)).sum() for mp, w in zip(maps, ws)).backward()
-    sd = {k: v.clone().requires_grad_(True) if k.startswith("backbone.") else v
-          for k, v in spec_state_dict("cityscapes").items()}
-    ref = O.vit_forward(x, sd, out_indices=list(range(12)))
-    sum((r * w).sum() for r, w in zip(ref, ws)).backward()
-    for name, p in bb.named_parameters():
-        if name == "proj":
-            continue
-        e = rel_err(p.grad, sd["backbone." + name].grad)
-        assert e < 2e-2, (name, e)
 
 
 def test_full_resolution_properties():
