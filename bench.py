@@ -477,13 +477,35 @@ def main():
             opt = None
             dti, si, _ = timed(model, None, batch, k_inf, 3, silog, world, dist_on)
             progress(f"inference {name} {dti / k_inf * 1e3:.2f} ms per step")
+            # the serving path: the same forward captured into one HIP graph and replayed (the eager
+            # forward's ~620 launches per step take about as long to issue as to run)
+            from denseclip_vit_multimodal_amd.serve import CapturedForward
+            cf = CapturedForward(model, batch[0], warmup=3)
+            for _ in range(3):
+                cf(batch[0])
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(k_inf):
+                cf(batch[0])
+            torch.cuda.synchronize()
+            dtg = time.perf_counter() - t0
+            if dist_on:
+                tg = torch.tensor([dtg], device="cuda")
+                dist.all_reduce(tg, op=dist.ReduceOp.MAX)
+                dtg = float(tg)
+            del cf
+            progress(f"inference {name} graph {dtg / k_inf * 1e3:.2f} ms per step")
             infer[name] = {"value": round(world * B * k_inf / dti, 4), "unit": "images/sec",
                            "ms_per_step": round(dti / k_inf * 1e3, 2), "steps": k_inf,
+                           "graph": {"value": round(world * B * k_inf / dtg, 4), "unit": "images/sec",
+                                     "ms_per_step": round(dtg / k_inf * 1e3, 2),
+                                     "what": "serve.CapturedForward: the step replayed from one HIP graph"},
                            "roofline_attn_fwd": roofline(si, "attn_fwd_fp8" if f8 else "attn_fwd", fl,
                                                          PEAK_FP8_MIXED_TFLOPS if f8 else PEAK_BF16_TFLOPS)}
         infer["fp8_over_bf16"] = round(infer["fp8"]["value"] / infer["bf16"]["value"], 4)
+        infer["fp8_over_bf16_graph"] = round(infer["fp8"]["graph"]["value"] / infer["bf16"]["graph"]["value"], 4)
         infer["what"] = ("inference forward (eval, seg + depth at full resolution, no grad), same batch / resolution, "
-                         "bf16 attention vs the configs[4] fp8 attention forward")
+                         "bf16 attention vs the configs[4] fp8 attention forward; eager launches and HIP-graph replay")
     ddp1 = None
     if extras and world == 1 and not dist_on:
         # DDP's own per-step cost at world size 1: the same mode-F step with the model wrapped in DDP

@@ -1360,7 +1360,11 @@ __device__ __forceinline__ void dq2_ds(Dq2Ctx<T, NW, QR>& c, const char* Kt, int
 #pragma unroll
     for (int r = 0; r < QR; ++r) {
 #pragma unroll
+#ifdef DCLIP_DIAG_NOEXP
+        for (int e = 0; e < 16; ++e) sacc[r][e] = sacc[r][e] * 0.5f * pacc[r][e];  // timing probe only
+#else
         for (int e = 0; e < 16; ++e) sacc[r][e] = __builtin_amdgcn_exp2f(sacc[r][e]) * pacc[r][e];  // pacc: DsScale (dP - delta)
+#endif
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             const frag sf = pack_frag<T>(sacc[r], s);
@@ -1444,8 +1448,12 @@ __device__ __forceinline__ void dq2_step(Dq2Ctx<T, NW, QR>& c, int t, f32x16 (&s
     constexpr int PIECES = Dq2Ctx<T, NW, QR>::PIECES;
     const char* Kt = c.smem + Q * 16384;
     const char* Kn = c.smem + ((Q + 1) & 3) * 16384;
+#ifndef DCLIP_DIAG_NOWAIT  // timing probes only (attention_dkdv6.hip)
     wait_vmcnt<2 * PIECES>();      // own pieces of tile t+1 landed (tile t+2 in flight)
+#endif
+#ifndef DCLIP_DIAG_NOBAR
     __builtin_amdgcn_s_barrier();  // everyone's; everyone done with step t-1 (slot (t+3) % 4 free)
+#endif
     dq2_issue<T, NW, BF, QR>(c, t + 3 < c.nt ? t + 3 : c.nt - 1, (Q + 3) & 3);
     dq2_sdp<T, NW, QR>(c, Kt, 1, sB, pB);  // unit (t, 1) on the matrix pipe ...
     dq2_ds<T, NW, QR>(c, Kt, 0, sA, pA);   // ... beside dS / dQ of unit (t, 0)

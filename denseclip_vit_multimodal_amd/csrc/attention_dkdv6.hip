@@ -123,8 +123,13 @@ __device__ __forceinline__ void seeds(f32x16& S, f32x16& P, const char* base, in
 template <typename T>
 __device__ __forceinline__ void fin_chunk(f32x16& S, f32x16& P, Packs& pk, int i) {
     typedef T t2 __attribute__((ext_vector_type(2)));
+#ifdef DCLIP_DIAG_NOEXP  // timing probe: a 4-cycle multiply in place of the 8-cycle exp
+    const float e0 = S[2 * i] * 0.5f;
+    const float e1 = S[2 * i + 1] * 0.5f;
+#else
     const float e0 = __builtin_amdgcn_exp2f(S[2 * i]);
     const float e1 = __builtin_amdgcn_exp2f(S[2 * i + 1]);
+#endif
     const float d0 = e0 * P[2 * i], d1 = e1 * P[2 * i + 1];
     const t2 pp = {(T)e0, (T)e1};
     const t2 dd = {(T)d0, (T)d1};
@@ -203,8 +208,14 @@ template <typename T, int Q>
 __device__ __forceinline__ void step6(Dkv2Ctx<T, 4>& c, K6<T>& k, int t, typename Mfma<T>::frag (&qa)[4],
                                       typename Mfma<T>::frag (&ga)[4], f32x16& S0, f32x16& P0) {
     typedef Dkv2Ctx<T, 4> X;
+    // DCLIP_DIAG_* (tools/ab_attn.py timing probes only, never in the product build: the results
+    // are wrong): NOWAIT skips the DMA wait, NOBAR the workgroup barrier
+#ifndef DCLIP_DIAG_NOWAIT
     wait_vmcnt<X::PIECES + 1>();    // own pieces of slice t+1 landed (slice t+2 in flight)
+#endif
+#ifndef DCLIP_DIAG_NOBAR
     __builtin_amdgcn_s_barrier();  // everyone's; everyone done with step t-1 (slot (t+3) % 4 free)
+#endif
     dkv2_issue<T, 4>(c, t + 3 < c.nt ? t + 3 : c.nt - 1, (Q + 3) & 3);
     const char* cur = c.smem + Q * X::SLOT;
     const char* nxt = c.smem + ((Q + 1) & 3) * X::SLOT;

@@ -251,6 +251,9 @@ class DenseCLIP(nn.Module):
         either way; the replay reads the parameters' values after the previous optimizer step,
         as an in-line replay would).  A no-op until the graph exists (the first call captures
         it in line) or when a text buffer was re-allocated since the capture."""
+        if self.graph_text == "side":  # serve.CapturedForward: the text path eager on the side stream, captured
+            self._text_side_eager(device)
+            return
         g = getattr(self, "_text_graph", None)
         if g is None or not self.graph_text:
             return
@@ -277,6 +280,27 @@ class DenseCLIP(nn.Module):
             g[1].replay()
         self._text_pending = (key, side)
 
+    def _text_side_eager(self, device):
+        """graph_text == "side" (set while serve.CapturedForward captures the forward): launch the text
+        path eagerly on the side stream, forked from the main stream and joined in _text_embeddings —
+        inside a stream capture this becomes a parallel branch of the captured graph, so a replay runs
+        the text kernels beside the backbone as _text_prelaunch's graph replay does in eager mode."""
+        device = torch.device(device)
+        if device.type != "cuda":
+            return
+        if device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        if getattr(self, "_texts_dev", None) is None or self._texts_dev.device != device:
+            self._texts_dev = self.texts.to(device)
+        main = torch.cuda.current_stream(device)
+        side = getattr(self, "_text_stream", None)
+        if side is None or side.device != device:
+            side = self._text_stream = torch.cuda.Stream(device=device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side), torch.no_grad():
+            out = self._text_forward(self._texts_dev)
+        self._text_side_out = (out, side)
+
     def _text_embeddings(self, B, device):
         """Class-name embeddings (denseclip.py:627-640).  The text path is batch-independent and,
         when frozen (the reference regime and the full fine-tune both freeze it,
@@ -299,6 +323,11 @@ class DenseCLIP(nn.Module):
         # no autograd graph is recorded when gradients are off (the score-map branch runs under
         # no_grad: its output is discarded, denseclip.py:747), trainable parameters or not
         frozen = not torch.is_grad_enabled() or not any(p.requires_grad for p in params)
+        side_out = getattr(self, "_text_side_out", None)
+        self._text_side_out = None
+        if side_out is not None:  # launched by _text_side_eager at the start of this forward
+            torch.cuda.current_stream(device).wait_stream(side_out[1])
+            return side_out[0].expand(B, -1, -1)
         if not (self.graph_text and frozen and device.type == "cuda"):
             return self._text_forward(texts).expand(B, -1, -1)
         # every device buffer the graph reads is in the key: a re-allocated one forces a new capture

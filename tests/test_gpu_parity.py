@@ -374,3 +374,27 @@ def test_ddp_two_ranks_mode_f_gradients_match_single_process(img):
     print(r.stdout[-1500:])
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     assert "grads check ok: True" in r.stdout
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_captured_forward_matches_eager(fp8):
+    """serve.CapturedForward (the eval forward replayed from one HIP graph, the text path captured
+    inline) gives the eager forward's seg / depth bit for bit, for new inputs copied into the
+    captured buffer, and refuses another input shape."""
+    from denseclip_vit_multimodal_amd.serve import CapturedForward
+    m = build("cityscapes", CITYSCAPES_CFG, torch.bfloat16)
+    m.backbone.attn_fp8 = fp8
+    x1 = images(2, 256, 512, seed=1).to(DEV).to(torch.bfloat16)
+    x2 = images(2, 256, 512, seed=2).to(DEV).to(torch.bfloat16)
+    with torch.no_grad():
+        e1 = {k: v.clone() for k, v in m(x1, return_loss=False).items()}
+        e2 = {k: v.clone() for k, v in m(x2, return_loss=False).items()}
+    cf = CapturedForward(m, x1)
+    assert m.graph_text  # restored after the capture
+    for x, e in ((x2, e2), (x1, e1), (x2, e2)):
+        out = cf(x)
+        torch.cuda.synchronize()
+        for k in ("seg", "depth"):
+            assert torch.equal(out[k], e[k]), k
+    with pytest.raises(ValueError):
+        cf(x1[:1])
