@@ -30,15 +30,16 @@ _SIGS = {
                             _i64, _i64, _f32, _c_void_p],
     "dclip_layernorm_bwd": [_c_void_p, _i32, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32,
                             _c_void_p, _c_void_p, _i64, _i64, _c_void_p],
-    "dclip_layernorm_bwd_res": [_c_void_p, _i32, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
-                                _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _i64, _i64, _c_void_p],
+    "dclip_layernorm_bwd_res": [_c_void_p, _i32, _c_void_p, _i64, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p,
+                                _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _i64, _i64,
+                                _c_void_p],
     "dclip_layernorm_bwd_ws_floats": [_i64, _i64],
     "dclip_layernorm_bwd_add": [_c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                                 _i32, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _i64, _i64,
                                 _c_void_p],
-    "dclip_layernorm_bwd_scaled_add": [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
-                                       _i32, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
-                                       _i64, _i64, _f32, _c_void_p, _i32, _c_void_p, _c_void_p],
+    "dclip_layernorm_bwd_scaled_add": [_c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                       _c_void_p, _c_void_p, _i32, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p,
+                                       _c_void_p, _c_void_p, _i64, _i64, _f32, _c_void_p, _i32, _c_void_p, _c_void_p],
     "dclip_gemm": [_i32, _i32, _c_void_p, _i64, _c_void_p, _i64, _i64, _i64, _i64, _i32, _f32, _c_void_p, _c_void_p,
                    _c_void_p,
                    _i32, _i64, _c_void_p, _i32, _i64, _c_void_p, _i64, _c_void_p],
@@ -81,9 +82,9 @@ _SIGS = {
                                _c_void_p],
     "dclip_add_readout_cast_scaled": [_c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _i64, _i32, _i32,
                                       _f32, _c_void_p, _i32, _c_void_p, _c_void_p],
-    "dclip_layernorm_bwd_scaled": [_c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
-                                   _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _i64, _f32, _c_void_p, _i32,
-                                   _c_void_p, _c_void_p],
+    "dclip_layernorm_bwd_scaled": [_c_void_p, _i32, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p,
+                                   _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _i64, _f32,
+                                   _c_void_p, _i32, _c_void_p, _c_void_p],
     "dclip_bn_workspace": [_i64, _i32],
     "dclip_bn_fwd": [_i32, _c_void_p, _i64, _i32, _i64, _c_void_p, _c_void_p, _f32, _f32, _c_void_p, _c_void_p,
                      _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p],

@@ -2034,6 +2034,116 @@ __global__ __launch_bounds__(512) void gemm_tail16_kernel(const T* __restrict__ 
     }
 }
 
+// The same M tail shaped for latency (round 5, the default): the tail kernel is ~1 % of the step
+// (97 launches of 8-15 us) and its time is global-memory round trips, not work.  A workgroup per 16
+// output columns (N / 16 workgroups: 48-192, not 12-48), W <= 16 waves each summing a K / W slice of
+// IT <= 6 32-deep steps with EVERY fragment load issued before the first MFMA (one round trip
+// instead of one per unrolled group of four), and the epilogue's side inputs (bias, column scales,
+// residual rows, GELU' pre-activations) loaded at launch by the threads that apply them, so their
+// latency hides behind the K loads.  The W slices are added in LDS in wave order (deterministic).
+// Needs N % 16 == 0 and W * IT = K / 32 (the launcher picks them).
+template <typename T, int EPI, typename OutT>
+__global__ __launch_bounds__(1024) void gemm_tail16x16_kernel(const T* __restrict__ A, int64_t lda,
+                                                              const T* __restrict__ B, int64_t ldb, int mt, int N,
+                                                              int W, int IT, int m0, const float* __restrict__ bias,
+                                                              const void* __restrict__ aux, int64_t ld_aux,
+                                                              void* __restrict__ C, int64_t ldc, void* __restrict__ C2,
+                                                              int64_t ldc2, Alpha alpha_arg) {
+    typedef typename Mfma<T>::frag frag;
+    constexpr int ITMAX = 6;
+    __shared__ float red[16][16][17];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int l16 = lane & 15, lq = lane >> 4;
+    const int n0 = blockIdx.x * 16;
+    const int t = threadIdx.x;
+    // the epilogue threads (row r, 8-column segment cb) fetch their side inputs first
+    const int er = t >> 1, ecb = (t & 1) * 8;
+    const bool epi = t < 2 * mt;
+    float bv[8], pre[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bv[e] = pre[e] = 0.f;
+    if (epi) {
+        const int nb = n0 + ecb;
+        if (bias != nullptr && EPI != DCLIP_EPI_GELU_BWD) load8<float>(bias + nb, bv, true, 8);
+        if constexpr (EPI == DCLIP_EPI_STORE_SCALED) load8<float>((const float*)aux + nb, pre, true, 8);
+        if constexpr (EPI == DCLIP_EPI_RESIDUAL)
+            load8<float>((const float*)aux + (int64_t)(m0 + er) * ld_aux + nb, pre, true, 8);
+        if constexpr (EPI == DCLIP_EPI_GELU_BWD) load8<T>((const T*)aux + (int64_t)(m0 + er) * ld_aux + nb, pre, true, 8);
+    }
+    const bool rowok = l16 < mt;
+    const int kbeg = wave * IT * 32;
+    const T* arow = A + (int64_t)(rowok ? l16 : 0) * lda + kbeg + 8 * lq;
+    const T* brow = B + (int64_t)(n0 + l16) * ldb + kbeg + 8 * lq;
+    frag zf;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) zf[j] = (T)0.f;
+    frag a[ITMAX], b[ITMAX];
+#pragma unroll
+    for (int it = 0; it < ITMAX; ++it) {
+        if (it < IT) {
+            a[it] = rowok ? *(const frag*)(arow + 32 * it) : zf;
+            b[it] = *(const frag*)(brow + 32 * it);
+        }
+    }
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int it = 0; it < ITMAX; ++it)
+        if (it < IT) acc = Mfma16<T>::mma(a[it], b[it], acc);  // D[4 lq + e][l16]
+#pragma unroll
+    for (int e = 0; e < 4; ++e) red[wave][4 * lq + e][l16] = acc[e];
+    __syncthreads();
+    if (epi) {
+        const float alpha = alpha_arg.get();
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            float sum = 0.f;
+            for (int w = 0; w < W; ++w) sum += red[w][er][ecb + e];
+            v[e] = sum * alpha + bv[e];
+        }
+        const int64_t m = m0 + er;
+        const int nb = n0 + ecb;
+        if constexpr (EPI == DCLIP_EPI_STORE) {
+            store8<OutT>((OutT*)C + m * ldc + nb, v, true, 8);
+        } else if constexpr (EPI == DCLIP_EPI_STORE_SCALED) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] *= pre[e];
+            store8<OutT>((OutT*)C + m * ldc + nb, v, true, 8);
+        } else if constexpr (EPI == DCLIP_EPI_GELU) {
+            float g[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                v[e] = (float)(OutT)v[e];  // the activation sees the rounded pre-activation
+                g[e] = quick_gelu(v[e]);
+            }
+            if (C != nullptr) store8<OutT>((OutT*)C + m * ldc + nb, v, true, 8);
+            store8<OutT>((OutT*)C2 + m * ldc2 + nb, g, true, 8);
+        } else if constexpr (EPI == DCLIP_EPI_RESIDUAL) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += pre[e];
+            store8<float>((float*)C + m * ldc + nb, v, true, 8);
+            if (C2 != nullptr) store8<T>((T*)C2 + m * ldc2 + nb, v, true, 8);
+        } else if constexpr (EPI == DCLIP_EPI_GELU_BWD) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] *= quick_gelu_grad(pre[e]);
+            store8<OutT>((OutT*)C + m * ldc + nb, v, true, 8);
+        }
+    }
+}
+
+// (W, IT) of gemm_tail16x16_kernel for K: the most waves (<= 16) whose slices are <= 6 steps of 32
+inline bool tail16x16_plan(int64_t K, int& W, int& IT) {
+    if (K % 32 != 0) return false;
+    const int s = (int)(K / 32);
+    for (int w = 16; w >= 1; --w)
+        if (s % w == 0 && s / w <= 6) {
+            W = w;
+            IT = s / w;
+            return true;
+        }
+    return false;
+}
+
 template <typename T, int EPI, typename OutT>
 __global__ void tail_combine_kernel(const float* __restrict__ ws, int splits, int rows, int N, int64_t m0,
                                     const float* __restrict__ bias, const void* __restrict__ aux, int64_t ld_aux,
@@ -2172,7 +2282,13 @@ bool launch_pers(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t
         if (ldc % 4 != 0 || (C2 != nullptr && ldc2 % 4 != 0) || (EPI == DCLIP_EPI_RESIDUAL && ld_aux % 4 != 0) ||
             (EPI == DCLIP_EPI_GELU_BWD && ld_aux % 4 != 0))
             return false;
-        if (tail > 0 && tail <= 16 && K % 256 == 0 && dclip_option(DCLIP_OPT_GEMM_TAIL) != 1) {
+        const int tail_opt = dclip_option(DCLIP_OPT_GEMM_TAIL);
+        int tw = 0, tit = 0;
+        if (tail > 0 && tail <= 16 && tail_opt == 0 && tail16x16_plan(K, tw, tit)) {
+            gemm_tail16x16_kernel<T, EPI, OutT><<<(unsigned)(N / 16), 64 * tw, 0, st>>>(
+                (const T*)A + Mfull * lda, lda, (const T*)B, ldb, (int)tail, (int)N, tw, tit, (int)Mfull, bias, aux,
+                ld_aux, C, ldc, C2, ldc2, alpha);
+        } else if (tail > 0 && tail <= 16 && K % 256 == 0 && tail_opt != 1) {
             gemm_tail16_kernel<T, EPI, OutT><<<(unsigned)(N / 64), 512, 0, st>>>(
                 (const T*)A + Mfull * lda, lda, (const T*)B, ldb, (int)tail, (int)N, (int)K, (int)Mfull, bias, aux,
                 ld_aux, C, ldc, C2, ldc2, alpha);

@@ -256,13 +256,17 @@ __global__ __launch_bounds__(512) void ln_bwd_fast(const TDY* __restrict__ dy, c
                                                    float* __restrict__ db, int64_t rows, float* part,
                                                    float* st = nullptr, int use = 0, float* spair = nullptr,
                                                    float target = 0.f, const void* __restrict__ add = nullptr,
-                                                   int ntok = 1, const float* __restrict__ add_scale = nullptr) {
+                                                   int ntok = 1, const float* __restrict__ add_scale = nullptr,
+                                                   const float* __restrict__ dy_scale = nullptr, int64_t dy_ntok = 0) {
     constexpr int cols = 256 * NV;
     constexpr bool ADD = !std::is_void<TA>::value;
     typedef typename std::conditional<ADD, TA, bf16>::type TAV;  // (a loadable type when ADD is off)
     const TAV* addp = (const TAV*)add;
     float sb = 1.f;
     if constexpr (ADD) sb = add_scale != nullptr ? *add_scale : 1.f;
+    // dy_scale: dy arrives on a gradient scale (fp16: the dX GEMM's output left on its operand's s),
+    // times *dy_scale (= 1/s) on load; dy_ntok > 0: dy's rows with row % dy_ntok == 0 (CLS) read as 0
+    const float dsc = dy_scale != nullptr ? *dy_scale : 1.f;
     __shared__ float red[8][2][4 * NV][64];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -317,6 +321,14 @@ __global__ __launch_bounds__(512) void ln_bwd_fast(const TDY* __restrict__ dy, c
             }
             nmu = mean[nrow];
             nrs = rstd[nrow];
+        }
+        if (dy_scale != nullptr) {
+#pragma unroll
+            for (int k = 0; k < 4 * NV; ++k) dv[k] *= dsc;
+        }
+        if (dy_ntok > 0 && row % dy_ntok == 0) {
+#pragma unroll
+            for (int k = 0; k < 4 * NV; ++k) dv[k] = 0.f;
         }
         float sg = 0.f, sgx = 0.f;
 #pragma unroll
@@ -437,12 +449,14 @@ void fwd_fast(const void* x, const float* w, const float* b, void* y, float* mea
 }
 
 template <typename TDY, typename TX, int NV>
-void bwd_fast(const void* dy, const void* x, const float* w, const float* mean, const float* rstd, const float* res,
-              float* dx, void* lp, int lp_dt, float* dw, float* db, float* ws, int64_t rows, hipStream_t st) {
+void bwd_fast(const void* dy, const float* dy_scale, int64_t dy_ntok, const void* x, const float* w, const float* mean,
+              const float* rstd, const float* res, float* dx, void* lp, int lp_dt, float* dw, float* db, float* ws,
+              int64_t rows, hipStream_t st) {
     const int64_t blocks = ln_bwd_blocks(rows);
     float* part = (dw || db) ? ws : nullptr;
     ln_bwd_fast<TDY, TX, NV><<<(unsigned)blocks, 512, 0, st>>>((const TDY*)dy, (const TX*)x, w, mean, rstd, res, dx,
-                                                              lp, lp_dt, dw, db, rows, part);
+                                                              lp, lp_dt, dw, db, rows, part, nullptr, 0, nullptr, 0.f,
+                                                              nullptr, 1, nullptr, dy_scale, dy_ntok);
     ln_dwdb_reduce(part, 256 * NV, blocks, dw, db, st);
 }
 
@@ -468,13 +482,16 @@ void fwd_dispatch_y(int y_dt, const void* x, const float* w, const float* b, voi
 }
 
 template <typename TDY, typename TX>
-void bwd_launch(const void* dy, const void* x, const float* w, const float* mean, const float* rstd,
-                const float* res, float* dx, void* lp, int lp_dt, float* dw, float* db, float* ws, int64_t rows, int cols,
-                hipStream_t st) {
+void bwd_launch(const void* dy, const float* dy_scale, int64_t dy_ntok, const void* x, const float* w,
+                const float* mean, const float* rstd, const float* res, float* dx, void* lp, int lp_dt, float* dw,
+                float* db, float* ws, int64_t rows, int cols, hipStream_t st) {
     switch (cols) {
-        case 512: return bwd_fast<TDY, TX, 2>(dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows, st);
-        case 768: return bwd_fast<TDY, TX, 3>(dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows, st);
-        case 1024: return bwd_fast<TDY, TX, 4>(dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows, st);
+        case 512:
+            return bwd_fast<TDY, TX, 2>(dy, dy_scale, dy_ntok, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows, st);
+        case 768:
+            return bwd_fast<TDY, TX, 3>(dy, dy_scale, dy_ntok, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows, st);
+        case 1024:
+            return bwd_fast<TDY, TX, 4>(dy, dy_scale, dy_ntok, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows, st);
         default: break;
     }
     int64_t blocks = (rows + 3) / 4;
@@ -484,24 +501,37 @@ void bwd_launch(const void* dy, const void* x, const float* w, const float* mean
 }
 
 template <typename TDY>
-void bwd_dispatch_x(int x_dt, const void* dy, const void* x, const float* w, const float* mean,
-                    const float* rstd, const float* res, float* dx, void* lp, int lp_dt, float* dw, float* db,
-                    float* ws, int64_t rows, int cols, hipStream_t st) {
-    if (x_dt == DCLIP_F32) bwd_launch<TDY, float>(dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows, cols, st);
-    else if (x_dt == DCLIP_F16) bwd_launch<TDY, f16>(dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows, cols, st);
-    else bwd_launch<TDY, bf16>(dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows, cols, st);
+void bwd_dispatch_x(int x_dt, const void* dy, const float* dy_scale, int64_t dy_ntok, const void* x, const float* w,
+                    const float* mean, const float* rstd, const float* res, float* dx, void* lp, int lp_dt, float* dw,
+                    float* db, float* ws, int64_t rows, int cols, hipStream_t st) {
+    if (x_dt == DCLIP_F32)
+        bwd_launch<TDY, float>(dy, dy_scale, dy_ntok, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows, cols, st);
+    else if (x_dt == DCLIP_F16)
+        bwd_launch<TDY, f16>(dy, dy_scale, dy_ntok, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows, cols, st);
+    else bwd_launch<TDY, bf16>(dy, dy_scale, dy_ntok, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows, cols, st);
 }
 
-template <typename TX, int NV>
-void bwd_fast_ds(const float* dy, const void* x, const float* w, const float* mean, const float* rstd,
-                 const float* res, float* dx, void* lp, float* dw, float* db, float* ws, int64_t rows, float* st, int use,
-                 float* spair, float target, hipStream_t s) {
+template <typename TDY, int NV>
+void bwd_fast_ds(const void* dy, const float* dy_scale, const float* x, const float* w, const float* mean,
+                 const float* rstd, const float* res, float* dx, void* lp, float* dw, float* db, float* ws, int64_t rows,
+                 float* st, int use, float* spair, float target, hipStream_t s) {
     const int64_t blocks = ln_bwd_blocks(rows);
     float* part = (dw || db) ? ws : nullptr;
-    ln_bwd_fast<float, TX, NV, true><<<(unsigned)blocks, 512, 0, s>>>(dy, (const TX*)x, w, mean, rstd, res, dx, lp,
-                                                                    DCLIP_F16, dw, db, rows, part, st, use, spair,
-                                                                    target);
+    ln_bwd_fast<TDY, float, NV, true><<<(unsigned)blocks, 512, 0, s>>>(
+        (const TDY*)dy, x, w, mean, rstd, res, dx, lp, DCLIP_F16, dw, db, rows, part, st, use, spair, target, nullptr, 1,
+        nullptr, dy_scale, 0);
     ln_dwdb_reduce(part, 256 * NV, blocks, dw, db, s);
+}
+
+template <typename TDY>
+void bwd_ds_cols(const void* dy, const float* dy_scale, const float* x, const float* w, const float* mean,
+                 const float* rstd, const float* res, float* dx, void* lp, float* dw, float* db, float* ws, int64_t rows,
+                 int64_t cols, float* st, int use, float* spair, float target, hipStream_t s) {
+    if (cols == 512)
+        bwd_fast_ds<TDY, 2>(dy, dy_scale, x, w, mean, rstd, res, dx, lp, dw, db, ws, rows, st, use, spair, target, s);
+    else if (cols == 768)
+        bwd_fast_ds<TDY, 3>(dy, dy_scale, x, w, mean, rstd, res, dx, lp, dw, db, ws, rows, st, use, spair, target, s);
+    else bwd_fast_ds<TDY, 4>(dy, dy_scale, x, w, mean, rstd, res, dx, lp, dw, db, ws, rows, st, use, spair, target, s);
 }
 
 template <typename TDY, int NV>
@@ -524,31 +554,33 @@ void bwd_add_cols(const void* dy, const float* x, const float* w, const float* m
     else bwd_fast_add<TDY, 4>(dy, x, w, mean, rstd, res, add, ntok, dx, lp, lp_dt, dw, db, ws, rows, s);
 }
 
-template <typename TA, int NV>
-void bwd_fast_ds_add(const float* dy, const float* x, const float* w, const float* mean, const float* rstd,
-                     const float* res, const void* add, const float* add_scale, int ntok, float* dx, void* lp, float* dw,
-                     float* db, float* ws, int64_t rows, float* st, int use, float* spair, float target, hipStream_t s) {
+template <typename TDY, typename TA, int NV>
+void bwd_fast_ds_add(const void* dy, const float* dy_scale, const float* x, const float* w, const float* mean,
+                     const float* rstd, const float* res, const void* add, const float* add_scale, int ntok, float* dx,
+                     void* lp, float* dw, float* db, float* ws, int64_t rows, float* st, int use, float* spair,
+                     float target, hipStream_t s) {
     const int64_t blocks = ln_bwd_blocks(rows);
     float* part = (dw || db) ? ws : nullptr;
-    ln_bwd_fast<float, float, NV, true, TA><<<(unsigned)blocks, 512, 0, s>>>(
-        dy, x, w, mean, rstd, res, dx, lp, DCLIP_F16, dw, db, rows, part, st, use, spair, target, add, ntok, add_scale);
+    ln_bwd_fast<TDY, float, NV, true, TA><<<(unsigned)blocks, 512, 0, s>>>(
+        (const TDY*)dy, x, w, mean, rstd, res, dx, lp, DCLIP_F16, dw, db, rows, part, st, use, spair, target, add, ntok,
+        add_scale, dy_scale, 0);
     ln_dwdb_reduce(part, 256 * NV, blocks, dw, db, s);
 }
 
-template <typename TA>
-void bwd_ds_add_cols(const float* dy, const float* x, const float* w, const float* mean, const float* rstd,
-                     const float* res, const void* add, const float* add_scale, int ntok, float* dx, void* lp,
-                     float* dw, float* db, float* ws, int64_t rows, int64_t cols, float* st, int use, float* spair, float target,
-                     hipStream_t s) {
+template <typename TDY, typename TA>
+void bwd_ds_add_cols(const void* dy, const float* dy_scale, const float* x, const float* w, const float* mean,
+                     const float* rstd, const float* res, const void* add, const float* add_scale, int ntok, float* dx,
+                     void* lp, float* dw, float* db, float* ws, int64_t rows, int64_t cols, float* st, int use,
+                     float* spair, float target, hipStream_t s) {
     if (cols == 512)
-        bwd_fast_ds_add<TA, 2>(dy, x, w, mean, rstd, res, add, add_scale, ntok, dx, lp, dw, db, ws, rows, st, use, spair,
-                               target, s);
+        bwd_fast_ds_add<TDY, TA, 2>(dy, dy_scale, x, w, mean, rstd, res, add, add_scale, ntok, dx, lp, dw, db, ws, rows,
+                                    st, use, spair, target, s);
     else if (cols == 768)
-        bwd_fast_ds_add<TA, 3>(dy, x, w, mean, rstd, res, add, add_scale, ntok, dx, lp, dw, db, ws, rows, st, use, spair,
-                               target, s);
+        bwd_fast_ds_add<TDY, TA, 3>(dy, dy_scale, x, w, mean, rstd, res, add, add_scale, ntok, dx, lp, dw, db, ws, rows,
+                                    st, use, spair, target, s);
     else
-        bwd_fast_ds_add<TA, 4>(dy, x, w, mean, rstd, res, add, add_scale, ntok, dx, lp, dw, db, ws, rows, st, use, spair,
-                               target, s);
+        bwd_fast_ds_add<TDY, TA, 4>(dy, dy_scale, x, w, mean, rstd, res, add, add_scale, ntok, dx, lp, dw, db, ws, rows,
+                                    st, use, spair, target, s);
 }
 
 }  // namespace
@@ -573,43 +605,53 @@ extern "C" int dclip_layernorm_bwd_add(const void* dy, int dy_dt, const float* x
     return 0;
 }
 
-extern "C" int dclip_layernorm_bwd_scaled_add(const float* dy, const float* x, const float* w, const float* mean,
-                                              const float* rstd, const float* res, const void* add, int add_dt,
-                                              const float* add_scale, int ntok, float* dx, void* lp, float* dw,
-                                              float* db, float* ws, int64_t rows, int64_t cols, float target, float* st, int use,
-                                              float* spair, void* stream) {
+extern "C" int dclip_layernorm_bwd_scaled_add(const void* dy, int dy_dt, const float* dy_scale, const float* x,
+                                              const float* w, const float* mean, const float* rstd, const float* res,
+                                              const void* add, int add_dt, const float* add_scale, int ntok, float* dx,
+                                              void* lp, float* dw, float* db, float* ws, int64_t rows, int64_t cols,
+                                              float target, float* st, int use, float* spair, void* stream) {
     DCLIP_HOST_CHECK(cols == 512 || cols == 768 || cols == 1024,
                      "dclip_layernorm_bwd_scaled_add: cols must be 512, 768 or 1024 (got %lld)", (long long)cols);
+    DCLIP_HOST_CHECK(dy_dt == DCLIP_F32 || dy_dt == DCLIP_F16, "dclip_layernorm_bwd_scaled_add: dy must be f32 or f16");
     DCLIP_HOST_CHECK(add != nullptr && ntok > 0 && (add_dt == DCLIP_F16 || add_dt == DCLIP_BF16),
                      "dclip_layernorm_bwd_scaled_add: a 16-bit add buffer and ntok > 0");
     DCLIP_HOST_CHECK(lp != nullptr && st != nullptr && spair != nullptr && target > 0.f && use >= 1,
                      "dclip_layernorm_bwd_scaled_add: lp, the scale state, use >= 1, the scale pair and target > 0");
     DCLIP_HOST_CHECK(rows > 0, "dclip_layernorm_bwd_scaled_add: rows must be > 0");
     hipStream_t s = (hipStream_t)stream;
-    if (add_dt == DCLIP_F16)
-        bwd_ds_add_cols<f16>(dy, x, w, mean, rstd, res, add, add_scale, ntok, dx, lp, dw, db, ws, rows, cols, st, use, spair,
-                             target, s);
-    else
-        bwd_ds_add_cols<bf16>(dy, x, w, mean, rstd, res, add, add_scale, ntok, dx, lp, dw, db, ws, rows, cols, st, use,
-                              spair, target, s);
+#define DS_ADD(TDY, TA)                                                                                       \
+    bwd_ds_add_cols<TDY, TA>(dy, dy_scale, x, w, mean, rstd, res, add, add_scale, ntok, dx, lp, dw, db, ws, rows, cols, st, \
+                             use, spair, target, s)
+    if (dy_dt == DCLIP_F32) {
+        if (add_dt == DCLIP_F16) DS_ADD(float, f16);
+        else DS_ADD(float, bf16);
+    } else {
+        if (add_dt == DCLIP_F16) DS_ADD(f16, f16);
+        else DS_ADD(f16, bf16);
+    }
+#undef DS_ADD
     DCLIP_LAUNCH_CHECK();
     return 0;
 }
 
-extern "C" int dclip_layernorm_bwd_scaled(const float* dy, const void* x, int x_dt, const float* w, const float* mean,
-                                          const float* rstd, const float* res, float* dx, void* lp, float* dw,
-                                          float* db, float* ws, int64_t rows, int64_t cols, float target, float* st, int use,
-                                          float* spair, void* stream) {
+extern "C" int dclip_layernorm_bwd_scaled(const void* dy, int dy_dt, const float* dy_scale, const void* x, int x_dt,
+                                          const float* w, const float* mean, const float* rstd, const float* res,
+                                          float* dx, void* lp, float* dw, float* db, float* ws, int64_t rows,
+                                          int64_t cols, float target, float* st, int use, float* spair, void* stream) {
     DCLIP_HOST_CHECK(cols == 512 || cols == 768 || cols == 1024,
                      "dclip_layernorm_bwd_scaled: cols must be 512, 768 or 1024 (got %lld)", (long long)cols);
     DCLIP_HOST_CHECK(x_dt == DCLIP_F32, "dclip_layernorm_bwd_scaled: x must be f32 (the residual stream)");
+    DCLIP_HOST_CHECK(dy_dt == DCLIP_F32 || dy_dt == DCLIP_F16, "dclip_layernorm_bwd_scaled: dy must be f32 or f16");
     DCLIP_HOST_CHECK(lp != nullptr && st != nullptr && spair != nullptr && target > 0.f && use >= 1,
                      "dclip_layernorm_bwd_scaled: lp, the scale state, use >= 1, the scale pair and target > 0");
     DCLIP_HOST_CHECK(rows > 0, "dclip_layernorm_bwd_scaled: rows must be > 0");
     hipStream_t s = (hipStream_t)stream;
-    if (cols == 512) bwd_fast_ds<float, 2>(dy, x, w, mean, rstd, res, dx, lp, dw, db, ws, rows, st, use, spair, target, s);
-    else if (cols == 768) bwd_fast_ds<float, 3>(dy, x, w, mean, rstd, res, dx, lp, dw, db, ws, rows, st, use, spair, target, s);
-    else bwd_fast_ds<float, 4>(dy, x, w, mean, rstd, res, dx, lp, dw, db, ws, rows, st, use, spair, target, s);
+    if (dy_dt == DCLIP_F32)
+        bwd_ds_cols<float>(dy, dy_scale, (const float*)x, w, mean, rstd, res, dx, lp, dw, db, ws, rows, cols, st, use,
+                           spair, target, s);
+    else
+        bwd_ds_cols<f16>(dy, dy_scale, (const float*)x, w, mean, rstd, res, dx, lp, dw, db, ws, rows, cols, st, use, spair,
+                         target, s);
     DCLIP_LAUNCH_CHECK();
     return 0;
 }
@@ -634,21 +676,28 @@ extern "C" int64_t dclip_layernorm_bwd_ws_floats(int64_t rows, int64_t cols) {
     return ln_bwd_blocks(rows) * 2 * cols;
 }
 
-extern "C" int dclip_layernorm_bwd_res(const void* dy, int dy_dt, const void* x, int x_dt, const float* w,
-                                       const float* mean, const float* rstd, const float* res, float* dx, void* lp,
-                                       int lp_dt, float* dw, float* db, float* ws, int64_t rows, int64_t cols,
-                                       void* stream) {
+extern "C" int dclip_layernorm_bwd_res(const void* dy, int dy_dt, const float* dy_scale, int64_t dy_ntok, const void* x,
+                                       int x_dt, const float* w, const float* mean, const float* rstd, const float* res,
+                                       float* dx, void* lp, int lp_dt, float* dw, float* db, float* ws, int64_t rows,
+                                       int64_t cols, void* stream) {
     DCLIP_HOST_CHECK(cols > 0 && cols % 4 == 0 && cols <= 64 * MAXV,
                      "dclip_layernorm_bwd: cols=%lld must be a multiple of 4 and <= %d", (long long)cols, 64 * MAXV);
+    DCLIP_HOST_CHECK((dy_scale == nullptr && dy_ntok == 0) || cols == 512 || cols == 768 || cols == 1024,
+                     "dclip_layernorm_bwd_res: dy_scale / dy_ntok need cols 512, 768 or 1024 (got %lld)", (long long)cols);
+    DCLIP_HOST_CHECK(dy_ntok >= 0, "dclip_layernorm_bwd_res: dy_ntok < 0");
     DCLIP_HOST_CHECK(lp == nullptr || lp_dt == DCLIP_BF16 || lp_dt == DCLIP_F16,
                      "dclip_layernorm_bwd_res: lp_dt must be F16 or BF16");
     if (rows == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
     if (dy_dt == DCLIP_F32)
-        bwd_dispatch_x<float>(x_dt, dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows, (int)cols, st);
+        bwd_dispatch_x<float>(x_dt, dy, dy_scale, dy_ntok, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows,
+                              (int)cols, st);
     else if (dy_dt == DCLIP_F16)
-        bwd_dispatch_x<f16>(x_dt, dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows, (int)cols, st);
-    else bwd_dispatch_x<bf16>(x_dt, dy, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows, (int)cols, st);
+        bwd_dispatch_x<f16>(x_dt, dy, dy_scale, dy_ntok, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows,
+                            (int)cols, st);
+    else
+        bwd_dispatch_x<bf16>(x_dt, dy, dy_scale, dy_ntok, x, w, mean, rstd, res, dx, lp, lp_dt, dw, db, ws, rows,
+                             (int)cols, st);
     DCLIP_LAUNCH_CHECK();
     return 0;
 }
@@ -656,6 +705,6 @@ extern "C" int dclip_layernorm_bwd_res(const void* dy, int dy_dt, const void* x,
 extern "C" int dclip_layernorm_bwd(const void* dy, int dy_dt, const void* x, int x_dt, const float* w,
                                    const float* mean, const float* rstd, float* dx, int accumulate,
                                    float* dw, float* db, int64_t rows, int64_t cols, void* stream) {
-    return dclip_layernorm_bwd_res(dy, dy_dt, x, x_dt, w, mean, rstd, accumulate ? dx : nullptr, dx, nullptr, 0, dw,
-                                   db, nullptr, rows, cols, stream);
+    return dclip_layernorm_bwd_res(dy, dy_dt, nullptr, 0, x, x_dt, w, mean, rstd, accumulate ? dx : nullptr, dx, nullptr,
+                                   0, dw, db, nullptr, rows, cols, stream);
 }

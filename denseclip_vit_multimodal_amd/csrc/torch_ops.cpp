@@ -94,29 +94,32 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_fwd(const Tensor& x, const Tensor& 
 }
 
 // dx = res + LN^T(dy) (res optional); dw / db accumulated in place
+// dy_scale: a (s, 1/s, ..) buffer whose 1/s multiplies dy on load (dy left on its gradient scale);
+// dy_ntok > 0: dy's rows with row % dy_ntok == 0 (CLS) read as 0
 Tensor layernorm_bwd(const Tensor& dy, const Tensor& x, const Tensor& w, const Tensor& mean, const Tensor& rstd,
-                     const c10::optional<Tensor>& res, Tensor& dw, Tensor& db) {
+                     const c10::optional<Tensor>& res, Tensor& dw, Tensor& db, const c10::optional<Tensor>& dy_scale,
+                     int64_t dy_ntok) {
     check_gpu(dy, "dy"); check_gpu(x, "x"); check_gpu(w, "w"); check_gpu(mean, "mean"); check_gpu(rstd, "rstd");
-    check_opt(res, "res");
+    check_opt(res, "res"); check_opt(dy_scale, "dy_scale");
     TORCH_CHECK(x.dim() == 2 && dy.sizes() == x.sizes(), "layernorm_bwd: dy and x (rows, cols)");
     check_vec(w, x.size(1), "LayerNorm weight"); check_vec(dw, x.size(1), "dw"); check_vec(db, x.size(1), "db");
     check_vec(mean, x.size(0), "mean"); check_vec(rstd, x.size(0), "rstd");
     c10::DeviceGuard g(x.device());
     Tensor dx = at::empty(x.sizes(), like(x, at::kFloat));
     Tensor ws = ln_ws(x, dw, db);
-    DCLIP_CALL(dclip_layernorm_bwd_res(dy.data_ptr(), dt_code(dy.scalar_type()), x.data_ptr(), dt_code(x.scalar_type()),
-                                       ptr<float>(w), ptr<float>(mean), ptr<float>(rstd), optr<float>(res), ptr<float>(dx),
-                                       nullptr, 0, ptr<float>(dw), ptr<float>(db), ptr<float>(ws), x.size(0), x.size(1),
-                                       stream_of(x)));
+    DCLIP_CALL(dclip_layernorm_bwd_res(dy.data_ptr(), dt_code(dy.scalar_type()), scale_entry(dy_scale, 1), dy_ntok,
+                                       x.data_ptr(), dt_code(x.scalar_type()), ptr<float>(w), ptr<float>(mean),
+                                       ptr<float>(rstd), optr<float>(res), ptr<float>(dx), nullptr, 0, ptr<float>(dw),
+                                       ptr<float>(db), ptr<float>(ws), x.size(0), x.size(1), stream_of(x)));
     return dx;
 }
 
 // the same plus lp = (lp_dtype) dx, the next GEMM's 16-bit operand
 std::tuple<Tensor, Tensor> layernorm_bwd_lp(const Tensor& dy, const Tensor& x, const Tensor& w, const Tensor& mean,
                                             const Tensor& rstd, const c10::optional<Tensor>& res, Tensor& dw,
-                                            Tensor& db, at::ScalarType lp_dtype) {
+                                            Tensor& db, at::ScalarType lp_dtype, const c10::optional<Tensor>& dy_scale) {
     check_gpu(dy, "dy"); check_gpu(x, "x"); check_gpu(w, "w"); check_gpu(mean, "mean"); check_gpu(rstd, "rstd");
-    check_opt(res, "res");
+    check_opt(res, "res"); check_opt(dy_scale, "dy_scale");
     TORCH_CHECK(x.dim() == 2 && dy.sizes() == x.sizes(), "layernorm_bwd: dy and x (rows, cols)");
     check_vec(w, x.size(1), "LayerNorm weight"); check_vec(dw, x.size(1), "dw"); check_vec(db, x.size(1), "db");
     check_vec(mean, x.size(0), "mean"); check_vec(rstd, x.size(0), "rstd");
@@ -124,10 +127,11 @@ std::tuple<Tensor, Tensor> layernorm_bwd_lp(const Tensor& dy, const Tensor& x, c
     Tensor dx = at::empty(x.sizes(), like(x, at::kFloat));
     Tensor lp = at::empty(x.sizes(), like(x, lp_dtype));
     Tensor ws = ln_ws(x, dw, db);
-    DCLIP_CALL(dclip_layernorm_bwd_res(dy.data_ptr(), dt_code(dy.scalar_type()), x.data_ptr(), dt_code(x.scalar_type()),
-                                       ptr<float>(w), ptr<float>(mean), ptr<float>(rstd), optr<float>(res), ptr<float>(dx),
-                                       lp.data_ptr(), dt_code(lp_dtype), ptr<float>(dw), ptr<float>(db), ptr<float>(ws),
-                                       x.size(0), x.size(1), stream_of(x)));
+    DCLIP_CALL(dclip_layernorm_bwd_res(dy.data_ptr(), dt_code(dy.scalar_type()), scale_entry(dy_scale, 1), 0,
+                                       x.data_ptr(), dt_code(x.scalar_type()), ptr<float>(w), ptr<float>(mean),
+                                       ptr<float>(rstd), optr<float>(res), ptr<float>(dx), lp.data_ptr(), dt_code(lp_dtype),
+                                       ptr<float>(dw), ptr<float>(db), ptr<float>(ws), x.size(0), x.size(1),
+                                       stream_of(x)));
     return {dx, lp};
 }
 
@@ -402,11 +406,13 @@ std::tuple<Tensor, Tensor, Tensor> add_readout_cast_scaled(const Tensor& a, cons
 std::tuple<Tensor, Tensor, Tensor> layernorm_bwd_scaled(const Tensor& dy, const Tensor& x, const Tensor& w,
                                                         const Tensor& mean, const Tensor& rstd,
                                                         const c10::optional<Tensor>& res, Tensor& dw, Tensor& db,
-                                                        Tensor& st, int64_t use, double target) {
+                                                        Tensor& st, int64_t use, double target,
+                                                        const c10::optional<Tensor>& dy_scale) {
     check_gpu(dy, "dy"); check_gpu(x, "x"); check_gpu(w, "w"); check_gpu(mean, "mean"); check_gpu(rstd, "rstd");
-    check_opt(res, "res");
+    check_opt(res, "res"); check_opt(dy_scale, "dy_scale");
     TORCH_CHECK(x.dim() == 2 && dy.sizes() == x.sizes() && x.size(0) > 0, "layernorm_bwd_scaled: dy and x (rows, cols)");
-    TORCH_CHECK(dy.scalar_type() == at::kFloat && x.scalar_type() == at::kFloat, "layernorm_bwd_scaled: f32 dy and x");
+    TORCH_CHECK((dy.scalar_type() == at::kFloat || dy.scalar_type() == at::kHalf) && x.scalar_type() == at::kFloat,
+                "layernorm_bwd_scaled: f32 or f16 dy, f32 x");
     check_vec(w, x.size(1), "LayerNorm weight"); check_vec(dw, x.size(1), "dw"); check_vec(db, x.size(1), "db");
     check_vec(mean, x.size(0), "mean"); check_vec(rstd, x.size(0), "rstd");
     c10::DeviceGuard g(x.device());
@@ -414,8 +420,9 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_bwd_scaled(const Tensor& dy, const 
     Tensor lp = at::empty(x.sizes(), like(x, at::kHalf));
     Tensor pair = at::empty({4}, x.options());
     Tensor ws = ln_ws(x, dw, db);
-    DCLIP_CALL(dclip_layernorm_bwd_scaled(ptr<float>(dy), x.data_ptr(), dt_code(x.scalar_type()), ptr<float>(w),
-                                          ptr<float>(mean), ptr<float>(rstd), optr<float>(res), ptr<float>(dx),
+    DCLIP_CALL(dclip_layernorm_bwd_scaled(dy.data_ptr(), dt_code(dy.scalar_type()), scale_entry(dy_scale, 1), x.data_ptr(),
+                                          dt_code(x.scalar_type()), ptr<float>(w), ptr<float>(mean), ptr<float>(rstd),
+                                          optr<float>(res), ptr<float>(dx),
                                           lp.data_ptr(), ptr<float>(dw), ptr<float>(db), ptr<float>(ws), x.size(0), x.size(1),
                                           (float)target, scale_state(st, x), (int)use, ptr<float>(pair), stream_of(x)));
     return {dx, lp, pair};
@@ -429,14 +436,14 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_bwd_scaled_add(const Tensor& dy, co
                                                             const c10::optional<Tensor>& res, const Tensor& add,
                                                             const c10::optional<Tensor>& add_scale, int64_t ntok,
                                                             Tensor& dw, Tensor& db, Tensor& st, int64_t use,
-                                                            double target) {
+                                                            double target, const c10::optional<Tensor>& dy_scale) {
     check_gpu(dy, "dy"); check_gpu(x, "x"); check_gpu(w, "w"); check_gpu(mean, "mean"); check_gpu(rstd, "rstd");
-    check_gpu(add, "add"); check_opt(res, "res"); check_opt(add_scale, "add_scale");
+    check_gpu(add, "add"); check_opt(res, "res"); check_opt(add_scale, "add_scale"); check_opt(dy_scale, "dy_scale");
     TORCH_CHECK(x.dim() == 2 && dy.sizes() == x.sizes() && add.sizes() == x.sizes() && x.size(0) > 0,
                 "layernorm_bwd_scaled_add: dy, x and add (rows, cols)");
-    TORCH_CHECK(dy.scalar_type() == at::kFloat && x.scalar_type() == at::kFloat &&
+    TORCH_CHECK((dy.scalar_type() == at::kFloat || dy.scalar_type() == at::kHalf) && x.scalar_type() == at::kFloat &&
                     (add.scalar_type() == at::kHalf || add.scalar_type() == at::kBFloat16),
-                "layernorm_bwd_scaled_add: f32 dy and x, a 16-bit add buffer");
+                "layernorm_bwd_scaled_add: f32 or f16 dy, f32 x, a 16-bit add buffer");
     TORCH_CHECK(ntok > 0 && x.size(0) % ntok == 0, "layernorm_bwd_scaled_add: rows must be a multiple of ntok");
     check_vec(w, x.size(1), "LayerNorm weight"); check_vec(dw, x.size(1), "dw"); check_vec(db, x.size(1), "db");
     check_vec(mean, x.size(0), "mean"); check_vec(rstd, x.size(0), "rstd");
@@ -445,7 +452,8 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_bwd_scaled_add(const Tensor& dy, co
     Tensor lp = at::empty(x.sizes(), like(x, at::kHalf));
     Tensor pair = at::empty({4}, x.options());
     Tensor ws = ln_ws(x, dw, db);
-    DCLIP_CALL(dclip_layernorm_bwd_scaled_add(ptr<float>(dy), ptr<float>(x), ptr<float>(w), ptr<float>(mean),
+    DCLIP_CALL(dclip_layernorm_bwd_scaled_add(dy.data_ptr(), dt_code(dy.scalar_type()), scale_entry(dy_scale, 1),
+                                              ptr<float>(x), ptr<float>(w), ptr<float>(mean),
                                               ptr<float>(rstd), optr<float>(res), add.data_ptr(),
                                               dt_code(add.scalar_type()), scale_entry(add_scale, 1), (int)ntok,
                                               ptr<float>(dx), lp.data_ptr(), ptr<float>(dw), ptr<float>(db),
@@ -873,9 +881,9 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> cityscapes_prepare(const Tensor& img,
 TORCH_LIBRARY(dclip, m) {
     m.def("layernorm_fwd(Tensor x, Tensor w, Tensor b, ScalarType out_dtype, float eps) -> (Tensor, Tensor, Tensor)");
     m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, Tensor? res, Tensor(a!) dw, "
-          "Tensor(b!) db) -> Tensor");
+          "Tensor(b!) db, Tensor? dy_scale=None, int dy_ntok=0) -> Tensor");
     m.def("layernorm_bwd_lp(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, Tensor? res, Tensor(a!) dw, "
-          "Tensor(b!) db, ScalarType lp_dtype) -> (Tensor, Tensor)");
+          "Tensor(b!) db, ScalarType lp_dtype, Tensor? dy_scale=None) -> (Tensor, Tensor)");
     m.def("layernorm_bwd_add(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, Tensor? res, Tensor add, "
           "int ntok, Tensor(a!) dw, Tensor(b!) db, ScalarType lp_dtype) -> (Tensor, Tensor)");
     m.def("gemm(Tensor A, Tensor B, int epi, Tensor? bias, Tensor? aux, ScalarType out_dtype, float alpha, "
@@ -897,10 +905,10 @@ TORCH_LIBRARY(dclip, m) {
     m.def("add_readout_cast_scaled(Tensor a, Tensor? b, int ntok, Tensor? b_scale, Tensor(a!) st, int use, float target) "
           "-> (Tensor, Tensor, Tensor)");
     m.def("layernorm_bwd_scaled(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, Tensor? res, Tensor(a!) dw, "
-          "Tensor(b!) db, Tensor(c!) st, int use, float target) -> (Tensor, Tensor, Tensor)");
+          "Tensor(b!) db, Tensor(c!) st, int use, float target, Tensor? dy_scale=None) -> (Tensor, Tensor, Tensor)");
     m.def("layernorm_bwd_scaled_add(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, Tensor? res, "
           "Tensor add, Tensor? add_scale, int ntok, Tensor(a!) dw, Tensor(b!) db, Tensor(c!) st, int use, "
-          "float target) -> (Tensor, Tensor, Tensor)");
+          "float target, Tensor? dy_scale=None) -> (Tensor, Tensor, Tensor)");
     m.def("attn_fwd(Tensor qkv, int B, int N, int H, float scale) -> (Tensor, Tensor)");
     m.def("attn_fwd_fp8(Tensor qkv, int B, int N, int H) -> (Tensor, Tensor)");
     m.def("attn_bwd(Tensor qkv, Tensor o, Tensor dout, Tensor lse, int B, int N, int H, float scale) -> Tensor");

@@ -83,7 +83,7 @@ int dclip_abi_version(void);
 #define DCLIP_OPT_ATTN_BWD_BLOCK 8   /* CLS-split dK/dV pass: 0 (default) / 6: 64 keys per wave, AGPR dK / dV (attention_dkdv6.hip); 5: software-pipelined 32 keys per wave; 1: the unpipelined one */
 #define DCLIP_OPT_GEMM_TN_COLSUM 9   /* 0 (default): the 256x256 weight-gradient kernel sums dY's columns (bias gradient) itself; 1: a separate pass */
 #define DCLIP_OPT_GEMM_EPI 10      /* persistent NT GEMM epilogue: 0 (default) row-major through LDS, whole 128-B lines per store; 1 the accumulator-layout stores (16 rows x 64 B) */
-#define DCLIP_OPT_GEMM_TAIL 11     /* persistent NT GEMM M tail (<= 16 rows, K % 256 == 0): 0 (default) one MFMA launch over K slices; 1 the 256-row split-K tile + combine pair */
+#define DCLIP_OPT_GEMM_TAIL 11     /* persistent NT GEMM M tail (<= 16 rows): 0 (default) one latency-shaped MFMA launch (16 columns per workgroup, every K-slice load issued up front, side inputs prefetched); 1 the 256-row split-K tile + combine pair; 2 round 4's one launch (64 columns per workgroup, 8 waves, K % 256 == 0) */
 #define DCLIP_OPT_ATTN_FP8_QK 12   /* dclip_attn_fwd_fp8: 0 (default) S = QK^T on the 16-bit MFMA, P V on the fp8 one; 1 both on fp8 (the round-3 kernel) */
 #define DCLIP_OPT_ATTN_DQ_ISSUE 13  /* CLS-split dQ pass LDS-DMA issue: 0 (default) a ragged-tile branch; 1 branch-free per-lane select */
 #define DCLIP_OPT_ATTN_DQ_ROWS 14   /* CLS-split dQ pass query rows per wave: 32 (default; 8 waves, two per SIMD) or 64 (4 waves, one per SIMD) */
@@ -109,10 +109,16 @@ int dclip_layernorm_bwd(const void* dy, int dy_dt, const void* x, int x_dt,
  * null or alias dx) and, when lp is non-null, a 16-bit copy lp = (lp_dt) dx (lp_dt F16 or
  * BF16) — the next GEMM's operand, without a separate clone / cast pass (the
  * x + f(LN(x)) residual of models.py:292-293, backward).                              */
-int dclip_layernorm_bwd_res(const void* dy, int dy_dt, const void* x, int x_dt,
-                            const float* w, const float* mean, const float* rstd,
+int dclip_layernorm_bwd_res(const void* dy, int dy_dt, const float* dy_scale, int64_t dy_ntok,
+                            const void* x, int x_dt, const float* w, const float* mean, const float* rstd,
                             const float* res, float* dx, void* lp, int lp_dt, float* dw, float* db,
                             float* ws, int64_t rows, int64_t cols, void* stream);
+/* dy_scale, dy_ntok (ABI 6; dclip_layernorm_bwd_res, _scaled, _scaled_add): dy is read as
+ * dy * (*dy_scale) when dy_scale is non-null (an f16 dy still on its gradient scale s, dy_scale
+ * pointing at 1/s: the fp16 backward's dX GEMMs write their output for the LN backward in f16 on
+ * the scale their operand carries), and rows with row % dy_ntok == 0 read as 0 when dy_ntok > 0
+ * (a token-buffer gradient whose CLS rows are not part of it: the ln_post read-out's).  NULL / 0:
+ * dy as given.  Need cols in {512, 768, 1024}.                                               */
 /* ws (ABI 5; dclip_layernorm_bwd_res, _scaled, _add, _scaled_add): the caller's scratch of
  * dclip_layernorm_bwd_ws_floats(rows, cols) floats (contents on entry irrelevant, clobbered) for
  * the per-workgroup dw / db partials, summed into dw / db in a fixed order (deterministic) by a
@@ -405,16 +411,16 @@ int dclip_add_readout_amax(const float* a, const void* b, int b_dt, const float*
  *   dclip_add_readout_cast_scaled: sum = a (+ b * (*b_scale_ptr), b's CLS rows read as 0; b may be
  *     null, then sum is not written), lp = (f16)(sum * s).  models.py:565 -> 577-597 as
  *     dclip_add_readout_cast.  cols % 8 == 0.
- *   dclip_layernorm_bwd_scaled: dclip_layernorm_bwd_res with an f32 dy / x and lp = (f16)(dx * s)
- *     (models.py:243-249 backward).  cols in {512, 768, 1024}.                              */
+ *   dclip_layernorm_bwd_scaled: dclip_layernorm_bwd_res with an f32 x, dy f32 or (ABI 6) f16 on
+ *     dy_scale, and lp = (f16)(dx * s) (models.py:243-249 backward).  cols in {512, 768, 1024}. */
 #define DCLIP_DS_STATE_FLOATS 196
 int dclip_add_readout_cast_scaled(const float* a, const void* b, int b_dt, const float* b_scale_ptr, float* sum,
                                   void* lp, int64_t rows, int cols, int ntok, float target, float* st, int use,
                                   float* spair, void* stream);
-int dclip_layernorm_bwd_scaled(const float* dy, const void* x, int x_dt, const float* w, const float* mean,
-                               const float* rstd, const float* res, float* dx, void* lp, float* dw, float* db,
-                               float* ws, int64_t rows, int64_t cols, float target, float* st, int use,
-                               float* spair, void* stream);
+int dclip_layernorm_bwd_scaled(const void* dy, int dy_dt, const float* dy_scale, const void* x, int x_dt,
+                               const float* w, const float* mean, const float* rstd, const float* res, float* dx,
+                               void* lp, float* dw, float* db, float* ws, int64_t rows, int64_t cols, float target,
+                               float* st, int use, float* spair, void* stream);
 
 /* LayerNorm backward of a block's ln_1 with the PREVIOUS block's read-out map gradient folded in
  * (models.py:243-249 backward + the models.py:565 -> 577-597 read-out's gradient):
@@ -426,16 +432,16 @@ int dclip_layernorm_bwd_scaled(const float* dy, const void* x, int x_dt, const f
 int dclip_layernorm_bwd_add(const void* dy, int dy_dt, const float* x, const float* w, const float* mean,
                             const float* rstd, const float* res, const void* add, int ntok, float* dx, void* lp,
                             int lp_dt, float* dw, float* db, float* ws, int64_t rows, int64_t cols, void* stream);
-/* The fp16 backward's form: dclip_layernorm_bwd_scaled (f32 dy / x, lp = (f16)(dx * s) on the
+/* The fp16 backward's form: dclip_layernorm_bwd_scaled (dy f32 or f16 on dy_scale, f32 x, lp = (f16)(dx * s) on the
  * delayed scale of st's use `use`, (s, 1/s) to spair) with dx = (res + LN^T(dy)) + add * (*add_scale)
  * (add: f16 or bf16 (add_dt), CLS rows read as 0; add_scale may be NULL = 1) — in place of
  * dclip_layernorm_bwd_res + dclip_add_readout_cast_scaled on the same site state.  cols in
  * {512, 768, 1024}. */
-int dclip_layernorm_bwd_scaled_add(const float* dy, const float* x, const float* w, const float* mean,
-                                   const float* rstd, const float* res, const void* add, int add_dt,
-                                   const float* add_scale, int ntok, float* dx, void* lp, float* dw, float* db,
-                                   float* ws, int64_t rows, int64_t cols, float target, float* st, int use,
-                                   float* spair, void* stream);
+int dclip_layernorm_bwd_scaled_add(const void* dy, int dy_dt, const float* dy_scale, const float* x,
+                                   const float* w, const float* mean, const float* rstd, const float* res,
+                                   const void* add, int add_dt, const float* add_scale, int ntok, float* dx,
+                                   void* lp, float* dw, float* db, float* ws, int64_t rows, int64_t cols,
+                                   float target, float* st, int use, float* spair, void* stream);
 
 /* Train-mode BatchNorm2d (+ optionally the ReLU after it) on a channels-last 16-bit map viewed as
  * rows (B*H*W) of C channels at a row pitch of ld elements (ld = C for a whole map; larger for a

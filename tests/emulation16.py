@@ -11,8 +11,8 @@ Rounding points (ops.PatchEmbedFn / ops.BlockFn / ops.ReadoutFn, csrc/attention.
             (unnormalised, fp32 row sums); o; z and h = QuickGELU(z); 16-bit read-out maps
   backward  the embedding gradient (dclip_tokens_bwd's cast); the MLP branch's gradient dy (the
             cast or, with the read-out fold, dclip_layernorm_bwd_add's copy); dz (EPI_GELU_BWD
-            output); dxh2 / dxh1 when LN_DY_LP (bf16: the dX GEMMs write bf16 for the LN
-            backward); the attention branch's gradient dyo (the LN backward's lp copy); dO (the
+            output); dxh2 / dxh1 when LN_DY_LP (the dX GEMMs write 16 bits for the LN backward:
+            bf16, or fp16 on the operand's gradient scale); the attention branch's gradient dyo (the LN backward's lp copy); dO (the
             out-projection dX GEMM output); dS and P inside the attention backward; dqkv
   fp32      residual stream, LN statistics and backward, softmax statistics, every accumulation
 fp16 gradients are rounded on a per-tensor power-of-two scale (16 / max|g|, ops.grad_scale; the
@@ -136,11 +136,16 @@ def vit_forward16(img, p, dt, pre="backbone.", patch=16, heads=12, layers=12, ou
     """oracle.vit_forward (models.py:543-597) with the HIP path's 16-bit rounding points (module
     docstring).  map_dt: the read-out maps' dtype (None: fp32 maps, the backbone's default for fp32
     images; a 16-bit dtype: maps stored and their gradients arriving in it, DenseCLIP's HIP-neck
-    path).  ln_dy_lp: the bf16 LN-backward inputs (default ops.LN_DY_LP's rule: bf16 only)."""
+    path).  ln_dy_lp: the 16-bit LN-backward inputs (default: ops.LN_DY_LP for bf16, ops.LN_DY_LP_FP16
+    at the fast LN widths 512 / 768 / 1024 for fp16 — on the gradient scale its GEMM operand carries)."""
     if out_indices is None:
         out_indices = [layers - 1]
     if ln_dy_lp is None:
-        ln_dy_lp = dt == torch.bfloat16
+        from denseclip_vit_multimodal_amd import ops
+        if dt == torch.bfloat16:
+            ln_dy_lp = ops.LN_DY_LP
+        else:
+            ln_dy_lp = ops.LN_DY_LP_FP16 and p[pre + "ln_pre.weight"].shape[0] in (512, 768, 1024)
     B = img.shape[0]
     rf = lambda t: RoundFwd.apply(t, dt)  # noqa: E731
     x = RoundBwd.apply(F.conv2d(rf(img), rf(p[pre + "conv1.weight"]), stride=patch), dt)

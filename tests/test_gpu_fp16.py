@@ -143,6 +143,64 @@ def test_layernorm_bwd_scaled(cols):
         s_expect = host_scale(dx1)
 
 
+@pytest.mark.parametrize("cols", [768, 1024])
+@pytest.mark.parametrize("form", ["res", "lp", "scaled", "scaled_add"])
+def test_layernorm_bwd_f16_dy_on_scale(cols, form):
+    """ABI 6: an fp16 dy still on its gradient scale s, read as dy * 1/s (dy_scale = the (s, 1/s)
+    pair) by every LN backward form the fp16 block uses == the same form on the fp32 dy * 1/s
+    (bitwise: one fp32 multiply either way, the rest the same instruction stream)."""
+    from denseclip_vit_multimodal_amd import ops
+    rows, ntok = 4 * 257, 257
+    x = torch.randn(rows, cols, device=DEV)
+    w = torch.rand(cols, device=DEV) + 0.5
+    b = torch.randn(cols, device=DEV)
+    _, mean, rstd = ops.layernorm_fwd(x, w, b, torch.float16)
+    s = 2.0 ** 22
+    pair = torch.tensor([s, 1.0 / s, 0.0, 0.0], device=DEV)
+    dyh = (torch.randn(rows, cols, device=DEV) * 1e-6 * s).half()  # scaled: a 16-magnitude fp16 operand
+    dyf = dyh.float() * pair[1]
+    res = torch.randn(rows, cols, device=DEV) * 1e-6
+    add = (torch.randn(rows, cols, device=DEV) * 8).half()
+    out = []
+    for dy, sc in ((dyf, None), (dyh, pair)):
+        dw, db = torch.zeros(cols, device=DEV), torch.zeros(cols, device=DEV)
+        if form == "res":
+            r = (ops.layernorm_bwd(dy, x, w, mean, rstd, dw, db, res=res, dy_scale=sc),)
+        elif form == "lp":
+            r = ops.layernorm_bwd(dy, x, w, mean, rstd, dw, db, res=res, lp_dtype=torch.float16, dy_scale=sc)
+        elif form == "scaled":
+            r = ops.layernorm_bwd_scaled(dy, x, w, mean, rstd, dw, db, res, _ds_state(2.0 ** 17), 0, dy_scale=sc)
+        else:
+            r = ops.layernorm_bwd_scaled_add(dy, x, w, mean, rstd, dw, db, res, add, ntok, pair, _ds_state(2.0 ** 17),
+                                             0, dy_scale=sc)
+        out.append(tuple(r) + (dw, db))
+    for a, c in zip(*out):
+        assert torch.equal(a, c)
+
+
+def test_layernorm_bwd_dy_ntok_masks_cls_rows():
+    """dy_ntok: a token-buffer gradient whose CLS rows (row % ntok == 0) hold garbage reads them as
+    0 — the ln_post read-out's backward straight from the neck's 16-bit gradient buffer (bitwise the
+    fp32 copy with the CLS rows zeroed and the heads' 1/s multiplied in, the path it replaces)."""
+    from denseclip_vit_multimodal_amd import ops
+    rows, cols, ntok = 3 * 129, 768, 129
+    x = torch.randn(rows, cols, device=DEV)
+    w = torch.rand(cols, device=DEV) + 0.5
+    b = torch.randn(cols, device=DEV)
+    _, mean, rstd = ops.layernorm_fwd(x, w, b, torch.float16)
+    hs = torch.tensor([2.0 ** 10, 2.0 ** -10, 0.0, 0.0], device=DEV)
+    g = torch.randn(rows, cols, device=DEV).half()
+    g.view(3, ntok, cols)[:, 0] = float("nan")  # never read
+    ref = g.float()
+    ref.view(3, ntok, cols)[:, 0].zero_()
+    ref.mul_(hs[1])
+    dw0, db0 = torch.zeros(cols, device=DEV), torch.zeros(cols, device=DEV)
+    dx0 = ops.layernorm_bwd(ref, x, w, mean, rstd, dw0, db0)
+    dw1, db1 = torch.zeros(cols, device=DEV), torch.zeros(cols, device=DEV)
+    dx1 = ops.layernorm_bwd(g, x, w, mean, rstd, dw1, db1, dy_scale=hs, dy_ntok=ntok)
+    assert torch.equal(dx1, dx0) and torch.equal(dw1, dw0) and torch.equal(db1, db0)
+
+
 @pytest.mark.parametrize("adt", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("with_scale", [True, False])
 def test_layernorm_bwd_scaled_add(adt, with_scale):

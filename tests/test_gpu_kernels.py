@@ -90,7 +90,7 @@ def test_layernorm_bwd_res(cols, lpdt):
     # the C ABI also takes res aliasing dx (in place), as the op layer's callers once did
     from denseclip_vit_multimodal_amd import _native as Nat
     dx2 = res.clone()
-    Nat.call("dclip_layernorm_bwd_res", dy.data_ptr(), Nat.BF16, x.data_ptr(), Nat.F32, w.data_ptr(), mu.data_ptr(),
+    Nat.call("dclip_layernorm_bwd_res", dy.data_ptr(), Nat.BF16, None, 0, x.data_ptr(), Nat.F32, w.data_ptr(), mu.data_ptr(),
              rs.data_ptr(), dx2.data_ptr(), dx2.data_ptr(), None, 0, dw.data_ptr(), None, None, rows, cols,
              torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
@@ -291,15 +291,21 @@ def test_gemm_persistent_epilogue_bitwise(M, C, dt):
             assert torch.equal(a, b), k
 
 
-@pytest.mark.parametrize("K", [768, 3072])
-def test_gemm_m_tail_single_launch(K):
-    """The persistent GEMM's 8-row M tail (8 x 8193 tokens) in one MFMA launch (default) against
-    the split-K tile + combine pair (DCLIP_OPT_GEMM_TAIL 1) and an fp32 reference, every epilogue:
-    the rows before the tail are untouched by the choice (bitwise), the tail rows agree to fp32
-    summation order."""
+def O_qgelu_grad(z):
+    """d/dz of QuickGELU z * sigmoid(1.702 z) (models.py:252-254)."""
+    sg = torch.sigmoid(1.702 * z)
+    return sg + 1.702 * z * sg * (1 - sg)
+
+
+@pytest.mark.parametrize("K,mt,other", [(768, 8, 1), (3072, 8, 1), (768, 8, 2), (2304, 8, 2), (3072, 13, 2)])
+def test_gemm_m_tail_single_launch(K, mt, other):
+    """The persistent GEMM's M tail (8 x 8193 tokens: 8 rows) in the latency-shaped launch (default,
+    gemm_tail16x16_kernel) against the split-K tile + combine pair (DCLIP_OPT_GEMM_TAIL 1), round 4's
+    one-launch kernel (2) and an fp32 reference, every epilogue: the rows before the tail are untouched
+    by the choice (bitwise), the tail rows agree to fp32 summation order."""
     from denseclip_vit_multimodal_amd import _native as Nat
     O = ops()
-    M, C = 65544, 768
+    M, C = 65536 + mt, 768
     dt = torch.bfloat16
     torch.manual_seed(11)
     A = torch.randn(M, K, device=DEV).to(dt)
@@ -320,18 +326,23 @@ def test_gemm_m_tail_single_launch(K):
                 "gelu_bwd": O.gemm(A, Wn, Nat.EPI_GELU_BWD, aux=z0)}
 
     new = run_all()
+    again = run_all()
     try:
-        Nat.call("dclip_set_option", Nat.OPT_GEMM_TAIL, 1)
+        Nat.call("dclip_set_option", Nat.OPT_GEMM_TAIL, other)
         old = run_all()
     finally:
         Nat.call("dclip_set_option", Nat.OPT_GEMM_TAIL, 0)
-    ref = A[-8:].float() @ Wn.float().t() + bias
+    ref = A[-mt:].float() @ Wn.float().t() + bias
     for k in new:
-        assert torch.equal(new[k][:-8], old[k][:-8]), k
+        assert torch.equal(new[k], again[k]), k  # deterministic
+        assert torch.equal(new[k][:-mt], old[k][:-mt]), k
         tol = 1e-5 if new[k].dtype == torch.float32 else TOL[dt]
-        assert rel_err(new[k][-8:].float(), old[k][-8:].float()) < tol, k
-    assert rel_err(new["store32"][-8:], ref) < 1e-5
-    assert rel_err(new["resid"][-8:], res[-8:] + ref) < 1e-5
+        assert rel_err(new[k][-mt:].float(), old[k][-mt:].float()) < tol, k
+    assert rel_err(new["store32"][-mt:], ref) < 1e-5
+    assert rel_err(new["resid"][-mt:], res[-mt:] + ref) < 1e-5
+    assert rel_err(new["scaled"][-mt:].float(), (ref * sc).to(dt).float()) < TOL[dt]
+    assert rel_err(new["gelu_bwd"][-mt:].float(),
+                   (ref - bias) * O_qgelu_grad(z0[-mt:].float())) < TOL[dt]
 
 
 @pytest.fixture
