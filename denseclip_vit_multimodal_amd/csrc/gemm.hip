@@ -650,6 +650,13 @@ __device__ __forceinline__ void store_pair16(OutT* row_base, int col_i, const f3
     *(u32x4*)(row_base + col) = w;
 }
 
+// a 16-byte global store, with the streaming (nontemporal) hint when NTS
+template <bool NTS, typename V>
+__device__ __forceinline__ void st16(V* p, const V& v) {
+    if constexpr (NTS) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 template <typename OutT>
 __device__ __forceinline__ void store4_out(OutT* p, const f32x4& v) {
     if constexpr (sizeof(OutT) == 4) {
@@ -786,7 +793,7 @@ __device__ __forceinline__ void pers_epilogue(const f32x4 (&acc)[Cfg::NB][Cfg::M
 // XOR swizzles keep both sides free of bank conflicts:
 //   16-bit image (128-B rows, 16-B chunks c): physical chunk c ^ ((row >> 1) & 7)
 //   f32 image    (256-B rows, 16-B chunks c): physical chunk c ^ (row & 15)
-template <typename T, int EPI, typename OutT, typename Cfg>
+template <typename T, int EPI, typename OutT, typename Cfg, bool NTS = false>
 __device__ __forceinline__ void pers_epilogue_lds(const f32x4 (&acc)[Cfg::NB][Cfg::MB],
                                                   const PersCols<EPI, Cfg::NB>& pc, int mw, int nw, int l16, int lq,
                                                   int lane, float alpha, const void* __restrict__ aux, int64_t ld_aux,
@@ -859,7 +866,7 @@ __device__ __forceinline__ void pers_epilogue_lds(const f32x4 (&acc)[Cfg::NB][Cf
                 const int col = nw + 4 * cc;
                 if constexpr (EPI == DCLIP_EPI_RESIDUAL) {
                     x += cur[q];
-                    *(f32x4*)((float*)C + row * ldc + col) = x;
+                    st16<NTS>((f32x4*)((float*)C + row * ldc + col), x);
                     if (C2 != nullptr) {
                         const t4 y = {(T)x[0], (T)x[1], (T)x[2], (T)x[3]};
                         *(t4*)((T*)C2 + row * ldc2 + col) = y;
@@ -880,9 +887,9 @@ __device__ __forceinline__ void pers_epilogue_lds(const f32x4 (&acc)[Cfg::NB][Cf
                 const int64_t row = row0 + rr;
                 const int col = nw + 8 * cc;
                 if (EPI != DCLIP_EPI_GELU || C != nullptr)  // GELU: z optional
-                    *(u32x4*)((OutT*)C + row * ldc + col) = *(const u32x4*)(img + off);
+                    st16<NTS>((u32x4*)((OutT*)C + row * ldc + col), *(const u32x4*)(img + off));
                 if constexpr (EPI == DCLIP_EPI_GELU)
-                    *(u32x4*)((OutT*)C2 + row * ldc2 + col) = *(const u32x4*)(img + 2048 + off);
+                    st16<NTS>((u32x4*)((OutT*)C2 + row * ldc2 + col), *(const u32x4*)(img + 2048 + off));
             }
         }
         asm volatile("" ::: "memory");  // the next chunk's writes stay behind these reads
@@ -960,7 +967,7 @@ __device__ __forceinline__ int pers_resolve(unsigned* __restrict__ sched, int v,
     return ntiles;
 }
 
-template <typename T, int EPI, typename OutT, int NW = 8, bool ELDS = false, bool DYN = false>
+template <typename T, int EPI, typename OutT, int NW = 8, bool ELDS = false, bool DYN = false, bool NTS = false>
 __global__ __launch_bounds__(64 * NW, 1) void gemm_nt_pers_kernel(
     const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb, int K, int tiles_m, int tiles_n,
     const float* __restrict__ bias, const void* __restrict__ aux, int64_t ld_aux, void* __restrict__ C, int64_t ldc,
@@ -1114,7 +1121,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_nt_pers_kernel(
         }
         if constexpr (NW == 8) {
             if constexpr (epi_lds)
-                pers_epilogue_lds<T, EPI, OutT, Cfg>(acc, pc, m0 + wm * 128, n0 + wn * Cfg::WTN, l16, lq, lane, alpha,
+                pers_epilogue_lds<T, EPI, OutT, Cfg, NTS>(acc, pc, m0 + wm * 128, n0 + wn * Cfg::WTN, l16, lq, lane, alpha,
                                                      aux, ld_aux, C, ldc, C2, ldc2, smem + Cfg::SMEM + wave * EPI_IMG);
             else
                 pers_epilogue<T, EPI, OutT, Cfg>(acc, pc, m0 + wm * 128, n0 + wn * Cfg::WTN, l16, lq, alpha, aux, ld_aux,
@@ -2261,6 +2268,21 @@ unsigned* gemm_sched_counters(hipStream_t st) {
     return base[dev] + 512 * used[dev]++;
 }
 
+// Streaming (nontemporal) epilogue stores for the wide forward outputs (qkv, the MLP's z / h:
+// N >= 2048): they leave L2 to the operands the K-loop re-reads (B, the weight, by every row of
+// tiles; A by the N / 256 column tiles of a row) instead of evicting them — qkv -11 %, c_fc -14 %
+// per call, the 7-GEMM set -4.2 %, the step -0.2 % (bf16 and fp16; profiles/r05/r5p: the consumers
+// read them from HBM rather than the Infinity Cache, which takes back most of it).  The residual
+// stream (read by the LayerNorm right after), the narrow dX outputs and the GELU' epilogue (which
+// reads its pre-activations beside the stores) measured equal or slower and keep plain stores.
+// DCLIP_OPT_GEMM_EPI: 0 this rule, 2 always, 3 never.
+inline bool pers_streaming_stores(int epi, int64_t N) {
+    const int o = dclip_option(DCLIP_OPT_GEMM_EPI);
+    if (o == 2) return true;
+    if (o != 0) return false;
+    return N >= 2048 && epi != DCLIP_EPI_GELU_BWD && epi != DCLIP_EPI_RESIDUAL;
+}
+
 template <typename T, int EPI, typename OutT, int NW = 8, bool PIPE = false>
 bool launch_pers(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
                  Alpha alpha, const float* bias, const void* aux, int64_t ld_aux, void* C, int64_t ldc, void* C2,
@@ -2326,6 +2348,10 @@ bool launch_pers(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t
                 gemm_nt_pers_kernel<T, EPI, OutT, NW, true, NW == 8><<<G, 64 * NW, 0, st>>>(
                     (const T*)A, lda, (const T*)B, ldb, (int)K, (int)(Mfull / 256), (int)(N / 256), bias, aux, ld_aux, C,
                     ldc, C2, ldc2, alpha, sched);
+            else if (NW == 8 && pers_streaming_stores(EPI, N))
+                gemm_nt_pers_kernel<T, EPI, OutT, NW, true, false, true><<<G, 64 * NW, 0, st>>>(
+                    (const T*)A, lda, (const T*)B, ldb, (int)K, (int)(Mfull / 256), (int)(N / 256), bias, aux, ld_aux, C,
+                    ldc, C2, ldc2, alpha);
             else if (NW == 8 && dclip_option(DCLIP_OPT_GEMM_EPI) != 1)
                 gemm_nt_pers_kernel<T, EPI, OutT, NW, true><<<G, 64 * NW, 0, st>>>(
                     (const T*)A, lda, (const T*)B, ldb, (int)K, (int)(Mfull / 256), (int)(N / 256), bias, aux, ld_aux, C,

@@ -3,7 +3,7 @@ at the bench shape (M = 8 x 8193 = 256k + 8), bf16, with the model's epilogues; 
 round, medians of per-call HIP-event times (main kernel + tail together).  Under rocprofv3 the
 tail kernels' own durations are in the kernel stats.
 
-  python tools/ab_gemm_tail.py [rounds]
+  python tools/ab_gemm_tail.py [rounds] [option id] [values, comma-separated]   (default: 11 0,2,1)
 """
 import os
 import sys
@@ -17,6 +17,8 @@ from denseclip_vit_multimodal_amd import ops as O  # noqa: E402
 M, C = 8 * 8193, 768
 bf = torch.bfloat16
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 7
+OPT = int(sys.argv[2]) if len(sys.argv) > 2 else Nat.OPT_GEMM_TAIL
+opts = [int(v) for v in sys.argv[3].split(",")] if len(sys.argv) > 3 else [0, 2, 1]
 torch.manual_seed(0)
 dev = "cuda"
 
@@ -55,20 +57,19 @@ def ev(fn, reps=10):
     return e0.elapsed_time(e1) / reps * 1e3
 
 
-opts = [0, 2, 1]
 res_t = {(n, o): [] for n, _ in cases for o in opts}
 try:
     for r in range(rounds):
         for n, fn in cases:
             for o in opts:
-                Nat.call("dclip_set_option", Nat.OPT_GEMM_TAIL, o)
+                Nat.call("dclip_set_option", OPT, o)
                 res_t[(n, o)].append(ev(fn))
 finally:
-    Nat.call("dclip_set_option", Nat.OPT_GEMM_TAIL, 0)
+    Nat.call("dclip_set_option", OPT, 0)
 tot = {o: 0.0 for o in opts}
 for n, _ in cases:
     med = {o: sorted(res_t[(n, o)])[rounds // 2] for o in opts}
     for o in opts:
         tot[o] += med[o]
-    print(f"{n:16s} " + "  ".join(f"opt{o} {med[o]:7.1f} us" for o in opts) + f"  new-r4 {med[0] - med[2]:+6.1f} us", flush=True)
+    print(f"{n:16s} " + "  ".join(f"opt{o} {med[o]:7.1f} us" for o in opts) + f"  {opts[0]}-{opts[1]} {med[opts[0]] - med[opts[1]]:+6.1f} us", flush=True)
 print("set    " + "  ".join(f"opt{o} {tot[o]:7.1f} us" for o in opts))
