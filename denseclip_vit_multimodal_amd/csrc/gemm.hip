@@ -967,7 +967,8 @@ __device__ __forceinline__ int pers_resolve(unsigned* __restrict__ sched, int v,
     return ntiles;
 }
 
-template <typename T, int EPI, typename OutT, int NW = 8, bool ELDS = false, bool DYN = false, bool NTS = false>
+template <typename T, int EPI, typename OutT, int NW = 8, bool ELDS = false, bool DYN = false, bool NTS = false,
+          bool PF = false>
 __global__ __launch_bounds__(64 * NW, 1) void gemm_nt_pers_kernel(
     const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb, int K, int tiles_m, int tiles_n,
     const float* __restrict__ bias, const void* __restrict__ aux, int64_t ld_aux, void* __restrict__ C, int64_t ldc,
@@ -1067,6 +1068,40 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_nt_pers_kernel(
             }
             const char* At = smem + slot * Cfg::STAGE_BYTES;
             const char* Bt = At + Cfg::A_BYTES;
+            if constexpr (PF && NW == 8) {
+                // fragment reads one group ahead: a group = the 8 MFMAs of one pair of A fragments
+                // (both 32-deep halves of the K-step: 8 groups); each group's reads are issued before
+                // the previous group's MFMAs, so a read has 8 MFMAs (~128 cycles) to land instead of
+                // the 4 hipcc leaves it when it streams the A fragments two at a time
+                frag fb[2][Cfg::NB], fa[4];
+                auto rd_b = [&](int ks) {
+#pragma unroll
+                    for (int i = 0; i < Cfg::NB; ++i)
+                        fb[ks][i] = big_frag<T, 64>(Bt, wn * Cfg::WTN + i * 16 + l16, ks * 4 + lq);
+                };
+                auto rd_a = [&](int ks, int p) {
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+                        fa[(2 * p + h) & 3] = big_frag<T, 64>(At, wm * Cfg::WTM + (2 * p + h) * 16 + l16, ks * 4 + lq);
+                };
+                rd_b(0);
+                rd_a(0, 0);
+#pragma unroll
+                for (int g = 0; g < 8; ++g) {
+                    const int ks = g >> 2, p = g & 3;
+                    if (g + 1 < 8) {
+                        if (((g + 1) & 3) == 0) rd_b((g + 1) >> 2);
+                        rd_a((g + 1) >> 2, (g + 1) & 3);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+#pragma unroll
+                        for (int i = 0; i < Cfg::NB; ++i)
+                            acc[i][2 * p + h] = Mfma16<T>::mma(fb[ks][i], fa[(2 * p + h) & 3], acc[i][2 * p + h]);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            } else {
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
                 frag fb[Cfg::NB], fa[Cfg::MB];
@@ -1084,6 +1119,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_nt_pers_kernel(
 #pragma unroll
                         for (int i = 0; i < Cfg::NB; ++i) acc[i][j] = Mfma16<T>::mma(fb[i], fa[j], acc[i][j]);
                 }
+            }
             }
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (DYN) {
@@ -1457,6 +1493,46 @@ __device__ __forceinline__ void tn_stage_buf(const void* A, uint32_t abytes, con
 #endif
 }
 
+// One full 64-token K-step of the 8-wave TN kernel with the transposed fragment reads issued one
+// group ahead (a group = the 8 MFMAs of one pair of A fragments; 8 groups per K-step), as
+// gemm_nt_pers_kernel's PF K-loop; the fused column sums (CS, do_cs waves) take each A pair right
+// after its MFMAs.
+template <typename T, typename Cfg, bool CS>
+__device__ __forceinline__ void tn_kstep_pf(f32x4 (&acc)[Cfg::NB][Cfg::MB], float (&cs)[Cfg::MB], const char* At,
+                                            const char* Bt, int wm, int wn, int lane, bool do_cs) {
+    typedef typename Mfma<T>::frag frag;
+    frag fb[2][Cfg::NB], fa[4];
+    auto rd_b = [&](int ks) {
+#pragma unroll
+        for (int i = 0; i < Cfg::NB; ++i) fb[ks][i] = tn_frag<T>(Bt, ks, wn * Cfg::WTN + i * 16, lane);
+    };
+    auto rd_a = [&](int ks, int p) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) fa[(2 * p + h) & 3] = tn_frag<T>(At, ks, wm * Cfg::WTM + (2 * p + h) * 16, lane);
+    };
+    rd_b(0);
+    rd_a(0, 0);
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+        const int ks = g >> 2, p = g & 3;
+        if (g + 1 < 8) {
+            if (((g + 1) & 3) == 0) rd_b((g + 1) >> 2);
+            rd_a((g + 1) >> 2, (g + 1) & 3);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int i = 0; i < Cfg::NB; ++i)
+                acc[i][2 * p + h] = Mfma16<T>::mma(fb[ks][i], fa[(2 * p + h) & 3], acc[i][2 * p + h]);
+        if (CS && do_cs) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) cs[2 * p + h] = frag_sum8(fa[(2 * p + h) & 3], cs[2 * p + h]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 // CS: also accumulate the column sums of A over the K range (alpha * sum_k A[k][m] into colsum,
 // the bias gradient when A is dY): the tiles in column 0 of the tile grid own them, and of their
 // waves the ones with wn == 0 (the other three hold the same A fragments) add their fragments
@@ -1467,7 +1543,7 @@ __device__ __forceinline__ void tn_stage_buf(const void* A, uint32_t abytes, con
 // 0.75 LDS reads per MFMA (this pass is LDS-bound).  Its 256 accumulator registers
 // live in AGPRs as "+a" operands of inline-asm MFMAs (tn_mfma_row): left to itself, hipcc shuttled
 // them between the two files (~300 v_accvgpr copies per 128 MFMAs).
-template <typename T, int EPI, int BKT = 64, int STAGES = 2, bool CS = false, int NW = 8>
+template <typename T, int EPI, int BKT = 64, int STAGES = 2, bool CS = false, int NW = 8, bool PF = false>
 __global__ __launch_bounds__(64 * NW, 1) void gemm_tn_big_kernel(const T* __restrict__ A, int64_t lda,
                                                              const T* __restrict__ B, int64_t ldb, int M, int N,
                                                              int Kreal, int k_chunk, int tiles_m, int tiles_n,
@@ -1550,6 +1626,9 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_tn_big_kernel(const T* __rest
         const char* At = smem + (kt_ % STAGES) * STAGE;                                                             \
         const char* Bt = At + BKT * 512;                                                                            \
         const int k0 = kbeg + kt_ * BKT;                                                                            \
+        if (PF && NW == 8 && BKT == 64 && !(RAGGED)) {                                                              \
+            tn_kstep_pf<T, Cfg, CS>(acc, cs, At, Bt, wm, wn, lane, do_cs);                                          \
+        } else                                                                                                      \
         _Pragma("unroll") for (int ks = 0; ks < BKT / 32; ++ks) {                                                   \
             frag fb[Cfg::NB], fa[Cfg::MB];                                                                          \
             _Pragma("unroll") for (int i = 0; i < Cfg::NB; ++i) fb[i] = tn_frag<T>(Bt, ks, wn * Cfg::WTN + i * 16, lane); \
@@ -2283,6 +2362,17 @@ inline bool pers_streaming_stores(int epi, int64_t N) {
     return N >= 2048 && epi != DCLIP_EPI_GELU_BWD && epi != DCLIP_EPI_RESIDUAL;
 }
 
+// The K-loop with the fragment reads one group ahead (gemm_nt_pers_kernel PF) on every epilogue but
+// GELU: c_proj -6 %, the dX GEMMs -3..-6 %, out_proj -4 %, qkv -1 %, but the MLP-up GEMM with the
+// GELU epilogue +3 % (profiles/r05/r5u).  DCLIP_OPT_GEMM_KLOOP: 0 this rule, 1 every NT and TN
+// 8-wave K-loop (the TN kernel measured 1-5 % slower with it), 2 none.
+inline bool pers_prefetch_kloop(int epi) {
+    const int o = dclip_option(DCLIP_OPT_GEMM_KLOOP);
+    if (o == 1) return true;
+    if (o != 0) return false;
+    return epi != DCLIP_EPI_GELU;
+}
+
 template <typename T, int EPI, typename OutT, int NW = 8, bool PIPE = false>
 bool launch_pers(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
                  Alpha alpha, const float* bias, const void* aux, int64_t ld_aux, void* C, int64_t ldc, void* C2,
@@ -2348,14 +2438,18 @@ bool launch_pers(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t
                 gemm_nt_pers_kernel<T, EPI, OutT, NW, true, NW == 8><<<G, 64 * NW, 0, st>>>(
                     (const T*)A, lda, (const T*)B, ldb, (int)K, (int)(Mfull / 256), (int)(N / 256), bias, aux, ld_aux, C,
                     ldc, C2, ldc2, alpha, sched);
-            else if (NW == 8 && pers_streaming_stores(EPI, N))
-                gemm_nt_pers_kernel<T, EPI, OutT, NW, true, false, true><<<G, 64 * NW, 0, st>>>(
-                    (const T*)A, lda, (const T*)B, ldb, (int)K, (int)(Mfull / 256), (int)(N / 256), bias, aux, ld_aux, C,
-                    ldc, C2, ldc2, alpha);
-            else if (NW == 8 && dclip_option(DCLIP_OPT_GEMM_EPI) != 1)
-                gemm_nt_pers_kernel<T, EPI, OutT, NW, true><<<G, 64 * NW, 0, st>>>(
-                    (const T*)A, lda, (const T*)B, ldb, (int)K, (int)(Mfull / 256), (int)(N / 256), bias, aux, ld_aux, C,
-                    ldc, C2, ldc2, alpha);
+#define PERS_LAUNCH(NTS_, PF_)                                                                                  \
+    gemm_nt_pers_kernel<T, EPI, OutT, NW, true, false, NTS_, PF_><<<G, 64 * NW, 0, st>>>(                        \
+        (const T*)A, lda, (const T*)B, ldb, (int)K, (int)(Mfull / 256), (int)(N / 256), bias, aux, ld_aux, C, ldc, C2, \
+        ldc2, alpha)
+            else if (NW == 8 && dclip_option(DCLIP_OPT_GEMM_EPI) != 1) {
+                const bool nts = pers_streaming_stores(EPI, N), pf = pers_prefetch_kloop(EPI);
+                if (nts && pf) PERS_LAUNCH(true, true);
+                else if (nts) PERS_LAUNCH(true, false);
+                else if (pf) PERS_LAUNCH(false, true);
+                else PERS_LAUNCH(false, false);
+            }
+#undef PERS_LAUNCH
             else
                 gemm_nt_pers_kernel<T, EPI, OutT, NW, false><<<G, 64 * NW, 0, st>>>(
                     (const T*)A, lda, (const T*)B, ldb, (int)K, (int)(Mfull / 256), (int)(N / 256), bias, aux, ld_aux, C,
@@ -2565,6 +2659,7 @@ extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda
     const int k_chunk = (int)(K_pad / splits);
     dim3 grid(tiles_m * tiles_n, splits);
     const int tn_opt = dclip_option(DCLIP_OPT_GEMM_TN_TILE);
+    const bool tn_pf = dclip_option(DCLIP_OPT_GEMM_KLOOP) == 1;
     const bool big = tn_opt != 1 && M >= 256 && N >= 256;
     // the big kernel sums A's columns itself (DCLIP_OPT_GEMM_TN_COLSUM 1: the separate pass)
     const bool fused_cs = colsum_a && big && dclip_option(DCLIP_OPT_GEMM_TN_COLSUM) != 1;
@@ -2578,8 +2673,8 @@ extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda
     gemm_tn_kernel<T, EPI, float><<<grid, 256, 0, st>>>((const T*)A, lda, (const T*)B, ldb, (int)M, (int)N,   \
                                                         (int)K, k_chunk, tiles_m, tiles_n, nullptr, OUT,        \
                                                         EPI == DCLIP_EPI_SPLITK ? N : ldc, (int64_t)M * N, alpha)
-#define TN_BIG_V(T, EPI, OUT, BKT, STG, CS, NW)                                                                \
-    gemm_tn_big_kernel<T, EPI, BKT, STG, CS, NW><<<dim3(tm2 * tn2 * splits), 64 * NW, 0, st>>>(                \
+#define TN_BIG_V(T, EPI, OUT, BKT, STG, CS, NW, ...)                                                           \
+    gemm_tn_big_kernel<T, EPI, BKT, STG, CS, NW, ##__VA_ARGS__><<<dim3(tm2 * tn2 * splits), 64 * NW, 0, st>>>( \
         (const T*)A, lda, (const T*)B, ldb, (int)M, (int)N, (int)K, k_chunk, tm2, tn2, OUT,                     \
         EPI == DCLIP_EPI_SPLITK ? N : ldc, (int64_t)M * N, alpha, EPI == DCLIP_EPI_SPLITK ? cs_part : colsum_a)
 #define TN_BIG(T, EPI, OUT)                                                                                    \
@@ -2588,6 +2683,8 @@ extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda
         else if (tn_opt == 3) TN_BIG_V(T, EPI, OUT, 32, 5, false, 8);                                          \
         else if (tn_opt == 4 && fused_cs) TN_BIG_V(T, EPI, OUT, 64, 2, true, 4);                               \
         else if (tn_opt == 4) TN_BIG_V(T, EPI, OUT, 64, 2, false, 4);                                          \
+        else if (fused_cs && tn_pf) TN_BIG_V(T, EPI, OUT, 64, 2, true, 8, true);                               \
+        else if (tn_pf) TN_BIG_V(T, EPI, OUT, 64, 2, false, 8, true);                                          \
         else if (fused_cs) TN_BIG_V(T, EPI, OUT, 64, 2, true, 8);                                              \
         else TN_BIG_V(T, EPI, OUT, 64, 2, false, 8);                                                           \
     } while (0)

@@ -89,7 +89,8 @@ int dclip_abi_version(void);
 #define DCLIP_OPT_ATTN_DQ_ROWS 14   /* CLS-split dQ pass query rows per wave: 32 (default; 8 waves, two per SIMD) or 64 (4 waves, one per SIMD) */
 #define DCLIP_OPT_ATTN_DQ_DEFER 15  /* CLS-split dQ pass: 0 (default) a unit's dQ MFMAs right after its softmax; 1 half a step later, beside the next unit's S / dP chains */
 #define DCLIP_OPT_GEMM_SCHED 16     /* persistent NT GEMM tile walk: 0 (default) static (round * G + block); 1 work-conserving (every tile claimed: round-0 ownership bitmap, XCD-local ranges, stealing) */
-#define DCLIP_OPT_COUNT 17
+#define DCLIP_OPT_GEMM_KLOOP 17     /* 8-wave GEMM K-loops: 0 (default) the persistent NT kernel with its fragment reads issued one 8-MFMA group ahead except on the GELU epilogue, the TN kernel as compiled; 1 read-ahead in every NT and TN K-loop; 2 none */
+#define DCLIP_OPT_COUNT 18
 int dclip_set_option(int id, int value);
 
 /* LayerNorm over the last dim (cols), eps, affine w/b (fp32).  y = (x-mu)*rstd*w+b.

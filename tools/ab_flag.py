@@ -54,7 +54,9 @@ def main():
     silog = SILogLoss()
     res = {repr(v): [] for v in vals}
     for r in range(a.rounds):
-        for v in vals:
+        # the arms' order reversed every other round (ABBA): a drift of the box within a round
+        # (clock, temperature) would otherwise favour the arm that always runs first
+        for v in (vals if r % 2 == 0 else vals[::-1]):
             setv(v)
             bench.run_steps(model, opt, batch, 3, silog)
             torch.cuda.synchronize()

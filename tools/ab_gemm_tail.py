@@ -44,6 +44,11 @@ cases.append(("dX c_fc", lambda a=a, w=w: O.gemm(a, w)))
 a, w, _ = mk(4 * C, C)
 z = torch.randn(M, 4 * C, device=dev).to(bf)
 cases.append(("dX c_proj gelu'", lambda a=a, w=w: O.gemm(a, w, Nat.EPI_GELU_BWD, aux=z)))
+for name, n, k in [("dW in_proj", 3 * C, C), ("dW out_proj", C, C), ("dW c_fc", 4 * C, C), ("dW c_proj", C, 4 * C)]:
+    dy = torch.randn(M, n, device=dev).to(bf)
+    xx = torch.randn(M, k, device=dev).to(bf)
+    dbz = torch.zeros(n, device=dev)
+    cases.append((name, lambda dy=dy, xx=xx, dbz=dbz: O.weight_grad(dy, xx, db=dbz.zero_())[0]))
 
 
 def ev(fn, reps=10):
@@ -57,11 +62,26 @@ def ev(fn, reps=10):
     return e0.elapsed_time(e1) / reps * 1e3
 
 
+# the arms' outputs bitwise (every option here changes scheduling / launch shape, not arithmetic order,
+# except the M tail's K split: compared to fp32 summation order instead)
+try:
+    for n, fn in cases:
+        outs = []
+        for o in opts:
+            Nat.call("dclip_set_option", OPT, o)
+            r = fn()
+            outs.append(r[0] if isinstance(r, tuple) else r)
+        for o, r in zip(opts[1:], outs[1:]):
+            same = torch.equal(r[:-8], outs[0][:-8])
+            tail = (r[-8:].float() - outs[0][-8:].float()).abs().max().item()
+            print(f"{n:16s} opt{o} vs opt{opts[0]}: rows before the tail bitwise {same}, tail max |d| {tail:.2e}", flush=True)
+finally:
+    Nat.call("dclip_set_option", OPT, 0)
 res_t = {(n, o): [] for n, _ in cases for o in opts}
 try:
     for r in range(rounds):
         for n, fn in cases:
-            for o in opts:
+            for o in (opts if r % 2 == 0 else opts[::-1]):  # ABBA: no arm always first
                 Nat.call("dclip_set_option", OPT, o)
                 res_t[(n, o)].append(ev(fn))
 finally:
