@@ -291,6 +291,41 @@ def test_gemm_persistent_epilogue_bitwise(M, C, dt):
             assert torch.equal(a, b), k
 
 
+@pytest.mark.parametrize("opt", [1, 2])
+def test_gemm_kloop_read_ahead_is_bitwise(opt):
+    """DCLIP_OPT_GEMM_KLOOP changes only the issue order of the 8-wave K-loops' fragment reads
+    (one 8-MFMA group ahead): every NT epilogue and the TN weight gradient (with its fused bias
+    sums) are bitwise equal across 0 (default: NT read-ahead but GELU), 1 (everywhere) and 2 (none)."""
+    from denseclip_vit_multimodal_amd import _native as Nat
+    O = ops()
+    M, C = 65544, 768
+    dt = torch.bfloat16
+    torch.manual_seed(5)
+    A = torch.randn(M, C, device=DEV).to(dt)
+    A4 = torch.randn(M, 4 * C, device=DEV).to(dt)
+    W = (torch.randn(3 * C, C, device=DEV) * C ** -0.5).to(dt)
+    Wd = (torch.randn(C, 4 * C, device=DEV) * (4 * C) ** -0.5).to(dt)
+    bias = torch.randn(3 * C, device=DEV)
+    res = torch.randn(M, C, device=DEV)
+    z = torch.randn(M, 3 * C, device=DEV).to(dt)
+
+    def run():
+        db = torch.zeros(3 * C, device=DEV)
+        dw = O.weight_grad(A4[:, :3 * C].contiguous(), A, db=db)[0]
+        return [O.gemm(A, W, bias=bias), O.gemm(A, W, Nat.EPI_GELU, bias=bias)[1],
+                O.gemm(A4, Wd, Nat.EPI_RESIDUAL, bias=bias[:C], aux=res), O.gemm(A, W, Nat.EPI_GELU_BWD, aux=z),
+                O.gemm(A4, Wd, out_dtype=torch.float32), dw, db]
+
+    base = run()
+    try:
+        Nat.call("dclip_set_option", Nat.OPT_GEMM_KLOOP, opt)
+        other = run()
+    finally:
+        Nat.call("dclip_set_option", Nat.OPT_GEMM_KLOOP, 0)
+    for i, (a, b) in enumerate(zip(base, other)):
+        assert torch.equal(a, b), i
+
+
 def O_qgelu_grad(z):
     """d/dz of QuickGELU z * sigmoid(1.702 z) (models.py:252-254)."""
     sg = torch.sigmoid(1.702 * z)
