@@ -545,10 +545,13 @@ def refresh_weight_copies(params):
     """Refresh, in place, the plain and transposed compute-dtype copies WEIGHTS holds for these
     fp32 parameters (the entries earlier forwards / backwards created), and re-stamp them valid.
     The copies keep their storage, so the device descriptor of the launch is built once and
-    reused while the set of copies is unchanged.  A no-op during stream capture and for
-    parameters without cached copies; derived layouts (get_with) stay lazy."""
-    if not torch.cuda.is_available() or torch.cuda.is_current_stream_capturing():
+    reused while the set of copies is unchanged.  A no-op for parameters without cached copies;
+    derived layouts (get_with) stay lazy.  During stream capture (a whole train step captured into
+    a graph, train.CapturedTrainStep) the launch is captured with the descriptor an eager step
+    built, so every replay refreshes the copies after its optimizer step."""
+    if not torch.cuda.is_available():
         return
+    capturing = torch.cuda.is_current_stream_capturing()
     groups = {}
     for p in params:
         cache = p.__dict__.get("_dclip_cache")
@@ -577,6 +580,11 @@ def refresh_weight_copies(params):
         key = tuple((w.data_ptr(), 0 if vp is None else vp.data_ptr(), 0 if vt is None else vt.data_ptr(), r, c)
                     for _, _, w, vp, vt, _, r, c in items)
         ent = _REFRESH_DESC.get((dev, dt))
+        if capturing and (ent is None or ent[0] != key):
+            # a new descriptor needs a host -> device copy; replays without the refresh would read
+            # stale copies: the set of copies must be the one an eager step already refreshed
+            raise RuntimeError("refresh_weight_copies: the cached weight copies changed since the last eager "
+                               "optimizer step; run one eager step before capturing the train step")
         if ent is None or ent[0] != key:
             table, tiles = [], 0
             for src, dp, dtp, r, c in key:

@@ -126,9 +126,15 @@ def wrap_ddp(model, device=None, grad_dtype=None):
     return ddp
 
 
-def make_optimizer(params, fused=None):
+def make_optimizer(params, fused=None, capturable=False):
+    """AdamW(lr 2e-5, weight decay 0.01) as the reference trainer builds it (train_denseclip.py:1061),
+    fused on GPU parameters; capturable=True keeps its step counts on the device (required by
+    CapturedTrainStep)."""
+    params = list(params)
     if fused is None:
         fused = all(p.is_cuda for p in params)
+    if capturable:
+        return torch.optim.AdamW(params, lr=2e-5, weight_decay=0.01, fused=fused, capturable=True)
     return torch.optim.AdamW(params, lr=2e-5, weight_decay=0.01, fused=fused)
 
 
@@ -189,6 +195,63 @@ def train_step(model, opt, batch, silog=None, seg_weight=1.0, silog_weight=0.1):
     # overflow there); bf16 / fp32 keep the reference's loss-only rule
     step_unless_nonfinite(opt, loss, check_grads=fp16_backward(model, img))
     return loss.detach()
+
+
+class CapturedTrainStep:
+    """train_step captured once into one HIP graph and replayed: forward, loss, backward, the
+    non-finite check and the fused AdamW update (skipped on the device when the flag is set), and
+    the refresh of the 16-bit weight copies the next forward reads — every launch of the step
+    replayed from one hipGraphLaunch, so the host issues nothing per kernel and the step runs at
+    the GPU's pace with the inter-kernel gaps of a graph (ops are stream-ordered and capture-safe:
+    outputs from the caching allocator, no host synchronisation; the frozen text path becomes a
+    parallel branch of the graph as in serve.CapturedForward).
+
+    Call it with a batch of the captured shapes / dtypes (copied into the static input buffers)
+    or with no argument (the same batch again); it returns the step's loss tensor (the SAME
+    tensor every call).  Requirements: one process (no DDP: its bucketed all-reduce hooks are not
+    captured here), a fused AdamW built with capturable=True (its step counts live on the device),
+    and parameters that stay where they are.  fp16 models take exact gradient scales in the
+    captured step (ops.FP16_DELAYED_SCALE: the delayed scales' use counter is host state)."""
+
+    def __init__(self, model, opt, batch, silog=None, seg_weight=1.0, silog_weight=0.1, warmup=3):
+        if isinstance(model, torch.nn.parallel.DistributedDataParallel):
+            raise RuntimeError("CapturedTrainStep: one process only (DDP's all-reduce hooks are not captured)")
+        if not all(g.get("fused") and g.get("capturable") for g in opt.param_groups):
+            raise RuntimeError("CapturedTrainStep: needs a fused AdamW with capturable=True "
+                               "(make_optimizer(..., capturable=True))")
+        if not all(t.is_cuda for t in batch):
+            raise RuntimeError("CapturedTrainStep: GPU batch tensors only (no CPU fallback)")
+        self.static = [t.detach().clone() for t in batch]
+        args = (silog, seg_weight, silog_weight)
+        m = _unwrap(model)
+        saved = getattr(m, "graph_text", None)
+        if saved is not None:
+            m.graph_text = "side"  # the text path as a forked branch of this capture (no nested graph)
+        try:
+            dev = self.static[0].device
+            side = torch.cuda.Stream(device=dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(max(1, warmup)):  # caches, allocator pools, the weight-refresh descriptor
+                    train_step(model, opt, self.static, *args)
+            torch.cuda.current_stream(dev).wait_stream(side)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self.loss = train_step(model, opt, self.static, *args)
+        finally:
+            if saved is not None:
+                m.graph_text = saved
+
+    def __call__(self, batch=None):
+        if batch is not None:
+            for s, t in zip(self.static, batch):
+                if s.shape != t.shape or s.dtype != t.dtype:
+                    raise ValueError(f"CapturedTrainStep was captured for {tuple(s.shape)} {s.dtype}, "
+                                     f"got {tuple(t.shape)} {t.dtype}")
+                if s.data_ptr() != t.data_ptr():
+                    s.copy_(t)
+        self.graph.replay()
+        return self.loss
 
 
 def fp16_backward(model, img=None):
