@@ -408,7 +408,10 @@ def test_captured_train_step_matches_eager(cdt):
     nothing at random), five eager steps against three warm-up steps + two replays — losses and
     every parameter within fp32 rounding, and the replays see new batches copied into the captured
     buffers.  Refuses a non-capturable optimizer.  fp16: the captured step takes exact gradient
-    scales (ops.FP16_DELAYED_SCALE's use counter is host state), so the eager arm runs with them too."""
+    scales (ops.FP16_DELAYED_SCALE's use counter is host state), so the eager arm runs with them too;
+    and at this tiny width the weight gradients' bias sums take the small-shape path (per-column
+    atomics: summation order not fixed), which fp16's finer mantissa carries from step to step —
+    so the replay is held to the spread of two eager runs (bf16: both exact)."""
     import torch.nn as nn
     from denseclip_vit_multimodal_amd import ops
     from denseclip_vit_multimodal_amd import DenseCLIP
@@ -432,6 +435,8 @@ def test_captured_train_step_matches_eager(cdt):
     try:
         ma, oa = make()
         la = [float(train_step(ma, oa, b)) for b in (b1, b1, b1, b2, b1)]
+        mc, oc = make()
+        lc = [float(train_step(mc, oc, b)) for b in (b1, b1, b1, b2, b1)]
         mb, ob = make()
         with pytest.raises(RuntimeError):
             CapturedTrainStep(mb, make_optimizer([p for p in mb.parameters() if p.requires_grad]), b1)
@@ -440,10 +445,13 @@ def test_captured_train_step_matches_eager(cdt):
         torch.cuda.synchronize()
     finally:
         ops.FP16_DELAYED_SCALE = saved
+    spread = max(abs(x - y) for x, y in zip(la, lc))
     for x, y in zip(lb, la[3:]):
-        assert abs(x - y) <= 1e-5 * abs(y), (lb, la)
-    pa = dict(ma.named_parameters())
+        assert abs(x - y) <= max(1e-5 * abs(y), 4 * spread), (lb, la, lc)
+    pa, pc = dict(ma.named_parameters()), dict(mc.named_parameters())
     for n, p in mb.named_parameters():
         ref = pa[n].detach()
-        err = float((p.detach() - ref).abs().max()) / max(float(ref.abs().max()), 1e-30)
-        assert err < 1e-5, (n, err)
+        scale = max(float(ref.abs().max()), 1e-30)
+        err = float((p.detach() - ref).abs().max()) / scale
+        run_to_run = float((pc[n].detach() - ref).abs().max()) / scale
+        assert err < max(1e-5, 4 * run_to_run), (n, err, run_to_run)
