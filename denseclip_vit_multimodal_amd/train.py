@@ -100,13 +100,25 @@ def loss_fn(out, seg, depth, mask, silog=None, seg_weight=1.0, silog_weight=0.1)
     return loss
 
 
-def wrap_ddp(model, device=None, grad_dtype=None):
-    """DDP over the default process group (RCCL on GPUs, gloo on CPU).  100 MB buckets:
+# wrap_ddp's data-parallel implementation: "allreduce" (GradAllReduce: bucketed in-place
+# all-reduces of the gradients autograd produced) or "ddp" (torch's DistributedDataParallel)
+DP_IMPL = "allreduce"
+
+
+def wrap_ddp(model, device=None, grad_dtype=None, impl=None):
+    """Data parallelism over the default process group (RCCL on GPUs, gloo on CPU): GradAllReduce
+    (DP_IMPL "allreduce", the default) or torch DDP ("ddp", and always for grad_dtype bf16).
+    DDP: 100 MB buckets:
     fewer, larger all-reduces suit xGMI's per-link ring bandwidth; the buckets are views of
     the gradients (no copy).  Trainable parameters that get no gradient in this config
     (`gradless_parameter_names`) are left out of the reduction rather than searched for every
     step (find_unused_parameters).  grad_dtype=torch.bfloat16 all-reduces the buckets in bf16
     (half the xGMI bytes; the sum is rounded to 8 mantissa bits) via DDP's compression hook."""
+    impl = impl or DP_IMPL
+    if impl not in ("allreduce", "ddp"):
+        raise ValueError(f"unknown data-parallel implementation {impl!r}")
+    if impl == "allreduce" and grad_dtype in (None, torch.float32):
+        return GradAllReduce(model)
     from torch.nn.parallel import DistributedDataParallel as DDP
     ignore = set(gradless_parameter_names(model))
     if ignore:
@@ -124,6 +136,110 @@ def wrap_ddp(model, device=None, grad_dtype=None):
     elif grad_dtype not in (None, torch.float32):
         raise ValueError(f"unsupported gradient all-reduce dtype {grad_dtype}")
     return ddp
+
+
+class GradAllReduce(torch.nn.Module):
+    """Data parallelism over the default process group without DDP's gradient copies: the same
+    contract as wrap_ddp (parameters broadcast from rank 0 at wrap time, buffers before every
+    forward, gradients averaged over the ranks before the optimizer step, overlapped with the
+    backward, ~100 MB buckets in reverse registration order, the gradless parameters left out)
+    — but each bucket's collective runs on the gradient tensors autograd produced, in place.
+
+    Why: DDP keeps a flat bucket per ~100 MB and copies every gradient into it (or accumulates
+    into bucket views): at ViT-B/16 ~250 device copies and ~100 fills per step, +3 % of the step at
+    world size 1 (profiles/r05/r5ac) — a fixed cost of every N > 1 step.  Here a post-accumulate-
+    grad hook counts each bucket's arrivals; the bucket whose last gradient lands is reduced at
+    once (RCCL: one coalesced group of in-place AVG all-reduces on the process group's stream; gloo:
+    SUM then / world), and a callback queued on the autograd engine waits for every bucket at the
+    end of the backward (the current stream waits on the collectives' stream; no host sync for
+    RCCL).  Gradients of `set_to_none` steps are stolen by autograd, so nothing is copied."""
+
+    def __init__(self, module, bucket_cap_mb=100, broadcast_buffers=True):
+        super().__init__()
+        import torch.distributed as dist
+        self.module = module
+        self._dist = dist
+        ignore = set(gradless_parameter_names(module))
+        params = [(n, p) for n, p in module.named_parameters() if p.requires_grad and n not in ignore]
+        # the parameters not ignored (DDP's attribute: frozen ones included; only those with
+        # requires_grad are reduced)
+        self._module_parameters = [p for n, p in module.named_parameters() if n not in ignore]
+        with torch.no_grad():
+            for _, p in params:
+                dist.broadcast(p.data, 0)
+        self._buffers_to_sync = [b for b in module.buffers()] if broadcast_buffers else []
+        cap = bucket_cap_mb * 2 ** 20
+        self._buckets, cur, size = [], [], 0
+        for _, p in reversed(params):  # gradients arrive roughly in reverse registration order
+            cur.append(p)
+            size += p.numel() * p.element_size()
+            if size >= cap:
+                self._buckets.append(cur)
+                cur, size = [], 0
+        if cur:
+            self._buckets.append(cur)
+        self._bucket_of = {}
+        for i, b in enumerate(self._buckets):
+            for p in b:
+                self._bucket_of[p] = i
+        self._nccl = dist.get_backend() == "nccl"
+        self._world = dist.get_world_size()
+        # one rank: the average is the identity and no collective is issued (set False to exercise
+        # the collective path anyway — bench.py's ddp1 line prices RCCL's one-rank all-reduce so)
+        self.skip_collectives = self._world == 1
+        self._pending = None
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for _, p in params]
+
+    def forward(self, *args, **kwargs):
+        if self._buffers_to_sync and self._world > 1:
+            with torch.no_grad():
+                for b in self._buffers_to_sync:
+                    self._dist.broadcast(b, 0)
+        self._pending = None
+        return self.module(*args, **kwargs)
+
+    def _launch(self, i):
+        grads = [p.grad for p in self._buckets[i] if p.grad is not None]
+        st = self._pending
+        st["launched"][i] = True
+        if not grads or self.skip_collectives:
+            return
+        d = self._dist
+        if self._nccl:
+            try:
+                with d._coalescing_manager(async_ops=True) as cm:
+                    for g in grads:
+                        d.all_reduce(g, op=d.ReduceOp.AVG)
+                st["works"].append((cm, None))
+            except (AttributeError, TypeError, RuntimeError):  # no coalescing: one async call per tensor
+                for g in grads:
+                    st["works"].append((d.all_reduce(g, op=d.ReduceOp.AVG, async_op=True), None))
+        else:
+            for g in grads:
+                st["works"].append((d.all_reduce(g, async_op=True), g))
+
+    def _on_grad(self, p):
+        if self._pending is None:
+            self._pending = {"ready": [0] * len(self._buckets), "launched": [False] * len(self._buckets), "works": []}
+            torch.autograd.Variable._execution_engine.queue_callback(self._finish)
+        i = self._bucket_of[p]
+        st = self._pending
+        st["ready"][i] += 1
+        if st["ready"][i] == len(self._buckets[i]):
+            self._launch(i)
+
+    def _finish(self):
+        st = self._pending
+        if st is None:
+            return
+        for i, done in enumerate(st["launched"]):
+            if not done:  # a bucket some of whose parameters got no gradient this step
+                self._launch(i)
+        for w, g in st["works"]:
+            w.wait()
+            if g is not None:  # gloo has no AVG
+                g.div_(self._world)
+        self._pending = None
 
 
 def make_optimizer(params, fused=None, capturable=False):
@@ -214,8 +330,8 @@ class CapturedTrainStep:
     captured step (ops.FP16_DELAYED_SCALE: the delayed scales' use counter is host state)."""
 
     def __init__(self, model, opt, batch, silog=None, seg_weight=1.0, silog_weight=0.1, warmup=3):
-        if isinstance(model, torch.nn.parallel.DistributedDataParallel):
-            raise RuntimeError("CapturedTrainStep: one process only (DDP's all-reduce hooks are not captured)")
+        if isinstance(model, (torch.nn.parallel.DistributedDataParallel, GradAllReduce)):
+            raise RuntimeError("CapturedTrainStep: one process only (the data-parallel all-reduce hooks are not captured)")
         if not all(g.get("fused") and g.get("capturable") for g in opt.param_groups):
             raise RuntimeError("CapturedTrainStep: needs a fused AdamW with capturable=True "
                                "(make_optimizer(..., capturable=True))")

@@ -63,15 +63,15 @@ def _batch(rank, B=2, layers=3, C=128, h=4, w=8, H=16, W=32):
     return maps, seg, depth, mask
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, impl=None, bucket_mb=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.set_num_threads(1)
     from denseclip_vit_multimodal_amd.utils import init_distributed, cleanup
-    from denseclip_vit_multimodal_amd.train import wrap_ddp, loss_fn, make_optimizer
+    from denseclip_vit_multimodal_amd.train import GradAllReduce, wrap_ddp, loss_fn, make_optimizer
     init_distributed(rank, world, backend="gloo")
     try:
-        model = wrap_ddp(_model())
+        model = GradAllReduce(_model(), bucket_cap_mb=bucket_mb) if bucket_mb else wrap_ddp(_model(), impl=impl)
         opt = make_optimizer([p for p in model.parameters() if p.requires_grad])
         maps, seg, depth, mask = _batch(rank)
         out = model(maps, gt_semantic_seg=seg, gt_depth=depth)
@@ -94,10 +94,16 @@ def _free_port():
 
 
 @pytest.mark.timeout(300)
-def test_ddp_world2_matches_single_process(tmp_path):
+@pytest.mark.parametrize("impl,bucket_mb", [("allreduce", None), ("ddp", None), ("allreduce", 0.01)],
+                         ids=["allreduce", "ddp", "allreduce_many_buckets"])
+def test_ddp_world2_matches_single_process(tmp_path, impl, bucket_mb):
+    """Both data-parallel implementations of wrap_ddp (train.GradAllReduce, the default, and torch
+    DDP), and GradAllReduce with ~10 KB buckets (dozens of buckets, launched as their last
+    gradient lands): averaged gradients = the single-process gradient of the concatenated batch,
+    identical parameters on both ranks after the step."""
     from denseclip_vit_multimodal_amd.train import loss_fn
     world = 2
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), impl, bucket_mb), nprocs=world, join=True)
     r = [torch.load(tmp_path / f"rank{i}.pt", weights_only=True) for i in range(world)]
 
     # single process: mean of the per-rank losses over the same shards (same thread count

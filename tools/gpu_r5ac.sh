@@ -1,0 +1,9 @@
+# DDP world-size-1 overhead: wrapper variants, one process each (two passes, alternating order)
+set -o pipefail
+cd /root/repo
+export TMPDIR=/tmp
+O=gpurun_out/r5ac; mkdir -p $O
+for v in none default static keepgrad nobucketview nobucketview keepgrad static default none; do
+  MASTER_PORT=$((29600 + RANDOM % 200)) timeout -k 10 200 python3 tools/ddp_probe.py $v 10 >> $O/ddp_probe.log 2>&1 || { tail -20 $O/ddp_probe.log; exit 3; }
+done
+grep "ms/step" $O/ddp_probe.log
