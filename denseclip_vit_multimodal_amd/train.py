@@ -187,6 +187,7 @@ class GradAllReduce(torch.nn.Module):
         # one rank: the average is the identity and no collective is issued (set False to exercise
         # the collective path anyway — bench.py's ddp1 line prices RCCL's one-rank all-reduce so)
         self.skip_collectives = self._world == 1
+        self.coalesce = True  # RCCL: a bucket's all-reduces as one group call
         self._pending = None
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for _, p in params]
 
@@ -205,15 +206,14 @@ class GradAllReduce(torch.nn.Module):
         if not grads or self.skip_collectives:
             return
         d = self._dist
-        if self._nccl:
-            try:
-                with d._coalescing_manager(async_ops=True) as cm:
-                    for g in grads:
-                        d.all_reduce(g, op=d.ReduceOp.AVG)
-                st["works"].append((cm, None))
-            except (AttributeError, TypeError, RuntimeError):  # no coalescing: one async call per tensor
+        if self._nccl and self.coalesce:
+            with d._coalescing_manager(async_ops=True) as cm:
                 for g in grads:
-                    st["works"].append((d.all_reduce(g, op=d.ReduceOp.AVG, async_op=True), None))
+                    d.all_reduce(g, op=d.ReduceOp.AVG)
+            st["works"].append((cm, None))
+        elif self._nccl:  # one async call per tensor
+            for g in grads:
+                st["works"].append((d.all_reduce(g, op=d.ReduceOp.AVG, async_op=True), None))
         else:
             for g in grads:
                 st["works"].append((d.all_reduce(g, async_op=True), g))
