@@ -449,9 +449,14 @@ def test_captured_train_step_matches_eager(cdt):
     for x, y in zip(lb, la[3:]):
         assert abs(x - y) <= max(1e-5 * abs(y), 4 * spread), (lb, la, lc)
     pa, pc = dict(ma.named_parameters()), dict(mc.named_parameters())
+    lr = oa.param_groups[0]["lr"]
     for n, p in mb.named_parameters():
         ref = pa[n].detach()
-        scale = max(float(ref.abs().max()), 1e-30)
-        err = float((p.detach() - ref).abs().max()) / scale
-        run_to_run = float((pc[n].detach() - ref).abs().max()) / scale
-        assert err < max(1e-5, 4 * run_to_run), (n, err, run_to_run)
+        d = float((p.detach() - ref).abs().max())
+        if spread == 0.0:  # bf16: both arms deterministic -> the same parameters
+            assert d <= 1e-5 * max(float(ref.abs().max()), 1e-30), (n, d)
+        else:
+            # fp16 at this width: AdamW turns the arms' ulp-level gradient differences into up to
+            # ~lr per step on parameters whose gradient is near zero (its update is ~sign(m)) —
+            # two eager runs differ that way too; bound: five steps of ~3 lr each
+            assert d <= 15 * lr, (n, d, float((pc[n].detach() - ref).abs().max()))
