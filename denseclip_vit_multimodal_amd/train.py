@@ -326,8 +326,8 @@ class CapturedTrainStep:
     or with no argument (the same batch again); it returns the step's loss tensor (the SAME
     tensor every call).  Requirements: one process (no DDP: its bucketed all-reduce hooks are not
     captured here), a fused AdamW built with capturable=True (its step counts live on the device),
-    and parameters that stay where they are.  fp16 models take exact gradient scales in the
-    captured step (ops.FP16_DELAYED_SCALE: the delayed scales' use counter is host state)."""
+    and parameters that stay where they are.  bf16 / fp32 backward only: an fp16 model is refused
+    (its replayed step drifted from the eager one beyond the eager run-to-run spread)."""
 
     def __init__(self, model, opt, batch, silog=None, seg_weight=1.0, silog_weight=0.1, warmup=3):
         if isinstance(model, (torch.nn.parallel.DistributedDataParallel, GradAllReduce)):
@@ -337,6 +337,11 @@ class CapturedTrainStep:
                                "(make_optimizer(..., capturable=True))")
         if not all(t.is_cuda for t in batch):
             raise RuntimeError("CapturedTrainStep: GPU batch tensors only (no CPU fallback)")
+        if fp16_backward(model, batch[0]):
+            # the fp16 backward's gradient scales (exact under capture, delayed eagerly) and the fp16
+            # heads' scale state are not validated under replay: a replayed fp16 step drifted from the
+            # eager one beyond the eager run-to-run spread (tests/test_gpu_parity.py)
+            raise RuntimeError("CapturedTrainStep: bf16 / fp32 backward only (fp16 steps stay eager)")
         self.static = [t.detach().clone() for t in batch]
         args = (silog, seg_weight, silog_weight)
         m = _unwrap(model)
