@@ -523,29 +523,46 @@ def main():
             model, opt = setup("F")
             model = wrap_ddp(model, dev)
             opt = make_optimizer([p for p in model.parameters() if p.requires_grad])
-            # the collectives issued even on one rank (GradAllReduce skips the identity there by
-            # default): the line prices the wrapper AND RCCL's all-reduce call path
-            if hasattr(model, "skip_collectives"):
-                model.skip_collectives = False
-            dtd, _, lossd = timed(model, opt, batch, k_sub, 3, silog, 1, True)
-            ms_d = dtd / k_sub * 1e3
-            progress(f"ddp1 {ms_d:.2f} ms per step")
-            ms_w = None
-            if hasattr(model, "skip_collectives"):  # the wrapper alone (hooks, bucket bookkeeping)
-                model.skip_collectives = True
-                dtw, _, _ = timed(model, opt, batch, k_sub, 1, silog, 1, True)
-                ms_w = dtw / k_sub * 1e3
-                progress(f"ddp1 without collectives {ms_w:.2f} ms per step")
+            # the unwrapped step timed in the same process beside it: a box drifts by ~2 % over a
+            # bench run (the A/A control), so the overhead is read against blocks of the
+            # plain step interleaved with the wrapped ones (P D W W D P: linear drift cancels)
+            plain, plain_opt = setup("F")
+            run_steps(plain, plain_opt, batch, 3, silog)
+            run_steps(model, opt, batch, 3, silog)
+            has_skip = hasattr(model, "skip_collectives")
+            blocks = {"P": [], "D": [], "W": []}
+            for arm in ("P", "D", "W", "W", "D", "P") if has_skip else ("P", "D", "D", "P"):
+                if arm == "P":
+                    dtb, _, _ = timed(plain, plain_opt, batch, k_sub, 0, silog, 1, True)
+                else:
+                    # D: the collectives issued even on one rank (GradAllReduce skips the identity
+                    # there by default): the wrapper AND RCCL's all-reduce call path; W: the wrapper
+                    # alone (hooks, bucket bookkeeping)
+                    if has_skip:
+                        model.skip_collectives = arm == "W"
+                    dtb, _, lossd = timed(model, opt, batch, k_sub, 0, silog, 1, True)
+                blocks[arm].append(dtb / k_sub * 1e3)
+            ms_p = sum(blocks["P"]) / len(blocks["P"])
+            ms_d = sum(blocks["D"]) / len(blocks["D"])
+            ms_w = sum(blocks["W"]) / len(blocks["W"]) if blocks["W"] else None
+            progress(f"ddp1 {ms_d:.2f} ms per step (plain beside it {ms_p:.2f}, wrapper alone {ms_w})")
             head_ms = dt / args.steps * 1e3
-            ddp1 = {"value": round(B * k_sub / dtd, 4), "unit": "images/sec", "ms_per_step": round(ms_d, 2),
+            ddp1 = {"value": round(B * 1e3 / ms_d, 4), "unit": "images/sec", "ms_per_step": round(ms_d, 2),
+                    "ms_per_step_plain_interleaved": round(ms_p, 2),
+                    "overhead": round(ms_d / ms_p - 1.0, 4),
                     "overhead_vs_headline": round(ms_d / head_ms - 1.0, 4), "loss": round(lossd, 4),
                     "ms_per_step_without_collectives": round(ms_w, 2) if ms_w else None,
-                    "overhead_without_collectives": round(ms_w / head_ms - 1.0, 4) if ms_w else None,
+                    "overhead_without_collectives": round(ms_w / ms_p - 1.0, 4) if ms_w else None,
+                    "blocks_ms": {k: [round(x, 2) for x in v] for k, v in blocks.items()},
                     "what": "mode F under the data-parallel wrapper (train.wrap_ddp: GradAllReduce, in-place "
                             "AVG all-reduces of ~100 MB gradient buckets launched during the backward as each "
                             "bucket's last gradient lands) on an RCCL process group of world size 1, with the "
                             "collectives issued (RCCL's one-rank all-reduce of the 393 MB of gradients) and, "
-                            "`_without_collectives`, the wrapper alone (it skips the identity on one rank)"}
+                            "`_without_collectives`, the wrapper alone (it skips the identity on one rank); "
+                            "`overhead` against the unwrapped step timed in blocks interleaved with the wrapped "
+                            "ones (P D W W D P, k steps each), `overhead_vs_headline` against the headline run "
+                            "minutes earlier"}
+            del plain, plain_opt
         finally:
             release()
             if dist.is_initialized():
