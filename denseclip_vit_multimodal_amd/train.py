@@ -164,9 +164,10 @@ class GradAllReduce(torch.nn.Module):
         # the parameters not ignored (DDP's attribute: frozen ones included; only those with
         # requires_grad are reduced)
         self._module_parameters = [p for n, p in module.named_parameters() if n not in ignore]
-        with torch.no_grad():
-            for _, p in params:
-                dist.broadcast(p.data, 0)
+        from torch.distributed.distributed_c10d import _get_default_group
+        if params and dist.get_world_size() > 1:
+            with torch.no_grad():  # rank 0's initial parameters, flattened into ~250 MB broadcasts
+                dist._broadcast_coalesced(_get_default_group(), [p.data for _, p in params], 250 * 2 ** 20, 0)
         self._buffers_to_sync = [b for b in module.buffers()] if broadcast_buffers else []
         cap = bucket_cap_mb * 2 ** 20
         self._buckets, cur, size = [], [], 0
@@ -193,9 +194,11 @@ class GradAllReduce(torch.nn.Module):
 
     def forward(self, *args, **kwargs):
         if self._buffers_to_sync and self._world > 1:
+            # rank 0's buffers (BN running statistics: 45 small tensors at ViT-B/16) in one
+            # flattened broadcast per dtype, as DDP's buffer sync does — not one collective each
+            from torch.distributed.distributed_c10d import _get_default_group
             with torch.no_grad():
-                for b in self._buffers_to_sync:
-                    self._dist.broadcast(b, 0)
+                self._dist._broadcast_coalesced(_get_default_group(), self._buffers_to_sync, 250 * 2 ** 20, 0)
         self._pending = None
         return self.module(*args, **kwargs)
 

@@ -71,8 +71,16 @@ def _worker(rank, world, port, out_dir, impl=None, bucket_mb=None):
     from denseclip_vit_multimodal_amd.train import GradAllReduce, wrap_ddp, loss_fn, make_optimizer
     init_distributed(rank, world, backend="gloo")
     try:
-        model = GradAllReduce(_model(), bucket_cap_mb=bucket_mb) if bucket_mb else wrap_ddp(_model(), impl=impl)
+        m = _model()
+        with torch.no_grad():  # rank 1 starts elsewhere: wrapping broadcasts rank 0's parameters
+            for p in m.parameters():
+                p.add_(float(rank))
+        model = GradAllReduce(m, bucket_cap_mb=bucket_mb) if bucket_mb else wrap_ddp(m, impl=impl)
         opt = make_optimizer([p for p in model.parameters() if p.requires_grad])
+        with torch.no_grad():  # rank 1's BN statistics off: the wrapper's forward restores rank 0's
+            for b in model.module.buffers():
+                if b.is_floating_point():
+                    b.add_(float(rank))
         maps, seg, depth, mask = _batch(rank)
         out = model(maps, gt_semantic_seg=seg, gt_depth=depth)
         loss = loss_fn(out, seg, depth, mask)
@@ -81,7 +89,8 @@ def _worker(rank, world, port, out_dir, impl=None, bucket_mb=None):
         grads = {n: p.grad.clone() for n, p in model.module.named_parameters()}
         opt.step()
         params = {n: p.detach().clone() for n, p in model.module.named_parameters()}
-        torch.save({"grads": grads, "params": params, "loss": loss.detach()},
+        bufs = {n: b.clone() for n, b in model.module.named_buffers()}
+        torch.save({"grads": grads, "params": params, "loss": loss.detach(), "buffers": bufs},
                    os.path.join(out_dir, f"rank{rank}.pt"))
     finally:
         cleanup()
@@ -100,7 +109,8 @@ def test_ddp_world2_matches_single_process(tmp_path, impl, bucket_mb):
     """Both data-parallel implementations of wrap_ddp (train.GradAllReduce, the default, and torch
     DDP), and GradAllReduce with ~10 KB buckets (dozens of buckets, launched as their last
     gradient lands): averaged gradients = the single-process gradient of the concatenated batch,
-    identical parameters on both ranks after the step."""
+    identical parameters on both ranks after the step, rank 0's parameters broadcast at wrap time
+    and its buffers before the forward (rank 1 starts with different values of both)."""
     from denseclip_vit_multimodal_amd.train import loss_fn
     world = 2
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), impl, bucket_mb), nprocs=world, join=True)
@@ -125,6 +135,10 @@ def test_ddp_world2_matches_single_process(tmp_path, impl, bucket_mb):
     for n in r[0]["params"]:
         assert torch.equal(r[0]["params"][n], r[1]["params"][n]), n
     assert not torch.equal(r[0]["loss"], r[1]["loss"])  # the shards really differ
+    rb = dict(ref.named_buffers())
+    assert rb and set(rb) == set(r[1]["buffers"])
+    for n, b in rb.items():  # rank 1's perturbed buffers were overwritten with rank 0's
+        assert torch.equal(r[1]["buffers"][n], b) and torch.equal(r[0]["buffers"][n], b), n
 
 
 def test_rank_shards_are_distinct():
