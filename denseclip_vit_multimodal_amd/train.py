@@ -142,7 +142,8 @@ class GradAllReduce(torch.nn.Module):
     """Data parallelism over the default process group without DDP's gradient copies: the same
     contract as wrap_ddp (parameters broadcast from rank 0 at wrap time, buffers before every
     forward, gradients averaged over the ranks before the optimizer step, overlapped with the
-    backward, ~100 MB buckets in reverse registration order, the gradless parameters left out)
+    backward, ~100 MB buckets in reverse registration order — the last to complete ~25 MB, so
+    little is left exposed after the backward — the gradless parameters left out)
     — but each bucket's collective runs on the gradient tensors autograd produced, in place.
 
     Why: DDP keeps a flat bucket per ~100 MB and copies every gradient into it (or accumulates
@@ -154,7 +155,7 @@ class GradAllReduce(torch.nn.Module):
     end of the backward (the current stream waits on the collectives' stream; no host sync for
     RCCL).  Gradients of `set_to_none` steps are stolen by autograd, so nothing is copied."""
 
-    def __init__(self, module, bucket_cap_mb=100, broadcast_buffers=True):
+    def __init__(self, module, bucket_cap_mb=100, broadcast_buffers=True, last_bucket_cap_mb=25):
         super().__init__()
         import torch.distributed as dist
         self.module = module
@@ -169,16 +170,21 @@ class GradAllReduce(torch.nn.Module):
             with torch.no_grad():  # rank 0's initial parameters, flattened into ~250 MB broadcasts
                 dist._broadcast_coalesced(_get_default_group(), [p.data for _, p in params], 250 * 2 ** 20, 0)
         self._buffers_to_sync = [b for b in module.buffers()] if broadcast_buffers else []
-        cap = bucket_cap_mb * 2 ** 20
-        self._buckets, cur, size = [], [], 0
-        for _, p in reversed(params):  # gradients arrive roughly in reverse registration order
+        # gradients arrive roughly in reverse registration order, so the bucket of the FIRST
+        # registered parameters (patch embedding, block 0) completes last and its all-reduce is the
+        # one left exposed after the backward: it is cut at last_bucket_cap_mb (~block 0 at
+        # ViT-B/16), the others at bucket_cap_mb (few, large collectives for xGMI's ring links)
+        caps = (min(last_bucket_cap_mb, bucket_cap_mb) * 2 ** 20, bucket_cap_mb * 2 ** 20)
+        fwd, cur, size = [], [], 0
+        for _, p in params:
             cur.append(p)
             size += p.numel() * p.element_size()
-            if size >= cap:
-                self._buckets.append(cur)
+            if size >= caps[1 if fwd else 0]:
+                fwd.append(cur)
                 cur, size = [], 0
         if cur:
-            self._buckets.append(cur)
+            fwd.append(cur)
+        self._buckets = [list(reversed(b)) for b in reversed(fwd)]  # in the order they complete
         self._bucket_of = {}
         for i, b in enumerate(self._buckets):
             for p in b:

@@ -76,6 +76,8 @@ def _worker(rank, world, port, out_dir, impl=None, bucket_mb=None):
             for p in m.parameters():
                 p.add_(float(rank))
         model = GradAllReduce(m, bucket_cap_mb=bucket_mb) if bucket_mb else wrap_ddp(m, impl=impl)
+        if bucket_mb:
+            assert len(model._buckets) >= 5, len(model._buckets)
         opt = make_optimizer([p for p in model.parameters() if p.requires_grad])
         with torch.no_grad():  # rank 1's BN statistics off: the wrapper's forward restores rank 0's
             for b in model.module.buffers():
@@ -107,7 +109,7 @@ def _free_port():
                          ids=["allreduce", "ddp", "allreduce_many_buckets"])
 def test_ddp_world2_matches_single_process(tmp_path, impl, bucket_mb):
     """Both data-parallel implementations of wrap_ddp (train.GradAllReduce, the default, and torch
-    DDP), and GradAllReduce with ~10 KB buckets (dozens of buckets, launched as their last
+    DDP), and GradAllReduce with ~10 KB buckets (six buckets, each launched as its last
     gradient lands): averaged gradients = the single-process gradient of the concatenated batch,
     identical parameters on both ranks after the step, rank 0's parameters broadcast at wrap time
     and its buffers before the forward (rank 1 starts with different values of both)."""
