@@ -1,0 +1,81 @@
+"""Subprocess body of test_gpu_headline.test_grad_allreduce_rccl_world_size_1 (its own process, so
+the RCCL process group it creates does not outlive it).
+
+One rank on an RCCL ("nccl") group: the tiny context-decoder DenseCLIP in bf16 trained one step
+bare and one step under train.GradAllReduce with the collectives issued (skip_collectives False:
+at world size 1 the wrapper otherwise skips the identity), coalesced and per-tensor.  The AVG
+all-reduce of one rank is x / 1, so every gradient must come back equal to the bare model's (a
+collective that read a gradient before its producer wrote it would not); and every bucket must
+have been launched.  Prints one JSON line."""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.dirname(HERE))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+import torch.nn as nn  # noqa: E402
+
+from helpers import CITYSCAPES_CLASSES, TINY_CTX_CFG  # noqa: E402
+
+
+def make():
+    from denseclip_vit_multimodal_amd import DenseCLIP
+    from denseclip_vit_multimodal_amd.train import freeze_for_mode
+    torch.manual_seed(0)
+    m = DenseCLIP(class_names=CITYSCAPES_CLASSES, **TINY_CTX_CFG).to("cuda").train()
+    m.backbone.compute_dtype = torch.bfloat16
+    for mod in m.modules():
+        if isinstance(mod, nn.Dropout):
+            mod.p = 0.0
+    freeze_for_mode(m, "F")
+    return m
+
+
+def grads(model, batch):
+    from denseclip_vit_multimodal_amd.train import loss_fn
+    img, seg, depth, mask = batch
+    out = model(img, gt_semantic_seg=seg, gt_depth=depth, return_loss=True)
+    loss = loss_fn(out, seg, depth, mask)
+    loss.backward()
+    torch.cuda.synchronize()
+    inner = model.module if hasattr(model, "module") else model
+    return {n: p.grad.detach().clone() for n, p in inner.named_parameters() if p.grad is not None}
+
+
+def main():
+    from denseclip_vit_multimodal_amd.train import GradAllReduce, synth_batch
+    dist.init_process_group("nccl")
+    try:
+        batch = synth_batch(2, 128, 256, torch.device("cuda"), 0, image_dtype=torch.bfloat16)
+        ref = grads(make(), batch)
+        res = {"grads": len(ref)}
+        for coalesce in (True, False):
+            w = GradAllReduce(make(), bucket_cap_mb=1, last_bucket_cap_mb=1)
+            w.skip_collectives = False
+            w.coalesce = coalesce
+            launched = []
+            orig = w._launch
+
+            def count(i, orig=orig, launched=launched):
+                launched.append(i)
+                orig(i)
+
+            w._launch = count
+            g = grads(w, batch)
+            assert set(g) == set(ref), sorted(set(g) ^ set(ref))
+            # the same gradients (the tiny widths' bias sums use float atomics: order noise only)
+            bad = [n for n in ref if float((g[n] - ref[n]).abs().max()) > 1e-5 * float(ref[n].abs().max()) + 1e-30]
+            assert not bad, bad[:5]
+            assert sorted(launched) == list(range(len(w._buckets))), (launched, len(w._buckets))
+            res[f"buckets_coalesce_{coalesce}"] = len(w._buckets)
+        print(json.dumps(res))
+    finally:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -158,14 +158,32 @@ def _bench(args, nproc=1, port=29571, timeout=420):
 
 @pytest.mark.parametrize("grad_dtype", ["fp32", "bf16"])
 def test_bench_rccl_ddp_world_size_1(grad_dtype):
-    """bench.py under torch.distributed.run with init_process_group("nccl") (RCCL) and DDP forced
-    at world size 1 (reference train_denseclip.py:1050-1054, utils.py:102-107): the timing
-    barrier / max-reduce and DDP's bucket all-reduces run through RCCL; mode F at 512x1024."""
+    """bench.py under torch.distributed.run with init_process_group("nccl") (RCCL) and the
+    data-parallel wrapper forced at world size 1 (reference train_denseclip.py:1050-1054,
+    utils.py:102-107): the timing barrier / max-reduce run through RCCL, and with bf16 gradients
+    torch DDP's compressed bucket all-reduces (fp32: GradAllReduce, which skips the one-rank
+    identity — its RCCL path is test_grad_allreduce_rccl_world_size_1); mode F at 512x1024."""
     line = _bench(["--ddp", "--grad-dtype", grad_dtype, "--steps", "2", "--warmup", "1", "--batch", "2",
                    "--height", "512", "--width", "1024", "--no-mode-r", "--cpu-baseline", "off"],
                   port=29571 if grad_dtype == "fp32" else 29572)
     assert line["config"]["ddp"] is True and line["config"]["grad_allreduce_dtype"] == grad_dtype
     assert line["n_gpus"] == 1 and line["value"] > 0 and line["loss"] == line["loss"]  # finite, not NaN
+
+
+def test_grad_allreduce_rccl_world_size_1():
+    """train.GradAllReduce's RCCL path (coalesced and per-tensor in-place AVG all-reduces launched
+    from the backward's post-accumulate-grad hooks, ~1 MB buckets) on a one-rank "nccl" group with
+    the collectives issued: every bucket launched, the gradients those of the bare model
+    (tests/rccl_allreduce_worker.py, in its own process)."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="29574",
+               RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "rccl_allreduce_worker.py")], cwd=ROOT,
+                       env=env, capture_output=True, text=True, timeout=300)
+    if r.returncode != 0:
+        print("---- stdout ----\n" + r.stdout[-4000:] + "\n---- stderr ----\n" + r.stderr[-8000:])
+    assert r.returncode == 0
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res["grads"] > 0 and res["buckets_coalesce_True"] > 1 and res["buckets_coalesce_False"] > 1, res
 
 
 def test_bench_fp8_attention_trains():
