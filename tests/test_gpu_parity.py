@@ -441,9 +441,10 @@ def test_captured_train_step_matches_eager():
 
 
 def test_captured_train_step_refuses_fp16():
-    """An fp16-backward model stays eager: its replayed step drifted from the eager one beyond the
-    spread of two eager fp16 runs (round 5), so CapturedTrainStep refuses it rather than replay a
-    step it does not match."""
+    """An fp16-backward model stays eager (train.CapturedTrainStep): a captured fp16 step takes exact
+    gradient scales, slower than the eager delayed ones, and its match with eager has no fixed
+    reference to be tested against (two eager fp16 runs of this model part within four steps;
+    tools/captured_fp16_probe.py)."""
     from denseclip_vit_multimodal_amd import DenseCLIP
     from denseclip_vit_multimodal_amd.train import CapturedTrainStep, freeze_for_mode, make_optimizer, synth_batch
     m = DenseCLIP(class_names=CITYSCAPES_CLASSES, **TINY_CTX_CFG).to(DEV).train()
