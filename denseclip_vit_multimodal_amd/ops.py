@@ -268,8 +268,8 @@ def watch_fp16_overflow(flag):
     scales: once the copy has landed (an event query, never a wait) a non-zero flag re-primes every
     site, so the next backward takes exact scales instead of scales from an overflowed step's
     maxima (whose non-finite values keep the previous, too large, scale at every later site)."""
-    if not _DELAYED or not flag.is_cuda or torch.cuda.is_current_stream_capturing():
-        return
+    if not FP16_DELAYED_SCALE or not _DELAYED or not flag.is_cuda or torch.cuda.is_current_stream_capturing():
+        return  # (the queue is drained only by delayed-scale backwards: nothing to queue without them)
     host = torch.empty((), dtype=torch.float32, pin_memory=True)
     host.copy_(flag.detach().reshape(()).float(), non_blocking=True)
     ev = torch.cuda.Event()

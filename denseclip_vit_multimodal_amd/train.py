@@ -350,10 +350,10 @@ class CapturedTrainStep:
             raise RuntimeError("CapturedTrainStep: GPU batch tensors only (no CPU fallback)")
         if fp16_backward(model, batch[0]):
             # fp16 stays eager: under capture the backward takes exact gradient scales (slower than
-            # the eager delayed ones), and replay-vs-eager equality has no fixed reference — two eager
-            # fp16 runs of the tiny test model part by O(1) in relative gradient within four steps
-            # (AdamW's sign-like updates amplify summation-order noise); the first replayed step
-            # sits inside that spread (tools/captured_fp16_probe.py, profiles/r05/r5ar)
+            # the eager delayed ones), and replay-vs-eager equality has no fixed reference — eager
+            # fp16 steps are not bit-reproducible run to run (the tiny test model parts by O(1) in
+            # relative gradient within four steps, profiles/r05/r5ar; at the bench widths 2 of 6
+            # three-step runs diverged, r5at), so a replay can be held to nothing exact
             raise RuntimeError("CapturedTrainStep: bf16 / fp32 backward only (fp16 steps stay eager)")
         self.static = [t.detach().clone() for t in batch]
         args = (silog, seg_weight, silog_weight)
