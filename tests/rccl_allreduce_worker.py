@@ -4,9 +4,9 @@ the RCCL process group it creates does not outlive it).
 One rank on an RCCL ("nccl") group: the tiny context-decoder DenseCLIP in bf16 trained one step
 bare and one step under train.GradAllReduce with the collectives issued (skip_collectives False:
 at world size 1 the wrapper otherwise skips the identity), coalesced and per-tensor.  The AVG
-all-reduce of one rank is x / 1, so every gradient must come back equal to the bare model's (a
-collective that read a gradient before its producer wrote it would not); and every bucket must
-have been launched.  Prints one JSON line."""
+all-reduce of one rank is x / 1, so every gradient must come back equal to the bare model's up to
+the run-to-run noise of the heads' weight gradients (a collective that read a gradient before its
+producer wrote it would not); and every bucket must have been launched.  Prints one JSON line."""
 import json
 import os
 import sys
@@ -67,8 +67,12 @@ def main():
             w._launch = count
             g = grads(w, batch)
             assert set(g) == set(ref), sorted(set(g) ^ set(ref))
-            # the same gradients (the tiny widths' bias sums use float atomics: order noise only)
-            bad = [n for n in ref if float((g[n] - ref[n]).abs().max()) > 1e-5 * float(ref[n].abs().max()) + 1e-30]
+            # the same gradients up to run-to-run noise: the FCN heads' merged-tail weight gradients are
+            # not bit-reproducible between two bare runs either (profiles/r05/r5au; r5av saw 1 of 69
+            # tensors past 1e-5 here) — a collective that read a gradient before its producer wrote
+            # it would leave an O(1) difference, far past 1e-3 of the tensor's largest entry
+            bad = [(n, float((g[n] - ref[n]).abs().max()) / (float(ref[n].abs().max()) + 1e-30)) for n in ref
+                   if float((g[n] - ref[n]).abs().max()) > 1e-3 * float(ref[n].abs().max()) + 1e-30]
             assert not bad, bad[:5]
             assert sorted(launched) == list(range(len(w._buckets))), (launched, len(w._buckets))
             res[f"buckets_coalesce_{coalesce}"] = len(w._buckets)
