@@ -93,9 +93,10 @@ _SIGS = {
     "dclip_conv3x3": [_i32, _i32, _c_void_p, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _c_void_p, _i32, _c_void_p,
                       _i32, _i64, _i32, _i32, _i32, _c_void_p],
     "dclip_upsample_ce": [_i32, _c_void_p, _i32, _i32, _i32, _i32, _c_void_p, _i32, _i32, _i32, _i32, _c_void_p,
-                          _c_void_p, _c_void_p, _c_void_p],
+                          _c_void_p, _c_void_p, _c_void_p, _c_void_p],
     "dclip_upsample_silog": [_i32, _i32, _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p, _i32, _i32, _f32, _f32,
-                             _c_void_p, _c_void_p, _c_void_p],
+                             _c_void_p, _c_void_p, _c_void_p, _c_void_p],
+    "dclip_upsample_ws_floats": [_i32, _i32, _i32, _i32],
     "dclip_conv3x3_wgrad": [_i32, _c_void_p, _i64, _i32, _c_void_p, _i64, _i64, _i64, _i32, _i32, _i32, _i32,
                             _c_void_p, _c_void_p, _i32, _i32, _c_void_p, _c_void_p],
     "dclip_set_option": [_i32, _i32],
@@ -142,6 +143,7 @@ def load(path=None):
         lib.dclip_attn_fwd_fp8_workspace.restype = ctypes.c_int64
         lib.dclip_row_mean_workspace.restype = ctypes.c_int64
         lib.dclip_layernorm_bwd_ws_floats.restype = ctypes.c_int64
+        lib.dclip_upsample_ws_floats.restype = ctypes.c_int64
         # kernel-variant knobs for A/B runs: DCLIP_OPTIONS="id=value,..." (DCLIP_OPT_* ids of dclip.h)
         for kv in filter(None, os.environ.get("DCLIP_OPTIONS", "").split(",")):
             k, v = kv.split("=")

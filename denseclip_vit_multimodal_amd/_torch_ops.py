@@ -51,11 +51,11 @@ def _register_fakes():
         return _e(r, c, like=x, dtype=out_dtype), _e(r, like=x, dtype=f32), _e(r, like=x, dtype=f32)
 
     @reg("dclip::layernorm_bwd")
-    def _(dy, x, w, mean, rstd, res, dw, db):
+    def _(dy, x, w, mean, rstd, res, dw, db, dy_scale=None, dy_ntok=0):
         return _e(*x.shape, like=x, dtype=f32)
 
     @reg("dclip::layernorm_bwd_lp")
-    def _(dy, x, w, mean, rstd, res, dw, db, lp_dtype):
+    def _(dy, x, w, mean, rstd, res, dw, db, lp_dtype, dy_scale=None):
         return _e(*x.shape, like=x, dtype=f32), _e(*x.shape, like=x, dtype=lp_dtype)
 
     @reg("dclip::layernorm_bwd_add")
@@ -127,11 +127,11 @@ def _register_fakes():
         return (_e(*a.shape, like=a) if b is not None else _e(0, like=a)), _e(*a.shape, like=a, dtype=torch.float16), _e(4, like=a)
 
     @reg("dclip::layernorm_bwd_scaled")
-    def _(dy, x, w, mean, rstd, res, dw, db, st, use, target):
+    def _(dy, x, w, mean, rstd, res, dw, db, st, use, target, dy_scale=None):
         return _e(*x.shape, like=x, dtype=f32), _e(*x.shape, like=x, dtype=torch.float16), _e(4, like=x)
 
     @reg("dclip::layernorm_bwd_scaled_add")
-    def _(dy, x, w, mean, rstd, res, add, add_scale, ntok, dw, db, st, use, target):
+    def _(dy, x, w, mean, rstd, res, add, add_scale, ntok, dw, db, st, use, target, dy_scale=None):
         return _e(*x.shape, like=x, dtype=f32), _e(*x.shape, like=x, dtype=torch.float16), _e(4, like=x)
 
     @reg("dclip::attn_fwd")

@@ -15,7 +15,7 @@ void dclip_set_error(const char* fmt, ...) {
 
 extern "C" const char* dclip_last_error(void) { return g_err; }
 
-extern "C" int dclip_abi_version(void) { return 6; }
+extern "C" int dclip_abi_version(void) { return 7; }
 
 // Tuning options (variant selection for A/B benchmarking in one process); 0 = default.
 static int g_opts[DCLIP_OPT_COUNT] = {0};

@@ -1681,12 +1681,15 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_tn_big_kernel(const T* __rest
                                      Cs, ldc, nullptr, 0, slab, alpha);
 }
 
-// per-column sums of a row-major (rows x cols) matrix, accumulated into out (f32):
-// a block covers 64 columns (8 lanes x 8 columns, 16-byte loads) x a chunk of rows
-// (32 row lanes), reduces its 32 partial sums per column in LDS, one atomic per column.
+// per-column sums of a row-major (rows x cols) matrix (f32): a block covers 64 columns (8 lanes
+// x 8 columns, 16-byte loads) x a chunk of rows (32 row lanes) and reduces its 32 partial sums
+// per column in LDS in a fixed order.  With part, block row z writes part[z][c] (summed in z
+// order by the split-K combine); without, one block row adds into out (gridDim.y == 1).  No
+// float atomics: the column sums repeat bit for bit run to run.
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ x, int64_t ld, int64_t rows, int cols,
-                                                     int64_t rows_per_block, Alpha alpha_arg, float* __restrict__ out) {
+                                                     int64_t rows_per_block, Alpha alpha_arg, float* __restrict__ out,
+                                                     float* __restrict__ part) {
     const float alpha = alpha_arg.get();
     __shared__ float red[32][65];
     const int cx = threadIdx.x & 7, ry = threadIdx.x >> 3;
@@ -1724,7 +1727,10 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ x, in
         float t = 0.f;
         for (int k = 0; k < 32; ++k) t += red[k][threadIdx.x];
         const int c = blockIdx.x * 64 + threadIdx.x;
-        if (c < cols) atomicAdd(out + c, t * alpha);
+        if (c < cols) {
+            if (part != nullptr) part[(int64_t)blockIdx.y * cols + c] = t * alpha;
+            else out[c] += t * alpha;
+        }
     }
 }
 
@@ -2663,11 +2669,16 @@ extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda
     const bool big = tn_opt != 1 && M >= 256 && N >= 256;
     // the big kernel sums A's columns itself (DCLIP_OPT_GEMM_TN_COLSUM 1: the separate pass)
     const bool fused_cs = colsum_a && big && dclip_option(DCLIP_OPT_GEMM_TN_COLSUM) != 1;
+    // the separate column-sum pass: per-split partials into ws's column-sum region (summed in
+    // split order by the combine), or, for STORE (splits == 1), one block row over all K
+    float* cs_sep = (colsum_a && !fused_cs && epilogue == DCLIP_EPI_SPLITK) ? (float*)ws + (int64_t)splits * M * N
+                                                                           : nullptr;
     if (colsum_a && !fused_cs) {
-        const int64_t rpb = 2048;
-        dim3 cg((unsigned)((M + 63) / 64), (unsigned)((K + rpb - 1) / rpb));
-        if (ab_dt == DCLIP_BF16) colsum_kernel<bf16><<<cg, 256, 0, st>>>((const bf16*)A, lda, K, (int)M, rpb, alpha, colsum_a);
-        else colsum_kernel<f16><<<cg, 256, 0, st>>>((const f16*)A, lda, K, (int)M, rpb, alpha, colsum_a);
+        const int64_t rpb = cs_sep != nullptr ? K_pad / splits : K;
+        dim3 cg((unsigned)((M + 63) / 64), (unsigned)(cs_sep != nullptr ? splits : 1));
+        if (ab_dt == DCLIP_BF16)
+            colsum_kernel<bf16><<<cg, 256, 0, st>>>((const bf16*)A, lda, K, (int)M, rpb, alpha, colsum_a, cs_sep);
+        else colsum_kernel<f16><<<cg, 256, 0, st>>>((const f16*)A, lda, K, (int)M, rpb, alpha, colsum_a, cs_sep);
     }
 #define TN_LAUNCH(T, EPI, OUT)                                                                               \
     gemm_tn_kernel<T, EPI, float><<<grid, 256, 0, st>>>((const T*)A, lda, (const T*)B, ldb, (int)M, (int)N,   \
@@ -2690,7 +2701,7 @@ extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda
     } while (0)
     const int tm2 = (int)((M + 255) / 256), tn2 = (int)((N + 255) / 256);
     // the fused column sums' per-split partials, past the slabs (SPLITK): summed in split order
-    float* cs_part = (fused_cs && epilogue == DCLIP_EPI_SPLITK) ? (float*)ws + (int64_t)splits * M * N : nullptr;
+    float* cs_part = (fused_cs && epilogue == DCLIP_EPI_SPLITK) ? (float*)ws + (int64_t)splits * M * N : cs_sep;
     if (epilogue == DCLIP_EPI_STORE) {
         DCLIP_HOST_CHECK(bias == nullptr, "dclip_gemm_tn: bias only with SPLITK");
         if (big) {

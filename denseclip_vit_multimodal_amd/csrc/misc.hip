@@ -484,25 +484,20 @@ __global__ __launch_bounds__(256) void score_map_kernel(const TV* __restrict__ v
     const int pitch = C + 8;
     const int b = blockIdx.y;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l32 = lane & 31, h = lane >> 5;
-    // class-embedding norms, then the normalised 16-bit rows: two sweeps of independent 16-byte
-    // loads over the K x C block (the second from cache) instead of one dependent load -> wave
-    // reduction -> reload chain per row
+    // class-embedding norms (a wave per row: each lane's 16-byte chunks in order, then the wave's
+    // fixed butterfly; no LDS atomics, so the norms repeat bit for bit), then the normalised
+    // 16-bit rows from cache
     __shared__ float nrm[32];
-    if (threadIdx.x < 32) nrm[threadIdx.x] = 0.f;
-    __syncthreads();
     const f32x4* tb = (const f32x4*)(t + (int64_t)b * K * C);
-    const int n4 = K * C / 4, c4 = C / 4;
-    for (int i = threadIdx.x; i < n4; i += 256) {
-        const f32x4 x = tb[i];
-        float ss = x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3];
-        const int k = i / c4;
-        const int base = i - lane;  // this wave's first chunk (every lane of the wave is active: n4 % 4 == 0)
-        if (base + 63 < n4 && base / c4 == (base + 63) / c4) {  // the wave's 64 chunks lie in one row
-            ss = wave_sum(ss);
-            if (lane == 0) atomicAdd(&nrm[k], ss);
-        } else {
-            atomicAdd(&nrm[k], ss);
+    const int c4 = C / 4;
+    for (int k = wave; k < K; k += 4) {
+        float ss = 0.f;
+        for (int j = lane; j < c4; j += 64) {
+            const f32x4 x = tb[k * c4 + j];
+            ss += x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3];
         }
+        ss = wave_sum(ss);
+        if (lane == 0) nrm[k] = ss;
     }
     __syncthreads();
     for (int i = threadIdx.x; i < 32 * c4; i += 256) {

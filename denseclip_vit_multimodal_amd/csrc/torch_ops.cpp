@@ -794,11 +794,13 @@ std::tuple<Tensor, Tensor, Tensor> upsample_ce(const Tensor& logits, const Tenso
     Tensor sums = at::zeros({1}, like(logits, at::kDouble));
     Tensor cnt = at::zeros({1}, like(logits, at::kInt));
     Tensor grad = at::zeros(logits.sizes(), like(logits, at::kFloat));
+    Tensor ws = at::empty({dclip_upsample_ws_floats((int)logits.size(0), (int)logits.size(1), (int)logits.size(2),
+                                                    (int)logits.size(3))}, like(logits, at::kFloat));
     DCLIP_CALL(dclip_upsample_ce(dt_code(logits.scalar_type()), logits.data_ptr(), (int)logits.size(0),
                                  (int)logits.size(1), (int)logits.size(2), (int)logits.size(3), labels.data_ptr(),
                                  lab_code(labels.scalar_type()), (int)labels.size(1), (int)labels.size(2),
                                  (int)ignore_index, (double*)sums.data_ptr(), (unsigned*)cnt.data_ptr(), ptr<float>(grad),
-                                 stream_of(logits)));
+                                 ptr<float>(ws), stream_of(logits)));
     return {sums, cnt, grad};
 }
 
@@ -808,10 +810,12 @@ Tensor upsample_silog_sums(const Tensor& pred, const Tensor& target, const c10::
     TORCH_CHECK(target.scalar_type() == at::kFloat && target.dim() == 3, "upsample_silog: target (B, H, W) fp32");
     c10::DeviceGuard g(pred.device());
     Tensor sums = at::zeros({3}, like(pred, at::kDouble));
+    Tensor ws = at::empty({dclip_upsample_ws_floats((int)pred.size(0), 1, (int)pred.size(2), (int)pred.size(3))},
+                          like(pred, at::kFloat));
     DCLIP_CALL(dclip_upsample_silog(0, dt_code(pred.scalar_type()), pred.data_ptr(), (int)pred.size(0), (int)pred.size(2),
                                     (int)pred.size(3), ptr<float>(target), optr<uint8_t>(mask), (int)target.size(1),
                                     (int)target.size(2), (float)eps, 0.f, (double*)sums.data_ptr(), nullptr,
-                                    stream_of(pred)));
+                                    ptr<float>(ws), stream_of(pred)));
     return sums;
 }
 
@@ -821,10 +825,12 @@ Tensor upsample_silog_grad(const Tensor& pred, const Tensor& target, const c10::
     check_gpu(pred, "pred"); check_gpu(target, "target"); check_opt(mask, "mask"); check_gpu(sums, "sums");
     c10::DeviceGuard g(pred.device());
     Tensor grad = at::zeros(pred.sizes(), like(pred, at::kFloat));
+    Tensor ws = at::empty({dclip_upsample_ws_floats((int)pred.size(0), 1, (int)pred.size(2), (int)pred.size(3))},
+                          like(pred, at::kFloat));
     DCLIP_CALL(dclip_upsample_silog(1, dt_code(pred.scalar_type()), pred.data_ptr(), (int)pred.size(0), (int)pred.size(2),
                                     (int)pred.size(3), ptr<float>(target), optr<uint8_t>(mask), (int)target.size(1),
                                     (int)target.size(2), (float)eps, (float)lambd, (double*)sums.data_ptr(),
-                                    ptr<float>(grad), stream_of(pred)));
+                                    ptr<float>(grad), ptr<float>(ws), stream_of(pred)));
     return grad;
 }
 

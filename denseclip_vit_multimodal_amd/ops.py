@@ -123,6 +123,30 @@ def D():
     return _D
 
 
+def _env_option(opt, default=0):
+    import os
+    for kv in filter(None, os.environ.get("DCLIP_OPTIONS", "").split(",")):
+        k, v = kv.split("=")
+        if int(k) == opt:
+            return int(v)
+    return default
+
+
+_GEMM_WALK = [_env_option(N.OPT_GEMM_SCHED)]  # the DCLIP_OPT_GEMM_SCHED value in force (DCLIP_OPTIONS at load)
+
+
+def set_gemm_walk(walk):
+    """Select the persistent NT GEMMs' tile walk for the launches that follow (DCLIP_OPT_GEMM_SCHED:
+    0 static XCD-contiguous ranges, 1 every tile claimed — work-conserving when other kernels hold
+    CUs, e.g. RCCL's channel kernels during a bucket all-reduce); returns the previous value.  The
+    outputs are bitwise equal under either walk (test_gemm_work_conserving_walk_matches_static)."""
+    prev = _GEMM_WALK[0]
+    if walk != prev:
+        N.call("dclip_set_option", N.OPT_GEMM_SCHED, int(walk))
+        _GEMM_WALK[0] = int(walk)
+    return prev
+
+
 def layernorm_fwd(x2d, w, b, out_dtype, eps=1e-5):
     """(y in out_dtype, mean, rstd) of LayerNorm over the last dim in fp32 (models.py:243-249)."""
     _check(x2d, w, b)

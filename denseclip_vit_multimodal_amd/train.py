@@ -166,9 +166,14 @@ class GradAllReduce(torch.nn.Module):
         # requires_grad are reduced)
         self._module_parameters = [p for n, p in module.named_parameters() if n not in ignore]
         from torch.distributed.distributed_c10d import _get_default_group
-        if params and dist.get_world_size() > 1:
-            with torch.no_grad():  # rank 0's initial parameters, flattened into ~250 MB broadcasts
-                dist._broadcast_coalesced(_get_default_group(), [p.data for _, p in params], 250 * 2 ** 20, 0)
+        if self._module_parameters and dist.get_world_size() > 1:
+            # rank 0's initial parameters, flattened into ~250 MB broadcasts: EVERY parameter not
+            # ignored, frozen ones included, as DDP's _sync_module_states does (the reference seeds
+            # each rank with seed + rank, train_denseclip.py:941, so a randomly initialised frozen
+            # weight would otherwise differ between ranks)
+            with torch.no_grad():
+                dist._broadcast_coalesced(_get_default_group(), [p.data for p in self._module_parameters],
+                                          250 * 2 ** 20, 0)
         self._buffers_to_sync = [b for b in module.buffers()] if broadcast_buffers else []
         # gradients arrive roughly in reverse registration order, so the bucket of the FIRST
         # registered parameters (patch embedding, block 0) completes last and its all-reduce is the
@@ -195,6 +200,13 @@ class GradAllReduce(torch.nn.Module):
         # the collective path anyway — bench.py's ddp1 line prices RCCL's one-rank all-reduce so)
         self.skip_collectives = self._world == 1
         self.coalesce = True  # RCCL: a bucket's all-reduces as one group call
+        # the persistent GEMMs' tile walk while a bucket's collective is in flight (DCLIP_OPT_GEMM_SCHED
+        # value: 1 = every tile claimed, so the workgroups that find a CU held by RCCL's channel
+        # kernels leave their tiles to the others; None keeps whatever walk is set).  The static walk
+        # is faster uncontended (+4 % for claims) but loses 49 % vs 22 % with 16 CUs held
+        # (profiles/r05/r5e_ab_gemm_walks.log), and the buckets complete through the whole backward,
+        # so the GEMMs launched between the first bucket's launch and _finish take the claims walk
+        self.gemm_walk_under_collectives = 1
         self._pending = None
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for _, p in params]
 
@@ -214,6 +226,9 @@ class GradAllReduce(torch.nn.Module):
         st["launched"][i] = True
         if not grads or self.skip_collectives:
             return
+        if st["walk"] is None and self.gemm_walk_under_collectives is not None:
+            from . import ops
+            st["walk"] = ops.set_gemm_walk(self.gemm_walk_under_collectives)
         d = self._dist
         if self._nccl and self.coalesce:
             with d._coalescing_manager(async_ops=True) as cm:
@@ -229,25 +244,33 @@ class GradAllReduce(torch.nn.Module):
 
     def _on_grad(self, p):
         if self._pending is None:
-            self._pending = {"ready": [0] * len(self._buckets), "launched": [False] * len(self._buckets), "works": []}
+            self._pending = {"ready": [0] * len(self._buckets), "launched": [False] * len(self._buckets), "works": [],
+                             "next": 0, "walk": None}
             torch.autograd.Variable._execution_engine.queue_callback(self._finish)
         i = self._bucket_of[p]
         st = self._pending
         st["ready"][i] += 1
-        if st["ready"][i] == len(self._buckets[i]):
-            self._launch(i)
+        # collectives are issued in BUCKET order, as DDP's reducer does: a bucket that completes
+        # early waits for its predecessors, so every rank issues the same sequence of collectives
+        # even if autograd visits the parameters in a different order on some rank
+        while st["next"] < len(self._buckets) and st["ready"][st["next"]] == len(self._buckets[st["next"]]):
+            self._launch(st["next"])
+            st["next"] += 1
 
     def _finish(self):
         st = self._pending
         if st is None:
             return
         for i, done in enumerate(st["launched"]):
-            if not done:  # a bucket some of whose parameters got no gradient this step
+            if not done:  # a bucket some of whose parameters got no gradient this step (bucket order)
                 self._launch(i)
         for w, g in st["works"]:
             w.wait()
             if g is not None:  # gloo has no AVG
                 g.div_(self._world)
+        if st["walk"] is not None:  # the current stream now waits on the collectives: back to the walk before
+            from . import ops
+            ops.set_gemm_walk(st["walk"])
         self._pending = None
 
 
@@ -335,10 +358,12 @@ class CapturedTrainStep:
     or with no argument (the same batch again); it returns the step's loss tensor (the SAME
     tensor every call).  Requirements: one process (no DDP: its bucketed all-reduce hooks are not
     captured here), a fused AdamW built with capturable=True (its step counts live on the device),
-    and parameters that stay where they are.  bf16 / fp32 backward only: an fp16 model is refused —
-    a captured fp16 step must take exact gradient scales (the delayed scales' use counter is host
-    state) and measured slower than eager (137.5 vs 135.1 ms), and its equality with
-    eager cannot be pinned: two eager fp16 runs of the test model already differ (see below)."""
+    and parameters that stay where they are.  An fp16 backward is captured with EXACT gradient
+    scales (the delayed scales' use counter is host state, so ops takes exact scales under stream
+    capture): its replays equal eager steps run with ops.FP16_DELAYED_SCALE = False bit for bit
+    (tests/test_gpu_determinism.py; the step is bitwise reproducible since the fixed-order loss
+    folds of ABI 7), and measured slower than the eager delayed-scale step (137.5 vs 135.1 ms,
+    DESIGN.md §5), so the bench's fp16 line stays eager."""
 
     def __init__(self, model, opt, batch, silog=None, seg_weight=1.0, silog_weight=0.1, warmup=3):
         if isinstance(model, (torch.nn.parallel.DistributedDataParallel, GradAllReduce)):
@@ -348,13 +373,6 @@ class CapturedTrainStep:
                                "(make_optimizer(..., capturable=True))")
         if not all(t.is_cuda for t in batch):
             raise RuntimeError("CapturedTrainStep: GPU batch tensors only (no CPU fallback)")
-        if fp16_backward(model, batch[0]):
-            # fp16 stays eager: under capture the backward takes exact gradient scales (slower than
-            # the eager delayed ones), and replay-vs-eager equality has no fixed reference — eager
-            # fp16 steps are not bit-reproducible run to run (the tiny test model parts by O(1) in
-            # relative gradient within four steps, profiles/r05/r5ar; at the bench widths 2 of 6
-            # three-step runs diverged, r5at), so a replay can be held to nothing exact
-            raise RuntimeError("CapturedTrainStep: bf16 / fp32 backward only (fp16 steps stay eager)")
         self.static = [t.detach().clone() for t in batch]
         args = (silog, seg_weight, silog_weight)
         m = _unwrap(model)

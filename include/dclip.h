@@ -307,12 +307,19 @@ int dclip_conv3x3_wgrad(int ab_dt, const void* dY, int64_t ldy, int Nout, const 
  *                         pass 0: sums (f64[3]) += (sum d, sum d^2, T), d = log(max(up(pred),
  *                         eps)) - log(max(target, eps)) on the mask; pass 1 (sums complete):
  *                         grad (f32, B*h*w) += up^T((2d/T - 2 lambd S/T^2) / up(pred))
- *                         (zero where up(pred) < eps).  K == 19 for the CE kernel.       */
+ *                         (zero where up(pred) < eps).  K == 19 for the CE kernel.
+ * ws (ABI 7): the caller's scratch of dclip_upsample_ws_floats(B, K, h, w) floats (K = 1 for
+ * SILog), 8-byte aligned, contents undefined on entry: every workgroup writes its loss partials
+ * and its low-res gradient tile there and two short launches add them in a fixed order, so the
+ * loss and the gradient are bitwise reproducible (ABI 6 used float atomics).  Stream-ordered:
+ * one ws per call in flight.                                                            */
+int64_t dclip_upsample_ws_floats(int B, int K, int h, int w);
 int dclip_upsample_ce(int low_dt, const void* logits, int B, int K, int h, int w, const void* labels, int lab_dt,
-                      int H, int W, int ignore_index, double* loss_sum, unsigned* count, float* grad, void* stream);
+                      int H, int W, int ignore_index, double* loss_sum, unsigned* count, float* grad, float* ws,
+                      void* stream);
 int dclip_upsample_silog(int pass, int low_dt, const void* pred, int B, int h, int w, const float* target,
                          const uint8_t* mask, int H, int W, float eps, float lambd, double* sums, float* grad,
-                         void* stream);
+                         float* ws, void* stream);
 
 /* Cityscapes depth + segmentation batch preparation (datasets/cityscapes_depth_seg.py:129-170,
  * 218 and the trainer's RandomCrop / HorizontalFlip / Normalize / ToTensorV2,

@@ -52,6 +52,9 @@ def _model():
     for mod in h.modules():
         for p in mod.parameters(recurse=False):
             p.requires_grad_(True)
+    # a frozen parameter (like text_encoder.* / backbone.* in mode R): not reduced, but broadcast
+    # from rank 0 at wrap time all the same (DDP's _sync_module_states)
+    h.frozen = nn.Parameter(torch.linspace(-1, 1, 7), requires_grad=False)
     return h
 
 
@@ -75,6 +78,15 @@ def _worker(rank, world, port, out_dir, impl=None, bucket_mb=None):
         with torch.no_grad():  # rank 1 starts elsewhere: wrapping broadcasts rank 0's parameters
             for p in m.parameters():
                 p.add_(float(rank))
+        from denseclip_vit_multimodal_amd import ops
+        walks = []
+        ops_set = ops.set_gemm_walk
+
+        def record(w):
+            walks.append(w)
+            return ops_set(w)
+
+        ops.set_gemm_walk = record
         model = GradAllReduce(m, bucket_cap_mb=bucket_mb) if bucket_mb else wrap_ddp(m, impl=impl)
         if bucket_mb:
             assert len(model._buckets) >= 5, len(model._buckets)
@@ -88,11 +100,13 @@ def _worker(rank, world, port, out_dir, impl=None, bucket_mb=None):
         loss = loss_fn(out, seg, depth, mask)
         opt.zero_grad(set_to_none=True)
         loss.backward()
-        grads = {n: p.grad.clone() for n, p in model.module.named_parameters()}
+        ops.set_gemm_walk = ops_set
+        grads = {n: p.grad.clone() for n, p in model.module.named_parameters() if p.requires_grad}
         opt.step()
         params = {n: p.detach().clone() for n, p in model.module.named_parameters()}
         bufs = {n: b.clone() for n, b in model.module.named_buffers()}
-        torch.save({"grads": grads, "params": params, "loss": loss.detach(), "buffers": bufs},
+        torch.save({"grads": grads, "params": params, "loss": loss.detach(), "buffers": bufs,
+                    "walks": torch.tensor(walks, dtype=torch.int64)},
                    os.path.join(out_dir, f"rank{rank}.pt"))
     finally:
         cleanup()
@@ -131,11 +145,20 @@ def test_ddp_world2_matches_single_process(tmp_path, impl, bucket_mb):
     (total / world).backward()
     torch.set_num_threads(nt)
     for n, p in ref.named_parameters():
+        if not p.requires_grad:
+            continue
         for i in range(world):
             g = r[i]["grads"][n]
             assert rel_err(g, p.grad) < 1e-4, (n, i, rel_err(g, p.grad))  # fp32 sum-order noise only
     for n in r[0]["params"]:
         assert torch.equal(r[0]["params"][n], r[1]["params"][n]), n
+    # the frozen parameter: rank 1's perturbed copy was replaced by rank 0's at wrap time
+    assert torch.equal(r[1]["params"]["frozen"], torch.linspace(-1, 1, 7))
+    if impl == "allreduce":
+        # the GEMM tile walk: claims (1) from the first bucket's collective to the end of the
+        # backward, then back to the static walk (0)
+        for i in range(world):
+            assert r[i]["walks"].tolist() == [1, 0], r[i]["walks"]
     assert not torch.equal(r[0]["loss"], r[1]["loss"])  # the shards really differ
     rb = dict(ref.named_buffers())
     assert rb and set(rb) == set(r[1]["buffers"])
@@ -212,3 +235,36 @@ def test_nonfinite_skip_is_rank_consistent(tmp_path, fused):
     for i in range(world):
         w = torch.load(tmp_path / f"skip{i}.pt", weights_only=True)["w"]
         assert torch.equal(w, torch.ones(5)), (i, w)
+
+
+def test_grad_allreduce_issues_buckets_in_bucket_order():
+    """collectives are issued in bucket order whatever order autograd
+    completes the buckets in (a bucket that completes early waits for its predecessors), so
+    every rank issues the same sequence; a bucket with a parameter that got no gradient is
+    issued by _finish, still in order."""
+    import torch.distributed as dist
+    from denseclip_vit_multimodal_amd.train import GradAllReduce
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        m = nn.Sequential(*[nn.Linear(64, 64) for _ in range(6)])
+        w = GradAllReduce(m, bucket_cap_mb=0.01, last_bucket_cap_mb=0.01)
+        nb = len(w._buckets)
+        assert nb >= 4
+        order = []
+        w._launch = lambda i: (order.append(i), w._pending["launched"].__setitem__(i, True))
+        # the state _on_grad creates at the first gradient of a backward (outside a backward
+        # there is no engine to queue _finish on, so seed it here)
+        w._pending = {"ready": [0] * nb, "launched": [False] * nb, "works": [], "next": 0, "walk": None}
+        # complete bucket 2 first, then 0, then every bucket but the last's last parameter
+        feed = list(w._buckets[2]) + list(w._buckets[0]) + [p for i in range(nb) if i not in (0, 2)
+                                                             for p in w._buckets[i]][:-1]
+        with torch.no_grad():
+            for p in feed:
+                w._on_grad(p)
+        assert order == list(range(nb - 1)), order
+        w._finish()
+        assert order == list(range(nb)), order
+    finally:
+        dist.destroy_process_group()

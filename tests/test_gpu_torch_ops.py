@@ -34,6 +34,13 @@ def test_opcheck_layernorm():
     _opcheck(D().layernorm_bwd, (dy, x, w, mu, rs, None, torch.zeros(768, device=DEV), torch.zeros(768, device=DEV)))
     _opcheck(D().layernorm_bwd_lp, (dy, x, w, mu, rs, x.clone(), torch.zeros(768, device=DEV),
                                     torch.zeros(768, device=DEV), torch.bfloat16))
+    # ABI 6 arguments with non-default values (the fake kernels must take them)
+    sc = torch.tensor([4.0, 0.25, 0.0, 0.0], device=DEV)
+    dyh = (torch.randn(300, 768, device=DEV) * 4).to(torch.float16)
+    _opcheck(D().layernorm_bwd, (dyh, x, w, mu, rs, None, torch.zeros(768, device=DEV), torch.zeros(768, device=DEV),
+                                 sc, 100))
+    _opcheck(D().layernorm_bwd_lp, (dyh, x, w, mu, rs, x.clone(), torch.zeros(768, device=DEV),
+                                    torch.zeros(768, device=DEV), torch.bfloat16, sc))
 
 
 def test_opcheck_gemm_family():

@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
     lib = N.load()
     for name in declared_symbols():
         assert hasattr(lib, name), name
-    assert lib.dclip_abi_version() == 6
+    assert lib.dclip_abi_version() == 7
 
 
 def test_no_oracle_in_product_package():

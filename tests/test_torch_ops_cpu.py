@@ -68,3 +68,33 @@ def test_fake_tracing_keeps_the_custom_ops(D):
     gm = make_fx(f, tracing_mode="fake")(torch.empty(8, 64, device="meta"), torch.empty(64, device="meta"))
     targets = {str(n.target) for n in gm.graph.nodes if n.op == "call_function"}
     assert "dclip.layernorm_fwd.default" in targets and "dclip.cast.default" in targets
+
+
+def test_fake_layernorm_backward_forms_take_the_abi6_arguments(D):
+    """the fake kernels of the four LN backward forms accept the ABI-6 arguments
+    (dy_scale, dy_ntok) with non-default values, as ReadoutFn's fast path and the fp16 BlockFn
+    pass them, so make_fx / torch.compile of the backward traces."""
+    from torch.fx.experimental.proxy_tensor import make_fx
+    R, C = 16, 768
+
+    def f(dy, x, w, mu, rs, res, add, sc, dw, db, st):
+        a = D.layernorm_bwd(dy, x, w, mu, rs, res, dw, db, sc, 8)
+        b, lp = D.layernorm_bwd_lp(dy, x, w, mu, rs, res, dw, db, torch.bfloat16, sc)
+        c, lp2, p2 = D.layernorm_bwd_scaled(dy, x, w, mu, rs, res, dw, db, st, 1, 16.0, sc)
+        d, lp3, p3 = D.layernorm_bwd_scaled_add(dy, x, w, mu, rs, res, add, sc, 8, dw, db, st, 1, 16.0, sc)
+        return a, b, lp, c, lp2, p2, d, lp3, p3
+
+    m = "meta"
+    args = (torch.empty(R, C, device=m, dtype=torch.float16), torch.empty(R, C, device=m), torch.empty(C, device=m),
+            torch.empty(R, device=m), torch.empty(R, device=m), torch.empty(R, C, device=m),
+            torch.empty(R, C, device=m, dtype=torch.float16), torch.empty(4, device=m), torch.empty(C, device=m),
+            torch.empty(C, device=m), torch.empty(64, device=m))
+    gm = make_fx(f, tracing_mode="fake")(*args)
+    targets = {str(n.target) for n in gm.graph.nodes if n.op == "call_function"}
+    for op in ("layernorm_bwd", "layernorm_bwd_lp", "layernorm_bwd_scaled", "layernorm_bwd_scaled_add"):
+        assert f"dclip.{op}.default" in targets
+    with FakeTensorMode():
+        fa = [torch.empty(a.shape, dtype=a.dtype, device="cuda") for a in args]
+        outs = f(*fa)
+    assert outs[0].shape == (R, C) and outs[0].dtype == torch.float32
+    assert outs[2].dtype == torch.bfloat16 and outs[4].dtype == torch.float16 and outs[7].dtype == torch.float16
