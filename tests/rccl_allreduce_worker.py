@@ -69,6 +69,36 @@ def main():
             assert not bad, (len(bad), bad[:5])
             assert launched == list(range(len(w._buckets))), (launched, len(w._buckets))
             res[f"buckets_coalesce_{coalesce}"] = len(w._buckets)
+        # the tile walk under collectives: CUs held by a side-stream occupier
+        # (tools/cu_hog.hip, standing in for RCCL's channel kernels, which at world size 1 launch
+        # nothing) from every bucket launch, the GEMMs of the rest of the backward on the claims
+        # walk — the gradients still bit-identical, the walk back to static after the backward
+        import ctypes
+        from denseclip_vit_multimodal_amd import ops
+        hog = ctypes.CDLL(os.path.join(os.path.dirname(HERE), "tools", "libcu_hog.so"))
+        hog.cu_hog.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p]
+        sink = torch.zeros(64, dtype=torch.int32, device="cuda")
+        side = torch.cuda.Stream()
+        w = GradAllReduce(make(), bucket_cap_mb=25, last_bucket_cap_mb=25)
+        w.skip_collectives = False
+        assert w.gemm_walk_under_collectives == 1
+        orig = w._launch
+        walks = []
+
+        def hog_launch(i, orig=orig):
+            side.wait_stream(torch.cuda.current_stream())
+            assert hog.cu_hog(16, 300.0, sink.data_ptr(), side.cuda_stream) == 0
+            orig(i)
+            walks.append(ops._GEMM_WALK[0])
+
+        w._launch = hog_launch
+        g = grads(w, batch)
+        torch.cuda.synchronize()
+        bad = [n for n in ref if not torch.equal(g[n], ref[n])]
+        assert not bad, (len(bad), bad[:5])
+        assert walks and all(x == 1 for x in walks), walks
+        assert ops._GEMM_WALK[0] == 0
+        res["hog_windows"] = len(walks)
         print(json.dumps(res))
     finally:
         dist.destroy_process_group()

@@ -184,6 +184,7 @@ def test_grad_allreduce_rccl_world_size_1():
     assert r.returncode == 0
     res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert res["grads"] > 0 and res["buckets_coalesce_True"] > 1 and res["buckets_coalesce_False"] > 1, res
+    assert res["hog_windows"] > 1, res
 
 
 def test_bench_fp8_attention_trains():
