@@ -104,6 +104,9 @@ _SIGS = {
                                  _c_void_p, _c_void_p, _f32, _f32, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p,
                                  _c_void_p],
     "dclip_attn_bwd_workspace": [_i32, _i32, _i32],
+    "dclip_attn_bwd_fp8_workspace": [_i32, _i32, _i32],
+    "dclip_attn_bwd_fp8": [_i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i32,
+                           _i32, _f32, _c_void_p],
     "dclip_attn_fwd_fp8": [_i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i32, _i32, _c_void_p],
     "dclip_attn_fwd_fp8_workspace": [_i32, _i32, _i32],
     "dclip_gemm_tn_plan": [_i64, _i64, _i64, _c_void_p, _c_void_p],
@@ -139,6 +142,7 @@ def load(path=None):
         lib.dclip_abi_version.restype = ctypes.c_int
         lib.dclip_abi_version.argtypes = []
         lib.dclip_attn_bwd_workspace.restype = ctypes.c_int64  # a size, not a status
+        lib.dclip_attn_bwd_fp8_workspace.restype = ctypes.c_int64
         lib.dclip_bn_workspace.restype = ctypes.c_int64
         lib.dclip_attn_fwd_fp8_workspace.restype = ctypes.c_int64
         lib.dclip_row_mean_workspace.restype = ctypes.c_int64

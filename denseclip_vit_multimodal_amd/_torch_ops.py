@@ -146,6 +146,10 @@ def _register_fakes():
     def _(qkv, o, dout, lse, B, N, H, scale):
         return torch.empty_like(qkv)
 
+    @reg("dclip::attn_bwd_fp8")
+    def _(qkv, o, dout, lse, B, N, H, scale):
+        return torch.empty_like(qkv)
+
     @reg("dclip::im2col")
     def _(img, p, dtype):
         B, Cin, Hi, Wi = img.shape

@@ -2459,7 +2459,7 @@ void fwd_launch(const void* qkv, void* o, float* lse, int B, int N, int H, hipSt
 // partial last blocks and zero-filled tails)
 template <typename T>
 bool bwd2_launch(const void* qkv, const void* o, const void* dout, const float* lse, float* delta, void* dqkv, int B,
-                 int N, int H, float scale, hipStream_t st) {
+                 int N, int H, float scale, hipStream_t st, void* f8ws = nullptr) {
     if (N < 257 || dclip_option(DCLIP_OPT_ATTN_BWD_KERNEL) == 1) return false;
     // a ragged N - 1 (partial last query / key blocks, masked tails) in the default passes only
     const bool ragged = (N - 1) % 256 != 0;
@@ -2493,8 +2493,12 @@ bool bwd2_launch(const void* qkv, const void* o, const void* dout, const float* 
         else
             attn_bwd_dq2_kernel<T, 8><<<B * H * nq, 512, 0, st>>>((const T*)qkv, (const T*)o, (const T*)dout, lse,
                                                                    delta, nstat, (T*)dqkv, N, H, scale, r0kv);
-        attn_bwd_dkdv6_launch(std::is_same<T, bf16>::value ? DCLIP_BF16 : DCLIP_F16, qkv, dout, lse, delta, nstat,
-                              nstat + (int64_t)B * H * N, dqkv, B, N, H, 1.0f / LOG2E, r0q, st);
+        if (f8ws != nullptr)  // configs[4]: dV, dK on the block-scaled e4m3 MFMA
+            attn_bwd_dkdv8_launch(std::is_same<T, bf16>::value ? DCLIP_BF16 : DCLIP_F16, qkv, dout, lse, delta, nstat,
+                                  nstat + (int64_t)B * H * N, dqkv, B, N, H, 1.0f / LOG2E, r0q, f8ws, st);
+        else
+            attn_bwd_dkdv6_launch(std::is_same<T, bf16>::value ? DCLIP_BF16 : DCLIP_F16, qkv, dout, lse, delta, nstat,
+                                  nstat + (int64_t)B * H * N, dqkv, B, N, H, 1.0f / LOG2E, r0q, st);
         attn_bwd_row0_fold_merge<T><<<B * H, 64, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, r0kv, nq, r0q, nkb,
                                                           (T*)dqkv, N, H, scale, 1.0f / LOG2E);
         return true;
@@ -2526,8 +2530,8 @@ bool bwd2_launch(const void* qkv, const void* o, const void* dout, const float* 
 
 template <typename T>
 void bwd_launch(const void* qkv, const void* o, const void* dout, const float* lse, float* delta, void* dqkv,
-                int B, int N, int H, float scale, hipStream_t st) {
-    if (bwd2_launch<T>(qkv, o, dout, lse, delta, dqkv, B, N, H, scale, st)) return;
+                int B, int N, int H, float scale, hipStream_t st, void* f8ws = nullptr) {
+    if (bwd2_launch<T>(qkv, o, dout, lse, delta, dqkv, B, N, H, scale, st, f8ws)) return;
     // dQ (w.r.t. the unscaled q) = dZ K scale;  dK = dZ^T q scale = dZ^T q' / log2(e)
     if (dclip_option(DCLIP_OPT_ATTN_DQ_WAVES) == 4) {
         dim3 grid(((N + 127) / 128) * B * H);
@@ -2600,6 +2604,29 @@ extern "C" int dclip_attn_bwd(int dt, const void* qkv, const void* o, const void
     hipStream_t st = (hipStream_t)stream;
     if (dt == DCLIP_BF16) bwd_launch<bf16>(qkv, o, dout, lse, delta_ws, dqkv, B, N, H, scale, st);
     else bwd_launch<f16>(qkv, o, dout, lse, delta_ws, dqkv, B, N, H, scale, st);
+    DCLIP_LAUNCH_CHECK();
+    return 0;
+}
+
+// configs[4]'s backward (include/dclip.h): dclip_attn_bwd's workspace, then the fp8 images
+extern "C" int64_t dclip_attn_bwd_fp8_workspace(int B, int N, int H) {
+    return dclip_attn_bwd_workspace(B, N, H) + (attn_bwd_fp8_ws_bytes(B, N, H) + 3) / 4 + 64;
+}
+
+extern "C" int dclip_attn_bwd_fp8(int dt, const void* qkv, const void* o, const void* dout, const float* lse, float* ws,
+                                  void* dqkv, int B, int N, int H, int D, float scale, void* stream) {
+    DCLIP_HOST_CHECK(D == HD, "dclip_attn_bwd_fp8: head_dim must be 64 (got %d)", D);
+    DCLIP_HOST_CHECK(dt == DCLIP_BF16 || dt == DCLIP_F16, "dclip_attn_bwd_fp8: dtype must be f16/bf16");
+    DCLIP_HOST_CHECK(B > 0 && N > 0 && H > 0, "dclip_attn_bwd_fp8: empty problem");
+    DCLIP_HOST_CHECK(ws != nullptr && ((uintptr_t)ws % 16) == 0, "dclip_attn_bwd_fp8: ws (16-B aligned) required");
+    DCLIP_HOST_CHECK((int64_t)((N - 1 + 63) / 64) * (8192 + 256) < (1ll << 32),
+                     "dclip_attn_bwd_fp8: N too large for the fp8 image ring");
+    hipStream_t st = (hipStream_t)stream;
+    // the fp8 images past dclip_attn_bwd's part, rounded up to 256 B
+    const int64_t w16 = dclip_attn_bwd_workspace(B, N, H);
+    void* f8 = (void*)(((uintptr_t)(ws + w16) + 255) & ~(uintptr_t)255);
+    if (dt == DCLIP_BF16) bwd_launch<bf16>(qkv, o, dout, lse, ws, dqkv, B, N, H, scale, st, f8);
+    else bwd_launch<f16>(qkv, o, dout, lse, ws, dqkv, B, N, H, scale, st, f8);
     DCLIP_LAUNCH_CHECK();
     return 0;
 }

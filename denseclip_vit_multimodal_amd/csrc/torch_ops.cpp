@@ -513,6 +513,20 @@ Tensor attn_bwd(const Tensor& qkv, const Tensor& o, const Tensor& dout, const Te
     return dqkv;
 }
 
+// configs[4]'s backward: dV, dK on the block-scaled e4m3 MFMA (dclip_attn_bwd_fp8)
+Tensor attn_bwd_fp8(const Tensor& qkv, const Tensor& o, const Tensor& dout, const Tensor& lse, int64_t B, int64_t N,
+                    int64_t H, double scale) {
+    check_gpu(qkv, "qkv"); check_gpu(o, "o"); check_gpu(dout, "dout"); check_gpu(lse, "lse");
+    TORCH_CHECK(qkv.size(0) == B * N && o.sizes() == dout.sizes() && o.size(1) == 64 * H, "attn_bwd_fp8: shapes");
+    c10::DeviceGuard g(qkv.device());
+    Tensor ws = at::empty({dclip_attn_bwd_fp8_workspace((int)B, (int)N, (int)H)}, like(qkv, at::kFloat));
+    Tensor dqkv = at::empty_like(qkv);
+    DCLIP_CALL(dclip_attn_bwd_fp8(dt_code(qkv.scalar_type()), qkv.data_ptr(), o.data_ptr(), dout.data_ptr(),
+                                  ptr<float>(lse), ptr<float>(ws), dqkv.data_ptr(), (int)B, (int)N, (int)H, 64,
+                                  (float)scale, stream_of(qkv)));
+    return dqkv;
+}
+
 // ----------------------------------------------------------------------------- patch embedding
 Tensor im2col(const Tensor& img, int64_t p, at::ScalarType dtype) {
     check_gpu(img, "img");
@@ -918,6 +932,7 @@ TORCH_LIBRARY(dclip, m) {
     m.def("attn_fwd(Tensor qkv, int B, int N, int H, float scale) -> (Tensor, Tensor)");
     m.def("attn_fwd_fp8(Tensor qkv, int B, int N, int H) -> (Tensor, Tensor)");
     m.def("attn_bwd(Tensor qkv, Tensor o, Tensor dout, Tensor lse, int B, int N, int H, float scale) -> Tensor");
+    m.def("attn_bwd_fp8(Tensor qkv, Tensor o, Tensor dout, Tensor lse, int B, int N, int H, float scale) -> Tensor");
     m.def("im2col(Tensor img, int p, ScalarType dtype) -> Tensor");
     m.def("tokens_fwd(Tensor emb, Tensor cls, Tensor pos, int B, int P) -> Tensor");
     m.def("tokens_bwd(Tensor dx, ScalarType dtype, float scale, int B, int P, Tensor? scale_t=None) -> "
@@ -975,6 +990,7 @@ TORCH_LIBRARY_IMPL(dclip, CUDA, m) {
     m.impl("attn_fwd", &attn_fwd);
     m.impl("attn_fwd_fp8", &attn_fwd_fp8);
     m.impl("attn_bwd", &attn_bwd);
+    m.impl("attn_bwd_fp8", &attn_bwd_fp8);
     m.impl("im2col", &im2col);
     m.impl("tokens_fwd", &tokens_fwd);
     m.impl("tokens_bwd", &tokens_bwd);

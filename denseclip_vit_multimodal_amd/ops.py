@@ -439,10 +439,18 @@ def attn_fwd_fp8(qkv, B, Ntok, H):
     return o, lse
 
 
-def attn_bwd(qkv, o, dout, lse, B, Ntok, H, scale):
+# configs[4]: the backward of an fp8-forward block runs its dK / dV pass on the block-scaled e4m3
+# MFMA too (dclip_attn_bwd_fp8); False keeps the 16-bit backward (round 5's fp8 line)
+ATTN_BWD_FP8 = True
+
+
+def attn_bwd(qkv, o, dout, lse, B, Ntok, H, scale, fp8=False):
     _check(qkv, o, dout, lse)
     e0 = _tic()
-    dqkv = D().attn_bwd(qkv, o, dout, lse, B, Ntok, H, float(scale))
+    if fp8:
+        dqkv = D().attn_bwd_fp8(qkv, o, dout, lse, B, Ntok, H, float(scale))
+    else:
+        dqkv = D().attn_bwd(qkv, o, dout, lse, B, Ntok, H, float(scale))
     _toc("attn_bwd", e0)
     return dqkv
 
@@ -913,7 +921,7 @@ class BlockFn(torch.autograd.Function):
         if wg:
             dWo, dbo = weight_grad(dyo, o, db=zbo, scale=s2)
         del dyo
-        dqkv = attn_bwd(qkv, o, do, lse, B, Ntok, H, scale)  # linear in dO: carries s2
+        dqkv = attn_bwd(qkv, o, do, lse, B, Ntok, H, scale, fp8=bool(fp8) and ATTN_BWD_FP8)  # linear in dO: carries s2
         del do
         dxh1 = gemm(dqkv, WEIGHTS.get(w_in, cdt, transposed=True),
                     out_dtype=cdt if (dy_lp and s2 is None) or dy16 else torch.float32, scale=None if dy16 else s2)

@@ -183,6 +183,17 @@ int dclip_attn_fwd(int dt, const void* qkv, void* o, float* lse,
 int dclip_attn_bwd(int dt, const void* qkv, const void* o, const void* dout,
                    const float* lse, float* delta_ws, void* dqkv,
                    int B, int N, int H, int D, float scale, void* stream);
+
+/* configs[4]'s attention backward (ABI 7): dclip_attn_bwd's contract and results within e4m3
+ * rounding — on the CLS-split path (N >= 257) the dK / dV pass runs dV = P^T dO and dK = dS^T q' on
+ * the block-scaled e4m3 MFMA (v_mfma_scale_f32_32x32x64_f8f6f4, MX E8M0 scales per 32 queries: the
+ * Q / dO rows' from a pack pass, P's fixed at 2^-8, dS's per key from its amax), S, dP and the dQ
+ * pass stay 16-bit; elsewhere it is dclip_attn_bwd.  ws: dclip_attn_bwd_fp8_workspace(B, N, H)
+ * floats, 16-B aligned (dclip_attn_bwd's workspace, then the slices' e4m3 images).  Replaces the
+ * backward of models.py:287-289 under the fp8 attention of BASELINE configs[4].               */
+int64_t dclip_attn_bwd_fp8_workspace(int B, int N, int H);
+int dclip_attn_bwd_fp8(int dt, const void* qkv, const void* o, const void* dout, const float* lse, float* ws,
+                       void* dqkv, int B, int N, int H, int D, float scale, void* stream);
 int64_t dclip_attn_bwd_workspace(int B, int N, int H);
 
 /* fp8 attention forward (BASELINE config 5; inference only — there is no fp8 backward).

@@ -7,7 +7,7 @@ import torch
 from torch._subclasses.fake_tensor import FakeTensorMode
 
 OPS = ["layernorm_fwd", "layernorm_bwd", "layernorm_bwd_lp", "layernorm_bwd_add", "layernorm_bwd_scaled_add", "gemm", "gemm_gelu", "gemm_gelu_h", "gemm_residual_lp", "weight_grad", "gemm_tn", "cast", "grad_scale", "row_scale_add", "bn_eval",
-       "transpose2d", "weight_refresh", "transpose_batched", "add_readout_cast", "add_readout_amax", "add_readout_cast_scaled", "layernorm_bwd_scaled", "attn_fwd", "attn_fwd_fp8", "attn_bwd", "im2col", "tokens_fwd", "tokens_bwd",
+       "transpose2d", "weight_refresh", "transpose_batched", "add_readout_cast", "add_readout_amax", "add_readout_cast_scaled", "layernorm_bwd_scaled", "attn_fwd", "attn_fwd_fp8", "attn_bwd", "attn_bwd_fp8", "im2col", "tokens_fwd", "tokens_bwd",
        "pos_interp", "pos_interp_bwd", "row_mean", "score_map", "score_concat", "bilinear", "bilinear_bwd", "bn_fwd", "bn_bwd", "bn_fwd_rows", "bn_bwd_rows",
        "conv3x3", "conv3x3_wgrad", "upsample_ce", "upsample_silog_sums", "upsample_silog_grad", "cityscapes_prepare"]
 
