@@ -46,6 +46,9 @@ PEAK_FP8_TFLOPS = 5000.0  # MI355X dense fp8 (block-scaled f8f6f4 MFMA at 2x the
 # the fp8 attention's mix: QK^T (half the FLOPs) at the bf16 peak, P V at the fp8 one:
 # 1 / (0.5 / 2500 + 0.5 / 5000)
 PEAK_FP8_MIXED_TFLOPS = 1.0 / (0.5 / PEAK_BF16_TFLOPS + 0.5 / PEAK_FP8_TFLOPS)
+# configs[4]'s backward (dclip_attn_bwd_fp8): of its 5 useful N^2 matmuls S, dP, dQ run on the 16-bit MFMA
+# and dV, dK on the block-scaled e4m3 one
+PEAK_FP8_BWD_TFLOPS = 1.0 / (0.6 / PEAK_BF16_TFLOPS + 0.4 / PEAK_FP8_TFLOPS)
 PEAK_HBM_GBS = 8000.0
 FUSED_HEAD_LOSS = True  # resize + CE / SILog fused (same loss; no 1024x2048 logits in HBM)
 # backbone kwargs per --arch: ViT-B/16 is seg/configs/denseclip_cityscapes.yaml's own backbone;
@@ -321,6 +324,7 @@ def main():
     silog = SILogLoss()
 
     from denseclip_vit_multimodal_amd.train import synth_batch, wrap_ddp, make_optimizer
+    from denseclip_vit_multimodal_amd import ops
     B, H, W = args.batch, args.height, args.width
     img_dtype = torch.float16 if args.dtype == "fp16" else torch.bfloat16
     batch = synth_batch(B, H, W, dev, rank, image_dtype=img_dtype)
@@ -446,9 +450,12 @@ def main():
         fp8 = {"value": round(world * B * k_sub / dt8, 4), "unit": "images/sec",
                "ms_per_step": round(dt8 / k_sub * 1e3, 2), "loss": round(loss8, 4),
                "what": "BASELINE configs[4]: mode F, seg + depth heads, attention forward with P V on the e4m3 "
-                       "MFMA (MX E8M0 block scales) and the scores on the bf16 MFMA, 16-bit flash backward",
+                       "MFMA (MX E8M0 block scales) and the scores on the bf16 MFMA; backward: S, dP and the dQ "
+                       "pass on the bf16 MFMA, dV = P^T dO and dK = dS^T q on the block-scaled e4m3 MFMA"
+                       + ("" if ops.ATTN_BWD_FP8 else " (disabled: 16-bit flash backward)"),
                "roofline_attn_fwd": roofline(s8, "attn_fwd_fp8", fl, PEAK_FP8_MIXED_TFLOPS),
-               "roofline_attn_bwd": roofline(s8, "attn_bwd", fl_b, PEAK_BF16_TFLOPS)}
+               "roofline_attn_bwd": roofline(s8, "attn_bwd", fl_b,
+                                             PEAK_FP8_BWD_TFLOPS if ops.ATTN_BWD_FP8 else PEAK_BF16_TFLOPS)}
         # BASELINE configs[3]: ViT-L/14 backbone (C 1024, 24 layers, 16 heads, N = 10659)
         release()
         model, opt = setup("F", arch="vitl14")

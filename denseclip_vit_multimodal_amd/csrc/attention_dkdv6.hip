@@ -438,10 +438,11 @@ __device__ __forceinline__ int mx_e(float amax) {
 }
 __device__ __forceinline__ float pow2f(int e) { return __uint_as_float((unsigned)(127 + e) << 23); }
 
-// four f32 -> four e4m3 bytes of one dword, each divided by `inv` (a power of two)
+// four f32 -> four e4m3 bytes of one dword, each divided by `inv` (a power of two).  The first
+// convert writes the low word and keeps the high one, which the second then writes: its "old"
+// operand is a's own register (no v_mov of a zero per dword)
 __device__ __forceinline__ int cvt4_fp8(float a, float b, float c, float d, float inv) {
-    const s16x2 z = {0, 0};
-    s16x2 w = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(z, a, b, inv, false);
+    s16x2 w = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(__builtin_bit_cast(s16x2, a), a, b, inv, false);
     w = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(w, c, d, inv, true);
     return __builtin_bit_cast(int, w);
 }
