@@ -532,9 +532,20 @@ __global__ __launch_bounds__(256) void bwd_fp8_pack_kernel(const T* __restrict__
 // ---------------------------------------------------------------------------- the dK / dV pass
 template <typename T>
 struct Dkv8Ctx {
-    Dkv2Ctx<T, 4> c;    // the 16-bit ring's sources / offsets (its SLOT stride unused: SLOT8 here)
+    Dkv2Ctx<T, 4> c;    // the 16-bit ring's sources (its voff / SLOT stride unused here)
     rsrc_t rf;          // this (image, head)'s fp8 slice images
+    uint32_t hoff;      // the head's byte offset in a 16-bit row
 };
+
+// the lane id from an opaque asm statement: the DMA offsets below are recomputed at every issue
+// from it (a few VALU) instead of being held in VGPRs across the loop — held, the register
+// allocator spilled them, and a scratch reload before a DMA issue waits (vmcnt) for every ring
+// slice still in flight
+__device__ __forceinline__ int lane_opaque() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
 
 // slice t into ring slot `slot`: dkv2_issue's 16-bit pieces + statistics, then 2 KiB of the fp8
 // image per wave and 16 scale dwords per wave: 8 vmcnt entries per wave
@@ -544,21 +555,27 @@ __device__ __forceinline__ void dkv8_issue(Dkv8Ctx<T>& x, int t, int slot) {
     typedef Dkv2Ctx<T, 4> X;
     Dkv2Ctx<T, 4>& c = x.c;
     char* base = c.smem + slot * SLOT8;
+    const int ln = lane_opaque();
     const int r0 = 1 + 64 * t;
     const bool ragged = t == c.nt - 1 && c.rem < 64;  // wave-uniform
     const uint32_t soff = (uint32_t)r0 * c.ldmine;
     const int part = c.wave % 2;
     const bool is_l = c.wave < 2;
-    const uint32_t idx = (uint32_t)(part * X::SPW + c.lane);
+    const uint32_t idx = (uint32_t)(part * X::SPW + ln);
+    uint32_t vo[X::PIECES];
+    bool ok[X::PIECES];
+#pragma unroll
+    for (int i = 0; i < X::PIECES; ++i) {
+        const int r = ((c.wave * X::PIECES + i) & 7) * 8 + (ln >> 3);
+        vo[i] = (uint32_t)r * c.ldmine + (uint32_t)(((ln & 7) ^ xsw(r)) * 16) + x.hoff;
+        ok[i] = r < c.rem;
+    }
     if (__builtin_expect(ragged, 0)) {
 #pragma unroll
-        for (int i = 0; i < X::PIECES; ++i) {
-            const int piece = c.wave * X::PIECES + i;
-            const bool ok = (piece & 7) * 8 + (c.lane >> 3) < c.rem;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rmine, LDS_PTR(base + piece * 1024), 16,
-                                                     ok ? c.voff[i] + soff : 0xFFFFFFF0u, 0, 0, 0);
-        }
-        if (c.lane < X::SPW)
+        for (int i = 0; i < X::PIECES; ++i)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rmine, LDS_PTR(base + (c.wave * X::PIECES + i) * 1024), 16,
+                                                     ok[i] ? vo[i] + soff : 0xFFFFFFF0u, 0, 0, 0);
+        if (ln < X::SPW)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(is_l ? c.rl : c.rd,
                                                      LDS_PTR(base + 16384 + (is_l ? 0 : 256) + part * X::SPW * 4), 4,
                                                      (int)idx < c.rem ? (idx + (uint32_t)r0) * 4 : 0xFFFFFFF0u, 0, 0, 0);
@@ -566,21 +583,21 @@ __device__ __forceinline__ void dkv8_issue(Dkv8Ctx<T>& x, int t, int slot) {
 #pragma unroll
         for (int i = 0; i < X::PIECES; ++i)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rmine, LDS_PTR(base + (c.wave * X::PIECES + i) * 1024), 16,
-                                                     c.voff[i], soff, 0, 0);
-        if (c.lane < X::SPW)
+                                                     vo[i], soff, 0, 0);
+        if (ln < X::SPW)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(is_l ? c.rl : c.rd,
                                                      LDS_PTR(base + 16384 + (is_l ? 0 : 256) + part * X::SPW * 4), 4,
                                                      idx * 4, (uint32_t)r0 * 4, 0, 0);
     }
     // the fp8 image (always whole: the pack zero-fills a ragged last slice)
     const uint32_t fo = (uint32_t)t * F8_IMG;
-    const uint32_t lo = (uint32_t)(c.wave * 2048 + c.lane * 16);
+    const uint32_t lo = (uint32_t)(c.wave * 2048 + ln * 16);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(x.rf, LDS_PTR(base + SLOT16 + c.wave * 2048), 16, lo, fo, 0, 0);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(x.rf, LDS_PTR(base + SLOT16 + c.wave * 2048 + 1024), 16, lo + 1024, fo, 0,
                                              0);
-    if (c.lane < 16)
+    if (ln < 16)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(x.rf, LDS_PTR(base + SLOT16 + 8192 + c.wave * 64), 4,
-                                                 (uint32_t)(8192 + c.wave * 64 + c.lane * 4), fo, 0, 0);
+                                                 (uint32_t)(8192 + c.wave * 64 + ln * 4), fo, 0, 0);
 #endif
 }
 
@@ -638,10 +655,19 @@ __device__ __forceinline__ void chains8(K6<T>& k, int kb, const typename Mfma<T>
 }
 
 // one 64-query slice: S0 / P0 arrive seeded (sub 0, block 0) and qa / ga hold sub 0; both leave
-// holding the next slice's sub 0
+// holding the next slice's sub 0.  Every LDS operand is read one region ahead of its first MFMA
+// (at one wave per SIMD nothing else hides the read): sub 1's Q / dO fragments (qb / gb) in R1,
+// the e4m3 A fragments in R3 (in the registers sub 0's qa / ga held), the next slice's qa / ga in R5
+//   R1  S / dP block 0, sub 0   (8)        | loads qb / gb, block-1 seeds
+//   R2  S / dP block 1, sub 0   (8)        | VALU block 0 sub 0; seeds block 0 sub 1
+//   R3  S / dP block 0, sub 1   (8)        | VALU block 1 sub 0; e4m3 A fragments; seeds block 1 sub 1
+//   R4  S / dP block 1, sub 1   (8)        | VALU block 0 sub 1
+//   R5  dV / dK block 0 (e4m3)  (4 x 64 c) | VALU block 1 sub 1; next qa / ga
+//   R6  dV / dK block 1 (e4m3)  (4 x 64 c) | next seeds
 template <typename T, int Q>
 __device__ __forceinline__ void step8(Dkv8Ctx<T>& x, K6<T>& k, int t, typename Mfma<T>::frag (&qa)[4],
                                       typename Mfma<T>::frag (&ga)[4], f32x16& S0, f32x16& P0) {
+    typedef typename Mfma<T>::frag frag;
     Dkv2Ctx<T, 4>& c = x.c;
     wait_vmcnt<8>();                // own pieces of slice t+1 landed (slice t+2 in flight)
     __builtin_amdgcn_s_barrier();  // everyone's; everyone done with step t-1
@@ -649,32 +675,33 @@ __device__ __forceinline__ void step8(Dkv8Ctx<T>& x, K6<T>& k, int t, typename M
     const char* cur = c.smem + Q * SLOT8;
     const char* nxt = c.smem + ((Q + 1) & 3) * SLOT8;
     f32x16 S1, P1;
+    frag qb[4], gb[4];
     Pk8 pk;
-    // ---- R1: sub 0, block 0 chains
+    // ---- R1
     fence();
     chains8<T, 0, false>(k, 0, qa, ga, S0, P0, S1, P1, pk, 0);
+    load_qg<T>(qb, gb, cur, 1, c.l32, c.h);
     seeds(S1, P1, cur, 0, c.h);
     fence();
-    // ---- R2: sub 0, block 1 chains | block 0's softmax VALU (sub 0)
+    // ---- R2
     chains8<T, 0, true>(k, 1, qa, ga, S1, P1, S0, P0, pk, 0);
     fin8_ds<0>(P0, pk, 0);
-    load_qg<T>(qa, ga, cur, 1, c.l32, c.h);
     seeds(S0, P0, cur, 1, c.h);
     fence();
-    // ---- R3: sub 1, block 0 chains | block 1's VALU (sub 0)
-    chains8<T, 0, true>(k, 0, qa, ga, S0, P0, S1, P1, pk, 1);
+    // ---- R3
+    chains8<T, 0, true>(k, 0, qb, gb, S0, P0, S1, P1, pk, 1);
     fin8_ds<0>(P1, pk, 1);
-    seeds(S1, P1, cur, 1, c.h);
-    fence();
-    // ---- R4: sub 1, block 1 chains | block 0's VALU (sub 1)
-    chains8<T, 1, true>(k, 1, qa, ga, S1, P1, S0, P0, pk, 0);
-    fin8_ds<1>(P0, pk, 0);
     const char* f8 = cur + SLOT16;
     const int scw = *(const int*)(f8 + 8192 + c.lane * 4);
     const i32x8 g0 = tile_row8(f8 + 4096, c.l32, c.h), g1 = tile_row8(f8 + 4096, 32 + c.l32, c.h);
     const i32x8 q0 = tile_row8(f8, c.l32, c.h), q1 = tile_row8(f8, 32 + c.l32, c.h);
+    seeds(S1, P1, cur, 1, c.h);
     fence();
-    // ---- R5: block 0's dV / dK (fp8) | block 1's VALU (sub 1)
+    // ---- R4
+    chains8<T, 1, true>(k, 1, qb, gb, S1, P1, S0, P0, pk, 0);
+    fin8_ds<1>(P0, pk, 0);
+    fence();
+    // ---- R5
     const int sd0 = 127 - (c.h ? pk.e[0][1] : pk.e[0][0]);
     mfma8_acc<0>(k.dv[0][0], g0, scw, pk.p[0], E8M0_P);
     fin8_chunk(S1, P1, 0);
@@ -697,13 +724,13 @@ __device__ __forceinline__ void step8(Dkv8Ctx<T>& x, K6<T>& k, int t, typename M
     fence();
     mfma8_acc<3>(k.dk[0][1], q1, scw, pk.d[0], sd0);
     const int sd1 = 127 - (c.h ? pk.e[1][1] : pk.e[1][0]);
+    load_qg<T>(qa, ga, nxt, 0, c.l32, c.h);
     fence();
-    // ---- R6: block 1's dV / dK (fp8) | the next slice's sub-0 fragments and seeds
+    // ---- R6
     mfma8_acc<0>(k.dv[1][0], g0, scw, pk.p[1], E8M0_P);
     mfma8_acc<1>(k.dv[1][1], g1, scw, pk.p[1], E8M0_P);
     mfma8_acc<2>(k.dk[1][0], q0, scw, pk.d[1], sd1);
     mfma8_acc<3>(k.dk[1][1], q1, scw, pk.d[1], sd1);
-    load_qg<T>(qa, ga, nxt, 0, c.l32, c.h);
     seeds(S0, P0, nxt, 0, c.h);
     fence();
 }
@@ -774,22 +801,16 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv8_kernel(const T* __restr
     c.rl = make_rsrc(nlse + (int64_t)bh * N, (uint32_t)N * 4);
     c.rd = make_rsrc(ndelta + (int64_t)bh * N, (uint32_t)N * 4);
     x.rf = make_rsrc(f8 + (int64_t)bh * c.nt * F8_IMG, (uint32_t)c.nt * F8_IMG);
+    x.hoff = (uint32_t)(hd * HD * sizeof(T));
     const bool q_wave = c.wave * X::PIECES < 8;
     c.rmine = q_wave ? c.rs : c.rg;
     c.ldmine = q_wave ? c.ldq : c.ldg;
-#pragma unroll
-    for (int i = 0; i < X::PIECES; ++i) {
-        const int piece = c.wave * X::PIECES + i;
-        const int r = (piece & 7) * 8 + (c.lane >> 3);
-        const uint32_t chunk = (uint32_t)(((c.lane & 7) ^ xsw(r)) * 16);
-        c.voff[i] = piece < 8 ? (uint32_t)r * c.ldq + chunk + (uint32_t)(hd * HD * sizeof(T))
-                              : (uint32_t)r * c.ldg + chunk + (uint32_t)(hd * HD * sizeof(T));
-    }
     dkv8_issue<T>(x, 0, 0);
     dkv8_issue<T>(x, c.nt > 1 ? 1 : 0, 1);
     dkv8_issue<T>(x, c.nt > 2 ? 2 : c.nt - 1, 2);
 
-    // query 0 (CLS) folded in on the VALU, as dkdv6 (the accumulators carry 256 P / 256 DsScale dS)
+    // query 0 (CLS) folded in on the VALU, as dkdv6 (the MX scales dequantise the fp8 products exactly,
+    // so the accumulators hold P dO and DsScale dS q' as dkdv6's do)
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
         float spart = 0.f, ppart = 0.f;
@@ -809,8 +830,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv8_kernel(const T* __restr
             for (int g = 0; g < 4; ++g)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    k.dv[kb][db][4 * g + e] = PSC * p0 * (float)g0d[db][g][e];
-                    k.dk[kb][db][4 * g + e] = PSC * ds0 * (float)q0d[db][g][e];
+                    k.dv[kb][db][4 * g + e] = p0 * (float)g0d[db][g][e];
+                    k.dk[kb][db][4 * g + e] = ds0 * (float)q0d[db][g][e];
                 }
 #pragma unroll
         for (int s = 0; s < 4; ++s) frag_ds_scale<T>(k.vf[kb][s]);
@@ -858,8 +879,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv8_kernel(const T* __restr
     for (int kb = 0; kb < 2; ++kb) {
         if (kok[kb]) {
             T* rk = dqkv + ((int64_t)b * N + key[kb]) * ld + C + hd * HD;
-            store_row_t21<T>(rk, k.dk[kb], dk_scale / (DsScale<T>::v * PSC), c.h);
-            store_row_t21<T>(rk + C, k.dv[kb], 1.0f / PSC, c.h);
+            store_row_t21<T>(rk, k.dk[kb], dk_scale / DsScale<T>::v, c.h);
+            store_row_t21<T>(rk + C, k.dv[kb], 1.0f, c.h);
         }
     }
 }
