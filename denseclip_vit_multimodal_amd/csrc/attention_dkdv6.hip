@@ -408,7 +408,9 @@ typedef short s16x2 __attribute__((ext_vector_type(2)));
 
 constexpr int F8_IMG = 8192 + 256;                     // per slice: Q^T8 [64][64 B] | dO^T8 [64][64 B] | 64 scale dwords
 constexpr int SLOT16 = 2 * 8192 + 2 * 256;            // dkdv6's slot: Q | dO | -L | -DsScale delta
-constexpr int SLOT8 = SLOT16 + F8_IMG;
+// LDS: the 16-bit ring at dkdv6's stride (its slot offsets fit the 16-bit DS immediates), then a
+// ring of the fp8 images (addressed from a base of its own, likewise within the immediates)
+constexpr int F8_RING = 4 * SLOT16;
 constexpr float PSC = 256.0f;                          // P enters the MFMA as 256 P
 constexpr int E8M0_P = 127 - 8;                        // its E8M0 scale 2^-8
 
@@ -554,7 +556,8 @@ __device__ __forceinline__ void dkv8_issue(Dkv8Ctx<T>& x, int t, int slot) {
 #if defined(__HIP_DEVICE_COMPILE__)
     typedef Dkv2Ctx<T, 4> X;
     Dkv2Ctx<T, 4>& c = x.c;
-    char* base = c.smem + slot * SLOT8;
+    char* base = c.smem + slot * SLOT16;
+    char* fbase = c.smem + F8_RING + slot * F8_IMG;
     const int ln = lane_opaque();
     const int r0 = 1 + 64 * t;
     const bool ragged = t == c.nt - 1 && c.rem < 64;  // wave-uniform
@@ -562,19 +565,24 @@ __device__ __forceinline__ void dkv8_issue(Dkv8Ctx<T>& x, int t, int slot) {
     const int part = c.wave % 2;
     const bool is_l = c.wave < 2;
     const uint32_t idx = (uint32_t)(part * X::SPW + ln);
+    // piece p = 4 wave + i covers rows r = 8 (p & 7) + ln / 8 of the slice; with those bits
+    // xsw(r) = 4 ((ln >> 4) & 1) | (p & 3), so the lane part (row ln / 8, chunk (ln & 7) ^ 4 ((ln >> 4)
+    // & 1)) is computed once per issue and the piece part is wave-uniform (24-bit multiplies)
+    const uint32_t lrow = (uint32_t)__umul24((unsigned)(ln >> 3), c.ldmine) + x.hoff;
+    const uint32_t lch = (uint32_t)((ln & 7) ^ (((ln >> 4) & 1) << 2));
     uint32_t vo[X::PIECES];
-    bool ok[X::PIECES];
 #pragma unroll
     for (int i = 0; i < X::PIECES; ++i) {
-        const int r = ((c.wave * X::PIECES + i) & 7) * 8 + (ln >> 3);
-        vo[i] = (uint32_t)r * c.ldmine + (uint32_t)(((ln & 7) ^ xsw(r)) * 16) + x.hoff;
-        ok[i] = r < c.rem;
+        const int p = c.wave * X::PIECES + i;
+        vo[i] = lrow + (uint32_t)((p & 7) * 8) * c.ldmine + ((lch ^ (uint32_t)(p & 3)) << 4);
     }
     if (__builtin_expect(ragged, 0)) {
 #pragma unroll
-        for (int i = 0; i < X::PIECES; ++i)
+        for (int i = 0; i < X::PIECES; ++i) {
+            const bool ok = ((c.wave * X::PIECES + i) & 7) * 8 + (ln >> 3) < c.rem;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rmine, LDS_PTR(base + (c.wave * X::PIECES + i) * 1024), 16,
-                                                     ok[i] ? vo[i] + soff : 0xFFFFFFF0u, 0, 0, 0);
+                                                     ok ? vo[i] + soff : 0xFFFFFFF0u, 0, 0, 0);
+        }
         if (ln < X::SPW)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(is_l ? c.rl : c.rd,
                                                      LDS_PTR(base + 16384 + (is_l ? 0 : 256) + part * X::SPW * 4), 4,
@@ -592,11 +600,10 @@ __device__ __forceinline__ void dkv8_issue(Dkv8Ctx<T>& x, int t, int slot) {
     // the fp8 image (always whole: the pack zero-fills a ragged last slice)
     const uint32_t fo = (uint32_t)t * F8_IMG;
     const uint32_t lo = (uint32_t)(c.wave * 2048 + ln * 16);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(x.rf, LDS_PTR(base + SLOT16 + c.wave * 2048), 16, lo, fo, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(x.rf, LDS_PTR(base + SLOT16 + c.wave * 2048 + 1024), 16, lo + 1024, fo, 0,
-                                             0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(x.rf, LDS_PTR(fbase + c.wave * 2048), 16, lo, fo, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(x.rf, LDS_PTR(fbase + c.wave * 2048 + 1024), 16, lo + 1024, fo, 0, 0);
     if (ln < 16)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(x.rf, LDS_PTR(base + SLOT16 + 8192 + c.wave * 64), 4,
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(x.rf, LDS_PTR(fbase + 8192 + c.wave * 64), 4,
                                                  (uint32_t)(8192 + c.wave * 64 + ln * 4), fo, 0, 0);
 #endif
 }
@@ -620,16 +627,19 @@ template <int SUB>
 __device__ __forceinline__ void fin8_packp(const f32x16& S, Pk8& pk, int kb, int g) {
     pk.p[kb][4 * SUB + g] = cvt4_fp8(S[4 * g], S[4 * g + 1], S[4 * g + 2], S[4 * g + 3], 1.0f / PSC);
 }
-// the dS block scale (amax over the sub-slice's 32 queries of this key) and its four dwords
+// the dS block scale (amax over the sub-slice's 32 queries of this key) and its four dwords.  The
+// exponent is e = 8 - frexp_exp(amax): the block maps into [128, 256) of e4m3's range, which keeps
+// every value normal and costs 3 instructions (v_frexp_exp, v_sub, v_ldexp) instead of mx_e's
+// "largest e" search — e4m3's relative precision is the same at any exponent of its normal range
 template <int SUB>
 __device__ __forceinline__ void fin8_ds(const f32x16& P, Pk8& pk, int kb) {
     float am = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) am = fmaxf(am, fabsf(P[r]));
     am = xhalf_max(am);
-    const int e = mx_e(am);
+    const int e = 8 - __builtin_amdgcn_frexp_expf(am);
     pk.e[kb][SUB] = e;
-    const float inv = pow2f(-e);
+    const float inv = __builtin_amdgcn_ldexpf(1.0f, -e);
 #pragma unroll
     for (int g = 0; g < 4; ++g) pk.d[kb][4 * SUB + g] = cvt4_fp8(P[4 * g], P[4 * g + 1], P[4 * g + 2], P[4 * g + 3], inv);
 }
@@ -672,8 +682,8 @@ __device__ __forceinline__ void step8(Dkv8Ctx<T>& x, K6<T>& k, int t, typename M
     wait_vmcnt<8>();                // own pieces of slice t+1 landed (slice t+2 in flight)
     __builtin_amdgcn_s_barrier();  // everyone's; everyone done with step t-1
     dkv8_issue<T>(x, t + 3 < c.nt ? t + 3 : c.nt - 1, (Q + 3) & 3);
-    const char* cur = c.smem + Q * SLOT8;
-    const char* nxt = c.smem + ((Q + 1) & 3) * SLOT8;
+    const char* cur = c.smem + Q * SLOT16;
+    const char* nxt = c.smem + ((Q + 1) & 3) * SLOT16;
     f32x16 S1, P1;
     frag qb[4], gb[4];
     Pk8 pk;
@@ -691,7 +701,7 @@ __device__ __forceinline__ void step8(Dkv8Ctx<T>& x, K6<T>& k, int t, typename M
     // ---- R3
     chains8<T, 0, true>(k, 0, qb, gb, S0, P0, S1, P1, pk, 1);
     fin8_ds<0>(P1, pk, 1);
-    const char* f8 = cur + SLOT16;
+    const char* f8 = c.smem + F8_RING + Q * F8_IMG;
     const int scw = *(const int*)(f8 + 8192 + c.lane * 4);
     const i32x8 g0 = tile_row8(f8 + 4096, c.l32, c.h), g1 = tile_row8(f8 + 4096, 32 + c.l32, c.h);
     const i32x8 q0 = tile_row8(f8, c.l32, c.h), q1 = tile_row8(f8, 32 + c.l32, c.h);
@@ -746,7 +756,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv8_kernel(const T* __restr
     constexpr int NW = 4, KB = 64 * NW;
     typedef Dkv2Ctx<T, NW> X;
     typedef typename Mfma<T>::frag frag;
-    __shared__ __attribute__((aligned(16))) char smem[4 * SLOT8 + KB * 4];
+    __shared__ __attribute__((aligned(16))) char smem[F8_RING + 4 * F8_IMG + KB * 4];
     Dkv8Ctx<T> x;
     X& c = x.c;
     K6<T> k;
@@ -823,7 +833,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv8_kernel(const T* __restr
             }
         const float p0 = __builtin_amdgcn_exp2f(xhalf_sum(spart) - L0);
         const float ds0 = p0 * (xhalf_sum(ppart) - d0) * DsScale<T>::v;
-        ((float*)(smem + 4 * SLOT8))[c.wave * 64 + kb * 32 + c.l32] = kok[kb] ? ds0 : 0.f;
+        ((float*)(smem + F8_RING + 4 * F8_IMG))[c.wave * 64 + kb * 32 + c.l32] = kok[kb] ? ds0 : 0.f;
 #pragma unroll
         for (int db = 0; db < 2; ++db)
 #pragma unroll
@@ -860,7 +870,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv8_kernel(const T* __restr
         char* img = smem + c.wave * 64 * 128;
         r0_put<T>(img, k.kf[0], lane & 31, lane >> 5);
         r0_put<T>(img, k.kf[1], 32 + (lane & 31), lane >> 5);
-        const float aq = r0_colsum<T, 64>(img, (const float*)(smem + 4 * SLOT8) + c.wave * 64, lane);
+        const float aq = r0_colsum<T, 64>(img, (const float*)(smem + F8_RING + 4 * F8_IMG) + c.wave * 64, lane);
         float* part = (float*)(smem + NW * 64 * 128);
         part[c.wave * 64 + lane] = aq;
         __syncthreads();
