@@ -439,9 +439,11 @@ def attn_fwd_fp8(qkv, B, Ntok, H):
     return o, lse
 
 
-# configs[4]: the backward of an fp8-forward block runs its dK / dV pass on the block-scaled e4m3
-# MFMA too (dclip_attn_bwd_fp8); False keeps the 16-bit backward (round 5's fp8 line)
-ATTN_BWD_FP8 = True
+# configs[4]: True runs the backward of an fp8-forward block with its dK / dV pass on the block-scaled
+# e4m3 MFMA too (dclip_attn_bwd_fp8).  Off by default: measured no faster than the 16-bit pass (dkdv8
+# 2.88 vs dkdv6 2.84 ms per launch + a 50 us pack, profiles/r06/r6f) — that loop is issue-bound on the
+# per-element softmax VALU, not on the MFMA cycles the e4m3 products save
+ATTN_BWD_FP8 = False
 
 
 def attn_bwd(qkv, o, dout, lse, B, Ntok, H, scale, fp8=False):

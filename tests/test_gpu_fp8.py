@@ -420,16 +420,20 @@ def test_fp8_model_backbone_gradients_fp8_backward():
     from helpers import CITYSCAPES_CFG, CITYSCAPES_CLASSES, spec_state_dict, images
     from oracle import denseclip_oracle as O
     from denseclip_vit_multimodal_amd import DenseCLIP, ops
-    assert ops.ATTN_BWD_FP8
     m = DenseCLIP(class_names=CITYSCAPES_CLASSES, **CITYSCAPES_CFG)
     m.load_state_dict(spec_state_dict("cityscapes"))
     bb = m.backbone.to(DEV).train()
     bb.attn_fp8 = True
     x = images(1, 256, 512)
-    maps = bb(x.to(DEV).to(torch.bfloat16))
-    gen = torch.Generator().manual_seed(5)
-    ws = [torch.randn(mp.shape, generator=gen) for mp in maps]
-    sum((mp.float() * w.to(DEV)).sum() for mp, w in zip(maps, ws)).backward()
+    saved = ops.ATTN_BWD_FP8
+    ops.ATTN_BWD_FP8 = True  # the option (off by default: no faster)
+    try:
+        maps = bb(x.to(DEV).to(torch.bfloat16))
+        gen = torch.Generator().manual_seed(5)
+        ws = [torch.randn(mp.shape, generator=gen) for mp in maps]
+        sum((mp.float() * w.to(DEV)).sum() for mp, w in zip(maps, ws)).backward()
+    finally:
+        ops.ATTN_BWD_FP8 = saved
     sd = {k: v.clone().requires_grad_(True) if k.startswith("backbone.") else v
           for k, v in spec_state_dict("cityscapes").items()}
     ref = O.vit_forward(x, sd, out_indices=list(range(12)))
