@@ -2464,13 +2464,14 @@ bool bwd2_launch(const void* qkv, const void* o, const void* dout, const float* 
     // a ragged N - 1 (partial last query / key blocks, masked tails) in the default passes only
     const bool ragged = (N - 1) % 256 != 0;
     const int bwd_block = dclip_option(DCLIP_OPT_ATTN_BWD_BLOCK);
-    if (ragged && (dclip_option(DCLIP_OPT_ATTN_DQ_WAVES) == 4 || (bwd_block != 0 && bwd_block != 5 && bwd_block != 6)))
+    if (ragged && (dclip_option(DCLIP_OPT_ATTN_DQ_WAVES) == 4 ||
+                   (bwd_block != 0 && bwd_block != 5 && bwd_block != 6 && bwd_block != 7)))
         return false;
     const int nsplit = (N + R0_CHUNK - 1) / R0_CHUNK;
     float* ws0 = delta + (int64_t)B * H * N;
     float* nstat = ws0 + (int64_t)B * H * ((N + 63) / 64) * 192;  // [-lse | -delta], B*H*N each
     const bool dq4 = dclip_option(DCLIP_OPT_ATTN_DQ_WAVES) == 4;
-    if (bwd_block == 0 || bwd_block == 6) {
+    if (bwd_block == 0 || bwd_block == 6 || bwd_block == 7) {
         // default: the CLS row's sums folded into the two passes' epilogues (partials in ws0) and
         // one merge; 64 keys per wave, one wave per SIMD, AGPR dK / dV
         const int nq = (N - 1 + (dq4 ? 127 : 255)) / (dq4 ? 128 : 256), nkb = (N - 1 + 255) / 256;
@@ -2496,6 +2497,9 @@ bool bwd2_launch(const void* qkv, const void* o, const void* dout, const float* 
         if (f8ws != nullptr)  // configs[4]: dV, dK on the block-scaled e4m3 MFMA
             attn_bwd_dkdv8_launch(std::is_same<T, bf16>::value ? DCLIP_BF16 : DCLIP_F16, qkv, dout, lse, delta, nstat,
                                   nstat + (int64_t)B * H * N, dqkv, B, N, H, 1.0f / LOG2E, r0q, f8ws, st);
+        else if (bwd_block == 7)  // the software-pipelined dK/dV pass (bitwise equal)
+            attn_bwd_dkdv7_launch(std::is_same<T, bf16>::value ? DCLIP_BF16 : DCLIP_F16, qkv, dout, lse, delta, nstat,
+                                  nstat + (int64_t)B * H * N, dqkv, B, N, H, 1.0f / LOG2E, r0q, st);
         else
             attn_bwd_dkdv6_launch(std::is_same<T, bf16>::value ? DCLIP_BF16 : DCLIP_F16, qkv, dout, lse, delta, nstat,
                                   nstat + (int64_t)B * H * N, dqkv, B, N, H, 1.0f / LOG2E, r0q, st);

@@ -384,6 +384,322 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv6_kernel(const T* __restr
     }
 }
 
+// ============================================================================ dkdv7: software-pipelined dkdv6
+// attn_bwd_dkdv7_kernel (DCLIP_OPT_ATTN_BWD_BLOCK 7): dkdv6's arithmetic, bit for bit, in a schedule
+// that spreads the softmax VALU over all four MFMA regions of a sub-slice.  dkdv6 puts block 0's
+// VALU (16 exp + 16 mul + 16 converts, ~264 issue cycles) into R2 and block 1's into R3, each beside
+// 8 MFMAs whose gaps hold ~192 issue cycles (MI355X_MICROARCH.md: an MFMA holds the SIMD's vector
+// issue for 8 of its 32 cycles), while R1 and R4 carry none — so R2 / R3 overrun and R1 / R4 idle
+// the VALU.  Here the VALU of a block is split into its P half (exp + P convert, "chunkP") and its
+// dS half (multiply + dS convert, "chunkD"), and the sub-slices are software-pipelined, one period
+// per sub-slice j:
+//   X  S / dP chains block 1 (j)       | P 4..7 + D 0..3 of block 0 (j); j's transposed fragments
+//   Y  dV / dK block 0 (j)       (asm) | D 4..7 of block 0, P 0..4 of block 1 (j); j+1's Q / dO
+//                                        fragments and block-0 seeds
+//   Z  S / dP chains block 0 (j+1)     | P 5..7 + D 0..7 of block 1 (j)
+//   W  dV / dK block 1 (j)       (asm) | P 0..3 of block 0 (j+1); j+1's block-1 seeds; the ring's DMA
+//                                        issue (once per step, in a region with VALU slack)
+// ~130-200 issue cycles per region instead of 80 / 264 / 296 / 16.
+template <typename T>
+__device__ __forceinline__ void chunkP7(f32x16& S, Packs& pk, int i) {  // elements 2i, 2i+1: P = exp2(S), kept in S
+    typedef T t2 __attribute__((ext_vector_type(2)));
+    const float e0 = __builtin_amdgcn_exp2f(S[2 * i]);
+    const float e1 = __builtin_amdgcn_exp2f(S[2 * i + 1]);
+    S[2 * i] = e0;
+    S[2 * i + 1] = e1;
+    const t2 pp = {(T)e0, (T)e1};
+    pk.p[i >> 2][i & 3] = __builtin_bit_cast(unsigned, pp);
+}
+template <typename T>
+__device__ __forceinline__ void chunkD7(const f32x16& S, const f32x16& P, Packs& pk, int i) {  // dS = P dP'
+    typedef T t2 __attribute__((ext_vector_type(2)));
+    const float d0 = S[2 * i] * P[2 * i], d1 = S[2 * i + 1] * P[2 * i + 1];
+    const t2 dd = {(T)d0, (T)d1};
+    pk.d[i >> 2][i & 3] = __builtin_bit_cast(unsigned, dd);
+}
+
+// one sub-slice period (above).  In: qa / ga hold j's fragments, S0 / P0 = block 0's chains of j
+// with its P chunks 0..3 done (k0.p[0]), S1 / P1 seeded for j.  Out: the same for j + 1 (at cn, sn).
+template <typename T, bool ISSUE>
+__device__ __forceinline__ void period7(Dkv2Ctx<T, 4>& c, K6<T>& k, int t_issue, int slot_issue, const char* cj,
+                                        int sj, const char* cn, int sn, typename Mfma<T>::frag (&qa)[4],
+                                        typename Mfma<T>::frag (&ga)[4], f32x16& S0, f32x16& P0, f32x16& S1,
+                                        f32x16& P1, Packs& k0, Packs& k1) {
+    typedef typename Mfma<T>::frag frag;
+    frag gt[2][2], qt[2][2];
+    // ---- X
+    fence();
+    load_t<T>(gt, qt, cj, sj, c.lane);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        S1 = Mfma<T>::mma(qa[s], k.kf[1][s], S1);
+        chunkP7<T>(S0, k0, 4 + s);
+        fence();
+        P1 = Mfma<T>::mma(ga[s], k.vf[1][s], P1);
+        chunkD7<T>(S0, P0, k0, s);
+        fence();
+    }
+    // ---- Y
+    load_qg<T>(qa, ga, cn, sn, c.l32, c.h);
+    mfma_acc<T, true>(k.dv[0][0], gt[0][0], as_frag<T>(k0.p[0]));
+    chunkD7<T>(S0, P0, k0, 4);
+    chunkD7<T>(S0, P0, k0, 5);
+    fence();
+    mfma_acc<T, false>(k.dv[0][1], gt[0][1], as_frag<T>(k0.p[0]));
+    chunkP7<T>(S1, k1, 0);
+    fence();
+    mfma_acc<T, false>(k.dv[0][0], gt[1][0], as_frag<T>(k0.p[1]));
+    chunkD7<T>(S0, P0, k0, 6);
+    chunkD7<T>(S0, P0, k0, 7);
+    fence();
+    mfma_acc<T, false>(k.dv[0][1], gt[1][1], as_frag<T>(k0.p[1]));
+    chunkP7<T>(S1, k1, 1);
+    fence();
+    mfma_acc<T, false>(k.dk[0][0], qt[0][0], as_frag<T>(k0.d[0]));
+    chunkP7<T>(S1, k1, 2);
+    fence();
+    mfma_acc<T, false>(k.dk[0][1], qt[0][1], as_frag<T>(k0.d[0]));
+    chunkP7<T>(S1, k1, 3);
+    fence();
+    mfma_acc<T, false>(k.dk[0][0], qt[1][0], as_frag<T>(k0.d[1]));
+    chunkP7<T>(S1, k1, 4);
+    seeds(S0, P0, cn, sn, c.h);
+    fence();
+    mfma_acc<T, false>(k.dk[0][1], qt[1][1], as_frag<T>(k0.d[1]));
+    fence();
+    // ---- Z
+    S0 = Mfma<T>::mma(qa[0], k.kf[0][0], S0);
+    chunkP7<T>(S1, k1, 5);
+    chunkD7<T>(S1, P1, k1, 0);
+    fence();
+    P0 = Mfma<T>::mma(ga[0], k.vf[0][0], P0);
+    chunkP7<T>(S1, k1, 6);
+    chunkD7<T>(S1, P1, k1, 1);
+    fence();
+    S0 = Mfma<T>::mma(qa[1], k.kf[0][1], S0);
+    chunkP7<T>(S1, k1, 7);
+    chunkD7<T>(S1, P1, k1, 2);
+    fence();
+    P0 = Mfma<T>::mma(ga[1], k.vf[0][1], P0);
+    chunkD7<T>(S1, P1, k1, 3);
+    fence();
+    S0 = Mfma<T>::mma(qa[2], k.kf[0][2], S0);
+    chunkD7<T>(S1, P1, k1, 4);
+    fence();
+    P0 = Mfma<T>::mma(ga[2], k.vf[0][2], P0);
+    chunkD7<T>(S1, P1, k1, 5);
+    fence();
+    S0 = Mfma<T>::mma(qa[3], k.kf[0][3], S0);
+    chunkD7<T>(S1, P1, k1, 6);
+    fence();
+    P0 = Mfma<T>::mma(ga[3], k.vf[0][3], P0);
+    chunkD7<T>(S1, P1, k1, 7);
+    fence();
+    // ---- W
+    if constexpr (ISSUE) dkv2_issue<T, 4>(c, t_issue, slot_issue);
+    mfma_acc<T, true>(k.dv[1][0], gt[0][0], as_frag<T>(k1.p[0]));
+    chunkP7<T>(S0, k0, 0);
+    fence();
+    mfma_acc<T, false>(k.dv[1][1], gt[0][1], as_frag<T>(k1.p[0]));
+    chunkP7<T>(S0, k0, 1);
+    fence();
+    mfma_acc<T, false>(k.dv[1][0], gt[1][0], as_frag<T>(k1.p[1]));
+    chunkP7<T>(S0, k0, 2);
+    fence();
+    mfma_acc<T, false>(k.dv[1][1], gt[1][1], as_frag<T>(k1.p[1]));
+    chunkP7<T>(S0, k0, 3);
+    fence();
+    mfma_acc<T, false>(k.dk[1][0], qt[0][0], as_frag<T>(k1.d[0]));
+    mfma_acc<T, false>(k.dk[1][1], qt[0][1], as_frag<T>(k1.d[0]));
+    mfma_acc<T, false>(k.dk[1][0], qt[1][0], as_frag<T>(k1.d[1]));
+    mfma_acc<T, false>(k.dk[1][1], qt[1][1], as_frag<T>(k1.d[1]));
+    seeds(S1, P1, cn, sn, c.h);
+    fence();
+}
+
+// one 64-query slice t (slot Q): the ring's wait + barrier, then its two sub-slice periods; the
+// second one's Z region already runs the next slice's first block-0 chains (slot Q + 1, landed by
+// this step's wait), and the DMA of slice t + 3 is issued in the first period's W
+template <typename T, int Q>
+__device__ __forceinline__ void step7(Dkv2Ctx<T, 4>& c, K6<T>& k, int t, typename Mfma<T>::frag (&qa)[4],
+                                      typename Mfma<T>::frag (&ga)[4], f32x16& S0, f32x16& P0, f32x16& S1,
+                                      f32x16& P1, Packs& k0, Packs& k1) {
+    typedef Dkv2Ctx<T, 4> X;
+    wait_vmcnt<X::PIECES + 1>();    // own pieces of slice t+1 landed (slice t+2 in flight)
+    __builtin_amdgcn_s_barrier();  // everyone's; everyone done with slice t-1's slot
+    const char* cur = c.smem + Q * X::SLOT;
+    const char* nxt = c.smem + ((Q + 1) & 3) * X::SLOT;
+    period7<T, true>(c, k, t + 3 < c.nt ? t + 3 : c.nt - 1, (Q + 3) & 3, cur, 0, cur, 1, qa, ga, S0, P0, S1, P1,
+                     k0, k1);
+    period7<T, false>(c, k, 0, 0, cur, 1, nxt, 0, qa, ga, S0, P0, S1, P1, k0, k1);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv7_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
+                                                                const float* __restrict__ lse,
+                                                                const float* __restrict__ delta,
+                                                                const float* __restrict__ nlse,
+                                                                const float* __restrict__ ndelta,
+                                                                T* __restrict__ dqkv, int N, int H, float dk_scale,
+                                                                float* __restrict__ r0q) {
+    constexpr int NW = 4, KB = 64 * NW;
+    typedef Dkv2Ctx<T, NW> X;
+    typedef typename Mfma<T>::frag frag;
+    __shared__ __attribute__((aligned(16))) char smem[4 * X::SLOT + KB * 4];
+    X c;
+    K6<T> k;
+    c.smem = smem;
+    c.lane = threadIdx.x & 63;
+    c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    c.h = c.lane >> 5;
+    c.l32 = c.lane & 31;
+    const int nkb = (N - 1 + KB - 1) / KB;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int kblk = tile % nkb, bh = tile / nkb, b = bh / H, hd = bh % H;
+    const int C = H * HD;
+    const int64_t ld = 3 * (int64_t)C;
+    const T* Bb = qkv + (int64_t)b * N * ld;
+    const T* dOb = dout + (int64_t)b * N * C;
+    c.ldq = (uint32_t)(ld * sizeof(T));
+    c.ldg = (uint32_t)(C * sizeof(T));
+    c.nt = (N - 1 + 63) / 64;
+    c.rem = N - 1 - 64 * (c.nt - 1);
+    int key[2];
+    bool kok[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+        key[kb] = 1 + kblk * KB + c.wave * 64 + kb * 32 + c.l32;
+        kok[kb] = key[kb] < N;
+        const int kc = kok[kb] ? key[kb] : N - 1;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            k.kf[kb][s] = *(const frag*)(Bb + (int64_t)kc * ld + C + hd * HD + (2 * s + c.h) * 8);
+            k.vf[kb][s] = *(const frag*)(Bb + (int64_t)kc * ld + 2 * C + hd * HD + (2 * s + c.h) * 8);
+        }
+    }
+    frag q0[4], g0[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        q0[s] = *(const frag*)(Bb + hd * HD + (2 * s + c.h) * 8);
+        g0[s] = *(const frag*)(dOb + hd * HD + (2 * s + c.h) * 8);
+    }
+    typedef T t4 __attribute__((ext_vector_type(4)));
+    t4 q0d[2][4], g0d[2][4];
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            q0d[db][g] = *(const t4*)(Bb + hd * HD + db * 32 + 8 * g + 4 * c.h);
+            g0d[db][g] = *(const t4*)(dOb + hd * HD + db * 32 + 8 * g + 4 * c.h);
+        }
+    const float L0 = lse[(int64_t)bh * N], d0 = delta[(int64_t)bh * N];
+
+    c.rs = make_rsrc(Bb, (uint32_t)N * c.ldq);
+    c.rg = make_rsrc(dOb, (uint32_t)N * c.ldg);
+    c.rl = make_rsrc(nlse + (int64_t)bh * N, (uint32_t)N * 4);
+    c.rd = make_rsrc(ndelta + (int64_t)bh * N, (uint32_t)N * 4);
+    const bool q_wave = c.wave * X::PIECES < 8;
+    c.rmine = q_wave ? c.rs : c.rg;
+    c.ldmine = q_wave ? c.ldq : c.ldg;
+#pragma unroll
+    for (int i = 0; i < X::PIECES; ++i) {
+        const int piece = c.wave * X::PIECES + i;
+        const int r = (piece & 7) * 8 + (c.lane >> 3);
+        const uint32_t chunk = (uint32_t)(((c.lane & 7) ^ xsw(r)) * 16);
+        c.voff[i] = piece < 8 ? (uint32_t)r * c.ldq + chunk + (uint32_t)(hd * HD * sizeof(T))
+                              : (uint32_t)r * c.ldg + chunk + (uint32_t)(hd * HD * sizeof(T));
+    }
+    dkv2_issue<T, NW>(c, 0, 0);
+    dkv2_issue<T, NW>(c, c.nt > 1 ? 1 : 0, 1);
+    dkv2_issue<T, NW>(c, c.nt > 2 ? 2 : c.nt - 1, 2);
+
+    // query 0 (CLS) folded in on the VALU (dkdv6)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+        float spart = 0.f, ppart = 0.f;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                spart += (float)q0[s][j] * (float)k.kf[kb][s][j];
+                ppart += (float)g0[s][j] * (float)k.vf[kb][s][j];
+            }
+        const float p0 = __builtin_amdgcn_exp2f(xhalf_sum(spart) - L0);
+        const float ds0 = p0 * (xhalf_sum(ppart) - d0) * DsScale<T>::v;
+        ((float*)(smem + 4 * X::SLOT))[c.wave * 64 + kb * 32 + c.l32] = kok[kb] ? ds0 : 0.f;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    k.dv[kb][db][4 * g + e] = p0 * (float)g0d[db][g][e];
+                    k.dk[kb][db][4 * g + e] = ds0 * (float)q0d[db][g][e];
+                }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) frag_ds_scale<T>(k.vf[kb][s]);
+    }
+
+    wait_vmcnt<2 * (X::PIECES + 1)>();  // slice 0 landed (slices 1, 2 in flight)
+    __builtin_amdgcn_s_barrier();
+    // the pipeline's fill: block 0's chains of sub-slice 0 and their P chunks 0..3
+    frag qa[4], ga[4];
+    f32x16 S0, P0, S1, P1;
+    Packs k0, k1;
+    load_qg<T>(qa, ga, smem, 0, c.l32, c.h);
+    seeds(S0, P0, smem, 0, c.h);
+    fence();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        S0 = Mfma<T>::mma(qa[s], k.kf[0][s], S0);
+        P0 = Mfma<T>::mma(ga[s], k.vf[0][s], P0);
+    }
+    seeds(S1, P1, smem, 0, c.h);
+    fence();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) chunkP7<T>(S0, k0, i);
+    fence();
+    int t = 0;  // unrolled by four, then up to three single steps (slot immediates)
+    for (; t + 4 <= c.nt; t += 4) {
+        step7<T, 0>(c, k, t, qa, ga, S0, P0, S1, P1, k0, k1);
+        step7<T, 1>(c, k, t + 1, qa, ga, S0, P0, S1, P1, k0, k1);
+        step7<T, 2>(c, k, t + 2, qa, ga, S0, P0, S1, P1, k0, k1);
+        step7<T, 3>(c, k, t + 3, qa, ga, S0, P0, S1, P1, k0, k1);
+    }
+    if (t < c.nt) step7<T, 0>(c, k, t++, qa, ga, S0, P0, S1, P1, k0, k1);
+    if (t < c.nt) step7<T, 1>(c, k, t++, qa, ga, S0, P0, S1, P1, k0, k1);
+    if (t < c.nt) step7<T, 2>(c, k, t++, qa, ga, S0, P0, S1, P1, k0, k1);
+    wait_vmcnt<0>();
+    if (r0q != nullptr) {  // the CLS-row fold (dkdv6)
+        __syncthreads();
+        const int lane = __lane_id();
+        char* img = smem + c.wave * 64 * 128;
+        r0_put<T>(img, k.kf[0], lane & 31, lane >> 5);
+        r0_put<T>(img, k.kf[1], 32 + (lane & 31), lane >> 5);
+        const float aq = r0_colsum<T, 64>(img, (const float*)(smem + 4 * X::SLOT) + c.wave * 64, lane);
+        float* part = (float*)(smem + NW * 64 * 128);
+        part[c.wave * 64 + lane] = aq;
+        __syncthreads();
+        if (c.wave == 0) {
+            float sum = 0.f;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) sum += part[w * 64 + lane];
+            r0q[((int64_t)bh * nkb + kblk) * 64 + lane] = sum;
+        }
+    }
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3"
+                 : "+a"(k.dk[0][0]), "+a"(k.dk[0][1]), "+a"(k.dk[1][0]), "+a"(k.dk[1][1]), "+a"(k.dv[0][0]),
+                   "+a"(k.dv[0][1]), "+a"(k.dv[1][0]), "+a"(k.dv[1][1]));
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+        if (kok[kb]) {
+            T* rk = dqkv + ((int64_t)b * N + key[kb]) * ld + C + hd * HD;
+            store_row_t21<T>(rk, k.dk[kb], dk_scale / DsScale<T>::v, c.h);
+            store_row_t21<T>(rk + C, k.dv[kb], 1.0f, c.h);
+        }
+    }
+}
+
 // ============================================================================ fp8 dK / dV (configs[4])
 // attn_bwd_dkdv8_kernel: dkdv6's pass with dV^T += dO^T P and dK^T += Q^T dS on the block-scaled
 // e4m3 MFMA v_mfma_scale_f32_32x32x64_f8f6f4 (twice the bf16 rate: one instruction covers a whole
@@ -896,6 +1212,19 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv8_kernel(const T* __restr
 }
 
 }  // namespace
+
+// the software-pipelined form (DCLIP_OPT_ATTN_BWD_BLOCK 7), same contract as attn_bwd_dkdv6_launch
+void attn_bwd_dkdv7_launch(int dt, const void* qkv, const void* dout, const float* lse, const float* delta,
+                           const float* nlse, const float* ndelta, void* dqkv, int B, int N, int H, float dk_scale,
+                           float* r0q, hipStream_t st) {
+    const int grid = B * H * ((N - 1 + 255) / 256);
+    if (dt == DCLIP_BF16)
+        attn_bwd_dkdv7_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)qkv, (const bf16*)dout, lse, delta, nlse, ndelta,
+                                                          (bf16*)dqkv, N, H, dk_scale, r0q);
+    else
+        attn_bwd_dkdv7_kernel<f16><<<grid, 256, 0, st>>>((const f16*)qkv, (const f16*)dout, lse, delta, nlse, ndelta,
+                                                         (f16*)dqkv, N, H, dk_scale, r0q);
+}
 
 // launched by attention.hip's bwd2_launch (DCLIP_OPT_ATTN_BWD_BLOCK selects it); key 0 is the
 // fold merge's (attn_bwd_row0_fold_merge), which also takes the dQ_0 partials written to r0q

@@ -256,6 +256,10 @@ inline int64_t attn_row0_ws_floats(int B, int N, int H) { return (int64_t)B * H 
 void attn_bwd_dkdv6_launch(int dt, const void* qkv, const void* dout, const float* lse, const float* delta,
                            const float* nlse, const float* ndelta, void* dqkv, int B, int N, int H, float dk_scale,
                            float* r0q, hipStream_t st);
+// the software-pipelined dkdv6 (DCLIP_OPT_ATTN_BWD_BLOCK 7), bitwise equal to it
+void attn_bwd_dkdv7_launch(int dt, const void* qkv, const void* dout, const float* lse, const float* delta,
+                           const float* nlse, const float* ndelta, void* dqkv, int B, int N, int H, float dk_scale,
+                           float* r0q, hipStream_t st);
 // its fp8 form (configs[4]: dV, dK on the block-scaled e4m3 MFMA; attention_dkdv6.hip): the pack of
 // the slices' Q^T / dO^T e4m3 images into f8ws (attn_bwd_fp8_ws_bytes), then the pass
 int64_t attn_bwd_fp8_ws_bytes(int B, int N, int H);

@@ -723,6 +723,27 @@ def test_attention_dkdv6_matches_dkdv5(B, H, N, dt, bwd_block):
         assert max(errs) < 4 * TOL[dt], errs
 
 
+@pytest.mark.parametrize("B,H,N", [(3, 2, 257), (2, 2, 290), (2, 3, 803), (3, 2, 1345), (2, 2, 2049), (1, 2, 8193),
+                                   (1, 1, 10659)])
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+def test_attention_dkdv7_bitwise_dkdv6(B, H, N, dt, bwd_block):
+    """The software-pipelined dK/dV pass (DCLIP_OPT_ATTN_BWD_BLOCK 7, round 6) runs dkdv6's products in
+    the same per-accumulator order with the softmax VALU re-scheduled across the MFMA regions: the whole
+    dQKV equal BIT FOR BIT to dkdv6's, full and ragged N - 1, partial last key blocks included."""
+    O = ops()
+    C = 64 * H
+    torch.manual_seed(7)
+    qkv, _ = prescale((torch.randn(B * N, 3 * C, device=DEV) * 1.5).to(dt), H)
+    dout = torch.randn(B * N, C, device=DEV).to(dt)
+    o, lse = O.attn_fwd(qkv, B, N, H, 64 ** -0.5)
+    res = []
+    for v in (6, 7):
+        bwd_block(v)
+        res.append(O.attn_bwd(qkv, o, dout, lse, B, N, H, 64 ** -0.5))
+    assert torch.isfinite(res[1].float()).all()
+    assert torch.equal(res[0], res[1])
+
+
 @pytest.mark.parametrize("variant", ["rows64", "defer"])
 @pytest.mark.parametrize("B,H,N", [(3, 2, 257), (2, 2, 290), (2, 3, 803), (1, 2, 8193)])
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
