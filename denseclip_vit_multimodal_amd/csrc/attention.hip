@@ -2465,13 +2465,13 @@ bool bwd2_launch(const void* qkv, const void* o, const void* dout, const float* 
     const bool ragged = (N - 1) % 256 != 0;
     const int bwd_block = dclip_option(DCLIP_OPT_ATTN_BWD_BLOCK);
     if (ragged && (dclip_option(DCLIP_OPT_ATTN_DQ_WAVES) == 4 ||
-                   (bwd_block != 0 && bwd_block != 5 && bwd_block != 6 && bwd_block != 7)))
+                   (bwd_block != 0 && bwd_block != 5 && bwd_block != 6 && bwd_block != 7 && bwd_block != 8)))
         return false;
     const int nsplit = (N + R0_CHUNK - 1) / R0_CHUNK;
     float* ws0 = delta + (int64_t)B * H * N;
     float* nstat = ws0 + (int64_t)B * H * ((N + 63) / 64) * 192;  // [-lse | -delta], B*H*N each
     const bool dq4 = dclip_option(DCLIP_OPT_ATTN_DQ_WAVES) == 4;
-    if (bwd_block == 0 || bwd_block == 6 || bwd_block == 7) {
+    if (bwd_block == 0 || bwd_block == 6 || bwd_block == 7 || bwd_block == 8) {
         // default: the CLS row's sums folded into the two passes' epilogues (partials in ws0) and
         // one merge; 64 keys per wave, one wave per SIMD, AGPR dK / dV
         const int nq = (N - 1 + (dq4 ? 127 : 255)) / (dq4 ? 128 : 256), nkb = (N - 1 + 255) / 256;

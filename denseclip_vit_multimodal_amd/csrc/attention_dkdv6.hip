@@ -144,10 +144,12 @@ __device__ __forceinline__ void fin_chunk(f32x16& S, f32x16& P, Packs& pk, int i
 //   R4  dV / dK of block 1 (asm, AGPR)        (8)   | loads: next block-0 seeds
 // S0 / P0 arrive seeded and qa / ga hold this sub-slice; both leave holding the next one (`nb`,
 // `nsub`: the next sub-slice's slot and index)
-template <typename T>
+// ISSUE (DCLIP_OPT_ATTN_BWD_BLOCK 8, round 6): the step's ring DMA is issued at the start of R4 (8
+// bare asm MFMAs) instead of before R1
+template <typename T, bool ISSUE = false>
 __device__ __forceinline__ void sub6(K6<T>& k, int h, int l32, int lane, const char* base, int sub, const char* nb,
                                      int nsub, typename Mfma<T>::frag (&qa)[4], typename Mfma<T>::frag (&ga)[4],
-                                     f32x16& S0, f32x16& P0) {
+                                     f32x16& S0, f32x16& P0, Dkv2Ctx<T, 4>* ic = nullptr, int it = 0, int islot = 0) {
     typedef typename Mfma<T>::frag frag;
     f32x16 S1, P1;
     frag gt[2][2], qt[2][2];
@@ -191,6 +193,7 @@ __device__ __forceinline__ void sub6(K6<T>& k, int h, int l32, int lane, const c
     load_qg<T>(qa, ga, nb, nsub, l32, h);
     fence();
     // ---- R4
+    if constexpr (ISSUE) dkv2_issue<T, 4>(*ic, it, islot);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
         mfma_acc<T, true>(k.dv[1][0], gt[s][0], as_frag<T>(k1.p[s]));
@@ -204,7 +207,7 @@ __device__ __forceinline__ void sub6(K6<T>& k, int h, int l32, int lane, const c
 
 // one 64-query slice (two sub-slices), read one slice ahead as in attn_bwd_dkdv5_kernel: S0 / P0
 // and qa / ga arrive holding (this slice, sub 0) and leave holding (next slice, sub 0)
-template <typename T, int Q>
+template <typename T, int Q, bool LATE = false>
 __device__ __forceinline__ void step6(Dkv2Ctx<T, 4>& c, K6<T>& k, int t, typename Mfma<T>::frag (&qa)[4],
                                       typename Mfma<T>::frag (&ga)[4], f32x16& S0, f32x16& P0) {
     typedef Dkv2Ctx<T, 4> X;
@@ -216,14 +219,15 @@ __device__ __forceinline__ void step6(Dkv2Ctx<T, 4>& c, K6<T>& k, int t, typenam
 #ifndef DCLIP_DIAG_NOBAR
     __builtin_amdgcn_s_barrier();  // everyone's; everyone done with step t-1 (slot (t+3) % 4 free)
 #endif
-    dkv2_issue<T, 4>(c, t + 3 < c.nt ? t + 3 : c.nt - 1, (Q + 3) & 3);
+    if constexpr (!LATE) dkv2_issue<T, 4>(c, t + 3 < c.nt ? t + 3 : c.nt - 1, (Q + 3) & 3);
     const char* cur = c.smem + Q * X::SLOT;
     const char* nxt = c.smem + ((Q + 1) & 3) * X::SLOT;
-    sub6<T>(k, c.h, c.l32, c.lane, cur, 0, cur, 1, qa, ga, S0, P0);
+    sub6<T, LATE>(k, c.h, c.l32, c.lane, cur, 0, cur, 1, qa, ga, S0, P0, &c, t + 3 < c.nt ? t + 3 : c.nt - 1,
+                  (Q + 3) & 3);
     sub6<T>(k, c.h, c.l32, c.lane, cur, 1, nxt, 0, qa, ga, S0, P0);
 }
 
-template <typename T>
+template <typename T, bool LATE = false>
 __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv6_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
                                                                 const float* __restrict__ lse,
                                                                 const float* __restrict__ delta,
@@ -340,14 +344,14 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv6_kernel(const T* __restr
     seeds(S0, P0, smem, 0, c.h);
     int t = 0;  // unrolled by four, then up to three single steps (see attn_bwd_dq2_kernel)
     for (; t + 4 <= c.nt; t += 4) {
-        step6<T, 0>(c, k, t, qa, ga, S0, P0);
-        step6<T, 1>(c, k, t + 1, qa, ga, S0, P0);
-        step6<T, 2>(c, k, t + 2, qa, ga, S0, P0);
-        step6<T, 3>(c, k, t + 3, qa, ga, S0, P0);
+        step6<T, 0, LATE>(c, k, t, qa, ga, S0, P0);
+        step6<T, 1, LATE>(c, k, t + 1, qa, ga, S0, P0);
+        step6<T, 2, LATE>(c, k, t + 2, qa, ga, S0, P0);
+        step6<T, 3, LATE>(c, k, t + 3, qa, ga, S0, P0);
     }
-    if (t < c.nt) step6<T, 0>(c, k, t++, qa, ga, S0, P0);
-    if (t < c.nt) step6<T, 1>(c, k, t++, qa, ga, S0, P0);
-    if (t < c.nt) step6<T, 2>(c, k, t++, qa, ga, S0, P0);
+    if (t < c.nt) step6<T, 0, LATE>(c, k, t++, qa, ga, S0, P0);
+    if (t < c.nt) step6<T, 1, LATE>(c, k, t++, qa, ga, S0, P0);
+    if (t < c.nt) step6<T, 2, LATE>(c, k, t++, qa, ga, S0, P0);
     wait_vmcnt<0>();
     if (r0q != nullptr) {
         // CLS-row fold: this block's share of query 0's dQ_0 += dS_0 k (DsScale-scaled), one
@@ -1232,12 +1236,18 @@ void attn_bwd_dkdv6_launch(int dt, const void* qkv, const void* dout, const floa
                            const float* nlse, const float* ndelta, void* dqkv, int B, int N, int H, float dk_scale,
                            float* r0q, hipStream_t st) {
     const int grid = B * H * ((N - 1 + 255) / 256);
-    if (dt == DCLIP_BF16)
-        attn_bwd_dkdv6_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)qkv, (const bf16*)dout, lse, delta, nlse, ndelta,
-                                                          (bf16*)dqkv, N, H, dk_scale, r0q);
-    else
-        attn_bwd_dkdv6_kernel<f16><<<grid, 256, 0, st>>>((const f16*)qkv, (const f16*)dout, lse, delta, nlse, ndelta,
-                                                         (f16*)dqkv, N, H, dk_scale, r0q);
+    const bool late = dclip_option(DCLIP_OPT_ATTN_BWD_BLOCK) == 8;  // the DMA issue inside R4
+#define DKDV6(TT, L)                                                                                           \
+    attn_bwd_dkdv6_kernel<TT, L><<<grid, 256, 0, st>>>((const TT*)qkv, (const TT*)dout, lse, delta, nlse, ndelta, \
+                                                       (TT*)dqkv, N, H, dk_scale, r0q)
+    if (dt == DCLIP_BF16) {
+        if (late) DKDV6(bf16, true);
+        else DKDV6(bf16, false);
+    } else {
+        if (late) DKDV6(f16, true);
+        else DKDV6(f16, false);
+    }
+#undef DKDV6
 }
 
 // the fp8 dK / dV pass (configs[4]): the pack of the slices' Q^T / dO^T e4m3 images into f8ws

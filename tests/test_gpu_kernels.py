@@ -737,11 +737,11 @@ def test_attention_dkdv7_bitwise_dkdv6(B, H, N, dt, bwd_block):
     dout = torch.randn(B * N, C, device=DEV).to(dt)
     o, lse = O.attn_fwd(qkv, B, N, H, 64 ** -0.5)
     res = []
-    for v in (6, 7):
+    for v in (6, 7, 8):  # 8: dkdv6 with the ring's DMA issued inside R4
         bwd_block(v)
         res.append(O.attn_bwd(qkv, o, dout, lse, B, N, H, 64 ** -0.5))
     assert torch.isfinite(res[1].float()).all()
-    assert torch.equal(res[0], res[1])
+    assert torch.equal(res[0], res[1]) and torch.equal(res[0], res[2])
 
 
 @pytest.mark.parametrize("variant", ["rows64", "defer"])
