@@ -2465,12 +2465,30 @@ bool bwd2_launch(const void* qkv, const void* o, const void* dout, const float* 
     const bool ragged = (N - 1) % 256 != 0;
     const int bwd_block = dclip_option(DCLIP_OPT_ATTN_BWD_BLOCK);
     if (ragged && (dclip_option(DCLIP_OPT_ATTN_DQ_WAVES) == 4 ||
-                   (bwd_block != 0 && bwd_block != 5 && bwd_block != 6 && bwd_block != 7 && bwd_block != 8)))
+                   (bwd_block != 0 && bwd_block != 5 && bwd_block != 6 && bwd_block != 7 && bwd_block != 8 &&
+                    bwd_block != 9)))
         return false;
     const int nsplit = (N + R0_CHUNK - 1) / R0_CHUNK;
     float* ws0 = delta + (int64_t)B * H * N;
     float* nstat = ws0 + (int64_t)B * H * ((N + 63) / 64) * 192;  // [-lse | -delta], B*H*N each
     const bool dq4 = dclip_option(DCLIP_OPT_ATTN_DQ_WAVES) == 4;
+    if (bwd_block == 9 && f8ws == nullptr) {
+        // the one-pass backward (attention_bwd1.hip): prep (delta, statistics, key 0's terms), one
+        // key-major sweep for dK, dV and per-key-block dQ partials, the ordered dQ reduction; then
+        // the CLS row's merge as the two-pass path.  Workspace past the two-pass part: dS_q0 (B*H*N
+        // floats), then the partials (attn_bwd1_part_bytes, 256-B aligned)
+        const int64_t bhn = (int64_t)B * H * N;
+        float* ds0v = nstat + 2 * bhn;
+        void* part = (void*)(((uintptr_t)(ds0v + bhn) + 255) & ~(uintptr_t)255);
+        const int nqp = attn_bwd1_prep_blocks(N), nkb = (N - 1 + 255) / 256;
+        float* r0kv = ws0;
+        float* r0q = ws0 + (int64_t)B * H * nqp * 128;
+        attn_bwd1_launch(std::is_same<T, bf16>::value ? DCLIP_BF16 : DCLIP_F16, qkv, o, dout, lse, delta, nstat, ds0v,
+                         r0kv, r0q, part, dqkv, B, N, H, scale, st);
+        attn_bwd_row0_fold_merge<T><<<B * H, 64, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, r0kv, nqp, r0q, nkb,
+                                                          (T*)dqkv, N, H, scale, 1.0f / LOG2E);
+        return true;
+    }
     if (bwd_block == 0 || bwd_block == 6 || bwd_block == 7 || bwd_block == 8) {
         // default: the CLS row's sums folded into the two passes' epilogues (partials in ws0) and
         // one merge; 64 keys per wave, one wave per SIMD, AGPR dK / dV
@@ -2597,7 +2615,11 @@ extern "C" int dclip_attn_fwd(int dt, const void* qkv, void* o, float* lse, int 
 extern "C" int64_t dclip_attn_bwd_workspace(int B, int N, int H) {
     // delta (B*H*N) + the CLS-split row-0 partials (B*H*ceil(N/64)*192) + the negated
     // statistics the CLS-split dK/dV pass reads (-lse, -delta: 2*B*H*N)
-    return 3 * (int64_t)B * H * N + (int64_t)B * H * ((N + 63) / 64) * 192;
+    const int64_t two_pass = 3 * (int64_t)B * H * N + (int64_t)B * H * ((N + 63) / 64) * 192;
+    // the one-pass backward (DCLIP_OPT_ATTN_BWD_BLOCK 9): + dS_q0 (B*H*N) + the dQ partials
+    if (dclip_option(DCLIP_OPT_ATTN_BWD_BLOCK) == 9 && N >= 257)
+        return two_pass + (int64_t)B * H * N + (attn_bwd1_part_bytes(B, N, H) + 3) / 4 + 64;
+    return two_pass;
 }
 
 extern "C" int dclip_attn_bwd(int dt, const void* qkv, const void* o, const void* dout, const float* lse,

@@ -1,0 +1,556 @@
+// One-pass CLS-split attention backward (DCLIP_OPT_ATTN_BWD_BLOCK 9): dK, dV AND dQ from a single
+// key-major sweep, so every P / dS element is recomputed once (two-pass: twice) and the MFMA work is
+// 5 units (S, dP, dV, dK, dQ) instead of 7 (dQ pass: S, dP, dQ; dK/dV pass: S, dP, dV, dK).
+//
+// Replaces the backward of nn.MultiheadAttention's softmax(q k^T d^-0.5) v (reference
+// seg/denseclip/models.py:275, 287-289) with the arithmetic of the two-pass path
+// (attention.hip::attn_bwd_dq2_kernel + attention_dkdv6.hip::attn_bwd_dkdv6_kernel):
+//   P = exp2(S - L) (log2-domain lse), dS = P (dP - delta), dV = P^T dO, dK = dS^T q', dQ = dS K.
+//
+// Launch sequence (attn_bwd1_launch, then attention.hip's attn_bwd_row0_fold_merge):
+//   1. attn_bwd1_prep_kernel   per query: delta = rowsum(dO o O), the negated statistics the sweep
+//                              seeds its S / dP chains with, key 0's dS_q0 (kept for step 3) and the
+//                              key-0 column sums dK_0 / dV_0 as per-block partials (the CLS-row fold's
+//                              r0kv) — the prologue / epilogue work of the dQ pass, in the same
+//                              arithmetic (so dK / dV of keys 1.. equal the two-pass result bit for bit)
+//   2. attn_bwd1_kernel        the sweep: dkdv6's key-major loop (4 waves x 64 keys, one wave per
+//                              SIMD, AGPR dK / dV, Q / dO / statistics slices by LDS-DMA into a 4-slot
+//                              ring) plus, per 64-query slice, the slice's dS^T written to an LDS image
+//                              and one 32 x 32 dQ^T tile per wave summed over the workgroup's 256 keys
+//                              on the MFMA (K^T from a resident LDS image of the block's keys) —
+//                              stored as a 16-bit partial per (key block, query)
+//   3. attn_bwd1_dq_reduce     dQ[q] = sum over key blocks of the partials, in block order, + the key-0
+//                              term dS_q0 k_0 — deterministic, no atomics
+//
+// The dS^T image is [256 keys][64 queries] 16-bit with an 8-byte-unit XOR swizzle
+// (ds_unit_swz): conflict-free for both its writers (ds_write_b64 of 4 consecutive queries of one
+// key per lane, 16 keys per lane group) and its transposing readers (ds_read_b64_tr_b16).
+#include "dkdv_frag.h"
+
+namespace {
+
+constexpr int B1_NW = 4, B1_KB = 64 * B1_NW;  // waves, keys per workgroup
+typedef Dkv2Ctx<bf16, B1_NW> B1Ring;           // the ring geometry (SLOT, PIECES) is type-independent
+constexpr int B1_RING = 4 * B1Ring::SLOT;
+constexpr int B1_W0 = B1_RING;                 // the CLS-row fold's per-key weights dS_0 (KB floats)
+constexpr int B1_KIMG = B1_W0 + B1_KB * 4;     // K image [256 keys][64 d], swz layout
+constexpr int B1_DSIMG = B1_KIMG + B1_KB * 128;  // dS^T image [256 keys][64 queries], ds_unit_swz
+constexpr int B1_SMEM = B1_DSIMG + B1_KB * 128;
+static_assert(B1_KIMG % 128 == 0 && B1_DSIMG % 128 == 0, "images on 128-B rows");
+static_assert(B1_SMEM <= 160 * 1024, "LDS");
+
+// 8-byte unit XOR of row r in the dS^T image: a bijection of r & 15 (16 keys of one ds_write_b64
+// lane group hit 16 distinct units), with bit 3 flipped on r bit 1 (the transposing read's four rows
+// 4h + q land in four distinct 64-B bank quarters)
+__device__ __forceinline__ int ds_unit_swz(int row) { return (row & 15) ^ (((row >> 1) & 1) << 3); }
+
+// transposing read of the dS^T image (the B operand of dQ^T += K^T dS^T): element j of half h is
+// key rb*32 + 16s + 8(j>>2) + 4h + (j&3) — tr_frag's k-order, so it pairs with tr_frag(K image) —
+// and MFMA column (lane & 31) is query qb*32 + (lane & 31)
+template <typename T>
+__device__ __forceinline__ typename Mfma<T>::frag trds_frag(const char* __restrict__ img, int rb, int s, int qb, int lane) {
+    const int i = lane & 15, q = i >> 2, p = i & 3, g = lane >> 4, h = lane >> 5;
+    const int row = rb * 32 + 16 * s + 4 * h + q;
+    const int unit = qb * 8 + (g & 1) * 4 + p;
+    typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+    i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(img + row * 128 + 8 * (unit ^ ds_unit_swz(row))));
+    i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_i16x4*)(img + (row + 8) * 128 + 8 * (unit ^ ds_unit_swz(row + 8))));
+    typedef short s8 __attribute__((ext_vector_type(8)));
+    s8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(typename Mfma<T>::frag, v);
+}
+
+// the packed dS of one 32-key block (Packs::d, accumulator layout: lane = key, word j of fragment s
+// = queries 16s + 8(j>>1) + 4h + 2(j&1) + {0, 1}) into the dS^T image: four 8-byte stores of four
+// consecutive queries.  dsw = (key row * 128 + 8 (h ^ ds_unit_swz(row))) of block 0; block 1's rows
+// are 32 further (same swizzle), i.e. + 4 KiB
+template <int SUB, int KB>
+__device__ __forceinline__ void ds_put(char* dsimg, uint32_t dsw, const unsigned (&d)[2][4]) {
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const uint32_t c8 = 8u * (uint32_t)(SUB * 8 + 4 * s + 2 * i);
+            const u32x2 v = {d[s][2 * i], d[s][2 * i + 1]};
+            *(u32x2*)(dsimg + ((dsw ^ c8) + 4096u * KB)) = v;
+        }
+}
+
+// dkdv6's sub-slice (attention_dkdv6.hip::sub6, same arithmetic and region order) plus the dS^T
+// image writes of both blocks in R4 (block 0's packs are complete after R2, block 1's after R3;
+// R4 carries 8 bare asm MFMAs and no VALU of its own)
+template <typename T, int SUB>
+__device__ __forceinline__ void sub1(K6<T>& k, int h, int l32, int lane, const char* base, const char* nb, int nsub,
+                                     typename Mfma<T>::frag (&qa)[4], typename Mfma<T>::frag (&ga)[4], f32x16& S0,
+                                     f32x16& P0, char* dsimg, uint32_t dsw) {
+    typedef typename Mfma<T>::frag frag;
+    f32x16 S1, P1;
+    frag gt[2][2], qt[2][2];
+    Packs k0, k1;
+    // ---- R1
+    fence();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        S0 = Mfma<T>::mma(qa[s], k.kf[0][s], S0);
+        P0 = Mfma<T>::mma(ga[s], k.vf[0][s], P0);
+    }
+    load_t<T>(gt, qt, base, SUB, lane);
+    seeds(S1, P1, base, SUB, h);
+    fence();
+    // ---- R2
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        S1 = Mfma<T>::mma(qa[s], k.kf[1][s], S1);
+        fin_chunk<T>(S0, P0, k0, 2 * s);
+        fence();
+        P1 = Mfma<T>::mma(ga[s], k.vf[1][s], P1);
+        fin_chunk<T>(S0, P0, k0, 2 * s + 1);
+        fence();
+    }
+    // ---- R3
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        mfma_acc<T, false>(k.dv[0][0], gt[s][0], as_frag<T>(k0.p[s]));
+        fin_chunk<T>(S1, P1, k1, 4 * s);
+        fence();
+        mfma_acc<T, false>(k.dv[0][1], gt[s][1], as_frag<T>(k0.p[s]));
+        fin_chunk<T>(S1, P1, k1, 4 * s + 1);
+        fence();
+        mfma_acc<T, false>(k.dk[0][0], qt[s][0], as_frag<T>(k0.d[s]));
+        fin_chunk<T>(S1, P1, k1, 4 * s + 2);
+        fence();
+        mfma_acc<T, false>(k.dk[0][1], qt[s][1], as_frag<T>(k0.d[s]));
+        fin_chunk<T>(S1, P1, k1, 4 * s + 3);
+        fence();
+    }
+    load_qg<T>(qa, ga, nb, nsub, l32, h);
+    fence();
+    // ---- R4
+    ds_put<SUB, 0>(dsimg, dsw, k0.d);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        mfma_acc<T, true>(k.dv[1][0], gt[s][0], as_frag<T>(k1.p[s]));
+        mfma_acc<T, false>(k.dv[1][1], gt[s][1], as_frag<T>(k1.p[s]));
+        mfma_acc<T, false>(k.dk[1][0], qt[s][0], as_frag<T>(k1.d[s]));
+        mfma_acc<T, false>(k.dk[1][1], qt[s][1], as_frag<T>(k1.d[s]));
+    }
+    ds_put<SUB, 1>(dsimg, dsw, k1.d);
+    seeds(S0, P0, nb, nsub, h);
+    fence();
+}
+
+// dQ^T tile (32 d x 32 queries) of one slice: d block w & 1, query block w >> 1, summed over the
+// workgroup's 256 keys (16 MFMAs; A = K^T from the K image, B = dS^T from the dS^T image)
+template <typename T>
+__device__ __forceinline__ void dq_tile(f32x16& acc, const char* kimg, const char* dsimg, int qb, int db, int lane) {
+    acc = zero16();
+#pragma unroll
+    for (int rb = 0; rb < 8; ++rb)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+            acc = Mfma<T>::mma(tr_frag<T>(kimg, rb, s, db, lane), trds_frag<T>(dsimg, rb, s, qb, lane), acc);
+}
+
+// one 32-column half of an O^T-layout row (lane = query row; lane half h holds columns
+// 8g + 4h .. 8g + 4h + 3, g = 0..3) as two 16-B stores per lane (store_row_t21's permlane pairing)
+template <typename T>
+__device__ __forceinline__ void store_half_t21(T* row, const f32x16& acc, float scale, int h) {
+    typedef T t2 __attribute__((ext_vector_type(2)));
+    unsigned w[4][2];
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const t2 p = {(T)(acc[4 * g + 2 * j] * scale), (T)(acc[4 * g + 2 * j + 1] * scale)};
+            w[g][j] = __builtin_bit_cast(unsigned, p);
+        }
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int G = 0; G < 4; G += 2) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const auto r = __builtin_amdgcn_permlane32_swap(w[G][j], w[G + 1][j], false, false);
+            w[G][j] = r[0];
+            w[G + 1][j] = r[1];
+        }
+        const u32x4 v = {w[G][0], w[G][1], w[G + 1][0], w[G + 1][1]};
+        *(u32x4*)((char*)row + 16 * G + 16 * h) = v;
+    }
+}
+
+struct B1Out {
+    char* part;        // this workgroup's partial block: [Np rows][64] T, rows = queries
+    int qb, db;        // this wave's dQ tile
+    float sc;          // scale / DsScale
+};
+
+// one 64-query slice t in ring slot Q:
+//   wait (slice t+1 landed) + barrier A (everyone done with step t-1: its ring slot and its dS^T image
+//   reads); the dQ partial of slice t-1 stored (its stores are older than the DMA issued next, so
+//   the counted vmcnt of the next step still retires slice t+2 first); DMA of slice t+3; the two
+//   sub-slices (dK / dV as dkdv6, dS^T into the image); lgkmcnt(0) + barrier B; the slice's dQ^T tile
+template <typename T, int Q>
+__device__ __forceinline__ void step1(Dkv2Ctx<T, 4>& c, K6<T>& k, int t, typename Mfma<T>::frag (&qa)[4],
+                                      typename Mfma<T>::frag (&ga)[4], f32x16& S0, f32x16& P0, f32x16& dq,
+                                      const B1Out& out, char* kimg, char* dsimg, uint32_t dsw) {
+    typedef Dkv2Ctx<T, 4> X;
+    wait_vmcnt<X::PIECES + 1>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");  // no LDS access moves across a barrier
+    if (t > 0)  // wave-uniform
+        store_half_t21<T>((T*)(out.part + (size_t)(64 * (t - 1) + 1 + out.qb * 32 + c.l32) * 128) + out.db * 32, dq,
+                          out.sc, c.h);
+    dkv2_issue<T, 4>(c, t + 3 < c.nt ? t + 3 : c.nt - 1, (Q + 3) & 3);
+    const char* cur = c.smem + Q * X::SLOT;
+    const char* nxt = c.smem + ((Q + 1) & 3) * X::SLOT;
+    sub1<T, 0>(k, c.h, c.l32, c.lane, cur, cur, 1, qa, ga, S0, P0, dsimg, dsw);
+    sub1<T, 1>(k, c.h, c.l32, c.lane, cur, nxt, 0, qa, ga, S0, P0, dsimg, dsw);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    fence();
+    dq_tile<T>(dq, kimg, dsimg, out.qb, out.db, c.lane);
+    fence();
+}
+
+template <typename T>
+__global__ __launch_bounds__(256, 1) void attn_bwd1_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
+                                                           const float* __restrict__ lse,
+                                                           const float* __restrict__ delta,
+                                                           const float* __restrict__ nlse,
+                                                           const float* __restrict__ ndelta, T* __restrict__ dqkv,
+                                                           T* __restrict__ dqpart, int N, int H, float dk_scale,
+                                                           float scale, float* __restrict__ r0q) {
+    constexpr int NW = B1_NW, KB = B1_KB;
+    typedef Dkv2Ctx<T, NW> X;
+    typedef typename Mfma<T>::frag frag;
+    static_assert(X::SLOT == B1Ring::SLOT, "ring geometry");
+    __shared__ __attribute__((aligned(128))) char smem[B1_SMEM];
+    char* kimg = smem + B1_KIMG;
+    char* dsimg = smem + B1_DSIMG;
+    X c;
+    K6<T> k;
+    c.smem = smem;
+    c.lane = threadIdx.x & 63;
+    c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    c.h = c.lane >> 5;
+    c.l32 = c.lane & 31;
+    const int nkb = (N - 1 + KB - 1) / KB;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int kblk = tile % nkb, bh = tile / nkb, b = bh / H, hd = bh % H;
+    const int C = H * HD;
+    const int64_t ld = 3 * (int64_t)C;
+    const T* Bb = qkv + (int64_t)b * N * ld;
+    const T* dOb = dout + (int64_t)b * N * C;
+    c.ldq = (uint32_t)(ld * sizeof(T));
+    c.ldg = (uint32_t)(C * sizeof(T));
+    c.nt = (N - 1 + 63) / 64;
+    c.rem = N - 1 - 64 * (c.nt - 1);
+    B1Out out;
+    out.part = (char*)dqpart + (size_t)((int64_t)bh * nkb + kblk) * (size_t)(1 + 64 * c.nt) * 128;
+    out.qb = c.wave >> 1;
+    out.db = c.wave & 1;
+    out.sc = scale / DsScale<T>::v;
+    int key[2];
+    bool kok[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+        key[kb] = 1 + kblk * KB + c.wave * 64 + kb * 32 + c.l32;
+        kok[kb] = key[kb] < N;  // keys past N compute on key N - 1, store nothing, and are zero K rows
+        const int kc = kok[kb] ? key[kb] : N - 1;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            k.kf[kb][s] = *(const frag*)(Bb + (int64_t)kc * ld + C + hd * HD + (2 * s + c.h) * 8);
+            k.vf[kb][s] = *(const frag*)(Bb + (int64_t)kc * ld + 2 * C + hd * HD + (2 * s + c.h) * 8);
+        }
+    }
+    frag q0[4], g0[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        q0[s] = *(const frag*)(Bb + hd * HD + (2 * s + c.h) * 8);
+        g0[s] = *(const frag*)(dOb + hd * HD + (2 * s + c.h) * 8);
+    }
+    typedef T t4 __attribute__((ext_vector_type(4)));
+    t4 q0d[2][4], g0d[2][4];
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            q0d[db][g] = *(const t4*)(Bb + hd * HD + db * 32 + 8 * g + 4 * c.h);
+            g0d[db][g] = *(const t4*)(dOb + hd * HD + db * 32 + 8 * g + 4 * c.h);
+        }
+    const float L0 = lse[(int64_t)bh * N], d0 = delta[(int64_t)bh * N];
+
+    c.rs = make_rsrc(Bb, (uint32_t)N * c.ldq);
+    c.rg = make_rsrc(dOb, (uint32_t)N * c.ldg);
+    c.rl = make_rsrc(nlse + (int64_t)bh * N, (uint32_t)N * 4);
+    c.rd = make_rsrc(ndelta + (int64_t)bh * N, (uint32_t)N * 4);
+    const bool q_wave = c.wave * X::PIECES < 8;
+    c.rmine = q_wave ? c.rs : c.rg;
+    c.ldmine = q_wave ? c.ldq : c.ldg;
+#pragma unroll
+    for (int i = 0; i < X::PIECES; ++i) {
+        const int piece = c.wave * X::PIECES + i;
+        const int r = (piece & 7) * 8 + (c.lane >> 3);
+        const uint32_t chunk = (uint32_t)(((c.lane & 7) ^ xsw(r)) * 16);
+        c.voff[i] = piece < 8 ? (uint32_t)r * c.ldq + chunk + (uint32_t)(hd * HD * sizeof(T))
+                              : (uint32_t)r * c.ldg + chunk + (uint32_t)(hd * HD * sizeof(T));
+    }
+    dkv2_issue<T, NW>(c, 0, 0);
+    dkv2_issue<T, NW>(c, c.nt > 1 ? 1 : 0, 1);
+    dkv2_issue<T, NW>(c, c.nt > 2 ? 2 : c.nt - 1, 2);
+
+    // the K image (dQ's K^T operand): this wave's 64 key rows, zero rows for keys past N
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+        const int row = c.wave * 64 + kb * 32 + c.l32;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            frag v = k.kf[kb][s];
+            if (!kok[kb])
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = (T)0.f;
+            *(frag*)(kimg + row * 128 + (((2 * s + c.h) ^ xsw(row)) << 4)) = v;
+        }
+    }
+    // this lane's dS^T image write base (block 0's key row)
+    const int dsrow = c.wave * 64 + c.l32;
+    const uint32_t dsw = (uint32_t)(dsrow * 128 + 8 * (c.h ^ ds_unit_swz(dsrow)));
+
+    // query 0 (CLS) folded in on the VALU, as dkdv6
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+        float spart = 0.f, ppart = 0.f;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                spart += (float)q0[s][j] * (float)k.kf[kb][s][j];
+                ppart += (float)g0[s][j] * (float)k.vf[kb][s][j];
+            }
+        const float p0 = __builtin_amdgcn_exp2f(xhalf_sum(spart) - L0);
+        const float ds0 = p0 * (xhalf_sum(ppart) - d0) * DsScale<T>::v;
+        ((float*)(smem + B1_W0))[c.wave * 64 + kb * 32 + c.l32] = kok[kb] ? ds0 : 0.f;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    k.dv[kb][db][4 * g + e] = p0 * (float)g0d[db][g][e];
+                    k.dk[kb][db][4 * g + e] = ds0 * (float)q0d[db][g][e];
+                }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) frag_ds_scale<T>(k.vf[kb][s]);
+    }
+
+    wait_vmcnt<2 * (X::PIECES + 1)>();  // slice 0 landed (slices 1, 2 in flight)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the K image
+    __builtin_amdgcn_s_barrier();
+    frag qa[4], ga[4];
+    f32x16 S0, P0, dq;
+    load_qg<T>(qa, ga, smem, 0, c.l32, c.h);
+    seeds(S0, P0, smem, 0, c.h);
+    int t = 0;
+    for (; t + 4 <= c.nt; t += 4) {
+        step1<T, 0>(c, k, t, qa, ga, S0, P0, dq, out, kimg, dsimg, dsw);
+        step1<T, 1>(c, k, t + 1, qa, ga, S0, P0, dq, out, kimg, dsimg, dsw);
+        step1<T, 2>(c, k, t + 2, qa, ga, S0, P0, dq, out, kimg, dsimg, dsw);
+        step1<T, 3>(c, k, t + 3, qa, ga, S0, P0, dq, out, kimg, dsimg, dsw);
+    }
+    if (t < c.nt) step1<T, 0>(c, k, t++, qa, ga, S0, P0, dq, out, kimg, dsimg, dsw);
+    if (t < c.nt) step1<T, 1>(c, k, t++, qa, ga, S0, P0, dq, out, kimg, dsimg, dsw);
+    if (t < c.nt) step1<T, 2>(c, k, t++, qa, ga, S0, P0, dq, out, kimg, dsimg, dsw);
+    // the last slice's dQ partial
+    store_half_t21<T>((T*)(out.part + (size_t)(64 * (c.nt - 1) + 1 + out.qb * 32 + c.l32) * 128) + out.db * 32, dq,
+                      out.sc, c.h);
+    wait_vmcnt<0>();
+    if (r0q != nullptr) {
+        // CLS-row fold (dkdv6's): this block's share of dQ_0 += dS_0 k, one partial per workgroup
+        __syncthreads();
+        const int lane = __lane_id();
+        char* img = smem + c.wave * 64 * 128;
+        r0_put<T>(img, k.kf[0], lane & 31, lane >> 5);
+        r0_put<T>(img, k.kf[1], 32 + (lane & 31), lane >> 5);
+        const float aq = r0_colsum<T, 64>(img, (const float*)(smem + B1_W0) + c.wave * 64, lane);
+        float* part = (float*)(smem + NW * 64 * 128);
+        part[c.wave * 64 + lane] = aq;
+        __syncthreads();
+        if (c.wave == 0) {
+            float sum = 0.f;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) sum += part[w * 64 + lane];
+            r0q[((int64_t)bh * nkb + kblk) * 64 + lane] = sum;
+        }
+    }
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3"
+                 : "+a"(k.dk[0][0]), "+a"(k.dk[0][1]), "+a"(k.dk[1][0]), "+a"(k.dk[1][1]), "+a"(k.dv[0][0]),
+                   "+a"(k.dv[0][1]), "+a"(k.dv[1][0]), "+a"(k.dv[1][1]));
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+        if (kok[kb]) {
+            T* rk = dqkv + ((int64_t)b * N + key[kb]) * ld + C + hd * HD;
+            store_row_t21<T>(rk, k.dk[kb], dk_scale / DsScale<T>::v, c.h);
+            store_row_t21<T>(rk + C, k.dv[kb], 1.0f, c.h);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------- prep
+// Per query q >= 1 (128 per workgroup, 2 lanes per query as the dQ pass's rows): delta, the negated
+// statistics, dS_q0 (ds0v), and this block's share of key 0's column sums (r0kv: [dK_0 | dV_0], both
+// DsScale-scaled as the dQ pass's epilogue writes them); query 0's delta by block 0.  The dot products
+// follow attn_bwd_dq2_kernel's prologue term for term.
+template <typename T>
+__global__ __launch_bounds__(256) void attn_bwd1_prep_kernel(const T* __restrict__ qkv, const T* __restrict__ o,
+                                                             const T* __restrict__ dout, const float* __restrict__ lse,
+                                                             float* __restrict__ delta, float* __restrict__ nstat,
+                                                             float* __restrict__ ds0v, float* __restrict__ r0kv, int N,
+                                                             int H, int nqp) {
+    typedef typename Mfma<T>::frag frag;
+    constexpr int QB = 128;
+    __shared__ __attribute__((aligned(16))) char smem[4 * 32 * 128 + 2 * QB * 4 + 4 * 128 * 4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
+    const int blk = blockIdx.x % nqp, bh = blockIdx.x / nqp, b = bh / H, hd = bh % H;
+    const int C = H * HD;
+    const int64_t ld = 3 * (int64_t)C;
+    const T* Bb = qkv + (int64_t)b * N * ld;
+    const T* dOb = dout + (int64_t)b * N * C + hd * HD;
+    const int q = 1 + blk * QB + wave * 32 + l32;
+    const bool qok = q < N;
+    const int qc = qok ? q : N - 1;
+    frag qf[4], gf[4], of[4], k0[4], v0[4];
+    const T* Orow = o + ((int64_t)b * N + qc) * C + hd * HD;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        k0[s] = *(const frag*)(Bb + C + hd * HD + (2 * s + h) * 8);
+        v0[s] = *(const frag*)(Bb + 2 * C + hd * HD + (2 * s + h) * 8);
+        qf[s] = *(const frag*)(Bb + (int64_t)qc * ld + hd * HD + (2 * s + h) * 8);
+        gf[s] = *(const frag*)(dOb + (int64_t)qc * C + (2 * s + h) * 8);
+        of[s] = *(const frag*)(Orow + (2 * s + h) * 8);
+    }
+    const float L = lse[(int64_t)bh * N + qc];
+    float dpart = 0.f, spart = 0.f, ppart = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            dpart += (float)of[s][j] * (float)gf[s][j];
+            spart += (float)qf[s][j] * (float)k0[s][j];
+            ppart += (float)gf[s][j] * (float)v0[s][j];
+        }
+    const float dl = xhalf_sum(dpart);
+    const float p0 = __builtin_amdgcn_exp2f(xhalf_sum(spart) - L);
+    const float ds0 = p0 * (xhalf_sum(ppart) - dl) * DsScale<T>::v;
+    if (h == 0 && qok) {
+        delta[(int64_t)bh * N + q] = dl;
+        nstat[(int64_t)bh * N + q] = -L;
+        nstat[(int64_t)(gridDim.x / nqp) * N + (int64_t)bh * N + q] = -dl * DsScale<T>::v;
+        ds0v[(int64_t)bh * N + q] = ds0;
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) frag_ds_scale<T>(gf[s]);
+    float* w = (float*)(smem + 4 * 32 * 128);
+    if (h == 0) {
+        w[wave * 32 + l32] = qok ? ds0 : 0.f;
+        w[QB + wave * 32 + l32] = qok ? p0 : 0.f;
+    }
+    char* img = smem + wave * 32 * 128;
+    r0_put<T>(img, qf, l32, h);
+    const float ak = r0_colsum<T, 32>(img, w + wave * 32, lane);
+    asm volatile("" ::: "memory");
+    r0_put<T>(img, gf, l32, h);
+    const float av = r0_colsum<T, 32>(img, w + QB + wave * 32, lane);
+    float* part = (float*)(smem + 4 * 32 * 128 + 2 * QB * 4);
+    part[wave * 128 + lane] = ak;
+    part[wave * 128 + 64 + lane] = av;
+    if (blk == 0 && wave == 0) {  // delta of query 0 (attn_bwd_dq2_kernel's epilogue term)
+        const int64_t r0 = (int64_t)b * N * C + hd * HD + lane;
+        const float d0 = wave_sum((float)dout[r0] * (float)o[r0]);
+        if (lane == 0) delta[(int64_t)bh * N] = d0;
+    }
+    __syncthreads();
+    if (threadIdx.x < 128) {
+        float sum = 0.f;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) sum += part[v * 128 + threadIdx.x];
+        r0kv[((int64_t)bh * nqp + blk) * 128 + threadIdx.x] = sum;
+    }
+}
+
+// ---------------------------------------------------------------------------- dQ reduce
+// dQ[q] = sum_j part_j[q] (key blocks in order) + dS_q0 k_0 scale / DsScale, queries 1..N-1; 8 lanes
+// per query row (8 columns each), 32 rows per workgroup
+template <typename T>
+__global__ __launch_bounds__(256) void attn_bwd1_dq_reduce(const T* __restrict__ dqpart, const float* __restrict__ ds0v,
+                                                           const T* __restrict__ qkv, T* __restrict__ dqkv, int N, int H,
+                                                           int nkb, int nrb, float sc) {
+    typedef T t8 __attribute__((ext_vector_type(8)));
+    const int rb = blockIdx.x % nrb, bh = blockIdx.x / nrb, b = bh / H, hd = bh % H;
+    const int q = 1 + rb * 32 + (threadIdx.x >> 3), c8 = (threadIdx.x & 7) * 8;
+    if (q >= N) return;
+    const int C = H * HD;
+    const int64_t ld = 3 * (int64_t)C;
+    const int64_t Np = 1 + 64 * (int64_t)((N - 1 + 63) / 64);
+    const t8 kv = *(const t8*)(qkv + (int64_t)b * N * ld + C + hd * HD + c8);
+    const float w = ds0v[(int64_t)bh * N + q] * sc;
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = w * (float)kv[e];
+    const T* p = dqpart + ((int64_t)bh * nkb * Np + q) * 64 + c8;
+    int j = 0;
+    for (; j + 4 <= nkb; j += 4) {
+        t8 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *(const t8*)(p + (int64_t)(j + u) * Np * 64);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[e] += (float)v[u][e];
+    }
+    for (; j < nkb; ++j) {
+        const t8 v = *(const t8*)(p + (int64_t)j * Np * 64);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += (float)v[e];
+    }
+    t8 r;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) r[e] = (T)acc[e];
+    *(t8*)(dqkv + ((int64_t)b * N + q) * ld + hd * HD + c8) = r;
+}
+
+template <typename T>
+void bwd1_launch(const void* qkv, const void* o, const void* dout, const float* lse, float* delta, float* nstat,
+                 float* ds0v, float* r0kv, int nqp, float* r0q, void* dqpart, void* dqkv, int B, int N, int H,
+                 float scale, hipStream_t st) {
+    const int nkb = (N - 1 + B1_KB - 1) / B1_KB;
+    attn_bwd1_prep_kernel<T><<<B * H * nqp, 256, 0, st>>>((const T*)qkv, (const T*)o, (const T*)dout, lse, delta, nstat,
+                                                          ds0v, r0kv, N, H, nqp);
+    attn_bwd1_kernel<T><<<B * H * nkb, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, nstat,
+                                                     nstat + (int64_t)B * H * N, (T*)dqkv, (T*)dqpart, N, H,
+                                                     1.0f / LOG2E, scale, r0q);
+    const int nrb = (N - 1 + 31) / 32;
+    attn_bwd1_dq_reduce<T><<<B * H * nrb, 256, 0, st>>>((const T*)dqpart, ds0v, (const T*)qkv, (T*)dqkv, N, H, nkb, nrb,
+                                                        scale / DsScale<T>::v);
+}
+
+}  // namespace
+
+int attn_bwd1_prep_blocks(int N) { return (N - 1 + 127) / 128; }
+
+int64_t attn_bwd1_part_bytes(int B, int N, int H) {
+    const int64_t nkb = (N - 1 + B1_KB - 1) / B1_KB, np = 1 + 64 * (int64_t)((N - 1 + 63) / 64);
+    return (int64_t)B * H * nkb * np * 128;
+}
+
+void attn_bwd1_launch(int dt, const void* qkv, const void* o, const void* dout, const float* lse, float* delta,
+                      float* nstat, float* ds0v, float* r0kv, float* r0q, void* dqpart, void* dqkv, int B, int N,
+                      int H, float scale, hipStream_t st) {
+    const int nqp = attn_bwd1_prep_blocks(N);
+    if (dt == DCLIP_BF16)
+        bwd1_launch<bf16>(qkv, o, dout, lse, delta, nstat, ds0v, r0kv, nqp, r0q, dqpart, dqkv, B, N, H, scale, st);
+    else
+        bwd1_launch<f16>(qkv, o, dout, lse, delta, nstat, ds0v, r0kv, nqp, r0q, dqpart, dqkv, B, N, H, scale, st);
+}

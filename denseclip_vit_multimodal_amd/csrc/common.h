@@ -266,3 +266,11 @@ int64_t attn_bwd_fp8_ws_bytes(int B, int N, int H);
 void attn_bwd_dkdv8_launch(int dt, const void* qkv, const void* dout, const float* lse, const float* delta,
                            const float* nlse, const float* ndelta, void* dqkv, int B, int N, int H, float dk_scale,
                            float* r0q, void* f8ws, hipStream_t st);
+// the one-pass backward (attention_bwd1.hip, DCLIP_OPT_ATTN_BWD_BLOCK 9): prep + sweep + ordered dQ
+// reduction (the CLS row's merge is the caller's); r0kv gets attn_bwd1_prep_blocks(N) partials per
+// (image, head), r0q one per key block; dqpart holds attn_bwd1_part_bytes
+int attn_bwd1_prep_blocks(int N);
+int64_t attn_bwd1_part_bytes(int B, int N, int H);
+void attn_bwd1_launch(int dt, const void* qkv, const void* o, const void* dout, const float* lse, float* delta,
+                      float* nstat, float* ds0v, float* r0kv, float* r0q, void* dqpart, void* dqkv, int B, int N,
+                      int H, float scale, hipStream_t st);

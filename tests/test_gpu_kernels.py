@@ -744,6 +744,43 @@ def test_attention_dkdv7_bitwise_dkdv6(B, H, N, dt, bwd_block):
     assert torch.equal(res[0], res[1]) and torch.equal(res[0], res[2])
 
 
+@pytest.mark.parametrize("B,H,N", [(3, 2, 257), (2, 2, 290), (2, 3, 803), (3, 2, 1345), (2, 2, 2049), (1, 2, 8193),
+                                   (1, 1, 10659)])
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+def test_attention_onepass_bwd(B, H, N, dt, bwd_block):
+    """The one-pass backward (DCLIP_OPT_ATTN_BWD_BLOCK 9, round 6, attention_bwd1.hip): one key-major
+    sweep computes dK, dV and per-key-block 16-bit dQ partials, an ordered pass sums them.  dK / dV of
+    keys 1..N-1 are dkdv6's products on the same statistics (the prep kernel repeats the dQ pass's
+    delta arithmetic): equal BIT FOR BIT to the two-pass result.  dQ is summed in another order, with
+    one 16-bit rounding per 256-key partial: within 3e-3 (fp16) / 1.5e-2 (bf16) of the two-pass dQ and
+    no further from fp32 autograd than 1.25x the two-pass error + one unit roundoff.  Full and ragged
+    N - 1, partial last key blocks, the CLS row included."""
+    O = ops()
+    C = 64 * H
+    torch.manual_seed(9)
+    qkv, qref = prescale((torch.randn(B * N, 3 * C, device=DEV) * 1.5).to(dt), H)
+    dout = torch.randn(B * N, C, device=DEV).to(dt)
+    o, lse = O.attn_fwd(qkv, B, N, H, 64 ** -0.5)
+    res = []
+    for v in (0, 9):
+        bwd_block(v)
+        res.append(O.attn_bwd(qkv, o, dout, lse, B, N, H, 64 ** -0.5).float())
+    a, b = res
+    assert torch.isfinite(b).all()
+    rest = torch.ones(B * N, dtype=torch.bool, device=DEV)
+    rest[::N] = False
+    assert torch.equal(b[rest, C:], a[rest, C:])  # dK, dV of keys 1..N-1
+    assert rel_err(b[~rest, C:], a[~rest, C:]) < 1e-4, rel_err(b[~rest, C:], a[~rest, C:])  # key 0
+    u = {torch.float16: 2.0 ** -11, torch.bfloat16: 2.0 ** -8}[dt]
+    assert rel_err(b[:, :C], a[:, :C]) < 1.5 * TOL[dt], rel_err(b[:, :C], a[:, :C])
+    if N <= 2049:
+        q32 = qref.clone().requires_grad_(True)
+        attn_ref(q32, B, N, H).backward(dout.float())
+        g = q32.grad[:, :C]
+        ea, eb = rel_err(a[:, :C], g), rel_err(b[:, :C], g)
+        assert eb < 1.25 * ea + u, (eb, ea)
+
+
 @pytest.mark.parametrize("variant", ["rows64", "defer"])
 @pytest.mark.parametrize("B,H,N", [(3, 2, 257), (2, 2, 290), (2, 3, 803), (1, 2, 8193)])
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
