@@ -2466,13 +2466,13 @@ bool bwd2_launch(const void* qkv, const void* o, const void* dout, const float* 
     const int bwd_block = dclip_option(DCLIP_OPT_ATTN_BWD_BLOCK);
     if (ragged && (dclip_option(DCLIP_OPT_ATTN_DQ_WAVES) == 4 ||
                    (bwd_block != 0 && bwd_block != 5 && bwd_block != 6 && bwd_block != 7 && bwd_block != 8 &&
-                    bwd_block != 9)))
+                    bwd_block != 9 && bwd_block != 10)))
         return false;
     const int nsplit = (N + R0_CHUNK - 1) / R0_CHUNK;
     float* ws0 = delta + (int64_t)B * H * N;
     float* nstat = ws0 + (int64_t)B * H * ((N + 63) / 64) * 192;  // [-lse | -delta], B*H*N each
     const bool dq4 = dclip_option(DCLIP_OPT_ATTN_DQ_WAVES) == 4;
-    if (bwd_block == 9 && f8ws == nullptr) {
+    if ((bwd_block == 9 || bwd_block == 10) && f8ws == nullptr) {
         // the one-pass backward (attention_bwd1.hip): prep (delta, statistics, key 0's terms), one
         // key-major sweep for dK, dV and per-key-block dQ partials, the ordered dQ reduction; then
         // the CLS row's merge as the two-pass path.  Workspace past the two-pass part: dS_q0 (B*H*N
@@ -2617,7 +2617,7 @@ extern "C" int64_t dclip_attn_bwd_workspace(int B, int N, int H) {
     // statistics the CLS-split dK/dV pass reads (-lse, -delta: 2*B*H*N)
     const int64_t two_pass = 3 * (int64_t)B * H * N + (int64_t)B * H * ((N + 63) / 64) * 192;
     // the one-pass backward (DCLIP_OPT_ATTN_BWD_BLOCK 9): + dS_q0 (B*H*N) + the dQ partials
-    if (dclip_option(DCLIP_OPT_ATTN_BWD_BLOCK) == 9 && N >= 257)
+    if ((dclip_option(DCLIP_OPT_ATTN_BWD_BLOCK) == 9 || dclip_option(DCLIP_OPT_ATTN_BWD_BLOCK) == 10) && N >= 257)
         return two_pass + (int64_t)B * H * N + (attn_bwd1_part_bytes(B, N, H) + 3) / 4 + 64;
     return two_pass;
 }

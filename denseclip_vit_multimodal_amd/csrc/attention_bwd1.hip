@@ -33,11 +33,31 @@ constexpr int B1_NW = 4, B1_KB = 64 * B1_NW;  // waves, keys per workgroup
 typedef Dkv2Ctx<bf16, B1_NW> B1Ring;           // the ring geometry (SLOT, PIECES) is type-independent
 constexpr int B1_RING = 4 * B1Ring::SLOT;
 constexpr int B1_W0 = B1_RING;                 // the CLS-row fold's per-key weights dS_0 (KB floats)
-constexpr int B1_KIMG = B1_W0 + B1_KB * 4;     // K image [256 keys][64 d], swz layout
-constexpr int B1_DSIMG = B1_KIMG + B1_KB * 128;  // dS^T image [256 keys][64 queries], ds_unit_swz
-constexpr int B1_SMEM = B1_DSIMG + B1_KB * 128;
-static_assert(B1_KIMG % 128 == 0 && B1_DSIMG % 128 == 0, "images on 128-B rows");
-static_assert(B1_SMEM <= 160 * 1024, "LDS");
+constexpr int B1_SMEM = B1_W0 + B1_KB * 4;     // ring + weights (one array: the ring's LDS-DMA target)
+constexpr int B1_IMG = B1_KB * 128;            // K image / dS^T image: [256 keys][64] 16-bit each
+// the two images are separate __shared__ arrays: their reads provably do not alias the ring's
+// in-flight LDS-DMA writes (one array holding everything made hipcc wait vmcnt(0), i.e. for the whole
+// ring, before the first dS^T image read of every step)
+static_assert(B1_SMEM + 2 * B1_IMG <= 160 * 1024, "LDS");
+
+// the lane id re-read where it is used (an opaque asm: nothing derived from it is hoisted out of the
+// sweep's loop, so the dS^T / K image addresses are recomputed per step instead of holding ~14 VGPRs
+// across it — the loop runs at the 256-VGPR limit)
+__device__ __forceinline__ int lane_now() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
+// a 16-bit fragment moved into the accumulator file (the sweep's dK / dV sums use 128 of its 256
+// registers): the K / V fragments are B operands of the S / dP MFMAs only (gfx950 MFMAs read A / B
+// from AGPRs), so keeping them there frees 64 arch VGPRs for the dQ tile
+template <typename F>
+__device__ __forceinline__ F to_agpr(F v) {
+    F r;
+    asm volatile("" : "=a"(r) : "0"(v));
+    return r;
+}
 
 // 8-byte unit XOR of row r in the dS^T image: a bijection of r & 15 (16 keys of one ds_write_b64
 // lane group hit 16 distinct units), with bit 3 flipped on r bit 1 (the transposing read's four rows
@@ -46,16 +66,24 @@ __device__ __forceinline__ int ds_unit_swz(int row) { return (row & 15) ^ (((row
 
 // transposing read of the dS^T image (the B operand of dQ^T += K^T dS^T): element j of half h is
 // key rb*32 + 16s + 8(j>>2) + 4h + (j&3) — tr_frag's k-order, so it pairs with tr_frag(K image) —
-// and MFMA column (lane & 31) is query qb*32 + (lane & 31)
-template <typename T>
-__device__ __forceinline__ typename Mfma<T>::frag trds_frag(const char* __restrict__ img, int rb, int s, int qb, int lane) {
+// and MFMA column (lane & 31) is query qb*32 + (lane & 31).  The swizzle depends on the row only
+// through row & 15 = 4h + q (+ 8 for the upper half), so a lane's two addresses are fixed per query
+// block (ds_tr_base) and (rb, s) is an immediate offset
+struct DsTrBase {
+    uint32_t lo, hi;
+};
+__device__ __forceinline__ DsTrBase ds_tr_base(int qb, int lane) {
     const int i = lane & 15, q = i >> 2, p = i & 3, g = lane >> 4, h = lane >> 5;
-    const int row = rb * 32 + 16 * s + 4 * h + q;
+    const int r = 4 * h + q;
     const int unit = qb * 8 + (g & 1) * 4 + p;
+    return {(uint32_t)(r * 128 + 8 * (unit ^ ds_unit_swz(r))), (uint32_t)((r + 8) * 128 + 8 * (unit ^ ds_unit_swz(r + 8)))};
+}
+template <typename T>
+__device__ __forceinline__ typename Mfma<T>::frag trds_frag(const char* __restrict__ img, DsTrBase a, int rb, int s) {
     typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
-    i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(img + row * 128 + 8 * (unit ^ ds_unit_swz(row))));
-    i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lds_i16x4*)(img + (row + 8) * 128 + 8 * (unit ^ ds_unit_swz(row + 8))));
+    const int off = (rb * 32 + 16 * s) * 128;
+    i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(img + a.lo + off));
+    i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(img + a.hi + off));
     typedef short s8 __attribute__((ext_vector_type(8)));
     s8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     return __builtin_bit_cast(typename Mfma<T>::frag, v);
@@ -65,6 +93,10 @@ __device__ __forceinline__ typename Mfma<T>::frag trds_frag(const char* __restri
 // = queries 16s + 8(j>>1) + 4h + 2(j&1) + {0, 1}) into the dS^T image: four 8-byte stores of four
 // consecutive queries.  dsw = (key row * 128 + 8 (h ^ ds_unit_swz(row))) of block 0; block 1's rows
 // are 32 further (same swizzle), i.e. + 4 KiB
+__device__ __forceinline__ uint32_t ds_put_base(int wave) {
+    const int lane = threadIdx.x & 63, row = wave * 64 + (lane & 31);
+    return (uint32_t)(row * 128 + 8 * ((lane >> 5) ^ ds_unit_swz(row)));
+}
 template <int SUB, int KB>
 __device__ __forceinline__ void ds_put(char* dsimg, uint32_t dsw, const unsigned (&d)[2][4]) {
     typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
@@ -84,7 +116,7 @@ __device__ __forceinline__ void ds_put(char* dsimg, uint32_t dsw, const unsigned
 template <typename T, int SUB>
 __device__ __forceinline__ void sub1(K6<T>& k, int h, int l32, int lane, const char* base, const char* nb, int nsub,
                                      typename Mfma<T>::frag (&qa)[4], typename Mfma<T>::frag (&ga)[4], f32x16& S0,
-                                     f32x16& P0, char* dsimg, uint32_t dsw) {
+                                     f32x16& P0, char* dsimg, int wave) {
     typedef typename Mfma<T>::frag frag;
     f32x16 S1, P1;
     frag gt[2][2], qt[2][2];
@@ -128,6 +160,7 @@ __device__ __forceinline__ void sub1(K6<T>& k, int h, int l32, int lane, const c
     load_qg<T>(qa, ga, nb, nsub, l32, h);
     fence();
     // ---- R4
+    const uint32_t dsw = ds_put_base(wave);
     ds_put<SUB, 0>(dsimg, dsw, k0.d);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -142,30 +175,47 @@ __device__ __forceinline__ void sub1(K6<T>& k, int h, int l32, int lane, const c
 }
 
 // dQ^T tile (32 d x 32 queries) of one slice: d block w & 1, query block w >> 1, summed over the
-// workgroup's 256 keys (16 MFMAs; A = K^T from the K image, B = dS^T from the dS^T image)
+// workgroup's 256 keys (16 MFMAs; A = K^T from the K image, B = dS^T from the dS^T image), each
+// k-step's four transposing reads issued one k-step ahead of its MFMA
 template <typename T>
-__device__ __forceinline__ void dq_tile(f32x16& acc, const char* kimg, const char* dsimg, int qb, int db, int lane) {
+__device__ __forceinline__ void dq_tile(f32x16& acc, const char* kimg, const char* dsimg, int qb, int db) {
+    typedef typename Mfma<T>::frag frag;
+    const int lane = threadIdx.x & 63;
+    const DsTrBase dsb = ds_tr_base(qb, lane);
+    frag a[2], b[2];
+    a[0] = tr_frag<T>(kimg, 0, 0, db, lane);
+    b[0] = trds_frag<T>(dsimg, dsb, 0, 0);
     acc = zero16();
 #pragma unroll
-    for (int rb = 0; rb < 8; ++rb)
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-            acc = Mfma<T>::mma(tr_frag<T>(kimg, rb, s, db, lane), trds_frag<T>(dsimg, rb, s, qb, lane), acc);
+    for (int ks = 0; ks < 16; ++ks) {
+        if (ks + 1 < 16) {
+            a[(ks + 1) & 1] = tr_frag<T>(kimg, (ks + 1) >> 1, (ks + 1) & 1, db, lane);
+            b[(ks + 1) & 1] = trds_frag<T>(dsimg, dsb, (ks + 1) >> 1, (ks + 1) & 1);
+        }
+        acc = Mfma<T>::mma(a[ks & 1], b[ks & 1], acc);
+    }
 }
 
-// one 32-column half of an O^T-layout row (lane = query row; lane half h holds columns
-// 8g + 4h .. 8g + 4h + 3, g = 0..3) as two 16-B stores per lane (store_row_t21's permlane pairing)
+// one 32-column half of a dQ^T tile (lane = query row; lane half h holds columns 8g + 4h .. 8g + 4h + 3,
+// g = 0..3) as two 16-B buffer stores per lane (store_row_t21's permlane pairing): row `row0 + lane`
+// of the workgroup's partial block, columns 32 db .. 32 db + 31
 template <typename T>
-__device__ __forceinline__ void store_half_t21(T* row, const f32x16& acc, float scale, int h) {
+__device__ __forceinline__ void store_dq_half(rsrc_t rp, uint32_t row0, int db, const f32x16& acc, float scale) {
     typedef T t2 __attribute__((ext_vector_type(2)));
     unsigned w[4][2];
 #pragma unroll
     for (int g = 0; g < 4; ++g)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            const t2 p = {(T)(acc[4 * g + 2 * j] * scale), (T)(acc[4 * g + 2 * j + 1] * scale)};
+            // bf16 partials are stored unscaled (the reduction applies scale / DsScale, a power of two:
+            // the same bits); fp16 ones scaled (their range)
+            const float a0 = acc[4 * g + 2 * j], a1 = acc[4 * g + 2 * j + 1];
+            const t2 p = std::is_same<T, bf16>::value ? t2{(T)a0, (T)a1} : t2{(T)(a0 * scale), (T)(a1 * scale)};
             w[g][j] = __builtin_bit_cast(unsigned, p);
         }
+    const int lane = lane_now();
+    const uint32_t vo = (uint32_t)(((lane & 31) * 128) + 16 * (lane >> 5) + 64 * db);
+    const uint32_t so = row0 * 128;
     typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int G = 0; G < 4; G += 2) {
@@ -176,12 +226,12 @@ __device__ __forceinline__ void store_half_t21(T* row, const f32x16& acc, float 
             w[G + 1][j] = r[1];
         }
         const u32x4 v = {w[G][0], w[G][1], w[G + 1][0], w[G + 1][1]};
-        *(u32x4*)((char*)row + 16 * G + 16 * h) = v;
+        __builtin_amdgcn_raw_buffer_store_b128(v, rp, vo + 16 * G, so, 0);
     }
 }
 
 struct B1Out {
-    char* part;        // this workgroup's partial block: [Np rows][64] T, rows = queries
+    rsrc_t part;       // this workgroup's partial block: [Np rows][64] T, rows = queries
     int qb, db;        // this wave's dQ tile
     float sc;          // scale / DsScale
 };
@@ -194,24 +244,23 @@ struct B1Out {
 template <typename T, int Q>
 __device__ __forceinline__ void step1(Dkv2Ctx<T, 4>& c, K6<T>& k, int t, typename Mfma<T>::frag (&qa)[4],
                                       typename Mfma<T>::frag (&ga)[4], f32x16& S0, f32x16& P0, f32x16& dq,
-                                      const B1Out& out, char* kimg, char* dsimg, uint32_t dsw) {
+                                      const B1Out& out, char* kimg, char* dsimg) {
     typedef Dkv2Ctx<T, 4> X;
     wait_vmcnt<X::PIECES + 1>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");  // no LDS access moves across a barrier
     if (t > 0)  // wave-uniform
-        store_half_t21<T>((T*)(out.part + (size_t)(64 * (t - 1) + 1 + out.qb * 32 + c.l32) * 128) + out.db * 32, dq,
-                          out.sc, c.h);
+        store_dq_half<T>(out.part, (uint32_t)(64 * (t - 1) + 1 + out.qb * 32), out.db, dq, out.sc);
     dkv2_issue<T, 4>(c, t + 3 < c.nt ? t + 3 : c.nt - 1, (Q + 3) & 3);
     const char* cur = c.smem + Q * X::SLOT;
     const char* nxt = c.smem + ((Q + 1) & 3) * X::SLOT;
-    sub1<T, 0>(k, c.h, c.l32, c.lane, cur, cur, 1, qa, ga, S0, P0, dsimg, dsw);
-    sub1<T, 1>(k, c.h, c.l32, c.lane, cur, nxt, 0, qa, ga, S0, P0, dsimg, dsw);
+    sub1<T, 0>(k, c.h, c.l32, c.lane, cur, cur, 1, qa, ga, S0, P0, dsimg, c.wave);
+    sub1<T, 1>(k, c.h, c.l32, c.lane, cur, nxt, 0, qa, ga, S0, P0, dsimg, c.wave);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     fence();
-    dq_tile<T>(dq, kimg, dsimg, out.qb, out.db, c.lane);
+    dq_tile<T>(dq, kimg, dsimg, out.qb, out.db);
     fence();
 }
 
@@ -228,8 +277,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd1_kernel(const T* __restrict__
     typedef typename Mfma<T>::frag frag;
     static_assert(X::SLOT == B1Ring::SLOT, "ring geometry");
     __shared__ __attribute__((aligned(128))) char smem[B1_SMEM];
-    char* kimg = smem + B1_KIMG;
-    char* dsimg = smem + B1_DSIMG;
+    __shared__ __attribute__((aligned(128))) char kimg[B1_IMG];   // K image, swz layout
+    __shared__ __attribute__((aligned(128))) char dsimg[B1_IMG];  // dS^T image, ds_unit_swz layout
     X c;
     K6<T> k;
     c.smem = smem;
@@ -249,7 +298,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd1_kernel(const T* __restrict__
     c.nt = (N - 1 + 63) / 64;
     c.rem = N - 1 - 64 * (c.nt - 1);
     B1Out out;
-    out.part = (char*)dqpart + (size_t)((int64_t)bh * nkb + kblk) * (size_t)(1 + 64 * c.nt) * 128;
+    out.part = make_rsrc((const char*)dqpart + (size_t)((int64_t)bh * nkb + kblk) * (size_t)(1 + 64 * c.nt) * 128,
+                         (uint32_t)(1 + 64 * c.nt) * 128);
     out.qb = c.wave >> 1;
     out.db = c.wave & 1;
     out.sc = scale / DsScale<T>::v;
@@ -315,9 +365,6 @@ __global__ __launch_bounds__(256, 1) void attn_bwd1_kernel(const T* __restrict__
             *(frag*)(kimg + row * 128 + (((2 * s + c.h) ^ xsw(row)) << 4)) = v;
         }
     }
-    // this lane's dS^T image write base (block 0's key row)
-    const int dsrow = c.wave * 64 + c.l32;
-    const uint32_t dsw = (uint32_t)(dsrow * 128 + 8 * (c.h ^ ds_unit_swz(dsrow)));
 
     // query 0 (CLS) folded in on the VALU, as dkdv6
 #pragma unroll
@@ -345,6 +392,13 @@ __global__ __launch_bounds__(256, 1) void attn_bwd1_kernel(const T* __restrict__
 #pragma unroll
         for (int s = 0; s < 4; ++s) frag_ds_scale<T>(k.vf[kb][s]);
     }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            k.kf[kb][s] = to_agpr(k.kf[kb][s]);
+            k.vf[kb][s] = to_agpr(k.vf[kb][s]);
+        }
 
     wait_vmcnt<2 * (X::PIECES + 1)>();  // slice 0 landed (slices 1, 2 in flight)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the K image
@@ -355,17 +409,16 @@ __global__ __launch_bounds__(256, 1) void attn_bwd1_kernel(const T* __restrict__
     seeds(S0, P0, smem, 0, c.h);
     int t = 0;
     for (; t + 4 <= c.nt; t += 4) {
-        step1<T, 0>(c, k, t, qa, ga, S0, P0, dq, out, kimg, dsimg, dsw);
-        step1<T, 1>(c, k, t + 1, qa, ga, S0, P0, dq, out, kimg, dsimg, dsw);
-        step1<T, 2>(c, k, t + 2, qa, ga, S0, P0, dq, out, kimg, dsimg, dsw);
-        step1<T, 3>(c, k, t + 3, qa, ga, S0, P0, dq, out, kimg, dsimg, dsw);
+        step1<T, 0>(c, k, t, qa, ga, S0, P0, dq, out, kimg, dsimg);
+        step1<T, 1>(c, k, t + 1, qa, ga, S0, P0, dq, out, kimg, dsimg);
+        step1<T, 2>(c, k, t + 2, qa, ga, S0, P0, dq, out, kimg, dsimg);
+        step1<T, 3>(c, k, t + 3, qa, ga, S0, P0, dq, out, kimg, dsimg);
     }
-    if (t < c.nt) step1<T, 0>(c, k, t++, qa, ga, S0, P0, dq, out, kimg, dsimg, dsw);
-    if (t < c.nt) step1<T, 1>(c, k, t++, qa, ga, S0, P0, dq, out, kimg, dsimg, dsw);
-    if (t < c.nt) step1<T, 2>(c, k, t++, qa, ga, S0, P0, dq, out, kimg, dsimg, dsw);
+    if (t < c.nt) step1<T, 0>(c, k, t++, qa, ga, S0, P0, dq, out, kimg, dsimg);
+    if (t < c.nt) step1<T, 1>(c, k, t++, qa, ga, S0, P0, dq, out, kimg, dsimg);
+    if (t < c.nt) step1<T, 2>(c, k, t++, qa, ga, S0, P0, dq, out, kimg, dsimg);
     // the last slice's dQ partial
-    store_half_t21<T>((T*)(out.part + (size_t)(64 * (c.nt - 1) + 1 + out.qb * 32 + c.l32) * 128) + out.db * 32, dq,
-                      out.sc, c.h);
+    store_dq_half<T>(out.part, (uint32_t)(64 * (c.nt - 1) + 1 + out.qb * 32), out.db, dq, out.sc);
     wait_vmcnt<0>();
     if (r0q != nullptr) {
         // CLS-row fold (dkdv6's): this block's share of dQ_0 += dS_0 k, one partial per workgroup
@@ -382,6 +435,377 @@ __global__ __launch_bounds__(256, 1) void attn_bwd1_kernel(const T* __restrict__
             float sum = 0.f;
 #pragma unroll
             for (int w = 0; w < NW; ++w) sum += part[w * 64 + lane];
+            r0q[((int64_t)bh * nkb + kblk) * 64 + lane] = sum;
+        }
+    }
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3"
+                 : "+a"(k.dk[0][0]), "+a"(k.dk[0][1]), "+a"(k.dk[1][0]), "+a"(k.dk[1][1]), "+a"(k.dv[0][0]),
+                   "+a"(k.dv[0][1]), "+a"(k.dv[1][0]), "+a"(k.dv[1][1]));
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+        if (kok[kb]) {
+            T* rk = dqkv + ((int64_t)b * N + key[kb]) * ld + C + hd * HD;
+            store_row_t21<T>(rk, k.dk[kb], dk_scale / DsScale<T>::v, c.h);
+            store_row_t21<T>(rk + C, k.dv[kb], 1.0f, c.h);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------- the pipelined sweep (option 10)
+// attn_bwd1b_kernel: attn_bwd1_kernel's arithmetic (dK / dV bit for bit; dQ the same products summed
+// in the same per-tile order) with the slice's dQ^T tile taken OFF its own barrier: the dS^T image is
+// double-buffered and the 16 dQ MFMAs of slice t - 1 are spread over the eight regions of step t
+// (two per region, operands read at the region's start, the MFMAs at its end, the tile's accumulator
+// in AGPRs), beside the softmax VALU that leaves the matrix pipe idle in dkdv6.  LDS for the second
+// dS^T buffer comes from a 3-slot ring (DMA one slice ahead instead of two) and from reading the S
+// chains' K fragments out of the K image (4 ds_read_b128 per block) instead of holding them in 32
+// VGPRs.
+constexpr int B2_RING = 3 * B1Ring::SLOT;
+constexpr int B2_SMEM = B2_RING + B1_KB * 4;  // ring + the CLS-row fold's weights
+static_assert(B2_SMEM + 3 * B1_IMG <= 160 * 1024, "LDS");
+
+// acc (AGPR) = x . b (FIRST: C = 0) or acc += x . b, the A operand x (a K^T fragment) held in AGPRs
+template <typename T, bool FIRST>
+__device__ __forceinline__ void mfma_dq(f32x16& acc, const typename Mfma<T>::frag& x, const typename Mfma<T>::frag& b) {
+    if constexpr (FIRST) {
+        if constexpr (std::is_same<T, bf16>::value)
+            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=a"(acc) : "a"(x), "v"(b));
+        else
+            asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=a"(acc) : "a"(x), "v"(b));
+    } else {
+        if constexpr (std::is_same<T, bf16>::value)
+            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "a"(x), "v"(b));
+        else
+            asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(acc) : "a"(x), "v"(b));
+    }
+}
+
+// the K fragments of block kb (B operands of the S chains) from the K image
+template <typename T>
+__device__ __forceinline__ void load_kf(typename Mfma<T>::frag (&kf)[4], const char* kimg, int wave, int kb, int l32,
+                                        int h) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) kf[s] = row_frag<T>(kimg, wave * 64 + kb * 32 + l32, 2 * s + h);
+}
+
+struct DqOps {
+    int db;           // this wave's d block
+    DsTrBase dsb;     // dS^T image read addresses (its query block)
+};
+
+// the dS^T operands of dQ k-steps KS, KS + 1 (keys 16 KS .. 16 KS + 31) of the previous slice's tile
+template <typename T, int KS>
+__device__ __forceinline__ void dq_load2(typename Mfma<T>::frag (&b)[2], const char* dsprev, const DqOps& d) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) b[j] = trds_frag<T>(dsprev, d.dsb, (KS + j) >> 1, (KS + j) & 1);
+}
+
+// k-steps KS, KS + 1: the K^T operands are the wave's resident AGPR fragments kt[KS], kt[KS + 1]
+template <typename T, int KS, bool FIRST>
+__device__ __forceinline__ void dq_mma2(f32x16& acc, const typename Mfma<T>::frag (&kt)[16],
+                                        const typename Mfma<T>::frag (&b)[2]) {
+    mfma_dq<T, FIRST>(acc, kt[KS], b[0]);
+    mfma_dq<T, false>(acc, kt[KS + 1], b[1]);
+}
+
+// one 32-query sub-slice (sub6's regions and arithmetic) + this sub-slice's dS^T into buffer dscur +
+// k-steps 8 SUB .. 8 SUB + 7 of the previous slice's dQ^T tile from buffer dsprev.  kf0 arrives holding
+// block 0's K fragments and leaves holding them again (re-read in R4 for the next sub-slice)
+template <typename T, int SUB>
+__device__ __forceinline__ void sub2(K6<T>& k, int h, int l32, int lane, int wave, const char* base, const char* nb,
+                                     int nsub, typename Mfma<T>::frag (&qa)[4], typename Mfma<T>::frag (&ga)[4],
+                                     typename Mfma<T>::frag (&kf0)[4], f32x16& S0, f32x16& P0, f32x16& dq,
+                                     const typename Mfma<T>::frag (&kt)[16], const char* kimg, char* dscur,
+                                     const char* dsprev, const DqOps& dqo) {
+    typedef typename Mfma<T>::frag frag;
+    f32x16 S1, P1;
+    frag gt[2][2], qt[2][2], kf1[4], dbf[2];
+    Packs k0, k1;
+    // ---- R1
+    fence();
+    dq_load2<T, 8 * SUB>(dbf, dsprev, dqo);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        S0 = Mfma<T>::mma(qa[s], kf0[s], S0);
+        asm volatile("" : "+a"(k.vf[0][s]));  // V fragments stay in AGPRs (MFMA B operands)
+        P0 = Mfma<T>::mma(ga[s], k.vf[0][s], P0);
+    }
+    load_t<T>(gt, qt, base, SUB, lane);
+    seeds(S1, P1, base, SUB, h);
+    load_kf<T>(kf1, kimg, wave, 1, l32, h);
+    dq_mma2<T, 8 * SUB, SUB == 0>(dq, kt, dbf);
+    fence();
+    // ---- R2
+    dq_load2<T, 8 * SUB + 2>(dbf, dsprev, dqo);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        S1 = Mfma<T>::mma(qa[s], kf1[s], S1);
+        fin_chunk<T>(S0, P0, k0, 2 * s);
+        fence();
+        asm volatile("" : "+a"(k.vf[1][s]));
+        P1 = Mfma<T>::mma(ga[s], k.vf[1][s], P1);
+        fin_chunk<T>(S0, P0, k0, 2 * s + 1);
+        fence();
+    }
+    dq_mma2<T, 8 * SUB + 2, false>(dq, kt, dbf);
+    fence();
+    // ---- R3
+    dq_load2<T, 8 * SUB + 4>(dbf, dsprev, dqo);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        mfma_acc<T, false>(k.dv[0][0], gt[s][0], as_frag<T>(k0.p[s]));
+        fin_chunk<T>(S1, P1, k1, 4 * s);
+        fence();
+        mfma_acc<T, false>(k.dv[0][1], gt[s][1], as_frag<T>(k0.p[s]));
+        fin_chunk<T>(S1, P1, k1, 4 * s + 1);
+        fence();
+        mfma_acc<T, false>(k.dk[0][0], qt[s][0], as_frag<T>(k0.d[s]));
+        fin_chunk<T>(S1, P1, k1, 4 * s + 2);
+        fence();
+        mfma_acc<T, false>(k.dk[0][1], qt[s][1], as_frag<T>(k0.d[s]));
+        fin_chunk<T>(S1, P1, k1, 4 * s + 3);
+        fence();
+    }
+    load_qg<T>(qa, ga, nb, nsub, l32, h);
+    dq_mma2<T, 8 * SUB + 4, false>(dq, kt, dbf);
+    fence();
+    // ---- R4
+    dq_load2<T, 8 * SUB + 6>(dbf, dsprev, dqo);
+    const uint32_t dsw = ds_put_base(wave);
+    ds_put<SUB, 0>(dscur, dsw, k0.d);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        mfma_acc<T, true>(k.dv[1][0], gt[s][0], as_frag<T>(k1.p[s]));
+        mfma_acc<T, false>(k.dv[1][1], gt[s][1], as_frag<T>(k1.p[s]));
+        mfma_acc<T, false>(k.dk[1][0], qt[s][0], as_frag<T>(k1.d[s]));
+        mfma_acc<T, false>(k.dk[1][1], qt[s][1], as_frag<T>(k1.d[s]));
+    }
+    ds_put<SUB, 1>(dscur, dsw, k1.d);
+    seeds(S0, P0, nb, nsub, h);
+    load_kf<T>(kf0, kimg, wave, 0, l32, h);
+    dq_mma2<T, 8 * SUB + 6, false>(dq, kt, dbf);
+    fence();
+}
+
+// the dQ^T accumulator (AGPR, written by asm MFMAs) readable: >= 12 wait states after the last one
+__device__ __forceinline__ void dq_settle(f32x16& dq) { asm volatile("s_nop 7\n\ts_nop 7" : "+a"(dq)); }
+
+// slice t in ring slot Q = t % 3, its dS^T into buffer DB = t & 1:
+//   vmcnt(0) + lgkmcnt(0) + barrier (slice t + 1 and every wave's dS^T of slice t - 1 landed; every wave
+//   done with step t - 1, so slot (t - 1) % 3 and buffer DB are free); the dQ partial of slice t - 2
+//   (accumulated during step t - 1) stored; DMA of slice t + 2 into slot (t - 1) % 3; the two sub-slices
+template <typename T, int Q, int DB>
+__device__ __forceinline__ void step2(Dkv2Ctx<T, 4>& c, K6<T>& k, int t, typename Mfma<T>::frag (&qa)[4],
+                                      typename Mfma<T>::frag (&ga)[4], typename Mfma<T>::frag (&kf0)[4],
+                                      f32x16& S0, f32x16& P0, f32x16& dq, const B1Out& out, const DqOps& dqo,
+                                      const typename Mfma<T>::frag (&kt)[16], const char* kimg, char* dsimg) {
+    typedef Dkv2Ctx<T, 4> X;
+    wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t >= 2) {  // wave-uniform
+        dq_settle(dq);
+        store_dq_half<T>(out.part, (uint32_t)(64 * (t - 2) + 1 + out.qb * 32), out.db, dq, out.sc);
+    }
+    dkv2_issue<T, 4>(c, t + 2 < c.nt ? t + 2 : c.nt - 1, (Q + 2) % 3);
+    const char* cur = c.smem + Q * X::SLOT;
+    const char* nxt = c.smem + ((Q + 1) % 3) * X::SLOT;
+    char* dscur = dsimg + DB * B1_IMG;
+    const char* dsprev = dsimg + (DB ^ 1) * B1_IMG;
+    sub2<T, 0>(k, c.h, c.l32, c.lane, c.wave, cur, cur, 1, qa, ga, kf0, S0, P0, dq, kt, kimg, dscur, dsprev, dqo);
+    sub2<T, 1>(k, c.h, c.l32, c.lane, c.wave, cur, nxt, 0, qa, ga, kf0, S0, P0, dq, kt, kimg, dscur, dsprev, dqo);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256, 1) void attn_bwd1b_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
+                                                            const float* __restrict__ lse,
+                                                            const float* __restrict__ delta,
+                                                            const float* __restrict__ nlse,
+                                                            const float* __restrict__ ndelta, T* __restrict__ dqkv,
+                                                            T* __restrict__ dqpart, int N, int H, float dk_scale,
+                                                            float scale, float* __restrict__ r0q) {
+    constexpr int NW = B1_NW, KB = B1_KB;
+    typedef Dkv2Ctx<T, NW> X;
+    typedef typename Mfma<T>::frag frag;
+    static_assert(X::SLOT == B1Ring::SLOT, "ring geometry");
+    __shared__ __attribute__((aligned(128))) char smem[B2_SMEM];
+    __shared__ __attribute__((aligned(128))) char kimg[B1_IMG];       // K image, swz layout
+    __shared__ __attribute__((aligned(128))) char dsimg[2 * B1_IMG];  // two dS^T images, ds_unit_swz layout
+    X c;
+    K6<T> k;
+    c.smem = smem;
+    c.lane = threadIdx.x & 63;
+    c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    c.h = c.lane >> 5;
+    c.l32 = c.lane & 31;
+    const int nkb = (N - 1 + KB - 1) / KB;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int kblk = tile % nkb, bh = tile / nkb, b = bh / H, hd = bh % H;
+    const int C = H * HD;
+    const int64_t ld = 3 * (int64_t)C;
+    const T* Bb = qkv + (int64_t)b * N * ld;
+    const T* dOb = dout + (int64_t)b * N * C;
+    c.ldq = (uint32_t)(ld * sizeof(T));
+    c.ldg = (uint32_t)(C * sizeof(T));
+    c.nt = (N - 1 + 63) / 64;
+    c.rem = N - 1 - 64 * (c.nt - 1);
+    B1Out out;
+    out.part = make_rsrc((const char*)dqpart + (size_t)((int64_t)bh * nkb + kblk) * (size_t)(1 + 64 * c.nt) * 128,
+                         (uint32_t)(1 + 64 * c.nt) * 128);
+    out.qb = c.wave >> 1;
+    out.db = c.wave & 1;
+    out.sc = scale / DsScale<T>::v;
+    DqOps dqo;
+    dqo.db = out.db;
+    dqo.dsb = ds_tr_base(out.qb, c.lane);
+    int key[2];
+    bool kok[2];
+    frag kf[2][4];  // the prologue's copies (the CLS fold and the K image); the loop reads the image
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+        key[kb] = 1 + kblk * KB + c.wave * 64 + kb * 32 + c.l32;
+        kok[kb] = key[kb] < N;
+        const int kc = kok[kb] ? key[kb] : N - 1;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            kf[kb][s] = *(const frag*)(Bb + (int64_t)kc * ld + C + hd * HD + (2 * s + c.h) * 8);
+            k.vf[kb][s] = *(const frag*)(Bb + (int64_t)kc * ld + 2 * C + hd * HD + (2 * s + c.h) * 8);
+        }
+    }
+    frag q0[4], g0[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        q0[s] = *(const frag*)(Bb + hd * HD + (2 * s + c.h) * 8);
+        g0[s] = *(const frag*)(dOb + hd * HD + (2 * s + c.h) * 8);
+    }
+    typedef T t4 __attribute__((ext_vector_type(4)));
+    t4 q0d[2][4], g0d[2][4];
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            q0d[db][g] = *(const t4*)(Bb + hd * HD + db * 32 + 8 * g + 4 * c.h);
+            g0d[db][g] = *(const t4*)(dOb + hd * HD + db * 32 + 8 * g + 4 * c.h);
+        }
+    const float L0 = lse[(int64_t)bh * N], d0 = delta[(int64_t)bh * N];
+
+    c.rs = make_rsrc(Bb, (uint32_t)N * c.ldq);
+    c.rg = make_rsrc(dOb, (uint32_t)N * c.ldg);
+    c.rl = make_rsrc(nlse + (int64_t)bh * N, (uint32_t)N * 4);
+    c.rd = make_rsrc(ndelta + (int64_t)bh * N, (uint32_t)N * 4);
+    const bool q_wave = c.wave * X::PIECES < 8;
+    c.rmine = q_wave ? c.rs : c.rg;
+    c.ldmine = q_wave ? c.ldq : c.ldg;
+#pragma unroll
+    for (int i = 0; i < X::PIECES; ++i) {
+        const int piece = c.wave * X::PIECES + i;
+        const int r = (piece & 7) * 8 + (c.lane >> 3);
+        const uint32_t chunk = (uint32_t)(((c.lane & 7) ^ xsw(r)) * 16);
+        c.voff[i] = piece < 8 ? (uint32_t)r * c.ldq + chunk + (uint32_t)(hd * HD * sizeof(T))
+                              : (uint32_t)r * c.ldg + chunk + (uint32_t)(hd * HD * sizeof(T));
+    }
+    dkv2_issue<T, NW>(c, 0, 0);
+    dkv2_issue<T, NW>(c, c.nt > 1 ? 1 : 0, 1);
+
+    // the K image: this wave's 64 key rows, zero rows for keys past N (the S chains of those keys then
+    // see zero keys; their dK / dV are not stored and their zero K rows add nothing to dQ)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+        const int row = c.wave * 64 + kb * 32 + c.l32;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            frag v = kf[kb][s];
+            if (!kok[kb])
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = (T)0.f;
+            *(frag*)(kimg + row * 128 + (((2 * s + c.h) ^ xsw(row)) << 4)) = v;
+        }
+    }
+    // query 0 (CLS) folded in on the VALU, as dkdv6
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+        float spart = 0.f, ppart = 0.f;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                spart += (float)q0[s][j] * (float)kf[kb][s][j];
+                ppart += (float)g0[s][j] * (float)k.vf[kb][s][j];
+            }
+        const float p0 = __builtin_amdgcn_exp2f(xhalf_sum(spart) - L0);
+        const float ds0 = p0 * (xhalf_sum(ppart) - d0) * DsScale<T>::v;
+        ((float*)(smem + B2_RING))[c.wave * 64 + kb * 32 + c.l32] = kok[kb] ? ds0 : 0.f;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    k.dv[kb][db][4 * g + e] = p0 * (float)g0d[db][g][e];
+                    k.dk[kb][db][4 * g + e] = ds0 * (float)q0d[db][g][e];
+                }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) frag_ds_scale<T>(k.vf[kb][s]);
+    }
+
+    wait_vmcnt<0>();  // slices 0, 1 landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the K image
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    frag qa[4], ga[4], kf0[4], kt[16];
+    f32x16 S0, P0, dq;
+    // the wave's K^T fragments of its d block over the 256 keys (dQ's A operands), resident in AGPRs
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) kt[ks] = to_agpr(tr_frag<T>(kimg, ks >> 1, ks & 1, dqo.db, c.lane));
+    load_qg<T>(qa, ga, smem, 0, c.l32, c.h);
+    seeds(S0, P0, smem, 0, c.h);
+    load_kf<T>(kf0, kimg, c.wave, 0, c.l32, c.h);
+    int t = 0;
+    for (; t + 6 <= c.nt; t += 6) {
+        step2<T, 0, 0>(c, k, t, qa, ga, kf0, S0, P0, dq, out, dqo, kt, kimg, dsimg);
+        step2<T, 1, 1>(c, k, t + 1, qa, ga, kf0, S0, P0, dq, out, dqo, kt, kimg, dsimg);
+        step2<T, 2, 0>(c, k, t + 2, qa, ga, kf0, S0, P0, dq, out, dqo, kt, kimg, dsimg);
+        step2<T, 0, 1>(c, k, t + 3, qa, ga, kf0, S0, P0, dq, out, dqo, kt, kimg, dsimg);
+        step2<T, 1, 0>(c, k, t + 4, qa, ga, kf0, S0, P0, dq, out, dqo, kt, kimg, dsimg);
+        step2<T, 2, 1>(c, k, t + 5, qa, ga, kf0, S0, P0, dq, out, dqo, kt, kimg, dsimg);
+    }
+    if (t < c.nt) step2<T, 0, 0>(c, k, t++, qa, ga, kf0, S0, P0, dq, out, dqo, kt, kimg, dsimg);
+    if (t < c.nt) step2<T, 1, 1>(c, k, t++, qa, ga, kf0, S0, P0, dq, out, dqo, kt, kimg, dsimg);
+    if (t < c.nt) step2<T, 2, 0>(c, k, t++, qa, ga, kf0, S0, P0, dq, out, dqo, kt, kimg, dsimg);
+    if (t < c.nt) step2<T, 0, 1>(c, k, t++, qa, ga, kf0, S0, P0, dq, out, dqo, kt, kimg, dsimg);
+    if (t < c.nt) step2<T, 1, 0>(c, k, t++, qa, ga, kf0, S0, P0, dq, out, dqo, kt, kimg, dsimg);
+    // the last two dQ partials: slice nt - 2 (accumulated during the last step) and slice nt - 1 (its
+    // dS^T complete behind this barrier)
+    wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (c.nt >= 2) {
+        dq_settle(dq);
+        store_dq_half<T>(out.part, (uint32_t)(64 * (c.nt - 2) + 1 + out.qb * 32), out.db, dq, out.sc);
+    }
+    {
+        f32x16 dql;
+        dq_tile<T>(dql, kimg, dsimg + ((c.nt - 1) & 1) * B1_IMG, out.qb, out.db);
+        store_dq_half<T>(out.part, (uint32_t)(64 * (c.nt - 1) + 1 + out.qb * 32), out.db, dql, out.sc);
+    }
+    wait_vmcnt<0>();
+    if (r0q != nullptr) {
+        // CLS-row fold (dkdv6's), the key rows read from the K image (same rows, same order)
+        __syncthreads();
+        const int lane = __lane_id();
+        const float* w = (const float*)(smem + B2_RING) + c.wave * 64;
+        float aq = 0.f;
+#pragma unroll 8
+        for (int r = 0; r < 64; ++r) aq += w[r] * (float)*(const T*)(kimg + swz(c.wave * 64 + r, lane));
+        float* part = (float*)smem;
+        part[c.wave * 64 + lane] = aq;
+        __syncthreads();
+        if (c.wave == 0) {
+            float sum = 0.f;
+#pragma unroll
+            for (int v = 0; v < NW; ++v) sum += part[v * 64 + lane];
             r0q[((int64_t)bh * nkb + kblk) * 64 + lane] = sum;
         }
     }
@@ -495,7 +919,10 @@ __global__ __launch_bounds__(256) void attn_bwd1_dq_reduce(const T* __restrict__
     const int64_t ld = 3 * (int64_t)C;
     const int64_t Np = 1 + 64 * (int64_t)((N - 1 + 63) / 64);
     const t8 kv = *(const t8*)(qkv + (int64_t)b * N * ld + C + hd * HD + c8);
-    const float w = ds0v[(int64_t)bh * N + q] * sc;
+    // bf16 partials are unscaled (store_dq_half): the key-0 term joins them unscaled and the sum is
+    // scaled once (sc is a power of two, so this equals scaling every term)
+    constexpr bool unscaled = std::is_same<T, bf16>::value;
+    const float w = ds0v[(int64_t)bh * N + q] * (unscaled ? 1.0f : sc);
     float acc[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[e] = w * (float)kv[e];
@@ -517,7 +944,7 @@ __global__ __launch_bounds__(256) void attn_bwd1_dq_reduce(const T* __restrict__
     }
     t8 r;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) r[e] = (T)acc[e];
+    for (int e = 0; e < 8; ++e) r[e] = (T)(unscaled ? acc[e] * sc : acc[e]);
     *(t8*)(dqkv + ((int64_t)b * N + q) * ld + hd * HD + c8) = r;
 }
 
@@ -528,9 +955,14 @@ void bwd1_launch(const void* qkv, const void* o, const void* dout, const float* 
     const int nkb = (N - 1 + B1_KB - 1) / B1_KB;
     attn_bwd1_prep_kernel<T><<<B * H * nqp, 256, 0, st>>>((const T*)qkv, (const T*)o, (const T*)dout, lse, delta, nstat,
                                                           ds0v, r0kv, N, H, nqp);
-    attn_bwd1_kernel<T><<<B * H * nkb, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, nstat,
-                                                     nstat + (int64_t)B * H * N, (T*)dqkv, (T*)dqpart, N, H,
-                                                     1.0f / LOG2E, scale, r0q);
+    if (dclip_option(DCLIP_OPT_ATTN_BWD_BLOCK) == 10)
+        attn_bwd1b_kernel<T><<<B * H * nkb, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, nstat,
+                                                          nstat + (int64_t)B * H * N, (T*)dqkv, (T*)dqpart, N, H,
+                                                          1.0f / LOG2E, scale, r0q);
+    else
+        attn_bwd1_kernel<T><<<B * H * nkb, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, nstat,
+                                                         nstat + (int64_t)B * H * N, (T*)dqkv, (T*)dqpart, N, H,
+                                                         1.0f / LOG2E, scale, r0q);
     const int nrb = (N - 1 + 31) / 32;
     attn_bwd1_dq_reduce<T><<<B * H * nrb, 256, 0, st>>>((const T*)dqpart, ds0v, (const T*)qkv, (T*)dqkv, N, H, nkb, nrb,
                                                         scale / DsScale<T>::v);

@@ -747,7 +747,8 @@ def test_attention_dkdv7_bitwise_dkdv6(B, H, N, dt, bwd_block):
 @pytest.mark.parametrize("B,H,N", [(3, 2, 257), (2, 2, 290), (2, 3, 803), (3, 2, 1345), (2, 2, 2049), (1, 2, 8193),
                                    (1, 1, 10659)])
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
-def test_attention_onepass_bwd(B, H, N, dt, bwd_block):
+@pytest.mark.parametrize("variant", [9, 10])
+def test_attention_onepass_bwd(B, H, N, dt, variant, bwd_block):
     """The one-pass backward (DCLIP_OPT_ATTN_BWD_BLOCK 9, round 6, attention_bwd1.hip): one key-major
     sweep computes dK, dV and per-key-block 16-bit dQ partials, an ordered pass sums them.  dK / dV of
     keys 1..N-1 are dkdv6's products on the same statistics (the prep kernel repeats the dQ pass's
@@ -762,7 +763,7 @@ def test_attention_onepass_bwd(B, H, N, dt, bwd_block):
     dout = torch.randn(B * N, C, device=DEV).to(dt)
     o, lse = O.attn_fwd(qkv, B, N, H, 64 ** -0.5)
     res = []
-    for v in (0, 9):
+    for v in (0, variant):
         bwd_block(v)
         res.append(O.attn_bwd(qkv, o, dout, lse, B, N, H, 64 ** -0.5).float())
     a, b = res
