@@ -200,7 +200,8 @@ __device__ __forceinline__ void dq_tile(f32x16& acc, const char* kimg, const cha
 // g = 0..3) as two 16-B buffer stores per lane (store_row_t21's permlane pairing): row `row0 + lane`
 // of the workgroup's partial block, columns 32 db .. 32 db + 31
 template <typename T>
-__device__ __forceinline__ void store_dq_half(rsrc_t rp, uint32_t row0, int db, const f32x16& acc, float scale) {
+__device__ __forceinline__ void store_dq_half(rsrc_t rp, uint32_t rs, uint32_t row0, int db, const f32x16& acc,
+                                              float scale) {
     typedef T t2 __attribute__((ext_vector_type(2)));
     unsigned w[4][2];
 #pragma unroll
@@ -214,8 +215,8 @@ __device__ __forceinline__ void store_dq_half(rsrc_t rp, uint32_t row0, int db, 
             w[g][j] = __builtin_bit_cast(unsigned, p);
         }
     const int lane = lane_now();
-    const uint32_t vo = (uint32_t)(((lane & 31) * 128) + 16 * (lane >> 5) + 64 * db);
-    const uint32_t so = row0 * 128;
+    const uint32_t vo = (uint32_t)(lane & 31) * rs + (uint32_t)(16 * (lane >> 5) + 64 * db);
+    const uint32_t so = row0 * rs;
     typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int G = 0; G < 4; G += 2) {
@@ -231,7 +232,8 @@ __device__ __forceinline__ void store_dq_half(rsrc_t rp, uint32_t row0, int db, 
 }
 
 struct B1Out {
-    rsrc_t part;       // this workgroup's partial block: [Np rows][64] T, rows = queries
+    rsrc_t part;       // this workgroup's partials: rows = queries, rs bytes apart (the key blocks of a
+    uint32_t rs;       // query are adjacent: [B*H][Np][nkb][64] T, so the reduction reads 4-KiB runs)
     int qb, db;        // this wave's dQ tile
     float sc;          // scale / DsScale
 };
@@ -250,7 +252,7 @@ __device__ __forceinline__ void step1(Dkv2Ctx<T, 4>& c, K6<T>& k, int t, typenam
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");  // no LDS access moves across a barrier
     if (t > 0)  // wave-uniform
-        store_dq_half<T>(out.part, (uint32_t)(64 * (t - 1) + 1 + out.qb * 32), out.db, dq, out.sc);
+        store_dq_half<T>(out.part, out.rs, (uint32_t)(64 * (t - 1) + 1 + out.qb * 32), out.db, dq, out.sc);
     dkv2_issue<T, 4>(c, t + 3 < c.nt ? t + 3 : c.nt - 1, (Q + 3) & 3);
     const char* cur = c.smem + Q * X::SLOT;
     const char* nxt = c.smem + ((Q + 1) & 3) * X::SLOT;
@@ -298,8 +300,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd1_kernel(const T* __restrict__
     c.nt = (N - 1 + 63) / 64;
     c.rem = N - 1 - 64 * (c.nt - 1);
     B1Out out;
-    out.part = make_rsrc((const char*)dqpart + (size_t)((int64_t)bh * nkb + kblk) * (size_t)(1 + 64 * c.nt) * 128,
-                         (uint32_t)(1 + 64 * c.nt) * 128);
+    out.rs = (uint32_t)nkb * 128;
+    out.part = make_rsrc((const char*)dqpart + ((size_t)bh * (size_t)(1 + 64 * c.nt) * nkb + kblk) * 128,
+                         (uint32_t)(1 + 64 * c.nt) * out.rs);
     out.qb = c.wave >> 1;
     out.db = c.wave & 1;
     out.sc = scale / DsScale<T>::v;
@@ -418,7 +421,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd1_kernel(const T* __restrict__
     if (t < c.nt) step1<T, 1>(c, k, t++, qa, ga, S0, P0, dq, out, kimg, dsimg);
     if (t < c.nt) step1<T, 2>(c, k, t++, qa, ga, S0, P0, dq, out, kimg, dsimg);
     // the last slice's dQ partial
-    store_dq_half<T>(out.part, (uint32_t)(64 * (c.nt - 1) + 1 + out.qb * 32), out.db, dq, out.sc);
+    store_dq_half<T>(out.part, out.rs, (uint32_t)(64 * (c.nt - 1) + 1 + out.qb * 32), out.db, dq, out.sc);
     wait_vmcnt<0>();
     if (r0q != nullptr) {
         // CLS-row fold (dkdv6's): this block's share of dQ_0 += dS_0 k, one partial per workgroup
@@ -460,9 +463,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd1_kernel(const T* __restrict__
 // dS^T buffer comes from a 3-slot ring (DMA one slice ahead instead of two) and from reading the S
 // chains' K fragments out of the K image (4 ds_read_b128 per block) instead of holding them in 32
 // VGPRs.
-constexpr int B2_RING = 3 * B1Ring::SLOT;
+constexpr int B2_RING = 4 * B1Ring::SLOT;
 constexpr int B2_SMEM = B2_RING + B1_KB * 4;  // ring + the CLS-row fold's weights
-static_assert(B2_SMEM + 3 * B1_IMG <= 160 * 1024, "LDS");
+static_assert(B2_SMEM + 2 * B1_IMG <= 160 * 1024, "LDS");
 
 // acc (AGPR) = x . b (FIRST: C = 0) or acc += x . b, the A operand x (a K^T fragment) held in AGPRs
 template <typename T, bool FIRST>
@@ -478,14 +481,6 @@ __device__ __forceinline__ void mfma_dq(f32x16& acc, const typename Mfma<T>::fra
         else
             asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(acc) : "a"(x), "v"(b));
     }
-}
-
-// the K fragments of block kb (B operands of the S chains) from the K image
-template <typename T>
-__device__ __forceinline__ void load_kf(typename Mfma<T>::frag (&kf)[4], const char* kimg, int wave, int kb, int l32,
-                                        int h) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) kf[s] = row_frag<T>(kimg, wave * 64 + kb * 32 + l32, 2 * s + h);
 }
 
 struct DqOps {
@@ -508,38 +503,62 @@ __device__ __forceinline__ void dq_mma2(f32x16& acc, const typename Mfma<T>::fra
     mfma_dq<T, false>(acc, kt[KS + 1], b[1]);
 }
 
+// the dQ^T accumulator (AGPR, written by asm MFMAs) readable: >= 12 wait states after the last one
+__device__ __forceinline__ void dq_settle(f32x16& dq) { asm volatile("s_nop 7\n\ts_nop 7" : "+a"(dq)); }
+
+// load_qg (dkdv_frag.h) with the four chunk offsets of a row derived from one base by XOR: chunk
+// (2s + h) ^ xsw(row) = 2s ^ (h ^ xsw(row)), so offset(s) = base ^ 32 s; the base passes through an
+// opaque asm, so the four offsets are not hoisted out of the loop as four live VGPRs
+template <typename T>
+__device__ __forceinline__ void load_qg_x(typename Mfma<T>::frag (&qa)[4], typename Mfma<T>::frag (&ga)[4],
+                                          const char* base, int sub, int l32, int h) {
+    uint32_t o = (uint32_t)(l32 * 128 + 16 * (h ^ xsw(l32)));
+    asm volatile("" : "+v"(o));
+    const char* Qt = base + sub * 32 * 128;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        qa[s] = *(const typename Mfma<T>::frag*)(Qt + (o ^ (32u * s)));
+        ga[s] = *(const typename Mfma<T>::frag*)(Qt + 8192 + (o ^ (32u * s)));
+    }
+}
+
 // one 32-query sub-slice (sub6's regions and arithmetic) + this sub-slice's dS^T into buffer dscur +
-// k-steps 8 SUB .. 8 SUB + 7 of the previous slice's dQ^T tile from buffer dsprev.  kf0 arrives holding
-// block 0's K fragments and leaves holding them again (re-read in R4 for the next sub-slice)
+// k-steps 8 SUB .. 8 SUB + 7 of the previous slice's dQ^T tile from buffer dsprev (two per region: the
+// dS^T operands read at the region's start, the MFMAs at its end)
 template <typename T, int SUB>
 __device__ __forceinline__ void sub2(K6<T>& k, int h, int l32, int lane, int wave, const char* base, const char* nb,
                                      int nsub, typename Mfma<T>::frag (&qa)[4], typename Mfma<T>::frag (&ga)[4],
-                                     typename Mfma<T>::frag (&kf0)[4], f32x16& S0, f32x16& P0, f32x16& dq,
-                                     const typename Mfma<T>::frag (&kt)[16], const char* kimg, char* dscur,
-                                     const char* dsprev, const DqOps& dqo) {
+                                     f32x16& S0, f32x16& P0, f32x16& dq, const typename Mfma<T>::frag (&kt)[16],
+                                     char* dscur, const char* dsprev, const DqOps& dqo, const B1Out* out = nullptr,
+                                     uint32_t store_row = 0xFFFFFFFFu) {
     typedef typename Mfma<T>::frag frag;
     f32x16 S1, P1;
-    frag gt[2][2], qt[2][2], kf1[4], dbf[2];
+    frag gt[2][2], qt[2][2], dbf[2];
     Packs k0, k1;
     // ---- R1
     fence();
     dq_load2<T, 8 * SUB>(dbf, dsprev, dqo);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-        S0 = Mfma<T>::mma(qa[s], kf0[s], S0);
+        S0 = Mfma<T>::mma(qa[s], k.kf[0][s], S0);
         asm volatile("" : "+a"(k.vf[0][s]));  // V fragments stay in AGPRs (MFMA B operands)
         P0 = Mfma<T>::mma(ga[s], k.vf[0][s], P0);
     }
+    if constexpr (SUB == 0) {
+        if (store_row != 0xFFFFFFFFu) {  // wave-uniform
+            dq_settle(dq);
+            store_dq_half<T>(out->part, out->rs, store_row, out->db, dq, out->sc);
+        }
+    }
     load_t<T>(gt, qt, base, SUB, lane);
     seeds(S1, P1, base, SUB, h);
-    load_kf<T>(kf1, kimg, wave, 1, l32, h);
     dq_mma2<T, 8 * SUB, SUB == 0>(dq, kt, dbf);
     fence();
     // ---- R2
     dq_load2<T, 8 * SUB + 2>(dbf, dsprev, dqo);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-        S1 = Mfma<T>::mma(qa[s], kf1[s], S1);
+        S1 = Mfma<T>::mma(qa[s], k.kf[1][s], S1);
         fin_chunk<T>(S0, P0, k0, 2 * s);
         fence();
         asm volatile("" : "+a"(k.vf[1][s]));
@@ -566,7 +585,7 @@ __device__ __forceinline__ void sub2(K6<T>& k, int h, int l32, int lane, int wav
         fin_chunk<T>(S1, P1, k1, 4 * s + 3);
         fence();
     }
-    load_qg<T>(qa, ga, nb, nsub, l32, h);
+    load_qg_x<T>(qa, ga, nb, nsub, l32, h);
     dq_mma2<T, 8 * SUB + 4, false>(dq, kt, dbf);
     fence();
     // ---- R4
@@ -582,39 +601,55 @@ __device__ __forceinline__ void sub2(K6<T>& k, int h, int l32, int lane, int wav
     }
     ds_put<SUB, 1>(dscur, dsw, k1.d);
     seeds(S0, P0, nb, nsub, h);
-    load_kf<T>(kf0, kimg, wave, 0, l32, h);
     dq_mma2<T, 8 * SUB + 6, false>(dq, kt, dbf);
     fence();
 }
 
-// the dQ^T accumulator (AGPR, written by asm MFMAs) readable: >= 12 wait states after the last one
-__device__ __forceinline__ void dq_settle(f32x16& dq) { asm volatile("s_nop 7\n\ts_nop 7" : "+a"(dq)); }
-
-// slice t in ring slot Q = t % 3, its dS^T into buffer DB = t & 1:
-//   vmcnt(0) + lgkmcnt(0) + barrier (slice t + 1 and every wave's dS^T of slice t - 1 landed; every wave
-//   done with step t - 1, so slot (t - 1) % 3 and buffer DB are free); the dQ partial of slice t - 2
-//   (accumulated during step t - 1) stored; DMA of slice t + 2 into slot (t - 1) % 3; the two sub-slices
+// slice t in ring slot Q = t % 4, its dS^T into buffer DB = t & 1:
+//   vmcnt (slice t + 1 landed, t + 2 in flight, as dkdv6) + lgkmcnt(0) + barrier (every wave's dS^T of
+//   slice t - 1 written; every wave done with step t - 1, so slot (t + 3) % 4 and buffer DB are free);
+//   the dQ partial of slice t - 2 (accumulated during step t - 1) stored; DMA of slice t + 3; the two
+//   sub-slices, which also accumulate slice t - 1's dQ^T tile
 template <typename T, int Q, int DB>
 __device__ __forceinline__ void step2(Dkv2Ctx<T, 4>& c, K6<T>& k, int t, typename Mfma<T>::frag (&qa)[4],
-                                      typename Mfma<T>::frag (&ga)[4], typename Mfma<T>::frag (&kf0)[4],
-                                      f32x16& S0, f32x16& P0, f32x16& dq, const B1Out& out, const DqOps& dqo,
-                                      const typename Mfma<T>::frag (&kt)[16], const char* kimg, char* dsimg) {
+                                      typename Mfma<T>::frag (&ga)[4], f32x16& S0, f32x16& P0, f32x16& dq,
+                                      const B1Out& out, const DqOps& dqo, const typename Mfma<T>::frag (&kt)[16],
+                                      char* dsimg) {
     typedef Dkv2Ctx<T, 4> X;
-    wait_vmcnt<0>();
+    wait_vmcnt<X::PIECES + 1>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t >= 2) {  // wave-uniform
-        dq_settle(dq);
-        store_dq_half<T>(out.part, (uint32_t)(64 * (t - 2) + 1 + out.qb * 32), out.db, dq, out.sc);
-    }
-    dkv2_issue<T, 4>(c, t + 2 < c.nt ? t + 2 : c.nt - 1, (Q + 2) % 3);
+    dkv2_issue<T, 4>(c, t + 3 < c.nt ? t + 3 : c.nt - 1, (Q + 3) & 3);
     const char* cur = c.smem + Q * X::SLOT;
-    const char* nxt = c.smem + ((Q + 1) % 3) * X::SLOT;
+    const char* nxt = c.smem + ((Q + 1) & 3) * X::SLOT;
     char* dscur = dsimg + DB * B1_IMG;
     const char* dsprev = dsimg + (DB ^ 1) * B1_IMG;
-    sub2<T, 0>(k, c.h, c.l32, c.lane, c.wave, cur, cur, 1, qa, ga, kf0, S0, P0, dq, kt, kimg, dscur, dsprev, dqo);
-    sub2<T, 1>(k, c.h, c.l32, c.lane, c.wave, cur, nxt, 0, qa, ga, kf0, S0, P0, dq, kt, kimg, dscur, dsprev, dqo);
+    // the dQ partial of slice t - 2 is stored from sub-slice 0's R1, beside its S / dP chains
+    sub2<T, 0>(k, c.h, c.l32, c.lane, c.wave, cur, cur, 1, qa, ga, S0, P0, dq, kt, dscur, dsprev, dqo, &out,
+               t >= 2 ? (uint32_t)(64 * (t - 2) + 1 + out.qb * 32) : 0xFFFFFFFFu);
+    sub2<T, 1>(k, c.h, c.l32, c.lane, c.wave, cur, nxt, 0, qa, ga, S0, P0, dq, kt, dscur, dsprev, dqo);
+}
+
+// the last slice's dQ^T tile (no slice follows to hide it in): 16 MFMAs on the resident K^T fragments
+template <typename T>
+__device__ __forceinline__ void dq_tile_kt(f32x16& acc, const typename Mfma<T>::frag (&kt)[16], const char* dsimg,
+                                           const DqOps& dqo) {
+    typename Mfma<T>::frag b[2];
+    dq_load2<T, 0>(b, dsimg, dqo);
+    dq_mma2<T, 0, true>(acc, kt, b);
+#pragma unroll
+    for (int ks = 2; ks < 16; ks += 2) {
+        switch (ks) {  // KS is a template argument
+            case 2: dq_load2<T, 2>(b, dsimg, dqo); dq_mma2<T, 2, false>(acc, kt, b); break;
+            case 4: dq_load2<T, 4>(b, dsimg, dqo); dq_mma2<T, 4, false>(acc, kt, b); break;
+            case 6: dq_load2<T, 6>(b, dsimg, dqo); dq_mma2<T, 6, false>(acc, kt, b); break;
+            case 8: dq_load2<T, 8>(b, dsimg, dqo); dq_mma2<T, 8, false>(acc, kt, b); break;
+            case 10: dq_load2<T, 10>(b, dsimg, dqo); dq_mma2<T, 10, false>(acc, kt, b); break;
+            case 12: dq_load2<T, 12>(b, dsimg, dqo); dq_mma2<T, 12, false>(acc, kt, b); break;
+            default: dq_load2<T, 14>(b, dsimg, dqo); dq_mma2<T, 14, false>(acc, kt, b); break;
+        }
+    }
 }
 
 template <typename T>
@@ -630,8 +665,10 @@ __global__ __launch_bounds__(256, 1) void attn_bwd1b_kernel(const T* __restrict_
     typedef typename Mfma<T>::frag frag;
     static_assert(X::SLOT == B1Ring::SLOT, "ring geometry");
     __shared__ __attribute__((aligned(128))) char smem[B2_SMEM];
-    __shared__ __attribute__((aligned(128))) char kimg[B1_IMG];       // K image, swz layout
-    __shared__ __attribute__((aligned(128))) char dsimg[2 * B1_IMG];  // two dS^T images, ds_unit_swz layout
+    // two dS^T images (ds_unit_swz layout); the prologue's K image (swz layout, read once into the
+    // resident K^T fragments) lives in the second, which step 1 overwrites
+    __shared__ __attribute__((aligned(128))) char dsimg[2 * B1_IMG];
+    char* kimg = dsimg + B1_IMG;
     X c;
     K6<T> k;
     c.smem = smem;
@@ -651,8 +688,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd1b_kernel(const T* __restrict_
     c.nt = (N - 1 + 63) / 64;
     c.rem = N - 1 - 64 * (c.nt - 1);
     B1Out out;
-    out.part = make_rsrc((const char*)dqpart + (size_t)((int64_t)bh * nkb + kblk) * (size_t)(1 + 64 * c.nt) * 128,
-                         (uint32_t)(1 + 64 * c.nt) * 128);
+    out.rs = (uint32_t)nkb * 128;
+    out.part = make_rsrc((const char*)dqpart + ((size_t)bh * (size_t)(1 + 64 * c.nt) * nkb + kblk) * 128,
+                         (uint32_t)(1 + 64 * c.nt) * out.rs);
     out.qb = c.wave >> 1;
     out.db = c.wave & 1;
     out.sc = scale / DsScale<T>::v;
@@ -661,7 +699,6 @@ __global__ __launch_bounds__(256, 1) void attn_bwd1b_kernel(const T* __restrict_
     dqo.dsb = ds_tr_base(out.qb, c.lane);
     int key[2];
     bool kok[2];
-    frag kf[2][4];  // the prologue's copies (the CLS fold and the K image); the loop reads the image
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
         key[kb] = 1 + kblk * KB + c.wave * 64 + kb * 32 + c.l32;
@@ -669,7 +706,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd1b_kernel(const T* __restrict_
         const int kc = kok[kb] ? key[kb] : N - 1;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-            kf[kb][s] = *(const frag*)(Bb + (int64_t)kc * ld + C + hd * HD + (2 * s + c.h) * 8);
+            k.kf[kb][s] = *(const frag*)(Bb + (int64_t)kc * ld + C + hd * HD + (2 * s + c.h) * 8);
             k.vf[kb][s] = *(const frag*)(Bb + (int64_t)kc * ld + 2 * C + hd * HD + (2 * s + c.h) * 8);
         }
     }
@@ -707,15 +744,16 @@ __global__ __launch_bounds__(256, 1) void attn_bwd1b_kernel(const T* __restrict_
     }
     dkv2_issue<T, NW>(c, 0, 0);
     dkv2_issue<T, NW>(c, c.nt > 1 ? 1 : 0, 1);
+    dkv2_issue<T, NW>(c, c.nt > 2 ? 2 : c.nt - 1, 2);
 
-    // the K image: this wave's 64 key rows, zero rows for keys past N (the S chains of those keys then
-    // see zero keys; their dK / dV are not stored and their zero K rows add nothing to dQ)
+    // the K image: this wave's 64 key rows, zero rows for keys past N (their dK / dV are not stored and
+    // their zero K^T columns add nothing to dQ)
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
         const int row = c.wave * 64 + kb * 32 + c.l32;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-            frag v = kf[kb][s];
+            frag v = k.kf[kb][s];
             if (!kok[kb])
 #pragma unroll
                 for (int j = 0; j < 8; ++j) v[j] = (T)0.f;
@@ -730,7 +768,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd1b_kernel(const T* __restrict_
         for (int s = 0; s < 4; ++s)
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                spart += (float)q0[s][j] * (float)kf[kb][s][j];
+                spart += (float)q0[s][j] * (float)k.kf[kb][s][j];
                 ppart += (float)g0[s][j] * (float)k.vf[kb][s][j];
             }
         const float p0 = __builtin_amdgcn_exp2f(xhalf_sum(spart) - L0);
@@ -749,32 +787,27 @@ __global__ __launch_bounds__(256, 1) void attn_bwd1b_kernel(const T* __restrict_
         for (int s = 0; s < 4; ++s) frag_ds_scale<T>(k.vf[kb][s]);
     }
 
-    wait_vmcnt<0>();  // slices 0, 1 landed
+    wait_vmcnt<2 * (X::PIECES + 1)>();  // slice 0 landed (slices 1, 2 in flight)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the K image
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    frag qa[4], ga[4], kf0[4], kt[16];
+    frag qa[4], ga[4], kt[16];
     f32x16 S0, P0, dq;
     // the wave's K^T fragments of its d block over the 256 keys (dQ's A operands), resident in AGPRs
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) kt[ks] = to_agpr(tr_frag<T>(kimg, ks >> 1, ks & 1, dqo.db, c.lane));
     load_qg<T>(qa, ga, smem, 0, c.l32, c.h);
     seeds(S0, P0, smem, 0, c.h);
-    load_kf<T>(kf0, kimg, c.wave, 0, c.l32, c.h);
     int t = 0;
-    for (; t + 6 <= c.nt; t += 6) {
-        step2<T, 0, 0>(c, k, t, qa, ga, kf0, S0, P0, dq, out, dqo, kt, kimg, dsimg);
-        step2<T, 1, 1>(c, k, t + 1, qa, ga, kf0, S0, P0, dq, out, dqo, kt, kimg, dsimg);
-        step2<T, 2, 0>(c, k, t + 2, qa, ga, kf0, S0, P0, dq, out, dqo, kt, kimg, dsimg);
-        step2<T, 0, 1>(c, k, t + 3, qa, ga, kf0, S0, P0, dq, out, dqo, kt, kimg, dsimg);
-        step2<T, 1, 0>(c, k, t + 4, qa, ga, kf0, S0, P0, dq, out, dqo, kt, kimg, dsimg);
-        step2<T, 2, 1>(c, k, t + 5, qa, ga, kf0, S0, P0, dq, out, dqo, kt, kimg, dsimg);
+    for (; t + 4 <= c.nt; t += 4) {
+        step2<T, 0, 0>(c, k, t, qa, ga, S0, P0, dq, out, dqo, kt, dsimg);
+        step2<T, 1, 1>(c, k, t + 1, qa, ga, S0, P0, dq, out, dqo, kt, dsimg);
+        step2<T, 2, 0>(c, k, t + 2, qa, ga, S0, P0, dq, out, dqo, kt, dsimg);
+        step2<T, 3, 1>(c, k, t + 3, qa, ga, S0, P0, dq, out, dqo, kt, dsimg);
     }
-    if (t < c.nt) step2<T, 0, 0>(c, k, t++, qa, ga, kf0, S0, P0, dq, out, dqo, kt, kimg, dsimg);
-    if (t < c.nt) step2<T, 1, 1>(c, k, t++, qa, ga, kf0, S0, P0, dq, out, dqo, kt, kimg, dsimg);
-    if (t < c.nt) step2<T, 2, 0>(c, k, t++, qa, ga, kf0, S0, P0, dq, out, dqo, kt, kimg, dsimg);
-    if (t < c.nt) step2<T, 0, 1>(c, k, t++, qa, ga, kf0, S0, P0, dq, out, dqo, kt, kimg, dsimg);
-    if (t < c.nt) step2<T, 1, 0>(c, k, t++, qa, ga, kf0, S0, P0, dq, out, dqo, kt, kimg, dsimg);
+    if (t < c.nt) step2<T, 0, 0>(c, k, t++, qa, ga, S0, P0, dq, out, dqo, kt, dsimg);
+    if (t < c.nt) step2<T, 1, 1>(c, k, t++, qa, ga, S0, P0, dq, out, dqo, kt, dsimg);
+    if (t < c.nt) step2<T, 2, 0>(c, k, t++, qa, ga, S0, P0, dq, out, dqo, kt, dsimg);
     // the last two dQ partials: slice nt - 2 (accumulated during the last step) and slice nt - 1 (its
     // dS^T complete behind this barrier)
     wait_vmcnt<0>();
@@ -783,23 +816,21 @@ __global__ __launch_bounds__(256, 1) void attn_bwd1b_kernel(const T* __restrict_
     asm volatile("" ::: "memory");
     if (c.nt >= 2) {
         dq_settle(dq);
-        store_dq_half<T>(out.part, (uint32_t)(64 * (c.nt - 2) + 1 + out.qb * 32), out.db, dq, out.sc);
+        store_dq_half<T>(out.part, out.rs, (uint32_t)(64 * (c.nt - 2) + 1 + out.qb * 32), out.db, dq, out.sc);
     }
-    {
-        f32x16 dql;
-        dq_tile<T>(dql, kimg, dsimg + ((c.nt - 1) & 1) * B1_IMG, out.qb, out.db);
-        store_dq_half<T>(out.part, (uint32_t)(64 * (c.nt - 1) + 1 + out.qb * 32), out.db, dql, out.sc);
-    }
+    dq_tile_kt<T>(dq, kt, dsimg + ((c.nt - 1) & 1) * B1_IMG, dqo);
+    dq_settle(dq);
+    store_dq_half<T>(out.part, out.rs, (uint32_t)(64 * (c.nt - 1) + 1 + out.qb * 32), out.db, dq, out.sc);
     wait_vmcnt<0>();
     if (r0q != nullptr) {
-        // CLS-row fold (dkdv6's), the key rows read from the K image (same rows, same order)
+        // CLS-row fold (dkdv6's)
         __syncthreads();
         const int lane = __lane_id();
-        const float* w = (const float*)(smem + B2_RING) + c.wave * 64;
-        float aq = 0.f;
-#pragma unroll 8
-        for (int r = 0; r < 64; ++r) aq += w[r] * (float)*(const T*)(kimg + swz(c.wave * 64 + r, lane));
-        float* part = (float*)smem;
+        char* img = smem + c.wave * 64 * 128;
+        r0_put<T>(img, k.kf[0], lane & 31, lane >> 5);
+        r0_put<T>(img, k.kf[1], 32 + (lane & 31), lane >> 5);
+        const float aq = r0_colsum<T, 64>(img, (const float*)(smem + B2_RING) + c.wave * 64, lane);
+        float* part = (float*)(smem + NW * 64 * 128);
         part[c.wave * 64 + lane] = aq;
         __syncthreads();
         if (c.wave == 0) {
@@ -926,19 +957,19 @@ __global__ __launch_bounds__(256) void attn_bwd1_dq_reduce(const T* __restrict__
     float acc[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[e] = w * (float)kv[e];
-    const T* p = dqpart + ((int64_t)bh * nkb * Np + q) * 64 + c8;
+    const T* p = dqpart + ((int64_t)bh * Np + q) * nkb * 64 + c8;  // this query's nkb partials, adjacent
     int j = 0;
-    for (; j + 4 <= nkb; j += 4) {
-        t8 v[4];
+    for (; j + 8 <= nkb; j += 8) {
+        t8 v[8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = *(const t8*)(p + (int64_t)(j + u) * Np * 64);
+        for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load((const t8*)(p + (j + u) * 64));
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < 8; ++u)
 #pragma unroll
             for (int e = 0; e < 8; ++e) acc[e] += (float)v[u][e];
     }
     for (; j < nkb; ++j) {
-        const t8 v = *(const t8*)(p + (int64_t)j * Np * 64);
+        const t8 v = __builtin_nontemporal_load((const t8*)(p + j * 64));
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[e] += (float)v[e];
     }
