@@ -613,7 +613,10 @@ def main():
         # per launch, 2.5x the forward's): it is the headline roofline whenever it ran
         rf_bwd = None
         if n_ab:
-            rf_bwd = {"kernel": "attn_bwd_dq2_kernel + attn_bwd_dkdv6_kernel (+ CLS-row fold merge)" if cls_split
+            fp8_bwd = args.attn_fp8 and ops.ATTN_BWD_FP8
+            rf_bwd = {"kernel": "attn_bwd1_prep_kernel + attn_bwd1b_kernel + attn_bwd1_dq_reduce (+ CLS-row fold merge)"
+                      if cls_split and not fp8_bwd else
+                      "attn_bwd_dq2_kernel + attn_bwd_dkdv8_kernel (+ pack, CLS-row fold merge)" if cls_split
                       else "attn_bwd_dq_kernel + attn_bwd_dkdv_kernel",
                       "bound": "mfma", "achieved": round(ach_b, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                       "frac": round(ach_b / PEAK_BF16_TFLOPS, 4), "traffic": traffic_b,

@@ -2472,11 +2472,12 @@ bool bwd2_launch(const void* qkv, const void* o, const void* dout, const float* 
     float* ws0 = delta + (int64_t)B * H * N;
     float* nstat = ws0 + (int64_t)B * H * ((N + 63) / 64) * 192;  // [-lse | -delta], B*H*N each
     const bool dq4 = dclip_option(DCLIP_OPT_ATTN_DQ_WAVES) == 4;
-    if ((bwd_block == 9 || bwd_block == 10) && f8ws == nullptr) {
-        // the one-pass backward (attention_bwd1.hip): prep (delta, statistics, key 0's terms), one
-        // key-major sweep for dK, dV and per-key-block dQ partials, the ordered dQ reduction; then
-        // the CLS row's merge as the two-pass path.  Workspace past the two-pass part: dS_q0 (B*H*N
-        // floats), then the partials (attn_bwd1_part_bytes, 256-B aligned)
+    if ((bwd_block == 0 || bwd_block == 9 || bwd_block == 10) && f8ws == nullptr) {
+        // default since round 6: the one-pass backward (attention_bwd1.hip): prep (delta, statistics,
+        // key 0's terms), one key-major sweep for dK, dV and per-key-block dQ partials, the ordered dQ
+        // reduction; then the CLS row's merge as the two-pass path (-3 % per launch, -1.1 % per train
+        // step against dq2 + dkdv6, profiles/r06/r6z, r6w).  Workspace past the two-pass part: dS_q0
+        // (B*H*N floats), then the partials (attn_bwd1_part_bytes, 256-B aligned)
         const int64_t bhn = (int64_t)B * H * N;
         float* ds0v = nstat + 2 * bhn;
         void* part = (void*)(((uintptr_t)(ds0v + bhn) + 255) & ~(uintptr_t)255);
@@ -2490,8 +2491,9 @@ bool bwd2_launch(const void* qkv, const void* o, const void* dout, const float* 
         return true;
     }
     if (bwd_block == 0 || bwd_block == 6 || bwd_block == 7 || bwd_block == 8) {
-        // default: the CLS row's sums folded into the two passes' epilogues (partials in ws0) and
-        // one merge; 64 keys per wave, one wave per SIMD, AGPR dK / dV
+        // the two-pass backward (option 6; and the fp8 backward's dQ pass under the default): the CLS
+        // row's sums folded into the two passes' epilogues (partials in ws0) and one merge; 64 keys per
+        // wave, one wave per SIMD, AGPR dK / dV
         const int nq = (N - 1 + (dq4 ? 127 : 255)) / (dq4 ? 128 : 256), nkb = (N - 1 + 255) / 256;
         float* r0kv = ws0;
         float* r0q = ws0 + (int64_t)B * H * nq * 128;
@@ -2612,12 +2614,17 @@ extern "C" int dclip_attn_fwd(int dt, const void* qkv, void* o, float* lse, int 
     return 0;
 }
 
+// delta (B*H*N) + the CLS-split row-0 partials (B*H*ceil(N/64)*192) + the negated statistics the
+// CLS-split dK/dV pass reads (-lse, -delta: 2*B*H*N)
+static int64_t bwd_ws_two_pass(int B, int N, int H) {
+    return 3 * (int64_t)B * H * N + (int64_t)B * H * ((N + 63) / 64) * 192;
+}
+
 extern "C" int64_t dclip_attn_bwd_workspace(int B, int N, int H) {
-    // delta (B*H*N) + the CLS-split row-0 partials (B*H*ceil(N/64)*192) + the negated
-    // statistics the CLS-split dK/dV pass reads (-lse, -delta: 2*B*H*N)
-    const int64_t two_pass = 3 * (int64_t)B * H * N + (int64_t)B * H * ((N + 63) / 64) * 192;
-    // the one-pass backward (DCLIP_OPT_ATTN_BWD_BLOCK 9): + dS_q0 (B*H*N) + the dQ partials
-    if ((dclip_option(DCLIP_OPT_ATTN_BWD_BLOCK) == 9 || dclip_option(DCLIP_OPT_ATTN_BWD_BLOCK) == 10) && N >= 257)
+    const int64_t two_pass = bwd_ws_two_pass(B, N, H);
+    // the one-pass backward (the default, options 9 / 10): + dS_q0 (B*H*N) + the dQ partials
+    const int blk = dclip_option(DCLIP_OPT_ATTN_BWD_BLOCK);
+    if ((blk == 0 || blk == 9 || blk == 10) && N >= 257 && dclip_option(DCLIP_OPT_ATTN_BWD_KERNEL) != 1)
         return two_pass + (int64_t)B * H * N + (attn_bwd1_part_bytes(B, N, H) + 3) / 4 + 64;
     return two_pass;
 }
@@ -2636,7 +2643,7 @@ extern "C" int dclip_attn_bwd(int dt, const void* qkv, const void* o, const void
 
 // configs[4]'s backward (include/dclip.h): dclip_attn_bwd's workspace, then the fp8 images
 extern "C" int64_t dclip_attn_bwd_fp8_workspace(int B, int N, int H) {
-    return dclip_attn_bwd_workspace(B, N, H) + (attn_bwd_fp8_ws_bytes(B, N, H) + 3) / 4 + 64;
+    return bwd_ws_two_pass(B, N, H) + (attn_bwd_fp8_ws_bytes(B, N, H) + 3) / 4 + 64;
 }
 
 extern "C" int dclip_attn_bwd_fp8(int dt, const void* qkv, const void* o, const void* dout, const float* lse, float* ws,
@@ -2649,7 +2656,7 @@ extern "C" int dclip_attn_bwd_fp8(int dt, const void* qkv, const void* o, const 
                      "dclip_attn_bwd_fp8: N too large for the fp8 image ring");
     hipStream_t st = (hipStream_t)stream;
     // the fp8 images past dclip_attn_bwd's part, rounded up to 256 B
-    const int64_t w16 = dclip_attn_bwd_workspace(B, N, H);
+    const int64_t w16 = bwd_ws_two_pass(B, N, H);
     void* f8 = (void*)(((uintptr_t)(ws + w16) + 255) & ~(uintptr_t)255);
     if (dt == DCLIP_BF16) bwd_launch<bf16>(qkv, o, dout, lse, ws, dqkv, B, N, H, scale, st, f8);
     else bwd_launch<f16>(qkv, o, dout, lse, ws, dqkv, B, N, H, scale, st, f8);

@@ -1,4 +1,5 @@
-// One-pass CLS-split attention backward (DCLIP_OPT_ATTN_BWD_BLOCK 9): dK, dV AND dQ from a single
+// One-pass CLS-split attention backward (the default since round 6; DCLIP_OPT_ATTN_BWD_BLOCK 0 / 10, and 9
+// for the unpipelined sweep attn_bwd1_kernel): dK, dV AND dQ from a single
 // key-major sweep, so every P / dS element is recomputed once (two-pass: twice) and the MFMA work is
 // 5 units (S, dP, dV, dK, dQ) instead of 7 (dQ pass: S, dP, dQ; dK/dV pass: S, dP, dV, dK).
 //
@@ -454,7 +455,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd1_kernel(const T* __restrict__
     }
 }
 
-// ---------------------------------------------------------------------------- the pipelined sweep (option 10)
+// ---------------------------------------------------------------------------- the pipelined sweep (default)
 // attn_bwd1b_kernel: attn_bwd1_kernel's arithmetic (dK / dV bit for bit; dQ the same products summed
 // in the same per-tile order) with the slice's dQ^T tile taken OFF its own barrier: the dS^T image is
 // double-buffered and the 16 dQ MFMAs of slice t - 1 are spread over the eight regions of step t
@@ -986,7 +987,7 @@ void bwd1_launch(const void* qkv, const void* o, const void* dout, const float* 
     const int nkb = (N - 1 + B1_KB - 1) / B1_KB;
     attn_bwd1_prep_kernel<T><<<B * H * nqp, 256, 0, st>>>((const T*)qkv, (const T*)o, (const T*)dout, lse, delta, nstat,
                                                           ds0v, r0kv, N, H, nqp);
-    if (dclip_option(DCLIP_OPT_ATTN_BWD_BLOCK) == 10)
+    if (dclip_option(DCLIP_OPT_ATTN_BWD_BLOCK) != 9)  // the pipelined sweep (default); 9: the barrier form
         attn_bwd1b_kernel<T><<<B * H * nkb, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, nstat,
                                                           nstat + (int64_t)B * H * N, (T*)dqkv, (T*)dqpart, N, H,
                                                           1.0f / LOG2E, scale, r0q);

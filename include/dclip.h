@@ -80,7 +80,7 @@ int dclip_abi_version(void);
 #define DCLIP_OPT_ATTN_DKDV_QS 5     /* dK/dV pass query rows per barrier: 64 (default) or 128 */
 #define DCLIP_OPT_ATTN_BWD_KERNEL 7  /* 0 (default): CLS-split passes for N >= 257 (a ragged N-1 with the default pass variants only); 1: generic */
 #define DCLIP_OPT_ATTN_FWD_KERNEL 6  /* 0 (default): CLS-split kernels (the pipelined attn_fwd3 when N - 1 is a multiple of 256, else attn_fwd2, ragged N-1 included); 1: generic; 2: attn_fwd3 4 waves x 64 rows; 3: attn_fwd3 8 waves; 4: attn_fwd2 always */
-#define DCLIP_OPT_ATTN_BWD_BLOCK 8   /* CLS-split dK/dV pass: 0 (default) / 6: 64 keys per wave, AGPR dK / dV (attention_dkdv6.hip); 7: its software-pipelined schedule; 8: its ring DMA inside R4; 9: the one-pass backward (attention_bwd1.hip: dK, dV and per-key-block dQ partials in one sweep, an ordered dQ reduction; a larger dclip_attn_bwd_workspace); 5: software-pipelined 32 keys per wave; 1: the unpipelined one */
+#define DCLIP_OPT_ATTN_BWD_BLOCK 8   /* CLS-split backward: 0 (default, round 6) / 10: the one-pass backward (attention_bwd1.hip: dK, dV and per-key-block dQ partials in one pipelined key-major sweep, an ordered dQ reduction; dclip_attn_bwd_workspace includes the partials, 3.2 GB at B=8, N=8193, H=12); 9: its unpipelined sweep; 6: the two-pass dQ + dK/dV passes, 64 keys per wave, AGPR dK / dV (attention_dkdv6.hip); 7: its software-pipelined schedule; 8: its ring DMA inside R4; 5: software-pipelined 32 keys per wave; 1: the unpipelined one */
 #define DCLIP_OPT_GEMM_TN_COLSUM 9   /* 0 (default): the 256x256 weight-gradient kernel sums dY's columns (bias gradient) itself; 1: a separate pass */
 #define DCLIP_OPT_GEMM_EPI 10      /* persistent NT GEMM epilogue: 0 (default) row-major through LDS, whole 128-B lines per store, streaming (nontemporal) stores for the wide forward outputs (N >= 2048, not RESIDUAL / GELU_BWD); 1 the accumulator-layout stores (16 rows x 64 B); 2 row-major, streaming stores for every output; 3 row-major, no streaming stores */
 #define DCLIP_OPT_GEMM_TAIL 11     /* persistent NT GEMM M tail (<= 16 rows): 0 (default) one latency-shaped MFMA launch (16 columns per workgroup, every K-slice load issued up front, side inputs prefetched); 1 the 256-row split-K tile + combine pair; 2 round 4's one launch (64 columns per workgroup, 8 waves, K % 256 == 0) */

@@ -13,7 +13,8 @@ Rounding points (ops.PatchEmbedFn / ops.BlockFn / ops.ReadoutFn, csrc/attention.
             cast or, with the read-out fold, dclip_layernorm_bwd_add's copy); dz (EPI_GELU_BWD
             output); dxh2 / dxh1 when LN_DY_LP (the dX GEMMs write 16 bits for the LN backward:
             bf16, or fp16 on the operand's gradient scale); the attention branch's gradient dyo (the LN backward's lp copy); dO (the
-            out-projection dX GEMM output); dS and P inside the attention backward; dqkv
+            out-projection dX GEMM output); dS and P inside the attention backward; the one-pass
+            attention backward's dQ partials (one per 256 keys, DQ_KEY_BLOCK); dqkv
   fp32      residual stream, LN statistics and backward, softmax statistics, every accumulation
 fp16 gradients are rounded on a per-tensor power-of-two scale (16 / max|g|, ops.grad_scale; the
 attention backward's dS on its own scale, as DsScale keeps it out of the subnormals), so the
@@ -78,6 +79,12 @@ class RoundBwd(torch.autograd.Function):
         return rnd(g, ctx.dt, scaled=True), None
 
 
+# the attention backward's dQ partial granularity (keys per 16-bit partial; 0: the two-pass backward,
+# whose dQ pass sums every key in fp32): the default CLS-split path since round 6 is the one-pass
+# backward (DCLIP_OPT_ATTN_BWD_BLOCK 0), 256 keys per partial, for N >= 257
+DQ_KEY_BLOCK = 256
+
+
 class Attn16(torch.autograd.Function):
     """softmax(q k^T d^-0.5) v on (BH, N, d) fp32 tensors holding 16-bit values, with the flash
     kernels' rounding points: P (unnormalised, against the row maximum) rounded before P.V and
@@ -105,6 +112,15 @@ class Attn16(torch.autograd.Function):
         delta = (do * o).sum(-1, keepdim=True)
         ds = rnd(p * (dp - delta), dt, scaled=True)
         dq = (ds @ k) * sc
+        n = q.shape[1]
+        if DQ_KEY_BLOCK and n >= 257:
+            # the one-pass backward (attention_bwd1.hip): queries 1.. sum 16-bit partials over key blocks
+            # 1 + DQ_KEY_BLOCK j .. (one rounding each) plus key 0's exact term; query 0 is exact
+            kb = DQ_KEY_BLOCK
+            rest = ds[:, 1:, :1] @ k[:, :1] * sc
+            for j0 in range(1, n, kb):
+                rest = rest + rnd((ds[:, 1:, j0:j0 + kb] @ k[:, j0:j0 + kb]) * sc, dt)
+            dq = torch.cat([dq[:, :1], rest], 1)
         dk = (ds.transpose(1, 2) @ q) * sc
         dv = rnd(p, dt).transpose(1, 2) @ do
         return dq, dk, dv, None, None

@@ -705,7 +705,7 @@ def test_attention_dkdv6_matches_dkdv5(B, H, N, dt, bwd_block):
     dout = torch.randn(B * N, C, device=DEV).to(dt)
     o, lse = O.attn_fwd(qkv, B, N, H, 64 ** -0.5)
     res = []
-    for v in (5, 0):  # dkdv5 (round 2's pass), then the default dkdv6
+    for v in (5, 6):  # dkdv5 (round 2's pass), then dkdv6 (the two-pass default of rounds 3-5)
         bwd_block(v)
         res.append(O.attn_bwd(qkv, o, dout, lse, B, N, H, 64 ** -0.5).float())
     a, b = res
@@ -718,7 +718,7 @@ def test_attention_dkdv6_matches_dkdv5(B, H, N, dt, bwd_block):
     assert torch.equal(b[rest, :C], a[rest, :C])
     assert rel_err(b[~rest], a[~rest]) < 1e-3, rel_err(b[~rest], a[~rest])
     if N <= 2049:
-        bwd_block(0)
+        bwd_block(6)
         errs = _attn_bwd_check(B, H, N, dt)
         assert max(errs) < 4 * TOL[dt], errs
 
@@ -747,15 +747,16 @@ def test_attention_dkdv7_bitwise_dkdv6(B, H, N, dt, bwd_block):
 @pytest.mark.parametrize("B,H,N", [(3, 2, 257), (2, 2, 290), (2, 3, 803), (3, 2, 1345), (2, 2, 2049), (1, 2, 8193),
                                    (1, 1, 10659)])
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
-@pytest.mark.parametrize("variant", [9, 10])
+@pytest.mark.parametrize("variant", [0, 9])
 def test_attention_onepass_bwd(B, H, N, dt, variant, bwd_block):
-    """The one-pass backward (DCLIP_OPT_ATTN_BWD_BLOCK 9, round 6, attention_bwd1.hip): one key-major
-    sweep computes dK, dV and per-key-block 16-bit dQ partials, an ordered pass sums them.  dK / dV of
-    keys 1..N-1 are dkdv6's products on the same statistics (the prep kernel repeats the dQ pass's
-    delta arithmetic): equal BIT FOR BIT to the two-pass result.  dQ is summed in another order, with
-    one 16-bit rounding per 256-key partial: within 3e-3 (fp16) / 1.5e-2 (bf16) of the two-pass dQ and
-    no further from fp32 autograd than 1.25x the two-pass error + one unit roundoff.  Full and ragged
-    N - 1, partial last key blocks, the CLS row included."""
+    """The one-pass backward (round 6, attention_bwd1.hip; the default, DCLIP_OPT_ATTN_BWD_BLOCK 0, and its
+    unpipelined sweep, option 9): one key-major sweep computes dK, dV and per-key-block 16-bit dQ
+    partials, an ordered pass sums them.  Against the two-pass backward (option 6): dK / dV of keys
+    1..N-1 are dkdv6's products on the same statistics (the prep kernel repeats the dQ pass's delta
+    arithmetic), equal BIT FOR BIT; dQ is summed in another order, with one 16-bit rounding per 256-key
+    partial: within 3e-3 (fp16) / 1.8e-2 (bf16) of the two-pass dQ and no further from fp32 autograd
+    than 1.25x the two-pass error + one unit roundoff.  Full and ragged N - 1, partial last key blocks,
+    the CLS row included."""
     O = ops()
     C = 64 * H
     torch.manual_seed(9)
@@ -763,7 +764,7 @@ def test_attention_onepass_bwd(B, H, N, dt, variant, bwd_block):
     dout = torch.randn(B * N, C, device=DEV).to(dt)
     o, lse = O.attn_fwd(qkv, B, N, H, 64 ** -0.5)
     res = []
-    for v in (0, variant):
+    for v in (6, variant):
         bwd_block(v)
         res.append(O.attn_bwd(qkv, o, dout, lse, B, N, H, 64 ** -0.5).float())
     a, b = res
@@ -801,11 +802,13 @@ def test_attention_dq_variants_match_default(B, H, N, dt, variant):
     o, lse = O.attn_fwd(qkv, B, N, H, 64 ** -0.5)
     res = []
     try:
+        N_.call("dclip_set_option", N_.OPT_ATTN_BWD_BLOCK, 6)  # the two-pass backward (its dQ pass)
         for v in (0, val):
             N_.call("dclip_set_option", opt, v)
             res.append(O.attn_bwd(qkv, o, dout, lse, B, N, H, 64 ** -0.5).float())
     finally:
         N_.call("dclip_set_option", opt, 0)
+        N_.call("dclip_set_option", N_.OPT_ATTN_BWD_BLOCK, 0)
     a, b = res
     assert torch.isfinite(b).all()
     rest = torch.ones(B * N, dtype=torch.bool, device=DEV)

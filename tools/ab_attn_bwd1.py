@@ -71,7 +71,9 @@ def main():
     res = {"compare": cmp}
     for k, v in t.items():
         m = sum(v) / len(v)
-        res[k] = {"ms_mean": round(m, 4), "ms_min": round(min(v), 4), "useful_tflops": round(flops / m / 1e9, 1),
+        med = sorted(v)[len(v) // 2]
+        res[k] = {"ms_mean": round(m, 4), "ms_median": round(med, 4), "ms_min": round(min(v), 4),
+                  "ms_max": round(max(v), 4), "useful_tflops": round(flops / m / 1e9, 1),
                   "frac_of_2500": round(flops / m / 1e9 / 2500, 4)}
     print(json.dumps(res))
 
