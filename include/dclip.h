@@ -172,11 +172,16 @@ int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda, const voi
 int dclip_attn_fwd(int dt, const void* qkv, void* o, float* lse,
                    int B, int N, int H, int D, float scale, void* stream);
 
-/* Attention backward (flash-style recompute from lse; no N x N buffer, no atomics):
- * a query-major dQ pass (which also writes delta = rowsum(dout*o) to delta_ws) and a
- * key-major dK/dV pass.  dout: (B*N, H*D) dt.  delta_ws: f32 workspace of
- * dclip_attn_bwd_workspace(B, N, H) floats (its first B*H*N receive delta; the rest holds
- * the CLS-split row-0 partials and the negated lse / delta planes of the dK/dV pass).
+/* Attention backward (flash-style recompute from lse; no N x N buffer, no atomics): for N >= 257
+ * (the CLS split) by default the one-pass backward (round 6: a prep pass writing delta =
+ * rowsum(dout*o) and the statistics, one key-major sweep for dK, dV and 16-bit dQ partials per
+ * 256-key block, an ordered reduction of the partials); with DCLIP_OPT_ATTN_BWD_BLOCK 6, and below
+ * N = 257, a query-major dQ pass (which also writes delta) and a key-major dK/dV pass.  dout:
+ * (B*N, H*D) dt.  delta_ws: f32 workspace of dclip_attn_bwd_workspace(B, N, H) floats — query it
+ * after setting options: it includes the one-pass form's partials (B*H*ceil((N-1)/256)*
+ * (1+64*ceil((N-1)/64))*128 bytes, 3.2 GB at B = 8, N = 8193, H = 12) when that form runs.  Its
+ * first B*H*N floats receive delta; the rest holds the CLS-split row-0 partials, the negated lse /
+ * delta planes, key 0's dS column and the dQ partials.
  * qkv as for dclip_attn_fwd (q pre-multiplied by scale*log2(e)); `scale` = d^-0.5.
  * dqkv: (B*N, 3*H*D) dt output, [dq | dk | dv] in the qkv layout: gradients with
  * respect to the UNSCALED q, k, v (i.e. the in-projection output before the q scale).  */
