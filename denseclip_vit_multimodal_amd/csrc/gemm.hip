@@ -1326,7 +1326,18 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_nt_pipe_kernel(
 // wave-instruction, 16-byte chunks XOR-swizzled by (row & 3) << 2 so the transposing
 // reads below are bank-conflict free) and the MFMA fragments (8 consecutive k for one
 // column) are gathered with ds_read_b64_tr_b16.  No transposed copies in HBM.
-template <typename T>
+//
+// One 16-byte LDS-DMA per lane (global_load_lds_dwordx4) written as an asm statement: invisible to
+// the compiler's LDS alias analysis, which otherwise waits vmcnt(0) before the first transposed
+// fragment read (ds_read_b64_tr_b16 builtin) after any LDS-DMA builtin — the next K-step's staging
+// then never overlaps this one's MFMAs.  The caller orders the ring with its own vmcnt wait before
+// the barrier that publishes a stage.  M0 = the wave's 1-KiB LDS piece (one wait state after it).
+__device__ __forceinline__ void glds16_asm(const void* src, const char* lds) {
+    const uint32_t la = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(lds));
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(la), "v"(src) : "memory", "m0");
+}
+
+template <typename T, bool AD = false>
 __device__ __forceinline__ void stage_tile_tn(const T* __restrict__ X, int64_t ldx, int k0, int krows,
                                               int col0, int cols, char* lds_tile, int wave, int lane) {
 #pragma unroll
@@ -1340,7 +1351,8 @@ __device__ __forceinline__ void stage_tile_tn(const T* __restrict__ X, int64_t l
         int gc = col0 + c * 8;
         gc = gc + 8 <= cols ? gc : cols - 8;  // tail columns: any in-bounds data, masked later
         const T* src = X + (int64_t)gr * ldx + gc;
-        __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(lds_tile + inst * 1024), 16, 0, 0);
+        if constexpr (AD) glds16_asm(src, lds_tile + inst * 1024);
+        else __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(lds_tile + inst * 1024), 16, 0, 0);
     }
 }
 
@@ -1478,7 +1490,14 @@ __device__ __forceinline__ void stage_tn_big(const T* __restrict__ X, int64_t ld
 // flight across each barrier (BKT 64 / 2 stages: the original one-step-ahead loop).
 // one K-step's LDS-DMA: this thread's PW pieces of A and of B (byte offsets va / vb + the step's
 // row offset ka / kb), as buffer loads (rows past the buffers' ends read 0)
-template <int PW, int BKT>
+//
+// AD: the LDS-DMA as an asm statement.  The compiler cannot tell a transposed fragment read
+// (ds_read_b64_tr_b16 builtin) from the ring slot an LDS-DMA builtin is filling, so with the builtin
+// it waits vmcnt(0) before the first fragment read of every K-step: the next K-step's staging never
+// overlaps this one's MFMAs.  The asm form is invisible to that analysis; the K-loop's own counted
+// wait before each barrier is what orders the ring (the slot read in step kt was filled in step
+// kt - 1 and waited for before step kt's barrier; nothing else in the loop touches vmcnt).
+template <int PW, int BKT, bool AD = false>
 __device__ __forceinline__ void tn_stage_buf(const void* A, uint32_t abytes, const void* B, uint32_t bbytes, char* base,
                                              const uint32_t (&va)[PW], const uint32_t (&vb)[PW], uint32_t ka,
                                              uint32_t kb, int wave) {
@@ -1486,9 +1505,20 @@ __device__ __forceinline__ void tn_stage_buf(const void* A, uint32_t abytes, con
     const rsrc_t ra = make_rsrc(A, abytes), rb = make_rsrc(B, bbytes);
 #pragma unroll
     for (int i = 0; i < PW; ++i) {
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, LDS_PTR(base + (wave * PW + i) * 1024), 16, va[i] + ka, 0, 0, 0);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, LDS_PTR(base + BKT * 512 + (wave * PW + i) * 1024), 16, vb[i] + kb,
-                                                 0, 0, 0);
+        if constexpr (AD) {
+            // M0 = the wave's 1-KiB LDS piece; one wait state between the M0 write and the DMA
+            const uint32_t la = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(base + (wave * PW + i) * 1024));
+            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(la),
+                         "v"(va[i] + ka), "s"(ra)
+                         : "memory", "m0");
+            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(la + BKT * 512),
+                         "v"(vb[i] + kb), "s"(rb)
+                         : "memory", "m0");
+        } else {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, LDS_PTR(base + (wave * PW + i) * 1024), 16, va[i] + ka, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, LDS_PTR(base + BKT * 512 + (wave * PW + i) * 1024), 16,
+                                                     vb[i] + kb, 0, 0, 0);
+        }
     }
 #endif
 }
@@ -1543,7 +1573,8 @@ __device__ __forceinline__ void tn_kstep_pf(f32x4 (&acc)[Cfg::NB][Cfg::MB], floa
 // 0.75 LDS reads per MFMA (this pass is LDS-bound).  Its 256 accumulator registers
 // live in AGPRs as "+a" operands of inline-asm MFMAs (tn_mfma_row): left to itself, hipcc shuttled
 // them between the two files (~300 v_accvgpr copies per 128 MFMAs).
-template <typename T, int EPI, int BKT = 64, int STAGES = 2, bool CS = false, int NW = 8, bool PF = false>
+template <typename T, int EPI, int BKT = 64, int STAGES = 2, bool CS = false, int NW = 8, bool PF = false,
+          bool AD = false>
 __global__ __launch_bounds__(64 * NW, 1) void gemm_tn_big_kernel(const T* __restrict__ A, int64_t lda,
                                                              const T* __restrict__ B, int64_t ldb, int M, int N,
                                                              int Kreal, int k_chunk, int tiles_m, int tiles_n,
@@ -1606,7 +1637,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_tn_big_kernel(const T* __rest
     // (the buffer resources live only inside tn_stage_buf, compiled for the device alone: a template
     // kernel body holding the device-only resource type makes hipcc drop the kernel's host stub)
 #define TN_STAGE(KT, SLOT)                                                                                          \
-    tn_stage_buf<PW, BKT>(A, abytes, B, bbytes, smem + (SLOT) * STAGE, va, vb,                                      \
+    tn_stage_buf<PW, BKT, AD>(A, abytes, B, bbytes, smem + (SLOT) * STAGE, va, vb,                                  \
                           (uint32_t)((int64_t)(kbeg + (KT) * BKT) * lda * sizeof(T)),                               \
                           (uint32_t)((int64_t)(kbeg + (KT) * BKT) * ldb * sizeof(T)), wave)
 #pragma unroll
@@ -1953,7 +1984,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_nt_kernel(
 // wgrad: dw[n = tap * Cin + ci][co]^T ... computed as C[m = co][n] = sum_p dout[p][co] * in[p + d(tap)][ci]
 // with the 128 x 128 "TN" tile (both operands staged as 64 pixel rows x 128 columns; the B
 // rows of a tile are the input pixels shifted by the tile's tap, zero rows outside the image).
-template <typename T>
+template <typename T, bool AD = false>
 __device__ __forceinline__ void stage_tile_tn_conv(const T* __restrict__ X, const T* __restrict__ zero, const PixGeo g,
                                                    int tap, int ci0, int k0, int krows, char* lds_tile, int wave,
                                                    int lane) {
@@ -1976,11 +2007,15 @@ __device__ __forceinline__ void stage_tile_tn_conv(const T* __restrict__ X, cons
         const bool ok = in_k && yy >= 0 && yy < g.H && xx >= 0 && xx < g.W;
         const T* src = ok ? X + (int64_t)b * g.bstride + g.off + ((int64_t)yy * g.W + xx) * g.ld + ci0 + c * 8
                           : zero + (c & 7) * 8;
-        __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(lds_tile + inst * 1024), 16, 0, 0);
+        if constexpr (AD) glds16_asm(src, lds_tile + inst * 1024);
+        else __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(lds_tile + inst * 1024), 16, 0, 0);
     }
 }
 
-template <typename T>
+// AD: the staging as asm LDS-DMA (glds16_asm) and a bare barrier behind a vmcnt wait at the end of
+// each K-step instead of __syncthreads (whose release fence drains the LDS-DMA as well, but the
+// compiler's own vmcnt(0) before the first fragment read had already serialised every K-step)
+template <typename T, bool AD = false>
 __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const T* __restrict__ dY, int64_t ldy,
                                                             const T* __restrict__ X, const T* __restrict__ zero,
                                                             PixGeo g, int Cin, int M, int N, int Kpix, int k_chunk,
@@ -2018,8 +2053,8 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const T* __restrict_
         const int k0 = kbeg + kt * BK;
         if (kt + 1 < nk) {
             char* nxt = smem + (cur ^ 1) * STAGE_BYTES;
-            stage_tile_tn<T>(dY, ldy, k0 + BK, Kpix, m0, M, nxt, wave, lane);
-            stage_tile_tn_conv<T>(X, zero, g, tap, ci0, k0 + BK, Kpix, nxt + TILE_BYTES, wave, lane);
+            stage_tile_tn<T, AD>(dY, ldy, k0 + BK, Kpix, m0, M, nxt, wave, lane);
+            stage_tile_tn_conv<T, AD>(X, zero, g, tap, ci0, k0 + BK, Kpix, nxt + TILE_BYTES, wave, lane);
         }
         // pixel rows past Kpix: the B rows are zero, so the clamped A duplicates add nothing
 #pragma unroll
@@ -2034,8 +2069,14 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const T* __restrict_
 #pragma unroll
                 for (int j = 0; j < 2; ++j) acc[i][j] = Mfma<T>::mma(fa[i], fb[j], acc[i][j]);
         }
-        __syncthreads();
+        if constexpr (AD) {  // the next stage landed (this wave's pieces), then everyone's; cur is free
+            wait_vmcnt<0>();
+            __builtin_amdgcn_s_barrier();
+        } else {
+            __syncthreads();
+        }
     }
+    if constexpr (AD) __syncthreads();  // the epilogue reuses the ring
     gemm_epilogue<T, DCLIP_EPI_SPLITK, float>(acc, smem, M, N, m0, n0, nullptr, nullptr, 0, C, N, nullptr, 0, slab,
                                                1.0f);
 }
@@ -2694,10 +2735,12 @@ extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda
         else if (tn_opt == 3) TN_BIG_V(T, EPI, OUT, 32, 5, false, 8);                                          \
         else if (tn_opt == 4 && fused_cs) TN_BIG_V(T, EPI, OUT, 64, 2, true, 4);                               \
         else if (tn_opt == 4) TN_BIG_V(T, EPI, OUT, 64, 2, false, 4);                                          \
-        else if (fused_cs && tn_pf) TN_BIG_V(T, EPI, OUT, 64, 2, true, 8, true);                               \
-        else if (tn_pf) TN_BIG_V(T, EPI, OUT, 64, 2, false, 8, true);                                          \
-        else if (fused_cs) TN_BIG_V(T, EPI, OUT, 64, 2, true, 8);                                              \
-        else TN_BIG_V(T, EPI, OUT, 64, 2, false, 8);                                                           \
+        else if (tn_opt == 5 && fused_cs) TN_BIG_V(T, EPI, OUT, 64, 2, true, 8);                               \
+        else if (tn_opt == 5) TN_BIG_V(T, EPI, OUT, 64, 2, false, 8);                                          \
+        else if (fused_cs && tn_pf) TN_BIG_V(T, EPI, OUT, 64, 2, true, 8, true, true);                         \
+        else if (tn_pf) TN_BIG_V(T, EPI, OUT, 64, 2, false, 8, true, true);                                    \
+        else if (fused_cs) TN_BIG_V(T, EPI, OUT, 64, 2, true, 8, false, true);                                 \
+        else TN_BIG_V(T, EPI, OUT, 64, 2, false, 8, false, true);                                              \
     } while (0)
     const int tm2 = (int)((M + 255) / 256), tn2 = (int)((N + 255) / 256);
     // the fused column sums' per-split partials, past the slabs (SPLITK): summed in split order
@@ -2795,14 +2838,19 @@ extern "C" int dclip_conv3x3_wgrad(int ab_dt, const void* dY, int64_t ldy, int N
     const int kp = (Kpix + 64 * splits - 1) / (64 * splits) * 64;  // pixel rows per split
     const int tiles_m = (Nout + BM - 1) / BM, tiles_n = N / BN;
     dim3 grid(tiles_m * tiles_n, splits);
-    if (ab_dt == DCLIP_BF16)
-        conv_wgrad_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)dY, ldy, (const bf16*)X, (const bf16*)zero, g,
-                                                      Cin, Nout, N, Kpix, kp, tiles_m, tiles_n, (float*)ws,
-                                                      (int64_t)Nout * N);
-    else
-        conv_wgrad_kernel<f16><<<grid, 256, 0, st>>>((const f16*)dY, ldy, (const f16*)X, (const f16*)zero, g, Cin,
-                                                     Nout, N, Kpix, kp, tiles_m, tiles_n, (float*)ws,
-                                                     (int64_t)Nout * N);
+    // DCLIP_OPT_GEMM_TN_TILE 5: the LDS-DMA builtin form (each K-step's staging serialised)
+#define WG_LAUNCH(T, AD)                                                                                        \
+    conv_wgrad_kernel<T, AD><<<grid, 256, 0, st>>>((const T*)dY, ldy, (const T*)X, (const T*)zero, g, Cin, Nout, N, \
+                                                   Kpix, kp, tiles_m, tiles_n, (float*)ws, (int64_t)Nout * N)
+    const bool ad = dclip_option(DCLIP_OPT_GEMM_TN_TILE) != 5;
+    if (ab_dt == DCLIP_BF16) {
+        if (ad) WG_LAUNCH(bf16, true);
+        else WG_LAUNCH(bf16, false);
+    } else {
+        if (ad) WG_LAUNCH(f16, true);
+        else WG_LAUNCH(f16, false);
+    }
+#undef WG_LAUNCH
     if (oihw || alpha_ptr != nullptr) {
         const int64_t total = (int64_t)Nout * Cin;
         const int blocks = (int)((total + 255) / 256 > 4096 ? 4096 : (total + 255) / 256);

@@ -388,7 +388,7 @@ def tn_tile(request):
     N.call("dclip_set_option", N.OPT_GEMM_TN_TILE, 0)
 
 
-@pytest.mark.parametrize("tn_tile", [0, 1, 4], indirect=True)
+@pytest.mark.parametrize("tn_tile", [0, 1, 4, 5], indirect=True)
 @pytest.mark.parametrize("M,N,K", [(777, 256, 128), (65544 // 8, 768, 3072), (5000, 2304, 768), (300, 264, 520)])
 def test_weight_grad_splitk(M, N, K, tn_tile):
     O = ops()
@@ -422,7 +422,7 @@ def test_weight_grad_fused_bias_sum(M, N, K, dt, tn_tile):
     assert rel_err(db, 0.5 * dy.double().sum(0)) < 1e-6
 
 
-@pytest.mark.parametrize("tn_tile", [0, 1, 4], indirect=True)
+@pytest.mark.parametrize("tn_tile", [0, 1, 4, 5], indirect=True)
 @pytest.mark.parametrize("K,M,N", [(64, 128, 128), (100, 136, 72), (1000, 256, 384), (8193, 768, 768), (70, 264, 520)])
 def test_gemm_tn(K, M, N, tn_tile):
     O = ops()
@@ -1263,6 +1263,36 @@ def test_conv3x3_wgrad_oihw_and_scale(Cin, Nout, splits):
     ref = torch.nn.grad.conv2d_weight(X.float().view(B, H, W, Cin).permute(0, 3, 1, 2), (Nout, Cin, 3, 3),
                                       dY.float().view(B, H, W, Nout).permute(0, 3, 1, 2), padding=1)
     assert rel_err(oihw, ref) < 1e-5
+
+
+@pytest.mark.parametrize("M,N,K", [(65544, 768, 3072), (65544, 2304, 768), (5000, 768, 768), (300, 264, 520)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_weight_grad_asm_lds_dma_bitwise(M, N, K, dt):
+    """Round 6 late: the 256x256 weight-gradient kernel and the conv weight-gradient kernel stage
+    their K-steps by LDS-DMA written as asm (the builtin made the compiler wait for each next
+    step's staging before the current step's first fragment read).  Same products, same order:
+    dW, db and the conv dW equal the builtin form's (DCLIP_OPT_GEMM_TN_TILE 5) bit for bit —
+    ragged token counts (the peeled last K-step) and several splits included."""
+    from denseclip_vit_multimodal_amd import _native as NT
+    O = ops()
+    torch.manual_seed(3)
+    dy = (torch.randn(M, N, device=DEV) + 0.2).to(dt)
+    x = torch.randn(M, K, device=DEV).to(dt)
+    B, H, W, Cin, Nout = 2, 40, 36, 256, 192
+    X = torch.randn(B * H * W, Cin, device=DEV).to(dt)
+    dY = torch.randn(B * H * W, Nout, device=DEV).to(dt)
+    cargs = (dY, Nout, Nout, X, H * W * Cin, 0, Cin, B, H, W, Cin, 3)
+    res = []
+    try:
+        for v in (5, 0):
+            NT.call("dclip_set_option", NT.OPT_GEMM_TN_TILE, v)
+            dW, db = O.weight_grad(dy, x, alpha=0.5)
+            res.append((dW, db, O.D().conv3x3_wgrad(*cargs, True)))
+    finally:
+        NT.call("dclip_set_option", NT.OPT_GEMM_TN_TILE, 0)
+    (a, b, c), (a2, b2, c2) = res
+    assert torch.equal(a, a2) and torch.equal(b, b2) and torch.equal(c, c2)
+    assert rel_err(a2, 0.5 * (dy.float().t() @ x.float())) < 1e-5
 
 
 @pytest.mark.parametrize("Cin,Cout", [(768, 128), (256, 64)])
