@@ -1371,7 +1371,8 @@ __device__ __forceinline__ typename Mfma<T>::frag tr_frag_tn(const char* img, in
     return __builtin_bit_cast(typename Mfma<T>::frag, v);
 }
 
-template <typename T, int EPI, typename OutT>
+// AD: asm LDS-DMA staging and a bare barrier behind a vmcnt wait per K-step (as conv_wgrad_kernel)
+template <typename T, int EPI, typename OutT, bool AD = false>
 __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(
     const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
     int M, int N, int Kreal, int k_chunk, int tiles_m, int tiles_n, const float* __restrict__ bias,
@@ -1412,8 +1413,8 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(
         const int k0 = kbeg + kt * BK;
         if (kt + 1 < nk) {
             char* nxt = smem + (cur ^ 1) * STAGE_BYTES;
-            stage_tile_tn<T>(A, lda, k0 + BK, Kreal, m0, M, nxt, wave, lane);
-            stage_tile_tn<T>(B, ldb, k0 + BK, Kreal, n0, N, nxt + TILE_BYTES, wave, lane);
+            stage_tile_tn<T, AD>(A, lda, k0 + BK, Kreal, m0, M, nxt, wave, lane);
+            stage_tile_tn<T, AD>(B, ldb, k0 + BK, Kreal, n0, N, nxt + TILE_BYTES, wave, lane);
         }
         const bool ragged = k0 + BK > Kreal;
 #pragma unroll
@@ -1435,8 +1436,14 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(
 #pragma unroll
                 for (int j = 0; j < 2; ++j) acc[i][j] = Mfma<T>::mma(fa[i], fb[j], acc[i][j]);
         }
-        __syncthreads();
+        if constexpr (AD) {
+            wait_vmcnt<0>();
+            __builtin_amdgcn_s_barrier();
+        } else {
+            __syncthreads();
+        }
     }
+    if constexpr (AD) __syncthreads();  // the epilogue reuses the ring
     gemm_epilogue<T, EPI, OutT>(acc, smem, M, N, m0, n0, bias, nullptr, 0, C, ldc, nullptr, 0, slab, alpha);
 }
 
@@ -2721,10 +2728,15 @@ extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda
             colsum_kernel<bf16><<<cg, 256, 0, st>>>((const bf16*)A, lda, K, (int)M, rpb, alpha, colsum_a, cs_sep);
         else colsum_kernel<f16><<<cg, 256, 0, st>>>((const f16*)A, lda, K, (int)M, rpb, alpha, colsum_a, cs_sep);
     }
-#define TN_LAUNCH(T, EPI, OUT)                                                                               \
-    gemm_tn_kernel<T, EPI, float><<<grid, 256, 0, st>>>((const T*)A, lda, (const T*)B, ldb, (int)M, (int)N,   \
-                                                        (int)K, k_chunk, tiles_m, tiles_n, nullptr, OUT,        \
-                                                        EPI == DCLIP_EPI_SPLITK ? N : ldc, (int64_t)M * N, alpha)
+#define TN_LAUNCH_V(T, EPI, OUT, AD)                                                                              \
+    gemm_tn_kernel<T, EPI, float, AD><<<grid, 256, 0, st>>>((const T*)A, lda, (const T*)B, ldb, (int)M, (int)N,    \
+                                                            (int)K, k_chunk, tiles_m, tiles_n, nullptr, OUT,         \
+                                                            EPI == DCLIP_EPI_SPLITK ? N : ldc, (int64_t)M * N, alpha)
+#define TN_LAUNCH(T, EPI, OUT)                                                                                    \
+    do {                                                                                                          \
+        if (tn_opt == 5) TN_LAUNCH_V(T, EPI, OUT, false);                                                         \
+        else TN_LAUNCH_V(T, EPI, OUT, true);                                                                      \
+    } while (0)
 #define TN_BIG_V(T, EPI, OUT, BKT, STG, CS, NW, ...)                                                           \
     gemm_tn_big_kernel<T, EPI, BKT, STG, CS, NW, ##__VA_ARGS__><<<dim3(tm2 * tn2 * splits), 64 * NW, 0, st>>>( \
         (const T*)A, lda, (const T*)B, ldb, (int)M, (int)N, (int)K, k_chunk, tm2, tn2, OUT,                     \
@@ -2769,6 +2781,7 @@ extern "C" int dclip_gemm_tn(int epilogue, int ab_dt, const void* A, int64_t lda
                                                      (float*)C, ldc, cs_part, colsum_a);
     }
 #undef TN_LAUNCH
+#undef TN_LAUNCH_V
 #undef TN_BIG
 #undef TN_BIG_V
     DCLIP_LAUNCH_CHECK();

@@ -76,7 +76,7 @@ int dclip_abi_version(void);
 #define DCLIP_OPT_ATTN_DQ_WAVES 1    /* 4 or 8 (default): dQ pass queries per workgroup / 32      */
 #define DCLIP_OPT_ATTN_DKDV_WAVES 2  /* 4 (default) or 8: dK/dV pass keys per workgroup / 32      */
 #define DCLIP_OPT_GEMM_TILE 3        /* dclip_gemm tiles: 0 auto (default: 6, 1 below 4096 rows), 1 128x128, 2 256x256, 3 256x128, 4 256x256 k32x4, 5 256x256 ping-pong, 6 persistent 256x256, 7 the same with 4 waves of 128x128, 8 / 9 persistent with pipelined fragment reads (8 / 4 waves) */
-#define DCLIP_OPT_GEMM_TN_TILE 4     /* dclip_gemm_tn tiles: 0 auto (default: 256x256 when M, N >= 256), 1 128x128, 2 256x256 with 32-row K-steps in a 4-deep ring, 3 the same 5-deep, 4 256x256 on 4 waves of 128x128, 5 the default 256x256 kernel (and the conv weight-gradient kernel) with the LDS-DMA builtin instead of the asm form (round 6 late: the builtin made every K-step wait for the next one's staging) */
+#define DCLIP_OPT_GEMM_TN_TILE 4     /* dclip_gemm_tn tiles: 0 auto (default: 256x256 when M, N >= 256), 1 128x128, 2 256x256 with 32-row K-steps in a 4-deep ring, 3 the same 5-deep, 4 256x256 on 4 waves of 128x128, 5 the weight-gradient kernels (256x256 and 128x128) and the conv weight-gradient kernel with the LDS-DMA builtin instead of the asm form (round 6 late: the builtin made every K-step wait for the next one's staging) */
 #define DCLIP_OPT_ATTN_DKDV_QS 5     /* dK/dV pass query rows per barrier: 64 (default) or 128 */
 #define DCLIP_OPT_ATTN_BWD_KERNEL 7  /* 0 (default): CLS-split passes for N >= 257 (a ragged N-1 with the default pass variants only); 1: generic */
 #define DCLIP_OPT_ATTN_FWD_KERNEL 6  /* 0 (default): CLS-split kernels (the pipelined attn_fwd3 when N - 1 is a multiple of 256, else attn_fwd2, ragged N-1 included); 1: generic; 2: attn_fwd3 4 waves x 64 rows; 3: attn_fwd3 8 waves; 4: attn_fwd2 always */

@@ -1265,11 +1265,12 @@ def test_conv3x3_wgrad_oihw_and_scale(Cin, Nout, splits):
     assert rel_err(oihw, ref) < 1e-5
 
 
-@pytest.mark.parametrize("M,N,K", [(65544, 768, 3072), (65544, 2304, 768), (5000, 768, 768), (300, 264, 520)])
+@pytest.mark.parametrize("M,N,K", [(65544, 768, 3072), (65544, 2304, 768), (5000, 768, 768), (300, 264, 520),
+                                   (2000, 128, 200)])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 def test_weight_grad_asm_lds_dma_bitwise(M, N, K, dt):
-    """Round 6 late: the 256x256 weight-gradient kernel and the conv weight-gradient kernel stage
-    their K-steps by LDS-DMA written as asm (the builtin made the compiler wait for each next
+    """Round 6 late: the weight-gradient kernels (256x256, and 128x128 below 256 rows / columns)
+    and the conv weight-gradient kernel stage their K-steps by LDS-DMA written as asm (the builtin made the compiler wait for each next
     step's staging before the current step's first fragment read).  Same products, same order:
     dW, db and the conv dW equal the builtin form's (DCLIP_OPT_GEMM_TN_TILE 5) bit for bit —
     ragged token counts (the peeled last K-step) and several splits included."""
