@@ -17,6 +17,7 @@ OPT_ATTN_FWD_WAVES, OPT_ATTN_DQ_WAVES, OPT_ATTN_DKDV_WAVES, OPT_GEMM_TILE, OPT_G
 OPT_ATTN_DKDV_QS, OPT_ATTN_FWD_KERNEL, OPT_ATTN_BWD_KERNEL, OPT_ATTN_BWD_BLOCK, OPT_GEMM_TN_COLSUM = 5, 6, 7, 8, 9
 OPT_GEMM_EPI, OPT_GEMM_TAIL, OPT_ATTN_FP8_QK, OPT_ATTN_DQ_ISSUE, OPT_ATTN_DQ_ROWS = 10, 11, 12, 13, 14
 OPT_ATTN_DQ_DEFER, OPT_GEMM_SCHED, OPT_GEMM_KLOOP = 15, 16, 17
+OPT_ATTN_DQ_REDUCE = 18
 OPT_ATTN_DQ_DEFER = 15
 
 _c_void_p = ctypes.c_void_p

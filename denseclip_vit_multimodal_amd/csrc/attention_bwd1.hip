@@ -980,6 +980,54 @@ __global__ __launch_bounds__(256) void attn_bwd1_dq_reduce(const T* __restrict__
     *(t8*)(dqkv + ((int64_t)b * N + q) * ld + hd * HD + c8) = r;
 }
 
+// the same sum (option DCLIP_OPT_ATTN_DQ_REDUCE 1): a workgroup takes 8 queries, whose partial runs
+// (nkb x 128 B each, adjacent) it reads front to back — every wave-instruction 1 KiB contiguous — into
+// LDS rows padded by 128 B (the two half-waves of the summing reads on different banks); then lane
+// pair (query t / 32, columns 2 (t % 32) + {0, 1}) adds the key blocks in block order onto the key-0
+// term, exactly as attn_bwd1_dq_reduce does, so the result is bit for bit the same
+constexpr int RQ_Q = 8;          // queries per workgroup
+constexpr int RQ_MAX_NKB = 56;   // LDS: 8 x (56 x 128 + 128) B = 57 KiB (under the 64-KiB dynamic default)
+template <typename T>
+__global__ __launch_bounds__(256) void attn_bwd1_dq_reduce_lds(const T* __restrict__ dqpart,
+                                                               const float* __restrict__ ds0v,
+                                                               const T* __restrict__ qkv, T* __restrict__ dqkv,
+                                                               int N, int H, int nkb, int nrb, float sc) {
+    typedef T t2 __attribute__((ext_vector_type(2)));
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    extern __shared__ __attribute__((aligned(16))) char rq_lds[];
+    const int rb = blockIdx.x % nrb, bh = blockIdx.x / nrb, b = bh / H, hd = bh % H;
+    const int q0 = 1 + rb * RQ_Q;
+    const int C = H * HD;
+    const int64_t ld = 3 * (int64_t)C;
+    const int64_t Np = 1 + 64 * (int64_t)((N - 1 + 63) / 64);
+    const int run = nkb * 128, stride = run + 128;  // bytes per query: in HBM / in LDS
+    // rows q0 .. q0 + 7 < Np always (Np - 1 is a multiple of 64), so the reads need no guard
+    const char* src = (const char*)(dqpart + ((int64_t)bh * Np + q0) * nkb * 64);
+    const int chunks = RQ_Q * nkb * 8;  // 16-B chunks of the 8 runs
+    for (int c = threadIdx.x; c < chunks; c += 256) {
+        const int qi = c / (nkb * 8), w = c - qi * (nkb * 8);
+        const u32x4 v = __builtin_nontemporal_load((const u32x4*)(src + (int64_t)c * 16));
+        *(u32x4*)(rq_lds + qi * stride + w * 16) = v;
+    }
+    __syncthreads();
+    const int qi = threadIdx.x >> 5, cp = threadIdx.x & 31;
+    const int q = q0 + qi;
+    if (q >= N) return;
+    const t2 kv = *(const t2*)(qkv + (int64_t)b * N * ld + C + hd * HD + 2 * cp);
+    constexpr bool unscaled = std::is_same<T, bf16>::value;
+    const float w = ds0v[(int64_t)bh * N + q] * (unscaled ? 1.0f : sc);
+    float a0 = w * (float)kv[0], a1 = w * (float)kv[1];
+    const char* row = rq_lds + qi * stride + cp * 4;
+#pragma unroll 8
+    for (int j = 0; j < nkb; ++j) {
+        const t2 v = *(const t2*)(row + j * 128);
+        a0 += (float)v[0];
+        a1 += (float)v[1];
+    }
+    const t2 r = {(T)(unscaled ? a0 * sc : a0), (T)(unscaled ? a1 * sc : a1)};
+    *(t2*)(dqkv + ((int64_t)b * N + q) * ld + hd * HD + 2 * cp) = r;
+}
+
 template <typename T>
 void bwd1_launch(const void* qkv, const void* o, const void* dout, const float* lse, float* delta, float* nstat,
                  float* ds0v, float* r0kv, int nqp, float* r0q, void* dqpart, void* dqkv, int B, int N, int H,
@@ -995,6 +1043,12 @@ void bwd1_launch(const void* qkv, const void* o, const void* dout, const float* 
         attn_bwd1_kernel<T><<<B * H * nkb, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, nstat,
                                                          nstat + (int64_t)B * H * N, (T*)dqkv, (T*)dqpart, N, H,
                                                          1.0f / LOG2E, scale, r0q);
+    if (dclip_option(DCLIP_OPT_ATTN_DQ_REDUCE) == 1 && nkb <= RQ_MAX_NKB) {
+        const int nrb = (N - 1 + RQ_Q - 1) / RQ_Q;
+        attn_bwd1_dq_reduce_lds<T><<<B * H * nrb, 256, RQ_Q * (nkb * 128 + 128), st>>>(
+            (const T*)dqpart, ds0v, (const T*)qkv, (T*)dqkv, N, H, nkb, nrb, scale / DsScale<T>::v);
+        return;
+    }
     const int nrb = (N - 1 + 31) / 32;
     attn_bwd1_dq_reduce<T><<<B * H * nrb, 256, 0, st>>>((const T*)dqpart, ds0v, (const T*)qkv, (T*)dqkv, N, H, nkb, nrb,
                                                         scale / DsScale<T>::v);

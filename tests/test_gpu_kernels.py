@@ -817,6 +817,32 @@ def test_attention_dq_variants_match_default(B, H, N, dt, variant):
     assert rel_err(b[~rest], a[~rest]) < 1e-5, rel_err(b[~rest], a[~rest])
 
 
+@pytest.mark.parametrize("B,H,N", [(3, 2, 257), (2, 2, 290), (2, 3, 803), (1, 2, 8193), (1, 1, 10659)])
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+def test_attention_onepass_dq_reduce_lds_bitwise(B, H, N, dt):
+    """The one-pass backward's dQ reduction read through LDS (DCLIP_OPT_ATTN_DQ_REDUCE 1: 8 queries per
+    workgroup, their partial runs read contiguously, then 2 columns per lane) adds the same terms in
+    the same key-block order as the default reduction: the whole backward output is BIT FOR BIT
+    equal, ragged N - 1 (a partial last group of 8 queries) included."""
+    from denseclip_vit_multimodal_amd import _native as N_
+    O = ops()
+    C = 64 * H
+    torch.manual_seed(11)
+    qkv, _ = prescale((torch.randn(B * N, 3 * C, device=DEV) * 1.5).to(dt), H)
+    dout = torch.randn(B * N, C, device=DEV).to(dt)
+    o, lse = O.attn_fwd(qkv, B, N, H, 64 ** -0.5)
+    res = []
+    try:
+        for v in (0, 1):
+            N_.call("dclip_set_option", N_.OPT_ATTN_DQ_REDUCE, v)
+            res.append(O.attn_bwd(qkv, o, dout, lse, B, N, H, 64 ** -0.5))
+    finally:
+        N_.call("dclip_set_option", N_.OPT_ATTN_DQ_REDUCE, 0)
+    a, b = res
+    assert torch.isfinite(b.float()).all()
+    assert torch.equal(a, b)
+
+
 def test_attention_bwd_full_length():
     """N = 8193 (the benchmark's sequence) through the CLS-split passes, against fp32 autograd."""
     errs = _attn_bwd_check(1, 1, 8193, torch.bfloat16)
