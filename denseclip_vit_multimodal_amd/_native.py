@@ -18,6 +18,7 @@ OPT_ATTN_DKDV_QS, OPT_ATTN_FWD_KERNEL, OPT_ATTN_BWD_KERNEL, OPT_ATTN_BWD_BLOCK, 
 OPT_GEMM_EPI, OPT_GEMM_TAIL, OPT_ATTN_FP8_QK, OPT_ATTN_DQ_ISSUE, OPT_ATTN_DQ_ROWS = 10, 11, 12, 13, 14
 OPT_ATTN_DQ_DEFER, OPT_GEMM_SCHED, OPT_GEMM_KLOOP = 15, 16, 17
 OPT_ATTN_DQ_REDUCE = 18
+OPT_ATTN_PREP_ORDER = 19
 OPT_ATTN_DQ_DEFER = 15
 
 _c_void_p = ctypes.c_void_p

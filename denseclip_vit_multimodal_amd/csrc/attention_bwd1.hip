@@ -864,12 +864,24 @@ __global__ __launch_bounds__(256) void attn_bwd1_prep_kernel(const T* __restrict
                                                              const T* __restrict__ dout, const float* __restrict__ lse,
                                                              float* __restrict__ delta, float* __restrict__ nstat,
                                                              float* __restrict__ ds0v, float* __restrict__ r0kv, int N,
-                                                             int H, int nqp) {
+                                                             int H, int nqp, int head_minor) {
     typedef typename Mfma<T>::frag frag;
     constexpr int QB = 128;
     __shared__ __attribute__((aligned(16))) char smem[4 * 32 * 128 + 2 * QB * 4 + 4 * 128 * 4];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
-    const int blk = blockIdx.x % nqp, bh = blockIdx.x / nqp, b = bh / H, hd = bh % H;
+    // workgroup -> (batch, head, query block): query block fastest (default), or (head_minor,
+    // DCLIP_OPT_ATTN_PREP_ORDER 1) the H heads of one query block on adjacent workgroups, so the
+    // 128-B head segments read at the same time are the adjacent pieces of the same token rows
+    int blk, bh;
+    if (head_minor) {
+        const int hm = blockIdx.x % H, r = blockIdx.x / H;
+        blk = r % nqp;
+        bh = (r / nqp) * H + hm;
+    } else {
+        blk = blockIdx.x % nqp;
+        bh = blockIdx.x / nqp;
+    }
+    const int b = bh / H, hd = bh % H;
     const int C = H * HD;
     const int64_t ld = 3 * (int64_t)C;
     const T* Bb = qkv + (int64_t)b * N * ld;
@@ -1034,7 +1046,8 @@ void bwd1_launch(const void* qkv, const void* o, const void* dout, const float* 
                  float scale, hipStream_t st) {
     const int nkb = (N - 1 + B1_KB - 1) / B1_KB;
     attn_bwd1_prep_kernel<T><<<B * H * nqp, 256, 0, st>>>((const T*)qkv, (const T*)o, (const T*)dout, lse, delta, nstat,
-                                                          ds0v, r0kv, N, H, nqp);
+                                                          ds0v, r0kv, N, H, nqp,
+                                                          dclip_option(DCLIP_OPT_ATTN_PREP_ORDER) == 1);
     if (dclip_option(DCLIP_OPT_ATTN_BWD_BLOCK) != 9)  // the pipelined sweep (default); 9: the barrier form
         attn_bwd1b_kernel<T><<<B * H * nkb, 256, 0, st>>>((const T*)qkv, (const T*)dout, lse, delta, nstat,
                                                           nstat + (int64_t)B * H * N, (T*)dqkv, (T*)dqpart, N, H,

@@ -91,7 +91,8 @@ int dclip_abi_version(void);
 #define DCLIP_OPT_GEMM_SCHED 16     /* persistent NT GEMM tile walk: 0 (default) static (round * G + block); 1 work-conserving (every tile claimed: round-0 ownership bitmap, XCD-local ranges, stealing) */
 #define DCLIP_OPT_GEMM_KLOOP 17     /* 8-wave GEMM K-loops: 0 (default) the persistent NT kernel with its fragment reads issued one 8-MFMA group ahead except on the GELU epilogue, the TN kernel as compiled; 1 read-ahead in every NT and TN K-loop; 2 none */
 #define DCLIP_OPT_ATTN_DQ_REDUCE 18 /* one-pass backward dQ reduction: 0 (default) 8 lanes per query, each lane its 8 columns over the key blocks; 1 8 queries per workgroup, their partial runs read contiguously into LDS (1 KiB per wave-instruction), then 2 columns per lane summed in the same key-block order (bitwise equal) */
-#define DCLIP_OPT_COUNT 19
+#define DCLIP_OPT_ATTN_PREP_ORDER 19 /* one-pass backward prep pass: 0 (default) query blocks of one head on adjacent workgroups; 1 the heads of one query block on adjacent workgroups (same per-workgroup work, bitwise equal) */
+#define DCLIP_OPT_COUNT 20
 int dclip_set_option(int id, int value);
 
 /* LayerNorm over the last dim (cols), eps, affine w/b (fp32).  y = (x-mu)*rstd*w+b.

@@ -819,12 +819,15 @@ def test_attention_dq_variants_match_default(B, H, N, dt, variant):
 
 @pytest.mark.parametrize("B,H,N", [(3, 2, 257), (2, 2, 290), (2, 3, 803), (1, 2, 8193), (1, 1, 10659)])
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
-def test_attention_onepass_dq_reduce_lds_bitwise(B, H, N, dt):
-    """The one-pass backward's dQ reduction read through LDS (DCLIP_OPT_ATTN_DQ_REDUCE 1: 8 queries per
-    workgroup, their partial runs read contiguously, then 2 columns per lane) adds the same terms in
-    the same key-block order as the default reduction: the whole backward output is BIT FOR BIT
-    equal, ragged N - 1 (a partial last group of 8 queries) included."""
+@pytest.mark.parametrize("which", ["reduce_lds", "prep_order"])
+def test_attention_onepass_dq_reduce_lds_bitwise(B, H, N, dt, which):
+    """One-pass backward variants that change no arithmetic: the dQ reduction read through LDS
+    (DCLIP_OPT_ATTN_DQ_REDUCE 1: 8 queries per workgroup, their partial runs read contiguously, then 2
+    columns per lane, the same terms in the same key-block order) and the prep pass with the heads of
+    a query block on adjacent workgroups (DCLIP_OPT_ATTN_PREP_ORDER 1).  The whole backward output is
+    BIT FOR BIT equal to the default's, ragged N - 1 (a partial last group of 8 queries) included."""
     from denseclip_vit_multimodal_amd import _native as N_
+    opt = {"reduce_lds": N_.OPT_ATTN_DQ_REDUCE, "prep_order": N_.OPT_ATTN_PREP_ORDER}[which]
     O = ops()
     C = 64 * H
     torch.manual_seed(11)
@@ -834,10 +837,10 @@ def test_attention_onepass_dq_reduce_lds_bitwise(B, H, N, dt):
     res = []
     try:
         for v in (0, 1):
-            N_.call("dclip_set_option", N_.OPT_ATTN_DQ_REDUCE, v)
+            N_.call("dclip_set_option", opt, v)
             res.append(O.attn_bwd(qkv, o, dout, lse, B, N, H, 64 ** -0.5))
     finally:
-        N_.call("dclip_set_option", N_.OPT_ATTN_DQ_REDUCE, 0)
+        N_.call("dclip_set_option", opt, 0)
     a, b = res
     assert torch.isfinite(b.float()).all()
     assert torch.equal(a, b)

@@ -1,9 +1,10 @@
-"""A/B of the one-pass attention backward's dQ reduction (DCLIP_OPT_ATTN_DQ_REDUCE 0: 8 lanes per
-query, vs 1: 8 queries per workgroup read contiguously through LDS) at the headline shape (B = 8,
+"""A/B of a one-pass attention backward option, 0 vs 1 (--opt ATTN_DQ_REDUCE: the dQ reduction with 8
+lanes per query vs 8 queries per workgroup read contiguously through LDS; --opt ATTN_PREP_ORDER: the
+prep pass's workgroups query-block-major vs head-minor) at the headline shape (B = 8,
 N = 8193, H = 12) in ONE process: bitwise comparison of the whole backward output, then the whole
 backward timed per launch with HIP events on the launch stream, arms alternated (ABBA) over rounds.
 
-  python tools/ab_dq_reduce.py [--rounds 8 --reps 10 --dtype bf16]
+  python tools/ab_dq_reduce.py [--opt ATTN_PREP_ORDER --rounds 8 --reps 10 --dtype bf16]
 """
 import argparse
 import json
@@ -23,6 +24,7 @@ def main():
     ap.add_argument("--B", type=int, default=8)
     ap.add_argument("--N", type=int, default=8193)
     ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--opt", default="ATTN_DQ_REDUCE", help="the option name (OPT_<name> of _native): ATTN_DQ_REDUCE or ATTN_PREP_ORDER")
     a = ap.parse_args()
     from denseclip_vit_multimodal_amd import ops
     from denseclip_vit_multimodal_amd import _native as NT
@@ -34,10 +36,11 @@ def main():
     qkv[:, :C] = (qkv[:, :C].float() * (64 ** -0.5 * 1.4426950408889634)).to(dt)
     dout = torch.randn(B * N, C, device="cuda", generator=g).to(dt)
     o, lse = ops.attn_fwd(qkv, B, N, H, 64 ** -0.5)
-    arms = {"reduce0": 0, "reduce1_lds": 1}
+    arms = {"opt0": 0, "opt1": 1}
+    OPT = getattr(NT, "OPT_" + a.opt)
 
     def run(v):
-        NT.call("dclip_set_option", NT.OPT_ATTN_DQ_REDUCE, v)
+        NT.call("dclip_set_option", OPT, v)
         return ops.attn_bwd(qkv, o, dout, lse, B, N, H, 64 ** -0.5)
 
     outs = [run(v) for v in arms.values()]
@@ -48,7 +51,7 @@ def main():
     for r in range(a.rounds):
         order = list(arms) if r % 2 == 0 else list(arms)[::-1]
         for name in order:
-            NT.call("dclip_set_option", NT.OPT_ATTN_DQ_REDUCE, arms[name])
+            NT.call("dclip_set_option", OPT, arms[name])
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(a.reps + 1)]
             ev[0].record()
             for i in range(a.reps):
@@ -56,7 +59,7 @@ def main():
                 ev[i + 1].record()
             torch.cuda.synchronize()
             t[name] += [ev[i].elapsed_time(ev[i + 1]) for i in range(a.reps)]
-    NT.call("dclip_set_option", NT.OPT_ATTN_DQ_REDUCE, 0)
+    NT.call("dclip_set_option", OPT, 0)
     for k, v in t.items():
         s = sorted(v)
         res[k] = {"ms_mean": round(sum(v) / len(v), 4), "ms_median": round(s[len(s) // 2], 4),
